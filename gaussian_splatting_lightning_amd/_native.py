@@ -1,0 +1,135 @@
+"""ctypes binding of libgsrast.so (include/gsrast.h).
+
+This is the product path: every rasterizer call goes through these C entry points.  There is no
+CPU or PyTorch fallback -- if the library is missing or cannot be loaded, importing the rasterizer
+raises, so a GPU run can never silently pass on another implementation.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgsrast.so")
+
+GSR_BUF_GEOM, GSR_BUF_BINNING, GSR_BUF_IMAGE, GSR_BUF_BWD_SCRATCH = 0, 1, 2, 3
+
+_fp = ctypes.c_void_p  # device pointers are passed as integers
+
+
+class ForwardArgs(ctypes.Structure):
+    _fields_ = [
+        ("P", ctypes.c_int), ("D", ctypes.c_int), ("M", ctypes.c_int), ("W", ctypes.c_int), ("H", ctypes.c_int),
+        ("background", _fp), ("means3D", _fp), ("colors_precomp", _fp), ("opacities", _fp), ("scales", _fp),
+        ("scale_modifier", ctypes.c_float), ("rotations", _fp), ("cov3D_precomp", _fp), ("viewmatrix", _fp),
+        ("projmatrix", _fp), ("campos", _fp), ("tan_fovx", ctypes.c_float), ("tan_fovy", ctypes.c_float),
+        ("shs", _fp), ("prefiltered", ctypes.c_int), ("antialiasing", ctypes.c_int), ("debug", ctypes.c_int),
+        ("out_color", _fp), ("out_invdepth", _fp), ("radii", _fp),
+    ]
+
+
+class BackwardArgs(ctypes.Structure):
+    _fields_ = [
+        ("P", ctypes.c_int), ("D", ctypes.c_int), ("M", ctypes.c_int), ("W", ctypes.c_int), ("H", ctypes.c_int),
+        ("R", ctypes.c_int64), ("background", _fp), ("means3D", _fp), ("colors_precomp", _fp),
+        ("opacities", _fp), ("scales", _fp), ("scale_modifier", ctypes.c_float), ("rotations", _fp),
+        ("cov3D_precomp", _fp), ("viewmatrix", _fp), ("projmatrix", _fp), ("campos", _fp),
+        ("tan_fovx", ctypes.c_float), ("tan_fovy", ctypes.c_float), ("dL_dpix", _fp), ("dL_dinvdepth", _fp),
+        ("shs", _fp), ("radii", _fp), ("geom_buffer", _fp), ("binning_buffer", _fp), ("image_buffer", _fp),
+        ("antialiasing", ctypes.c_int), ("debug", ctypes.c_int), ("dL_dmeans2D", _fp), ("dL_dcolors", _fp),
+        ("dL_dopacity", _fp), ("dL_dmeans3D", _fp), ("dL_dcov3D", _fp), ("dL_dsh", _fp), ("dL_dscales", _fp),
+        ("dL_drotations", _fp),
+    ]
+
+
+class StateLayout(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_size_t) for n in (
+        "geom_rec_a", "geom_rec_b", "geom_rec_c", "geom_tiles", "geom_order", "geom_inst_off", "geom_inst_start",
+        "geom_clamped", "geom_sorted_depth", "bin_point_list", "bin_inv", "bin_keys_sorted", "img_final_T", "img_n_contrib",
+        "img_ranges", "img_tile_last")]
+
+
+ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t)
+
+EXPORTED_SYMBOLS = (
+    "gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes",
+    "gsr_image_buffer_bytes", "gsr_bwd_scratch_bytes", "gsr_set_profiling", "gsr_num_stages", "gsr_stage_name",
+    "gsr_stage_times", "gsr_reset_stage_times", "gsr_last_error", "gsr_build_info", "gsr_state_layout_query",
+)
+
+_lib = None
+
+
+def load(path: str | None = None):
+    """Load libgsrast.so once (raises RuntimeError with build instructions if it is absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or os.environ.get("GSR_LIB", LIB_PATH)
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"libgsrast.so not found at {path}: build it with `python -m gaussian_splatting_lightning_amd.build` "
+            "(or __graft_entry__.build()); there is no CPU fallback.")
+    lib = ctypes.CDLL(path)
+    lib.gsr_forward.argtypes = [ctypes.POINTER(ForwardArgs), ALLOC_FN, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.POINTER(ctypes.c_int64)]
+    lib.gsr_forward.restype = ctypes.c_int
+    lib.gsr_backward.argtypes = [ctypes.POINTER(BackwardArgs), ALLOC_FN, ctypes.c_void_p, ctypes.c_void_p]
+    lib.gsr_backward.restype = ctypes.c_int
+    lib.gsr_mark_visible.argtypes = [ctypes.c_int, _fp, _fp, _fp, _fp, ctypes.c_void_p]
+    lib.gsr_mark_visible.restype = ctypes.c_int
+    lib.gsr_geom_buffer_bytes.argtypes = [ctypes.c_int]
+    lib.gsr_geom_buffer_bytes.restype = ctypes.c_size_t
+    lib.gsr_binning_buffer_bytes.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int]
+    lib.gsr_binning_buffer_bytes.restype = ctypes.c_size_t
+    lib.gsr_image_buffer_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.gsr_image_buffer_bytes.restype = ctypes.c_size_t
+    lib.gsr_bwd_scratch_bytes.argtypes = [ctypes.c_int, ctypes.c_int64]
+    lib.gsr_bwd_scratch_bytes.restype = ctypes.c_size_t
+    lib.gsr_set_profiling.argtypes = [ctypes.c_int]
+    lib.gsr_set_profiling.restype = None
+    lib.gsr_num_stages.restype = ctypes.c_int
+    lib.gsr_stage_name.argtypes = [ctypes.c_int]
+    lib.gsr_stage_name.restype = ctypes.c_char_p
+    lib.gsr_stage_times.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
+    lib.gsr_stage_times.restype = ctypes.c_int
+    lib.gsr_reset_stage_times.restype = None
+    lib.gsr_state_layout_query.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                           ctypes.POINTER(StateLayout)]
+    lib.gsr_state_layout_query.restype = None
+    lib.gsr_last_error.restype = ctypes.c_char_p
+    lib.gsr_build_info.restype = ctypes.c_char_p
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().gsr_last_error().decode(errors="replace")
+        if rc == 5:
+            raise NotImplementedError(f"{what}: {msg}")
+        raise RuntimeError(f"{what} failed (code {rc}): {msg}")
+
+
+def set_profiling(enable: bool) -> None:
+    load().gsr_set_profiling(1 if enable else 0)
+
+
+def reset_stage_times() -> None:
+    load().gsr_reset_stage_times()
+
+
+def stage_times() -> dict:
+    """{stage_name: (total_ms, calls)} accumulated since the last reset (synchronises pending events)."""
+    lib = load()
+    n = lib.gsr_num_stages()
+    tot = (ctypes.c_double * n)()
+    calls = (ctypes.c_int64 * n)()
+    lib.gsr_stage_times(tot, calls, n)
+    return {lib.gsr_stage_name(i).decode(): (tot[i], int(calls[i])) for i in range(n)}
+
+
+def state_layout(P: int, R: int, W: int, H: int) -> dict:
+    out = StateLayout()
+    load().gsr_state_layout_query(int(P), int(R), int(W), int(H), ctypes.byref(out))
+    return {name: getattr(out, name) for name, _ in StateLayout._fields_}

@@ -1,0 +1,77 @@
+"""Build libgsrast.so (the HIP rasterizer behind include/gsrast.h) in-tree for gfx950.
+
+    python -m gaussian_splatting_lightning_amd.build        # or __graft_entry__.build()
+
+Compiles every csrc/*.hip with hipcc --offload-arch=gfx950 in parallel and links one shared library
+next to this file, so the built .so travels with the repository snapshot to the GPU box.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+INCLUDE = os.path.join(REPO, "include")
+LIB = os.path.join(PKG, "libgsrast.so")
+OBJDIR = os.path.join(REPO, "build", "gsrast")
+ARCH = os.environ.get("GSR_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found: the HIP rasterizer cannot be built")
+
+
+def _flags():
+    return [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-I" + INCLUDE, "-I" + CSRC,
+            "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
+
+
+def _needs_rebuild(obj: str, src: str) -> bool:
+    if not os.path.exists(obj):
+        return True
+    deps = [src] + glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(INCLUDE, "gsrast.h")]
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(OBJDIR, exist_ok=True)
+    hipcc = _hipcc()
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    objs = [os.path.join(OBJDIR, os.path.basename(s)[:-4] + ".o") for s in srcs]
+    todo = [(s, o) for s, o in zip(srcs, objs) if force or _needs_rebuild(o, s)]
+
+    def compile_one(so):
+        src, obj = so
+        cmd = [hipcc, *_flags(), "-c", src, "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
+        if verbose and r.stderr.strip():
+            print(r.stderr, file=sys.stderr)
+        return obj
+
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=min(8, len(todo))) as ex:
+            list(ex.map(compile_one, todo))
+    if todo or force or not os.path.exists(LIB):
+        tmp = LIB + ".tmp"
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

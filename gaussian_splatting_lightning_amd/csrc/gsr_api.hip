@@ -1,0 +1,422 @@
+// gsr_api.hip -- the extern "C" boundary declared in include/gsrast.h.
+//
+// Mirrors the orchestration of the reference's CUDA entry points (rasterize_points.cu
+// RasterizeGaussiansCUDA / RasterizeGaussiansBackwardCUDA / markVisible and
+// rasterizer_impl.cu Rasterizer::forward/backward, SURVEY.md §2.1, [U]) with the MI355X stage list of
+// preprocess -> depth sort -> instance scan -> one 8-byte readback -> expand -> tile sort ->
+// ranges -> composite; backward: reverse composite -> big-Gaussian reduce -> preprocess backward.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "gsr_kernels.h"
+#include "gsrast.h"
+
+using namespace gsr;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define GSR_HIP(x)                                                                                  \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess) {                                                                     \
+            (void)hipGetLastError(); /* do not leave a sticky error for the caller's runtime */     \
+            return fail(GSR_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_));               \
+        }                                                                                           \
+    } while (0)
+
+// ---- per-stage profiling --------------------------------------------------------------------------
+enum Stage {
+    ST_PREPROCESS = 0,
+    ST_DEPTH_SORT,
+    ST_SCAN,
+    ST_READBACK,
+    ST_EXPAND,
+    ST_TILE_SORT,
+    ST_RANGES,
+    ST_RENDER_FWD,
+    ST_RENDER_BWD,
+    ST_BIG_REDUCE,
+    ST_PREPROCESS_BWD,
+    ST_COUNT
+};
+const char *kStageNames[ST_COUNT] = {"preprocess", "depth_sort", "instance_scan", "readback",
+                                     "expand",     "tile_sort",  "tile_ranges",   "render_fwd",
+                                     "render_bwd", "big_reduce", "preprocess_bwd"};
+
+struct Profiler {
+    std::mutex mu;
+    bool enabled = false;
+    std::vector<hipEvent_t> pool;
+    struct Pending {
+        int stage;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending;
+    double total_ms[ST_COUNT] = {};
+    int64_t calls[ST_COUNT] = {};
+
+    hipEvent_t get() {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        return e;
+    }
+    void drain() {
+        for (auto &p : pending) {
+            float ms = 0.f;
+            (void)hipEventSynchronize(p.b);
+            if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+                total_ms[p.stage] += ms;
+                calls[p.stage] += 1;
+            }
+            pool.push_back(p.a);
+            pool.push_back(p.b);
+        }
+        pending.clear();
+    }
+};
+Profiler &prof() {
+    static Profiler p;
+    return p;
+}
+
+// Scoped stage: records an event pair when profiling, synchronises + checks when debugging.
+struct StageScope {
+    hipStream_t s;
+    int stage;
+    bool debug;
+    hipEvent_t a = nullptr;
+    StageScope(hipStream_t s_, int st, bool dbg) : s(s_), stage(st), debug(dbg) {
+        Profiler &p = prof();
+        if (p.enabled) {
+            std::lock_guard<std::mutex> lk(p.mu);
+            a = p.get();
+            if (a) (void)hipEventRecord(a, s);
+        }
+    }
+    int finish() {
+        Profiler &p = prof();
+        if (a) {
+            std::lock_guard<std::mutex> lk(p.mu);
+            hipEvent_t b = p.get();
+            if (b) {
+                (void)hipEventRecord(b, s);
+                p.pending.push_back({stage, a, b});
+            }
+            if (p.pending.size() > 4096) p.drain();
+        }
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess && debug) {
+            e = hipStreamSynchronize(s);
+            if (e == hipSuccess) e = hipGetLastError();
+        }
+        if (e != hipSuccess)
+            return fail(GSR_ERR_HIP, std::string("stage ") + kStageNames[stage] + ": " + hipGetErrorString(e));
+        return GSR_OK;
+    }
+};
+
+#define GSR_STAGE(stage, dbg, ...)                      \
+    do {                                                \
+        StageScope sc_(stream, stage, dbg);             \
+        __VA_ARGS__;                                    \
+        int rc_ = sc_.finish();                         \
+        if (rc_ != GSR_OK) return rc_;                  \
+    } while (0)
+
+uint32_t *pinned_words() {
+    thread_local uint32_t *p = nullptr;
+    if (!p) {
+        if (hipHostMalloc((void **)&p, 256, hipHostMallocDefault) != hipSuccess) p = nullptr;
+    }
+    return p;
+}
+
+int check_common(int P, int D, int M, int W, int H, const float *means3D, const float *opac,
+                 const float *colors, const float *shs, const float *scales, const float *rots, const float *cov,
+                 const float *view, const float *proj, const float *campos, const float *bg) {
+    if (P < 0) return fail(GSR_ERR_ARG, "P must be >= 0");
+    if (W <= 0 || H <= 0) return fail(GSR_ERR_ARG, "image_width and image_height must be positive");
+    if ((int64_t)W * H > 0x7fffffffLL) return fail(GSR_ERR_ARG, "image too large");
+    if ((uint64_t)P > (uint64_t)SCAN_TILE * SCAN_MAX_BLOCKS - 1)
+        return fail(GSR_ERR_ARG, "too many Gaussians for the single-level scan");
+    if (P == 0) return GSR_OK;
+    if (!means3D || !opac) return fail(GSR_ERR_ARG, "means3D and opacities are required");
+    if (!view || !proj || !bg) return fail(GSR_ERR_ARG, "viewmatrix, projmatrix and bg are required");
+    if (!colors) {
+        if (!shs || M <= 0) return fail(GSR_ERR_ARG, "Please provide exactly one of either SHs or precomputed colors!");
+        if (D < 0 || D > 3) return fail(GSR_ERR_ARG, "sh_degree must be in [0, 3]");
+        if ((D + 1) * (D + 1) > M) return fail(GSR_ERR_ARG, "sh_degree needs (deg+1)^2 coefficients per Gaussian");
+        if (!campos) return fail(GSR_ERR_ARG, "campos is required with SHs");
+    }
+    if (!cov && (!scales || !rots))
+        return fail(GSR_ERR_ARG, "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+    return GSR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t gsr_geom_buffer_bytes(int P) {
+    GeomState g;
+    return carve_geom(nullptr, P, g);
+}
+size_t gsr_binning_buffer_bytes(int64_t R, int W, int H) {
+    BinningState b;
+    uint32_t T = (uint32_t)(((W + BLOCK_X - 1) / BLOCK_X) * ((H + BLOCK_Y - 1) / BLOCK_Y));
+    return carve_binning(nullptr, R, T, b);
+}
+size_t gsr_image_buffer_bytes(int W, int H) {
+    ImageState im;
+    return carve_image(nullptr, W, H, im);
+}
+size_t gsr_bwd_scratch_bytes(int P, int64_t R) {
+    (void)P;
+    return bwd_scratch_bytes(R);
+}
+
+void gsr_state_layout_query(int P, int64_t R, int W, int H, gsr_state_layout *out) {
+    if (!out) return;
+    char *const base = reinterpret_cast<char *>(size_t(1) << 40);  // any aligned non-null base
+    auto off = [&](const void *p) { return (size_t)(reinterpret_cast<const char *>(p) - base); };
+    GeomState g;
+    carve_geom(base, P, g);
+    BinningState b;
+    const uint32_t T = (uint32_t)(((W + BLOCK_X - 1) / BLOCK_X) * ((H + BLOCK_Y - 1) / BLOCK_Y));
+    carve_binning(base, R, T, b);
+    ImageState im;
+    carve_image(base, W, H, im);
+    out->geom_rec_a = off(g.rec_a);
+    out->geom_rec_b = off(g.rec_b);
+    out->geom_rec_c = off(g.rec_c);
+    out->geom_tiles = off(g.tiles);
+    out->geom_order = off(g.order);
+    out->geom_inst_off = off(g.inst_off);
+    out->geom_inst_start = off(g.inst_start);
+    out->geom_clamped = off(g.clamped);
+    out->geom_sorted_depth = off(g.sort.k[0]);
+    out->bin_point_list = off(b.point_list);
+    out->bin_inv = off(b.inv);
+    out->bin_keys_sorted = off(b.keys_sorted);
+    out->img_final_T = off(im.final_T);
+    out->img_n_contrib = off(im.n_contrib);
+    out->img_ranges = off(im.ranges);
+    out->img_tile_last = off(im.tile_last);
+}
+
+int gsr_forward(const gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *stream_ptr,
+                int64_t *num_rendered) {
+    if (!a || !alloc || !num_rendered) return fail(GSR_ERR_ARG, "null argument");
+    int rc = check_common(a->P, a->D, a->M, a->W, a->H, a->means3D, a->opacities, a->colors_precomp, a->shs,
+                          a->scales, a->rotations, a->cov3D_precomp, a->viewmatrix, a->projmatrix, a->campos,
+                          a->background);
+    if (rc) return rc;
+    if (!a->out_color || (a->P > 0 && !a->radii)) return fail(GSR_ERR_ARG, "out_color and radii are required");
+    hipStream_t stream = (hipStream_t)stream_ptr;
+    const bool dbg = a->debug != 0;
+    const int P = a->P, W = a->W, H = a->H;
+    const int gx = (W + BLOCK_X - 1) / BLOCK_X, gy = (H + BLOCK_Y - 1) / BLOCK_Y;
+    const uint32_t T = (uint32_t)(gx * gy);
+    *num_rendered = 0;
+    if (P == 0) {
+        // the reference returns its zero-initialised outputs untouched when P == 0
+        GSR_HIP(hipMemsetAsync(a->out_color, 0, sizeof(float) * 3 * (size_t)W * H, stream));
+        if (a->out_invdepth) GSR_HIP(hipMemsetAsync(a->out_invdepth, 0, sizeof(float) * (size_t)W * H, stream));
+        return GSR_OK;
+    }
+
+    GeomState g;
+    char *geom = alloc(alloc_ctx, GSR_BUF_GEOM, carve_geom(nullptr, P, g));
+    if (!geom) return fail(GSR_ERR_ALLOC, "geometry buffer allocation failed");
+    carve_geom(geom, P, g);
+    ImageState im;
+    char *img = alloc(alloc_ctx, GSR_BUF_IMAGE, carve_image(nullptr, W, H, im));
+    if (!img) return fail(GSR_ERR_ALLOC, "image buffer allocation failed");
+    carve_image(img, W, H, im);
+    GSR_HIP(hipMemsetAsync(g.counters, 0, CNT_WORDS * sizeof(uint32_t), stream));
+
+    PreprocessParams pp;
+    pp.P = P; pp.D = a->D; pp.M = a->M; pp.W = W; pp.H = H; pp.gx = gx; pp.gy = gy;
+    pp.tan_fovx = a->tan_fovx; pp.tan_fovy = a->tan_fovy;
+    pp.focal_x = W / (2.0f * a->tan_fovx);
+    pp.focal_y = H / (2.0f * a->tan_fovy);
+    pp.scale_modifier = a->scale_modifier;
+    pp.antialiasing = a->antialiasing;
+    pp.means3D = a->means3D; pp.opacities = a->opacities; pp.scales = a->scales; pp.rotations = a->rotations;
+    pp.cov3D_precomp = a->cov3D_precomp; pp.colors_precomp = a->colors_precomp; pp.shs = a->shs;
+    pp.view = a->viewmatrix; pp.proj = a->projmatrix; pp.campos = a->campos;
+    pp.radii = a->radii;
+    pp.g = g;
+    GSR_STAGE(ST_PREPROCESS, dbg, launch_preprocess(stream, pp));
+    GSR_STAGE(ST_DEPTH_SORT, dbg, launch_radix_sort(stream, g.sort, (uint32_t)P, 32, nullptr, nullptr, nullptr));
+    GSR_STAGE(ST_SCAN, dbg,
+              launch_exclusive_scan(stream, g.tiles, g.order, (uint32_t)P, g.inst_off, g.scan_tmp,
+                                    g.counters + CNT_OVERFLOW));
+    uint32_t *hw = pinned_words();
+    if (!hw) return fail(GSR_ERR_HIP, "pinned host buffer allocation failed");
+    GSR_STAGE(ST_READBACK, dbg, {
+        GSR_HIP(hipMemcpyAsync(hw, g.inst_off + P, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        GSR_HIP(hipMemcpyAsync(hw + 1, g.counters, CNT_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        GSR_HIP(hipStreamSynchronize(stream));
+    });
+    if (hw[1 + CNT_OVERFLOW]) return fail(GSR_ERR_OVERFLOW, "more than 2^32-1 tile instances");
+    const uint32_t R = hw[0];
+    *num_rendered = R;
+
+    BinningState b;
+    char *bin = alloc(alloc_ctx, GSR_BUF_BINNING, carve_binning(nullptr, R, T, b));
+    if (!bin) return fail(GSR_ERR_ALLOC, "binning buffer allocation failed");
+    carve_binning(bin, R, T, b);
+    if ((uint64_t)RS_BINS * div_up(R ? R : 1, RS_TILE) + 1 > (uint64_t)SCAN_TILE * SCAN_MAX_BLOCKS)
+        return fail(GSR_ERR_OVERFLOW, "too many tile instances for the single-level scan");
+    if (R > 0) {
+        ExpandParams ep;
+        ep.P = (uint32_t)P; ep.R = R; ep.gx = gx; ep.gy = gy;
+        ep.order = g.order; ep.inst_off = g.inst_off; ep.tiles = g.tiles; ep.rec_a = g.rec_a; ep.radii = a->radii;
+        ep.keys_out = b.sort.k[0]; ep.inst_gid = b.inst_gid; ep.inst_start = g.inst_start;
+        GSR_STAGE(ST_EXPAND, dbg, launch_expand(stream, ep));
+        GSR_STAGE(ST_TILE_SORT, dbg,
+                  launch_radix_sort(stream, b.sort, R, tile_key_bits(T), b.inst_gid, b.point_list, b.inv));
+    }
+    GSR_STAGE(ST_RANGES, dbg, {
+        GSR_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * T, stream));
+        launch_identify_ranges(stream, b.keys_sorted, R, im.ranges);
+    });
+    RenderFwdParams rp;
+    rp.W = W; rp.H = H; rp.gx = gx; rp.gy = gy; rp.num_tiles = (int)T;
+    rp.ranges = im.ranges; rp.point_list = b.point_list;
+    rp.rec_a = g.rec_a; rp.rec_b = g.rec_b; rp.rec_c = g.rec_c;
+    rp.bg = a->background;
+    rp.out_color = a->out_color; rp.out_invdepth = a->out_invdepth; rp.final_T = im.final_T;
+    rp.n_contrib = im.n_contrib; rp.tile_last = im.tile_last;
+    GSR_STAGE(ST_RENDER_FWD, dbg, launch_render_fwd(stream, rp));
+    return GSR_OK;
+}
+
+int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *stream_ptr) {
+    if (!a || !alloc) return fail(GSR_ERR_ARG, "null argument");
+    int rc = check_common(a->P, a->D, a->M, a->W, a->H, a->means3D, a->opacities, a->colors_precomp, a->shs,
+                          a->scales, a->rotations, a->cov3D_precomp, a->viewmatrix, a->projmatrix, a->campos,
+                          a->background);
+    if (rc) return rc;
+    if (a->P == 0) return GSR_OK;
+    if (!a->dL_dpix || !a->radii) return fail(GSR_ERR_ARG, "dL_dpix and radii are required");
+    if (!a->geom_buffer || !a->image_buffer || (a->R > 0 && !a->binning_buffer))
+        return fail(GSR_ERR_ARG, "forward buffers are required");
+    if (a->shs && a->M > 0 && !a->dL_dsh) return fail(GSR_ERR_ARG, "dL_dsh is required when shs are given");
+    if (a->R < 0 || a->R > 0xffffffffLL) return fail(GSR_ERR_ARG, "bad num_rendered");
+    hipStream_t stream = (hipStream_t)stream_ptr;
+    const bool dbg = a->debug != 0;
+    const int P = a->P, W = a->W, H = a->H;
+    const int gx = (W + BLOCK_X - 1) / BLOCK_X, gy = (H + BLOCK_Y - 1) / BLOCK_Y;
+    const uint32_t T = (uint32_t)(gx * gy);
+    const uint32_t R = (uint32_t)a->R;
+
+    GeomState g;
+    carve_geom(a->geom_buffer, P, g);
+    BinningState b;
+    carve_binning(a->binning_buffer, R, T, b);
+    ImageState im;
+    carve_image(a->image_buffer, W, H, im);
+    char *scratch = alloc(alloc_ctx, GSR_BUF_BWD_SCRATCH, bwd_scratch_bytes(R));
+    if (!scratch) return fail(GSR_ERR_ALLOC, "backward scratch allocation failed");
+    float *rows = reinterpret_cast<float *>(scratch);
+
+    if (R > 0) {
+        RenderBwdParams rp;
+        rp.W = W; rp.H = H; rp.gx = gx; rp.gy = gy; rp.num_tiles = (int)T;
+        rp.ranges = im.ranges; rp.point_list = b.point_list; rp.n_contrib = im.n_contrib;
+        rp.tile_last = im.tile_last;
+        rp.rec_a = g.rec_a; rp.rec_b = g.rec_b; rp.rec_c = g.rec_c;
+        rp.bg = a->background; rp.final_T = im.final_T; rp.dL_dpix = a->dL_dpix; rp.dL_dinvdepth = a->dL_dinvdepth;
+        rp.rows = rows;
+        GSR_STAGE(ST_RENDER_BWD, dbg, launch_render_bwd(stream, rp));
+        BigReduceParams bp;
+        bp.counters = g.counters; bp.big_list = g.big_list; bp.inst_start = g.inst_start; bp.tiles = g.tiles;
+        bp.inv = b.inv; bp.rows = rows;
+        GSR_STAGE(ST_BIG_REDUCE, dbg, launch_big_reduce(stream, bp, (uint32_t)P));
+    }
+    PreprocessBwdParams pp;
+    pp.P = P; pp.D = a->D; pp.M = a->M; pp.W = W; pp.H = H;
+    pp.tan_fovx = a->tan_fovx; pp.tan_fovy = a->tan_fovy;
+    pp.focal_x = W / (2.0f * a->tan_fovx);
+    pp.focal_y = H / (2.0f * a->tan_fovy);
+    pp.scale_modifier = a->scale_modifier;
+    pp.antialiasing = a->antialiasing;
+    pp.has_invdepth = a->dL_dinvdepth != nullptr;
+    pp.means3D = a->means3D; pp.opacities = a->opacities; pp.scales = a->scales; pp.rotations = a->rotations;
+    pp.cov3D_precomp = a->cov3D_precomp; pp.shs = (a->colors_precomp ? nullptr : a->shs);
+    pp.view = a->viewmatrix; pp.proj = a->projmatrix; pp.campos = a->campos;
+    pp.radii = a->radii; pp.tiles = g.tiles; pp.inst_start = g.inst_start; pp.inv = b.inv; pp.clamped = g.clamped;
+    pp.rows = rows;
+    pp.dL_dmeans2D = a->dL_dmeans2D; pp.dL_dcolors = a->dL_dcolors; pp.dL_dopacity = a->dL_dopacity;
+    pp.dL_dmeans3D = a->dL_dmeans3D; pp.dL_dcov3D = a->dL_dcov3D; pp.dL_dsh = a->dL_dsh;
+    pp.dL_dscales = a->dL_dscales; pp.dL_drot = a->dL_drotations;
+    if (pp.shs == nullptr && a->dL_dsh && a->M > 0)
+        GSR_HIP(hipMemsetAsync(a->dL_dsh, 0, sizeof(float) * (size_t)P * a->M * 3, stream));
+    GSR_STAGE(ST_PREPROCESS_BWD, dbg, launch_preprocess_bwd(stream, pp));
+    return GSR_OK;
+}
+
+int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix, uint8_t *present,
+                     void *stream_ptr) {
+    (void)projmatrix;
+    if (P < 0) return fail(GSR_ERR_ARG, "P must be >= 0");
+    if (P == 0) return GSR_OK;
+    if (!means3D || !viewmatrix || !present) return fail(GSR_ERR_ARG, "null argument");
+    hipStream_t s = (hipStream_t)stream_ptr;
+    launch_mark_visible(s, P, means3D, viewmatrix, present);
+    GSR_HIP(hipGetLastError());
+    return GSR_OK;
+}
+
+void gsr_set_profiling(int enable) {
+    Profiler &p = prof();
+    std::lock_guard<std::mutex> lk(p.mu);
+    p.enabled = enable != 0;
+}
+int gsr_num_stages(void) { return ST_COUNT; }
+const char *gsr_stage_name(int stage) { return (stage >= 0 && stage < ST_COUNT) ? kStageNames[stage] : ""; }
+int gsr_stage_times(double *total_ms, int64_t *calls, int max_stages) {
+    Profiler &p = prof();
+    std::lock_guard<std::mutex> lk(p.mu);
+    p.drain();
+    const int n = max_stages < ST_COUNT ? max_stages : ST_COUNT;
+    for (int i = 0; i < n; i++) {
+        if (total_ms) total_ms[i] = p.total_ms[i];
+        if (calls) calls[i] = p.calls[i];
+    }
+    return n;
+}
+void gsr_reset_stage_times(void) {
+    Profiler &p = prof();
+    std::lock_guard<std::mutex> lk(p.mu);
+    p.drain();
+    for (int i = 0; i < ST_COUNT; i++) {
+        p.total_ms[i] = 0;
+        p.calls[i] = 0;
+    }
+}
+const char *gsr_last_error(void) { return g_err.c_str(); }
+const char *gsr_build_info(void) {
+    return "gsrast: MI355X (gfx950) HIP rasterizer; wave64 tile compositing, LSD radix binning, "
+           "deterministic gradient rows; built " __DATE__ " " __TIME__;
+}
+
+}  // extern "C"

@@ -1,0 +1,310 @@
+// gsr_common.h -- shared device/host definitions for the MI355X Gaussian rasterizer.
+//
+// Layout of the three caller-owned scratch buffers (SURVEY.md §8(b) "Ownership"; the reference keeps
+// GeometryState/BinningState/ImageState in uint8 torch tensors, notes/rasterizer_note.h:27-40).  All
+// per-Gaussian render attributes are packed into 40 B so one tile batch gathers them with three
+// 16/16/8-byte loads per instance:
+//   rec_a = (x_pix, y_pix, conic.x, conic.y)   rec_b = (conic.z, opacity, r, g)   rec_c = (b, 1/depth)
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gsr {
+
+constexpr int BLOCK_X = 16;
+constexpr int BLOCK_Y = 16;
+constexpr int TILE_PIX = BLOCK_X * BLOCK_Y;
+constexpr int WAVE = 64;
+constexpr int PIX_PER_LANE = TILE_PIX / WAVE;  // one wave composites one 16x16 tile
+constexpr uint32_t BIG_GAUSSIAN_TILES = 64;   // per-Gaussian gradient rows reduced by a whole block above this
+constexpr int GRAD_ROW = 12;                   // floats per instance gradient row (10 used, 48 B)
+
+// counters block at the head of the geometry buffer (zeroed every forward)
+enum Counter : int { CNT_BIG = 0, CNT_TOTAL = 1, CNT_OVERFLOW = 2, CNT_WORDS = 16 };
+
+__host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }
+
+struct Carver {
+    char *base;
+    size_t off;
+    explicit Carver(char *b) : base(b), off(0) {}
+    template <class T>
+    T *take(size_t count, size_t alignment = 256) {
+        off = align_up(off, alignment);
+        T *p = base ? reinterpret_cast<T *>(base + off) : nullptr;
+        off += count * sizeof(T);
+        return p;
+    }
+};
+
+// radix-sort / scan tiling
+constexpr int RS_THREADS = 256;
+constexpr int RS_ITEMS = 16;
+constexpr int RS_TILE = RS_THREADS * RS_ITEMS;  // 4096 keys per block
+constexpr int RS_BINS = 256;
+constexpr int SCAN_TILE = 4096;
+constexpr int SCAN_MAX_BLOCKS = 1024 * 16;  // single-block scan of block sums
+
+inline uint32_t div_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+struct SortScratch {
+    uint32_t *k[2];
+    uint32_t *v[2];
+    uint32_t *counts;    // RS_BINS * nblocks
+    uint32_t *scan_tmp;  // block sums for scanning counts
+};
+
+inline void carve_sort(Carver &c, SortScratch &s, uint32_t n, bool need_v0) {
+    s.k[0] = c.take<uint32_t>(n ? n : 1);
+    s.k[1] = c.take<uint32_t>(n ? n : 1);
+    s.v[0] = need_v0 ? c.take<uint32_t>(n ? n : 1) : nullptr;
+    s.v[1] = c.take<uint32_t>(n ? n : 1);
+    uint32_t nb = div_up(n ? n : 1, RS_TILE);
+    s.counts = c.take<uint32_t>((size_t)RS_BINS * nb + 1);
+    s.scan_tmp = c.take<uint32_t>(div_up((size_t)RS_BINS * nb + 1, SCAN_TILE) + 1);
+}
+
+struct GeomState {
+    uint32_t *counters;    // CNT_WORDS
+    float4 *rec_a;         // P
+    float4 *rec_b;         // P
+    float2 *rec_c;         // P
+    uint32_t *depth_key;   // P: float bits of view depth, 0xffffffff if culled (aliases sort.k[0])
+    uint32_t *tiles;       // P: tiles touched
+    uint8_t *clamped;      // P: bit c set if SH colour channel c was clamped at 0
+    uint32_t *inst_off;    // P+1: exclusive scan of tiles in depth order, [P] = total
+    uint32_t *inst_start;  // P: first instance (expansion order) of each Gaussian
+    uint32_t *big_list;    // P: Gaussians with > BIG_GAUSSIAN_TILES tiles
+    uint32_t *scan_tmp;    // block sums for the instance scan
+    SortScratch sort;      // depth sort (P keys); final order lands in sort.v[0]
+    const uint32_t *order; // = sort.v[0] after the (even-pass) depth sort
+};
+
+inline size_t carve_geom(char *base, int P, GeomState &g) {
+    Carver c(base);
+    uint32_t n = (uint32_t)P;
+    g.counters = c.take<uint32_t>(CNT_WORDS);
+    g.rec_a = c.take<float4>(n);
+    g.rec_b = c.take<float4>(n);
+    g.rec_c = c.take<float2>(n);
+    g.tiles = c.take<uint32_t>(n);
+    g.clamped = c.take<uint8_t>(n);
+    g.inst_off = c.take<uint32_t>((size_t)n + 1);
+    g.inst_start = c.take<uint32_t>(n);
+    g.big_list = c.take<uint32_t>(n);
+    g.scan_tmp = c.take<uint32_t>(div_up(n + 1, SCAN_TILE) + 1);
+    carve_sort(c, g.sort, n, true);
+    g.depth_key = g.sort.k[0];  // preprocess writes the depth-sort keys in place
+    g.order = g.sort.v[0];
+    return c.off + 256;
+}
+
+inline int tile_key_bits(uint32_t num_tiles) {
+    int b = 0;
+    while (b < 32 && (uint64_t(1) << b) < num_tiles) b++;
+    return b < 1 ? 1 : b;
+}
+inline int radix_passes(int bits) { return (bits + 7) / 8; }
+
+struct BinningState {
+    uint32_t *inst_gid;    // R: Gaussian of each instance (expansion order)
+    uint32_t *point_list;  // R: Gaussian ids sorted by (tile, depth, id)
+    uint32_t *inv;         // R: expansion index -> sorted position
+    uint32_t *keys_sorted; // R: tile id of each sorted instance
+    SortScratch sort;      // tile sort (R keys)
+};
+
+inline size_t carve_binning(char *base, int64_t R, uint32_t num_tiles, BinningState &b) {
+    Carver c(base);
+    uint32_t n = (uint32_t)R;
+    b.inst_gid = c.take<uint32_t>(n ? n : 1);
+    b.point_list = c.take<uint32_t>(n ? n : 1);
+    b.inv = c.take<uint32_t>(n ? n : 1);
+    int passes = radix_passes(tile_key_bits(num_tiles));
+    carve_sort(c, b.sort, n, passes > 2);
+    // keys end in k[passes & 1]
+    b.keys_sorted = b.sort.k[passes & 1];
+    return c.off + 256;
+}
+
+struct ImageState {
+    float *final_T;       // W*H
+    uint32_t *n_contrib;  // W*H
+    uint2 *ranges;        // T
+    uint32_t *tile_last;  // T: max n_contrib over the tile's pixels
+};
+
+inline size_t carve_image(char *base, int W, int H, ImageState &im) {
+    Carver c(base);
+    size_t npix = (size_t)W * H;
+    uint32_t gx = (W + BLOCK_X - 1) / BLOCK_X, gy = (H + BLOCK_Y - 1) / BLOCK_Y;
+    im.final_T = c.take<float>(npix ? npix : 1);
+    im.n_contrib = c.take<uint32_t>(npix ? npix : 1);
+    im.ranges = c.take<uint2>((size_t)gx * gy + 1);
+    im.tile_last = c.take<uint32_t>((size_t)gx * gy + 1);
+    return c.off + 256;
+}
+
+inline size_t bwd_scratch_bytes(int64_t R) { return align_up((size_t)(R ? R : 1) * GRAD_ROW * sizeof(float), 256) + 256; }
+
+// ------------------------------------------------------------------------------------------------
+// device helpers
+// ------------------------------------------------------------------------------------------------
+#ifdef __HIPCC__
+
+struct Mat4 {
+    float m[16];
+};
+
+__device__ __forceinline__ Mat4 load_mat4(const float *__restrict__ p) {
+    Mat4 r;
+#pragma unroll
+    for (int i = 0; i < 16; i++) r.m[i] = p[i];
+    return r;
+}
+
+// [p,1] @ M with M stored row-major (torch) == transformPoint4x4 on the column-major view
+__device__ __forceinline__ float4 xform4(const float3 p, const Mat4 &m) {
+    return make_float4(m.m[0] * p.x + m.m[4] * p.y + m.m[8] * p.z + m.m[12],
+                       m.m[1] * p.x + m.m[5] * p.y + m.m[9] * p.z + m.m[13],
+                       m.m[2] * p.x + m.m[6] * p.y + m.m[10] * p.z + m.m[14],
+                       m.m[3] * p.x + m.m[7] * p.y + m.m[11] * p.z + m.m[15]);
+}
+__device__ __forceinline__ float3 xform3(const float3 p, const Mat4 &m) {
+    return make_float3(m.m[0] * p.x + m.m[4] * p.y + m.m[8] * p.z + m.m[12],
+                       m.m[1] * p.x + m.m[5] * p.y + m.m[9] * p.z + m.m[13],
+                       m.m[2] * p.x + m.m[6] * p.y + m.m[10] * p.z + m.m[14]);
+}
+
+__device__ __forceinline__ float3 load_f3(const float *__restrict__ p, int i) {
+    return make_float3(p[3 * i], p[3 * i + 1], p[3 * i + 2]);
+}
+
+// ndc -> pixel; the upstream form evaluates in double ((v + 1.0) * S - 1.0) * 0.5
+__device__ __forceinline__ float ndc2pix(float v, int S) { return (float)(((v + 1.0) * S - 1.0) * 0.5); }
+
+__device__ __forceinline__ void get_rect(float2 p, int radius, int gx, int gy, int2 &rmin, int2 &rmax) {
+    rmin.x = min(gx, max(0, (int)((p.x - radius) / BLOCK_X)));
+    rmin.y = min(gy, max(0, (int)((p.y - radius) / BLOCK_Y)));
+    rmax.x = min(gx, max(0, (int)((p.x + radius + BLOCK_X - 1) / BLOCK_X)));
+    rmax.y = min(gy, max(0, (int)((p.y + radius + BLOCK_Y - 1) / BLOCK_Y)));
+}
+
+// SH basis constants (utils/sh.py:7-28 of the reference)
+#define GSR_SH_C0 0.28209479177387814f
+#define GSR_SH_C1 0.4886025119029199f
+__constant__ const float SH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f,
+                                     -1.0925484305920792f, 0.5462742152960396f};
+__constant__ const float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f,
+                                     0.3731763325901154f, -0.4570457994644658f, 1.445305721320277f,
+                                     -0.5900435899266435f};
+
+// Rotation (glm column-major R[c][r]) from an unnormalised (w,x,y,z) quaternion.
+struct Mat3 {
+    float m[3][3];
+};
+__device__ __forceinline__ Mat3 quat_to_rot(float4 q) {
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    Mat3 R;
+    R.m[0][0] = 1.f - 2.f * (y * y + z * z); R.m[0][1] = 2.f * (x * y - r * z); R.m[0][2] = 2.f * (x * z + r * y);
+    R.m[1][0] = 2.f * (x * y + r * z); R.m[1][1] = 1.f - 2.f * (x * x + z * z); R.m[1][2] = 2.f * (y * z - r * x);
+    R.m[2][0] = 2.f * (x * z - r * y); R.m[2][1] = 2.f * (y * z + r * x); R.m[2][2] = 1.f - 2.f * (x * x + y * y);
+    return R;
+}
+
+// Sigma = R S S^T R^T as 6 upper-triangle values (render_tools.py:56-70)
+__device__ __forceinline__ void cov3d_from_scale_rot(float3 s, float mod, float4 q, float out[6]) {
+    Mat3 R = quat_to_rot(q);
+    const float sv[3] = {mod * s.x, mod * s.y, mod * s.z};
+    float M[3][3];
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+#pragma unroll
+        for (int r = 0; r < 3; r++) M[c][r] = sv[r] * R.m[c][r];
+    // Sigma[c][r] = sum_k M[r][k] * M[c][k]
+    auto sig = [&](int c, int r) { return M[r][0] * M[c][0] + M[r][1] * M[c][1] + M[r][2] * M[c][2]; };
+    out[0] = sig(0, 0); out[1] = sig(0, 1); out[2] = sig(0, 2);
+    out[3] = sig(1, 1); out[4] = sig(1, 2); out[5] = sig(2, 2);
+}
+
+// EWA Jacobian rows times the view rotation (render_tools.py:13-52): t0 = J0 * Rv, t1 = J1 * Rv.
+struct EwaT {
+    float t0[3], t1[3];
+    float3 t;  // view-space mean with clamped x, y
+    float xmul, ymul;
+};
+__device__ __forceinline__ EwaT ewa_T(float3 mean, const Mat4 &view, float fx, float fy, float tanx, float tany) {
+    EwaT e;
+    float3 t = xform3(mean, view);
+    const float limx = 1.3f * tanx, limy = 1.3f * tany;
+    const float txtz = t.x / t.z, tytz = t.y / t.z;
+    e.xmul = (txtz < -limx || txtz > limx) ? 0.f : 1.f;
+    e.ymul = (tytz < -limy || tytz > limy) ? 0.f : 1.f;
+    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+    const float j00 = fx / t.z, j02 = -(fx * t.x) / (t.z * t.z);
+    const float j11 = fy / t.z, j12 = -(fy * t.y) / (t.z * t.z);
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        e.t0[r] = view.m[4 * r + 0] * j00 + view.m[4 * r + 2] * j02;
+        e.t1[r] = view.m[4 * r + 1] * j11 + view.m[4 * r + 2] * j12;
+    }
+    e.t = t;
+    return e;
+}
+
+__device__ __forceinline__ float quad_form(const float a[3], const float c6[6], const float b[3]) {
+    // a^T V b with V the symmetric matrix of c6
+    const float v0 = c6[0] * b[0] + c6[1] * b[1] + c6[2] * b[2];
+    const float v1 = c6[1] * b[0] + c6[3] * b[1] + c6[4] * b[2];
+    const float v2 = c6[2] * b[0] + c6[4] * b[1] + c6[5] * b[2];
+    return a[0] * v0 + a[1] * v1 + a[2] * v2;
+}
+
+// --- wave64 primitives ---------------------------------------------------------------------------
+template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf, bool BOUND = false>
+__device__ __forceinline__ float dpp_mov(float old, float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL, ROW_MASK,
+                                                      BANK_MASK, BOUND));
+}
+
+// Sum over the 64 lanes (every lane must be active); the result is returned wave-uniform.
+__device__ __forceinline__ float wave_sum(float v) {
+    v += dpp_mov<0xB1>(0.f, v);            // quad_perm [1,0,3,2]
+    v += dpp_mov<0x4E>(0.f, v);            // quad_perm [2,3,0,1]
+    v += dpp_mov<0x141>(0.f, v);           // row_half_mirror
+    v += dpp_mov<0x140>(0.f, v);           // row_mirror -> row sums in every lane
+    v += dpp_mov<0x142, 0xa>(0.f, v);      // row_bcast:15 into rows 1, 3
+    v += dpp_mov<0x143, 0xc>(0.f, v);      // row_bcast:31 into rows 2, 3
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+    return v;
+}
+
+// inclusive prefix sum over the wave (lanes in order)
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = (uint32_t)__shfl_up((int)v, o);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt(int lane) { return (lane == 0) ? 0ull : (~0ull >> (64 - lane)); }
+
+// Orders LDS writes before later LDS reads of other lanes of the SAME wave (no s_barrier).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+#endif  // __HIPCC__
+
+}  // namespace gsr

@@ -1,0 +1,338 @@
+// gsr_forward.hip -- forward kernels: preprocess, tile expansion, tile ranges, compositing, frustum test.
+//
+// Semantics follow the upstream CUDA rasterizer the reference calls ([U]) and are
+// pinned against the reference's Python restatement through tests/golden (oracle/gsr_oracle.c):
+//   preprocess   <-> gs_lightning/rasterize/rasterize.py:52-94, render_tools.py:13-131
+//   binning      <-> rasterize.py:129-152, render_tools.py:134-139
+//   compositing  <-> rasterize.py:210-261 with the CUDA termination rule
+#include "gsr_kernels.h"
+#include "gsr_sh.h"
+
+namespace gsr {
+
+// ------------------------------------------------------------------------------------------------
+// preprocess: one thread per Gaussian.  Culls, projects, builds the conic and radius, evaluates SH,
+// and emits the packed render records plus the depth-sort key and tile count.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void preprocess_kernel(PreprocessParams p) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= p.P) return;
+    GeomState &g = p.g;
+    p.radii[i] = 0;
+    g.tiles[i] = 0;
+    g.depth_key[i] = 0xffffffffu;
+    g.clamped[i] = 0;
+
+    const Mat4 view = load_mat4(p.view);
+    const float3 mean = load_f3(p.means3D, i);
+    const float3 pv = xform3(mean, view);
+    if (!(pv.z > 0.2f)) return;  // in_frustum (camera_tools.py:5-8)
+
+    const Mat4 proj = load_mat4(p.proj);
+    const float4 ph = xform4(mean, proj);
+    const float pw = 1.0f / (ph.w + 0.0000001f);
+    const float ndc_x = ph.x * pw, ndc_y = ph.y * pw;
+
+    float c6[6];
+    if (p.cov3D_precomp) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) c6[k] = p.cov3D_precomp[6 * i + k];
+    } else {
+        const float4 q = make_float4(p.rotations[4 * i], p.rotations[4 * i + 1], p.rotations[4 * i + 2],
+                                     p.rotations[4 * i + 3]);
+        cov3d_from_scale_rot(load_f3(p.scales, i), p.scale_modifier, q, c6);
+    }
+    const EwaT e = ewa_T(mean, view, p.focal_x, p.focal_y, p.tan_fovx, p.tan_fovy);
+    float cxx = quad_form(e.t0, c6, e.t0);
+    const float cxy = quad_form(e.t1, c6, e.t0);
+    float cyy = quad_form(e.t1, c6, e.t1);
+    constexpr float h_var = 0.3f;
+    const float det_cov = cxx * cyy - cxy * cxy;
+    cxx += h_var;
+    cyy += h_var;
+    const float det = cxx * cyy - cxy * cxy;
+    float hscale = 1.0f;
+    if (p.antialiasing) hscale = sqrtf(fmaxf(0.000025f, det_cov / det));
+    if (det == 0.0f) return;
+    const float det_inv = 1.f / det;
+    const float conic_x = cyy * det_inv, conic_y = -cxy * det_inv, conic_z = cxx * det_inv;
+    const float mid = 0.5f * (cxx + cyy);
+    const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float radius = ceilf(3.f * sqrtf(fmaxf(l1, l2)));
+    const float2 pimg = make_float2(ndc2pix(ndc_x, p.W), ndc2pix(ndc_y, p.H));
+    int2 rmin, rmax;
+    get_rect(pimg, (int)radius, p.gx, p.gy, rmin, rmax);
+    const uint32_t area = (uint32_t)((rmax.x - rmin.x) * (rmax.y - rmin.y));
+    if (area == 0) return;
+
+    float3 rgb;
+    uint8_t clamp_bits = 0;
+    if (p.colors_precomp) {
+        rgb = load_f3(p.colors_precomp, i);
+    } else {
+        const float3 campos = make_float3(p.campos[0], p.campos[1], p.campos[2]);
+        float3 dir = mean - campos;
+        const float len = sqrtf(dot3(dir, dir));
+        dir = make_float3(dir.x / len, dir.y / len, dir.z / len);
+        rgb = sh_dispatch(p.D, p.shs + (size_t)i * p.M * 3, dir);
+        rgb = rgb + make_float3(0.5f, 0.5f, 0.5f);
+        clamp_bits = (rgb.x < 0.f ? 1 : 0) | (rgb.y < 0.f ? 2 : 0) | (rgb.z < 0.f ? 4 : 0);
+        rgb = make_float3(fmaxf(rgb.x, 0.f), fmaxf(rgb.y, 0.f), fmaxf(rgb.z, 0.f));
+    }
+    const float opacity = p.opacities[i] * hscale;
+    g.rec_a[i] = make_float4(pimg.x, pimg.y, conic_x, conic_y);
+    g.rec_b[i] = make_float4(conic_z, opacity, rgb.x, rgb.y);
+    g.rec_c[i] = make_float2(rgb.z, 1.f / pv.z);
+    g.clamped[i] = clamp_bits;
+    p.radii[i] = (int)radius;
+    g.tiles[i] = area;
+    g.depth_key[i] = __float_as_uint(pv.z);
+    if (area > BIG_GAUSSIAN_TILES) {
+        const uint32_t slot = atomicAdd(&g.counters[CNT_BIG], 1u);
+        g.big_list[slot] = (uint32_t)i;
+    }
+}
+
+void launch_preprocess(hipStream_t s, const PreprocessParams &p) {
+    if (p.P <= 0) return;
+    preprocess_kernel<<<div_up(p.P, 256), 256, 0, s>>>(p);
+}
+
+// ------------------------------------------------------------------------------------------------
+// expand: instances are laid out in depth-rank order (Gaussian order[r] owns [inst_off[r], inst_off[r+1])).
+// Each block owns a fixed slice of EXP_TILE instances (load balanced whatever the per-Gaussian tile
+// counts are); its threads find their owning rank by a binary search over an LDS copy of the block's
+// rank window and then walk EXP_PER consecutive instances, emitting the tile id (sort key) and the
+// Gaussian id of each.
+// ------------------------------------------------------------------------------------------------
+constexpr int EXP_PER = 8;
+constexpr int EXP_TILE = 256 * EXP_PER;
+
+// Wave-cooperative search: last index r in [0, n] with off[r] <= u (off non-decreasing, off[0] <= u).
+// 64 probes per step, so ~log64(n) dependent global loads instead of log2(n).
+__device__ __forceinline__ uint32_t wave_last_le(const uint32_t *__restrict__ off, uint32_t n, uint32_t u,
+                                                 int lane) {
+    uint32_t lo = 0, hi = n;
+    while (hi - lo >= 64) {
+        const uint32_t step = (hi - lo) / 65;
+        const uint32_t st = step ? step : 1;
+        const uint32_t probe = lo + (uint32_t)(lane + 1) * st;
+        const bool pred = probe <= hi && off[probe] <= u;
+        const uint32_t c = (uint32_t)__popcll(__ballot(pred));
+        const uint32_t nlo = lo + c * st;
+        const uint32_t nhi = (c < 64) ? lo + (c + 1) * st - 1 : hi;
+        lo = nlo;
+        hi = nhi;
+    }
+    const uint32_t probe = lo + (uint32_t)lane;
+    const bool pred = probe <= hi && off[probe] <= u;
+    return lo + (uint32_t)__popcll(__ballot(pred)) - 1;
+}
+
+__global__ __launch_bounds__(256) void expand_kernel(ExpandParams p) {
+    __shared__ uint32_t s_off[EXP_TILE + 2];
+    __shared__ int4 s_rect[EXP_TILE + 1];  // (gid, rmin.x, rmin.y, width)
+    __shared__ uint32_t s_lo, s_n;
+    const uint32_t u0 = blockIdx.x * EXP_TILE;
+    const uint32_t u1 = min(p.R, u0 + (uint32_t)EXP_TILE);
+    if (threadIdx.x < 64) {
+        // owner(u) = last r with inst_off[r] <= u.  Every visible Gaussian owns >= 1 instance and the
+        // culled ones are sorted to the end, so the owners of [u0, u1) are consecutive ranks.
+        const int lane = threadIdx.x;
+        const uint32_t lo = wave_last_le(p.inst_off, p.P, u0, lane);
+        const uint32_t hi = wave_last_le(p.inst_off, p.P, u1 - 1, lane);
+        if (lane == 0) {
+            s_lo = lo;
+            s_n = hi - lo + 1;
+        }
+    }
+    __syncthreads();
+    const uint32_t r_lo = s_lo, nr = s_n;  // nr <= EXP_TILE
+    for (uint32_t k = threadIdx.x; k < nr + 1; k += 256) s_off[k] = p.inst_off[r_lo + k];
+    for (uint32_t k = threadIdx.x; k < nr; k += 256) {
+        const uint32_t gid = p.order[r_lo + k];
+        const float4 a = p.rec_a[gid];
+        int2 rmin, rmax;
+        get_rect(make_float2(a.x, a.y), p.radii[gid], p.gx, p.gy, rmin, rmax);
+        s_rect[k] = make_int4((int)gid, rmin.x, rmin.y, rmax.x - rmin.x);
+    }
+    __syncthreads();
+    const uint32_t ub = u0 + threadIdx.x * EXP_PER;
+    if (ub >= u1) return;
+    // owner of ub within the window
+    uint32_t lo = 0, hi = nr - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (s_off[mid] <= ub) lo = mid; else hi = mid - 1;
+    }
+    uint32_t r = lo;
+    uint32_t next = s_off[r + 1];
+    int4 rect = s_rect[r];
+    uint32_t k = ub - s_off[r];
+    const uint32_t ue = min(u1, ub + (uint32_t)EXP_PER);
+    for (uint32_t u = ub; u < ue; u++) {
+        while (u >= next) {
+            r++;
+            next = s_off[r + 1];
+            rect = s_rect[r];
+            k = 0;
+        }
+        const uint32_t w = (uint32_t)rect.w;
+        const uint32_t ty = (uint32_t)rect.z + k / w, tx = (uint32_t)rect.y + k % w;
+        p.keys_out[u] = ty * (uint32_t)p.gx + tx;
+        p.inst_gid[u] = (uint32_t)rect.x;
+        if (k == 0) p.inst_start[rect.x] = u;
+        k++;
+    }
+}
+
+void launch_expand(hipStream_t s, const ExpandParams &p) {
+    if (p.R == 0) return;
+    expand_kernel<<<div_up(p.R, EXP_TILE), 256, 0, s>>>(p);
+}
+
+// ------------------------------------------------------------------------------------------------
+// ranges: [start, end) of every tile's run in the sorted instance list
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void identify_ranges_kernel(const uint32_t *__restrict__ keys, uint32_t R,
+                                                              uint2 *__restrict__ ranges) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= R) return;
+    const uint32_t cur = keys[i];
+    if (i == 0) {
+        ranges[cur].x = 0;
+    } else {
+        const uint32_t prev = keys[i - 1];
+        if (cur != prev) {
+            ranges[prev].y = i;
+            ranges[cur].x = i;
+        }
+    }
+    if (i == R - 1) ranges[cur].y = R;
+}
+
+void launch_identify_ranges(hipStream_t s, const uint32_t *keys_sorted, uint32_t R, uint2 *ranges) {
+    if (R == 0) return;
+    identify_ranges_kernel<<<div_up(R, 256), 256, 0, s>>>(keys_sorted, R, ranges);
+}
+
+// ------------------------------------------------------------------------------------------------
+// compositing: one wave per 16x16 tile, 4 pixels per lane (rows r, r+4, r+8, r+12).  Each batch of
+// 64 instances is gathered once per wave (one instance per lane) into the wave's LDS slice and then
+// broadcast to all lanes.  Front-to-back: alpha = min(0.99, o*exp(power)); skip alpha < 1/255; stop a
+// pixel before the Gaussian that would take T below 1e-4.  No block barriers: the four waves of a
+// block work on four independent tiles and retire independently.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void render_fwd_kernel(RenderFwdParams p) {
+    __shared__ float4 s_a[4][64];
+    __shared__ float4 s_b[4][64];
+    __shared__ float2 s_c[4][64];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tile = blockIdx.x * 4 + w;
+    if (tile >= p.num_tiles) return;
+    const int tx = tile % p.gx, ty = tile / p.gx;
+    const int px = tx * BLOCK_X + (lane & 15);
+    const int py0 = ty * BLOCK_Y + (lane >> 4);
+    const float pfx = (float)px;
+
+    float T[PIX_PER_LANE], C0[PIX_PER_LANE], C1[PIX_PER_LANE], C2[PIX_PER_LANE], ID[PIX_PER_LANE];
+    uint32_t last[PIX_PER_LANE];
+    bool active[PIX_PER_LANE];
+#pragma unroll
+    for (int k = 0; k < PIX_PER_LANE; k++) {
+        const int py = py0 + 4 * k;
+        active[k] = px < p.W && py < p.H;
+        T[k] = 1.0f;
+        C0[k] = C1[k] = C2[k] = ID[k] = 0.f;
+        last[k] = 0;
+    }
+    const uint2 range = p.ranges[tile];
+    uint32_t contributor = 0;
+    for (uint32_t base = range.x; base < range.y; base += 64) {
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < PIX_PER_LANE; k++) any |= active[k];
+        if (__ballot(any) == 0) break;
+        const uint32_t s = base + lane;
+        if (s < range.y) {
+            const uint32_t gid = p.point_list[s];
+            s_a[w][lane] = p.rec_a[gid];
+            s_b[w][lane] = p.rec_b[gid];
+            s_c[w][lane] = p.rec_c[gid];
+        }
+        wave_lds_sync();
+        const int cnt = (int)min(64u, range.y - base);
+        for (int j = 0; j < cnt; j++) {
+            const float4 a = s_a[w][j];
+            const float4 b = s_b[w][j];
+            const float2 c = s_c[w][j];
+            contributor++;
+#pragma unroll
+            for (int k = 0; k < PIX_PER_LANE; k++) {
+                if (!active[k]) continue;
+                const float dx = a.x - pfx, dy = a.y - (float)(py0 + 4 * k);
+                const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+                if (power > 0.0f) continue;
+                const float alpha = fminf(0.99f, b.y * expf(power));
+                if (alpha < 1.0f / 255.0f) continue;
+                const float test_T = T[k] * (1 - alpha);
+                if (test_T < 0.0001f) { active[k] = false; continue; }
+                C0[k] += b.z * alpha * T[k];
+                C1[k] += b.w * alpha * T[k];
+                C2[k] += c.x * alpha * T[k];
+                ID[k] += c.y * alpha * T[k];
+                T[k] = test_T;
+                last[k] = contributor;
+            }
+            bool still = false;
+#pragma unroll
+            for (int k = 0; k < PIX_PER_LANE; k++) still |= active[k];
+            if (__ballot(still) == 0) break;
+        }
+        wave_lds_sync();
+    }
+    const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
+    const size_t HW = (size_t)p.W * p.H;
+    uint32_t mx = 0;
+#pragma unroll
+    for (int k = 0; k < PIX_PER_LANE; k++) {
+        const int py = py0 + 4 * k;
+        if (px < p.W && py < p.H) {
+            const size_t pid = (size_t)py * p.W + px;
+            p.final_T[pid] = T[k];
+            p.n_contrib[pid] = last[k];
+            p.out_color[pid] = C0[k] + T[k] * bg0;
+            p.out_color[HW + pid] = C1[k] + T[k] * bg1;
+            p.out_color[2 * HW + pid] = C2[k] + T[k] * bg2;
+            if (p.out_invdepth) p.out_invdepth[pid] = ID[k];
+            mx = max(mx, last[k]);
+        }
+    }
+    mx = wave_max_u32(mx);
+    if (lane == 0) p.tile_last[tile] = mx;
+}
+
+void launch_render_fwd(hipStream_t s, const RenderFwdParams &p) {
+    if (p.num_tiles <= 0) return;
+    render_fwd_kernel<<<div_up(p.num_tiles, 4), 256, 0, s>>>(p);
+}
+
+// ------------------------------------------------------------------------------------------------
+// markVisible (checkFrustum): z_view > 0.2
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void mark_visible_kernel(int P, const float *__restrict__ means3D,
+                                                           const float *__restrict__ view,
+                                                           uint8_t *__restrict__ present) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= P) return;
+    const Mat4 v = load_mat4(view);
+    present[i] = xform3(load_f3(means3D, i), v).z > 0.2f ? 1 : 0;
+}
+
+void launch_mark_visible(hipStream_t s, int P, const float *means3D, const float *view, uint8_t *present) {
+    if (P <= 0) return;
+    mark_visible_kernel<<<div_up(P, 256), 256, 0, s>>>(P, means3D, view, present);
+}
+
+}  // namespace gsr

@@ -1,0 +1,91 @@
+// gsr_kernels.h -- host-side launchers of the HIP kernels (defined in gsr_*.hip).
+#pragma once
+
+#include "gsr_common.h"
+
+namespace gsr {
+
+// ---- scan / sort (gsr_sort.hip) ----
+// Exclusive scan of n u32 values (optionally gathered through idx: v[i] = in[idx[i]]).
+// out has n+1 entries; out[n] = total.  overflow_flag (device u32) is set if the total exceeds 2^32-1.
+void launch_exclusive_scan(hipStream_t s, const uint32_t *in, const uint32_t *idx, uint32_t n, uint32_t *out,
+                           uint32_t *block_tmp, uint32_t *overflow_flag);
+
+// LSD radix sort of n (key, value) pairs on bits [0, nbits).  Keys start in sc.k[0]; values are the
+// implicit iota 0..n-1.  After ceil(nbits/8) passes the keys are in sc.k[passes & 1] and the values in
+// sc.v[passes & 1].  With `gid_map` set, the last pass instead writes vals_final[pos] = gid_map[v] and
+// inv[v] = pos (the per-instance Gaussian id and the inverse permutation).
+void launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, const uint32_t *gid_map,
+                       uint32_t *vals_final, uint32_t *inv);
+
+// ---- forward (gsr_forward.hip) ----
+struct PreprocessParams {
+    int P, D, M, W, H, gx, gy;
+    float tan_fovx, tan_fovy, focal_x, focal_y, scale_modifier;
+    int antialiasing;
+    const float *means3D, *opacities, *scales, *rotations, *cov3D_precomp, *colors_precomp, *shs;
+    const float *view, *proj, *campos;
+    int *radii;
+    GeomState g;
+};
+void launch_preprocess(hipStream_t s, const PreprocessParams &p);
+
+struct ExpandParams {
+    uint32_t P, R;
+    int gx, gy;
+    const uint32_t *order, *inst_off, *tiles;
+    const float4 *rec_a;
+    const int *radii;
+    uint32_t *keys_out, *inst_gid, *inst_start;
+};
+void launch_expand(hipStream_t s, const ExpandParams &p);
+
+void launch_identify_ranges(hipStream_t s, const uint32_t *keys_sorted, uint32_t R, uint2 *ranges);
+
+struct RenderFwdParams {
+    int W, H, gx, gy, num_tiles;
+    const uint2 *ranges;
+    const uint32_t *point_list;
+    const float4 *rec_a, *rec_b;
+    const float2 *rec_c;
+    const float *bg;
+    float *out_color, *out_invdepth, *final_T;
+    uint32_t *n_contrib, *tile_last;
+};
+void launch_render_fwd(hipStream_t s, const RenderFwdParams &p);
+
+void launch_mark_visible(hipStream_t s, int P, const float *means3D, const float *view, uint8_t *present);
+
+// ---- backward (gsr_backward.hip) ----
+struct RenderBwdParams {
+    int W, H, gx, gy, num_tiles;
+    const uint2 *ranges;
+    const uint32_t *point_list, *n_contrib, *tile_last;
+    const float4 *rec_a, *rec_b;
+    const float2 *rec_c;
+    const float *bg, *final_T, *dL_dpix, *dL_dinvdepth;
+    float *rows;  // R x GRAD_ROW
+};
+void launch_render_bwd(hipStream_t s, const RenderBwdParams &p);
+
+struct BigReduceParams {
+    const uint32_t *counters, *big_list, *inst_start, *tiles, *inv;
+    float *rows;
+};
+void launch_big_reduce(hipStream_t s, const BigReduceParams &p, uint32_t max_big);
+
+struct PreprocessBwdParams {
+    int P, D, M, W, H;
+    float tan_fovx, tan_fovy, focal_x, focal_y, scale_modifier;
+    int antialiasing, has_invdepth;
+    const float *means3D, *opacities, *scales, *rotations, *cov3D_precomp, *shs;
+    const float *view, *proj, *campos;
+    const int *radii;
+    const uint32_t *tiles, *inst_start, *inv;
+    const uint8_t *clamped;
+    const float *rows;
+    float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales, *dL_drot;
+};
+void launch_preprocess_bwd(hipStream_t s, const PreprocessBwdParams &p);
+
+}  // namespace gsr

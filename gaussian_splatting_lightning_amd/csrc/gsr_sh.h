@@ -1,0 +1,125 @@
+// gsr_sh.h -- spherical-harmonics colour (degree <= 3) and its backward, compile-time degree.
+// Forward follows gs_lightning/utils/sh.py:41-98 + render_tools.py:118-131 of the reference
+// (+0.5 offset, clamp at 0, record the clamp); backward is the CUDA rule (clamped channels get zero
+// gradient, the view direction's normalisation is differentiated through dnormvdv).
+#pragma once
+#include "gsr_common.h"
+
+namespace gsr {
+
+__device__ __forceinline__ float3 f3(const float *p) { return make_float3(p[0], p[1], p[2]); }
+__device__ __forceinline__ float3 operator*(float a, float3 b) { return make_float3(a * b.x, a * b.y, a * b.z); }
+__device__ __forceinline__ float3 operator+(float3 a, float3 b) { return make_float3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ float3 operator-(float3 a, float3 b) { return make_float3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ float dot3(float3 a, float3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+
+template <int DEG>
+__device__ __forceinline__ float3 sh_eval(const float *__restrict__ sh, float3 dir) {
+    float3 res = GSR_SH_C0 * f3(sh);
+    if (DEG > 0) {
+        const float x = dir.x, y = dir.y, z = dir.z;
+        res = res - (GSR_SH_C1 * y) * f3(sh + 3) + (GSR_SH_C1 * z) * f3(sh + 6) - (GSR_SH_C1 * x) * f3(sh + 9);
+        if (DEG > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+            res = res + (SH_C2[0] * xy) * f3(sh + 12) + (SH_C2[1] * yz) * f3(sh + 15) +
+                  (SH_C2[2] * (2.0f * zz - xx - yy)) * f3(sh + 18) + (SH_C2[3] * xz) * f3(sh + 21) +
+                  (SH_C2[4] * (xx - yy)) * f3(sh + 24);
+            if (DEG > 2) {
+                res = res + (SH_C3[0] * y * (3.0f * xx - yy)) * f3(sh + 27) + (SH_C3[1] * xy * z) * f3(sh + 30) +
+                      (SH_C3[2] * y * (4.0f * zz - xx - yy)) * f3(sh + 33) +
+                      (SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy)) * f3(sh + 36) +
+                      (SH_C3[4] * x * (4.0f * zz - xx - yy)) * f3(sh + 39) +
+                      (SH_C3[5] * z * (xx - yy)) * f3(sh + 42) + (SH_C3[6] * x * (xx - 3.0f * yy)) * f3(sh + 45);
+            }
+        }
+    }
+    return res;
+}
+
+__device__ __forceinline__ float3 sh_dispatch(int deg, const float *__restrict__ sh, float3 dir) {
+    switch (deg) {
+        case 0: return sh_eval<0>(sh, dir);
+        case 1: return sh_eval<1>(sh, dir);
+        case 2: return sh_eval<2>(sh, dir);
+        default: return sh_eval<3>(sh, dir);
+    }
+}
+
+__device__ __forceinline__ float3 dnormvdv(float3 v, float3 dv) {
+    const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
+    const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+    return make_float3(((+sum2 - v.x * v.x) * dv.x - v.y * v.x * dv.y - v.z * v.x * dv.z) * invsum32,
+                       (-v.x * v.y * dv.x + (sum2 - v.y * v.y) * dv.y - v.z * v.y * dv.z) * invsum32,
+                       (-v.x * v.z * dv.x - v.y * v.z * dv.y + (sum2 - v.z * v.z) * dv.z) * invsum32);
+}
+
+__device__ __forceinline__ void st3(float *p, float3 v) {
+    p[0] = v.x;
+    p[1] = v.y;
+    p[2] = v.z;
+}
+
+// Writes dL/dsh for coefficients [0, (DEG+1)^2) and returns dL/dmean through the view direction.
+template <int DEG>
+__device__ __forceinline__ float3 sh_backward(const float *__restrict__ sh, float3 dir_orig, float3 dRGB,
+                                              float *__restrict__ dsh) {
+    const float len = sqrtf(dot3(dir_orig, dir_orig));
+    const float3 dir = make_float3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
+    float3 dx = make_float3(0, 0, 0), dy = dx, dz = dx;
+    const float x = dir.x, y = dir.y, z = dir.z;
+    st3(dsh, GSR_SH_C0 * dRGB);
+    if (DEG > 0) {
+        st3(dsh + 3, (-GSR_SH_C1 * y) * dRGB);
+        st3(dsh + 6, (GSR_SH_C1 * z) * dRGB);
+        st3(dsh + 9, (-GSR_SH_C1 * x) * dRGB);
+        dx = -GSR_SH_C1 * f3(sh + 9);
+        dy = -GSR_SH_C1 * f3(sh + 3);
+        dz = GSR_SH_C1 * f3(sh + 6);
+        if (DEG > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+            st3(dsh + 12, (SH_C2[0] * xy) * dRGB);
+            st3(dsh + 15, (SH_C2[1] * yz) * dRGB);
+            st3(dsh + 18, (SH_C2[2] * (2.f * zz - xx - yy)) * dRGB);
+            st3(dsh + 21, (SH_C2[3] * xz) * dRGB);
+            st3(dsh + 24, (SH_C2[4] * (xx - yy)) * dRGB);
+            const float3 s4 = f3(sh + 12), s5 = f3(sh + 15), s6 = f3(sh + 18), s7 = f3(sh + 21), s8 = f3(sh + 24);
+            dx = dx + (SH_C2[0] * y) * s4 + (SH_C2[2] * 2.f * -x) * s6 + (SH_C2[3] * z) * s7 + (SH_C2[4] * 2.f * x) * s8;
+            dy = dy + (SH_C2[0] * x) * s4 + (SH_C2[1] * z) * s5 + (SH_C2[2] * 2.f * -y) * s6 + (SH_C2[4] * 2.f * -y) * s8;
+            dz = dz + (SH_C2[1] * y) * s5 + (SH_C2[2] * 2.f * 2.f * z) * s6 + (SH_C2[3] * x) * s7;
+            if (DEG > 2) {
+                st3(dsh + 27, (SH_C3[0] * y * (3.f * xx - yy)) * dRGB);
+                st3(dsh + 30, (SH_C3[1] * xy * z) * dRGB);
+                st3(dsh + 33, (SH_C3[2] * y * (4.f * zz - xx - yy)) * dRGB);
+                st3(dsh + 36, (SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy)) * dRGB);
+                st3(dsh + 39, (SH_C3[4] * x * (4.f * zz - xx - yy)) * dRGB);
+                st3(dsh + 42, (SH_C3[5] * z * (xx - yy)) * dRGB);
+                st3(dsh + 45, (SH_C3[6] * x * (xx - 3.f * yy)) * dRGB);
+                const float3 s9 = f3(sh + 27), s10 = f3(sh + 30), s11 = f3(sh + 33), s12 = f3(sh + 36),
+                             s13 = f3(sh + 39), s14 = f3(sh + 42), s15 = f3(sh + 45);
+                dx = dx + (SH_C3[0] * 3.f * 2.f * xy) * s9 + (SH_C3[1] * yz) * s10 + (SH_C3[2] * -2.f * xy) * s11 +
+                     (SH_C3[3] * -3.f * 2.f * xz) * s12 + (SH_C3[4] * (-3.f * xx + 4.f * zz - yy)) * s13 +
+                     (SH_C3[5] * 2.f * xz) * s14 + (SH_C3[6] * 3.f * (xx - yy)) * s15;
+                dy = dy + (SH_C3[0] * 3.f * (xx - yy)) * s9 + (SH_C3[1] * xz) * s10 +
+                     (SH_C3[2] * (-3.f * yy + 4.f * zz - xx)) * s11 + (SH_C3[3] * -3.f * 2.f * yz) * s12 +
+                     (SH_C3[4] * -2.f * xy) * s13 + (SH_C3[5] * -2.f * yz) * s14 + (SH_C3[6] * -3.f * 2.f * xy) * s15;
+                dz = dz + (SH_C3[1] * xy) * s10 + (SH_C3[2] * 4.f * 2.f * yz) * s11 +
+                     (SH_C3[3] * 3.f * (2.f * zz - xx - yy)) * s12 + (SH_C3[4] * 4.f * 2.f * xz) * s13 +
+                     (SH_C3[5] * (xx - yy)) * s14;
+            }
+        }
+    }
+    const float3 dL_ddir = make_float3(dot3(dx, dRGB), dot3(dy, dRGB), dot3(dz, dRGB));
+    return dnormvdv(dir_orig, dL_ddir);
+}
+
+__device__ __forceinline__ float3 sh_backward_dispatch(int deg, const float *__restrict__ sh, float3 dir_orig,
+                                                       float3 dRGB, float *__restrict__ dsh) {
+    switch (deg) {
+        case 0: return sh_backward<0>(sh, dir_orig, dRGB, dsh);
+        case 1: return sh_backward<1>(sh, dir_orig, dRGB, dsh);
+        case 2: return sh_backward<2>(sh, dir_orig, dRGB, dsh);
+        default: return sh_backward<3>(sh, dir_orig, dRGB, dsh);
+    }
+}
+
+}  // namespace gsr

@@ -1,0 +1,282 @@
+// gsr_sort.hip -- device-wide exclusive scan and LSD radix sort for the binning stage.
+//
+// Replaces the reference's cub::DeviceScan::InclusiveSum over tiles_touched and
+// cub::DeviceRadixSort::SortPairs over (tile << 32 | depth) keys.  The MI355X design
+// splits that 45-bit sort in two cheaper ones (see DESIGN.md "Binning"):
+//   * a 32-bit depth sort over the P Gaussians (4 passes over P, not over the ~6.5x larger instance list),
+//   * a stable tile-id sort (ceil(log2 T) bits, 2 passes at 1080p) over the instances, which are
+//     expanded in depth order, so the result equals the reference's stable (tile, depth, index) order.
+// Each pass is histogram -> scan of the [digit][block] counts -> stable scatter.  The scatter ranks
+// keys inside a wave with eight 64-lane ballots (wave64 multisplit), keeps per-wave digit counters in
+// LDS, stages the block's output in LDS, and writes each digit's run contiguously.
+#include "gsr_kernels.h"
+
+namespace gsr {
+
+// ------------------------------------------------------------------------------------------------
+// exclusive scan
+// ------------------------------------------------------------------------------------------------
+template <bool GATHER>
+__device__ __forceinline__ uint32_t scan_load(const uint32_t *__restrict__ in, const uint32_t *__restrict__ idx,
+                                              uint32_t j) {
+    return GATHER ? in[idx[j]] : in[j];
+}
+
+template <bool GATHER>
+__global__ __launch_bounds__(256) void scan_reduce_kernel(const uint32_t *__restrict__ in,
+                                                          const uint32_t *__restrict__ idx, uint32_t n,
+                                                          uint32_t *__restrict__ block_sums) {
+    __shared__ uint32_t s_w[4];
+    const uint32_t base = blockIdx.x * SCAN_TILE;
+    uint32_t sum = 0;
+    for (int i = threadIdx.x; i < SCAN_TILE; i += 256) {
+        const uint32_t j = base + i;
+        if (j < n) sum += scan_load<GATHER>(in, idx, j);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += (uint32_t)__shfl_xor((int)sum, o);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) block_sums[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+// One block of 1024 threads scans up to SCAN_MAX_BLOCKS block sums in place (exclusive).
+__global__ __launch_bounds__(1024) void scan_sums_kernel(uint32_t *__restrict__ sums, uint32_t nb,
+                                                         uint32_t *__restrict__ total_out,
+                                                         uint32_t *__restrict__ overflow) {
+    __shared__ unsigned long long s_w[16];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    constexpr int PER = SCAN_MAX_BLOCKS / 1024;
+    uint32_t v[PER];
+    unsigned long long local = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const uint32_t j = tid * PER + k;
+        v[k] = j < nb ? sums[j] : 0u;
+        local += v[k];
+    }
+    // inclusive scan of 64-bit thread totals across the block
+    unsigned long long inc = local;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        unsigned long long t = __shfl_up(inc, o);
+        if (lane >= o) inc += t;
+    }
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    unsigned long long woff = 0;
+    for (int i = 0; i < w; i++) woff += s_w[i];
+    unsigned long long run = woff + inc - local;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const uint32_t j = tid * PER + k;
+        if (j < nb) sums[j] = (uint32_t)run;
+        run += v[k];
+    }
+    if (tid == 1023) {
+        if (total_out) *total_out = (uint32_t)run;
+        if (overflow && run > 0xffffffffull) *overflow = 1u;
+    }
+}
+
+template <bool GATHER>
+__global__ __launch_bounds__(256) void scan_down_kernel(const uint32_t *__restrict__ in,
+                                                        const uint32_t *__restrict__ idx, uint32_t n,
+                                                        const uint32_t *__restrict__ block_off,
+                                                        uint32_t *__restrict__ out) {
+    __shared__ uint32_t s_w[4];
+    constexpr int PER = SCAN_TILE / 256;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t base = blockIdx.x * SCAN_TILE + tid * PER;
+    uint32_t v[PER];
+    uint32_t local = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const uint32_t j = base + k;
+        v[k] = j < n ? scan_load<GATHER>(in, idx, j) : 0u;
+        local += v[k];
+    }
+    uint32_t inc = wave_inclusive_scan(local, lane);
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    uint32_t run = block_off[blockIdx.x] + inc - local;
+    for (int i = 0; i < w; i++) run += s_w[i];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const uint32_t j = base + k;
+        if (j < n) out[j] = run;
+        run += v[k];
+    }
+}
+
+void launch_exclusive_scan(hipStream_t s, const uint32_t *in, const uint32_t *idx, uint32_t n, uint32_t *out,
+                           uint32_t *block_tmp, uint32_t *overflow_flag) {
+    if (n == 0) {
+        (void)hipMemsetAsync(out, 0, sizeof(uint32_t), s);
+        return;
+    }
+    const uint32_t nb = div_up(n, SCAN_TILE);
+    if (idx) {
+        scan_reduce_kernel<true><<<nb, 256, 0, s>>>(in, idx, n, block_tmp);
+        scan_sums_kernel<<<1, 1024, 0, s>>>(block_tmp, nb, out + n, overflow_flag);
+        scan_down_kernel<true><<<nb, 256, 0, s>>>(in, idx, n, block_tmp, out);
+    } else {
+        scan_reduce_kernel<false><<<nb, 256, 0, s>>>(in, nullptr, n, block_tmp);
+        scan_sums_kernel<<<1, 1024, 0, s>>>(block_tmp, nb, out + n, overflow_flag);
+        scan_down_kernel<false><<<nb, 256, 0, s>>>(in, nullptr, n, block_tmp, out);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// radix sort pass: histogram
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rs_hist_kernel(const uint32_t *__restrict__ keys, uint32_t n, int shift,
+                                                      uint32_t *__restrict__ counts, uint32_t nb) {
+    __shared__ uint32_t h[4][RS_BINS];
+    const int tid = threadIdx.x, w = tid >> 6;
+    for (int i = tid; i < 4 * RS_BINS; i += 256) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * RS_TILE;
+    if (base + RS_TILE <= n) {
+        const uint4 *k4 = reinterpret_cast<const uint4 *>(keys + base);
+#pragma unroll
+        for (int i = 0; i < RS_TILE / 4 / 256; i++) {
+            const uint4 q = k4[i * 256 + tid];
+            atomicAdd(&h[w][(q.x >> shift) & 255u], 1u);
+            atomicAdd(&h[w][(q.y >> shift) & 255u], 1u);
+            atomicAdd(&h[w][(q.z >> shift) & 255u], 1u);
+            atomicAdd(&h[w][(q.w >> shift) & 255u], 1u);
+        }
+    } else {
+        for (int i = tid; i < RS_TILE; i += 256) {
+            const uint32_t j = base + i;
+            if (j < n) atomicAdd(&h[w][(keys[j] >> shift) & 255u], 1u);
+        }
+    }
+    __syncthreads();
+    counts[(size_t)tid * nb + blockIdx.x] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+}
+
+// ------------------------------------------------------------------------------------------------
+// radix sort pass: stable scatter
+// ------------------------------------------------------------------------------------------------
+template <bool IOTA_IN, bool EPILOGUE>
+__global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restrict__ keys_in,
+                                                         const uint32_t *__restrict__ vals_in, uint32_t n,
+                                                         int shift, const uint32_t *__restrict__ counts_scanned,
+                                                         uint32_t nb, uint32_t *__restrict__ keys_out,
+                                                         uint32_t *__restrict__ vals_out,
+                                                         const uint32_t *__restrict__ gid_map,
+                                                         uint32_t *__restrict__ inv_out) {
+    __shared__ uint32_t s_cnt[4][RS_BINS];  // per-wave running digit counts, then per-wave bases
+    __shared__ uint32_t s_dstart[RS_BINS];  // block-local start of each digit's run
+    __shared__ uint32_t s_gbase[RS_BINS];   // global start of this block's run of each digit
+    __shared__ uint32_t s_wsum[4];
+    __shared__ uint32_t s_keys[RS_TILE];
+    __shared__ uint32_t s_vals[RS_TILE];
+
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const uint32_t blk = blockIdx.x * RS_TILE;
+    for (int i = tid; i < 4 * RS_BINS; i += 256) (&s_cnt[0][0])[i] = 0;
+    __syncthreads();
+
+    // Each wave ranks a contiguous segment of 1024 keys, 64 at a time, in input order (stable).
+    uint32_t key[RS_ITEMS], val[RS_ITEMS], rank[RS_ITEMS];
+    const uint64_t lt = lanemask_lt(lane);
+#pragma unroll
+    for (int it = 0; it < RS_ITEMS; it++) {
+        const uint32_t j = blk + w * (RS_TILE / 4) + it * 64 + lane;
+        const bool valid = j < n;
+        const uint32_t k = valid ? keys_in[j] : 0u;
+        const uint32_t v = IOTA_IN ? j : (valid ? vals_in[j] : 0u);
+        const uint32_t d = (k >> shift) & 255u;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < 8; bit++) {
+            const bool set = (d >> bit) & 1u;
+            const uint64_t m = __ballot(set);
+            peers &= set ? m : ~m;
+        }
+        uint32_t r = 0;
+        if (valid) {
+            const uint32_t before = s_cnt[w][d];
+            const uint64_t lower = peers & lt;
+            r = before + (uint32_t)__popcll(lower);
+            if (lower == 0) s_cnt[w][d] = before + (uint32_t)__popcll(peers);
+        }
+        key[it] = k;
+        val[it] = v;
+        rank[it] = r;
+    }
+    __syncthreads();
+    {
+        const int d = tid;
+        const uint32_t c0 = s_cnt[0][d], c1 = s_cnt[1][d], c2 = s_cnt[2][d], c3 = s_cnt[3][d];
+        s_cnt[0][d] = 0;
+        s_cnt[1][d] = c0;
+        s_cnt[2][d] = c0 + c1;
+        s_cnt[3][d] = c0 + c1 + c2;
+        const uint32_t tot = c0 + c1 + c2 + c3;
+        const uint32_t inc = wave_inclusive_scan(tot, lane);
+        if (lane == 63) s_wsum[w] = inc;
+        __syncthreads();
+        uint32_t woff = 0;
+        for (int i = 0; i < w; i++) woff += s_wsum[i];
+        s_dstart[d] = woff + inc - tot;
+        s_gbase[d] = counts_scanned[(size_t)d * nb + blockIdx.x];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < RS_ITEMS; it++) {
+        const uint32_t j = blk + w * (RS_TILE / 4) + it * 64 + lane;
+        if (j < n) {
+            const uint32_t d = (key[it] >> shift) & 255u;
+            const uint32_t pos = s_dstart[d] + s_cnt[w][d] + rank[it];
+            s_keys[pos] = key[it];
+            s_vals[pos] = val[it];
+        }
+    }
+    __syncthreads();
+    const uint32_t cnt_blk = min((uint32_t)RS_TILE, n - blk);
+    for (uint32_t i = tid; i < cnt_blk; i += 256) {
+        const uint32_t k = s_keys[i], v = s_vals[i];
+        const uint32_t d = (k >> shift) & 255u;
+        const uint32_t gpos = s_gbase[d] + (i - s_dstart[d]);
+        keys_out[gpos] = k;
+        if (EPILOGUE) {
+            vals_out[gpos] = gid_map[v];
+            inv_out[v] = gpos;
+        } else {
+            vals_out[gpos] = v;
+        }
+    }
+}
+
+void launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, const uint32_t *gid_map,
+                       uint32_t *vals_final, uint32_t *inv) {
+    if (n == 0) return;
+    const uint32_t nb = div_up(n, RS_TILE);
+    const int passes = radix_passes(nbits);
+    for (int p = 0; p < passes; p++) {
+        const int shift = 8 * p, in = p & 1, out = (p + 1) & 1;
+        const bool first = p == 0, last = p == passes - 1;
+        rs_hist_kernel<<<nb, 256, 0, s>>>(sc.k[in], n, shift, sc.counts, nb);
+        launch_exclusive_scan(s, sc.counts, nullptr, RS_BINS * nb, sc.counts, sc.scan_tmp, nullptr);
+        const bool epi = last && gid_map != nullptr;
+        uint32_t *vout = epi ? vals_final : sc.v[out];
+        if (first && epi)
+            rs_scatter_kernel<true, true><<<nb, 256, 0, s>>>(sc.k[in], nullptr, n, shift, sc.counts, nb, sc.k[out],
+                                                             vout, gid_map, inv);
+        else if (first)
+            rs_scatter_kernel<true, false><<<nb, 256, 0, s>>>(sc.k[in], nullptr, n, shift, sc.counts, nb,
+                                                              sc.k[out], vout, nullptr, nullptr);
+        else if (epi)
+            rs_scatter_kernel<false, true><<<nb, 256, 0, s>>>(sc.k[in], sc.v[in], n, shift, sc.counts, nb,
+                                                              sc.k[out], vout, gid_map, inv);
+        else
+            rs_scatter_kernel<false, false><<<nb, 256, 0, s>>>(sc.k[in], sc.v[in], n, shift, sc.counts, nb,
+                                                               sc.k[out], vout, nullptr, nullptr);
+    }
+}
+
+}  // namespace gsr

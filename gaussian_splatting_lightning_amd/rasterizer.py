@@ -1,0 +1,272 @@
+"""Host-side mirror of the `diff_gaussian_rasterization` Python API, backed by libgsrast.so.
+
+The reference calls this API at
+    gs_lightning/lightning/gs_lightning_module.py:322-348   (training: settings, rasterizer(...), means2D grad)
+    scripts/render_trained_image.py:98-124                  (inference: means2D=None)
+    tests/rasterizer_python/test_mark_visible.py:13-14       (GaussianRasterizer(s).markVisible(points))
+The names, argument meaning, return values and error behaviour are those of the upstream package
+(graphdeco-inria/diff-gaussian-rasterization@dr_aa):
+    GaussianRasterizationSettings   13-field NamedTuple
+    GaussianRasterizer(settings)(means3D, means2D, opacities, shs, colors_precomp, scales, rotations,
+                                 cov3D_precomp) -> (color (3,H,W), radii (P,) int32, invdepth (1,H,W))
+    GaussianRasterizer.markVisible(positions) -> bool (P,)
+    rasterize_gaussians(...)        functional form
+Every computation runs in the HIP kernels on the tensors' device; the scratch state the backward needs
+(geometry/binning/image buffers) lives in uint8 tensors saved on the autograd context.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import NamedTuple, Optional
+
+import torch
+import torch.nn as nn
+
+from . import _native
+
+
+class GaussianRasterizationSettings(NamedTuple):
+    image_height: int
+    image_width: int
+    tanfovx: float
+    tanfovy: float
+    bg: torch.Tensor
+    scale_modifier: float
+    viewmatrix: torch.Tensor
+    projmatrix: torch.Tensor
+    sh_degree: int
+    campos: torch.Tensor
+    prefiltered: bool
+    debug: bool
+    antialiasing: bool
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    if t is None or t.numel() == 0:
+        return None
+    return t.data_ptr()
+
+
+def _prep(t: Optional[torch.Tensor], device, name: str) -> Optional[torch.Tensor]:
+    if t is None or t.numel() == 0:
+        return None
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{name} must be float32 (got {t.dtype})")
+    if t.device != device:
+        t = t.to(device)
+    return t.contiguous()
+
+
+class _Buffers:
+    """Caller-owned scratch buffers grown through the C callback (reference: resizeFunctional)."""
+
+    def __init__(self, device):
+        self.device = device
+        self.bufs = {}
+        self._cb = _native.ALLOC_FN(self._alloc)
+
+    def _alloc(self, _ctx, which, nbytes):
+        t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=self.device)
+        self.bufs[int(which)] = t
+        return t.data_ptr()
+
+    @property
+    def callback(self):
+        return self._cb
+
+    def get(self, which) -> torch.Tensor:
+        t = self.bufs.get(which)
+        return t if t is not None else torch.empty(0, dtype=torch.uint8, device=self.device)
+
+
+def _stream_handle(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class ForwardState(NamedTuple):
+    """Everything the backward needs from one forward call (tensors kept alive by autograd)."""
+    means3D: torch.Tensor
+    shs: Optional[torch.Tensor]
+    colors_precomp: Optional[torch.Tensor]
+    opacities: torch.Tensor
+    scales: Optional[torch.Tensor]
+    rotations: Optional[torch.Tensor]
+    cov3D_precomp: Optional[torch.Tensor]
+    radii: torch.Tensor
+    bg: torch.Tensor
+    viewmatrix: torch.Tensor
+    projmatrix: torch.Tensor
+    campos: Optional[torch.Tensor]
+    geom_buffer: torch.Tensor
+    binning_buffer: torch.Tensor
+    image_buffer: torch.Tensor
+    num_rendered: int
+    M: int
+
+
+def forward_raw(means3D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, raster_settings):
+    """One call of gsr_forward.  Returns (color (3,H,W), radii (P,), invdepth (1,H,W), ForwardState)."""
+    lib = _native.load()
+    device = means3D.device
+    if device.type != "cuda":
+        raise RuntimeError("the MI355X rasterizer needs its inputs on a HIP device (tensor.device.type == 'cuda')")
+    if means3D.ndim != 2 or means3D.shape[1] != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    rs = raster_settings
+    P = means3D.shape[0]
+    H, W = int(rs.image_height), int(rs.image_width)
+    means3D_c = _prep(means3D, device, "means3D")
+    sh_c = _prep(sh, device, "shs")
+    col_c = _prep(colors_precomp, device, "colors_precomp")
+    op_c = _prep(opacities, device, "opacities")
+    sc_c = _prep(scales, device, "scales")
+    rot_c = _prep(rotations, device, "rotations")
+    cov_c = _prep(cov3Ds_precomp, device, "cov3D_precomp")
+    bg = _prep(rs.bg, device, "bg")
+    view = _prep(rs.viewmatrix, device, "viewmatrix")
+    proj = _prep(rs.projmatrix, device, "projmatrix")
+    campos = _prep(rs.campos, device, "campos")
+    M = 0 if sh_c is None else (sh_c.shape[1] if sh_c.ndim == 3 else sh_c.shape[1] // 3)
+
+    color = torch.zeros(3, H, W, dtype=torch.float32, device=device)
+    invdepth = torch.zeros(1, H, W, dtype=torch.float32, device=device)
+    radii = torch.zeros(P, dtype=torch.int32, device=device)
+    bufs = _Buffers(device)
+    a = _native.ForwardArgs(
+        P=P, D=int(rs.sh_degree), M=M, W=W, H=H, background=_ptr(bg), means3D=_ptr(means3D_c),
+        colors_precomp=_ptr(col_c), opacities=_ptr(op_c), scales=_ptr(sc_c),
+        scale_modifier=float(rs.scale_modifier), rotations=_ptr(rot_c), cov3D_precomp=_ptr(cov_c),
+        viewmatrix=_ptr(view), projmatrix=_ptr(proj), campos=_ptr(campos), tan_fovx=float(rs.tanfovx),
+        tan_fovy=float(rs.tanfovy), shs=_ptr(sh_c), prefiltered=int(bool(rs.prefiltered)),
+        antialiasing=int(bool(rs.antialiasing)), debug=int(bool(rs.debug)), out_color=color.data_ptr(),
+        out_invdepth=invdepth.data_ptr(), radii=radii.data_ptr())
+    num_rendered = ctypes.c_int64(0)
+    rc = lib.gsr_forward(ctypes.byref(a), bufs.callback, None, _stream_handle(device), ctypes.byref(num_rendered))
+    _native.check(rc, "rasterize_gaussians")
+    state = ForwardState(means3D_c, sh_c, col_c, op_c, sc_c, rot_c, cov_c, radii, bg, view, proj, campos,
+                         bufs.get(_native.GSR_BUF_GEOM), bufs.get(_native.GSR_BUF_BINNING),
+                         bufs.get(_native.GSR_BUF_IMAGE), int(num_rendered.value), M)
+    return color, radii, invdepth, state
+
+
+def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_depth=None):
+    """One call of gsr_backward.  Returns a dict of gradients (means3D, means2D, shs, colors_precomp,
+    opacities, scales, rotations, cov3D_precomp); entries are None where the input was absent."""
+    lib = _native.load()
+    rs = raster_settings
+    st = state
+    device = st.means3D.device
+    P = st.means3D.shape[0]
+    M = st.M
+    H, W = int(rs.image_height), int(rs.image_width)
+    if grad_out_color is None:
+        grad_out_color = torch.zeros(3, H, W, dtype=torch.float32, device=device)
+    grad_out_color = grad_out_color.to(torch.float32).contiguous()
+    if grad_out_depth is not None:
+        grad_out_depth = grad_out_depth.to(torch.float32).contiguous()
+    f32 = dict(dtype=torch.float32, device=device)
+    dmeans2D = torch.empty(P, 3, **f32)
+    dcolors = torch.empty(P, 3, **f32)
+    dopac = torch.empty(P, 1, **f32)
+    dmeans3D = torch.empty(P, 3, **f32)
+    dcov = torch.empty(P, 6, **f32)
+    dsh = torch.empty(P, max(M, 0), 3, **f32)
+    dscales = torch.empty(P, 3, **f32)
+    drot = torch.empty(P, 4, **f32)
+    bufs = _Buffers(device)
+    a = _native.BackwardArgs(
+        P=P, D=int(rs.sh_degree), M=M, W=W, H=H, R=st.num_rendered, background=_ptr(st.bg),
+        means3D=_ptr(st.means3D), colors_precomp=_ptr(st.colors_precomp), opacities=_ptr(st.opacities),
+        scales=_ptr(st.scales), scale_modifier=float(rs.scale_modifier), rotations=_ptr(st.rotations),
+        cov3D_precomp=_ptr(st.cov3D_precomp), viewmatrix=_ptr(st.viewmatrix), projmatrix=_ptr(st.projmatrix),
+        campos=_ptr(st.campos), tan_fovx=float(rs.tanfovx), tan_fovy=float(rs.tanfovy),
+        dL_dpix=grad_out_color.data_ptr(), dL_dinvdepth=_ptr(grad_out_depth), shs=_ptr(st.shs),
+        radii=_ptr(st.radii), geom_buffer=_ptr(st.geom_buffer), binning_buffer=_ptr(st.binning_buffer),
+        image_buffer=_ptr(st.image_buffer), antialiasing=int(bool(rs.antialiasing)), debug=int(bool(rs.debug)),
+        dL_dmeans2D=dmeans2D.data_ptr(), dL_dcolors=dcolors.data_ptr(), dL_dopacity=dopac.data_ptr(),
+        dL_dmeans3D=dmeans3D.data_ptr(), dL_dcov3D=dcov.data_ptr(), dL_dsh=_ptr(dsh),
+        dL_dscales=dscales.data_ptr(), dL_drotations=drot.data_ptr())
+    rc = lib.gsr_backward(ctypes.byref(a), bufs.callback, None, _stream_handle(device))
+    _native.check(rc, "rasterize_gaussians_backward")
+    return dict(
+        means3D=dmeans3D, means2D=dmeans2D,
+        shs=dsh.view_as(st.shs) if st.shs is not None else None,
+        colors_precomp=dcolors if st.colors_precomp is not None else None,
+        colors=dcolors, opacities=dopac.view_as(st.opacities),
+        scales=dscales if st.scales is not None else None,
+        rotations=drot if st.rotations is not None else None,
+        cov3D_precomp=dcov if st.cov3D_precomp is not None else None, cov3D=dcov)
+
+
+class _RasterizeGaussians(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                raster_settings):
+        color, radii, invdepth, st = forward_raw(means3D, sh, colors_precomp, opacities, scales, rotations,
+                                                 cov3Ds_precomp, raster_settings)
+        ctx.raster_settings = raster_settings
+        ctx.meta = (st.num_rendered, st.M)
+        ctx.present = tuple(t is not None for t in st)
+        empty = torch.empty(0, device=means3D.device)
+        ctx.save_for_backward(*[(t if t is not None else empty) for t in st[:15]])
+        ctx.set_materialize_grads(False)
+        return color, radii, invdepth
+
+    @staticmethod
+    def backward(ctx, grad_out_color, _grad_radii, grad_out_depth):
+        saved = ctx.saved_tensors
+        tensors = [t if present else None for t, present in zip(saved, ctx.present[:15])]
+        st = ForwardState(*tensors, *ctx.meta)
+        g = backward_raw(st, ctx.raster_settings, grad_out_color, grad_out_depth)
+        need = ctx.needs_input_grad
+        return (g["means3D"] if need[0] else None,
+                g["means2D"] if need[1] else None,
+                g["shs"] if need[2] else None,
+                g["colors_precomp"] if need[3] else None,
+                g["opacities"] if need[4] else None,
+                g["scales"] if need[5] else None,
+                g["rotations"] if need[6] else None,
+                g["cov3D_precomp"] if need[7] else None,
+                None)
+
+
+def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                        raster_settings):
+    return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
+                                     cov3Ds_precomp, raster_settings)
+
+
+def mark_visible(positions: torch.Tensor, viewmatrix: torch.Tensor, projmatrix: torch.Tensor) -> torch.Tensor:
+    lib = _native.load()
+    device = positions.device
+    pos = _prep(positions, device, "positions")
+    view = _prep(viewmatrix, device, "viewmatrix")
+    proj = _prep(projmatrix, device, "projmatrix")
+    P = positions.shape[0]
+    present = torch.zeros(P, dtype=torch.bool, device=device)
+    if P:
+        rc = lib.gsr_mark_visible(P, _ptr(pos), _ptr(view), _ptr(proj), present.data_ptr(), _stream_handle(device))
+        _native.check(rc, "mark_visible")
+    return present
+
+
+class GaussianRasterizer(nn.Module):
+    def __init__(self, raster_settings: GaussianRasterizationSettings):
+        super().__init__()
+        self.raster_settings = raster_settings
+
+    def markVisible(self, positions: torch.Tensor) -> torch.Tensor:
+        with torch.no_grad():
+            rs = self.raster_settings
+            return mark_visible(positions, rs.viewmatrix, rs.projmatrix)
+
+    def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
+                cov3D_precomp=None):
+        rs = self.raster_settings
+        if (shs is None and colors_precomp is None) or (shs is not None and colors_precomp is not None):
+            raise Exception("Please provide excatly one of either SHs or precomputed colors!")
+        if ((scales is None or rotations is None) and cov3D_precomp is None) or (
+                (scales is not None or rotations is not None) and cov3D_precomp is not None):
+            raise Exception("Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!")
+        return rasterize_gaussians(means3D, means2D, shs, colors_precomp, opacities, scales, rotations,
+                                   cov3D_precomp, rs)

@@ -1,0 +1,154 @@
+/*
+ * gsrast.h -- C ABI of the MI355X-native differentiable Gaussian rasterizer.
+ *
+ * This is the drop-in boundary for the hot path that pomelyu/gaussian_splatting_lightning reaches
+ * through `diff_gaussian_rasterization` (reference call sites:
+ *   gs_lightning/lightning/gs_lightning_module.py:322-348   GaussianRasterizationSettings + GaussianRasterizer
+ *   scripts/render_trained_image.py:98-124                  inference call, means2D=None
+ *   tests/rasterizer_python/test_mark_visible.py:13-14      GaussianRasterizer(s).markVisible(points)).
+ * The submodule that normally implements it (graphdeco-inria/diff-gaussian-rasterization@dr_aa,
+ * .gitmodules:1-4) is not vendored; each entry point below replaces one of its pybind exports
+ * (`_C.rasterize_gaussians`, `_C.rasterize_gaussians_backward`, `_C.mark_visible`, SURVEY.md §2.1 and
+ * §8(b)).  Signatures are plain C: device pointers, sizes and a hipStream_t passed as void*.  No torch
+ * types cross this boundary; the Python host layer (gaussian_splatting_lightning_amd/rasterizer.py)
+ * binds it with ctypes.
+ *
+ * Conventions (identical to the reference's torch API):
+ *   means3D (P,3), opacities (P,1), scales (P,3), rotations (P,4) as (w,x,y,z), shs (P,M,3),
+ *   colors_precomp (P,3), cov3D_precomp (P,6) upper triangle, viewmatrix / projmatrix (4,4) row-major
+ *   in the row-vector convention (p_view = [p,1] @ V), campos (3), background (3);
+ *   out_color (3,H,W), out_invdepth (1,H,W), radii (P) int32.
+ * All pointers are DEVICE pointers (fp32, contiguous) unless stated; every launch goes on `stream`.
+ * Return value: 0 on success, nonzero error code; gsr_last_error() gives the message.
+ */
+#ifndef GSRAST_H
+#define GSRAST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Scratch buffers are owned by the caller and grown through this callback, mirroring the
+ * reference's resizeFunctional() lambdas over uint8 torch tensors (notes/rasterizer_note.h:27-40).
+ * `which` is one of GSR_BUF_*; the callback returns a device pointer to >= nbytes bytes that stays
+ * valid until the caller frees it (the forward's three buffers must survive until the backward). */
+typedef char *(*gsr_alloc_fn)(void *ctx, int which, size_t nbytes);
+
+enum { GSR_BUF_GEOM = 0, GSR_BUF_BINNING = 1, GSR_BUF_IMAGE = 2, GSR_BUF_BWD_SCRATCH = 3 };
+
+enum {
+    GSR_OK = 0,
+    GSR_ERR_ARG = 1,      /* invalid shape/pointer/option (RuntimeError in Python) */
+    GSR_ERR_HIP = 2,      /* HIP runtime error */
+    GSR_ERR_ALLOC = 3,    /* allocation callback returned NULL */
+    GSR_ERR_OVERFLOW = 4, /* more than 2^32-1 tile instances */
+    GSR_ERR_UNSUPPORTED = 5
+};
+
+typedef struct gsr_forward_args {
+    int P;                        /* number of Gaussians */
+    int D;                        /* active SH degree (0..3) */
+    int M;                        /* SH coefficients stored per Gaussian (shs.size(1)), 0 if none */
+    int W, H;                     /* image size */
+    const float *background;      /* (3) */
+    const float *means3D;         /* (P,3) */
+    const float *colors_precomp;  /* (P,3) or NULL (then shs is required) */
+    const float *opacities;       /* (P) */
+    const float *scales;          /* (P,3) or NULL (then cov3D_precomp is required) */
+    float scale_modifier;
+    const float *rotations;       /* (P,4) or NULL */
+    const float *cov3D_precomp;   /* (P,6) or NULL */
+    const float *viewmatrix;      /* (16) */
+    const float *projmatrix;      /* (16) */
+    const float *campos;          /* (3) */
+    float tan_fovx, tan_fovy;
+    const float *shs;             /* (P,M,3) or NULL */
+    int prefiltered;              /* accepted; the frustum test is applied either way */
+    int antialiasing;             /* EWA 2D filter opacity compensation (dr_aa) */
+    int debug;                    /* synchronise + check after every stage */
+    float *out_color;             /* (3,H,W) */
+    float *out_invdepth;          /* (H,W) or NULL */
+    int *radii;                   /* (P) */
+} gsr_forward_args;
+
+/* Replaces `_C.rasterize_gaussians` (rasterize_points.cu RasterizeGaussiansCUDA -> Rasterizer::forward).
+ * Runs preprocess, depth sort, scan, one device->host read of the instance count, tile expansion,
+ * tile sort, range identification and compositing.  *num_rendered receives the instance count. */
+int gsr_forward(const gsr_forward_args *args, gsr_alloc_fn alloc, void *alloc_ctx, void *stream,
+                int64_t *num_rendered);
+
+typedef struct gsr_backward_args {
+    int P, D, M, W, H;
+    int64_t R;                    /* num_rendered returned by gsr_forward */
+    const float *background;
+    const float *means3D;
+    const float *colors_precomp;  /* or NULL */
+    const float *opacities;
+    const float *scales;          /* or NULL */
+    float scale_modifier;
+    const float *rotations;       /* or NULL */
+    const float *cov3D_precomp;   /* or NULL */
+    const float *viewmatrix, *projmatrix, *campos;
+    float tan_fovx, tan_fovy;
+    const float *dL_dpix;         /* (3,H,W) */
+    const float *dL_dinvdepth;    /* (H,W) or NULL */
+    const float *shs;             /* or NULL */
+    const int *radii;             /* (P) from the forward */
+    char *geom_buffer, *binning_buffer, *image_buffer; /* from the forward */
+    int antialiasing, debug;
+    /* outputs, each fully written (no pre-zeroing needed); any may be NULL to skip it */
+    float *dL_dmeans2D;           /* (P,3), z = 0, NDC units (pixel grad * (W/2, H/2)) */
+    float *dL_dcolors;            /* (P,3) */
+    float *dL_dopacity;           /* (P) */
+    float *dL_dmeans3D;           /* (P,3) */
+    float *dL_dcov3D;             /* (P,6) */
+    float *dL_dsh;                /* (P,M,3) */
+    float *dL_dscales;            /* (P,3) */
+    float *dL_drotations;         /* (P,4) */
+} gsr_backward_args;
+
+/* Replaces `_C.rasterize_gaussians_backward` (RasterizeGaussiansBackwardCUDA -> Rasterizer::backward).
+ * Deterministic: per-tile gradient rows are reduced in fixed order (no float atomics). */
+int gsr_backward(const gsr_backward_args *args, gsr_alloc_fn alloc, void *alloc_ctx, void *stream);
+
+/* Replaces `_C.mark_visible` (checkFrustum): present[i] = z_view(means3D[i]) > 0.2. */
+int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
+                     uint8_t *present, void *stream);
+
+/* Buffer sizes the forward will request (host-only arithmetic; for planning and tests). */
+size_t gsr_geom_buffer_bytes(int P);
+size_t gsr_binning_buffer_bytes(int64_t R, int W, int H);
+size_t gsr_image_buffer_bytes(int W, int H);
+size_t gsr_bwd_scratch_bytes(int P, int64_t R);
+
+/* Byte offsets of the internal arrays inside the three forward buffers (host arithmetic only).  Used by
+ * the parity tests to compare the integer binning state (sorted instance list, tile ranges,
+ * per-pixel contributor counts) bit for bit against the oracle. */
+typedef struct gsr_state_layout {
+    size_t geom_rec_a, geom_rec_b, geom_rec_c; /* float4, float4, float2 per Gaussian */
+    size_t geom_tiles, geom_order, geom_inst_off, geom_inst_start, geom_clamped; /* u32, u32, u32, u32, u8 */
+    size_t geom_sorted_depth; /* u32 depth bits in depth-rank order (depth of order[r]) */
+    size_t bin_point_list, bin_inv, bin_keys_sorted;                  /* u32 per instance */
+    size_t img_final_T, img_n_contrib, img_ranges, img_tile_last;     /* f32/u32 per pixel, uint2/u32 per tile */
+} gsr_state_layout;
+void gsr_state_layout_query(int P, int64_t R, int W, int H, gsr_state_layout *out);
+
+/* Per-stage device timing (hipEvents on the launch stream).  When enabled, every forward/backward
+ * records an event pair around each stage; gsr_stage_times() returns the accumulated milliseconds
+ * and call counts since the last reset. */
+void gsr_set_profiling(int enable);
+int gsr_num_stages(void);
+const char *gsr_stage_name(int stage);
+int gsr_stage_times(double *total_ms, int64_t *calls, int max_stages);
+void gsr_reset_stage_times(void);
+
+const char *gsr_last_error(void);
+const char *gsr_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSRAST_H */

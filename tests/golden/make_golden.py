@@ -1,0 +1,194 @@
+#!/usr/bin/env python
+"""Generate the golden vectors in tests/golden/*.npz from the REFERENCE Python rasterizer.
+
+Runs only in the build container, where /root/reference exists (the GPU box never reads
+/root/reference).  It imports `gs_lightning.rasterize` from the reference exactly as SURVEY.md
+§8(c) describes, with three harness-only shims (no reference code is copied):
+
+  1. `kornia` is absent: a stand-in module provides `kornia.geometry.Quaternion(q).matrix()`
+     as the NON-normalising (w,x,y,z) -> R formula, which is what the CUDA backward
+     differentiates.  Forward values equal kornia's for unit quaternions.
+  2. `gs_lightning/__init__.py` eagerly imports lightning/datasets/modules (absent deps): a bare
+     package module with `__path__` = the reference directory is registered instead.
+  3. SH degree 3 hits the `< 3` guard bug (`gs_lightning/utils/sh.py:83`): SH inputs are
+     zero-padded to 25 coefficients, and the SH gradient is sliced back to the first 16.
+
+means2D gradients: the reference has no means2D input, so `ndc2Pix` (imported by name at
+`gs_lightning/rasterize/rasterize.py:10`) is wrapped to add a zero leaf; the CUDA-convention
+dL/dmeans2D is that pixel-space gradient times (W/2, H/2).
+
+Usage:  python -B tests/golden/make_golden.py   (writes tests/golden/*.npz)
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+os.environ.setdefault("TQDM_DISABLE", "1")
+sys.dont_write_bytecode = True
+
+
+def _install_shims():
+    def quat_matrix(q):
+        w, x, y, z = q[..., 0], q[..., 1], q[..., 2], q[..., 3]
+        r0 = torch.stack([1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)], -1)
+        r1 = torch.stack([2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)], -1)
+        r2 = torch.stack([2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)], -1)
+        return torch.stack([r0, r1, r2], -2)
+
+    class Quaternion:
+        def __init__(self, data):
+            self.data = data
+
+        def matrix(self):
+            return quat_matrix(self.data)
+
+    kornia = types.ModuleType("kornia")
+    kornia.geometry = types.SimpleNamespace(Quaternion=Quaternion)
+    sys.modules["kornia"] = kornia
+    pkg = types.ModuleType("gs_lightning")
+    pkg.__path__ = [os.path.join(REF, "gs_lightning")]
+    sys.modules["gs_lightning"] = pkg
+
+
+def _import_reference():
+    _install_shims()
+    import gs_lightning.rasterize as R  # noqa: E402
+    import gs_lightning.rasterize.rasterize as RR  # noqa: E402
+    return R, RR
+
+
+def reference_fwd_bwd(R, RR, scene, cam, bg, dcolor, dinv, scale_modifier=1.0, backward=True):
+    N = scene.means3D.shape[0]
+    M = scene.shs.shape[1]
+    means = scene.means3D.clone().requires_grad_(backward)
+    opac = scene.opacities.clone().requires_grad_(backward)
+    scales = scene.scales.clone().requires_grad_(backward)
+    rots = scene.rotations.clone().requires_grad_(backward)
+    shs = scene.shs.clone().requires_grad_(backward)
+    shs_in = torch.cat([shs, torch.zeros(N, 25 - M, 3)], 1) if M < 25 else shs
+    leaf = torch.zeros(N, 2, requires_grad=backward)
+    orig = RR.ndc2Pix
+    RR.ndc2Pix = lambda v, w, h: orig(v, w, h) + leaf
+    try:
+        img, radius, depth = R.rasterize_gaussian(
+            means3D=means, opacities=opac, scales=scales, rotations=rots, shs=shs_in,
+            scale_modifier=scale_modifier, image_width=cam.image_width, image_height=cam.image_height,
+            tanfovx=cam.tanfovx, tanfovy=cam.tanfovy, viewmatrix=cam.viewmatrix,
+            projmatrix=cam.projmatrix, campos=cam.campos, background=bg, sh_degree=scene.sh_degree)
+    finally:
+        RR.ndc2Pix = orig
+    out = dict(color=img.detach().numpy(), radii=radius.detach().numpy().astype(np.int32),
+               invdepth=depth.detach().numpy())
+    if backward:
+        loss = (img * dcolor).sum() + (depth * dinv).sum()
+        loss.backward()
+        W, H = cam.image_width, cam.image_height
+        g2 = torch.zeros(N, 3)
+        g2[:, 0] = leaf.grad[:, 0] * (0.5 * W)
+        g2[:, 1] = leaf.grad[:, 1] * (0.5 * H)
+        out.update(
+            grad_means3D=means.grad.numpy(), grad_means2D=g2.numpy(), grad_opacities=opac.grad.numpy(),
+            grad_scales=scales.grad.numpy(), grad_rotations=rots.grad.numpy(),
+            grad_shs=shs.grad[:, :M].numpy())
+    return out
+
+
+def _front_of_camera(scene, cam, zmin=0.5):
+    """Keep only Gaussians with z_view > zmin: Appendix A4 (the Python path still rasterizes
+    culled Gaussians into one tile) would otherwise make the two paths differ by design."""
+    ph = torch.cat([scene.means3D, torch.ones(len(scene.means3D), 1)], 1) @ cam.viewmatrix
+    keep = ph[:, 2] > zmin
+    from gaussian_splatting_lightning_amd.synthetic import Scene
+    return Scene(scene.means3D[keep].contiguous(), scene.scales[keep].contiguous(),
+                 scene.rotations[keep].contiguous(), scene.opacities[keep].contiguous(),
+                 scene.shs[keep].contiguous(), scene.sh_degree)
+
+
+def _case(R, RR, name, n, W, H, sh_degree, seed, opacity_scale, bg, scale_modifier=1.0,
+          backward=True, degree_coeffs=None):
+    sys.path.insert(0, REPO)
+    from gaussian_splatting_lightning_amd.synthetic import Scene, make_camera, make_scene, make_upstream
+    scene = make_scene(n, sh_degree=degree_coeffs if degree_coeffs is not None else sh_degree, seed=seed,
+                       opacity_scale=opacity_scale)
+    scene = Scene(scene.means3D, scene.scales, scene.rotations, scene.opacities, scene.shs, sh_degree)
+    cam = make_camera(W, H)
+    scene = _front_of_camera(scene, cam)
+    dcolor, dinv = make_upstream(W, H, seed)
+    bg_t = torch.tensor(bg, dtype=torch.float32)
+    out = reference_fwd_bwd(R, RR, scene, cam, bg_t, dcolor, dinv, scale_modifier, backward)
+    rec = dict(
+        means3D=scene.means3D.numpy(), scales=scene.scales.numpy(), rotations=scene.rotations.numpy(),
+        opacities=scene.opacities.numpy(), shs=scene.shs.numpy(), sh_degree=np.int32(sh_degree),
+        viewmatrix=cam.viewmatrix.numpy(), projmatrix=cam.projmatrix.numpy(), campos=cam.campos.numpy(),
+        tanfovx=np.float32(cam.tanfovx), tanfovy=np.float32(cam.tanfovy), image_height=np.int32(H),
+        image_width=np.int32(W), bg=bg_t.numpy(), scale_modifier=np.float32(scale_modifier))
+    if backward:
+        rec.update(dL_dcolor=dcolor.numpy(), dL_dinvdepth=dinv.numpy())
+    for k, v in out.items():
+        rec["ref_" + k] = v
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **rec)
+    print(f"wrote {path}: N={scene.means3D.shape[0]} {W}x{H} deg={sh_degree} "
+          f"({os.path.getsize(path) / 1024:.0f} KiB)")
+
+
+def _markvisible(R):
+    """Known answers for test_mark_visible.py (reference tests/rasterizer_python/test_cases.py)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "_ref_test_cases_src", os.path.join(REF, "tests/rasterizer_python/test_cases.py"))
+    # test_cases.py imports diff_gaussian_rasterization for its NamedTuple only; supply a stand-in.
+    from collections import namedtuple
+    fields = ["image_height", "image_width", "tanfovx", "tanfovy", "bg", "scale_modifier", "viewmatrix",
+              "projmatrix", "sh_degree", "campos", "prefiltered", "debug", "antialiasing"]
+    stub = types.ModuleType("diff_gaussian_rasterization")
+    stub.GaussianRasterizationSettings = namedtuple("GaussianRasterizationSettings", fields)
+    saved = sys.modules.get("diff_gaussian_rasterization")
+    sys.modules["diff_gaussian_rasterization"] = stub
+    try:
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+    finally:
+        if saved is None:
+            del sys.modules["diff_gaussian_rasterization"]
+        else:
+            sys.modules["diff_gaussian_rasterization"] = saved
+    pts = mod.points_3d.cpu()
+    views, projs, camps, vis = [], [], [], []
+    for s in mod.settings:
+        views.append(s.viewmatrix.cpu().numpy())
+        projs.append(s.projmatrix.cpu().numpy())
+        camps.append(s.campos.cpu().numpy())
+        vis.append(R.markVisible(pts, s.viewmatrix.cpu(), s.projmatrix.cpu()).numpy())
+    cs = mod.common_setting
+    path = os.path.join(HERE, "markvisible_treehill.npz")
+    np.savez_compressed(path, points=pts.numpy(), viewmatrix=np.stack(views), projmatrix=np.stack(projs),
+                        campos=np.stack(camps), visible=np.stack(vis), image_height=np.int32(cs["image_height"]),
+                        image_width=np.int32(cs["image_width"]), tanfovx=np.float32(cs["tanfovx"]),
+                        tanfovy=np.float32(cs["tanfovy"]))
+    print("wrote", path, [int(v.sum()) for v in vis])
+
+
+def main():
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    R, RR = _import_reference()
+    _markvisible(R)
+    # (iii) unsaturated SH3 mini case, partial edge tiles, coloured background: tight fwd+bwd parity
+    _case(R, RR, "unsat_sh3_150x100", 2000, 150, 100, 3, seed=3, opacity_scale=0.05, bg=[0.2, 0.5, 0.9])
+    # active degree 1 with 16 stored coefficients, scale_modifier != 1
+    _case(R, RR, "unsat_deg1of3_96x80", 1500, 96, 80, 1, seed=4, opacity_scale=0.05, bg=[1.0, 1.0, 1.0],
+          scale_modifier=0.8, degree_coeffs=3)
+    # (ii) BASELINE config 1: 10k Gaussians, 256x256, SH0, saturating opacities, black background
+    _case(R, RR, "cfg1_10k_256_sh0", 10000, 256, 256, 0, seed=0, opacity_scale=1.0, bg=[0.0, 0.0, 0.0])
+
+
+if __name__ == "__main__":
+    main()
