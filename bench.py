@@ -1,0 +1,239 @@
+#!/usr/bin/env python
+"""Benchmark: rasterizer forward+backward on BASELINE.json config 3 (1M Gaussians, 1920x1080, SH deg 3).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One step on every rank = one forward + backward of the HIP rasterizer (C ABI, include/gsrast.h) for that
+rank's view of the shared 1M-Gaussian scene (view k = the treehill view rotated 2*pi*k/8 about world y),
+with the upstream gradients dL/dimage, dL/dinvdepth fixed, followed by the per-view densification
+statistics and -- for N > 1 -- one RCCL all-reduce (sum) of the per-Gaussian gradients + statistics and a
+max-reduce of the radii (BASELINE.json config 4: one view per GPU).  Per-GPU work is fixed, so scaling is
+weak.  value = N * Gaussians * W * H / step time (Gaussians*pixels/s, whole job).
+
+Extra fields on the one JSON line:
+  roofline      dominant kernel, achieved algorithmic bytes / its average duration from hipEvents recorded
+                around each stage on the launch stream during the timed steps (SURVEY.md §8(d) bytes);
+  cpu_baseline  the oracle (oracle/gsr_oracle.c, C + OpenMP) on the same workload on the host cores;
+  stages_ms     average device time of every pipeline stage per step.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+METRIC = "rasterizer fwd+bwd ms & Gaussians·pixels/s @ 1M gauss, 1080p; 1/2/4/8-GPU"
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
+FP32_VALU_PEAK_TF = 157.3  # MI355X_MICROARCH.md chip table (spec)
+PY_REFERENCE_CFG3_S = 730.0  # reference Python rasterizer, cfg 3 fwd+bwd, 8-core Xeon
+
+CONFIGS = {
+    "cfg3": dict(n=1_000_000, W=1920, H=1080, deg=3, stress=0.0,
+                 desc="BASELINE config 3/4: 1M Gaussians, 1920x1080, SH deg 3, fwd+bwd, one view per GPU"),
+    "cfg2": dict(n=100_000, W=800, H=800, deg=3, stress=0.0, desc="BASELINE config 2: 100k Gaussians, 800x800, SH 3"),
+    "cfg5": dict(n=5_000_000, W=3840, H=2160, deg=3, stress=0.01,
+                 desc="BASELINE config 5: 5M Gaussians, 3840x2160, SH 3, 1% bloated (stress)"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stage-events", action="store_true", help="time without per-stage hipEvents")
+    ap.add_argument("--cpu-budget-s", type=float, default=20.0)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from gaussian_splatting_lightning_amd import _native
+    from gaussian_splatting_lightning_amd.rasterizer import GaussianRasterizationSettings, backward_raw, forward_raw
+    from gaussian_splatting_lightning_amd.synthetic import make_camera, make_scene, make_upstream
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    cfg = CONFIGS[args.config]
+    n, W, H, deg = cfg["n"], cfg["W"], cfg["H"], cfg["deg"]
+    num_views = max(world, 8) if args.config == "cfg3" else max(world, 1)
+
+    # ---- inputs: one shared scene (same seed on every rank), one view per rank ----
+    scene = make_scene(n, sh_degree=deg, seed=0, stress_fraction=cfg["stress"])
+    cam = make_camera(W, H, view_index=rank, num_views=num_views)
+    dcolor_cpu, dinv_cpu = make_upstream(W, H, seed=0)
+    sc = scene.to(dev)
+    c = cam.to(dev)
+    dcolor, dinv = dcolor_cpu.to(dev), dinv_cpu.to(dev)
+    settings = GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=c.tanfovx, tanfovy=c.tanfovy,
+        bg=torch.zeros(3, device=dev), scale_modifier=1.0, viewmatrix=c.viewmatrix, projmatrix=c.projmatrix,
+        sh_degree=deg, campos=c.campos, prefiltered=False, debug=False, antialiasing=False)
+    M = sc.shs.shape[1]
+
+    # Flat per-Gaussian reduction buffer: means3D 3 | scales 3 | rotations 4 | opacity 1 | shs 3M |
+    # densification stats 2 (|dL/dmeans2D[:, :2]| and the visibility count, gaussian_model.py:175-181).
+    widths = dict(means3D=3, scales=3, rotations=4, opacities=1, shs=3 * M, stats=2)
+    cols = sum(widths.values())
+    # column-block layout [field][Gaussian][width] so every destination view is contiguous
+    flat = torch.zeros(cols * n, dtype=torch.float32, device=dev)
+    views, off = {}, 0
+    for k, wdt in widths.items():
+        views[k] = flat[off * n:(off + wdt) * n].view(n, wdt)
+        off += wdt
+    out = dict(means3D=views["means3D"], scales=views["scales"], rotations=views["rotations"],
+               opacities=views["opacities"], shs=views["shs"].view(n, M, 3))
+    dmeans2D = torch.empty(n, 3, dtype=torch.float32, device=dev)
+    out["means2D"] = dmeans2D
+    radii_max = torch.empty(n, dtype=torch.int32, device=dev)
+
+    def step():
+        color, radii, invd, st = forward_raw(sc.means3D, sc.shs, None, sc.opacities, sc.scales, sc.rotations, None,
+                                             settings)
+        backward_raw(st, settings, dcolor, dinv, out=out)
+        stats = views["stats"]
+        torch.linalg.vector_norm(dmeans2D[:, :2], dim=1, out=stats[:, 0])
+        stats[:, 1].copy_(radii > 0)
+        radii_max.copy_(radii)
+        if world > 1:
+            dist.all_reduce(flat)
+            dist.all_reduce(radii_max, op=dist.ReduceOp.MAX)
+        return st
+
+    # ---- warmup ----
+    for _ in range(args.warmup):
+        st = step()
+    torch.cuda.synchronize()
+
+    # ---- timed region ----
+    use_events = not args.no_stage_events
+    _native.reset_stage_times()
+    _native.set_profiling(use_events)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    _native.set_profiling(False)
+    stages = _native.stage_times()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = 1e3 * elapsed / args.steps
+
+    # ---- per-launch statistics for the roofline (untimed) ----
+    lay = _native.state_layout(n, st.num_rendered, W, H)
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+    npix = W * H
+    nc = st.image_buffer[lay["img_n_contrib"]: lay["img_n_contrib"] + 4 * npix].view(torch.int32)
+    sum_contrib = int(nc.sum(dtype=torch.int64).item())
+    I = st.num_rendered
+    stage_avg = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in stages.items()}
+    algo_bytes = {
+        # F6 composite fwd = 8 B/T + 44 B/I + 24 B/P; B1 composite bwd adds 40 B/I of grads
+        "render_fwd": 8 * T + 44 * I + 24 * npix,
+        "render_bwd": 8 * T + 44 * I + 24 * npix + 40 * I,
+        "preprocess": n * (40 + 12 * M) + n * 48,
+        "preprocess_bwd": n * (40 + 12 * M) + 88 * n + n * (56 + 12 * M),
+    }
+    flops = {"render_fwd": 25.0 * sum_contrib, "render_bwd": 70.0 * sum_contrib}
+    dom = max(("render_fwd", "render_bwd"), key=lambda k: stage_avg.get(k, 0.0))
+    dom_ms = stage_avg.get(dom, 0.0)
+    roofline = None
+    if dom_ms > 0:
+        ach = algo_bytes[dom] / (dom_ms * 1e-3) / 1e9
+        traffic = None
+        pmc_path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc_path):
+            try:
+                pm = json.load(open(pmc_path))
+                e = pm.get(args.config, {}).get(dom)
+                traffic = e.get("hbm_bytes_per_launch") if e else None
+            except Exception:  # noqa: BLE001
+                traffic = None
+        roofline = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "algorithmic_bytes_per_launch": algo_bytes[dom], "avg_launch_ms": round(dom_ms, 4),
+                    "valu_tflops_est": round(flops[dom] / (dom_ms * 1e-3) / 1e12, 2),
+                    "valu_frac_est": round(flops[dom] / (dom_ms * 1e-3) / 1e12 / FP32_VALU_PEAK_TF, 4),
+                    "note": "composite is VALU-bound by construction (SURVEY §8(d)); valu_* uses 25/70 flop per "
+                            "evaluated (pixel, Gaussian) pair x sum(n_contrib)"}
+
+    # ---- CPU baseline: the oracle on the same workload, rank 0 at N=1 only ----
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle as O
+        inp = [t.numpy() for t in (scene.means3D, scene.opacities, scene.scales, scene.rotations, scene.shs)]
+        vm, pm_, cp = cam.viewmatrix.numpy(), cam.projmatrix.numpy(), cam.campos.numpy()
+        dcn, din = dcolor_cpu.numpy(), dinv_cpu.numpy()
+        times = []
+        t_start = time.perf_counter()
+        while len(times) < 5:
+            t1 = time.perf_counter()
+            _, _, _, run = O.forward(inp[0], inp[1], inp[2], inp[3], inp[4], vm, pm_, cp, np.zeros(3, np.float32),
+                                     cam.tanfovx, cam.tanfovy, H, W, deg)
+            run.backward(dcn, din)
+            times.append(time.perf_counter() - t1)
+            del run
+            if time.perf_counter() - t_start > args.cpu_budget_s:
+                break
+        tc = float(np.median(times))
+        cpu = {"value": n * W * H / tc, "unit": "Gaussians·pixels/s", "cores": O.num_threads(), "kind": "port",
+               "sample": f"{len(times)} full {args.config} steps (fwd+bwd, view 0) in oracle/gsr_oracle.c, median "
+                         f"{tc:.2f} s/step",
+               "reference_python": {"value": (n * W * H / PY_REFERENCE_CFG3_S) if args.config == "cfg3" else None,
+                                    "note": "BASELINE.md §2: gs_lightning/rasterize Python path, 8-core Xeon, "
+                                            "~730 s fwd+bwd (extrapolated), not re-run here"}}
+
+    value = world * n * W * H / (ms_per_step * 1e-3)
+    line = {
+        "metric": METRIC, "value": value, "unit": "Gaussians·pixels/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": cfg["desc"], "gaussians": n, "width": W, "height": H, "sh_degree": deg,
+                   "views_per_step": world, "parallelism": f"dp{world} (one view per GPU, RCCL all-reduce)",
+                   "instances_per_view": I, "sum_n_contrib": sum_contrib,
+                   "stage_events": use_events},
+        "roofline": roofline, "cpu_baseline": cpu,
+        "stages_ms": {k: round(v, 4) for k, v in stage_avg.items() if v > 0},
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

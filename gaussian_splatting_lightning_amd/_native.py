@@ -45,7 +45,7 @@ class BackwardArgs(ctypes.Structure):
 class StateLayout(ctypes.Structure):
     _fields_ = [(n, ctypes.c_size_t) for n in (
         "geom_rec_a", "geom_rec_b", "geom_rec_c", "geom_tiles", "geom_order", "geom_inst_off", "geom_inst_start",
-        "geom_clamped", "geom_sorted_depth", "bin_point_list", "bin_inv", "bin_keys_sorted", "img_final_T", "img_n_contrib",
+        "geom_clamped", "geom_sorted_depth", "geom_tile_mask", "bin_point_list", "bin_inv", "bin_keys_sorted", "img_final_T", "img_n_contrib",
         "img_ranges", "img_tile_last")]
 
 
@@ -55,6 +55,7 @@ EXPORTED_SYMBOLS = (
     "gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes",
     "gsr_image_buffer_bytes", "gsr_bwd_scratch_bytes", "gsr_set_profiling", "gsr_num_stages", "gsr_stage_name",
     "gsr_stage_times", "gsr_reset_stage_times", "gsr_last_error", "gsr_build_info", "gsr_state_layout_query",
+    "gsr_set_tuning",
 )
 
 _lib = None
@@ -97,6 +98,8 @@ def load(path: str | None = None):
     lib.gsr_state_layout_query.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                            ctypes.POINTER(StateLayout)]
     lib.gsr_state_layout_query.restype = None
+    lib.gsr_set_tuning.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    lib.gsr_set_tuning.restype = None
     lib.gsr_last_error.restype = ctypes.c_char_p
     lib.gsr_build_info.restype = ctypes.c_char_p
     _lib = lib
@@ -133,3 +136,8 @@ def state_layout(P: int, R: int, W: int, H: int) -> dict:
     out = StateLayout()
     load().gsr_state_layout_query(int(P), int(R), int(W), int(H), ctypes.byref(out))
     return {name: getattr(out, name) for name, _ in StateLayout._fields_}
+
+
+def set_tuning(name: str, value: int) -> None:
+    """Internal A/B knob (see gsr_set_tuning)."""
+    load().gsr_set_tuning(name.encode(), int(value))

@@ -19,6 +19,20 @@ using namespace gsr;
 
 namespace {
 
+std::mutex g_tune_mu;
+std::vector<std::pair<std::string, int>> g_tune;
+
+}  // namespace
+
+int gsr::tuning(const char *name, int default_value) {
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    for (auto &kv : g_tune)
+        if (kv.first == name) return kv.second;
+    return default_value;
+}
+
+namespace {
+
 thread_local std::string g_err;
 
 int fail(int code, const std::string &msg) {
@@ -210,6 +224,7 @@ void gsr_state_layout_query(int P, int64_t R, int W, int H, gsr_state_layout *ou
     out->geom_inst_off = off(g.inst_off);
     out->geom_inst_start = off(g.inst_start);
     out->geom_clamped = off(g.clamped);
+    out->geom_tile_mask = off(g.tile_mask);
     out->geom_sorted_depth = off(g.sort.k[0]);
     out->bin_point_list = off(b.point_list);
     out->bin_inv = off(b.inv);
@@ -258,6 +273,7 @@ int gsr_forward(const gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, 
     pp.focal_y = H / (2.0f * a->tan_fovy);
     pp.scale_modifier = a->scale_modifier;
     pp.antialiasing = a->antialiasing;
+    pp.cull = tuning("cull", 1);
     pp.means3D = a->means3D; pp.opacities = a->opacities; pp.scales = a->scales; pp.rotations = a->rotations;
     pp.cov3D_precomp = a->cov3D_precomp; pp.colors_precomp = a->colors_precomp; pp.shs = a->shs;
     pp.view = a->viewmatrix; pp.proj = a->projmatrix; pp.campos = a->campos;
@@ -288,7 +304,7 @@ int gsr_forward(const gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, 
     if (R > 0) {
         ExpandParams ep;
         ep.P = (uint32_t)P; ep.R = R; ep.gx = gx; ep.gy = gy;
-        ep.order = g.order; ep.inst_off = g.inst_off; ep.tiles = g.tiles; ep.rec_a = g.rec_a; ep.radii = a->radii;
+        ep.order = g.order; ep.inst_off = g.inst_off; ep.tiles = g.tiles; ep.tile_mask = g.tile_mask; ep.rec_a = g.rec_a; ep.radii = a->radii;
         ep.keys_out = b.sort.k[0]; ep.inst_gid = b.inst_gid; ep.inst_start = g.inst_start;
         GSR_STAGE(ST_EXPAND, dbg, launch_expand(stream, ep));
         GSR_STAGE(ST_TILE_SORT, dbg,
@@ -365,6 +381,8 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     pp.view = a->viewmatrix; pp.proj = a->projmatrix; pp.campos = a->campos;
     pp.radii = a->radii; pp.tiles = g.tiles; pp.inst_start = g.inst_start; pp.inv = b.inv; pp.clamped = g.clamped;
     pp.rows = rows;
+    pp.sh_vec16 = pp.shs && a->M == 16 && a->dL_dsh && (((uintptr_t)pp.shs | (uintptr_t)a->dL_dsh) & 15) == 0 &&
+                  tuning("sh_vec16", 1);
     pp.dL_dmeans2D = a->dL_dmeans2D; pp.dL_dcolors = a->dL_dcolors; pp.dL_dopacity = a->dL_dopacity;
     pp.dL_dmeans3D = a->dL_dmeans3D; pp.dL_dcov3D = a->dL_dcov3D; pp.dL_dsh = a->dL_dsh;
     pp.dL_dscales = a->dL_dscales; pp.dL_drot = a->dL_drotations;
@@ -384,6 +402,17 @@ int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const
     launch_mark_visible(s, P, means3D, viewmatrix, present);
     GSR_HIP(hipGetLastError());
     return GSR_OK;
+}
+
+void gsr_set_tuning(const char *name, int value) {
+    if (!name) return;
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    for (auto &kv : g_tune)
+        if (kv.first == name) {
+            kv.second = value;
+            return;
+        }
+    g_tune.emplace_back(name, value);
 }
 
 void gsr_set_profiling(int enable) {

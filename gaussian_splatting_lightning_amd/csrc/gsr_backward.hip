@@ -30,8 +30,8 @@ __device__ __forceinline__ void add_row(const float *__restrict__ rows, uint32_t
     acc[8] += c.x; acc[9] += c.y;
 }
 
-template <bool HAS_INV>
-__global__ __launch_bounds__(256) void render_bwd_kernel(RenderBwdParams p) {
+template <bool HAS_INV, int MIN_WAVES>
+__global__ __launch_bounds__(256, MIN_WAVES) void render_bwd_kernel(RenderBwdParams p) {
     __shared__ float4 s_a[4][64];
     __shared__ float4 s_b[4][64];
     __shared__ float2 s_c[4][64];
@@ -54,25 +54,26 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(RenderBwdParams p) {
 
     const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
     const size_t HW = (size_t)p.W * p.H;
-    float T[PIX_PER_LANE], Tf[PIX_PER_LANE], dp0[PIX_PER_LANE], dp1[PIX_PER_LANE], dp2[PIX_PER_LANE];
-    float dinv[PIX_PER_LANE], bgdot[PIX_PER_LANE];
-    float ar0[PIX_PER_LANE], ar1[PIX_PER_LANE], ar2[PIX_PER_LANE], lc0[PIX_PER_LANE], lc1[PIX_PER_LANE],
-        lc2[PIX_PER_LANE], ainv[PIX_PER_LANE], linv[PIX_PER_LANE], la[PIX_PER_LANE];
+    // Per-pixel state.  The reference keeps last_alpha / last_color and updates accum_rec lazily when the
+    // NEXT contributor arrives; here accum_rec is advanced eagerly right after a contributor is used,
+    // with the identical expression alpha*c + (1-alpha)*accum, which drops four registers per pixel.
+    float T[PIX_PER_LANE], nbg[PIX_PER_LANE], dp0[PIX_PER_LANE], dp1[PIX_PER_LANE], dp2[PIX_PER_LANE];
+    float dinv[PIX_PER_LANE], ar0[PIX_PER_LANE], ar1[PIX_PER_LANE], ar2[PIX_PER_LANE], ainv[PIX_PER_LANE];
     uint32_t lastc[PIX_PER_LANE];
 #pragma unroll
     for (int k = 0; k < PIX_PER_LANE; k++) {
         const int py = py0 + 4 * k;
         const bool inside = px < p.W && py < p.H;
         const size_t pid = inside ? (size_t)py * p.W + px : 0;
-        Tf[k] = inside ? p.final_T[pid] : 0.f;
-        T[k] = Tf[k];
+        const float Tf = inside ? p.final_T[pid] : 0.f;
+        T[k] = Tf;
         lastc[k] = inside ? p.n_contrib[pid] : 0u;
         dp0[k] = inside ? p.dL_dpix[pid] : 0.f;
         dp1[k] = inside ? p.dL_dpix[HW + pid] : 0.f;
         dp2[k] = inside ? p.dL_dpix[2 * HW + pid] : 0.f;
         dinv[k] = (HAS_INV && inside) ? p.dL_dinvdepth[pid] : 0.f;
-        bgdot[k] = bg0 * dp0[k] + bg1 * dp1[k] + bg2 * dp2[k];
-        ar0[k] = ar1[k] = ar2[k] = lc0[k] = lc1[k] = lc2[k] = ainv[k] = linv[k] = la[k] = 0.f;
+        nbg[k] = -Tf * (bg0 * dp0[k] + bg1 * dp1[k] + bg2 * dp2[k]);
+        ar0[k] = ar1[k] = ar2[k] = ainv[k] = 0.f;
     }
     const float ddelx_dx = 0.5f * p.W, ddely_dy = 0.5f * p.H;
 
@@ -100,34 +101,29 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(RenderBwdParams p) {
                 const float dx = a.x - pfx, dy = a.y - (float)(py0 + 4 * k);
                 const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
                 if (power > 0.0f) continue;
-                const float G = expf(power);
+                const float G = fast_exp(power);
                 const float alpha = fminf(0.99f, b.y * G);
                 if (alpha < 1.0f / 255.0f) continue;
                 any = true;
-                T[k] = T[k] / (1.f - alpha);
-                const float dchannel_dcolor = alpha * T[k];
-                float dL_dalpha = 0.0f;
-                ar0[k] = la[k] * lc0[k] + (1.f - la[k]) * ar0[k];
-                lc0[k] = b.z;
-                dL_dalpha += (b.z - ar0[k]) * dp0[k];
-                g[6] += dchannel_dcolor * dp0[k];
-                ar1[k] = la[k] * lc1[k] + (1.f - la[k]) * ar1[k];
-                lc1[k] = b.w;
+                const float one_m = 1.f - alpha;
+                const float r = fast_rcp(one_m);
+                T[k] = T[k] * r;
+                const float wgt = alpha * T[k];
+                float dL_dalpha = (b.z - ar0[k]) * dp0[k];
                 dL_dalpha += (b.w - ar1[k]) * dp1[k];
-                g[7] += dchannel_dcolor * dp1[k];
-                ar2[k] = la[k] * lc2[k] + (1.f - la[k]) * ar2[k];
-                lc2[k] = c.x;
                 dL_dalpha += (c.x - ar2[k]) * dp2[k];
-                g[8] += dchannel_dcolor * dp2[k];
+                g[6] += wgt * dp0[k];
+                g[7] += wgt * dp1[k];
+                g[8] += wgt * dp2[k];
+                ar0[k] = alpha * b.z + one_m * ar0[k];
+                ar1[k] = alpha * b.w + one_m * ar1[k];
+                ar2[k] = alpha * c.x + one_m * ar2[k];
                 if (HAS_INV) {
-                    ainv[k] = la[k] * linv[k] + (1.f - la[k]) * ainv[k];
-                    linv[k] = c.y;
                     dL_dalpha += (c.y - ainv[k]) * dinv[k];
-                    g[9] += dchannel_dcolor * dinv[k];
+                    g[9] += wgt * dinv[k];
+                    ainv[k] = alpha * c.y + one_m * ainv[k];
                 }
-                dL_dalpha *= T[k];
-                la[k] = alpha;
-                dL_dalpha += (-Tf[k] / (1.f - alpha)) * bgdot[k];
+                dL_dalpha = dL_dalpha * T[k] + nbg[k] * r;
                 const float dL_dG = b.y * dL_dalpha;
                 const float gdx = G * dx, gdy = G * dy;
                 const float dG_ddelx = -gdx * a.z - gdy * a.w;
@@ -155,10 +151,15 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(RenderBwdParams p) {
 
 void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
     if (p.num_tiles <= 0) return;
-    if (p.dL_dinvdepth)
-        render_bwd_kernel<true><<<div_up(p.num_tiles, 4), 256, 0, s>>>(p);
-    else
-        render_bwd_kernel<false><<<div_up(p.num_tiles, 4), 256, 0, s>>>(p);
+    const dim3 grid(div_up(p.num_tiles, 4)), block(256);
+    const bool occ4 = tuning("bwd_occ4", 1) != 0;
+    if (p.dL_dinvdepth) {
+        if (occ4) render_bwd_kernel<true, 4><<<grid, block, 0, s>>>(p);
+        else render_bwd_kernel<true, 1><<<grid, block, 0, s>>>(p);
+    } else {
+        if (occ4) render_bwd_kernel<false, 4><<<grid, block, 0, s>>>(p);
+        else render_bwd_kernel<false, 1><<<grid, block, 0, s>>>(p);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -250,7 +251,30 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         if (cnt > BIG_GAUSSIAN_TILES) {
             add_row(p.rows, p.inv[start], gs);
         } else {
-            for (uint32_t k = 0; k < cnt; k++) add_row(p.rows, p.inv[start + k], gs);
+            // issue the index loads, then all row loads of a group, before summing (memory-level parallelism)
+            for (uint32_t k0 = 0; k0 < cnt; k0 += 4) {
+                uint32_t sidx[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) sidx[j] = (k0 + j < cnt) ? p.inv[start + k0 + j] : 0xffffffffu;
+                float4 ra[4], rb[4], rc[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    if (sidx[j] != 0xffffffffu) {
+                        const float4 *src = reinterpret_cast<const float4 *>(p.rows + (size_t)sidx[j] * GRAD_ROW);
+                        ra[j] = src[0];
+                        rb[j] = src[1];
+                        rc[j] = src[2];
+                    } else {
+                        ra[j] = rb[j] = rc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    gs[0] += ra[j].x; gs[1] += ra[j].y; gs[2] += ra[j].z; gs[3] += ra[j].w;
+                    gs[4] += rb[j].x; gs[5] += rb[j].y; gs[6] += rb[j].z; gs[7] += rb[j].w;
+                    gs[8] += rc[j].x; gs[9] += rc[j].y;
+                }
+            }
         }
     }
     if (p.dL_dmeans2D) {
@@ -379,9 +403,27 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         const float3 dRGB = make_float3((cl & 1) ? 0.f : gs[6], (cl & 2) ? 0.f : gs[7], (cl & 4) ? 0.f : gs[8]);
         const float3 campos = make_float3(p.campos[0], p.campos[1], p.campos[2]);
         float *dsh = p.dL_dsh + (size_t)i * ncoef;  // required whenever shs is given (checked by the API)
-        dm = dm + sh_backward_dispatch(p.D, p.shs + (size_t)i * ncoef, mean - campos, dRGB, dsh);
-        const int used = (p.D + 1) * (p.D + 1) * 3;
-        for (int k = used; k < ncoef; k++) dsh[k] = 0.f;
+        const float *shp = p.shs + (size_t)i * ncoef;
+        if (p.sh_vec16) {
+            // 16 coefficients x 3 = 192 B per Gaussian: 12 float4 loads and stores per lane
+            float shv[48], dshv[48];
+            const float4 *s4 = reinterpret_cast<const float4 *>(shp);
+#pragma unroll
+            for (int k = 0; k < 12; k++) {
+                const float4 q = s4[k];
+                shv[4 * k] = q.x; shv[4 * k + 1] = q.y; shv[4 * k + 2] = q.z; shv[4 * k + 3] = q.w;
+            }
+#pragma unroll
+            for (int k = 0; k < 48; k++) dshv[k] = 0.f;
+            dm = dm + sh_backward_dispatch(p.D, shv, mean - campos, dRGB, dshv);
+            float4 *d4 = reinterpret_cast<float4 *>(dsh);
+#pragma unroll
+            for (int k = 0; k < 12; k++) d4[k] = make_float4(dshv[4 * k], dshv[4 * k + 1], dshv[4 * k + 2], dshv[4 * k + 3]);
+        } else {
+            dm = dm + sh_backward_dispatch(p.D, shp, mean - campos, dRGB, dsh);
+            const int used = (p.D + 1) * (p.D + 1) * 3;
+            for (int k = used; k < ncoef; k++) dsh[k] = 0.f;
+        }
     }
     if (p.dL_dmeans3D) {
         p.dL_dmeans3D[3 * i] = dm.x;

@@ -73,6 +73,7 @@ struct GeomState {
     uint32_t *depth_key;   // P: float bits of view depth, 0xffffffff if culled (aliases sort.k[0])
     uint32_t *tiles;       // P: tiles touched
     uint8_t *clamped;      // P: bit c set if SH colour channel c was clamped at 0
+    uint64_t *tile_mask;   // P: kept tiles of the rect (row-major bits) when area <= 64, else 0 (keep all)
     uint32_t *inst_off;    // P+1: exclusive scan of tiles in depth order, [P] = total
     uint32_t *inst_start;  // P: first instance (expansion order) of each Gaussian
     uint32_t *big_list;    // P: Gaussians with > BIG_GAUSSIAN_TILES tiles
@@ -90,6 +91,7 @@ inline size_t carve_geom(char *base, int P, GeomState &g) {
     g.rec_c = c.take<float2>(n);
     g.tiles = c.take<uint32_t>(n);
     g.clamped = c.take<uint8_t>(n);
+    g.tile_mask = c.take<uint64_t>(n);
     g.inst_off = c.take<uint32_t>((size_t)n + 1);
     g.inst_start = c.take<uint32_t>(n);
     g.big_list = c.take<uint32_t>(n);
@@ -191,6 +193,45 @@ __device__ __forceinline__ void get_rect(float2 p, int radius, int gx, int gy, i
     rmax.y = min(gy, max(0, (int)((p.y + radius + BLOCK_Y - 1) / BLOCK_Y)));
 }
 
+// Exact tile culling.  A (Gaussian, tile) instance is dropped only when NO pixel centre of the tile can
+// pass the compositing test `o * exp(power) >= 1/255` as the kernels evaluate it in fp32, so every output
+// and gradient is bitwise unchanged (the skipped instances would all hit `alpha < 1/255`).  q_min is the
+// exact minimum of the conic quadratic form over the tile's pixel rectangle (double precision); the fp32
+// evaluation of q at any pixel is within eps*q of the exact value, eps = 1e-5 (|a|+|b|+|c|) / lambda_min
+// (>= 25x the worst-case rounding of the 6-op power expression), and fast_exp is within 1e-5 relative.
+constexpr int CULL_MAX_AREA = 64;
+__host__ __device__ inline bool tile_has_contribution(double x, double y, double a, double b, double c, double o,
+                                                      int tx, int ty, int W, int H) {
+    if (!(o * 255.0 * (1.0 + 1e-5) >= 1.0)) return false;  // o*G <= o < 1/255 everywhere
+    const double lx = tx * BLOCK_X, ly = ty * BLOCK_Y;
+    const double hx = fmin((double)(tx * BLOCK_X + BLOCK_X - 1), (double)(W - 1));
+    const double hy = fmin((double)(ty * BLOCK_Y + BLOCK_Y - 1), (double)(H - 1));
+    if (x >= lx && x <= hx && y >= ly && y <= hy) return true;
+    const double tr = 0.5 * (a + c), df = 0.5 * (a - c);
+    const double lmin = tr - sqrt(df * df + b * b);
+    if (!(lmin > 0.0) || !(a > 0.0) || !(c > 0.0)) return true;
+    const double eps = 1e-5 * (fabs(a) + fabs(b) + fabs(c)) / lmin;
+    if (eps > 0.1) return true;
+    double qmin = 1e300;
+    const double xs[2] = {lx, hx}, ys[2] = {ly, hy};
+    for (int e = 0; e < 2; e++) {  // vertical edges x = X
+        const double dx = x - xs[e];
+        double py = y + b * dx / c;
+        py = fmin(fmax(py, ly), hy);
+        const double dy = y - py;
+        qmin = fmin(qmin, a * dx * dx + 2.0 * b * dx * dy + c * dy * dy);
+    }
+    for (int e = 0; e < 2; e++) {  // horizontal edges y = Y
+        const double dy = y - ys[e];
+        double px = x + b * dy / a;
+        px = fmin(fmax(px, lx), hx);
+        const double dx = x - px;
+        qmin = fmin(qmin, a * dx * dx + 2.0 * b * dx * dy + c * dy * dy);
+    }
+    const double qlo = qmin * (1.0 - eps) - 1e-6;
+    return !(qlo > 2.0 * log(255.0 * o * (1.0 + 1e-5)));
+}
+
 // SH basis constants (utils/sh.py:7-28 of the reference)
 #define GSR_SH_C0 0.28209479177387814f
 #define GSR_SH_C1 0.4886025119029199f
@@ -261,6 +302,12 @@ __device__ __forceinline__ float quad_form(const float a[3], const float c6[6], 
     const float v2 = c6[2] * b[0] + c6[4] * b[1] + c6[5] * b[2];
     return a[0] * v0 + a[1] * v1 + a[2] * v2;
 }
+
+// exp(x) as v_exp_f32(x * log2 e): 2 instructions instead of the 13 of the correctly rounded expf.
+// Used identically by the forward and the backward composite, so the backward's T recovery divides by
+// exactly the (1 - alpha) the forward multiplied with.  Relative error ~1e-7 (DESIGN.md "Numerics").
+__device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
 // --- wave64 primitives ---------------------------------------------------------------------------
 template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf, bool BOUND = false>

@@ -86,9 +86,24 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessParams p) {
     g.rec_c[i] = make_float2(rgb.z, 1.f / pv.z);
     g.clamped[i] = clamp_bits;
     p.radii[i] = (int)radius;
-    g.tiles[i] = area;
-    g.depth_key[i] = __float_as_uint(pv.z);
-    if (area > BIG_GAUSSIAN_TILES) {
+    uint64_t mask = 0;
+    uint32_t kept = area;
+    if (p.cull && area <= (uint32_t)CULL_MAX_AREA) {
+        const int w = rmax.x - rmin.x;
+        kept = 0;
+        for (int ty = rmin.y; ty < rmax.y; ty++)
+            for (int tx = rmin.x; tx < rmax.x; tx++)
+                if (tile_has_contribution(pimg.x, pimg.y, conic_x, conic_y, conic_z, opacity, tx, ty, p.W, p.H)) {
+                    mask |= 1ull << ((ty - rmin.y) * w + (tx - rmin.x));
+                    kept++;
+                }
+    }
+    g.tile_mask[i] = mask;
+    g.tiles[i] = kept;
+    // A Gaussian whose every tile is culled keeps its radius (reference output) but renders nothing; it is
+    // sorted behind all rendered ones so the expansion never meets an empty rank.
+    g.depth_key[i] = kept ? __float_as_uint(pv.z) : 0xffffffffu;
+    if (kept > BIG_GAUSSIAN_TILES) {
         const uint32_t slot = atomicAdd(&g.counters[CNT_BIG], 1u);
         g.big_list[slot] = (uint32_t)i;
     }
@@ -132,13 +147,14 @@ __device__ __forceinline__ uint32_t wave_last_le(const uint32_t *__restrict__ of
 
 __global__ __launch_bounds__(256) void expand_kernel(ExpandParams p) {
     __shared__ uint32_t s_off[EXP_TILE + 2];
-    __shared__ int4 s_rect[EXP_TILE + 1];  // (gid, rmin.x, rmin.y, width)
+    __shared__ int4 s_rect[EXP_TILE + 1];       // (gid, rmin.x, rmin.y, width)
+    __shared__ uint64_t s_mask[EXP_TILE + 1];   // kept-tile mask (0: all tiles of the rect)
     __shared__ uint32_t s_lo, s_n;
     const uint32_t u0 = blockIdx.x * EXP_TILE;
     const uint32_t u1 = min(p.R, u0 + (uint32_t)EXP_TILE);
     if (threadIdx.x < 64) {
-        // owner(u) = last r with inst_off[r] <= u.  Every visible Gaussian owns >= 1 instance and the
-        // culled ones are sorted to the end, so the owners of [u0, u1) are consecutive ranks.
+        // owner(u) = last r with inst_off[r] <= u.  Every Gaussian that renders owns >= 1 instance and the
+        // others are sorted to the end, so the owners of [u0, u1) are consecutive ranks.
         const int lane = threadIdx.x;
         const uint32_t lo = wave_last_le(p.inst_off, p.P, u0, lane);
         const uint32_t hi = wave_last_le(p.inst_off, p.P, u1 - 1, lane);
@@ -156,6 +172,7 @@ __global__ __launch_bounds__(256) void expand_kernel(ExpandParams p) {
         int2 rmin, rmax;
         get_rect(make_float2(a.x, a.y), p.radii[gid], p.gx, p.gy, rmin, rmax);
         s_rect[k] = make_int4((int)gid, rmin.x, rmin.y, rmax.x - rmin.x);
+        s_mask[k] = p.tile_mask[gid];
     }
     __syncthreads();
     const uint32_t ub = u0 + threadIdx.x * EXP_PER;
@@ -169,17 +186,25 @@ __global__ __launch_bounds__(256) void expand_kernel(ExpandParams p) {
     uint32_t r = lo;
     uint32_t next = s_off[r + 1];
     int4 rect = s_rect[r];
+    uint64_t m = s_mask[r];
     uint32_t k = ub - s_off[r];
+    for (uint32_t j = 0; j < k && m; j++) m &= m - 1;  // skip the kept tiles of earlier threads
     const uint32_t ue = min(u1, ub + (uint32_t)EXP_PER);
     for (uint32_t u = ub; u < ue; u++) {
         while (u >= next) {
             r++;
             next = s_off[r + 1];
             rect = s_rect[r];
+            m = s_mask[r];
             k = 0;
         }
+        uint32_t bit = k;
+        if (m) {  // culled rect: the k-th kept tile is the lowest remaining mask bit
+            bit = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1;
+        }
         const uint32_t w = (uint32_t)rect.w;
-        const uint32_t ty = (uint32_t)rect.z + k / w, tx = (uint32_t)rect.y + k % w;
+        const uint32_t ty = (uint32_t)rect.z + bit / w, tx = (uint32_t)rect.y + bit % w;
         p.keys_out[u] = ty * (uint32_t)p.gx + tx;
         p.inst_gid[u] = (uint32_t)rect.x;
         if (k == 0) p.inst_start[rect.x] = u;
@@ -224,7 +249,7 @@ void launch_identify_ranges(hipStream_t s, const uint32_t *keys_sorted, uint32_t
 // pixel before the Gaussian that would take T below 1e-4.  No block barriers: the four waves of a
 // block work on four independent tiles and retire independently.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void render_fwd_kernel(RenderFwdParams p) {
+__global__ __launch_bounds__(256, 8) void render_fwd_kernel(RenderFwdParams p) {
     __shared__ float4 s_a[4][64];
     __shared__ float4 s_b[4][64];
     __shared__ float2 s_c[4][64];
@@ -274,7 +299,7 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(RenderFwdParams p) {
                 const float dx = a.x - pfx, dy = a.y - (float)(py0 + 4 * k);
                 const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
                 if (power > 0.0f) continue;
-                const float alpha = fminf(0.99f, b.y * expf(power));
+                const float alpha = fminf(0.99f, b.y * fast_exp(power));
                 if (alpha < 1.0f / 255.0f) continue;
                 const float test_T = T[k] * (1 - alpha);
                 if (test_T < 0.0001f) { active[k] = false; continue; }

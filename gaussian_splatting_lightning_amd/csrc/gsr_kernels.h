@@ -5,6 +5,9 @@
 
 namespace gsr {
 
+// Internal tuning knobs (A/B experiments in one process; defaults are the shipped configuration).
+int tuning(const char *name, int default_value);
+
 // ---- scan / sort (gsr_sort.hip) ----
 // Exclusive scan of n u32 values (optionally gathered through idx: v[i] = in[idx[i]]).
 // out has n+1 entries; out[n] = total.  overflow_flag (device u32) is set if the total exceeds 2^32-1.
@@ -23,6 +26,7 @@ struct PreprocessParams {
     int P, D, M, W, H, gx, gy;
     float tan_fovx, tan_fovy, focal_x, focal_y, scale_modifier;
     int antialiasing;
+    int cull;  // exact tile culling (see tile_has_contribution)
     const float *means3D, *opacities, *scales, *rotations, *cov3D_precomp, *colors_precomp, *shs;
     const float *view, *proj, *campos;
     int *radii;
@@ -34,6 +38,7 @@ struct ExpandParams {
     uint32_t P, R;
     int gx, gy;
     const uint32_t *order, *inst_off, *tiles;
+    const uint64_t *tile_mask;
     const float4 *rec_a;
     const int *radii;
     uint32_t *keys_out, *inst_gid, *inst_start;
@@ -78,6 +83,7 @@ struct PreprocessBwdParams {
     int P, D, M, W, H;
     float tan_fovx, tan_fovy, focal_x, focal_y, scale_modifier;
     int antialiasing, has_invdepth;
+    int sh_vec16;  // M == 16 and shs / dL_dsh 16-byte aligned: vectorised SH path
     const float *means3D, *opacities, *scales, *rotations, *cov3D_precomp, *shs;
     const float *view, *proj, *campos;
     const int *radii;

@@ -149,9 +149,12 @@ def forward_raw(means3D, sh, colors_precomp, opacities, scales, rotations, cov3D
     return color, radii, invdepth, state
 
 
-def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_depth=None):
+def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_depth=None, out=None):
     """One call of gsr_backward.  Returns a dict of gradients (means3D, means2D, shs, colors_precomp,
-    opacities, scales, rotations, cov3D_precomp); entries are None where the input was absent."""
+    opacities, scales, rotations, cov3D_precomp); entries are None where the input was absent.
+    `out` may supply preallocated contiguous float32 destinations (e.g. views into one flat buffer that is
+    then all-reduced): keys means2D (P,3), colors (P,3), opacities (P,1), means3D (P,3), cov3D (P,6),
+    shs (P,M,3), scales (P,3), rotations (P,4)."""
     lib = _native.load()
     rs = raster_settings
     st = state
@@ -165,14 +168,24 @@ def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_
     if grad_out_depth is not None:
         grad_out_depth = grad_out_depth.to(torch.float32).contiguous()
     f32 = dict(dtype=torch.float32, device=device)
-    dmeans2D = torch.empty(P, 3, **f32)
-    dcolors = torch.empty(P, 3, **f32)
-    dopac = torch.empty(P, 1, **f32)
-    dmeans3D = torch.empty(P, 3, **f32)
-    dcov = torch.empty(P, 6, **f32)
-    dsh = torch.empty(P, max(M, 0), 3, **f32)
-    dscales = torch.empty(P, 3, **f32)
-    drot = torch.empty(P, 4, **f32)
+    out = out or {}
+
+    def dst(name, *shape):
+        t = out.get(name)
+        if t is None:
+            return torch.empty(*shape, **f32)
+        if tuple(t.shape) != shape or t.dtype != torch.float32 or not t.is_contiguous():
+            raise RuntimeError(f"out[{name!r}] must be a contiguous float32 tensor of shape {shape}")
+        return t
+
+    dmeans2D = dst("means2D", P, 3)
+    dcolors = dst("colors", P, 3)
+    dopac = dst("opacities", P, 1)
+    dmeans3D = dst("means3D", P, 3)
+    dcov = dst("cov3D", P, 6)
+    dsh = dst("shs", P, max(M, 0), 3)
+    dscales = dst("scales", P, 3)
+    drot = dst("rotations", P, 4)
     bufs = _Buffers(device)
     a = _native.BackwardArgs(
         P=P, D=int(rs.sh_degree), M=M, W=W, H=H, R=st.num_rendered, background=_ptr(st.bg),

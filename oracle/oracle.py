@@ -53,8 +53,8 @@ def _load():
     lib.oracle_mark_visible.argtypes = [ctypes.c_int, _f, _f, _f, _u8]
     lib.oracle_num_threads.restype = ctypes.c_int
     lib.oracle_bin_count.restype = ctypes.c_longlong
-    lib.oracle_bin_count.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f, _i]
-    lib.oracle_bin.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f, _i, _f, _u32, _u32]
+    lib.oracle_bin_count.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f, _i, _f, ctypes.c_int]
+    lib.oracle_bin.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f, _i, _f, _f, ctypes.c_int, _u32, _u32, _u32]
     _lib = lib
     return lib
 
@@ -84,20 +84,24 @@ def mark_visible(means3D, viewmatrix, projmatrix) -> np.ndarray:
     return out.astype(bool)
 
 
-def bin_instances(xy, radii, depths, image_width, image_height):
-    """Binning alone: (point_list (R,), ranges (T,2)) for given pixel centres, radii and view depths."""
+def bin_instances(xy, radii, depths, conic_opacity, image_width, image_height, cull=True):
+    """Binning alone: (point_list (R,), ranges (T,2), tiles (P,)) for given pixel centres, radii, view
+    depths and (conic, opacity) -- the product's exact culling rule restated in C when cull=True."""
     lib = _load()
     xy = _c32(xy).reshape(-1, 2)
     P = xy.shape[0]
     r = np.ascontiguousarray(np.asarray(radii, np.int32))
     d = _c32(depths).reshape(-1)
+    co = _c32(conic_opacity).reshape(-1, 4)
     W, H = int(image_width), int(image_height)
-    R = int(lib.oracle_bin_count(P, W, H, _fp(xy), r.ctypes.data_as(_i)))
+    R = int(lib.oracle_bin_count(P, W, H, _fp(xy), r.ctypes.data_as(_i), _fp(co), int(bool(cull))))
     pl = np.zeros(max(R, 1), np.uint32)
     T = ((W + 15) // 16) * ((H + 15) // 16)
     rg = np.zeros((T, 2), np.uint32)
-    lib.oracle_bin(P, W, H, _fp(xy), r.ctypes.data_as(_i), _fp(d), pl.ctypes.data_as(_u32), rg.ctypes.data_as(_u32))
-    return pl[:R], rg
+    tt = np.zeros(max(P, 1), np.uint32)
+    lib.oracle_bin(P, W, H, _fp(xy), r.ctypes.data_as(_i), _fp(d), _fp(co), int(bool(cull)), pl.ctypes.data_as(_u32),
+                   rg.ctypes.data_as(_u32), tt.ctypes.data_as(_u32))
+    return pl[:R], rg, tt[:P]
 
 
 class OracleRun:

