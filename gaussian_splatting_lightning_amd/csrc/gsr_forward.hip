@@ -338,9 +338,112 @@ __global__ __launch_bounds__(256, 8) void render_fwd_kernel(RenderFwdParams p) {
     if (lane == 0) p.tile_last[tile] = mx;
 }
 
+// v3: the four pixels of a lane are updated with predication instead of exec-mask branches, so the
+// compiler can interleave the four independent pixel chains and no per-pixel branch bookkeeping is issued.
+// Colour accumulation uses w = alpha * T once per contributor (one FMA per channel).
+template <int MIN_WAVES>
+__global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v3_kernel(RenderFwdParams p) {
+    __shared__ float4 s_a[4][64];
+    __shared__ float4 s_b[4][64];
+    __shared__ float2 s_c[4][64];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tile = blockIdx.x * 4 + w;
+    if (tile >= p.num_tiles) return;
+    const int tx = tile % p.gx, ty = tile / p.gx;
+    const int px = tx * BLOCK_X + (lane & 15);
+    const int py0 = ty * BLOCK_Y + (lane >> 4);
+    const float pfx = (float)px;
+
+    float T[PIX_PER_LANE], C0[PIX_PER_LANE], C1[PIX_PER_LANE], C2[PIX_PER_LANE], ID[PIX_PER_LANE];
+    float pfy[PIX_PER_LANE];
+    uint32_t last[PIX_PER_LANE];
+    bool active[PIX_PER_LANE];
+#pragma unroll
+    for (int k = 0; k < PIX_PER_LANE; k++) {
+        const int py = py0 + 4 * k;
+        active[k] = px < p.W && py < p.H;
+        pfy[k] = (float)py;
+        T[k] = 1.0f;
+        C0[k] = C1[k] = C2[k] = ID[k] = 0.f;
+        last[k] = 0;
+    }
+    const uint2 range = p.ranges[tile];
+    uint32_t contributor = 0;
+    for (uint32_t base = range.x; base < range.y; base += 64) {
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < PIX_PER_LANE; k++) any |= active[k];
+        if (__ballot(any) == 0) break;
+        const uint32_t s = base + lane;
+        if (s < range.y) {
+            const uint32_t gid = p.point_list[s];
+            s_a[w][lane] = p.rec_a[gid];
+            s_b[w][lane] = p.rec_b[gid];
+            s_c[w][lane] = p.rec_c[gid];
+        }
+        wave_lds_sync();
+        const int cnt = (int)min(64u, range.y - base);
+        for (int j = 0; j < cnt; j++) {
+            const float4 a = s_a[w][j];
+            const float4 b = s_b[w][j];
+            const float2 c = s_c[w][j];
+            contributor++;
+            bool still = false;
+#pragma unroll
+            for (int k = 0; k < PIX_PER_LANE; k++) {
+                const float dx = a.x - pfx, dy = a.y - pfy[k];
+                const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+                const float alpha = fminf(0.99f, b.y * fast_exp(power));
+                const bool ok = active[k] && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+                const float test_T = T[k] * (1 - alpha);
+                const bool stop = ok && test_T < 0.0001f;
+                const bool take = ok && !stop;
+                const float wgt = take ? alpha * T[k] : 0.f;
+                C0[k] = fmaf(b.z, wgt, C0[k]);
+                C1[k] = fmaf(b.w, wgt, C1[k]);
+                C2[k] = fmaf(c.x, wgt, C2[k]);
+                ID[k] = fmaf(c.y, wgt, ID[k]);
+                T[k] = take ? test_T : T[k];
+                last[k] = take ? contributor : last[k];
+                active[k] = active[k] && !stop;
+                still |= active[k];
+            }
+            if (__ballot(still) == 0) break;
+        }
+        wave_lds_sync();
+    }
+    const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
+    const size_t HW = (size_t)p.W * p.H;
+    uint32_t mx = 0;
+#pragma unroll
+    for (int k = 0; k < PIX_PER_LANE; k++) {
+        const int py = py0 + 4 * k;
+        if (px < p.W && py < p.H) {
+            const size_t pid = (size_t)py * p.W + px;
+            p.final_T[pid] = T[k];
+            p.n_contrib[pid] = last[k];
+            p.out_color[pid] = C0[k] + T[k] * bg0;
+            p.out_color[HW + pid] = C1[k] + T[k] * bg1;
+            p.out_color[2 * HW + pid] = C2[k] + T[k] * bg2;
+            if (p.out_invdepth) p.out_invdepth[pid] = ID[k];
+            mx = max(mx, last[k]);
+        }
+    }
+    mx = wave_max_u32(mx);
+    if (lane == 0) p.tile_last[tile] = mx;
+}
+
 void launch_render_fwd(hipStream_t s, const RenderFwdParams &p) {
     if (p.num_tiles <= 0) return;
-    render_fwd_kernel<<<div_up(p.num_tiles, 4), 256, 0, s>>>(p);
+    const dim3 grid(div_up(p.num_tiles, 4)), block(256);
+    const int version = tuning("fwd_version", 3);
+    const int minw = tuning("fwd_minwaves", 4);
+    if (version == 3) {
+        if (minw >= 8) render_fwd_v3_kernel<8><<<grid, block, 0, s>>>(p);
+        else render_fwd_v3_kernel<4><<<grid, block, 0, s>>>(p);
+    } else {
+        render_fwd_kernel<<<grid, block, 0, s>>>(p);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
