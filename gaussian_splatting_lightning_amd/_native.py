@@ -24,14 +24,14 @@ class ForwardArgs(ctypes.Structure):
         ("scale_modifier", ctypes.c_float), ("rotations", _fp), ("cov3D_precomp", _fp), ("viewmatrix", _fp),
         ("projmatrix", _fp), ("campos", _fp), ("tan_fovx", ctypes.c_float), ("tan_fovy", ctypes.c_float),
         ("shs", _fp), ("prefiltered", ctypes.c_int), ("antialiasing", ctypes.c_int), ("debug", ctypes.c_int),
-        ("out_color", _fp), ("out_invdepth", _fp), ("radii", _fp),
+        ("out_color", _fp), ("out_invdepth", _fp), ("radii", _fp), ("num_big_out", ctypes.c_int64),
     ]
 
 
 class BackwardArgs(ctypes.Structure):
     _fields_ = [
         ("P", ctypes.c_int), ("D", ctypes.c_int), ("M", ctypes.c_int), ("W", ctypes.c_int), ("H", ctypes.c_int),
-        ("R", ctypes.c_int64), ("background", _fp), ("means3D", _fp), ("colors_precomp", _fp),
+        ("R", ctypes.c_int64), ("num_big", ctypes.c_int64), ("background", _fp), ("means3D", _fp), ("colors_precomp", _fp),
         ("opacities", _fp), ("scales", _fp), ("scale_modifier", ctypes.c_float), ("rotations", _fp),
         ("cov3D_precomp", _fp), ("viewmatrix", _fp), ("projmatrix", _fp), ("campos", _fp),
         ("tan_fovx", ctypes.c_float), ("tan_fovy", ctypes.c_float), ("dL_dpix", _fp), ("dL_dinvdepth", _fp),
@@ -45,8 +45,8 @@ class BackwardArgs(ctypes.Structure):
 class StateLayout(ctypes.Structure):
     _fields_ = [(n, ctypes.c_size_t) for n in (
         "geom_rec_a", "geom_rec_b", "geom_rec_c", "geom_tiles", "geom_order", "geom_inst_off", "geom_inst_start",
-        "geom_clamped", "geom_sorted_depth", "geom_tile_mask", "bin_point_list", "bin_inv", "bin_keys_sorted", "img_final_T", "img_n_contrib",
-        "img_ranges", "img_tile_last")]
+        "geom_clamped", "geom_sorted_depth", "geom_tile_mask", "bin_point_list", "bin_inv", "bin_keys_sorted", "bin_sorted_u", "bin_inst_gid",
+        "img_final_T", "img_n_contrib", "img_ranges", "img_tile_last", "img_tile_loaded")]
 
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t)
@@ -85,7 +85,7 @@ def load(path: str | None = None):
     lib.gsr_binning_buffer_bytes.restype = ctypes.c_size_t
     lib.gsr_image_buffer_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
     lib.gsr_image_buffer_bytes.restype = ctypes.c_size_t
-    lib.gsr_bwd_scratch_bytes.argtypes = [ctypes.c_int, ctypes.c_int64]
+    lib.gsr_bwd_scratch_bytes.argtypes = [ctypes.c_int64, ctypes.c_int64]
     lib.gsr_bwd_scratch_bytes.restype = ctypes.c_size_t
     lib.gsr_set_profiling.argtypes = [ctypes.c_int]
     lib.gsr_set_profiling.restype = None

@@ -200,10 +200,7 @@ size_t gsr_image_buffer_bytes(int W, int H) {
     ImageState im;
     return carve_image(nullptr, W, H, im);
 }
-size_t gsr_bwd_scratch_bytes(int P, int64_t R) {
-    (void)P;
-    return bwd_scratch_bytes(R);
-}
+size_t gsr_bwd_scratch_bytes(int64_t R, int64_t num_big) { return bwd_scratch_bytes(R, num_big); }
 
 void gsr_state_layout_query(int P, int64_t R, int W, int H, gsr_state_layout *out) {
     if (!out) return;
@@ -229,13 +226,16 @@ void gsr_state_layout_query(int P, int64_t R, int W, int H, gsr_state_layout *ou
     out->bin_point_list = off(b.point_list);
     out->bin_inv = off(b.inv);
     out->bin_keys_sorted = off(b.keys_sorted);
+    out->bin_sorted_u = off(b.sorted_u);
+    out->bin_inst_gid = off(b.inst_gid);
+    out->img_tile_loaded = off(im.tile_loaded);
     out->img_final_T = off(im.final_T);
     out->img_n_contrib = off(im.n_contrib);
     out->img_ranges = off(im.ranges);
     out->img_tile_last = off(im.tile_last);
 }
 
-int gsr_forward(const gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *stream_ptr,
+int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *stream_ptr,
                 int64_t *num_rendered) {
     if (!a || !alloc || !num_rendered) return fail(GSR_ERR_ARG, "null argument");
     int rc = check_common(a->P, a->D, a->M, a->W, a->H, a->means3D, a->opacities, a->colors_precomp, a->shs,
@@ -249,6 +249,7 @@ int gsr_forward(const gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, 
     const int gx = (W + BLOCK_X - 1) / BLOCK_X, gy = (H + BLOCK_Y - 1) / BLOCK_Y;
     const uint32_t T = (uint32_t)(gx * gy);
     *num_rendered = 0;
+    a->num_big_out = 0;
     if (P == 0) {
         // the reference returns its zero-initialised outputs untouched when P == 0
         GSR_HIP(hipMemsetAsync(a->out_color, 0, sizeof(float) * 3 * (size_t)W * H, stream));
@@ -280,7 +281,7 @@ int gsr_forward(const gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, 
     pp.radii = a->radii;
     pp.g = g;
     GSR_STAGE(ST_PREPROCESS, dbg, launch_preprocess(stream, pp));
-    GSR_STAGE(ST_DEPTH_SORT, dbg, launch_radix_sort(stream, g.sort, (uint32_t)P, 32, nullptr, nullptr, nullptr));
+    GSR_STAGE(ST_DEPTH_SORT, dbg, launch_radix_sort(stream, g.sort, (uint32_t)P, 32));
     GSR_STAGE(ST_SCAN, dbg,
               launch_exclusive_scan(stream, g.tiles, g.order, (uint32_t)P, g.inst_off, g.scan_tmp,
                                     g.counters + CNT_OVERFLOW));
@@ -294,6 +295,8 @@ int gsr_forward(const gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, 
     if (hw[1 + CNT_OVERFLOW]) return fail(GSR_ERR_OVERFLOW, "more than 2^32-1 tile instances");
     const uint32_t R = hw[0];
     *num_rendered = R;
+    const uint32_t nbig = hw[1 + CNT_BIG];
+    a->num_big_out = nbig;
 
     BinningState b;
     char *bin = alloc(alloc_ctx, GSR_BUF_BINNING, carve_binning(nullptr, R, T, b));
@@ -307,8 +310,8 @@ int gsr_forward(const gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, 
         ep.order = g.order; ep.inst_off = g.inst_off; ep.tiles = g.tiles; ep.tile_mask = g.tile_mask; ep.rec_a = g.rec_a; ep.radii = a->radii;
         ep.keys_out = b.sort.k[0]; ep.inst_gid = b.inst_gid; ep.inst_start = g.inst_start;
         GSR_STAGE(ST_EXPAND, dbg, launch_expand(stream, ep));
-        GSR_STAGE(ST_TILE_SORT, dbg,
-                  launch_radix_sort(stream, b.sort, R, tile_key_bits(T), b.inst_gid, b.point_list, b.inv));
+        GSR_STAGE(ST_TILE_SORT, dbg, launch_radix_sort(stream, b.sort, R, tile_key_bits(T)));
+        GSR_HIP(hipMemsetAsync(b.inv, 0xff, sizeof(uint32_t) * (size_t)R, stream));
     }
     GSR_STAGE(ST_RANGES, dbg, {
         GSR_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * T, stream));
@@ -316,7 +319,8 @@ int gsr_forward(const gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, 
     });
     RenderFwdParams rp;
     rp.W = W; rp.H = H; rp.gx = gx; rp.gy = gy; rp.num_tiles = (int)T;
-    rp.ranges = im.ranges; rp.point_list = b.point_list;
+    rp.ranges = im.ranges; rp.sorted_u = b.sorted_u; rp.inst_gid = b.inst_gid;
+    rp.point_list = b.point_list; rp.inv = b.inv; rp.tile_loaded = im.tile_loaded;
     rp.rec_a = g.rec_a; rp.rec_b = g.rec_b; rp.rec_c = g.rec_c;
     rp.bg = a->background;
     rp.out_color = a->out_color; rp.out_invdepth = a->out_invdepth; rp.final_T = im.final_T;
@@ -350,23 +354,26 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     carve_binning(a->binning_buffer, R, T, b);
     ImageState im;
     carve_image(a->image_buffer, W, H, im);
-    char *scratch = alloc(alloc_ctx, GSR_BUF_BWD_SCRATCH, bwd_scratch_bytes(R));
+    if (a->num_big < 0 || a->num_big > a->P) return fail(GSR_ERR_ARG, "bad num_big");
+    const uint32_t nbig = (uint32_t)a->num_big;
+    char *scratch = alloc(alloc_ctx, GSR_BUF_BWD_SCRATCH, bwd_scratch_bytes(R, nbig));
     if (!scratch) return fail(GSR_ERR_ALLOC, "backward scratch allocation failed");
     float *rows = reinterpret_cast<float *>(scratch);
+    float *bigsum = bwd_bigsum_ptr(scratch, R);
 
     if (R > 0) {
         RenderBwdParams rp;
         rp.W = W; rp.H = H; rp.gx = gx; rp.gy = gy; rp.num_tiles = (int)T;
         rp.ranges = im.ranges; rp.point_list = b.point_list; rp.n_contrib = im.n_contrib;
-        rp.tile_last = im.tile_last;
+        rp.tile_last = im.tile_last; rp.tile_loaded = im.tile_loaded;
         rp.rec_a = g.rec_a; rp.rec_b = g.rec_b; rp.rec_c = g.rec_c;
         rp.bg = a->background; rp.final_T = im.final_T; rp.dL_dpix = a->dL_dpix; rp.dL_dinvdepth = a->dL_dinvdepth;
         rp.rows = rows;
         GSR_STAGE(ST_RENDER_BWD, dbg, launch_render_bwd(stream, rp));
         BigReduceParams bp;
-        bp.counters = g.counters; bp.big_list = g.big_list; bp.inst_start = g.inst_start; bp.tiles = g.tiles;
-        bp.inv = b.inv; bp.rows = rows;
-        GSR_STAGE(ST_BIG_REDUCE, dbg, launch_big_reduce(stream, bp, (uint32_t)P));
+        bp.big_list = g.big_list; bp.inst_start = g.inst_start; bp.tiles = g.tiles;
+        bp.inv = b.inv; bp.rows = rows; bp.bigsum = bigsum;
+        GSR_STAGE(ST_BIG_REDUCE, dbg, launch_big_reduce(stream, bp, nbig));
     }
     PreprocessBwdParams pp;
     pp.P = P; pp.D = a->D; pp.M = a->M; pp.W = W; pp.H = H;
@@ -380,6 +387,7 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     pp.cov3D_precomp = a->cov3D_precomp; pp.shs = (a->colors_precomp ? nullptr : a->shs);
     pp.view = a->viewmatrix; pp.proj = a->projmatrix; pp.campos = a->campos;
     pp.radii = a->radii; pp.tiles = g.tiles; pp.inst_start = g.inst_start; pp.inv = b.inv; pp.clamped = g.clamped;
+    pp.big_slot = g.big_slot; pp.bigsum = bigsum;
     pp.rows = rows;
     pp.sh_vec16 = pp.shs && a->M == 16 && a->dL_dsh && (((uintptr_t)pp.shs | (uintptr_t)a->dL_dsh) & 15) == 0 &&
                   tuning("sh_vec16", 1);

@@ -30,125 +30,6 @@ __device__ __forceinline__ void add_row(const float *__restrict__ rows, uint32_t
     acc[8] += c.x; acc[9] += c.y;
 }
 
-template <bool HAS_INV, int MIN_WAVES>
-__global__ __launch_bounds__(256, MIN_WAVES) void render_bwd_kernel(RenderBwdParams p) {
-    __shared__ float4 s_a[4][64];
-    __shared__ float4 s_b[4][64];
-    __shared__ float2 s_c[4][64];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tile = blockIdx.x * 4 + w;
-    if (tile >= p.num_tiles) return;
-    const int tx = tile % p.gx, ty = tile / p.gx;
-    const int px = tx * BLOCK_X + (lane & 15);
-    const int py0 = ty * BLOCK_Y + (lane >> 4);
-    const float pfx = (float)px;
-    const uint2 range = p.ranges[tile];
-    const uint32_t tl = p.tile_last[tile];
-
-    // Instances past the last contributor of every pixel receive exactly zero gradient.
-    for (uint32_t s = range.x + tl + lane; s < range.y; s += 64) {
-        const float z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        store_row(p.rows, s, z);
-    }
-    if (tl == 0) return;
-
-    const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
-    const size_t HW = (size_t)p.W * p.H;
-    // Per-pixel state.  The reference keeps last_alpha / last_color and updates accum_rec lazily when the
-    // NEXT contributor arrives; here accum_rec is advanced eagerly right after a contributor is used,
-    // with the identical expression alpha*c + (1-alpha)*accum, which drops four registers per pixel.
-    float T[PIX_PER_LANE], nbg[PIX_PER_LANE], dp0[PIX_PER_LANE], dp1[PIX_PER_LANE], dp2[PIX_PER_LANE];
-    float dinv[PIX_PER_LANE], ar0[PIX_PER_LANE], ar1[PIX_PER_LANE], ar2[PIX_PER_LANE], ainv[PIX_PER_LANE];
-    uint32_t lastc[PIX_PER_LANE];
-#pragma unroll
-    for (int k = 0; k < PIX_PER_LANE; k++) {
-        const int py = py0 + 4 * k;
-        const bool inside = px < p.W && py < p.H;
-        const size_t pid = inside ? (size_t)py * p.W + px : 0;
-        const float Tf = inside ? p.final_T[pid] : 0.f;
-        T[k] = Tf;
-        lastc[k] = inside ? p.n_contrib[pid] : 0u;
-        dp0[k] = inside ? p.dL_dpix[pid] : 0.f;
-        dp1[k] = inside ? p.dL_dpix[HW + pid] : 0.f;
-        dp2[k] = inside ? p.dL_dpix[2 * HW + pid] : 0.f;
-        dinv[k] = (HAS_INV && inside) ? p.dL_dinvdepth[pid] : 0.f;
-        nbg[k] = -Tf * (bg0 * dp0[k] + bg1 * dp1[k] + bg2 * dp2[k]);
-        ar0[k] = ar1[k] = ar2[k] = ainv[k] = 0.f;
-    }
-    const float ddelx_dx = 0.5f * p.W, ddely_dy = 0.5f * p.H;
-
-    for (int bend = (int)tl; bend > 0; bend -= 64) {
-        const int cnt = min(64, bend);
-        // lane j holds list index bend-1-j (descending)
-        if (lane < cnt) {
-            const uint32_t gid = p.point_list[range.x + (uint32_t)(bend - 1 - lane)];
-            s_a[w][lane] = p.rec_a[gid];
-            s_b[w][lane] = p.rec_b[gid];
-            s_c[w][lane] = p.rec_c[gid];
-        }
-        wave_lds_sync();
-        float row[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        for (int j = 0; j < cnt; j++) {
-            const uint32_t idx = (uint32_t)(bend - 1 - j);
-            const float4 a = s_a[w][j];
-            const float4 b = s_b[w][j];
-            const float2 c = s_c[w][j];
-            float g[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-            bool any = false;
-#pragma unroll
-            for (int k = 0; k < PIX_PER_LANE; k++) {
-                if (idx >= lastc[k]) continue;
-                const float dx = a.x - pfx, dy = a.y - (float)(py0 + 4 * k);
-                const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
-                if (power > 0.0f) continue;
-                const float G = fast_exp(power);
-                const float alpha = fminf(0.99f, b.y * G);
-                if (alpha < 1.0f / 255.0f) continue;
-                any = true;
-                const float one_m = 1.f - alpha;
-                const float r = fast_rcp(one_m);
-                T[k] = T[k] * r;
-                const float wgt = alpha * T[k];
-                float dL_dalpha = (b.z - ar0[k]) * dp0[k];
-                dL_dalpha += (b.w - ar1[k]) * dp1[k];
-                dL_dalpha += (c.x - ar2[k]) * dp2[k];
-                g[6] += wgt * dp0[k];
-                g[7] += wgt * dp1[k];
-                g[8] += wgt * dp2[k];
-                ar0[k] = alpha * b.z + one_m * ar0[k];
-                ar1[k] = alpha * b.w + one_m * ar1[k];
-                ar2[k] = alpha * c.x + one_m * ar2[k];
-                if (HAS_INV) {
-                    dL_dalpha += (c.y - ainv[k]) * dinv[k];
-                    g[9] += wgt * dinv[k];
-                    ainv[k] = alpha * c.y + one_m * ainv[k];
-                }
-                dL_dalpha = dL_dalpha * T[k] + nbg[k] * r;
-                const float dL_dG = b.y * dL_dalpha;
-                const float gdx = G * dx, gdy = G * dy;
-                const float dG_ddelx = -gdx * a.z - gdy * a.w;
-                const float dG_ddely = -gdy * b.x - gdx * a.w;
-                g[0] += dL_dG * dG_ddelx * ddelx_dx;
-                g[1] += dL_dG * dG_ddely * ddely_dy;
-                g[2] += -0.5f * gdx * dx * dL_dG;
-                g[3] += -0.5f * gdx * dy * dL_dG;
-                g[4] += -0.5f * gdy * dy * dL_dG;
-                g[5] += G * dL_dalpha;
-            }
-            if (__ballot(any)) {
-#pragma unroll
-                for (int v = 0; v < 10; v++) {
-                    if (!HAS_INV && v == 9) continue;
-                    const float sum = wave_sum(g[v]);
-                    row[v] = (lane == j) ? sum : row[v];
-                }
-            }
-        }
-        if (lane < cnt) store_row(p.rows, range.x + (uint32_t)(bend - 1 - lane), row);
-        wave_lds_sync();
-    }
-}
-
 // ------------------------------------------------------------------------------------------------
 // v3: moment accumulation + two-level reduction.
 //   Per active (pixel, instance) pair a lane accumulates q = G * dL/dalpha and the moments q, q dx, q dy,
@@ -187,7 +68,10 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_bwd_v3_kernel(RenderBwd
     const uint2 range = p.ranges[tile];
     const uint32_t tl = p.tile_last[tile];
 
-    for (uint32_t s = range.x + tl + lane; s < range.y; s += 64) {
+    // Loaded instances past every pixel's last contributor get exactly zero gradient; instances the
+    // forward never loaded have inv = INV_NONE and are skipped by the per-Gaussian reduction.
+    const uint32_t loaded = p.tile_loaded[tile];
+    for (uint32_t s = range.x + tl + lane; s < range.x + loaded; s += 64) {
         const float z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         store_row(p.rows, s, z);
     }
@@ -311,210 +195,51 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_bwd_v3_kernel(RenderBwd
     }
 }
 
-// v4: v3 with the per-pixel body predicated instead of branched.
-template <bool HAS_INV, int MIN_WAVES>
-__global__ __launch_bounds__(256, MIN_WAVES) void render_bwd_v4_kernel(RenderBwdParams p) {
-    __shared__ float4 s_a[4][BWD_BATCH];
-    __shared__ float4 s_b[4][BWD_BATCH];
-    __shared__ float2 s_c[4][BWD_BATCH];
-    __shared__ float4 s_part[4][BWD_BATCH][2][3];  // [wave][instance][half][10 sums + 2 pad]
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tile = blockIdx.x * 4 + w;
-    if (tile >= p.num_tiles) return;
-    const int tx = tile % p.gx, ty = tile / p.gx;
-    const int px = tx * BLOCK_X + (lane & 15);
-    const int py0 = ty * BLOCK_Y + (lane >> 4);
-    const float pfx = (float)px;
-    const uint2 range = p.ranges[tile];
-    const uint32_t tl = p.tile_last[tile];
-
-    for (uint32_t s = range.x + tl + lane; s < range.y; s += 64) {
-        const float z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        store_row(p.rows, s, z);
-    }
-    if (tl == 0) return;
-
-    const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
-    const size_t HW = (size_t)p.W * p.H;
-    float T[PIX_PER_LANE], nbg[PIX_PER_LANE], dp0[PIX_PER_LANE], dp1[PIX_PER_LANE], dp2[PIX_PER_LANE];
-    float dinv[PIX_PER_LANE], ar0[PIX_PER_LANE], ar1[PIX_PER_LANE], ar2[PIX_PER_LANE], ainv[PIX_PER_LANE];
-    uint32_t lastc[PIX_PER_LANE];
-#pragma unroll
-    for (int k = 0; k < PIX_PER_LANE; k++) {
-        const int py = py0 + 4 * k;
-        const bool inside = px < p.W && py < p.H;
-        const size_t pid = inside ? (size_t)py * p.W + px : 0;
-        const float Tf = inside ? p.final_T[pid] : 0.f;
-        T[k] = Tf;
-        lastc[k] = inside ? p.n_contrib[pid] : 0u;
-        dp0[k] = inside ? p.dL_dpix[pid] : 0.f;
-        dp1[k] = inside ? p.dL_dpix[HW + pid] : 0.f;
-        dp2[k] = inside ? p.dL_dpix[2 * HW + pid] : 0.f;
-        dinv[k] = (HAS_INV && inside) ? p.dL_dinvdepth[pid] : 0.f;
-        nbg[k] = -Tf * (bg0 * dp0[k] + bg1 * dp1[k] + bg2 * dp2[k]);
-        ar0[k] = ar1[k] = ar2[k] = ainv[k] = 0.f;
-    }
-    const float hW = 0.5f * p.W, hH = 0.5f * p.H;
-
-    for (int bend = (int)tl; bend > 0; bend -= BWD_BATCH) {
-        const int cnt = min(BWD_BATCH, bend);
-        float4 my_a = make_float4(0, 0, 0, 0), my_b = my_a;
-        if (lane < cnt) {
-            const uint32_t gid = p.point_list[range.x + (uint32_t)(bend - 1 - lane)];
-            my_a = p.rec_a[gid];
-            my_b = p.rec_b[gid];
-            s_a[w][lane] = my_a;
-            s_b[w][lane] = my_b;
-            s_c[w][lane] = p.rec_c[gid];
-        }
-        wave_lds_sync();
-        for (int j = 0; j < cnt; j++) {
-            const uint32_t idx = (uint32_t)(bend - 1 - j);
-            const float4 a = s_a[w][j];
-            const float4 b = s_b[w][j];
-            const float2 c = s_c[w][j];
-            float m[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-            bool any = false;
-#pragma unroll
-            for (int k = 0; k < PIX_PER_LANE; k++) {
-                // predicated: every lane evaluates the pixel, state and sums change only where ok
-                const float dx = a.x - pfx, dy = a.y - (float)(py0 + 4 * k);
-                const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
-                const float G = fast_exp(power);
-                const float alpha = fminf(0.99f, b.y * G);
-                const bool ok = idx < lastc[k] && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
-                any |= ok;
-                const float one_m = 1.f - alpha;
-                const float r = fast_rcp(one_m);
-                const float Tn = T[k] * r;
-                T[k] = ok ? Tn : T[k];
-                const float wgt = ok ? alpha * Tn : 0.f;
-                float dL_dalpha = (b.z - ar0[k]) * dp0[k];
-                dL_dalpha += (b.w - ar1[k]) * dp1[k];
-                dL_dalpha += (c.x - ar2[k]) * dp2[k];
-                m[6] = fmaf(wgt, dp0[k], m[6]);
-                m[7] = fmaf(wgt, dp1[k], m[7]);
-                m[8] = fmaf(wgt, dp2[k], m[8]);
-                const float al = ok ? alpha : 0.f;  // al = 0 leaves the running blend unchanged
-                ar0[k] = al * b.z + (1.f - al) * ar0[k];
-                ar1[k] = al * b.w + (1.f - al) * ar1[k];
-                ar2[k] = al * c.x + (1.f - al) * ar2[k];
-                if (HAS_INV) {
-                    dL_dalpha += (c.y - ainv[k]) * dinv[k];
-                    m[9] = fmaf(wgt, dinv[k], m[9]);
-                    ainv[k] = al * c.y + (1.f - al) * ainv[k];
-                }
-                dL_dalpha = dL_dalpha * Tn + nbg[k] * r;
-                const float q = ok ? G * dL_dalpha : 0.f;
-                const float qdx = q * dx, qdy = q * dy;
-                m[0] += q;
-                m[1] += qdx;
-                m[2] += qdy;
-                m[3] = fmaf(qdx, dx, m[3]);
-                m[4] = fmaf(qdx, dy, m[4]);
-                m[5] = fmaf(qdy, dy, m[5]);
-            }
-            float4 *dst = &s_part[w][j][0][0];
-            if (__ballot(any)) {
-#pragma unroll
-                for (int v = 0; v < 10; v++) m[v] = dpp_rows_then_pairs(m[v]);
-                if ((lane & 31) == 31) {  // lanes 31 / 63: (row0 + row1) / (row2 + row3)
-                    float4 *d = dst + 3 * (lane >> 5);
-                    d[0] = make_float4(m[0], m[1], m[2], m[3]);
-                    d[1] = make_float4(m[4], m[5], m[6], m[7]);
-                    d[2] = make_float4(m[8], m[9], 0.f, 0.f);
-                }
-            } else if ((lane & 31) == 31) {
-                float4 *d = dst + 3 * (lane >> 5);
-                d[0] = d[1] = d[2] = make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-        }
-        wave_lds_sync();
-        if (lane < cnt) {
-            const float4 *src = &s_part[w][lane][0][0];
-            const float4 u0 = src[0], u1 = src[1], u2 = src[2], v0 = src[3], v1 = src[4], v2 = src[5];
-            const float S = u0.x + v0.x, Sx = u0.y + v0.y, Sy = u0.z + v0.z, Sxx = u0.w + v0.w;
-            const float Sxy = u1.x + v1.x, Syy = u1.y + v1.y;
-            const float o = my_b.y, ca = my_a.z, cb = my_a.w, cc = my_b.x;
-            float row[10];
-            row[0] = -o * hW * (ca * Sx + cb * Sy);
-            row[1] = -o * hH * (cb * Sx + cc * Sy);
-            row[2] = -0.5f * o * Sxx;
-            row[3] = -0.5f * o * Sxy;
-            row[4] = -0.5f * o * Syy;
-            row[5] = S;
-            row[6] = u1.z + v1.z;
-            row[7] = u1.w + v1.w;
-            row[8] = u2.x + v2.x;
-            row[9] = u2.y + v2.y;
-            store_row(p.rows, range.x + (uint32_t)(bend - 1 - lane), row);
-        }
-        wave_lds_sync();
-    }
-}
-
-template <bool HAS_INV>
-static void launch_bwd_variant(hipStream_t s, const RenderBwdParams &p, int version, int minw) {
-    const dim3 grid(div_up(p.num_tiles, 4)), block(256);
-    if (version == 4) {
-        switch (minw) {
-            case 5: render_bwd_v4_kernel<HAS_INV, 5><<<grid, block, 0, s>>>(p); break;
-            case 4: render_bwd_v4_kernel<HAS_INV, 4><<<grid, block, 0, s>>>(p); break;
-            default: render_bwd_v4_kernel<HAS_INV, 1><<<grid, block, 0, s>>>(p); break;
-        }
-    } else if (version == 3) {
-        switch (minw) {
-            case 5: render_bwd_v3_kernel<HAS_INV, 5><<<grid, block, 0, s>>>(p); break;
-            case 4: render_bwd_v3_kernel<HAS_INV, 4><<<grid, block, 0, s>>>(p); break;
-            default: render_bwd_v3_kernel<HAS_INV, 1><<<grid, block, 0, s>>>(p); break;
-        }
-    } else {
-        if (minw >= 4) render_bwd_kernel<HAS_INV, 4><<<grid, block, 0, s>>>(p);
-        else render_bwd_kernel<HAS_INV, 1><<<grid, block, 0, s>>>(p);
-    }
-}
-
 void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
     if (p.num_tiles <= 0) return;
-    const int version = tuning("bwd_version", 3);
+    const dim3 grid(div_up(p.num_tiles, 4)), block(256);
     const int minw = tuning("bwd_minwaves", 4);
-    if (p.dL_dinvdepth) launch_bwd_variant<true>(s, p, version, minw);
-    else launch_bwd_variant<false>(s, p, version, minw);
+    if (p.dL_dinvdepth) {
+        if (minw >= 4) render_bwd_v3_kernel<true, 4><<<grid, block, 0, s>>>(p);
+        else render_bwd_v3_kernel<true, 1><<<grid, block, 0, s>>>(p);
+    } else {
+        if (minw >= 4) render_bwd_v3_kernel<false, 4><<<grid, block, 0, s>>>(p);
+        else render_bwd_v3_kernel<false, 1><<<grid, block, 0, s>>>(p);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
 // Gaussians with many instances: one block sums all their rows (fixed stride order, deterministic)
-// and stores the total in the Gaussian's first row, which the preprocess backward then reads alone.
+// into bigsum[slot], which the preprocess backward then reads instead of walking the rows.
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void big_reduce_kernel(BigReduceParams p) {
     __shared__ float s_part[4][10];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t nbig = p.counters[CNT_BIG];
-    for (uint32_t bi = blockIdx.x; bi < nbig; bi += gridDim.x) {
-        const uint32_t gidx = p.big_list[bi];
-        const uint32_t start = p.inst_start[gidx], cnt = p.tiles[gidx];
-        float acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        for (uint32_t k = threadIdx.x; k < cnt; k += 256) add_row(p.rows, p.inv[start + k], acc);
+    const uint32_t bi = blockIdx.x;
+    const uint32_t gidx = p.big_list[bi];
+    const uint32_t start = p.inst_start[gidx], cnt = p.tiles[gidx];
+    float acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t k = threadIdx.x; k < cnt; k += 256) {
+        const uint32_t sidx = p.inv[start + k];
+        if (sidx != INV_NONE) add_row(p.rows, sidx, acc);
+    }
 #pragma unroll
-        for (int v = 0; v < 10; v++) {
-            const float sum = wave_sum(acc[v]);
-            if (lane == 0) s_part[w][v] = sum;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            float tot[10];
+    for (int v = 0; v < 10; v++) {
+        const float sum = wave_sum(acc[v]);
+        if (lane == 0) s_part[w][v] = sum;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float tot[10];
 #pragma unroll
-            for (int v = 0; v < 10; v++) tot[v] = ((s_part[0][v] + s_part[1][v]) + s_part[2][v]) + s_part[3][v];
-            store_row(p.rows, p.inv[start], tot);
-        }
-        __syncthreads();
+        for (int v = 0; v < 10; v++) tot[v] = ((s_part[0][v] + s_part[1][v]) + s_part[2][v]) + s_part[3][v];
+        store_row(p.bigsum, bi, tot);
     }
 }
 
-void launch_big_reduce(hipStream_t s, const BigReduceParams &p, uint32_t max_big) {
-    if (max_big == 0) return;
-    const uint32_t grid = max_big < 2048u ? max_big : 2048u;
-    big_reduce_kernel<<<grid, 256, 0, s>>>(p);
+void launch_big_reduce(hipStream_t s, const BigReduceParams &p, uint32_t nbig) {
+    if (nbig == 0) return;
+    big_reduce_kernel<<<nbig, 256, 0, s>>>(p);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -569,17 +294,17 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
     if (vis) {
         const uint32_t start = p.inst_start[i], cnt = p.tiles[i];
         if (cnt > BIG_GAUSSIAN_TILES) {
-            add_row(p.rows, p.inv[start], gs);
+            add_row(p.bigsum, p.big_slot[i], gs);
         } else {
             // issue the index loads, then all row loads of a group, before summing (memory-level parallelism)
             for (uint32_t k0 = 0; k0 < cnt; k0 += 4) {
                 uint32_t sidx[4];
 #pragma unroll
-                for (int j = 0; j < 4; j++) sidx[j] = (k0 + j < cnt) ? p.inv[start + k0 + j] : 0xffffffffu;
+                for (int j = 0; j < 4; j++) sidx[j] = (k0 + j < cnt) ? p.inv[start + k0 + j] : INV_NONE;
                 float4 ra[4], rb[4], rc[4];
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    if (sidx[j] != 0xffffffffu) {
+                    if (sidx[j] != INV_NONE) {
                         const float4 *src = reinterpret_cast<const float4 *>(p.rows + (size_t)sidx[j] * GRAD_ROW);
                         ra[j] = src[0];
                         rb[j] = src[1];

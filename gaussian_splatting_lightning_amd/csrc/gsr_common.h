@@ -77,6 +77,7 @@ struct GeomState {
     uint32_t *inst_off;    // P+1: exclusive scan of tiles in depth order, [P] = total
     uint32_t *inst_start;  // P: first instance (expansion order) of each Gaussian
     uint32_t *big_list;    // P: Gaussians with > BIG_GAUSSIAN_TILES tiles
+    uint32_t *big_slot;    // P: index of a big Gaussian in big_list (valid only for big ones)
     uint32_t *scan_tmp;    // block sums for the instance scan
     SortScratch sort;      // depth sort (P keys); final order lands in sort.v[0]
     const uint32_t *order; // = sort.v[0] after the (even-pass) depth sort
@@ -95,6 +96,7 @@ inline size_t carve_geom(char *base, int P, GeomState &g) {
     g.inst_off = c.take<uint32_t>((size_t)n + 1);
     g.inst_start = c.take<uint32_t>(n);
     g.big_list = c.take<uint32_t>(n);
+    g.big_slot = c.take<uint32_t>(n);
     g.scan_tmp = c.take<uint32_t>(div_up(n + 1, SCAN_TILE) + 1);
     carve_sort(c, g.sort, n, true);
     g.depth_key = g.sort.k[0];  // preprocess writes the depth-sort keys in place
@@ -111,11 +113,14 @@ inline int radix_passes(int bits) { return (bits + 7) / 8; }
 
 struct BinningState {
     uint32_t *inst_gid;    // R: Gaussian of each instance (expansion order)
-    uint32_t *point_list;  // R: Gaussian ids sorted by (tile, depth, id)
-    uint32_t *inv;         // R: expansion index -> sorted position
+    uint32_t *point_list;  // R: Gaussian ids sorted by (tile, depth, id); written by the forward composite
+                           //    for the instances it loads (every instance any pixel can reach)
+    uint32_t *inv;         // R: expansion index -> sorted position, for loaded instances; else INV_NONE
     uint32_t *keys_sorted; // R: tile id of each sorted instance
+    uint32_t *sorted_u;    // R: expansion index of each sorted instance (radix-sort values)
     SortScratch sort;      // tile sort (R keys)
 };
+constexpr uint32_t INV_NONE = 0xffffffffu;
 
 inline size_t carve_binning(char *base, int64_t R, uint32_t num_tiles, BinningState &b) {
     Carver c(base);
@@ -124,9 +129,10 @@ inline size_t carve_binning(char *base, int64_t R, uint32_t num_tiles, BinningSt
     b.point_list = c.take<uint32_t>(n ? n : 1);
     b.inv = c.take<uint32_t>(n ? n : 1);
     int passes = radix_passes(tile_key_bits(num_tiles));
-    carve_sort(c, b.sort, n, passes > 2);
-    // keys end in k[passes & 1]
+    carve_sort(c, b.sort, n, passes >= 2);
+    // keys and values end in slot (passes & 1)
     b.keys_sorted = b.sort.k[passes & 1];
+    b.sorted_u = b.sort.v[passes & 1];
     return c.off + 256;
 }
 
@@ -135,6 +141,7 @@ struct ImageState {
     uint32_t *n_contrib;  // W*H
     uint2 *ranges;        // T
     uint32_t *tile_last;  // T: max n_contrib over the tile's pixels
+    uint32_t *tile_loaded; // T: instances of the tile the forward composite gathered (>= tile_last)
 };
 
 inline size_t carve_image(char *base, int W, int H, ImageState &im) {
@@ -145,10 +152,18 @@ inline size_t carve_image(char *base, int W, int H, ImageState &im) {
     im.n_contrib = c.take<uint32_t>(npix ? npix : 1);
     im.ranges = c.take<uint2>((size_t)gx * gy + 1);
     im.tile_last = c.take<uint32_t>((size_t)gx * gy + 1);
+    im.tile_loaded = c.take<uint32_t>((size_t)gx * gy + 1);
     return c.off + 256;
 }
 
-inline size_t bwd_scratch_bytes(int64_t R) { return align_up((size_t)(R ? R : 1) * GRAD_ROW * sizeof(float), 256) + 256; }
+// backward scratch: one gradient row per instance, then one summed row per big Gaussian
+inline size_t bwd_scratch_bytes(int64_t R, int64_t nbig) {
+    return align_up((size_t)(R ? R : 1) * GRAD_ROW * sizeof(float), 256) +
+           align_up((size_t)(nbig ? nbig : 1) * GRAD_ROW * sizeof(float), 256) + 256;
+}
+inline float *bwd_bigsum_ptr(char *scratch, int64_t R) {
+    return reinterpret_cast<float *>(scratch + align_up((size_t)(R ? R : 1) * GRAD_ROW * sizeof(float), 256));
+}
 
 // ------------------------------------------------------------------------------------------------
 // device helpers

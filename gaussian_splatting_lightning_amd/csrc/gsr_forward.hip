@@ -106,6 +106,7 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessParams p) {
     if (kept > BIG_GAUSSIAN_TILES) {
         const uint32_t slot = atomicAdd(&g.counters[CNT_BIG], 1u);
         g.big_list[slot] = (uint32_t)i;
+        g.big_slot[i] = slot;
     }
 }
 
@@ -248,96 +249,10 @@ void launch_identify_ranges(hipStream_t s, const uint32_t *keys_sorted, uint32_t
 // broadcast to all lanes.  Front-to-back: alpha = min(0.99, o*exp(power)); skip alpha < 1/255; stop a
 // pixel before the Gaussian that would take T below 1e-4.  No block barriers: the four waves of a
 // block work on four independent tiles and retire independently.
+// The batch gather also materialises, for exactly the instances it loads, the sorted Gaussian id list
+// (point_list) and the inverse permutation (inv) that the backward needs, so the tile sort itself writes
+// only coalesced runs; instances no pixel reaches are never gathered and keep inv = INV_NONE.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 8) void render_fwd_kernel(RenderFwdParams p) {
-    __shared__ float4 s_a[4][64];
-    __shared__ float4 s_b[4][64];
-    __shared__ float2 s_c[4][64];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tile = blockIdx.x * 4 + w;
-    if (tile >= p.num_tiles) return;
-    const int tx = tile % p.gx, ty = tile / p.gx;
-    const int px = tx * BLOCK_X + (lane & 15);
-    const int py0 = ty * BLOCK_Y + (lane >> 4);
-    const float pfx = (float)px;
-
-    float T[PIX_PER_LANE], C0[PIX_PER_LANE], C1[PIX_PER_LANE], C2[PIX_PER_LANE], ID[PIX_PER_LANE];
-    uint32_t last[PIX_PER_LANE];
-    bool active[PIX_PER_LANE];
-#pragma unroll
-    for (int k = 0; k < PIX_PER_LANE; k++) {
-        const int py = py0 + 4 * k;
-        active[k] = px < p.W && py < p.H;
-        T[k] = 1.0f;
-        C0[k] = C1[k] = C2[k] = ID[k] = 0.f;
-        last[k] = 0;
-    }
-    const uint2 range = p.ranges[tile];
-    uint32_t contributor = 0;
-    for (uint32_t base = range.x; base < range.y; base += 64) {
-        bool any = false;
-#pragma unroll
-        for (int k = 0; k < PIX_PER_LANE; k++) any |= active[k];
-        if (__ballot(any) == 0) break;
-        const uint32_t s = base + lane;
-        if (s < range.y) {
-            const uint32_t gid = p.point_list[s];
-            s_a[w][lane] = p.rec_a[gid];
-            s_b[w][lane] = p.rec_b[gid];
-            s_c[w][lane] = p.rec_c[gid];
-        }
-        wave_lds_sync();
-        const int cnt = (int)min(64u, range.y - base);
-        for (int j = 0; j < cnt; j++) {
-            const float4 a = s_a[w][j];
-            const float4 b = s_b[w][j];
-            const float2 c = s_c[w][j];
-            contributor++;
-#pragma unroll
-            for (int k = 0; k < PIX_PER_LANE; k++) {
-                if (!active[k]) continue;
-                const float dx = a.x - pfx, dy = a.y - (float)(py0 + 4 * k);
-                const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
-                if (power > 0.0f) continue;
-                const float alpha = fminf(0.99f, b.y * fast_exp(power));
-                if (alpha < 1.0f / 255.0f) continue;
-                const float test_T = T[k] * (1 - alpha);
-                if (test_T < 0.0001f) { active[k] = false; continue; }
-                C0[k] += b.z * alpha * T[k];
-                C1[k] += b.w * alpha * T[k];
-                C2[k] += c.x * alpha * T[k];
-                ID[k] += c.y * alpha * T[k];
-                T[k] = test_T;
-                last[k] = contributor;
-            }
-            bool still = false;
-#pragma unroll
-            for (int k = 0; k < PIX_PER_LANE; k++) still |= active[k];
-            if (__ballot(still) == 0) break;
-        }
-        wave_lds_sync();
-    }
-    const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
-    const size_t HW = (size_t)p.W * p.H;
-    uint32_t mx = 0;
-#pragma unroll
-    for (int k = 0; k < PIX_PER_LANE; k++) {
-        const int py = py0 + 4 * k;
-        if (px < p.W && py < p.H) {
-            const size_t pid = (size_t)py * p.W + px;
-            p.final_T[pid] = T[k];
-            p.n_contrib[pid] = last[k];
-            p.out_color[pid] = C0[k] + T[k] * bg0;
-            p.out_color[HW + pid] = C1[k] + T[k] * bg1;
-            p.out_color[2 * HW + pid] = C2[k] + T[k] * bg2;
-            if (p.out_invdepth) p.out_invdepth[pid] = ID[k];
-            mx = max(mx, last[k]);
-        }
-    }
-    mx = wave_max_u32(mx);
-    if (lane == 0) p.tile_last[tile] = mx;
-}
-
 // v3: the four pixels of a lane are updated with predication instead of exec-mask branches, so the
 // compiler can interleave the four independent pixel chains and no per-pixel branch bookkeeping is issued.
 // Colour accumulation uses w = alpha * T once per contributor (one FMA per channel).
@@ -369,6 +284,7 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v3_kernel(RenderFwd
     }
     const uint2 range = p.ranges[tile];
     uint32_t contributor = 0;
+    uint32_t loaded_end = range.x;
     for (uint32_t base = range.x; base < range.y; base += 64) {
         bool any = false;
 #pragma unroll
@@ -376,11 +292,15 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v3_kernel(RenderFwd
         if (__ballot(any) == 0) break;
         const uint32_t s = base + lane;
         if (s < range.y) {
-            const uint32_t gid = p.point_list[s];
+            const uint32_t u = p.sorted_u[s];
+            const uint32_t gid = p.inst_gid[u];
+            p.point_list[s] = gid;
+            p.inv[u] = s;
             s_a[w][lane] = p.rec_a[gid];
             s_b[w][lane] = p.rec_b[gid];
             s_c[w][lane] = p.rec_c[gid];
         }
+        loaded_end = min(range.y, base + 64u);
         wave_lds_sync();
         const int cnt = (int)min(64u, range.y - base);
         for (int j = 0; j < cnt; j++) {
@@ -430,20 +350,17 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v3_kernel(RenderFwd
         }
     }
     mx = wave_max_u32(mx);
-    if (lane == 0) p.tile_last[tile] = mx;
+    if (lane == 0) {
+        p.tile_last[tile] = mx;
+        p.tile_loaded[tile] = loaded_end - range.x;
+    }
 }
 
 void launch_render_fwd(hipStream_t s, const RenderFwdParams &p) {
     if (p.num_tiles <= 0) return;
     const dim3 grid(div_up(p.num_tiles, 4)), block(256);
-    const int version = tuning("fwd_version", 3);
-    const int minw = tuning("fwd_minwaves", 4);
-    if (version == 3) {
-        if (minw >= 8) render_fwd_v3_kernel<8><<<grid, block, 0, s>>>(p);
-        else render_fwd_v3_kernel<4><<<grid, block, 0, s>>>(p);
-    } else {
-        render_fwd_kernel<<<grid, block, 0, s>>>(p);
-    }
+    if (tuning("fwd_minwaves", 4) >= 8) render_fwd_v3_kernel<8><<<grid, block, 0, s>>>(p);
+    else render_fwd_v3_kernel<4><<<grid, block, 0, s>>>(p);
 }
 
 // ------------------------------------------------------------------------------------------------

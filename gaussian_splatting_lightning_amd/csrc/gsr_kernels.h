@@ -16,10 +16,8 @@ void launch_exclusive_scan(hipStream_t s, const uint32_t *in, const uint32_t *id
 
 // LSD radix sort of n (key, value) pairs on bits [0, nbits).  Keys start in sc.k[0]; values are the
 // implicit iota 0..n-1.  After ceil(nbits/8) passes the keys are in sc.k[passes & 1] and the values in
-// sc.v[passes & 1].  With `gid_map` set, the last pass instead writes vals_final[pos] = gid_map[v] and
-// inv[v] = pos (the per-instance Gaussian id and the inverse permutation).
-void launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, const uint32_t *gid_map,
-                       uint32_t *vals_final, uint32_t *inv);
+// sc.v[passes & 1].
+void launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits);
 
 // ---- forward (gsr_forward.hip) ----
 struct PreprocessParams {
@@ -50,7 +48,8 @@ void launch_identify_ranges(hipStream_t s, const uint32_t *keys_sorted, uint32_t
 struct RenderFwdParams {
     int W, H, gx, gy, num_tiles;
     const uint2 *ranges;
-    const uint32_t *point_list;
+    const uint32_t *sorted_u, *inst_gid;
+    uint32_t *point_list, *inv, *tile_loaded;
     const float4 *rec_a, *rec_b;
     const float2 *rec_c;
     const float *bg;
@@ -65,7 +64,7 @@ void launch_mark_visible(hipStream_t s, int P, const float *means3D, const float
 struct RenderBwdParams {
     int W, H, gx, gy, num_tiles;
     const uint2 *ranges;
-    const uint32_t *point_list, *n_contrib, *tile_last;
+    const uint32_t *point_list, *n_contrib, *tile_last, *tile_loaded;
     const float4 *rec_a, *rec_b;
     const float2 *rec_c;
     const float *bg, *final_T, *dL_dpix, *dL_dinvdepth;
@@ -74,10 +73,11 @@ struct RenderBwdParams {
 void launch_render_bwd(hipStream_t s, const RenderBwdParams &p);
 
 struct BigReduceParams {
-    const uint32_t *counters, *big_list, *inst_start, *tiles, *inv;
-    float *rows;
+    const uint32_t *big_list, *inst_start, *tiles, *inv;
+    const float *rows;
+    float *bigsum;  // nbig x GRAD_ROW
 };
-void launch_big_reduce(hipStream_t s, const BigReduceParams &p, uint32_t max_big);
+void launch_big_reduce(hipStream_t s, const BigReduceParams &p, uint32_t nbig);
 
 struct PreprocessBwdParams {
     int P, D, M, W, H;
@@ -87,9 +87,9 @@ struct PreprocessBwdParams {
     const float *means3D, *opacities, *scales, *rotations, *cov3D_precomp, *shs;
     const float *view, *proj, *campos;
     const int *radii;
-    const uint32_t *tiles, *inst_start, *inv;
+    const uint32_t *tiles, *inst_start, *inv, *big_slot;
     const uint8_t *clamped;
-    const float *rows;
+    const float *rows, *bigsum;
     float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales, *dL_drot;
 };
 void launch_preprocess_bwd(hipStream_t s, const PreprocessBwdParams &p);

@@ -160,14 +160,12 @@ __global__ __launch_bounds__(256) void rs_hist_kernel(const uint32_t *__restrict
 // ------------------------------------------------------------------------------------------------
 // radix sort pass: stable scatter
 // ------------------------------------------------------------------------------------------------
-template <bool IOTA_IN, bool EPILOGUE>
+template <bool IOTA_IN>
 __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restrict__ keys_in,
                                                          const uint32_t *__restrict__ vals_in, uint32_t n,
                                                          int shift, const uint32_t *__restrict__ counts_scanned,
                                                          uint32_t nb, uint32_t *__restrict__ keys_out,
-                                                         uint32_t *__restrict__ vals_out,
-                                                         const uint32_t *__restrict__ gid_map,
-                                                         uint32_t *__restrict__ inv_out) {
+                                                         uint32_t *__restrict__ vals_out) {
     __shared__ uint32_t s_cnt[4][RS_BINS];  // per-wave running digit counts, then per-wave bases
     __shared__ uint32_t s_dstart[RS_BINS];  // block-local start of each digit's run
     __shared__ uint32_t s_gbase[RS_BINS];   // global start of this block's run of each digit
@@ -243,39 +241,23 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restr
         const uint32_t d = (k >> shift) & 255u;
         const uint32_t gpos = s_gbase[d] + (i - s_dstart[d]);
         keys_out[gpos] = k;
-        if (EPILOGUE) {
-            vals_out[gpos] = gid_map[v];
-            inv_out[v] = gpos;
-        } else {
-            vals_out[gpos] = v;
-        }
+        vals_out[gpos] = v;
     }
 }
 
-void launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, const uint32_t *gid_map,
-                       uint32_t *vals_final, uint32_t *inv) {
+void launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits) {
     if (n == 0) return;
     const uint32_t nb = div_up(n, RS_TILE);
     const int passes = radix_passes(nbits);
     for (int p = 0; p < passes; p++) {
         const int shift = 8 * p, in = p & 1, out = (p + 1) & 1;
-        const bool first = p == 0, last = p == passes - 1;
         rs_hist_kernel<<<nb, 256, 0, s>>>(sc.k[in], n, shift, sc.counts, nb);
         launch_exclusive_scan(s, sc.counts, nullptr, RS_BINS * nb, sc.counts, sc.scan_tmp, nullptr);
-        const bool epi = last && gid_map != nullptr;
-        uint32_t *vout = epi ? vals_final : sc.v[out];
-        if (first && epi)
-            rs_scatter_kernel<true, true><<<nb, 256, 0, s>>>(sc.k[in], nullptr, n, shift, sc.counts, nb, sc.k[out],
-                                                             vout, gid_map, inv);
-        else if (first)
-            rs_scatter_kernel<true, false><<<nb, 256, 0, s>>>(sc.k[in], nullptr, n, shift, sc.counts, nb,
-                                                              sc.k[out], vout, nullptr, nullptr);
-        else if (epi)
-            rs_scatter_kernel<false, true><<<nb, 256, 0, s>>>(sc.k[in], sc.v[in], n, shift, sc.counts, nb,
-                                                              sc.k[out], vout, gid_map, inv);
+        if (p == 0)
+            rs_scatter_kernel<true><<<nb, 256, 0, s>>>(sc.k[in], nullptr, n, shift, sc.counts, nb, sc.k[out], sc.v[out]);
         else
-            rs_scatter_kernel<false, false><<<nb, 256, 0, s>>>(sc.k[in], sc.v[in], n, shift, sc.counts, nb,
-                                                               sc.k[out], vout, nullptr, nullptr);
+            rs_scatter_kernel<false><<<nb, 256, 0, s>>>(sc.k[in], sc.v[in], n, shift, sc.counts, nb, sc.k[out],
+                                                        sc.v[out]);
     }
 }
 

@@ -101,6 +101,7 @@ class ForwardState(NamedTuple):
     binning_buffer: torch.Tensor
     image_buffer: torch.Tensor
     num_rendered: int
+    num_big: int
     M: int
 
 
@@ -145,7 +146,7 @@ def forward_raw(means3D, sh, colors_precomp, opacities, scales, rotations, cov3D
     _native.check(rc, "rasterize_gaussians")
     state = ForwardState(means3D_c, sh_c, col_c, op_c, sc_c, rot_c, cov_c, radii, bg, view, proj, campos,
                          bufs.get(_native.GSR_BUF_GEOM), bufs.get(_native.GSR_BUF_BINNING),
-                         bufs.get(_native.GSR_BUF_IMAGE), int(num_rendered.value), M)
+                         bufs.get(_native.GSR_BUF_IMAGE), int(num_rendered.value), int(a.num_big_out), M)
     return color, radii, invdepth, state
 
 
@@ -188,7 +189,7 @@ def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_
     drot = dst("rotations", P, 4)
     bufs = _Buffers(device)
     a = _native.BackwardArgs(
-        P=P, D=int(rs.sh_degree), M=M, W=W, H=H, R=st.num_rendered, background=_ptr(st.bg),
+        P=P, D=int(rs.sh_degree), M=M, W=W, H=H, R=st.num_rendered, num_big=st.num_big, background=_ptr(st.bg),
         means3D=_ptr(st.means3D), colors_precomp=_ptr(st.colors_precomp), opacities=_ptr(st.opacities),
         scales=_ptr(st.scales), scale_modifier=float(rs.scale_modifier), rotations=_ptr(st.rotations),
         cov3D_precomp=_ptr(st.cov3D_precomp), viewmatrix=_ptr(st.viewmatrix), projmatrix=_ptr(st.projmatrix),
@@ -218,7 +219,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         color, radii, invdepth, st = forward_raw(means3D, sh, colors_precomp, opacities, scales, rotations,
                                                  cov3Ds_precomp, raster_settings)
         ctx.raster_settings = raster_settings
-        ctx.meta = (st.num_rendered, st.M)
+        ctx.meta = (st.num_rendered, st.num_big, st.M)
         ctx.present = tuple(t is not None for t in st)
         empty = torch.empty(0, device=means3D.device)
         ctx.save_for_backward(*[(t if t is not None else empty) for t in st[:15]])

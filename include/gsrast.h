@@ -72,17 +72,19 @@ typedef struct gsr_forward_args {
     float *out_color;             /* (3,H,W) */
     float *out_invdepth;          /* (H,W) or NULL */
     int *radii;                   /* (P) */
+    int64_t num_big_out;          /* OUTPUT: Gaussians with > 64 instances (pass to gsr_backward) */
 } gsr_forward_args;
 
 /* Replaces `_C.rasterize_gaussians` (rasterize_points.cu RasterizeGaussiansCUDA -> Rasterizer::forward).
  * Runs preprocess, depth sort, scan, one device->host read of the instance count, tile expansion,
  * tile sort, range identification and compositing.  *num_rendered receives the instance count. */
-int gsr_forward(const gsr_forward_args *args, gsr_alloc_fn alloc, void *alloc_ctx, void *stream,
+int gsr_forward(gsr_forward_args *args, gsr_alloc_fn alloc, void *alloc_ctx, void *stream,
                 int64_t *num_rendered);
 
 typedef struct gsr_backward_args {
     int P, D, M, W, H;
     int64_t R;                    /* num_rendered returned by gsr_forward */
+    int64_t num_big;              /* num_big_out returned by gsr_forward */
     const float *background;
     const float *means3D;
     const float *colors_precomp;  /* or NULL */
@@ -122,7 +124,7 @@ int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const
 size_t gsr_geom_buffer_bytes(int P);
 size_t gsr_binning_buffer_bytes(int64_t R, int W, int H);
 size_t gsr_image_buffer_bytes(int W, int H);
-size_t gsr_bwd_scratch_bytes(int P, int64_t R);
+size_t gsr_bwd_scratch_bytes(int64_t R, int64_t num_big);
 
 /* Byte offsets of the internal arrays inside the three forward buffers (host arithmetic only).  Used by
  * the parity tests to compare the integer binning state (sorted instance list, tile ranges,
@@ -133,7 +135,9 @@ typedef struct gsr_state_layout {
     size_t geom_sorted_depth; /* u32 depth bits in depth-rank order (depth of order[r]) */
     size_t geom_tile_mask;    /* u64 kept-tile mask of the rect (exact culling), 0 = all tiles */
     size_t bin_point_list, bin_inv, bin_keys_sorted;                  /* u32 per instance */
+    size_t bin_sorted_u, bin_inst_gid;                                /* u32 per instance */
     size_t img_final_T, img_n_contrib, img_ranges, img_tile_last;     /* f32/u32 per pixel, uint2/u32 per tile */
+    size_t img_tile_loaded;                                           /* u32 per tile */
 } gsr_state_layout;
 void gsr_state_layout_query(int P, int64_t R, int W, int H, gsr_state_layout *out);
 

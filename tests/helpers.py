@@ -97,8 +97,15 @@ def hip_state_arrays(out: dict) -> dict:
         return buf[off: off + nbytes].view(dtype).cpu().numpy() if n else np.zeros(0)
 
     i32 = torch.int32
+    sorted_u = view(st.binning_buffer, lay["bin_sorted_u"], R, i32).astype(np.int64)
+    inst_gid = view(st.binning_buffer, lay["bin_inst_gid"], R, i32).astype(np.uint32)
     res = dict(
-        point_list=view(st.binning_buffer, lay["bin_point_list"], R, i32).astype(np.uint32),
+        point_list=inst_gid[sorted_u] if R else np.zeros(0, np.uint32),
+        point_list_written=view(st.binning_buffer, lay["bin_point_list"], R, i32).astype(np.uint32),
+        inv=view(st.binning_buffer, lay["bin_inv"], R, i32).astype(np.uint32),
+        sorted_u=sorted_u.astype(np.uint32),
+        tile_loaded=view(st.image_buffer, lay["img_tile_loaded"], T, i32).astype(np.uint32),
+        tile_last=view(st.image_buffer, lay["img_tile_last"], T, i32).astype(np.uint32),
         ranges=view(st.image_buffer, lay["img_ranges"], 2 * T, i32).astype(np.uint32).reshape(T, 2),
         n_contrib=view(st.image_buffer, lay["img_n_contrib"], W * H, i32).astype(np.uint32).reshape(H, W),
         final_T=view(st.image_buffer, lay["img_final_T"], W * H, torch.float32).reshape(H, W),

@@ -37,6 +37,16 @@ def compare_forward(inp, hip, oracle_out):
     assert np.array_equal(hs["point_list"], pl)
     assert np.array_equal(hs["ranges"], rg)
     assert np.array_equal(hs["tiles"], tt)
+    # The forward gathers every instance any pixel can reach; for exactly those it writes the sorted id
+    # list and the inverse permutation (sorted position of each expansion index); others keep INV_NONE.
+    loaded = np.zeros(len(pl), bool)
+    for t in np.nonzero(hs["tile_loaded"])[0]:
+        loaded[rg[t, 0]: rg[t, 0] + hs["tile_loaded"][t]] = True
+    assert np.all(hs["tile_loaded"] >= hs["tile_last"])
+    assert np.array_equal(hs["point_list_written"][loaded], pl[loaded])
+    s_idx = np.nonzero(loaded)[0]
+    assert np.array_equal(hs["inv"][hs["sorted_u"][s_idx]], s_idx.astype(np.uint32))
+    assert np.sum(hs["inv"] != 0xFFFFFFFF) == loaded.sum()
     assert abs(hs["num_rendered"] - run.num_rendered) <= 1e-4 * run.num_rendered + 2
     ft, nc = run.image_state()
     assert np.mean(hs["n_contrib"] == nc) >= 0.999
