@@ -215,36 +215,57 @@ __device__ __forceinline__ void get_rect(float2 p, int radius, int gx, int gy, i
 // evaluation of q at any pixel is within eps*q of the exact value, eps = 1e-5 (|a|+|b|+|c|) / lambda_min
 // (>= 25x the worst-case rounding of the 6-op power expression), and fast_exp is within 1e-5 relative.
 constexpr int CULL_MAX_AREA = 64;
-__host__ __device__ inline bool tile_has_contribution(double x, double y, double a, double b, double c, double o,
-                                                      int tx, int ty, int W, int H) {
-    if (!(o * 255.0 * (1.0 + 1e-5) >= 1.0)) return false;  // o*G <= o < 1/255 everywhere
+struct CullGauss {
+    double x, y, a, b, c, inv_a, inv_c, thr;
+    int mode;  // 0: test each tile, 1: keep every tile, 2: drop every tile
+};
+// Per-Gaussian part of the test (once per Gaussian): the error-adjusted threshold on q_min.
+__host__ __device__ inline CullGauss cull_setup(double x, double y, double a, double b, double c, double o) {
+    CullGauss g{x, y, a, b, c, 0.0, 0.0, 0.0, 0};
+    if (!(o * 255.0 * (1.0 + 1e-5) >= 1.0)) {  // o*G <= o < 1/255 everywhere
+        g.mode = 2;
+        return g;
+    }
+    const double tr = 0.5 * (a + c), df = 0.5 * (a - c);
+    const double lmin = tr - sqrt(df * df + b * b);
+    if (!(lmin > 0.0) || !(a > 0.0) || !(c > 0.0)) {
+        g.mode = 1;
+        return g;
+    }
+    const double eps = 1e-5 * (fabs(a) + fabs(b) + fabs(c)) / lmin;
+    if (eps > 0.1) {
+        g.mode = 1;
+        return g;
+    }
+    g.inv_a = 1.0 / a;
+    g.inv_c = 1.0 / c;
+    // cull iff q_min (1 - eps) - 1e-6 > 2 ln(255 o (1 + 1e-5))
+    g.thr = (2.0 * log(255.0 * o * (1.0 + 1e-5)) + 1e-6) / (1.0 - eps);
+    return g;
+}
+// Per-tile part: exact minimum of the quadratic form over the tile's pixel rectangle (4 edges).
+__host__ __device__ inline bool cull_keep(const CullGauss &g, int tx, int ty, int W, int H) {
+    if (g.mode == 2) return false;
+    if (g.mode == 1) return true;
     const double lx = tx * BLOCK_X, ly = ty * BLOCK_Y;
     const double hx = fmin((double)(tx * BLOCK_X + BLOCK_X - 1), (double)(W - 1));
     const double hy = fmin((double)(ty * BLOCK_Y + BLOCK_Y - 1), (double)(H - 1));
-    if (x >= lx && x <= hx && y >= ly && y <= hy) return true;
-    const double tr = 0.5 * (a + c), df = 0.5 * (a - c);
-    const double lmin = tr - sqrt(df * df + b * b);
-    if (!(lmin > 0.0) || !(a > 0.0) || !(c > 0.0)) return true;
-    const double eps = 1e-5 * (fabs(a) + fabs(b) + fabs(c)) / lmin;
-    if (eps > 0.1) return true;
+    if (g.x >= lx && g.x <= hx && g.y >= ly && g.y <= hy) return true;
     double qmin = 1e300;
     const double xs[2] = {lx, hx}, ys[2] = {ly, hy};
-    for (int e = 0; e < 2; e++) {  // vertical edges x = X
-        const double dx = x - xs[e];
-        double py = y + b * dx / c;
-        py = fmin(fmax(py, ly), hy);
-        const double dy = y - py;
-        qmin = fmin(qmin, a * dx * dx + 2.0 * b * dx * dy + c * dy * dy);
+    for (int e = 0; e < 2; e++) {  // vertical edges x = X: minimise over y
+        const double dx = g.x - xs[e];
+        const double py = fmin(fmax(g.y + g.b * dx * g.inv_c, ly), hy);
+        const double dy = g.y - py;
+        qmin = fmin(qmin, g.a * dx * dx + 2.0 * g.b * dx * dy + g.c * dy * dy);
     }
-    for (int e = 0; e < 2; e++) {  // horizontal edges y = Y
-        const double dy = y - ys[e];
-        double px = x + b * dy / a;
-        px = fmin(fmax(px, lx), hx);
-        const double dx = x - px;
-        qmin = fmin(qmin, a * dx * dx + 2.0 * b * dx * dy + c * dy * dy);
+    for (int e = 0; e < 2; e++) {  // horizontal edges y = Y: minimise over x
+        const double dy = g.y - ys[e];
+        const double px = fmin(fmax(g.x + g.b * dy * g.inv_a, lx), hx);
+        const double dx = g.x - px;
+        qmin = fmin(qmin, g.a * dx * dx + 2.0 * g.b * dx * dy + g.c * dy * dy);
     }
-    const double qlo = qmin * (1.0 - eps) - 1e-6;
-    return !(qlo > 2.0 * log(255.0 * o * (1.0 + 1e-5)));
+    return !(qmin > g.thr);
 }
 
 // SH basis constants (utils/sh.py:7-28 of the reference)

@@ -90,10 +90,11 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessParams p) {
     uint32_t kept = area;
     if (p.cull && area <= (uint32_t)CULL_MAX_AREA) {
         const int w = rmax.x - rmin.x;
+        const CullGauss cg = cull_setup(pimg.x, pimg.y, conic_x, conic_y, conic_z, opacity);
         kept = 0;
         for (int ty = rmin.y; ty < rmax.y; ty++)
             for (int tx = rmin.x; tx < rmax.x; tx++)
-                if (tile_has_contribution(pimg.x, pimg.y, conic_x, conic_y, conic_z, opacity, tx, ty, p.W, p.H)) {
+                if (cull_keep(cg, tx, ty, p.W, p.H)) {
                     mask |= 1ull << ((ty - rmin.y) * w + (tx - rmin.x));
                     kept++;
                 }
