@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stage-events", action="store_true", help="time without per-stage hipEvents")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"))
+    ap.add_argument("--exchange", default="compact", choices=("compact", "dense"),
+                    help="N>1 gradient exchange (gaussian_splatting_lightning_amd/multiview.py)")
     return ap.parse_args()
 
 
@@ -69,6 +72,7 @@ def main():
 
     from gaussian_splatting_lightning_amd import _native
     from gaussian_splatting_lightning_amd.rasterizer import GaussianRasterizationSettings, backward_raw, forward_raw
+    from gaussian_splatting_lightning_amd.multiview import ViewGradReducer
     from gaussian_splatting_lightning_amd.synthetic import make_camera, make_scene, make_upstream
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -76,10 +80,13 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    dev = torch.device("cuda", local_rank)
+    dev = torch.device("cuda", local_rank % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:  # rehearsal of the N>1 path on fewer GPUs than ranks (RCCL needs one GPU per rank)
+            dist.init_process_group(args.dist_backend)
     cfg = CONFIGS[args.config]
     n, W, H, deg = cfg["n"], cfg["W"], cfg["H"], cfg["deg"]
     num_views = max(world, 8) if args.config == "cfg3" else max(world, 1)
@@ -97,33 +104,17 @@ def main():
         sh_degree=deg, campos=c.campos, prefiltered=False, debug=False, antialiasing=False)
     M = sc.shs.shape[1]
 
-    # Flat per-Gaussian reduction buffer: means3D 3 | scales 3 | rotations 4 | opacity 1 | shs 3M |
-    # densification stats 2 (|dL/dmeans2D[:, :2]| and the visibility count, gaussian_model.py:175-181).
-    widths = dict(means3D=3, scales=3, rotations=4, opacities=1, shs=3 * M, stats=2)
-    cols = sum(widths.values())
-    # column-block layout [field][Gaussian][width] so every destination view is contiguous
-    flat = torch.zeros(cols * n, dtype=torch.float32, device=dev)
-    views, off = {}, 0
-    for k, wdt in widths.items():
-        views[k] = flat[off * n:(off + wdt) * n].view(n, wdt)
-        off += wdt
-    out = dict(means3D=views["means3D"], scales=views["scales"], rotations=views["rotations"],
-               opacities=views["opacities"], shs=views["shs"].view(n, M, 3))
-    dmeans2D = torch.empty(n, 3, dtype=torch.float32, device=dev)
-    out["means2D"] = dmeans2D
-    radii_max = torch.empty(n, dtype=torch.int32, device=dev)
+    # Per-Gaussian gradient destinations + the cross-rank exchange (multiview.py): one view per rank; dense
+    # all-reduce at N=1 (nothing to exchange), compact SH exchange at N>1 unless --exchange dense.
+    mode = args.exchange if world > 1 else "dense"
+    red = ViewGradReducer(n, M, deg, dev, mode=mode)
 
     def step():
         color, radii, invd, st = forward_raw(sc.means3D, sc.shs, None, sc.opacities, sc.scales, sc.rotations, None,
                                              settings)
-        backward_raw(st, settings, dcolor, dinv, out=out)
-        stats = views["stats"]
-        torch.linalg.vector_norm(dmeans2D[:, :2], dim=1, out=stats[:, 0])
-        stats[:, 1].copy_(radii > 0)
-        radii_max.copy_(radii)
-        if world > 1:
-            dist.all_reduce(flat)
-            dist.all_reduce(radii_max, op=dist.ReduceOp.MAX)
+        backward_raw(st, settings, dcolor, dinv, out=red.backward_out(), compact_sh=red.compact)
+        red.record_view(red.means2D, radii)
+        red.reduce(sc.means3D, c.campos)
         return st
 
     # ---- warmup ----
@@ -223,7 +214,7 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": cfg["desc"], "gaussians": n, "width": W, "height": H, "sh_degree": deg,
-                   "views_per_step": world, "parallelism": f"dp{world} (one view per GPU, RCCL all-reduce)",
+                   "views_per_step": world, "parallelism": f"dp{world} (one view per GPU, RCCL gradient exchange: {mode})",
                    "instances_per_view": I, "sum_n_contrib": sum_contrib,
                    "stage_events": use_events},
         "roofline": roofline, "cpu_baseline": cpu,

@@ -39,6 +39,7 @@ class BackwardArgs(ctypes.Structure):
         ("antialiasing", ctypes.c_int), ("debug", ctypes.c_int), ("dL_dmeans2D", _fp), ("dL_dcolors", _fp),
         ("dL_dopacity", _fp), ("dL_dmeans3D", _fp), ("dL_dcov3D", _fp), ("dL_dsh", _fp), ("dL_dscales", _fp),
         ("dL_drotations", _fp),
+        ("dL_dcolors_sh", _fp),
     ]
 
 
@@ -52,7 +53,7 @@ class StateLayout(ctypes.Structure):
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t)
 
 EXPORTED_SYMBOLS = (
-    "gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes",
+    "gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_sh_backward_views", "gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes",
     "gsr_image_buffer_bytes", "gsr_bwd_scratch_bytes", "gsr_set_profiling", "gsr_num_stages", "gsr_stage_name",
     "gsr_stage_times", "gsr_reset_stage_times", "gsr_last_error", "gsr_build_info", "gsr_state_layout_query",
     "gsr_set_tuning",
@@ -79,6 +80,9 @@ def load(path: str | None = None):
     lib.gsr_backward.restype = ctypes.c_int
     lib.gsr_mark_visible.argtypes = [ctypes.c_int, _fp, _fp, _fp, _fp, ctypes.c_void_p]
     lib.gsr_mark_visible.restype = ctypes.c_int
+    lib.gsr_sh_backward_views.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _fp, _fp, _fp, _fp,
+                                          ctypes.c_void_p]
+    lib.gsr_sh_backward_views.restype = ctypes.c_int
     lib.gsr_geom_buffer_bytes.argtypes = [ctypes.c_int]
     lib.gsr_geom_buffer_bytes.restype = ctypes.c_size_t
     lib.gsr_binning_buffer_bytes.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int]

@@ -62,11 +62,12 @@ enum Stage {
     ST_RENDER_BWD,
     ST_BIG_REDUCE,
     ST_PREPROCESS_BWD,
+    ST_SH_VIEWS,
     ST_COUNT
 };
 const char *kStageNames[ST_COUNT] = {"preprocess", "depth_sort", "instance_scan", "readback",
                                      "expand",     "tile_sort",  "tile_ranges",   "render_fwd",
-                                     "render_bwd", "big_reduce", "preprocess_bwd"};
+                                     "render_bwd", "big_reduce", "preprocess_bwd", "sh_views"};
 
 struct Profiler {
     std::mutex mu;
@@ -339,7 +340,8 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     if (!a->dL_dpix || !a->radii) return fail(GSR_ERR_ARG, "dL_dpix and radii are required");
     if (!a->geom_buffer || !a->image_buffer || (a->R > 0 && !a->binning_buffer))
         return fail(GSR_ERR_ARG, "forward buffers are required");
-    if (a->shs && a->M > 0 && !a->dL_dsh) return fail(GSR_ERR_ARG, "dL_dsh is required when shs are given");
+    if (a->shs && a->M > 0 && !a->dL_dsh && !a->dL_dcolors_sh)
+        return fail(GSR_ERR_ARG, "dL_dsh (or dL_dcolors_sh) is required when shs are given");
     if (a->R < 0 || a->R > 0xffffffffLL) return fail(GSR_ERR_ARG, "bad num_rendered");
     hipStream_t stream = (hipStream_t)stream_ptr;
     const bool dbg = a->debug != 0;
@@ -389,14 +391,30 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     pp.radii = a->radii; pp.tiles = g.tiles; pp.inst_start = g.inst_start; pp.inv = b.inv; pp.clamped = g.clamped;
     pp.big_slot = g.big_slot; pp.bigsum = bigsum;
     pp.rows = rows;
-    pp.sh_vec16 = pp.shs && a->M == 16 && a->dL_dsh && (((uintptr_t)pp.shs | (uintptr_t)a->dL_dsh) & 15) == 0 &&
+    pp.sh_vec16 = pp.shs && a->M == 16 && (((uintptr_t)pp.shs | (uintptr_t)a->dL_dsh) & 15) == 0 &&
                   tuning("sh_vec16", 1);
     pp.dL_dmeans2D = a->dL_dmeans2D; pp.dL_dcolors = a->dL_dcolors; pp.dL_dopacity = a->dL_dopacity;
     pp.dL_dmeans3D = a->dL_dmeans3D; pp.dL_dcov3D = a->dL_dcov3D; pp.dL_dsh = a->dL_dsh;
+    pp.dL_dcolors_sh = a->dL_dcolors_sh;
     pp.dL_dscales = a->dL_dscales; pp.dL_drot = a->dL_drotations;
     if (pp.shs == nullptr && a->dL_dsh && a->M > 0)
         GSR_HIP(hipMemsetAsync(a->dL_dsh, 0, sizeof(float) * (size_t)P * a->M * 3, stream));
+    if (pp.shs == nullptr && a->dL_dcolors_sh)
+        GSR_HIP(hipMemsetAsync(a->dL_dcolors_sh, 0, sizeof(float) * (size_t)P * 3, stream));
     GSR_STAGE(ST_PREPROCESS_BWD, dbg, launch_preprocess_bwd(stream, pp));
+    return GSR_OK;
+}
+
+int gsr_sh_backward_views(int P, int D, int M, int V, const float *means3D, const float *campos,
+                          const float *dL_dcolors_sh, float *dL_dsh, void *stream_ptr) {
+    if (P < 0 || V < 0) return fail(GSR_ERR_ARG, "P and V must be >= 0");
+    if (D < 0 || D > 3) return fail(GSR_ERR_ARG, "sh_degree must be in [0, 3]");
+    if (M <= 0 || M > 16 || (D + 1) * (D + 1) > M)
+        return fail(GSR_ERR_ARG, "M must hold (deg+1)^2 <= M <= 16 coefficients");
+    if (P == 0) return GSR_OK;
+    if (!means3D || !dL_dsh || (V > 0 && (!campos || !dL_dcolors_sh))) return fail(GSR_ERR_ARG, "null argument");
+    hipStream_t stream = (hipStream_t)stream_ptr;
+    GSR_STAGE(ST_SH_VIEWS, 0, launch_sh_backward_views(stream, P, D, M, V, means3D, campos, dL_dcolors_sh, dL_dsh));
     return GSR_OK;
 }
 

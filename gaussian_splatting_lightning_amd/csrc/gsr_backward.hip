@@ -340,6 +340,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
             for (int k = 0; k < 6; k++) p.dL_dcov3D[6 * i + k] = 0.f;
         if (p.dL_dsh)
             for (int k = 0; k < ncoef; k++) p.dL_dsh[(size_t)i * ncoef + k] = 0.f;
+        if (p.dL_dcolors_sh) { p.dL_dcolors_sh[3 * i] = 0.f; p.dL_dcolors_sh[3 * i + 1] = 0.f; p.dL_dcolors_sh[3 * i + 2] = 0.f; }
         if (p.dL_dscales) { p.dL_dscales[3 * i] = 0.f; p.dL_dscales[3 * i + 1] = 0.f; p.dL_dscales[3 * i + 2] = 0.f; }
         if (p.dL_drot)
             for (int k = 0; k < 4; k++) p.dL_drot[4 * i + k] = 0.f;
@@ -447,7 +448,12 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         const uint8_t cl = p.clamped[i];
         const float3 dRGB = make_float3((cl & 1) ? 0.f : gs[6], (cl & 2) ? 0.f : gs[7], (cl & 4) ? 0.f : gs[8]);
         const float3 campos = make_float3(p.campos[0], p.campos[1], p.campos[2]);
-        float *dsh = p.dL_dsh + (size_t)i * ncoef;  // required whenever shs is given (checked by the API)
+        if (p.dL_dcolors_sh) {
+            p.dL_dcolors_sh[3 * i] = dRGB.x;
+            p.dL_dcolors_sh[3 * i + 1] = dRGB.y;
+            p.dL_dcolors_sh[3 * i + 2] = dRGB.z;
+        }
+        float *dsh = p.dL_dsh ? p.dL_dsh + (size_t)i * ncoef : nullptr;  // null only with dL_dcolors_sh (API)
         const float *shp = p.shs + (size_t)i * ncoef;
         if (p.sh_vec16) {
             // 16 coefficients x 3 = 192 B per Gaussian: 12 float4 loads and stores per lane
@@ -461,13 +467,19 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
 #pragma unroll
             for (int k = 0; k < 48; k++) dshv[k] = 0.f;
             dm = dm + sh_backward_dispatch(p.D, shv, mean - campos, dRGB, dshv);
-            float4 *d4 = reinterpret_cast<float4 *>(dsh);
+            if (dsh) {
+                float4 *d4 = reinterpret_cast<float4 *>(dsh);
 #pragma unroll
-            for (int k = 0; k < 12; k++) d4[k] = make_float4(dshv[4 * k], dshv[4 * k + 1], dshv[4 * k + 2], dshv[4 * k + 3]);
-        } else {
+                for (int k = 0; k < 12; k++)
+                    d4[k] = make_float4(dshv[4 * k], dshv[4 * k + 1], dshv[4 * k + 2], dshv[4 * k + 3]);
+            }
+        } else if (dsh) {
             dm = dm + sh_backward_dispatch(p.D, shp, mean - campos, dRGB, dsh);
             const int used = (p.D + 1) * (p.D + 1) * 3;
             for (int k = used; k < ncoef; k++) dsh[k] = 0.f;
+        } else {
+            float dtmp[48];  // dL/dsh discarded (compact multi-view mode); only the direction term is kept
+            dm = dm + sh_backward_dispatch(p.D, shp, mean - campos, dRGB, dtmp);
         }
     }
     if (p.dL_dmeans3D) {

@@ -91,7 +91,12 @@ struct PreprocessBwdParams {
     const uint8_t *clamped;
     const float *rows, *bigsum;
     float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales, *dL_drot;
+    float *dL_dcolors_sh;  // clamp-masked colour gradient (may be null)
 };
 void launch_preprocess_bwd(hipStream_t s, const PreprocessBwdParams &p);
+
+// ---- multi-view SH gradient (gsr_views.hip) ----
+void launch_sh_backward_views(hipStream_t s, int P, int D, int M, int V, const float *means3D, const float *campos,
+                              const float *dcolors_sh, float *dsh);
 
 }  // namespace gsr

@@ -112,6 +112,34 @@ __device__ __forceinline__ float3 sh_backward(const float *__restrict__ sh, floa
     return dnormvdv(dir_orig, dL_ddir);
 }
 
+// SH basis values b[0..(DEG+1)^2) at unit direction (x,y,z); b[k] * dRGB is sh_backward's dL/dsh[k].
+template <int DEG>
+__device__ __forceinline__ void sh_basis(float x, float y, float z, float *b) {
+    b[0] = GSR_SH_C0;
+    if (DEG > 0) {
+        b[1] = -GSR_SH_C1 * y;
+        b[2] = GSR_SH_C1 * z;
+        b[3] = -GSR_SH_C1 * x;
+        if (DEG > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+            b[4] = SH_C2[0] * xy;
+            b[5] = SH_C2[1] * yz;
+            b[6] = SH_C2[2] * (2.f * zz - xx - yy);
+            b[7] = SH_C2[3] * xz;
+            b[8] = SH_C2[4] * (xx - yy);
+            if (DEG > 2) {
+                b[9] = SH_C3[0] * y * (3.f * xx - yy);
+                b[10] = SH_C3[1] * xy * z;
+                b[11] = SH_C3[2] * y * (4.f * zz - xx - yy);
+                b[12] = SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy);
+                b[13] = SH_C3[4] * x * (4.f * zz - xx - yy);
+                b[14] = SH_C3[5] * z * (xx - yy);
+                b[15] = SH_C3[6] * x * (xx - 3.f * yy);
+            }
+        }
+    }
+}
+
 __device__ __forceinline__ float3 sh_backward_dispatch(int deg, const float *__restrict__ sh, float3 dir_orig,
                                                        float3 dRGB, float *__restrict__ dsh) {
     switch (deg) {

@@ -1,0 +1,67 @@
+// gsr_views.hip -- multi-view SH gradient from compact per-view colour-gradient factors.
+//
+// Data-parallel training renders one view per GPU.  The SH coefficient gradient of view v is rank one per
+// Gaussian: dL/dsh_v[g] = basis(dir_v(g)) (x) dRGB_v[g] (computeColorFromSH backward of the CUDA submodule),
+// so instead of all-reducing (P, 16, 3) floats, ranks all-gather the (P, 3) factors dRGB_v and every rank
+// expands the sum over views here.  One thread per Gaussian; the per-view camera positions are wave-uniform
+// (scalar loads); 48 accumulators stay in VGPRs; the 192-B output row is written with float4 stores.
+#include "gsr_kernels.h"
+#include "gsr_sh.h"
+
+namespace gsr {
+
+template <int DEG>
+__global__ __launch_bounds__(256) void sh_backward_views_kernel(int P, int M, int V, const float *__restrict__ means3D,
+                                                                const float *__restrict__ campos,
+                                                                const float *__restrict__ dc,
+                                                                float *__restrict__ dsh) {
+    constexpr int NB = (DEG + 1) * (DEG + 1);
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const float mx = means3D[3 * i], my = means3D[3 * i + 1], mz = means3D[3 * i + 2];
+    float acc[3 * NB];
+#pragma unroll
+    for (int k = 0; k < 3 * NB; k++) acc[k] = 0.f;
+    for (int v = 0; v < V; v++) {
+        const float *d = dc + ((size_t)v * P + i) * 3;
+        const float r = d[0], g = d[1], b = d[2];
+        if (r == 0.f && g == 0.f && b == 0.f) continue;  // not rendered (or fully clamped) in view v
+        const float dx = mx - campos[3 * v], dy = my - campos[3 * v + 1], dz = mz - campos[3 * v + 2];
+        const float len = sqrtf(dx * dx + dy * dy + dz * dz);
+        float basis[16];
+        sh_basis<DEG>(dx / len, dy / len, dz / len, basis);
+#pragma unroll
+        for (int k = 0; k < NB; k++) {
+            acc[3 * k] += basis[k] * r;
+            acc[3 * k + 1] += basis[k] * g;
+            acc[3 * k + 2] += basis[k] * b;
+        }
+    }
+    float *o = dsh + (size_t)i * M * 3;
+    if (M == 16 && (((uintptr_t)dsh) & 15) == 0) {
+        float row[48];
+#pragma unroll
+        for (int k = 0; k < 48; k++) row[k] = k < 3 * NB ? acc[k < 3 * NB ? k : 0] : 0.f;
+        float4 *o4 = reinterpret_cast<float4 *>(o);
+#pragma unroll
+        for (int k = 0; k < 12; k++) o4[k] = make_float4(row[4 * k], row[4 * k + 1], row[4 * k + 2], row[4 * k + 3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3 * NB; k++) o[k] = acc[k];
+        for (int k = 3 * NB; k < 3 * M; k++) o[k] = 0.f;
+    }
+}
+
+void launch_sh_backward_views(hipStream_t s, int P, int D, int M, int V, const float *means3D, const float *campos,
+                              const float *dcolors_sh, float *dsh) {
+    if (P <= 0) return;
+    const dim3 grid(div_up(P, 256)), block(256);
+    switch (D) {
+        case 0: sh_backward_views_kernel<0><<<grid, block, 0, s>>>(P, M, V, means3D, campos, dcolors_sh, dsh); break;
+        case 1: sh_backward_views_kernel<1><<<grid, block, 0, s>>>(P, M, V, means3D, campos, dcolors_sh, dsh); break;
+        case 2: sh_backward_views_kernel<2><<<grid, block, 0, s>>>(P, M, V, means3D, campos, dcolors_sh, dsh); break;
+        default: sh_backward_views_kernel<3><<<grid, block, 0, s>>>(P, M, V, means3D, campos, dcolors_sh, dsh); break;
+    }
+}
+
+}  // namespace gsr

@@ -150,12 +150,15 @@ def forward_raw(means3D, sh, colors_precomp, opacities, scales, rotations, cov3D
     return color, radii, invdepth, state
 
 
-def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_depth=None, out=None):
+def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_depth=None, out=None,
+                 compact_sh=False):
     """One call of gsr_backward.  Returns a dict of gradients (means3D, means2D, shs, colors_precomp,
     opacities, scales, rotations, cov3D_precomp); entries are None where the input was absent.
     `out` may supply preallocated contiguous float32 destinations (e.g. views into one flat buffer that is
     then all-reduced): keys means2D (P,3), colors (P,3), opacities (P,1), means3D (P,3), cov3D (P,6),
-    shs (P,M,3), scales (P,3), rotations (P,4)."""
+    shs (P,M,3), scales (P,3), rotations (P,4), colors_sh (P,3).
+    compact_sh=True skips dL/dshs and returns the clamp-masked colour gradient "colors_sh" instead -- the
+    per-view factor that `sh_backward_views` expands after an all-gather (multiview.py)."""
     lib = _native.load()
     rs = raster_settings
     st = state
@@ -184,7 +187,8 @@ def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_
     dopac = dst("opacities", P, 1)
     dmeans3D = dst("means3D", P, 3)
     dcov = dst("cov3D", P, 6)
-    dsh = dst("shs", P, max(M, 0), 3)
+    dsh = None if compact_sh else dst("shs", P, max(M, 0), 3)
+    dcsh = dst("colors_sh", P, 3) if (compact_sh or "colors_sh" in out) else None
     dscales = dst("scales", P, 3)
     drot = dst("rotations", P, 4)
     bufs = _Buffers(device)
@@ -199,12 +203,12 @@ def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_
         image_buffer=_ptr(st.image_buffer), antialiasing=int(bool(rs.antialiasing)), debug=int(bool(rs.debug)),
         dL_dmeans2D=dmeans2D.data_ptr(), dL_dcolors=dcolors.data_ptr(), dL_dopacity=dopac.data_ptr(),
         dL_dmeans3D=dmeans3D.data_ptr(), dL_dcov3D=dcov.data_ptr(), dL_dsh=_ptr(dsh),
-        dL_dscales=dscales.data_ptr(), dL_drotations=drot.data_ptr())
+        dL_dscales=dscales.data_ptr(), dL_drotations=drot.data_ptr(), dL_dcolors_sh=_ptr(dcsh))
     rc = lib.gsr_backward(ctypes.byref(a), bufs.callback, None, _stream_handle(device))
     _native.check(rc, "rasterize_gaussians_backward")
     return dict(
         means3D=dmeans3D, means2D=dmeans2D,
-        shs=dsh.view_as(st.shs) if st.shs is not None else None,
+        shs=dsh.view_as(st.shs) if (st.shs is not None and dsh is not None) else None, colors_sh=dcsh,
         colors_precomp=dcolors if st.colors_precomp is not None else None,
         colors=dcolors, opacities=dopac.view_as(st.opacities),
         scales=dscales if st.scales is not None else None,
@@ -248,6 +252,28 @@ def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales,
                         raster_settings):
     return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
                                      cov3Ds_precomp, raster_settings)
+
+
+def sh_backward_views(means3D: torch.Tensor, campos: torch.Tensor, dcolors_sh: torch.Tensor, sh_degree: int, M: int,
+                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dL/dshs (P,M,3) summed over V views from the compact per-view factors: campos (V,3) and the clamp-masked
+    colour gradients dcolors_sh (V,P,3) that backward_raw(..., compact_sh=True) returns (gsr_sh_backward_views)."""
+    lib = _native.load()
+    device = means3D.device
+    m = _prep(means3D, device, "means3D")
+    c = _prep(campos, device, "campos").reshape(-1, 3)
+    d = _prep(dcolors_sh, device, "dcolors_sh")
+    P, V = m.shape[0], c.shape[0]
+    if tuple(d.shape) != (V, P, 3):
+        raise RuntimeError(f"dcolors_sh must have shape {(V, P, 3)}, got {tuple(d.shape)}")
+    if out is None:
+        out = torch.empty(P, M, 3, dtype=torch.float32, device=device)
+    elif tuple(out.shape) != (P, M, 3) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise RuntimeError(f"out must be a contiguous float32 tensor of shape {(P, M, 3)}")
+    rc = lib.gsr_sh_backward_views(P, int(sh_degree), int(M), V, _ptr(m), _ptr(c), _ptr(d), out.data_ptr(),
+                                   _stream_handle(device))
+    _native.check(rc, "sh_backward_views")
+    return out
 
 
 def mark_visible(positions: torch.Tensor, viewmatrix: torch.Tensor, projmatrix: torch.Tensor) -> torch.Tensor:

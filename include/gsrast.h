@@ -107,14 +107,26 @@ typedef struct gsr_backward_args {
     float *dL_dopacity;           /* (P) */
     float *dL_dmeans3D;           /* (P,3) */
     float *dL_dcov3D;             /* (P,6) */
-    float *dL_dsh;                /* (P,M,3) */
+    float *dL_dsh;                /* (P,M,3); may be NULL only when dL_dcolors_sh is given */
     float *dL_dscales;            /* (P,3) */
     float *dL_drotations;         /* (P,4) */
+    /* (P,3) colour gradient with computeColorFromSH's clamp mask applied, i.e. the factor that multiplies
+     * the SH basis in dL/dsh.  With dL_dsh == NULL this is the compact per-view SH gradient that
+     * gsr_sh_backward_views expands (multi-view data parallelism); NULL to skip. */
+    float *dL_dcolors_sh;
 } gsr_backward_args;
 
 /* Replaces `_C.rasterize_gaussians_backward` (RasterizeGaussiansBackwardCUDA -> Rasterizer::backward).
  * Deterministic: per-tile gradient rows are reduced in fixed order (no float atomics). */
 int gsr_backward(const gsr_backward_args *args, gsr_alloc_fn alloc, void *alloc_ctx, void *stream);
+
+/* Multi-view SH gradient from compact per-view factors (no counterpart in the reference, whose batch size is
+ * one view: gs_lightning_module.py:139-141).  dL_dsh[g] = sum_v basis(normalize(means3D[g] - campos[v]))
+ * (x) dL_dcolors_sh[v][g], i.e. the sum over views of gsr_backward's dL_dsh -- what an all-reduce of dL_dsh
+ * computes, from 12 B per Gaussian per view instead of 12*M B.  campos (V,3), dL_dcolors_sh (V,P,3),
+ * dL_dsh (P,M,3) fully written (coefficients above the active degree are zero).  Device pointers. */
+int gsr_sh_backward_views(int P, int D, int M, int V, const float *means3D, const float *campos,
+                          const float *dL_dcolors_sh, float *dL_dsh, void *stream);
 
 /* Replaces `_C.mark_visible` (checkFrustum): present[i] = z_view(means3D[i]) > 0.2. */
 int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,

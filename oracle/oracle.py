@@ -55,6 +55,8 @@ def _load():
     lib.oracle_bin_count.restype = ctypes.c_longlong
     lib.oracle_bin_count.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f, _i, _f, ctypes.c_int]
     lib.oracle_bin.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f, _i, _f, _f, ctypes.c_int, _u32, _u32, _u32]
+    lib.oracle_get_clamped.argtypes = [ctypes.c_void_p, _u8]
+    lib.oracle_sh_backward_views.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f, _f, _f, _f]
     _lib = lib
     return lib
 
@@ -82,6 +84,18 @@ def mark_visible(means3D, viewmatrix, projmatrix) -> np.ndarray:
     out = np.zeros(m.shape[0], dtype=np.uint8)
     lib.oracle_mark_visible(m.shape[0], _fp(m), _fp(v), _fp(p), out.ctypes.data_as(_u8))
     return out.astype(bool)
+
+
+def sh_backward_views(means3D, campos, dcolors_sh, sh_degree, M) -> np.ndarray:
+    """sum over views v of the SH gradient for clamp-masked colour gradients dcolors_sh (V,P,3) seen from campos
+    (V,3) -> (P,M,3)."""
+    lib = _load()
+    m = _c32(means3D).reshape(-1, 3)
+    c = _c32(campos).reshape(-1, 3)
+    d = _c32(dcolors_sh).reshape(c.shape[0], m.shape[0], 3)
+    out = np.zeros((m.shape[0], M, 3), np.float32)
+    lib.oracle_sh_backward_views(m.shape[0], int(sh_degree), int(M), c.shape[0], _fp(m), _fp(c), _fp(d), _fp(out))
+    return out
 
 
 def bin_instances(xy, radii, depths, conic_opacity, image_width, image_height, cull=True):
@@ -148,6 +162,11 @@ class OracleRun:
         tt = np.zeros(P, np.uint32)
         self._lib.oracle_get_geom(self._h, _fp(d), _fp(xy), _fp(co), _fp(rgb), tt.ctypes.data_as(_u32))
         return dict(depths=d, xy=xy, conic_opacity=co, rgb=rgb, tiles_touched=tt)
+
+    def clamped(self) -> np.ndarray:
+        out = np.zeros((self.P, 3), np.uint8)
+        self._lib.oracle_get_clamped(self._h, out.ctypes.data_as(_u8))
+        return out
 
     def backward(self, dL_dcolor, dL_dinvdepth=None):
         P, M = self.P, self.M

@@ -1,0 +1,62 @@
+"""World-size-N worker for tests/test_multiview.py (gloo on CPU).  Each rank renders its own view with the
+oracle (test infrastructure: the HIP path needs a GPU), fills a ViewGradReducer from it and runs the exchange."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+N, W, H, DEG = 1500, 96, 64, 3
+
+
+def view_inputs(view, world):
+    from tests.helpers import scene_inputs
+    return scene_inputs(N, W, H, sh_degree=DEG, seed=3, view_index=view, num_views=world)
+
+
+def oracle_view(view, world):
+    """Per-view oracle gradients plus the per-view densification inputs."""
+    from tests.helpers import run_oracle, upstream
+    inp = view_inputs(view, world)
+    _, radii, _, run = run_oracle(inp)
+    dc, di = upstream(W, H, seed=view)
+    g = run.backward(dc, di)
+    g["colors_sh"] = g["colors"] * (1 - run.clamped()).astype(np.float32)
+    g["radii"] = radii
+    g["campos"] = inp["campos"]
+    g["means3D_in"] = inp["means3D"]
+    return g
+
+
+def oracle_sh_views(means3D, campos, dcolors_sh, sh_degree, M, out):
+    from oracle import oracle as O
+    r = O.sh_backward_views(means3D.numpy(), campos.numpy(), dcolors_sh.numpy(), sh_degree, M)
+    out.copy_(torch.from_numpy(r))
+    return out
+
+
+def worker(rank, world, port, mode, result_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gaussian_splatting_lightning_amd.multiview import ViewGradReducer
+        g = oracle_view(rank, world)
+        red = ViewGradReducer(N, 16, DEG, "cpu", mode=mode, sh_views_fn=oracle_sh_views)
+        out = red.backward_out()
+        for k in ("means3D", "scales", "rotations", "opacities", "means2D"):
+            out[k].copy_(torch.from_numpy(g[k]).reshape(out[k].shape))
+        if red.compact:
+            out["colors_sh"].copy_(torch.from_numpy(g["colors_sh"]))
+        else:
+            out["shs"].copy_(torch.from_numpy(g["shs"]))
+        red.record_view(red.means2D, torch.from_numpy(g["radii"]))
+        red.reduce(torch.from_numpy(g["means3D_in"]), torch.from_numpy(g["campos"]))
+        res = {k: v.numpy() for k, v in red.grads.items()}
+        res["stats"] = red.stats.numpy()
+        res["radii_max"] = red.radii_max.numpy()
+        np.savez(os.path.join(result_dir, f"rank{rank}.npz"), **res)
+    finally:
+        dist.destroy_process_group()

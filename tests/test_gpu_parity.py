@@ -14,7 +14,7 @@ import pytest
 import torch
 
 from tests.helpers import (close_fraction, golden_inputs, hip_state_arrays, load_golden, rel_l2, run_hip,
-                           run_oracle, scene_inputs, upstream)
+                           run_oracle, scene_inputs, settings_for, upstream)
 
 pytestmark = pytest.mark.gpu
 
@@ -278,3 +278,69 @@ def test_exact_culling_is_bitwise_invisible(gpu_device):
         assert np.array_equal(cull[k], full[k]), k
     for k in GRADS:
         assert np.array_equal(cull["grads"][k], full["grads"][k]), k
+
+
+def test_gs_lightning_rasterize_api(gpu_device):
+    """rasterize_gaussian / markVisible with gs_lightning/rasterize/rasterize.py:28-46's signature, checked
+    against that function's own outputs and autograd gradients (unsaturated golden)."""
+    from gaussian_splatting_lightning_amd.rasterize import markVisible, rasterize_gaussian
+    z = load_golden("unsat_sh3_150x100")
+    t = {k: torch.as_tensor(z[k], device=gpu_device) for k in
+         ("means3D", "opacities", "scales", "rotations", "shs", "viewmatrix", "projmatrix", "campos", "bg")}
+    leaves = {k: t[k].clone().requires_grad_(True) for k in ("means3D", "opacities", "scales", "rotations", "shs")}
+    img, radii, depth = rasterize_gaussian(
+        leaves["means3D"], leaves["opacities"], leaves["scales"], leaves["rotations"], leaves["shs"],
+        float(z["scale_modifier"]), int(z["image_width"]), int(z["image_height"]), float(z["tanfovx"]),
+        float(z["tanfovy"]), t["viewmatrix"], t["projmatrix"], t["campos"], t["bg"], int(z["sh_degree"]))
+    assert img.shape == z["ref_color"].shape and depth.shape == z["ref_invdepth"].shape
+    assert radii.dtype == torch.float32
+    assert np.abs(img.detach().cpu().numpy() - z["ref_color"]).max() <= 1e-5
+    assert np.abs(depth.detach().cpu().numpy() - z["ref_invdepth"]).max() <= 1e-5
+    r = radii.cpu().numpy()
+    on = r > 0
+    assert np.array_equal(r[on], z["ref_radii"][on])
+    (img * torch.as_tensor(z["dL_dcolor"], device=gpu_device)).sum().add_(
+        (depth * torch.as_tensor(z["dL_dinvdepth"], device=gpu_device)).sum()).backward()
+    for k in ("means3D", "opacities", "scales", "rotations", "shs"):
+        assert rel_l2(leaves[k].grad.cpu().numpy(), z["ref_grad_" + k]) <= 1e-4, k
+    vis = markVisible(t["means3D"], t["viewmatrix"], t["projmatrix"]).cpu().numpy()
+    from oracle import oracle as O
+    assert np.array_equal(vis, O.mark_visible(z["means3D"], z["viewmatrix"], z["projmatrix"]))
+
+
+def test_compact_sh_views_matches_dense(gpu_device):
+    """backward_raw(compact_sh=True) + gsr_sh_backward_views over 3 views == the sum of the dense per-view
+    dL/dshs; every other gradient of the compact backward is bitwise the dense one."""
+    from gaussian_splatting_lightning_amd.rasterizer import backward_raw, forward_raw, sh_backward_views
+    V = 3
+    dense_sum, factors, camposes = None, [], []
+    for v in range(V):
+        inp = scene_inputs(4000, 160, 120, sh_degree=3, seed=5, view_index=v, num_views=V)
+        rs = settings_for(inp, gpu_device)
+        t = {k: torch.as_tensor(inp[k], device=gpu_device) for k in
+             ("means3D", "opacities", "scales", "rotations", "shs")}
+        dc, di = (torch.as_tensor(a, device=gpu_device) for a in upstream(160, 120, seed=v))
+        _, _, _, st = forward_raw(t["means3D"], t["shs"], None, t["opacities"], t["scales"], t["rotations"], None, rs)
+        gd = backward_raw(st, rs, dc, di)
+        gc = backward_raw(st, rs, dc, di, compact_sh=True)
+        assert gc["shs"] is None
+        for k in ("means3D", "means2D", "opacities", "scales", "rotations", "colors"):
+            assert torch.equal(gd[k], gc[k]), k
+        dense_sum = gd["shs"].clone() if dense_sum is None else dense_sum + gd["shs"]
+        factors.append(gc["colors_sh"])
+        camposes.append(rs.campos)
+        if v == 0:
+            one = sh_backward_views(t["means3D"], rs.campos.view(1, 3), gc["colors_sh"].unsqueeze(0), 3, 16)
+            ref1 = gd["shs"].cpu().numpy()
+            np.testing.assert_allclose(one.cpu().numpy(), ref1, rtol=1e-5, atol=1e-6 * np.abs(ref1).max())
+    got = sh_backward_views(t["means3D"], torch.stack(camposes), torch.stack(factors), 3, 16)
+    # summing views cancels: compare at 1e-6 of the largest coefficient gradient
+    ds = dense_sum.cpu().numpy()
+    np.testing.assert_allclose(got.cpu().numpy(), ds, rtol=1e-5, atol=1e-6 * np.abs(ds).max())
+    ref = O_sh_views(t["means3D"], torch.stack(camposes), torch.stack(factors))
+    np.testing.assert_allclose(got.cpu().numpy(), ref, rtol=1e-5, atol=1e-6 * np.abs(ref).max())
+
+
+def O_sh_views(means3D, campos, factors):
+    from oracle import oracle as O
+    return O.sh_backward_views(means3D.cpu().numpy(), campos.cpu().numpy(), factors.cpu().numpy(), 3, 16)
