@@ -44,11 +44,11 @@ __device__ __forceinline__ void add_row(const float *__restrict__ rows, uint32_t
 constexpr int BWD_BATCH = 32;
 
 __device__ __forceinline__ float dpp_rows_then_pairs(float v) {
-    v += dpp_mov<0xB1>(0.f, v);        // quad_perm [1,0,3,2]
-    v += dpp_mov<0x4E>(0.f, v);        // quad_perm [2,3,0,1]
-    v += dpp_mov<0x141>(0.f, v);       // row_half_mirror
-    v += dpp_mov<0x140>(0.f, v);       // row_mirror: every lane holds its 16-lane row sum
-    v += dpp_mov<0x142, 0xa>(0.f, v);  // row_bcast:15 -> rows 1 and 3 hold (r0 + r1), (r2 + r3)
+    v = dpp_add<0xB1>(v);        // quad_perm [1,0,3,2]
+    v = dpp_add<0x4E>(v);        // quad_perm [2,3,0,1]
+    v = dpp_add<0x141>(v);       // row_half_mirror
+    v = dpp_add<0x140>(v);       // row_mirror: every lane holds its 16-lane row sum
+    v = dpp_add<0x142, 0xa>(v);  // row_bcast:15 -> lanes 31 / 63 hold (r0 + r1), (r2 + r3)
     return v;
 }
 

@@ -352,14 +352,22 @@ __device__ __forceinline__ float dpp_mov(float old, float v) {
                                                       BANK_MASK, BOUND));
 }
 
+// v + (v moved across lanes by DPP CTRL).  No `old` operand: lanes outside ROW_MASK/BANK_MASK receive an
+// undefined value, so callers only read lanes the pattern fully defines.  Without an old value the compiler
+// folds the move into the add (v_add_f32_dpp) instead of zero-initialising a temporary first.
+template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf>
+__device__ __forceinline__ float dpp_add(float v) {
+    return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, ROW_MASK, BANK_MASK, false));
+}
+
 // Sum over the 64 lanes (every lane must be active); the result is returned wave-uniform.
 __device__ __forceinline__ float wave_sum(float v) {
-    v += dpp_mov<0xB1>(0.f, v);            // quad_perm [1,0,3,2]
-    v += dpp_mov<0x4E>(0.f, v);            // quad_perm [2,3,0,1]
-    v += dpp_mov<0x141>(0.f, v);           // row_half_mirror
-    v += dpp_mov<0x140>(0.f, v);           // row_mirror -> row sums in every lane
-    v += dpp_mov<0x142, 0xa>(0.f, v);      // row_bcast:15 into rows 1, 3
-    v += dpp_mov<0x143, 0xc>(0.f, v);      // row_bcast:31 into rows 2, 3
+    v = dpp_add<0xB1>(v);        // quad_perm [1,0,3,2]
+    v = dpp_add<0x4E>(v);        // quad_perm [2,3,0,1]
+    v = dpp_add<0x141>(v);       // row_half_mirror
+    v = dpp_add<0x140>(v);       // row_mirror -> row sums in every lane
+    v = dpp_add<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3 (lane 31 = r0 + r1)
+    v = dpp_add<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3 (lane 63 = total)
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
