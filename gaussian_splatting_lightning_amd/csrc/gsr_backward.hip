@@ -81,6 +81,7 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_bwd_v3_kernel(RenderBwd
     const size_t HW = (size_t)p.W * p.H;
     float T[PIX_PER_LANE], nbg[PIX_PER_LANE], dp0[PIX_PER_LANE], dp1[PIX_PER_LANE], dp2[PIX_PER_LANE];
     float dinv[PIX_PER_LANE], ar0[PIX_PER_LANE], ar1[PIX_PER_LANE], ar2[PIX_PER_LANE], ainv[PIX_PER_LANE];
+    float pfy[PIX_PER_LANE];
     uint32_t lastc[PIX_PER_LANE];
 #pragma unroll
     for (int k = 0; k < PIX_PER_LANE; k++) {
@@ -89,6 +90,7 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_bwd_v3_kernel(RenderBwd
         const size_t pid = inside ? (size_t)py * p.W + px : 0;
         const float Tf = inside ? p.final_T[pid] : 0.f;
         T[k] = Tf;
+        pfy[k] = (float)py;
         lastc[k] = inside ? p.n_contrib[pid] : 0u;
         dp0[k] = inside ? p.dL_dpix[pid] : 0.f;
         dp1[k] = inside ? p.dL_dpix[HW + pid] : 0.f;
@@ -106,25 +108,28 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_bwd_v3_kernel(RenderBwd
             const uint32_t gid = p.point_list[range.x + (uint32_t)(bend - 1 - lane)];
             my_a = p.rec_a[gid];
             my_b = p.rec_b[gid];
-            s_a[w][lane] = my_a;
-            s_b[w][lane] = my_b;
+            s_a[w][lane] = stage_rec_a(my_a);
+            s_b[w][lane] = stage_rec_b(my_b);
             s_c[w][lane] = p.rec_c[gid];
         }
         wave_lds_sync();
         for (int j = 0; j < cnt; j++) {
             const uint32_t idx = (uint32_t)(bend - 1 - j);
-            const float4 a = s_a[w][j];
-            const float4 b = s_b[w][j];
-            const float2 c = s_c[w][j];
-            float m[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+            const float4 a = s_a[w][j];  // x, y, A, B
+            const float4 b = s_b[w][j];  // C, o, r, g
+            const float2 c = s_c[w][j];  // b, 1/depth
+            const float dx = a.x - pfx;
+            const float P0 = (a.z * dx) * dx, L = a.w * dx;
+            // per lane: Q0 = sum q, Q1 = sum q dy, Q2 = sum q dy^2 over its pixels (dx is shared), colour weights
+            float Q0 = 0.f, Q1 = 0.f, Q2 = 0.f, w0 = 0.f, w1 = 0.f, w2 = 0.f, w3 = 0.f;
             bool any = false;
 #pragma unroll
             for (int k = 0; k < PIX_PER_LANE; k++) {
                 if (idx >= lastc[k]) continue;
-                const float dx = a.x - pfx, dy = a.y - (float)(py0 + 4 * k);
-                const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
-                if (power > 0.0f) continue;
-                const float G = fast_exp(power);
+                const float dy = a.y - pfy[k];
+                const float power2 = power2_at(b.x, dy, P0, L);
+                if (power2 > 0.0f) continue;
+                const float G = __builtin_amdgcn_exp2f(power2);
                 const float alpha = fminf(0.99f, b.y * G);
                 if (alpha < 1.0f / 255.0f) continue;
                 any = true;
@@ -132,32 +137,42 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_bwd_v3_kernel(RenderBwd
                 const float r = fast_rcp(one_m);
                 T[k] = T[k] * r;
                 const float wgt = alpha * T[k];
-                float dL_dalpha = (b.z - ar0[k]) * dp0[k];
-                dL_dalpha += (b.w - ar1[k]) * dp1[k];
-                dL_dalpha += (c.x - ar2[k]) * dp2[k];
-                m[6] += wgt * dp0[k];
-                m[7] += wgt * dp1[k];
-                m[8] += wgt * dp2[k];
-                ar0[k] = alpha * b.z + one_m * ar0[k];
-                ar1[k] = alpha * b.w + one_m * ar1[k];
-                ar2[k] = alpha * c.x + one_m * ar2[k];
+                const float d0 = b.z - ar0[k], d1 = b.w - ar1[k], d2 = c.x - ar2[k];
+                float dL_dalpha = d0 * dp0[k];
+                dL_dalpha = fmaf(d1, dp1[k], dL_dalpha);
+                dL_dalpha = fmaf(d2, dp2[k], dL_dalpha);
+                w0 = fmaf(wgt, dp0[k], w0);
+                w1 = fmaf(wgt, dp1[k], w1);
+                w2 = fmaf(wgt, dp2[k], w2);
+                ar0[k] = fmaf(alpha, d0, ar0[k]);  // alpha c + (1 - alpha) accum
+                ar1[k] = fmaf(alpha, d1, ar1[k]);
+                ar2[k] = fmaf(alpha, d2, ar2[k]);
                 if (HAS_INV) {
-                    dL_dalpha += (c.y - ainv[k]) * dinv[k];
-                    m[9] += wgt * dinv[k];
-                    ainv[k] = alpha * c.y + one_m * ainv[k];
+                    const float di = c.y - ainv[k];
+                    dL_dalpha = fmaf(di, dinv[k], dL_dalpha);
+                    w3 = fmaf(wgt, dinv[k], w3);
+                    ainv[k] = fmaf(alpha, di, ainv[k]);
                 }
-                dL_dalpha = dL_dalpha * T[k] + nbg[k] * r;
+                dL_dalpha = fmaf(dL_dalpha, T[k], nbg[k] * r);
                 const float q = G * dL_dalpha;
-                const float qdx = q * dx, qdy = q * dy;
-                m[0] += q;
-                m[1] += qdx;
-                m[2] += qdy;
-                m[3] += qdx * dx;
-                m[4] += qdx * dy;
-                m[5] += qdy * dy;
+                const float qdy = q * dy;
+                Q0 += q;
+                Q1 += qdy;
+                Q2 = fmaf(qdy, dy, Q2);
             }
             float4 *dst = &s_part[w][j][0][0];
             if (__ballot(any)) {
+                float m[10];
+                m[0] = Q0;
+                m[1] = Q0 * dx;
+                m[2] = Q1;
+                m[3] = m[1] * dx;
+                m[4] = Q1 * dx;
+                m[5] = Q2;
+                m[6] = w0;
+                m[7] = w1;
+                m[8] = w2;
+                m[9] = w3;
 #pragma unroll
                 for (int v = 0; v < 10; v++) m[v] = dpp_rows_then_pairs(m[v]);
                 if ((lane & 31) == 31) {  // lanes 31 / 63: (row0 + row1) / (row2 + row3)

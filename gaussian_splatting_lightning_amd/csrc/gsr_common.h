@@ -213,7 +213,8 @@ __device__ __forceinline__ void get_rect(float2 p, int radius, int gx, int gy, i
 // and gradient is bitwise unchanged (the skipped instances would all hit `alpha < 1/255`).  q_min is the
 // exact minimum of the conic quadratic form over the tile's pixel rectangle (double precision); the fp32
 // evaluation of q at any pixel is within eps*q of the exact value, eps = 1e-5 (|a|+|b|+|c|) / lambda_min
-// (>= 25x the worst-case rounding of the 6-op power expression), and fast_exp is within 1e-5 relative.
+// (>= 25x the worst-case rounding of the prescaled 5-op power2 expression), and v_exp_f32 is within 1e-5
+// relative.
 constexpr int CULL_MAX_AREA = 64;
 struct CullGauss {
     double x, y, a, b, c, inv_a, inv_c, thr;
@@ -340,10 +341,26 @@ __device__ __forceinline__ float quad_form(const float a[3], const float c6[6], 
 }
 
 // exp(x) as v_exp_f32(x * log2 e): 2 instructions instead of the 13 of the correctly rounded expf.
-// Used identically by the forward and the backward composite, so the backward's T recovery divides by
-// exactly the (1 - alpha) the forward multiplied with.  Relative error ~1e-7 (DESIGN.md "Numerics").
 __device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 __device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// Compositing exponent, evaluated identically by the forward and the backward composite (so the backward's
+// T recovery divides by exactly the (1 - alpha) the forward multiplied with).  In base 2 and with the conic
+// prescaled when a batch is staged into LDS -- (A, B, C) = -log2(e) (a/2, b, c/2) -- the exponent is
+//     power2 = log2(e) * power = A dx^2 + B dx dy + C dy^2,   G = v_exp_f32(power2).
+// A lane's pixels share one column, so P0 = A dx^2 and L = B dx are formed once per instance and every pixel
+// costs dy, fma, fma.  Relative error vs the reference's expf(power) ~1e-7 (DESIGN.md "Numerics").
+constexpr float NEG_HALF_LOG2E = -0.72134752044448170f;
+constexpr float NEG_LOG2E = -1.4426950408889634f;
+__device__ __forceinline__ float4 stage_rec_a(float4 a) {  // (x, y, conic.x, conic.y) -> (x, y, A, B)
+    return make_float4(a.x, a.y, a.z * NEG_HALF_LOG2E, a.w * NEG_LOG2E);
+}
+__device__ __forceinline__ float4 stage_rec_b(float4 b) {  // (conic.z, o, r, g) -> (C, o, r, g)
+    return make_float4(b.x * NEG_HALF_LOG2E, b.y, b.z, b.w);
+}
+__device__ __forceinline__ float power2_at(float C, float dy, float P0, float L) {
+    return fmaf(dy, fmaf(C, dy, L), P0);
+}
 
 // --- wave64 primitives ---------------------------------------------------------------------------
 template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf, bool BOUND = false>

@@ -297,25 +297,26 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v3_kernel(RenderFwd
             const uint32_t gid = p.inst_gid[u];
             p.point_list[s] = gid;
             p.inv[u] = s;
-            s_a[w][lane] = p.rec_a[gid];
-            s_b[w][lane] = p.rec_b[gid];
+            s_a[w][lane] = stage_rec_a(p.rec_a[gid]);
+            s_b[w][lane] = stage_rec_b(p.rec_b[gid]);
             s_c[w][lane] = p.rec_c[gid];
         }
         loaded_end = min(range.y, base + 64u);
         wave_lds_sync();
         const int cnt = (int)min(64u, range.y - base);
         for (int j = 0; j < cnt; j++) {
-            const float4 a = s_a[w][j];
-            const float4 b = s_b[w][j];
-            const float2 c = s_c[w][j];
+            const float4 a = s_a[w][j];  // x, y, A, B (stage_rec_a)
+            const float4 b = s_b[w][j];  // C, o, r, g
+            const float2 c = s_c[w][j];  // b, 1/depth
             contributor++;
             bool still = false;
+            const float dx = a.x - pfx;
+            const float P0 = (a.z * dx) * dx, L = a.w * dx;
 #pragma unroll
             for (int k = 0; k < PIX_PER_LANE; k++) {
-                const float dx = a.x - pfx, dy = a.y - pfy[k];
-                const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
-                const float alpha = fminf(0.99f, b.y * fast_exp(power));
-                const bool ok = active[k] && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+                const float power2 = power2_at(b.x, a.y - pfy[k], P0, L);
+                const float alpha = fminf(0.99f, b.y * __builtin_amdgcn_exp2f(power2));
+                const bool ok = active[k] && !(power2 > 0.0f) && !(alpha < 1.0f / 255.0f);
                 const float test_T = T[k] * (1 - alpha);
                 const bool stop = ok && test_T < 0.0001f;
                 const bool take = ok && !stop;
