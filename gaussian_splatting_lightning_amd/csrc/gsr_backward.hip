@@ -37,19 +37,48 @@ __device__ __forceinline__ void add_row(const float *__restrict__ rows, uint32_t
 //   dG/ddelta = -G (conic . delta), every conic / mean / opacity gradient term of the reference is a
 //   uniform combination of these moments, applied once per instance after the reduction:
 //     dopacity = S,  dconic = -o/2 (Sxx, Sxy, Syy),  dmean2D = -o (W/2, H/2) * (a Sx + b Sy, b Sx + c Sy).
-//   The 10 per-lane sums are reduced with 5 DPP steps (row sums, then row_bcast:15 pairs) and the two
-//   half-wave partials of every instance go to LDS; after each batch of 32 instances lane j adds the two
-//   partials of instance j, applies the uniform conversion and stores the gradient row.
+//   The 10 per-lane sums are reduced across the wave by a transposing permlane/DPP reduction
+//   (wave_reduce10_store) into LDS; after each batch of 32 instances lane j reads the 10 totals of instance j,
+//   applies the uniform conversion and stores the gradient row.
 // ------------------------------------------------------------------------------------------------
 constexpr int BWD_BATCH = 32;
+constexpr int PART = 12;  // floats per instance in the LDS partial buffer (10 sums + 2 pad)
 
-__device__ __forceinline__ float dpp_rows_then_pairs(float v) {
-    v = dpp_add<0xB1>(v);        // quad_perm [1,0,3,2]
-    v = dpp_add<0x4E>(v);        // quad_perm [2,3,0,1]
-    v = dpp_add<0x141>(v);       // row_half_mirror
-    v = dpp_add<0x140>(v);       // row_mirror: every lane holds its 16-lane row sum
-    v = dpp_add<0x142, 0xa>(v);  // row_bcast:15 -> lanes 31 / 63 hold (r0 + r1), (r2 + r3)
-    return v;
+// x + y after v_permlane32_swap(x, y): lanes 0-31 hold x[l] + x[l+32], lanes 32-63 hold y[l-32] + y[l]
+// (lane mapping measured on MI355X by tools/probes/permlane_probe.hip).
+__device__ __forceinline__ float sum_swap32(float x, float y) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// x + y after v_permlane16_swap(x, y): even rows hold x summed over the row pair, odd rows hold y.
+__device__ __forceinline__ float sum_swap16(float x, float y) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// Transposing reduction of 10 per-lane values over the wave: each exchange level halves the number of live
+// registers by keeping one value of a pair on each side of the lane split (permlane32 / permlane16 swaps for
+// lane bits 5 and 4, a DPP row_ror:8 exchange for bit 3), then bits 0-2 are summed with DPP.  ~30 VALU ops
+// instead of 50 (5 DPP adds per value).  Lane l ends with the wave total of value 4 b3 + 2 b4 + b5 in c0 and
+// of value 8 + b5 in c8 (b = bits of l); lanes with l % 8 == 0 store them.
+__device__ __forceinline__ void wave_reduce10_store(const float m[10], float *__restrict__ dst, int lane) {
+    const float a0 = sum_swap32(m[0], m[1]), a1 = sum_swap32(m[2], m[3]), a2 = sum_swap32(m[4], m[5]);
+    const float a3 = sum_swap32(m[6], m[7]), a4 = sum_swap32(m[8], m[9]);  // a_i: value 2 i + b5
+    const float b0 = sum_swap16(a0, a1);  // value 2 b4 + b5
+    const float b1 = sum_swap16(a2, a3);  // value 4 + 2 b4 + b5
+    float c8 = sum_swap16(a4, a4);        // value 8 + b5
+    const bool hi3 = (lane & 8) != 0;
+    const float keep = hi3 ? b1 : b0, send = hi3 ? b0 : b1;
+    float c0 = keep + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send), 0x128, 0xf, 0xf, false));
+    c8 = dpp_add<0x128>(c8);  // row_ror:8 (= lane ^ 8)
+    c0 = dpp_add<0xB1>(c0);   // quad_perm [1,0,3,2]
+    c8 = dpp_add<0xB1>(c8);
+    c0 = dpp_add<0x4E>(c0);   // quad_perm [2,3,0,1]
+    c8 = dpp_add<0x4E>(c8);
+    c0 = dpp_add<0x141>(c0);  // row_half_mirror: lanes {l, l^7} -> all 8 lanes of the half row
+    c8 = dpp_add<0x141>(c8);
+    if ((lane & 7) == 0) dst[((lane >> 1) & 4) | ((lane >> 3) & 2) | (lane >> 5)] = c0;
+    if ((lane & 31) == 0) dst[8 + (lane >> 5)] = c8;
 }
 
 template <bool HAS_INV, int MIN_WAVES>
@@ -57,7 +86,7 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_bwd_v3_kernel(RenderBwd
     __shared__ float4 s_a[4][BWD_BATCH];
     __shared__ float4 s_b[4][BWD_BATCH];
     __shared__ float2 s_c[4][BWD_BATCH];
-    __shared__ float4 s_part[4][BWD_BATCH][2][3];  // [wave][instance][half][10 sums + 2 pad]
+    __shared__ __attribute__((aligned(16))) float s_part[4][BWD_BATCH][PART];  // [wave][instance][10 sums]
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tile = blockIdx.x * 4 + w;
     if (tile >= p.num_tiles) return;
@@ -160,7 +189,7 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_bwd_v3_kernel(RenderBwd
                 Q1 += qdy;
                 Q2 = fmaf(qdy, dy, Q2);
             }
-            float4 *dst = &s_part[w][j][0][0];
+            float *dst = s_part[w][j];
             if (__ballot(any)) {
                 float m[10];
                 m[0] = Q0;
@@ -173,25 +202,17 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_bwd_v3_kernel(RenderBwd
                 m[7] = w1;
                 m[8] = w2;
                 m[9] = w3;
-#pragma unroll
-                for (int v = 0; v < 10; v++) m[v] = dpp_rows_then_pairs(m[v]);
-                if ((lane & 31) == 31) {  // lanes 31 / 63: (row0 + row1) / (row2 + row3)
-                    float4 *d = dst + 3 * (lane >> 5);
-                    d[0] = make_float4(m[0], m[1], m[2], m[3]);
-                    d[1] = make_float4(m[4], m[5], m[6], m[7]);
-                    d[2] = make_float4(m[8], m[9], 0.f, 0.f);
-                }
-            } else if ((lane & 31) == 31) {
-                float4 *d = dst + 3 * (lane >> 5);
-                d[0] = d[1] = d[2] = make_float4(0.f, 0.f, 0.f, 0.f);
+                wave_reduce10_store(m, dst, lane);
+            } else if (lane < 10) {
+                dst[lane] = 0.f;
             }
         }
         wave_lds_sync();
         if (lane < cnt) {
-            const float4 *src = &s_part[w][lane][0][0];
-            const float4 u0 = src[0], u1 = src[1], u2 = src[2], v0 = src[3], v1 = src[4], v2 = src[5];
-            const float S = u0.x + v0.x, Sx = u0.y + v0.y, Sy = u0.z + v0.z, Sxx = u0.w + v0.w;
-            const float Sxy = u1.x + v1.x, Syy = u1.y + v1.y;
+            const float4 *src = reinterpret_cast<const float4 *>(s_part[w][lane]);
+            const float4 u0 = src[0], u1 = src[1];
+            const float2 u2 = *reinterpret_cast<const float2 *>(s_part[w][lane] + 8);
+            const float S = u0.x, Sx = u0.y, Sy = u0.z, Sxx = u0.w, Sxy = u1.x, Syy = u1.y;
             const float o = my_b.y, ca = my_a.z, cb = my_a.w, cc = my_b.x;
             float row[10];
             row[0] = -o * hW * (ca * Sx + cb * Sy);
@@ -200,10 +221,10 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_bwd_v3_kernel(RenderBwd
             row[3] = -0.5f * o * Sxy;
             row[4] = -0.5f * o * Syy;
             row[5] = S;
-            row[6] = u1.z + v1.z;
-            row[7] = u1.w + v1.w;
-            row[8] = u2.x + v2.x;
-            row[9] = u2.y + v2.y;
+            row[6] = u1.z;
+            row[7] = u1.w;
+            row[8] = u2.x;
+            row[9] = u2.y;
             store_row(p.rows, range.x + (uint32_t)(bend - 1 - lane), row);
         }
         wave_lds_sync();
