@@ -362,6 +362,24 @@ __device__ __forceinline__ float power2_at(float C, float dy, float P0, float L)
     return fmaf(dy, fmaf(C, dy, L), P0);
 }
 
+// --- per-instance gradient rows (render_bwd -> big_reduce / preprocess_bwd) -------------------------
+// Row layout: [0] dmean2D.x  [1] dmean2D.y  [2] dconic.x  [3] dconic.y  [4] dconic.w  [5] dopacity
+//             [6..8] dcolor  [9] dinvdepth  [10..11] pad
+__device__ __forceinline__ void store_row(float *__restrict__ rows, uint32_t s, const float r[10]) {
+    float4 *dst = reinterpret_cast<float4 *>(rows + (size_t)s * GRAD_ROW);
+    dst[0] = make_float4(r[0], r[1], r[2], r[3]);
+    dst[1] = make_float4(r[4], r[5], r[6], r[7]);
+    dst[2] = make_float4(r[8], r[9], 0.f, 0.f);
+}
+
+__device__ __forceinline__ void add_row(const float *__restrict__ rows, uint32_t s, float acc[10]) {
+    const float4 *src = reinterpret_cast<const float4 *>(rows + (size_t)s * GRAD_ROW);
+    const float4 a = src[0], b = src[1], c = src[2];
+    acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+    acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+    acc[8] += c.x; acc[9] += c.y;
+}
+
 // --- wave64 primitives ---------------------------------------------------------------------------
 template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf, bool BOUND = false>
 __device__ __forceinline__ float dpp_mov(float old, float v) {

@@ -257,13 +257,13 @@ void launch_identify_ranges(hipStream_t s, const uint32_t *keys_sorted, uint32_t
 // v3: the four pixels of a lane are updated with predication instead of exec-mask branches, so the
 // compiler can interleave the four independent pixel chains and no per-pixel branch bookkeeping is issued.
 // Colour accumulation uses w = alpha * T once per contributor (one FMA per channel).
-template <int MIN_WAVES>
-__global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v3_kernel(RenderFwdParams p) {
-    __shared__ float4 s_a[4][64];
-    __shared__ float4 s_b[4][64];
-    __shared__ float2 s_c[4][64];
+template <int MIN_WAVES, int WPB, bool PIPE>
+__global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_fwd_v3_kernel(RenderFwdParams p) {
+    __shared__ float4 s_a[WPB][65];
+    __shared__ float4 s_b[WPB][65];
+    __shared__ float2 s_c[WPB][65];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tile = blockIdx.x * 4 + w;
+    const int tile = blockIdx.x * WPB + w;
     if (tile >= p.num_tiles) return;
     const int tx = tile % p.gx, ty = tile / p.gx;
     const int px = tx * BLOCK_X + (lane & 15);
@@ -304,10 +304,22 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v3_kernel(RenderFwd
         loaded_end = min(range.y, base + 64u);
         wave_lds_sync();
         const int cnt = (int)min(64u, range.y - base);
+        float4 a = s_a[w][0], b = s_b[w][0];
+        float2 c = s_c[w][0];
         for (int j = 0; j < cnt; j++) {
-            const float4 a = s_a[w][j];  // x, y, A, B (stage_rec_a)
-            const float4 b = s_b[w][j];  // C, o, r, g
-            const float2 c = s_c[w][j];  // b, 1/depth
+            // a: x, y, A, B (stage_rec_a); b: C, o, r, g; c: b, 1/depth.  With PIPE the next instance's
+            // LDS reads are issued before this one's math (slot 64 is a harmless pad).
+            float4 an, bn;
+            float2 cn;
+            if (PIPE) {
+                an = s_a[w][j + 1];
+                bn = s_b[w][j + 1];
+                cn = s_c[w][j + 1];
+            } else {
+                a = s_a[w][j];
+                b = s_b[w][j];
+                c = s_c[w][j];
+            }
             contributor++;
             bool still = false;
             const float dx = a.x - pfx;
@@ -331,6 +343,11 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v3_kernel(RenderFwd
                 still |= active[k];
             }
             if (__ballot(still) == 0) break;
+            if (PIPE) {
+                a = an;
+                b = bn;
+                c = cn;
+            }
         }
         wave_lds_sync();
     }
@@ -361,8 +378,15 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v3_kernel(RenderFwd
 void launch_render_fwd(hipStream_t s, const RenderFwdParams &p) {
     if (p.num_tiles <= 0) return;
     const dim3 grid(div_up(p.num_tiles, 4)), block(256);
-    if (tuning("fwd_minwaves", 4) >= 8) render_fwd_v3_kernel<8><<<grid, block, 0, s>>>(p);
-    else render_fwd_v3_kernel<4><<<grid, block, 0, s>>>(p);
+    const int pipe = tuning("fwd_pipe", 0), wpb = tuning("fwd_wpb", 1);
+    if (wpb == 1) {
+        const dim3 g1(p.num_tiles), b1(64);
+        if (pipe) render_fwd_v3_kernel<4, 1, true><<<g1, b1, 0, s>>>(p);
+        else render_fwd_v3_kernel<4, 1, false><<<g1, b1, 0, s>>>(p);
+    } else {
+        if (pipe) render_fwd_v3_kernel<4, 4, true><<<grid, block, 0, s>>>(p);
+        else render_fwd_v3_kernel<4, 4, false><<<grid, block, 0, s>>>(p);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------

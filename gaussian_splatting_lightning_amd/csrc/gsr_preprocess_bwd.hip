@@ -1,0 +1,274 @@
+// gsr_preprocess_bwd.hip -- per-Gaussian backward: gathers the instance gradient rows of every Gaussian
+// (deterministic fixed order, through the inverse permutation), then the preprocess backward of the CUDA
+// submodule restated: 2D conic -> cov2D -> cov3D -> scale / rotation, 2D mean -> 3D mean, SH -> colour.
+// Its own translation unit so it can be compiled without SLP packing (build.py FILE_FLAGS).
+#include "gsr_kernels.h"
+#include "gsr_sh.h"
+
+namespace gsr {
+
+// ------------------------------------------------------------------------------------------------
+// preprocess backward: one thread per Gaussian
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void cov3d_backward(float3 scale, float mod, float4 rot, const float dc[6],
+                                               float3 &dscale, float4 &drot) {
+    const float r = rot.x, x = rot.y, y = rot.z, z = rot.w;
+    const Mat3 R = quat_to_rot(rot);
+    const float s[3] = {mod * scale.x, mod * scale.y, mod * scale.z};
+    float M[3][3], dSig[3][3], dM[3][3], dMt[3][3];
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+#pragma unroll
+        for (int rr = 0; rr < 3; rr++) M[c][rr] = s[rr] * R.m[c][rr];
+    dSig[0][0] = dc[0]; dSig[0][1] = 0.5f * dc[1]; dSig[0][2] = 0.5f * dc[2];
+    dSig[1][0] = 0.5f * dc[1]; dSig[1][1] = dc[3]; dSig[1][2] = 0.5f * dc[4];
+    dSig[2][0] = 0.5f * dc[2]; dSig[2][1] = 0.5f * dc[4]; dSig[2][2] = dc[5];
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+#pragma unroll
+        for (int rr = 0; rr < 3; rr++)
+            dM[c][rr] = 2.0f * (M[0][rr] * dSig[c][0] + M[1][rr] * dSig[c][1] + M[2][rr] * dSig[c][2]);
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+#pragma unroll
+        for (int rr = 0; rr < 3; rr++) dMt[c][rr] = dM[rr][c];
+    // dL/ds (w.r.t. the modified scale, as upstream; DESIGN.md notes the scale_modifier factor)
+    dscale.x = R.m[0][0] * dMt[0][0] + R.m[1][0] * dMt[0][1] + R.m[2][0] * dMt[0][2];
+    dscale.y = R.m[0][1] * dMt[1][0] + R.m[1][1] * dMt[1][1] + R.m[2][1] * dMt[1][2];
+    dscale.z = R.m[0][2] * dMt[2][0] + R.m[1][2] * dMt[2][1] + R.m[2][2] * dMt[2][2];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        dMt[0][k] *= s[0];
+        dMt[1][k] *= s[1];
+        dMt[2][k] *= s[2];
+    }
+    drot.x = 2 * z * (dMt[0][1] - dMt[1][0]) + 2 * y * (dMt[2][0] - dMt[0][2]) + 2 * x * (dMt[1][2] - dMt[2][1]);
+    drot.y = 2 * y * (dMt[1][0] + dMt[0][1]) + 2 * z * (dMt[2][0] + dMt[0][2]) + 2 * r * (dMt[1][2] - dMt[2][1]) -
+             4 * x * (dMt[2][2] + dMt[1][1]);
+    drot.z = 2 * x * (dMt[1][0] + dMt[0][1]) + 2 * r * (dMt[2][0] - dMt[0][2]) + 2 * z * (dMt[1][2] + dMt[2][1]) -
+             4 * y * (dMt[2][2] + dMt[0][0]);
+    drot.w = 2 * r * (dMt[0][1] - dMt[1][0]) + 2 * x * (dMt[2][0] + dMt[0][2]) + 2 * y * (dMt[1][2] + dMt[2][1]) -
+             4 * z * (dMt[1][1] + dMt[0][0]);
+}
+
+__global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams p) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= p.P) return;
+    const bool vis = p.radii[i] > 0;
+    float gs[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (vis) {
+        const uint32_t start = p.inst_start[i], cnt = p.tiles[i];
+        if (cnt > BIG_GAUSSIAN_TILES) {
+            add_row(p.bigsum, p.big_slot[i], gs);
+        } else {
+            // issue the index loads, then all row loads of a group, before summing (memory-level parallelism)
+            for (uint32_t k0 = 0; k0 < cnt; k0 += 4) {
+                uint32_t sidx[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) sidx[j] = (k0 + j < cnt) ? p.inv[start + k0 + j] : INV_NONE;
+                float4 ra[4], rb[4], rc[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    if (sidx[j] != INV_NONE) {
+                        const float4 *src = reinterpret_cast<const float4 *>(p.rows + (size_t)sidx[j] * GRAD_ROW);
+                        ra[j] = src[0];
+                        rb[j] = src[1];
+                        rc[j] = src[2];
+                    } else {
+                        ra[j] = rb[j] = rc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    gs[0] += ra[j].x; gs[1] += ra[j].y; gs[2] += ra[j].z; gs[3] += ra[j].w;
+                    gs[4] += rb[j].x; gs[5] += rb[j].y; gs[6] += rb[j].z; gs[7] += rb[j].w;
+                    gs[8] += rc[j].x; gs[9] += rc[j].y;
+                }
+            }
+        }
+    }
+    if (p.dL_dmeans2D) {
+        p.dL_dmeans2D[3 * i] = gs[0];
+        p.dL_dmeans2D[3 * i + 1] = gs[1];
+        p.dL_dmeans2D[3 * i + 2] = 0.f;
+    }
+    if (p.dL_dcolors) {
+        p.dL_dcolors[3 * i] = gs[6];
+        p.dL_dcolors[3 * i + 1] = gs[7];
+        p.dL_dcolors[3 * i + 2] = gs[8];
+    }
+    const int ncoef = p.M * 3;
+    if (!vis) {
+        if (p.dL_dopacity) p.dL_dopacity[i] = 0.f;
+        if (p.dL_dmeans3D) { p.dL_dmeans3D[3 * i] = 0.f; p.dL_dmeans3D[3 * i + 1] = 0.f; p.dL_dmeans3D[3 * i + 2] = 0.f; }
+        if (p.dL_dcov3D)
+            for (int k = 0; k < 6; k++) p.dL_dcov3D[6 * i + k] = 0.f;
+        if (p.dL_dsh)
+            for (int k = 0; k < ncoef; k++) p.dL_dsh[(size_t)i * ncoef + k] = 0.f;
+        if (p.dL_dcolors_sh) { p.dL_dcolors_sh[3 * i] = 0.f; p.dL_dcolors_sh[3 * i + 1] = 0.f; p.dL_dcolors_sh[3 * i + 2] = 0.f; }
+        if (p.dL_dscales) { p.dL_dscales[3 * i] = 0.f; p.dL_dscales[3 * i + 1] = 0.f; p.dL_dscales[3 * i + 2] = 0.f; }
+        if (p.dL_drot)
+            for (int k = 0; k < 4; k++) p.dL_drot[4 * i + k] = 0.f;
+        return;
+    }
+    const Mat4 view = load_mat4(p.view);
+    const float3 mean = load_f3(p.means3D, i);
+    float c6[6];
+    float3 scale = make_float3(0, 0, 0);
+    float4 rot = make_float4(1, 0, 0, 0);
+    if (p.cov3D_precomp) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) c6[k] = p.cov3D_precomp[6 * i + k];
+    } else {
+        scale = load_f3(p.scales, i);
+        rot = make_float4(p.rotations[4 * i], p.rotations[4 * i + 1], p.rotations[4 * i + 2], p.rotations[4 * i + 3]);
+        cov3d_from_scale_rot(scale, p.scale_modifier, rot, c6);
+    }
+    // ---- computeCov2D backward ----
+    const EwaT e = ewa_T(mean, view, p.focal_x, p.focal_y, p.tan_fovx, p.tan_fovy);
+    float c_xx = quad_form(e.t0, c6, e.t0), c_xy = quad_form(e.t1, c6, e.t0), c_yy = quad_form(e.t1, c6, e.t1);
+    constexpr float h_var = 0.3f;
+    float dopac = gs[5];
+    float d_inside_root = 0.f;
+    if (p.antialiasing) {
+        const float det_cov = c_xx * c_yy - c_xy * c_xy;
+        c_xx += h_var;
+        c_yy += h_var;
+        const float det_cov_plus = c_xx * c_yy - c_xy * c_xy;
+        const float hs = sqrtf(fmaxf(0.000025f, det_cov / det_cov_plus));
+        const float d_hs = dopac * p.opacities[i];
+        dopac = dopac * hs;
+        d_inside_root = (det_cov / det_cov_plus) <= 0.000025f ? 0.f : d_hs / (2 * hs);
+    } else {
+        c_xx += h_var;
+        c_yy += h_var;
+    }
+    float dL_dc_xx = 0.f, dL_dc_xy = 0.f, dL_dc_yy = 0.f;
+    if (p.antialiasing) {
+        const float x = c_xx, y = c_yy, z = c_xy, wv = h_var;
+        const float q = wv * wv + wv * (x + y) + x * y - z * z;
+        const float denom_f = d_inside_root / (q * q);
+        dL_dc_xx = wv * (wv * y + y * y + z * z) * denom_f;
+        dL_dc_yy = wv * (wv * x + x * x + z * z) * denom_f;
+        dL_dc_xy = -2.f * wv * z * (wv + x + y) * denom_f;
+    }
+    if (p.dL_dopacity) p.dL_dopacity[i] = dopac;
+    const float dcx = gs[2], dcy = gs[3], dcz = gs[4];
+    const float denom = c_xx * c_yy - c_xy * c_xy;
+    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    float dcov[6] = {0, 0, 0, 0, 0, 0};
+    const float *t0 = e.t0, *t1 = e.t1;
+    if (denom2inv != 0) {
+        dL_dc_xx += denom2inv * (-c_yy * c_yy * dcx + 2 * c_xy * c_yy * dcy + (denom - c_xx * c_yy) * dcz);
+        dL_dc_yy += denom2inv * (-c_xx * c_xx * dcz + 2 * c_xx * c_xy * dcy + (denom - c_xx * c_yy) * dcx);
+        dL_dc_xy += denom2inv * 2 * (c_xy * c_yy * dcx - (denom + 2 * c_xy * c_xy) * dcy + c_xx * c_xy * dcz);
+        dcov[0] = (t0[0] * t0[0] * dL_dc_xx + t0[0] * t1[0] * dL_dc_xy + t1[0] * t1[0] * dL_dc_yy);
+        dcov[3] = (t0[1] * t0[1] * dL_dc_xx + t0[1] * t1[1] * dL_dc_xy + t1[1] * t1[1] * dL_dc_yy);
+        dcov[5] = (t0[2] * t0[2] * dL_dc_xx + t0[2] * t1[2] * dL_dc_xy + t1[2] * t1[2] * dL_dc_yy);
+        dcov[1] = 2 * t0[0] * t0[1] * dL_dc_xx + (t0[0] * t1[1] + t0[1] * t1[0]) * dL_dc_xy + 2 * t1[0] * t1[1] * dL_dc_yy;
+        dcov[2] = 2 * t0[0] * t0[2] * dL_dc_xx + (t0[0] * t1[2] + t0[2] * t1[0]) * dL_dc_xy + 2 * t1[0] * t1[2] * dL_dc_yy;
+        dcov[4] = 2 * t0[2] * t0[1] * dL_dc_xx + (t0[1] * t1[2] + t0[2] * t1[1]) * dL_dc_xy + 2 * t1[1] * t1[2] * dL_dc_yy;
+    }
+    if (p.dL_dcov3D)
+        for (int k = 0; k < 6; k++) p.dL_dcov3D[6 * i + k] = dcov[k];
+    float dT0[3], dT1[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        // row k of the symmetric Vrk
+        const float vk0 = k == 0 ? c6[0] : (k == 1 ? c6[1] : c6[2]);
+        const float vk1 = k == 0 ? c6[1] : (k == 1 ? c6[3] : c6[4]);
+        const float vk2 = k == 0 ? c6[2] : (k == 1 ? c6[4] : c6[5]);
+        const float v0 = t0[0] * vk0 + t0[1] * vk1 + t0[2] * vk2;
+        const float v1 = t1[0] * vk0 + t1[1] * vk1 + t1[2] * vk2;
+        dT0[k] = 2 * v0 * dL_dc_xx + v1 * dL_dc_xy;
+        dT1[k] = 2 * v1 * dL_dc_yy + v0 * dL_dc_xy;
+    }
+    const float *vm = view.m;
+    const float dJ00 = vm[0] * dT0[0] + vm[4] * dT0[1] + vm[8] * dT0[2];
+    const float dJ02 = vm[2] * dT0[0] + vm[6] * dT0[1] + vm[10] * dT0[2];
+    const float dJ11 = vm[1] * dT1[0] + vm[5] * dT1[1] + vm[9] * dT1[2];
+    const float dJ12 = vm[2] * dT1[0] + vm[6] * dT1[1] + vm[10] * dT1[2];
+    const float3 t = e.t;
+    const float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
+    const float hx = p.focal_x, hy = p.focal_y;
+    const float dtx = e.xmul * -hx * tz2 * dJ02;
+    const float dty = e.ymul * -hy * tz2 * dJ12;
+    float dtz = -hx * tz2 * dJ00 - hy * tz2 * dJ11 + (2 * hx * t.x) * tz3 * dJ02 + (2 * hy * t.y) * tz3 * dJ12;
+    if (p.has_invdepth) dtz -= gs[9] / (t.z * t.z);
+    float3 dm = make_float3(vm[0] * dtx + vm[1] * dty + vm[2] * dtz, vm[4] * dtx + vm[5] * dty + vm[6] * dtz,
+                            vm[8] * dtx + vm[9] * dty + vm[10] * dtz);
+    // ---- 2D mean -> 3D mean through the projection ----
+    const Mat4 proj = load_mat4(p.proj);
+    const float *pm = proj.m;
+    const float4 mh = xform4(mean, proj);
+    const float m_w = 1.0f / (mh.w + 0.0000001f);
+    const float mul1 = (pm[0] * mean.x + pm[4] * mean.y + pm[8] * mean.z + pm[12]) * m_w * m_w;
+    const float mul2 = (pm[1] * mean.x + pm[5] * mean.y + pm[9] * mean.z + pm[13]) * m_w * m_w;
+    const float g2x = gs[0], g2y = gs[1];
+    dm.x += (pm[0] * m_w - pm[3] * mul1) * g2x + (pm[1] * m_w - pm[3] * mul2) * g2y;
+    dm.y += (pm[4] * m_w - pm[7] * mul1) * g2x + (pm[5] * m_w - pm[7] * mul2) * g2y;
+    dm.z += (pm[8] * m_w - pm[11] * mul1) * g2x + (pm[9] * m_w - pm[11] * mul2) * g2y;
+    // ---- SH backward ----
+    if (p.shs && p.M > 0) {
+        const uint8_t cl = p.clamped[i];
+        const float3 dRGB = make_float3((cl & 1) ? 0.f : gs[6], (cl & 2) ? 0.f : gs[7], (cl & 4) ? 0.f : gs[8]);
+        const float3 campos = make_float3(p.campos[0], p.campos[1], p.campos[2]);
+        if (p.dL_dcolors_sh) {
+            p.dL_dcolors_sh[3 * i] = dRGB.x;
+            p.dL_dcolors_sh[3 * i + 1] = dRGB.y;
+            p.dL_dcolors_sh[3 * i + 2] = dRGB.z;
+        }
+        float *dsh = p.dL_dsh ? p.dL_dsh + (size_t)i * ncoef : nullptr;  // null only with dL_dcolors_sh (API)
+        const float *shp = p.shs + (size_t)i * ncoef;
+        if (p.sh_vec16) {
+            // 16 coefficients x 3 = 192 B per Gaussian: 12 float4 loads and stores per lane
+            float shv[48], dshv[48];
+            const float4 *s4 = reinterpret_cast<const float4 *>(shp);
+#pragma unroll
+            for (int k = 0; k < 12; k++) {
+                const float4 q = s4[k];
+                shv[4 * k] = q.x; shv[4 * k + 1] = q.y; shv[4 * k + 2] = q.z; shv[4 * k + 3] = q.w;
+            }
+#pragma unroll
+            for (int k = 0; k < 48; k++) dshv[k] = 0.f;
+            dm = dm + sh_backward_dispatch(p.D, shv, mean - campos, dRGB, dshv);
+            if (dsh) {
+                float4 *d4 = reinterpret_cast<float4 *>(dsh);
+#pragma unroll
+                for (int k = 0; k < 12; k++)
+                    d4[k] = make_float4(dshv[4 * k], dshv[4 * k + 1], dshv[4 * k + 2], dshv[4 * k + 3]);
+            }
+        } else if (dsh) {
+            dm = dm + sh_backward_dispatch(p.D, shp, mean - campos, dRGB, dsh);
+            const int used = (p.D + 1) * (p.D + 1) * 3;
+            for (int k = used; k < ncoef; k++) dsh[k] = 0.f;
+        } else {
+            float dtmp[48];  // dL/dsh discarded (compact multi-view mode); only the direction term is kept
+            dm = dm + sh_backward_dispatch(p.D, shp, mean - campos, dRGB, dtmp);
+        }
+    }
+    if (p.dL_dmeans3D) {
+        p.dL_dmeans3D[3 * i] = dm.x;
+        p.dL_dmeans3D[3 * i + 1] = dm.y;
+        p.dL_dmeans3D[3 * i + 2] = dm.z;
+    }
+    // ---- cov3D backward ----
+    if (!p.cov3D_precomp && (p.dL_dscales || p.dL_drot)) {
+        float3 dsc;
+        float4 dr;
+        cov3d_backward(scale, p.scale_modifier, rot, dcov, dsc, dr);
+        if (p.dL_dscales) { p.dL_dscales[3 * i] = dsc.x; p.dL_dscales[3 * i + 1] = dsc.y; p.dL_dscales[3 * i + 2] = dsc.z; }
+        if (p.dL_drot) { p.dL_drot[4 * i] = dr.x; p.dL_drot[4 * i + 1] = dr.y; p.dL_drot[4 * i + 2] = dr.z; p.dL_drot[4 * i + 3] = dr.w; }
+    } else {
+        if (p.dL_dscales) { p.dL_dscales[3 * i] = 0.f; p.dL_dscales[3 * i + 1] = 0.f; p.dL_dscales[3 * i + 2] = 0.f; }
+        if (p.dL_drot)
+            for (int k = 0; k < 4; k++) p.dL_drot[4 * i + k] = 0.f;
+    }
+}
+
+void launch_preprocess_bwd(hipStream_t s, const PreprocessBwdParams &p) {
+    if (p.P <= 0) return;
+    preprocess_bwd_kernel<<<div_up(p.P, 256), 256, 0, s>>>(p);
+}
+
+}  // namespace gsr
