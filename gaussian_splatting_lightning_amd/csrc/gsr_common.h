@@ -48,11 +48,21 @@ constexpr int SCAN_MAX_BLOCKS = 1024 * 16;  // single-block scan of block sums
 
 inline uint32_t div_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
+constexpr int RS_MAX_PASSES = 4;
+// onesweep control block: [0, 4) pass tile counters, [4] error flag, [8, 8 + 4 * 256) digit histograms of
+// every pass; followed by the look-back status words (RS_MAX_PASSES x nblocks x RS_BINS).  One memset
+// clears control + status before a sort.
+constexpr int RS_CTRL_COUNTER = 0, RS_CTRL_ERR = 4, RS_CTRL_HIST = 8;
+constexpr int RS_CTRL_WORDS = RS_CTRL_HIST + RS_MAX_PASSES * RS_BINS;
+constexpr uint32_t RS_ONESWEEP_MAX_N = (1u << 30) - 1;  // 30-bit counts in the look-back words
+
 struct SortScratch {
     uint32_t *k[2];
     uint32_t *v[2];
-    uint32_t *counts;    // RS_BINS * nblocks
+    uint32_t *counts;    // RS_BINS * nblocks (multi-kernel path)
     uint32_t *scan_tmp;  // block sums for scanning counts
+    uint32_t *ctrl;      // RS_CTRL_WORDS, then the look-back status words (onesweep path)
+    uint32_t *status;
 };
 
 inline void carve_sort(Carver &c, SortScratch &s, uint32_t n, bool need_v0) {
@@ -63,6 +73,8 @@ inline void carve_sort(Carver &c, SortScratch &s, uint32_t n, bool need_v0) {
     uint32_t nb = div_up(n ? n : 1, RS_TILE);
     s.counts = c.take<uint32_t>((size_t)RS_BINS * nb + 1);
     s.scan_tmp = c.take<uint32_t>(div_up((size_t)RS_BINS * nb + 1, SCAN_TILE) + 1);
+    s.ctrl = c.take<uint32_t>(RS_CTRL_WORDS + (size_t)RS_MAX_PASSES * nb * RS_BINS);
+    s.status = s.ctrl + RS_CTRL_WORDS;
 }
 
 struct GeomState {

@@ -245,10 +245,211 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restr
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// onesweep radix sort: one histogram pass over the keys for every digit, then ONE kernel per digit pass
+// whose blocks obtain their global digit offsets by decoupled look-back (each block publishes its digit
+// counts, then its inclusive prefix; a block only waits on blocks that started before it, since block
+// ids come from an atomic ticket).  3 + passes launches instead of 5 per pass.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t LB_AGG = 1u << 30, LB_INC = 2u << 30, LB_MASK = (1u << 30) - 1;
+constexpr uint32_t LB_SPIN_LIMIT = 1u << 24;  // safety net: a broken chain raises an error, never hangs
+
+__device__ __forceinline__ uint32_t lb_load(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Digit histograms of every pass in one read of the keys.  Keys that share a digit inside a wave are
+// aggregated by ballot (8 ballots per digit, one LDS add per distinct digit), so skewed digits -- the top
+// byte of depth keys is nearly constant -- cause no atomic serialisation.
+__global__ __launch_bounds__(256) void rs_multi_hist_kernel(const uint32_t *__restrict__ keys, uint32_t n,
+                                                            int passes, uint32_t *__restrict__ ctrl) {
+    __shared__ uint32_t h[RS_MAX_PASSES][RS_BINS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    for (int i = tid; i < RS_MAX_PASSES * RS_BINS; i += 256) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const uint64_t lt = lanemask_lt(lane);
+    const uint32_t stride = gridDim.x * 256;
+    for (uint32_t base = blockIdx.x * 256; base < n; base += stride) {  // uniform trip count per wave
+        const uint32_t j = base + tid;
+        const bool valid = j < n;
+        const uint32_t k = valid ? keys[j] : 0u;
+        for (int p = 0; p < passes; p++) {
+            const uint32_t d = (k >> (8 * p)) & 255u;
+            uint64_t peers = __ballot(valid);
+#pragma unroll
+            for (int bit = 0; bit < 8; bit++) {
+                const bool set = (d >> bit) & 1u;
+                const uint64_t m = __ballot(set);
+                peers &= set ? m : ~m;
+            }
+            if (valid && (peers & lt) == 0) atomicAdd(&h[p][d], (uint32_t)__popcll(peers));
+        }
+    }
+    __syncthreads();
+    for (int p = 0; p < passes; p++) {
+        const uint32_t c = h[p][tid];
+        if (c) atomicAdd(&ctrl[RS_CTRL_HIST + p * RS_BINS + tid], c);
+    }
+}
+
+// exclusive scan of every pass's 256 digit counts, in place
+__global__ __launch_bounds__(256) void rs_hist_scan_kernel(uint32_t *__restrict__ ctrl, int passes) {
+    __shared__ uint32_t s_w[4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int p = 0; p < passes; p++) {
+        uint32_t *h = ctrl + RS_CTRL_HIST + p * RS_BINS;
+        const uint32_t v = h[tid];
+        const uint32_t inc = wave_inclusive_scan(v, lane);
+        if (lane == 63) s_w[w] = inc;
+        __syncthreads();
+        uint32_t off = 0;
+        for (int i = 0; i < w; i++) off += s_w[i];
+        h[tid] = off + inc - v;
+        __syncthreads();
+    }
+}
+
+template <bool IOTA_IN>
+__global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__restrict__ keys_in,
+                                                          const uint32_t *__restrict__ vals_in, uint32_t n,
+                                                          int pass, uint32_t *__restrict__ ctrl,
+                                                          uint32_t *__restrict__ status,
+                                                          uint32_t *__restrict__ keys_out,
+                                                          uint32_t *__restrict__ vals_out) {
+    __shared__ uint32_t s_cnt[4][RS_BINS];  // per-wave running digit counts, then per-wave bases
+    __shared__ uint32_t s_dstart[RS_BINS];  // block-local start of each digit's run
+    __shared__ uint32_t s_gbase[RS_BINS];   // global start of this block's run of each digit
+    __shared__ uint32_t s_wsum[4];
+    __shared__ uint32_t s_bid;
+    __shared__ uint32_t s_keys[RS_TILE];
+    __shared__ uint32_t s_vals[RS_TILE];
+
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int shift = 8 * pass;
+    if (tid == 0) s_bid = atomicAdd(&ctrl[RS_CTRL_COUNTER + pass], 1u);
+    for (int i = tid; i < 4 * RS_BINS; i += 256) (&s_cnt[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t bid = s_bid;
+    const uint32_t blk = bid * RS_TILE;
+
+    uint32_t key[RS_ITEMS], val[RS_ITEMS], rank[RS_ITEMS];
+    const uint64_t lt = lanemask_lt(lane);
+#pragma unroll
+    for (int it = 0; it < RS_ITEMS; it++) {
+        const uint32_t j = blk + w * (RS_TILE / 4) + it * 64 + lane;
+        const bool valid = j < n;
+        const uint32_t k = valid ? keys_in[j] : 0u;
+        const uint32_t v = IOTA_IN ? j : (valid ? vals_in[j] : 0u);
+        const uint32_t d = (k >> shift) & 255u;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < 8; bit++) {
+            const bool set = (d >> bit) & 1u;
+            const uint64_t m = __ballot(set);
+            peers &= set ? m : ~m;
+        }
+        uint32_t r = 0;
+        if (valid) {
+            const uint32_t before = s_cnt[w][d];
+            const uint64_t lower = peers & lt;
+            r = before + (uint32_t)__popcll(lower);
+            if (lower == 0) s_cnt[w][d] = before + (uint32_t)__popcll(peers);
+        }
+        key[it] = k;
+        val[it] = v;
+        rank[it] = r;
+    }
+    __syncthreads();
+    {
+        const int d = tid;
+        const uint32_t c0 = s_cnt[0][d], c1 = s_cnt[1][d], c2 = s_cnt[2][d], c3 = s_cnt[3][d];
+        const uint32_t tot = c0 + c1 + c2 + c3;
+        uint32_t *st = status + (size_t)bid * RS_BINS + d;
+        lb_store(st, (bid == 0 ? LB_INC : LB_AGG) | tot);  // publish early: successors can proceed
+        s_cnt[0][d] = 0;
+        s_cnt[1][d] = c0;
+        s_cnt[2][d] = c0 + c1;
+        s_cnt[3][d] = c0 + c1 + c2;
+        const uint32_t inc = wave_inclusive_scan(tot, lane);
+        if (lane == 63) s_wsum[w] = inc;
+        uint32_t excl = 0;
+        if (bid > 0) {
+            uint32_t look = bid - 1, spins = 0;
+            while (true) {
+                const uint32_t v = lb_load(status + (size_t)look * RS_BINS + d);
+                const uint32_t f = v & ~LB_MASK;
+                if (f == 0) {
+                    if (++spins > LB_SPIN_LIMIT) {
+                        atomicOr(&ctrl[RS_CTRL_ERR], 1u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                excl += v & LB_MASK;
+                if (f == LB_INC || look == 0) break;
+                --look;
+            }
+            lb_store(st, LB_INC | (excl + tot));
+        }
+        s_gbase[d] = ctrl[RS_CTRL_HIST + pass * RS_BINS + d] + excl;
+        __syncthreads();
+        uint32_t woff = 0;
+        for (int i = 0; i < w; i++) woff += s_wsum[i];
+        s_dstart[d] = woff + inc - tot;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < RS_ITEMS; it++) {
+        const uint32_t j = blk + w * (RS_TILE / 4) + it * 64 + lane;
+        if (j < n) {
+            const uint32_t d = (key[it] >> shift) & 255u;
+            const uint32_t pos = s_dstart[d] + s_cnt[w][d] + rank[it];
+            s_keys[pos] = key[it];
+            s_vals[pos] = val[it];
+        }
+    }
+    __syncthreads();
+    const uint32_t cnt_blk = min((uint32_t)RS_TILE, n - blk);
+    for (uint32_t i = tid; i < cnt_blk; i += 256) {
+        const uint32_t k = s_keys[i], v = s_vals[i];
+        const uint32_t d = (k >> shift) & 255u;
+        const uint32_t gpos = s_gbase[d] + (i - s_dstart[d]);
+        keys_out[gpos] = k;
+        vals_out[gpos] = v;
+    }
+}
+
+static void launch_radix_sort_onesweep(hipStream_t s, SortScratch &sc, uint32_t n, int passes) {
+    const uint32_t nb = div_up(n, RS_TILE);
+    (void)hipMemsetAsync(sc.ctrl, 0, sizeof(uint32_t) * (RS_CTRL_WORDS + (size_t)passes * nb * RS_BINS), s);
+    const uint32_t hb = min(div_up(n, 256u * 8u), 2048u);
+    rs_multi_hist_kernel<<<max(hb, 1u), 256, 0, s>>>(sc.k[0], n, passes, sc.ctrl);
+    rs_hist_scan_kernel<<<1, 256, 0, s>>>(sc.ctrl, passes);
+    for (int p = 0; p < passes; p++) {
+        const int in = p & 1, out = (p + 1) & 1;
+        uint32_t *st = sc.status + (size_t)p * nb * RS_BINS;
+        if (p == 0)
+            rs_onesweep_kernel<true><<<nb, 256, 0, s>>>(sc.k[in], nullptr, n, p, sc.ctrl, st, sc.k[out], sc.v[out]);
+        else
+            rs_onesweep_kernel<false><<<nb, 256, 0, s>>>(sc.k[in], sc.v[in], n, p, sc.ctrl, st, sc.k[out],
+                                                         sc.v[out]);
+    }
+}
+
 void launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits) {
     if (n == 0) return;
     const uint32_t nb = div_up(n, RS_TILE);
     const int passes = radix_passes(nbits);
+    // onesweep knob: bit 0 = depth-size sorts (nbits == 32), bit 1 = tile sorts
+    const int os = tuning("onesweep", 3);
+    if (n <= RS_ONESWEEP_MAX_N && passes <= RS_MAX_PASSES && (os & (nbits == 32 ? 1 : 2))) {
+        launch_radix_sort_onesweep(s, sc, n, passes);
+        return;
+    }
     for (int p = 0; p < passes; p++) {
         const int shift = 8 * p, in = p & 1, out = (p + 1) & 1;
         rs_hist_kernel<<<nb, 256, 0, s>>>(sc.k[in], n, shift, sc.counts, nb);
