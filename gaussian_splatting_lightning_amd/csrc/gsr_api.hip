@@ -361,6 +361,9 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     char *scratch = alloc(alloc_ctx, GSR_BUF_BWD_SCRATCH, bwd_scratch_bytes(R, nbig));
     if (!scratch) return fail(GSR_ERR_ALLOC, "backward scratch allocation failed");
     float *rows = reinterpret_cast<float *>(scratch);
+    // Gaussian-major gradient rows: render_bwd scatters its 48-B rows to the instances' expansion indices so
+    // the per-Gaussian gather in preprocess_bwd reads each Gaussian's rows contiguously.
+    const int rows_by_u = tuning("rows_by_u", 1);
     float *bigsum = bwd_bigsum_ptr(scratch, R);
 
     if (R > 0) {
@@ -371,10 +374,12 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
         rp.rec_a = g.rec_a; rp.rec_b = g.rec_b; rp.rec_c = g.rec_c;
         rp.bg = a->background; rp.final_T = im.final_T; rp.dL_dpix = a->dL_dpix; rp.dL_dinvdepth = a->dL_dinvdepth;
         rp.rows = rows;
+        rp.sorted_u = b.sorted_u;
+        rp.rows_by_u = rows_by_u;
         GSR_STAGE(ST_RENDER_BWD, dbg, launch_render_bwd(stream, rp));
         BigReduceParams bp;
         bp.big_list = g.big_list; bp.inst_start = g.inst_start; bp.tiles = g.tiles;
-        bp.inv = b.inv; bp.rows = rows; bp.bigsum = bigsum;
+        bp.inv = b.inv; bp.rows = rows; bp.bigsum = bigsum; bp.rows_by_u = rows_by_u;
         GSR_STAGE(ST_BIG_REDUCE, dbg, launch_big_reduce(stream, bp, nbig));
     }
     PreprocessBwdParams pp;
@@ -389,6 +394,7 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     pp.cov3D_precomp = a->cov3D_precomp; pp.shs = (a->colors_precomp ? nullptr : a->shs);
     pp.view = a->viewmatrix; pp.proj = a->projmatrix; pp.campos = a->campos;
     pp.radii = a->radii; pp.tiles = g.tiles; pp.inst_start = g.inst_start; pp.inv = b.inv; pp.clamped = g.clamped;
+    pp.rows_by_u = rows_by_u;
     pp.big_slot = g.big_slot; pp.bigsum = bigsum;
     pp.rows = rows;
     pp.sh_vec16 = pp.shs && a->M == 16 && (((uintptr_t)pp.shs | (uintptr_t)a->dL_dsh) & 15) == 0 &&

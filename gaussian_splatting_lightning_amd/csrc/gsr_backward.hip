@@ -85,7 +85,7 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_bwd_v3_kernel(Rend
     const uint32_t loaded = p.tile_loaded[tile];
     for (uint32_t s = range.x + tl + lane; s < range.x + loaded; s += 64) {
         const float z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        store_row(p.rows, s, z);
+        store_row(p.rows, p.rows_by_u ? p.sorted_u[s] : s, z);
     }
     if (tl == 0) return;
 
@@ -93,7 +93,7 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_bwd_v3_kernel(Rend
     const size_t HW = (size_t)p.W * p.H;
     float T[PIX_PER_LANE], nbg[PIX_PER_LANE], dp0[PIX_PER_LANE], dp1[PIX_PER_LANE], dp2[PIX_PER_LANE];
     float dinv[PIX_PER_LANE], ar0[PIX_PER_LANE], ar1[PIX_PER_LANE], ar2[PIX_PER_LANE], ainv[PIX_PER_LANE];
-    float pfy[PIX_PER_LANE];
+    const float pfy0 = (float)py0;
     uint32_t lastc[PIX_PER_LANE];
 #pragma unroll
     for (int k = 0; k < PIX_PER_LANE; k++) {
@@ -102,7 +102,6 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_bwd_v3_kernel(Rend
         const size_t pid = inside ? (size_t)py * p.W + px : 0;
         const float Tf = inside ? p.final_T[pid] : 0.f;
         T[k] = Tf;
-        pfy[k] = (float)py;
         lastc[k] = inside ? p.n_contrib[pid] : 0u;
         dp0[k] = inside ? p.dL_dpix[pid] : 0.f;
         dp1[k] = inside ? p.dL_dpix[HW + pid] : 0.f;
@@ -116,8 +115,11 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_bwd_v3_kernel(Rend
     for (int bend = (int)tl; bend > 0; bend -= BWD_BATCH) {
         const int cnt = min(BWD_BATCH, bend);
         float4 my_a = make_float4(0, 0, 0, 0), my_b = my_a;
+        uint32_t my_row = 0;
         if (lane < cnt) {
-            const uint32_t gid = p.point_list[range.x + (uint32_t)(bend - 1 - lane)];
+            const uint32_t s_me = range.x + (uint32_t)(bend - 1 - lane);
+            my_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
+            const uint32_t gid = p.point_list[s_me];
             my_a = p.rec_a[gid];
             my_b = p.rec_b[gid];
             s_a[w][lane] = stage_rec_a(my_a);
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_bwd_v3_kernel(Rend
             const float4 a = s_a[w][j];  // x, y, A, B
             const float4 b = s_b[w][j];  // C, o, r, g
             const float2 c = s_c[w][j];  // b, 1/depth
-            const float dx = a.x - pfx;
+            const float dx = a.x - pfx, dy0 = a.y - pfy0;
             const float P0 = (a.z * dx) * dx, L = a.w * dx;
             // per lane: Q0 = sum q, Q1 = sum q dy, Q2 = sum q dy^2 over its pixels (dx is shared), colour weights
             float Q0 = 0.f, Q1 = 0.f, Q2 = 0.f, w0 = 0.f, w1 = 0.f, w2 = 0.f, w3 = 0.f;
@@ -138,7 +140,7 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_bwd_v3_kernel(Rend
 #pragma unroll
             for (int k = 0; k < PIX_PER_LANE; k++) {
                 if (idx >= lastc[k]) continue;
-                const float dy = a.y - pfy[k];
+                const float dy = dy0 - (float)(4 * k);  // = a.y - (py0 + 4k), rounded as in the forward
                 const float power2 = power2_at(b.x, dy, P0, L);
                 if (power2 > 0.0f) continue;
                 const float G = __builtin_amdgcn_exp2f(power2);
@@ -208,7 +210,7 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_bwd_v3_kernel(Rend
             row[7] = u1.w;
             row[8] = u2.x;
             row[9] = u2.y;
-            store_row(p.rows, range.x + (uint32_t)(bend - 1 - lane), row);
+            store_row(p.rows, my_row, row);
         }
         wave_lds_sync();
     }
@@ -216,7 +218,7 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_bwd_v3_kernel(Rend
 
 void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
     if (p.num_tiles <= 0) return;
-    const int minw = tuning("bwd_minwaves", 4), wpb = tuning("bwd_wpb", 4);
+    const int minw = tuning("bwd_minwaves", 5), wpb = tuning("bwd_wpb", 4);
     const dim3 block(64 * (wpb == 1 ? 1 : 4)), grid(wpb == 1 ? p.num_tiles : div_up(p.num_tiles, 4));
 #define GSR_BWD_LAUNCH(INV, MW)                                                                        \
     do {                                                                                               \
@@ -224,11 +226,11 @@ void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
         else render_bwd_v3_kernel<INV, MW, 4><<<grid, block, 0, s>>>(p);                               \
     } while (0)
     if (p.dL_dinvdepth) {
-        if (minw >= 4) GSR_BWD_LAUNCH(true, 4);
-        else GSR_BWD_LAUNCH(true, 1);
+        if (minw >= 5) GSR_BWD_LAUNCH(true, 5);
+        else GSR_BWD_LAUNCH(true, 4);
     } else {
-        if (minw >= 4) GSR_BWD_LAUNCH(false, 4);
-        else GSR_BWD_LAUNCH(false, 1);
+        if (minw >= 5) GSR_BWD_LAUNCH(false, 5);
+        else GSR_BWD_LAUNCH(false, 4);
     }
 #undef GSR_BWD_LAUNCH
 }
@@ -246,7 +248,7 @@ __global__ __launch_bounds__(256) void big_reduce_kernel(BigReduceParams p) {
     float acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (uint32_t k = threadIdx.x; k < cnt; k += 256) {
         const uint32_t sidx = p.inv[start + k];
-        if (sidx != INV_NONE) add_row(p.rows, sidx, acc);
+        if (sidx != INV_NONE) add_row(p.rows, p.rows_by_u ? start + k : sidx, acc);
     }
 #pragma unroll
     for (int v = 0; v < 10; v++) {

@@ -322,11 +322,11 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_fwd_v3_kernel(Rend
             }
             contributor++;
             bool still = false;
-            const float dx = a.x - pfx;
+            const float dx = a.x - pfx, dy0 = a.y - pfy[0];
             const float P0 = (a.z * dx) * dx, L = a.w * dx;
 #pragma unroll
             for (int k = 0; k < PIX_PER_LANE; k++) {
-                const float power2 = power2_at(b.x, a.y - pfy[k], P0, L);
+                const float power2 = power2_at(b.x, dy0 - (float)(4 * k), P0, L);  // dy as in the backward
                 const float alpha = fminf(0.99f, b.y * __builtin_amdgcn_exp2f(power2));
                 const bool ok = active[k] && !(power2 > 0.0f) && !(alpha < 1.0f / 255.0f);
                 const float test_T = T[k] * (1 - alpha);

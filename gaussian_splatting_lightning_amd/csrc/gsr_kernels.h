@@ -65,15 +65,18 @@ struct RenderBwdParams {
     int W, H, gx, gy, num_tiles;
     const uint2 *ranges;
     const uint32_t *point_list, *n_contrib, *tile_last, *tile_loaded;
+    const uint32_t *sorted_u;  // sorted position -> expansion index u (rows_by_u)
     const float4 *rec_a, *rec_b;
     const float2 *rec_c;
     const float *bg, *final_T, *dL_dpix, *dL_dinvdepth;
-    float *rows;  // R x GRAD_ROW
+    float *rows;    // R x GRAD_ROW
+    int rows_by_u;  // 1: row of an instance at its expansion index u (Gaussian-major), 0: at its sorted position
 };
 void launch_render_bwd(hipStream_t s, const RenderBwdParams &p);
 
 struct BigReduceParams {
     const uint32_t *big_list, *inst_start, *tiles, *inv;
+    int rows_by_u;
     const float *rows;
     float *bigsum;  // nbig x GRAD_ROW
 };
@@ -88,6 +91,7 @@ struct PreprocessBwdParams {
     const float *view, *proj, *campos;
     const int *radii;
     const uint32_t *tiles, *inst_start, *inv, *big_slot;
+    int rows_by_u;
     const uint8_t *clamped;
     const float *rows, *bigsum;
     float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales, *dL_drot;

@@ -70,7 +70,8 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     if (sidx[j] != INV_NONE) {
-                        const float4 *src = reinterpret_cast<const float4 *>(p.rows + (size_t)sidx[j] * GRAD_ROW);
+                        const size_t ri = p.rows_by_u ? (size_t)(start + k0 + j) : (size_t)sidx[j];
+                        const float4 *src = reinterpret_cast<const float4 *>(p.rows + ri * GRAD_ROW);
                         ra[j] = src[0];
                         rb[j] = src[1];
                         rc[j] = src[2];

@@ -183,10 +183,11 @@ def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_
         return t
 
     dmeans2D = dst("means2D", P, 3)
-    dcolors = dst("colors", P, 3)
+    # dL/dcolors and dL/dcov3D are outputs only for precomputed colours / covariances (or when asked for)
+    dcolors = dst("colors", P, 3) if (st.colors_precomp is not None or "colors" in out) else None
     dopac = dst("opacities", P, 1)
     dmeans3D = dst("means3D", P, 3)
-    dcov = dst("cov3D", P, 6)
+    dcov = dst("cov3D", P, 6) if (st.cov3D_precomp is not None or "cov3D" in out) else None
     dsh = None if compact_sh else dst("shs", P, max(M, 0), 3)
     dcsh = dst("colors_sh", P, 3) if (compact_sh or "colors_sh" in out) else None
     dscales = dst("scales", P, 3)
@@ -201,8 +202,8 @@ def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_
         dL_dpix=grad_out_color.data_ptr(), dL_dinvdepth=_ptr(grad_out_depth), shs=_ptr(st.shs),
         radii=_ptr(st.radii), geom_buffer=_ptr(st.geom_buffer), binning_buffer=_ptr(st.binning_buffer),
         image_buffer=_ptr(st.image_buffer), antialiasing=int(bool(rs.antialiasing)), debug=int(bool(rs.debug)),
-        dL_dmeans2D=dmeans2D.data_ptr(), dL_dcolors=dcolors.data_ptr(), dL_dopacity=dopac.data_ptr(),
-        dL_dmeans3D=dmeans3D.data_ptr(), dL_dcov3D=dcov.data_ptr(), dL_dsh=_ptr(dsh),
+        dL_dmeans2D=dmeans2D.data_ptr(), dL_dcolors=_ptr(dcolors), dL_dopacity=dopac.data_ptr(),
+        dL_dmeans3D=dmeans3D.data_ptr(), dL_dcov3D=_ptr(dcov), dL_dsh=_ptr(dsh),
         dL_dscales=dscales.data_ptr(), dL_drotations=drot.data_ptr(), dL_dcolors_sh=_ptr(dcsh))
     rc = lib.gsr_backward(ctypes.byref(a), bufs.callback, None, _stream_handle(device))
     _native.check(rc, "rasterize_gaussians_backward")

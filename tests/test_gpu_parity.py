@@ -324,7 +324,7 @@ def test_compact_sh_views_matches_dense(gpu_device):
         gd = backward_raw(st, rs, dc, di)
         gc = backward_raw(st, rs, dc, di, compact_sh=True)
         assert gc["shs"] is None
-        for k in ("means3D", "means2D", "opacities", "scales", "rotations", "colors"):
+        for k in ("means3D", "means2D", "opacities", "scales", "rotations"):
             assert torch.equal(gd[k], gc[k]), k
         dense_sum = gd["shs"].clone() if dense_sum is None else dense_sum + gd["shs"]
         factors.append(gc["colors_sh"])
