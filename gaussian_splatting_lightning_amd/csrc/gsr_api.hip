@@ -154,10 +154,16 @@ struct StageScope {
         if (rc_ != GSR_OK) return rc_;                  \
     } while (0)
 
+hipEvent_t readback_event() {
+    thread_local hipEvent_t e = nullptr;
+    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+    return e;
+}
+
 uint32_t *pinned_words() {
     thread_local uint32_t *p = nullptr;
     if (!p) {
-        if (hipHostMalloc((void **)&p, 256, hipHostMallocDefault) != hipSuccess) p = nullptr;
+        if (hipHostMalloc((void **)&p, 4096, hipHostMallocDefault) != hipSuccess) p = nullptr;
     }
     return p;
 }
@@ -282,21 +288,29 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     pp.radii = a->radii;
     pp.g = g;
     GSR_STAGE(ST_PREPROCESS, dbg, launch_preprocess(stream, pp));
+    // The instance total only needs the per-Gaussian tile counts, so it is read back right after the
+    // preprocess: the host waits on that copy while the GPU runs the depth sort and the ordered scan, and
+    // the binning launches are queued before the GPU drains (no idle gap at the only host sync).
+    uint32_t *hw = pinned_words();
+    hipEvent_t rb_ev = readback_event();
+    if (!hw || !rb_ev) return fail(GSR_ERR_HIP, "pinned host buffer / event allocation failed");
+    GSR_HIP(hipMemcpyAsync(hw, g.counters, CNT_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    GSR_HIP(hipEventRecord(rb_ev, stream));
     GSR_STAGE(ST_DEPTH_SORT, dbg, launch_radix_sort(stream, g.sort, (uint32_t)P, 32));
     GSR_STAGE(ST_SCAN, dbg,
               launch_exclusive_scan(stream, g.tiles, g.order, (uint32_t)P, g.inst_off, g.scan_tmp,
                                     g.counters + CNT_OVERFLOW));
-    uint32_t *hw = pinned_words();
-    if (!hw) return fail(GSR_ERR_HIP, "pinned host buffer allocation failed");
-    GSR_STAGE(ST_READBACK, dbg, {
-        GSR_HIP(hipMemcpyAsync(hw, g.inst_off + P, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-        GSR_HIP(hipMemcpyAsync(hw + 1, g.counters, CNT_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-        GSR_HIP(hipStreamSynchronize(stream));
-    });
-    if (hw[1 + CNT_OVERFLOW]) return fail(GSR_ERR_OVERFLOW, "more than 2^32-1 tile instances");
-    const uint32_t R = hw[0];
+    GSR_STAGE(ST_READBACK, dbg, GSR_HIP(hipEventSynchronize(rb_ev)));
+    uint64_t total64 = 0;
+    for (int k = 0; k < CNT_NPART; k++) {
+        uint64_t part;
+        memcpy(&part, hw + CNT_PARTIALS + 2 * k, sizeof(part));
+        total64 += part;
+    }
+    if (total64 > 0xffffffffull) return fail(GSR_ERR_OVERFLOW, "more than 2^32-1 tile instances");
+    const uint32_t R = (uint32_t)total64;
     *num_rendered = R;
-    const uint32_t nbig = hw[1 + CNT_BIG];
+    const uint32_t nbig = hw[CNT_BIG];
     a->num_big_out = nbig;
 
     BinningState b;

@@ -21,7 +21,9 @@ constexpr uint32_t BIG_GAUSSIAN_TILES = 64;   // per-Gaussian gradient rows redu
 constexpr int GRAD_ROW = 12;                   // floats per instance gradient row (10 used, 48 B)
 
 // counters block at the head of the geometry buffer (zeroed every forward)
-enum Counter : int { CNT_BIG = 0, CNT_TOTAL = 1, CNT_OVERFLOW = 2, CNT_WORDS = 16 };
+// counters: [CNT_BIG] big-Gaussian count, [CNT_OVERFLOW] scan overflow flag, then CNT_NPART 64-bit partial
+// sums of the instance total (spread over addresses so the per-block atomics do not serialise)
+enum Counter : int { CNT_BIG = 0, CNT_OVERFLOW = 2, CNT_PARTIALS = 16, CNT_NPART = 64, CNT_WORDS = 16 + 2 * 64 };
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }
 

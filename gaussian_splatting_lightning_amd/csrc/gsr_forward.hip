@@ -14,10 +14,9 @@ namespace gsr {
 // preprocess: one thread per Gaussian.  Culls, projects, builds the conic and radius, evaluates SH,
 // and emits the packed render records plus the depth-sort key and tile count.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void preprocess_kernel(PreprocessParams p) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= p.P) return;
-    GeomState &g = p.g;
+// Returns the number of tiles the Gaussian is binned into (0 if culled).
+__device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &p, const int i) {
+    const GeomState &g = p.g;
     p.radii[i] = 0;
     g.tiles[i] = 0;
     g.depth_key[i] = 0xffffffffu;
@@ -26,7 +25,7 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessParams p) {
     const Mat4 view = load_mat4(p.view);
     const float3 mean = load_f3(p.means3D, i);
     const float3 pv = xform3(mean, view);
-    if (!(pv.z > 0.2f)) return;  // in_frustum (camera_tools.py:5-8)
+    if (!(pv.z > 0.2f)) return 0u;  // in_frustum (camera_tools.py:5-8)
 
     const Mat4 proj = load_mat4(p.proj);
     const float4 ph = xform4(mean, proj);
@@ -53,7 +52,7 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessParams p) {
     const float det = cxx * cyy - cxy * cxy;
     float hscale = 1.0f;
     if (p.antialiasing) hscale = sqrtf(fmaxf(0.000025f, det_cov / det));
-    if (det == 0.0f) return;
+    if (det == 0.0f) return 0u;
     const float det_inv = 1.f / det;
     const float conic_x = cyy * det_inv, conic_y = -cxy * det_inv, conic_z = cxx * det_inv;
     const float mid = 0.5f * (cxx + cyy);
@@ -64,7 +63,7 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessParams p) {
     int2 rmin, rmax;
     get_rect(pimg, (int)radius, p.gx, p.gy, rmin, rmax);
     const uint32_t area = (uint32_t)((rmax.x - rmin.x) * (rmax.y - rmin.y));
-    if (area == 0) return;
+    if (area == 0) return 0u;
 
     float3 rgb;
     uint8_t clamp_bits = 0;
@@ -108,6 +107,25 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessParams p) {
         const uint32_t slot = atomicAdd(&g.counters[CNT_BIG], 1u);
         g.big_list[slot] = (uint32_t)i;
         g.big_slot[i] = slot;
+    }
+    return kept;
+}
+
+__global__ __launch_bounds__(256) void preprocess_kernel(PreprocessParams p) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    __shared__ uint32_t s_w[4];
+    uint32_t kept = i < p.P ? preprocess_gaussian(p, i) : 0u;
+    // instance total for the early host readback (gsr_forward): block sum, one 64-bit atomic per block into
+    // one of CNT_NPART partial counters
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) kept += (uint32_t)__shfl_xor((int)kept, o);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = kept;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long tot = (unsigned long long)s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        if (tot)
+            atomicAdd(reinterpret_cast<unsigned long long *>(p.g.counters + CNT_PARTIALS) + (blockIdx.x % CNT_NPART),
+                      tot);
     }
 }
 

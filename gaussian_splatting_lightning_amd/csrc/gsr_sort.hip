@@ -445,7 +445,7 @@ void launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits) {
     const uint32_t nb = div_up(n, RS_TILE);
     const int passes = radix_passes(nbits);
     // onesweep knob: bit 0 = depth-size sorts (nbits == 32), bit 1 = tile sorts
-    const int os = tuning("onesweep", 3);
+    const int os = tuning("onesweep", 1);
     if (n <= RS_ONESWEEP_MAX_N && passes <= RS_MAX_PASSES && (os & (nbits == 32 ? 1 : 2))) {
         launch_radix_sort_onesweep(s, sc, n, passes);
         return;
