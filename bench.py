@@ -113,7 +113,7 @@ def main():
         color, radii, invd, st = forward_raw(sc.means3D, sc.shs, None, sc.opacities, sc.scales, sc.rotations, None,
                                              settings)
         backward_raw(st, settings, dcolor, dinv, out=red.backward_out(), compact_sh=red.compact)
-        red.record_view(red.means2D, radii)
+        red.record_view(red.means2D, radii, stats_written=True)
         red.reduce(sc.means3D, c.campos)
         return st
 

@@ -40,6 +40,7 @@ class BackwardArgs(ctypes.Structure):
         ("dL_dopacity", _fp), ("dL_dmeans3D", _fp), ("dL_dcov3D", _fp), ("dL_dsh", _fp), ("dL_dscales", _fp),
         ("dL_drotations", _fp),
         ("dL_dcolors_sh", _fp),
+        ("densify_stats", _fp),
     ]
 
 

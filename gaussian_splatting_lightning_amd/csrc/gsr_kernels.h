@@ -96,6 +96,7 @@ struct PreprocessBwdParams {
     const float *rows, *bigsum;
     float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales, *dL_drot;
     float *dL_dcolors_sh;  // clamp-masked colour gradient (may be null)
+    float *densify_stats;  // (P,2) |dL/dmeans2D[:2]|, radii > 0 (may be null)
 };
 void launch_preprocess_bwd(hipStream_t s, const PreprocessBwdParams &p);
 

@@ -93,6 +93,9 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         p.dL_dmeans2D[3 * i + 1] = gs[1];
         p.dL_dmeans2D[3 * i + 2] = 0.f;
     }
+    if (p.densify_stats)  // torch.linalg.vector_norm(grad[:, :2]) and the visibility count of this view
+        *reinterpret_cast<float2 *>(p.densify_stats + 2 * i) =
+            make_float2(sqrtf(gs[0] * gs[0] + gs[1] * gs[1]), vis ? 1.f : 0.f);
     if (p.dL_dcolors) {
         p.dL_dcolors[3 * i] = gs[6];
         p.dL_dcolors[3 * i + 1] = gs[7];

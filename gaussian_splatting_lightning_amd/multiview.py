@@ -41,7 +41,7 @@ class ViewGradReducer:
 
         st = forward_raw(...)
         backward_raw(st, settings, dcolor, dinv, out=red.backward_out(), compact_sh=red.compact)
-        red.record_view(red.means2D, radii)
+        red.record_view(red.means2D, radii, stats_written=True)  # stats come from the backward kernel
         red.reduce(means3D, campos)          # collectives + SH expansion
         red.grads["shs"], red.grads["means3D"], red.stats, red.radii_max, ...
     """
@@ -84,19 +84,25 @@ class ViewGradReducer:
     # ---- per view ----
     def backward_out(self) -> Dict[str, torch.Tensor]:
         out = dict(means3D=self.views["means3D"], scales=self.views["scales"], rotations=self.views["rotations"],
-                   opacities=self.views["opacities"], means2D=self.means2D)
+                   opacities=self.views["opacities"], means2D=self.means2D, densify_stats=self.views["stats"])
         if self.compact:
             out["colors_sh"] = self.colors_sh
         else:
             out["shs"] = self.shs
         return out
 
-    def record_view(self, dmeans2D: torch.Tensor, radii: torch.Tensor) -> None:
-        """Densification statistics of this rank's view (gaussian_model.py:175-181), before the exchange."""
-        st = self.views["stats"]
-        torch.linalg.vector_norm(dmeans2D[:, :2], dim=1, out=st[:, 0])
-        st[:, 1].copy_(radii > 0)
-        self.radii_max.copy_(radii)
+    def record_view(self, dmeans2D: torch.Tensor, radii: torch.Tensor, stats_written: bool = False) -> None:
+        """Densification statistics of this rank's view (gaussian_model.py:175-181), before the exchange.
+        backward_raw(out=backward_out()) already wrote them (gsr_backward's densify_stats) unless
+        stats_written is False and they are formed here from dmeans2D / radii."""
+        if not stats_written:
+            st = self.views["stats"]
+            torch.linalg.vector_norm(dmeans2D[:, :2], dim=1, out=st[:, 0])
+            st[:, 1].copy_(radii > 0)
+        if self.world > 1:
+            self.radii_max.copy_(radii)
+        else:
+            self.radii_max = radii
 
     # ---- exchange ----
     def reduce(self, means3D: torch.Tensor, campos: torch.Tensor) -> None:

@@ -156,7 +156,8 @@ def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_
     opacities, scales, rotations, cov3D_precomp); entries are None where the input was absent.
     `out` may supply preallocated contiguous float32 destinations (e.g. views into one flat buffer that is
     then all-reduced): keys means2D (P,3), colors (P,3), opacities (P,1), means3D (P,3), cov3D (P,6),
-    shs (P,M,3), scales (P,3), rotations (P,4), colors_sh (P,3).
+    shs (P,M,3), scales (P,3), rotations (P,4), colors_sh (P,3), densify_stats (P,2) (|dL/dmeans2D[:2]| and
+    radii > 0 of this view, gaussian_model.py:175-181).
     compact_sh=True skips dL/dshs and returns the clamp-masked colour gradient "colors_sh" instead -- the
     per-view factor that `sh_backward_views` expands after an all-gather (multiview.py)."""
     lib = _native.load()
@@ -190,6 +191,7 @@ def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_
     dcov = dst("cov3D", P, 6) if (st.cov3D_precomp is not None or "cov3D" in out) else None
     dsh = None if compact_sh else dst("shs", P, max(M, 0), 3)
     dcsh = dst("colors_sh", P, 3) if (compact_sh or "colors_sh" in out) else None
+    dstats = dst("densify_stats", P, 2) if "densify_stats" in out else None
     dscales = dst("scales", P, 3)
     drot = dst("rotations", P, 4)
     bufs = _Buffers(device)
@@ -204,7 +206,8 @@ def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_
         image_buffer=_ptr(st.image_buffer), antialiasing=int(bool(rs.antialiasing)), debug=int(bool(rs.debug)),
         dL_dmeans2D=dmeans2D.data_ptr(), dL_dcolors=_ptr(dcolors), dL_dopacity=dopac.data_ptr(),
         dL_dmeans3D=dmeans3D.data_ptr(), dL_dcov3D=_ptr(dcov), dL_dsh=_ptr(dsh),
-        dL_dscales=dscales.data_ptr(), dL_drotations=drot.data_ptr(), dL_dcolors_sh=_ptr(dcsh))
+        dL_dscales=dscales.data_ptr(), dL_drotations=drot.data_ptr(), dL_dcolors_sh=_ptr(dcsh),
+        densify_stats=_ptr(dstats))
     rc = lib.gsr_backward(ctypes.byref(a), bufs.callback, None, _stream_handle(device))
     _native.check(rc, "rasterize_gaussians_backward")
     return dict(

@@ -114,6 +114,9 @@ typedef struct gsr_backward_args {
      * the SH basis in dL/dsh.  With dL_dsh == NULL this is the compact per-view SH gradient that
      * gsr_sh_backward_views expands (multi-view data parallelism); NULL to skip. */
     float *dL_dcolors_sh;
+    /* (P,2) densification statistics of this view (gaussian_model.py:175-181): [i][0] = |dL/dmeans2D[i][:2]|,
+     * [i][1] = 1 if radii[i] > 0 else 0; NULL to skip. */
+    float *densify_stats;
 } gsr_backward_args;
 
 /* Replaces `_C.rasterize_gaussians_backward` (RasterizeGaussiansBackwardCUDA -> Rasterizer::backward).

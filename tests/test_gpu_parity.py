@@ -344,3 +344,19 @@ def test_compact_sh_views_matches_dense(gpu_device):
 def O_sh_views(means3D, campos, factors):
     from oracle import oracle as O
     return O.sh_backward_views(means3D.cpu().numpy(), campos.cpu().numpy(), factors.cpu().numpy(), 3, 16)
+
+
+def test_densify_stats_from_backward(gpu_device):
+    """gsr_backward's densify_stats == torch.linalg.vector_norm(dL/dmeans2D[:, :2]) and radii > 0
+    (gaussian_model.py:175-181), so the trainer's per-view statistics need no extra kernels."""
+    from gaussian_splatting_lightning_amd.rasterizer import backward_raw, forward_raw
+    inp = scene_inputs(5000, 200, 150, sh_degree=2, seed=9)
+    rs = settings_for(inp, gpu_device)
+    t = {k: torch.as_tensor(inp[k], device=gpu_device) for k in ("means3D", "opacities", "scales", "rotations", "shs")}
+    dc, di = (torch.as_tensor(a, device=gpu_device) for a in upstream(200, 150, seed=2))
+    _, radii, _, st = forward_raw(t["means3D"], t["shs"], None, t["opacities"], t["scales"], t["rotations"], None, rs)
+    stats = torch.full((5000, 2), -1.0, device=gpu_device)
+    g = backward_raw(st, rs, dc, di, out={"densify_stats": stats})
+    ref = torch.linalg.vector_norm(g["means2D"][:, :2], dim=1)
+    assert torch.allclose(stats[:, 0], ref, rtol=1e-6, atol=0)
+    assert torch.equal(stats[:, 1], (radii > 0).float())
