@@ -75,7 +75,8 @@ inline void carve_sort(Carver &c, SortScratch &s, uint32_t n, bool need_v0) {
     uint32_t nb = div_up(n ? n : 1, RS_TILE);
     s.counts = c.take<uint32_t>((size_t)RS_BINS * nb + 1);
     s.scan_tmp = c.take<uint32_t>(div_up((size_t)RS_BINS * nb + 1, SCAN_TILE) + 1);
-    s.ctrl = c.take<uint32_t>(RS_CTRL_WORDS + (size_t)RS_MAX_PASSES * nb * RS_BINS);
+    const uint32_t nb_os = div_up(n ? n : 1, RS_TILE / 2);  // onesweep tiles may be half a RS_TILE
+    s.ctrl = c.take<uint32_t>(RS_CTRL_WORDS + (size_t)RS_MAX_PASSES * nb_os * RS_BINS);
     s.status = s.ctrl + RS_CTRL_WORDS;
 }
 

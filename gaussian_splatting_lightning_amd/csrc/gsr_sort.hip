@@ -312,7 +312,7 @@ __global__ __launch_bounds__(256) void rs_hist_scan_kernel(uint32_t *__restrict_
     }
 }
 
-template <bool IOTA_IN>
+template <bool IOTA_IN, int ITEMS>
 __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__restrict__ keys_in,
                                                           const uint32_t *__restrict__ vals_in, uint32_t n,
                                                           int pass, uint32_t *__restrict__ ctrl,
@@ -324,8 +324,8 @@ __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__rest
     __shared__ uint32_t s_gbase[RS_BINS];   // global start of this block's run of each digit
     __shared__ uint32_t s_wsum[4];
     __shared__ uint32_t s_bid;
-    __shared__ uint32_t s_keys[RS_TILE];
-    __shared__ uint32_t s_vals[RS_TILE];
+    __shared__ uint32_t s_keys[ITEMS * 256];
+    __shared__ uint32_t s_vals[ITEMS * 256];
 
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int shift = 8 * pass;
@@ -333,13 +333,14 @@ __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__rest
     for (int i = tid; i < 4 * RS_BINS; i += 256) (&s_cnt[0][0])[i] = 0;
     __syncthreads();
     const uint32_t bid = s_bid;
-    const uint32_t blk = bid * RS_TILE;
+    constexpr uint32_t TILE = ITEMS * 256;
+    const uint32_t blk = bid * TILE;
 
-    uint32_t key[RS_ITEMS], val[RS_ITEMS], rank[RS_ITEMS];
+    uint32_t key[ITEMS], val[ITEMS], rank[ITEMS];
     const uint64_t lt = lanemask_lt(lane);
 #pragma unroll
-    for (int it = 0; it < RS_ITEMS; it++) {
-        const uint32_t j = blk + w * (RS_TILE / 4) + it * 64 + lane;
+    for (int it = 0; it < ITEMS; it++) {
+        const uint32_t j = blk + w * (TILE / 4) + it * 64 + lane;
         const bool valid = j < n;
         const uint32_t k = valid ? keys_in[j] : 0u;
         const uint32_t v = IOTA_IN ? j : (valid ? vals_in[j] : 0u);
@@ -403,8 +404,8 @@ __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__rest
     }
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < RS_ITEMS; it++) {
-        const uint32_t j = blk + w * (RS_TILE / 4) + it * 64 + lane;
+    for (int it = 0; it < ITEMS; it++) {
+        const uint32_t j = blk + w * (TILE / 4) + it * 64 + lane;
         if (j < n) {
             const uint32_t d = (key[it] >> shift) & 255u;
             const uint32_t pos = s_dstart[d] + s_cnt[w][d] + rank[it];
@@ -413,7 +414,7 @@ __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__rest
         }
     }
     __syncthreads();
-    const uint32_t cnt_blk = min((uint32_t)RS_TILE, n - blk);
+    const uint32_t cnt_blk = min(TILE, n - blk);
     for (uint32_t i = tid; i < cnt_blk; i += 256) {
         const uint32_t k = s_keys[i], v = s_vals[i];
         const uint32_t d = (k >> shift) & 255u;
@@ -423,8 +424,9 @@ __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__rest
     }
 }
 
+template <int ITEMS>
 static void launch_radix_sort_onesweep(hipStream_t s, SortScratch &sc, uint32_t n, int passes) {
-    const uint32_t nb = div_up(n, RS_TILE);
+    const uint32_t nb = div_up(n, (uint32_t)ITEMS * 256u);
     (void)hipMemsetAsync(sc.ctrl, 0, sizeof(uint32_t) * (RS_CTRL_WORDS + (size_t)passes * nb * RS_BINS), s);
     const uint32_t hb = min(div_up(n, 256u * 8u), 2048u);
     rs_multi_hist_kernel<<<max(hb, 1u), 256, 0, s>>>(sc.k[0], n, passes, sc.ctrl);
@@ -433,10 +435,11 @@ static void launch_radix_sort_onesweep(hipStream_t s, SortScratch &sc, uint32_t 
         const int in = p & 1, out = (p + 1) & 1;
         uint32_t *st = sc.status + (size_t)p * nb * RS_BINS;
         if (p == 0)
-            rs_onesweep_kernel<true><<<nb, 256, 0, s>>>(sc.k[in], nullptr, n, p, sc.ctrl, st, sc.k[out], sc.v[out]);
+            rs_onesweep_kernel<true, ITEMS><<<nb, 256, 0, s>>>(sc.k[in], nullptr, n, p, sc.ctrl, st, sc.k[out],
+                                                               sc.v[out]);
         else
-            rs_onesweep_kernel<false><<<nb, 256, 0, s>>>(sc.k[in], sc.v[in], n, p, sc.ctrl, st, sc.k[out],
-                                                         sc.v[out]);
+            rs_onesweep_kernel<false, ITEMS><<<nb, 256, 0, s>>>(sc.k[in], sc.v[in], n, p, sc.ctrl, st, sc.k[out],
+                                                                sc.v[out]);
     }
 }
 
@@ -447,7 +450,7 @@ void launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits) {
     // onesweep knob: bit 0 = depth-size sorts (nbits == 32), bit 1 = tile sorts
     const int os = tuning("onesweep", 1);
     if (n <= RS_ONESWEEP_MAX_N && passes <= RS_MAX_PASSES && (os & (nbits == 32 ? 1 : 2))) {
-        launch_radix_sort_onesweep(s, sc, n, passes);
+        launch_radix_sort_onesweep<RS_ITEMS>(s, sc, n, passes);  // 8- and 32-key/thread tiles measured slower
         return;
     }
     for (int p = 0; p < passes; p++) {
