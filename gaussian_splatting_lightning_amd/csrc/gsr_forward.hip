@@ -14,8 +14,17 @@ namespace gsr {
 // preprocess: one thread per Gaussian.  Culls, projects, builds the conic and radius, evaluates SH,
 // and emits the packed render records plus the depth-sort key and tile count.
 // ------------------------------------------------------------------------------------------------
-// Returns the number of tiles the Gaussian is binned into (0 if culled).
-__device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &p, const int i) {
+// Per-Gaussian state handed from the projection to the wave-cooperative tile culling.
+struct CullIn {
+    CullGauss cg;
+    int rx, ry, rw;   // rect origin and width (tiles)
+    uint32_t depth;   // float bits of the view depth
+    bool need;        // cull the rect's tiles cooperatively
+};
+
+// Projection, conic, radius, SH colour and render records of one Gaussian.  Returns the area of its tile
+// rect (0: not rendered); the tile culling, tile count and sort key are finished by preprocess_kernel.
+__device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &p, const int i, CullIn &ci) {
     const GeomState &g = p.g;
     p.radii[i] = 0;
     g.tiles[i] = 0;
@@ -85,41 +94,67 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
     g.rec_c[i] = make_float2(rgb.z, 1.f / pv.z);
     g.clamped[i] = clamp_bits;
     p.radii[i] = (int)radius;
-    uint64_t mask = 0;
-    uint32_t kept = area;
-    if (p.cull && area <= (uint32_t)CULL_MAX_AREA) {
-        const int w = rmax.x - rmin.x;
-        const CullGauss cg = cull_setup(pimg.x, pimg.y, conic_x, conic_y, conic_z, opacity);
-        kept = 0;
-        for (int ty = rmin.y; ty < rmax.y; ty++)
-            for (int tx = rmin.x; tx < rmax.x; tx++)
-                if (cull_keep(cg, tx, ty, p.W, p.H)) {
-                    mask |= 1ull << ((ty - rmin.y) * w + (tx - rmin.x));
-                    kept++;
-                }
-    }
-    g.tile_mask[i] = mask;
-    g.tiles[i] = kept;
-    // A Gaussian whose every tile is culled keeps its radius (reference output) but renders nothing; it is
-    // sorted behind all rendered ones so the expansion never meets an empty rank.
-    g.depth_key[i] = kept ? __float_as_uint(pv.z) : 0xffffffffu;
-    if (kept > BIG_GAUSSIAN_TILES) {
-        const uint32_t slot = atomicAdd(&g.counters[CNT_BIG], 1u);
-        g.big_list[slot] = (uint32_t)i;
-        g.big_slot[i] = slot;
-    }
-    return kept;
+    ci.need = p.cull && area <= (uint32_t)CULL_MAX_AREA;
+    if (ci.need) ci.cg = cull_setup(pimg.x, pimg.y, conic_x, conic_y, conic_z, opacity);
+    ci.rx = rmin.x;
+    ci.ry = rmin.y;
+    ci.rw = rmax.x - rmin.x;
+    ci.depth = __float_as_uint(pv.z);
+    return area;
 }
 
+// Exact tile culling is balanced across the wave: the (Gaussian, tile) pairs of all 64 lanes' rects are
+// enumerated jointly (prefix sum of the rect areas, each lane takes every 64th pair, owner found by binary
+// search), so a wave costs ceil(sum of areas / 64) tile tests instead of its largest rect.
 __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessParams p) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    __shared__ CullGauss s_cg[4][64];
+    __shared__ int4 s_rect[4][64];        // rx, ry, rw, start of the lane's pairs
+    __shared__ unsigned long long s_mask[4][64];
     __shared__ uint32_t s_w[4];
-    uint32_t kept = i < p.P ? preprocess_gaussian(p, i) : 0u;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    CullIn ci;
+    ci.need = false;
+    const uint32_t area = i < p.P ? preprocess_gaussian(p, i, ci) : 0u;
+    const uint32_t need_area = ci.need ? area : 0u;
+    const uint32_t incl = wave_inclusive_scan(need_area, lane);
+    const uint32_t total = __shfl((int)incl, 63);
+    if (ci.need) s_cg[w][lane] = ci.cg;
+    s_rect[w][lane] = make_int4(ci.rx, ci.ry, ci.rw, (int)(incl - need_area));
+    s_mask[w][lane] = 0ull;
+    wave_lds_sync();
+    for (uint32_t j = lane; j < total; j += 64) {
+        int o = 0;
+#pragma unroll
+        for (int step = 32; step; step >>= 1)
+            if ((uint32_t)s_rect[w][o + step].w <= j) o += step;
+        const int4 r = s_rect[w][o];
+        const uint32_t t = j - (uint32_t)r.w;
+        const int tx = r.x + (int)(t % (uint32_t)r.z), ty = r.y + (int)(t / (uint32_t)r.z);
+        if (cull_keep(s_cg[w][o], tx, ty, p.W, p.H)) atomicOr(&s_mask[w][o], 1ull << t);
+    }
+    wave_lds_sync();
+    uint32_t kept = area;
+    if (i < p.P && area > 0) {
+        const GeomState &g = p.g;
+        const uint64_t mask = ci.need ? s_mask[w][lane] : 0ull;
+        if (ci.need) kept = (uint32_t)__popcll(mask);
+        g.tile_mask[i] = mask;
+        g.tiles[i] = kept;
+        // A Gaussian whose every tile is culled keeps its radius (reference output) but renders nothing; it
+        // is sorted behind all rendered ones so the expansion never meets an empty rank.
+        g.depth_key[i] = kept ? ci.depth : 0xffffffffu;
+        if (kept > BIG_GAUSSIAN_TILES) {
+            const uint32_t slot = atomicAdd(&g.counters[CNT_BIG], 1u);
+            g.big_list[slot] = (uint32_t)i;
+            g.big_slot[i] = slot;
+        }
+    }
     // instance total for the early host readback (gsr_forward): block sum, one 64-bit atomic per block into
     // one of CNT_NPART partial counters
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) kept += (uint32_t)__shfl_xor((int)kept, o);
-    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = kept;
+    if (lane == 0) s_w[w] = kept;
     __syncthreads();
     if (threadIdx.x == 0) {
         const unsigned long long tot = (unsigned long long)s_w[0] + s_w[1] + s_w[2] + s_w[3];
