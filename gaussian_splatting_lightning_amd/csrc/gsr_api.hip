@@ -332,8 +332,11 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
         GSR_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * T, stream));
         launch_identify_ranges(stream, b.keys_sorted, R, im.ranges);
     });
+    const int lpt = tuning("lpt", 1);
+    if (lpt) launch_tile_order(stream, im.ranges, nullptr, 0, (int)T, im.order_fwd);
     RenderFwdParams rp;
     rp.W = W; rp.H = H; rp.gx = gx; rp.gy = gy; rp.num_tiles = (int)T;
+    rp.tile_order = lpt ? im.order_fwd : nullptr;
     rp.ranges = im.ranges; rp.sorted_u = b.sorted_u; rp.inst_gid = b.inst_gid;
     rp.point_list = b.point_list; rp.inv = b.inv; rp.tile_loaded = im.tile_loaded;
     rp.rec_a = g.rec_a; rp.rec_b = g.rec_b; rp.rec_c = g.rec_c;
@@ -384,6 +387,9 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
         RenderBwdParams rp;
         rp.W = W; rp.H = H; rp.gx = gx; rp.gy = gy; rp.num_tiles = (int)T;
         rp.ranges = im.ranges; rp.point_list = b.point_list; rp.n_contrib = im.n_contrib;
+        const int lpt = tuning("lpt", 1);
+        if (lpt) launch_tile_order(stream, im.ranges, im.tile_last, 1, (int)T, im.order_bwd);
+        rp.tile_order = lpt ? im.order_bwd : nullptr;
         rp.tile_last = im.tile_last; rp.tile_loaded = im.tile_loaded;
         rp.rec_a = g.rec_a; rp.rec_b = g.rec_b; rp.rec_c = g.rec_c;
         rp.bg = a->background; rp.final_T = im.final_T; rp.dL_dpix = a->dL_dpix; rp.dL_dinvdepth = a->dL_dinvdepth;

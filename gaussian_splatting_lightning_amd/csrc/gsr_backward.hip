@@ -71,8 +71,9 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_bwd_v3_kernel(Rend
     __shared__ float2 s_c[WPB][BWD_BATCH];
     __shared__ __attribute__((aligned(16))) float s_part[WPB][BWD_BATCH][PART];  // [wave][instance][10 sums]
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tile = blockIdx.x * WPB + w;
-    if (tile >= p.num_tiles) return;
+    const int slot = blockIdx.x * WPB + w;
+    if (slot >= p.num_tiles) return;
+    const int tile = p.tile_order ? (int)p.tile_order[slot] : slot;
     const int tx = tile % p.gx, ty = tile / p.gx;
     const int px = tx * BLOCK_X + (lane & 15);
     const int py0 = ty * BLOCK_Y + (lane >> 4);

@@ -157,6 +157,8 @@ struct ImageState {
     uint2 *ranges;        // T
     uint32_t *tile_last;  // T: max n_contrib over the tile's pixels
     uint32_t *tile_loaded; // T: instances of the tile the forward composite gathered (>= tile_last)
+    uint32_t *order_fwd;   // tiles in descending forward work (instances in range), LPT launch order
+    uint32_t *order_bwd;   // tiles in descending backward work (tile_last)
 };
 
 inline size_t carve_image(char *base, int W, int H, ImageState &im) {
@@ -168,6 +170,8 @@ inline size_t carve_image(char *base, int W, int H, ImageState &im) {
     im.ranges = c.take<uint2>((size_t)gx * gy + 1);
     im.tile_last = c.take<uint32_t>((size_t)gx * gy + 1);
     im.tile_loaded = c.take<uint32_t>((size_t)gx * gy + 1);
+    im.order_fwd = c.take<uint32_t>((size_t)gx * gy + 1);
+    im.order_bwd = c.take<uint32_t>((size_t)gx * gy + 1);
     return c.off + 256;
 }
 

@@ -297,6 +297,42 @@ void launch_identify_ranges(hipStream_t s, const uint32_t *keys_sorted, uint32_t
     identify_ranges_kernel<<<div_up(R, 256), 256, 0, s>>>(keys_sorted, R, ranges);
 }
 
+// LPT (longest first) launch order for the composite kernels: tile costs vary ~2x around the image centre,
+// and the GPU runs only ~8 tile waves per SIMD, so launching heavy tiles first keeps the tail short.  One
+// workgroup: bucket histogram of the tile weights (8 instances per bucket), descending exclusive scan,
+// scatter.  Order inside a bucket is arbitrary -- it only changes which tile runs when, never a result.
+__global__ __launch_bounds__(1024) void tile_order_kernel(const uint2 *__restrict__ ranges,
+                                                          const uint32_t *__restrict__ tile_last, int use_last,
+                                                          int T, uint32_t *__restrict__ order) {
+    __shared__ uint32_t hist[256];
+    const int tid = threadIdx.x;
+    if (tid < 256) hist[tid] = 0;
+    __syncthreads();
+    auto bucket = [&](int t) -> uint32_t {
+        const uint32_t w = use_last ? tile_last[t] : ranges[t].y - ranges[t].x;
+        return 255u - min(255u, w >> 3);  // heaviest first
+    };
+    for (int t = tid; t < T; t += 1024) atomicAdd(&hist[bucket(t)], 1u);
+    __syncthreads();
+    if (tid < 64) {  // exclusive scan of the 256 buckets by one wave, 4 per lane
+        const uint32_t a = hist[4 * tid], b = hist[4 * tid + 1], c = hist[4 * tid + 2], d = hist[4 * tid + 3];
+        const uint32_t sum = a + b + c + d;
+        const uint32_t excl = wave_inclusive_scan(sum, tid) - sum;
+        hist[4 * tid] = excl;
+        hist[4 * tid + 1] = excl + a;
+        hist[4 * tid + 2] = excl + a + b;
+        hist[4 * tid + 3] = excl + a + b + c;
+    }
+    __syncthreads();
+    for (int t = tid; t < T; t += 1024) order[atomicAdd(&hist[bucket(t)], 1u)] = (uint32_t)t;
+}
+
+void launch_tile_order(hipStream_t s, const uint2 *ranges, const uint32_t *tile_last, int use_last, int T,
+                       uint32_t *order) {
+    if (T <= 0) return;
+    tile_order_kernel<<<1, 1024, 0, s>>>(ranges, tile_last, use_last, T, order);
+}
+
 // ------------------------------------------------------------------------------------------------
 // compositing: one wave per 16x16 tile, 4 pixels per lane (rows r, r+4, r+8, r+12).  Each batch of
 // 64 instances is gathered once per wave (one instance per lane) into the wave's LDS slice and then
@@ -316,8 +352,9 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_fwd_v3_kernel(Rend
     __shared__ float4 s_b[WPB][65];
     __shared__ float2 s_c[WPB][65];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tile = blockIdx.x * WPB + w;
-    if (tile >= p.num_tiles) return;
+    const int slot = blockIdx.x * WPB + w;
+    if (slot >= p.num_tiles) return;
+    const int tile = p.tile_order ? (int)p.tile_order[slot] : slot;
     const int tx = tile % p.gx, ty = tile / p.gx;
     const int px = tx * BLOCK_X + (lane & 15);
     const int py0 = ty * BLOCK_Y + (lane >> 4);

@@ -45,9 +45,14 @@ void launch_expand(hipStream_t s, const ExpandParams &p);
 
 void launch_identify_ranges(hipStream_t s, const uint32_t *keys_sorted, uint32_t R, uint2 *ranges);
 
+// Tiles ordered by descending work (range length, or tile_last when use_last) for an LPT launch order.
+void launch_tile_order(hipStream_t s, const uint2 *ranges, const uint32_t *tile_last, int use_last, int T,
+                       uint32_t *order);
+
 struct RenderFwdParams {
     int W, H, gx, gy, num_tiles;
     const uint2 *ranges;
+    const uint32_t *tile_order;  // launch slot -> tile (heaviest first), or null for identity
     const uint32_t *sorted_u, *inst_gid;
     uint32_t *point_list, *inv, *tile_loaded;
     const float4 *rec_a, *rec_b;
@@ -64,6 +69,7 @@ void launch_mark_visible(hipStream_t s, int P, const float *means3D, const float
 struct RenderBwdParams {
     int W, H, gx, gy, num_tiles;
     const uint2 *ranges;
+    const uint32_t *tile_order;  // launch slot -> tile (heaviest first), or null for identity
     const uint32_t *point_list, *n_contrib, *tile_last, *tile_loaded;
     const uint32_t *sorted_u;  // sorted position -> expansion index u (rows_by_u)
     const float4 *rec_a, *rec_b;
