@@ -219,7 +219,7 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_bwd_v3_kernel(Rend
 
 void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
     if (p.num_tiles <= 0) return;
-    const int minw = tuning("bwd_minwaves", 5), wpb = tuning("bwd_wpb", 4);
+    const int minw = tuning("bwd_minwaves", 5), wpb = tuning("bwd_wpb", 1);
     const dim3 block(64 * (wpb == 1 ? 1 : 4)), grid(wpb == 1 ? p.num_tiles : div_up(p.num_tiles, 4));
 #define GSR_BWD_LAUNCH(INV, MW)                                                                        \
     do {                                                                                               \

@@ -468,7 +468,7 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_fwd_v3_kernel(Rend
 void launch_render_fwd(hipStream_t s, const RenderFwdParams &p) {
     if (p.num_tiles <= 0) return;
     const dim3 grid(div_up(p.num_tiles, 4)), block(256);
-    const int pipe = tuning("fwd_pipe", 0), wpb = tuning("fwd_wpb", 1);
+    const int pipe = tuning("fwd_pipe", 0), wpb = tuning("fwd_wpb", 4);
     if (wpb == 1) {
         const dim3 g1(p.num_tiles), b1(64);
         if (pipe) render_fwd_v3_kernel<4, 1, true><<<g1, b1, 0, s>>>(p);
