@@ -57,7 +57,7 @@ EXPORTED_SYMBOLS = (
     "gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_sh_backward_views", "gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes",
     "gsr_image_buffer_bytes", "gsr_bwd_scratch_bytes", "gsr_set_profiling", "gsr_num_stages", "gsr_stage_name",
     "gsr_stage_times", "gsr_reset_stage_times", "gsr_last_error", "gsr_build_info", "gsr_state_layout_query",
-    "gsr_set_tuning",
+    "gsr_set_tuning", "gsr_ssim_num_partials", "gsr_ssim_forward", "gsr_ssim_backward",
 )
 
 _lib = None
@@ -84,6 +84,14 @@ def load(path: str | None = None):
     lib.gsr_sh_backward_views.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _fp, _fp, _fp, _fp,
                                           ctypes.c_void_p]
     lib.gsr_sh_backward_views.restype = ctypes.c_int
+    lib.gsr_ssim_num_partials.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.gsr_ssim_num_partials.restype = ctypes.c_size_t
+    lib.gsr_ssim_forward.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _fp, _fp, ctypes.c_int, _fp, _fp, _fp,
+                                     _fp, ctypes.c_void_p]
+    lib.gsr_ssim_forward.restype = ctypes.c_int
+    lib.gsr_ssim_backward.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _fp, _fp, ctypes.c_int, _fp, _fp, _fp,
+                                      _fp, _fp, ctypes.c_void_p]
+    lib.gsr_ssim_backward.restype = ctypes.c_int
     lib.gsr_geom_buffer_bytes.argtypes = [ctypes.c_int]
     lib.gsr_geom_buffer_bytes.restype = ctypes.c_size_t
     lib.gsr_binning_buffer_bytes.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int]

@@ -445,6 +445,40 @@ int gsr_sh_backward_views(int P, int D, int M, int V, const float *means3D, cons
     return GSR_OK;
 }
 
+size_t gsr_ssim_num_partials(int planes, int H, int W) {
+    return (planes > 0 && H > 0 && W > 0) ? ssim_num_partials(planes, H, W) : 0;
+}
+
+int gsr_ssim_forward(int planes, int H, int W, const float *img1, const float *img2, int valid_padding,
+                     float *partial_sums, float *dm_dmu1, float *dm_dsigma1_sq, float *dm_dsigma12, void *stream_ptr) {
+    if (planes <= 0 || H <= 0 || W <= 0) return fail(GSR_ERR_ARG, "ssim: empty image");
+    if ((int64_t)planes * H * W > 0x7fffffffLL) return fail(GSR_ERR_ARG, "ssim: image too large");
+    if (planes > 65535) return fail(GSR_ERR_ARG, "ssim: too many planes");
+    if (!img1 || !img2 || !partial_sums) return fail(GSR_ERR_ARG, "ssim: null argument");
+    if ((dm_dmu1 == nullptr) != (dm_dsigma1_sq == nullptr) || (dm_dmu1 == nullptr) != (dm_dsigma12 == nullptr))
+        return fail(GSR_ERR_ARG, "ssim: derivative maps must be all given or all NULL");
+    hipStream_t s = (hipStream_t)stream_ptr;
+    launch_ssim_forward(s, planes, H, W, img1, img2, valid_padding, partial_sums, dm_dmu1, dm_dsigma1_sq, dm_dsigma12);
+    GSR_HIP(hipGetLastError());
+    return GSR_OK;
+}
+
+int gsr_ssim_backward(int planes, int H, int W, const float *img1, const float *img2, int valid_padding,
+                      const float *dL_dmean, const float *dm_dmu1, const float *dm_dsigma1_sq,
+                      const float *dm_dsigma12, float *dL_dimg1, void *stream_ptr) {
+    if (planes <= 0 || H <= 0 || W <= 0) return fail(GSR_ERR_ARG, "ssim: empty image");
+    if (planes > 65535) return fail(GSR_ERR_ARG, "ssim: too many planes");
+    if (!img1 || !img2 || !dL_dmean || !dm_dmu1 || !dm_dsigma1_sq || !dm_dsigma12 || !dL_dimg1)
+        return fail(GSR_ERR_ARG, "ssim: null argument");
+    const int64_t counted = (int64_t)planes * (valid_padding ? (int64_t)(H - 10) * (W - 10) : (int64_t)H * W);
+    if (counted <= 0) return fail(GSR_ERR_ARG, "ssim: image smaller than the valid window");
+    hipStream_t s = (hipStream_t)stream_ptr;
+    launch_ssim_backward(s, planes, H, W, img1, img2, valid_padding, dL_dmean, (float)(1.0 / (double)counted), dm_dmu1,
+                         dm_dsigma1_sq, dm_dsigma12, dL_dimg1);
+    GSR_HIP(hipGetLastError());
+    return GSR_OK;
+}
+
 int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix, uint8_t *present,
                      void *stream_ptr) {
     (void)projmatrix;

@@ -110,4 +110,12 @@ void launch_preprocess_bwd(hipStream_t s, const PreprocessBwdParams &p);
 void launch_sh_backward_views(hipStream_t s, int P, int D, int M, int V, const float *means3D, const float *campos,
                               const float *dcolors_sh, float *dsh);
 
+// ---- fused SSIM loss (gsr_ssim.hip) ----
+size_t ssim_num_partials(int planes, int H, int W);
+void launch_ssim_forward(hipStream_t s, int planes, int H, int W, const float *img1, const float *img2, int valid,
+                         float *partial, float *d_mu1, float *d_s11, float *d_s12);
+void launch_ssim_backward(hipStream_t s, int planes, int H, int W, const float *img1, const float *img2, int valid,
+                          const float *dL_dmean, float inv_n, const float *d_mu1, const float *d_s11,
+                          const float *d_s12, float *dL_dimg1);
+
 }  // namespace gsr

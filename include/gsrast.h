@@ -135,6 +135,20 @@ int gsr_sh_backward_views(int P, int D, int M, int V, const float *means3D, cons
 int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
                      uint8_t *present, void *stream);
 
+/* Fused SSIM loss -- replaces `fused_ssim(img1, img2, padding, train)` (rahul-goel/fused-ssim, imported at
+ * gs_lightning_module.py:10 and used as 1 - fused_ssim(render, gt) at :100,279).  Images are (B,C,H,W)
+ * contiguous fp32 device arrays; planes = B*C.  11x11 Gaussian window (sigma 1.5), C1 = 0.01^2, C2 = 0.03^2,
+ * zero-padded "same" filtering; valid_padding = 1 averages only pixels >= 5 px from the border.
+ * Forward: writes gsr_ssim_num_partials() partial sums of the SSIM map (mean = sum / counted pixels) and, when
+ * the three derivative maps (planes*H*W each) are non-NULL, the per-pixel derivatives the backward needs.
+ * Backward: dL_dimg1 from dL_dmean (device scalar: gradient of the mean SSIM) and the derivative maps. */
+size_t gsr_ssim_num_partials(int planes, int H, int W);
+int gsr_ssim_forward(int planes, int H, int W, const float *img1, const float *img2, int valid_padding,
+                     float *partial_sums, float *dm_dmu1, float *dm_dsigma1_sq, float *dm_dsigma12, void *stream);
+int gsr_ssim_backward(int planes, int H, int W, const float *img1, const float *img2, int valid_padding,
+                      const float *dL_dmean, const float *dm_dmu1, const float *dm_dsigma1_sq,
+                      const float *dm_dsigma12, float *dL_dimg1, void *stream);
+
 /* Buffer sizes the forward will request (host-only arithmetic; for planning and tests). */
 size_t gsr_geom_buffer_bytes(int P);
 size_t gsr_binning_buffer_bytes(int64_t R, int W, int H);
