@@ -228,7 +228,7 @@ void gsr_state_layout_query(int P, int64_t R, int W, int H, gsr_state_layout *ou
     out->geom_inst_off = off(g.inst_off);
     out->geom_inst_start = off(g.inst_start);
     out->geom_clamped = off(g.clamped);
-    out->geom_tile_mask = off(g.tile_mask);
+    out->geom_expand_rec = off(g.exp_rec);
     out->geom_sorted_depth = off(g.sort.k[0]);
     out->bin_point_list = off(b.point_list);
     out->bin_inv = off(b.inv);
@@ -322,7 +322,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     if (R > 0) {
         ExpandParams ep;
         ep.P = (uint32_t)P; ep.R = R; ep.gx = gx; ep.gy = gy;
-        ep.order = g.order; ep.inst_off = g.inst_off; ep.tiles = g.tiles; ep.tile_mask = g.tile_mask; ep.rec_a = g.rec_a; ep.radii = a->radii;
+        ep.order = g.order; ep.inst_off = g.inst_off; ep.tiles = g.tiles; ep.exp_rec = g.exp_rec;
         ep.keys_out = b.sort.k[0]; ep.inst_gid = b.inst_gid; ep.inst_start = g.inst_start;
         GSR_STAGE(ST_EXPAND, dbg, launch_expand(stream, ep));
         GSR_STAGE(ST_TILE_SORT, dbg, launch_radix_sort(stream, b.sort, R, tile_key_bits(T)));

@@ -88,7 +88,8 @@ struct GeomState {
     uint32_t *depth_key;   // P: float bits of view depth, 0xffffffff if culled (aliases sort.k[0])
     uint32_t *tiles;       // P: tiles touched
     uint8_t *clamped;      // P: bit c set if SH colour channel c was clamped at 0
-    uint64_t *tile_mask;   // P: kept tiles of the rect (row-major bits) when area <= 64, else 0 (keep all)
+    uint4 *exp_rec;        // P: expansion record {kept-tile mask lo, hi, rmin.x | rmin.y << 16, rect width}; mask 0 =
+                           //    all tiles of the rect (area > 64 or culling off).  One 16-B gather per Gaussian.
     uint32_t *inst_off;    // P+1: exclusive scan of tiles in depth order, [P] = total
     uint32_t *inst_start;  // P: first instance (expansion order) of each Gaussian
     uint32_t *big_list;    // P: Gaussians with > BIG_GAUSSIAN_TILES tiles
@@ -107,7 +108,7 @@ inline size_t carve_geom(char *base, int P, GeomState &g) {
     g.rec_c = c.take<float2>(n);
     g.tiles = c.take<uint32_t>(n);
     g.clamped = c.take<uint8_t>(n);
-    g.tile_mask = c.take<uint64_t>(n);
+    g.exp_rec = c.take<uint4>(n);
     g.inst_off = c.take<uint32_t>((size_t)n + 1);
     g.inst_start = c.take<uint32_t>(n);
     g.big_list = c.take<uint32_t>(n);

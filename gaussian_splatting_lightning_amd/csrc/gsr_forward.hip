@@ -139,7 +139,8 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessParams p) {
         const GeomState &g = p.g;
         const uint64_t mask = ci.need ? s_mask[w][lane] : 0ull;
         if (ci.need) kept = (uint32_t)__popcll(mask);
-        g.tile_mask[i] = mask;
+        g.exp_rec[i] = make_uint4((uint32_t)mask, (uint32_t)(mask >> 32), (uint32_t)ci.rx | ((uint32_t)ci.ry << 16),
+                                  (uint32_t)ci.rw);
         g.tiles[i] = kept;
         // A Gaussian whose every tile is culled keeps its radius (reference output) but renders nothing; it
         // is sorted behind all rendered ones so the expansion never meets an empty rank.
@@ -204,6 +205,7 @@ __global__ __launch_bounds__(256) void expand_kernel(ExpandParams p) {
     __shared__ uint32_t s_off[EXP_TILE + 2];
     __shared__ int4 s_rect[EXP_TILE + 1];       // (gid, rmin.x, rmin.y, width)
     __shared__ uint64_t s_mask[EXP_TILE + 1];   // kept-tile mask (0: all tiles of the rect)
+    static_assert(sizeof(uint4) == 16, "expansion record");
     __shared__ uint32_t s_lo, s_n;
     const uint32_t u0 = blockIdx.x * EXP_TILE;
     const uint32_t u1 = min(p.R, u0 + (uint32_t)EXP_TILE);
@@ -223,11 +225,9 @@ __global__ __launch_bounds__(256) void expand_kernel(ExpandParams p) {
     for (uint32_t k = threadIdx.x; k < nr + 1; k += 256) s_off[k] = p.inst_off[r_lo + k];
     for (uint32_t k = threadIdx.x; k < nr; k += 256) {
         const uint32_t gid = p.order[r_lo + k];
-        const float4 a = p.rec_a[gid];
-        int2 rmin, rmax;
-        get_rect(make_float2(a.x, a.y), p.radii[gid], p.gx, p.gy, rmin, rmax);
-        s_rect[k] = make_int4((int)gid, rmin.x, rmin.y, rmax.x - rmin.x);
-        s_mask[k] = p.tile_mask[gid];
+        const uint4 e = p.exp_rec[gid];  // rect and kept-tile mask from the preprocess: one 16-B gather
+        s_rect[k] = make_int4((int)gid, (int)(e.z & 0xffffu), (int)(e.z >> 16), (int)e.w);
+        s_mask[k] = (uint64_t)e.x | ((uint64_t)e.y << 32);
     }
     __syncthreads();
     const uint32_t ub = u0 + threadIdx.x * EXP_PER;

@@ -36,9 +36,7 @@ struct ExpandParams {
     uint32_t P, R;
     int gx, gy;
     const uint32_t *order, *inst_off, *tiles;
-    const uint64_t *tile_mask;
-    const float4 *rec_a;
-    const int *radii;
+    const uint4 *exp_rec;
     uint32_t *keys_out, *inst_gid, *inst_start;
 };
 void launch_expand(hipStream_t s, const ExpandParams &p);

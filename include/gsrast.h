@@ -162,7 +162,7 @@ typedef struct gsr_state_layout {
     size_t geom_rec_a, geom_rec_b, geom_rec_c; /* float4, float4, float2 per Gaussian */
     size_t geom_tiles, geom_order, geom_inst_off, geom_inst_start, geom_clamped; /* u32, u32, u32, u32, u8 */
     size_t geom_sorted_depth; /* u32 depth bits in depth-rank order (depth of order[r]) */
-    size_t geom_tile_mask;    /* u64 kept-tile mask of the rect (exact culling), 0 = all tiles */
+    size_t geom_expand_rec;   /* uint4 {kept-tile mask lo, hi, rmin.x | rmin.y << 16, rect width} (mask 0 = all) */
     size_t bin_point_list, bin_inv, bin_keys_sorted;                  /* u32 per instance */
     size_t bin_sorted_u, bin_inst_gid;                                /* u32 per instance */
     size_t img_final_T, img_n_contrib, img_ranges, img_tile_last;     /* f32/u32 per pixel, uint2/u32 per tile */
