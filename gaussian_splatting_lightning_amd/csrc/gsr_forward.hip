@@ -207,6 +207,7 @@ __global__ __launch_bounds__(256) void expand_kernel(ExpandParams p) {
     __shared__ uint64_t s_mask[EXP_TILE + 1];   // kept-tile mask (0: all tiles of the rect)
     static_assert(sizeof(uint4) == 16, "expansion record");
     __shared__ uint32_t s_lo, s_n;
+    __shared__ uint2 s_out[EXP_TILE];           // (tile key, gid) staged for coalesced stores
     const uint32_t u0 = blockIdx.x * EXP_TILE;
     const uint32_t u1 = min(p.R, u0 + (uint32_t)EXP_TILE);
     if (threadIdx.x < 64) {
@@ -231,39 +232,45 @@ __global__ __launch_bounds__(256) void expand_kernel(ExpandParams p) {
     }
     __syncthreads();
     const uint32_t ub = u0 + threadIdx.x * EXP_PER;
-    if (ub >= u1) return;
-    // owner of ub within the window
-    uint32_t lo = 0, hi = nr - 1;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1) >> 1;
-        if (s_off[mid] <= ub) lo = mid; else hi = mid - 1;
+    if (ub < u1) {
+        // owner of ub within the window
+        uint32_t lo = 0, hi = nr - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (s_off[mid] <= ub) lo = mid; else hi = mid - 1;
+        }
+        uint32_t r = lo;
+        uint32_t next = s_off[r + 1];
+        int4 rect = s_rect[r];
+        uint64_t m = s_mask[r];
+        uint32_t k = ub - s_off[r];
+        for (uint32_t j = 0; j < k && m; j++) m &= m - 1;  // skip the kept tiles of earlier threads
+        const uint32_t ue = min(u1, ub + (uint32_t)EXP_PER);
+        for (uint32_t u = ub; u < ue; u++) {
+            while (u >= next) {
+                r++;
+                next = s_off[r + 1];
+                rect = s_rect[r];
+                m = s_mask[r];
+                k = 0;
+            }
+            uint32_t bit = k;
+            if (m) {  // culled rect: the k-th kept tile is the lowest remaining mask bit
+                bit = (uint32_t)__builtin_ctzll(m);
+                m &= m - 1;
+            }
+            const uint32_t w = (uint32_t)rect.w;
+            const uint32_t ty = (uint32_t)rect.z + bit / w, tx = (uint32_t)rect.y + bit % w;
+            s_out[u - u0] = make_uint2(ty * (uint32_t)p.gx + tx, (uint32_t)rect.x);
+            if (k == 0) p.inst_start[rect.x] = u;
+            k++;
+        }
     }
-    uint32_t r = lo;
-    uint32_t next = s_off[r + 1];
-    int4 rect = s_rect[r];
-    uint64_t m = s_mask[r];
-    uint32_t k = ub - s_off[r];
-    for (uint32_t j = 0; j < k && m; j++) m &= m - 1;  // skip the kept tiles of earlier threads
-    const uint32_t ue = min(u1, ub + (uint32_t)EXP_PER);
-    for (uint32_t u = ub; u < ue; u++) {
-        while (u >= next) {
-            r++;
-            next = s_off[r + 1];
-            rect = s_rect[r];
-            m = s_mask[r];
-            k = 0;
-        }
-        uint32_t bit = k;
-        if (m) {  // culled rect: the k-th kept tile is the lowest remaining mask bit
-            bit = (uint32_t)__builtin_ctzll(m);
-            m &= m - 1;
-        }
-        const uint32_t w = (uint32_t)rect.w;
-        const uint32_t ty = (uint32_t)rect.z + bit / w, tx = (uint32_t)rect.y + bit % w;
-        p.keys_out[u] = ty * (uint32_t)p.gx + tx;
-        p.inst_gid[u] = (uint32_t)rect.x;
-        if (k == 0) p.inst_start[rect.x] = u;
-        k++;
+    __syncthreads();
+    for (uint32_t u = u0 + threadIdx.x; u < u1; u += 256) {
+        const uint2 o = s_out[u - u0];
+        p.keys_out[u] = o.x;
+        p.inst_gid[u] = o.y;
     }
 }
 
