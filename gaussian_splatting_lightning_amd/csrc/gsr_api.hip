@@ -272,7 +272,9 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     char *img = alloc(alloc_ctx, GSR_BUF_IMAGE, carve_image(nullptr, W, H, im));
     if (!img) return fail(GSR_ERR_ALLOC, "image buffer allocation failed");
     carve_image(img, W, H, im);
-    GSR_HIP(hipMemsetAsync(g.counters, 0, CNT_WORDS * sizeof(uint32_t), stream));
+    const size_t clear_bytes = (size_t)(reinterpret_cast<char *>(g.scan_status + div_up(P + 1, SCAN_TILE) + 1) -
+                                        reinterpret_cast<char *>(g.counters));
+    GSR_HIP(hipMemsetAsync(g.counters, 0, clear_bytes, stream));  // counters + instance-scan look-back words
 
     PreprocessParams pp;
     pp.P = P; pp.D = a->D; pp.M = a->M; pp.W = W; pp.H = H; pp.gx = gx; pp.gy = gy;
@@ -297,9 +299,14 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     GSR_HIP(hipMemcpyAsync(hw, g.counters, CNT_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
     GSR_HIP(hipEventRecord(rb_ev, stream));
     GSR_STAGE(ST_DEPTH_SORT, dbg, launch_radix_sort(stream, g.sort, (uint32_t)P, 32));
-    GSR_STAGE(ST_SCAN, dbg,
-              launch_exclusive_scan(stream, g.tiles, g.order, (uint32_t)P, g.inst_off, g.scan_tmp,
-                                    g.counters + CNT_OVERFLOW));
+    if (tuning("scan_lookback", 1))
+        GSR_STAGE(ST_SCAN, dbg,
+                  launch_exclusive_scan_lookback(stream, g.tiles, g.order, (uint32_t)P, g.inst_off, g.scan_status,
+                                                 g.counters + CNT_SCAN_TICKET, g.counters + CNT_OVERFLOW));
+    else
+        GSR_STAGE(ST_SCAN, dbg,
+                  launch_exclusive_scan(stream, g.tiles, g.order, (uint32_t)P, g.inst_off, g.scan_tmp,
+                                        g.counters + CNT_OVERFLOW));
     GSR_STAGE(ST_READBACK, dbg, GSR_HIP(hipEventSynchronize(rb_ev)));
     uint64_t total64 = 0;
     for (int k = 0; k < CNT_NPART; k++) {

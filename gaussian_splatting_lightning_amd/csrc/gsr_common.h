@@ -23,7 +23,8 @@ constexpr int GRAD_ROW = 12;                   // floats per instance gradient r
 // counters block at the head of the geometry buffer (zeroed every forward)
 // counters: [CNT_BIG] big-Gaussian count, [CNT_OVERFLOW] scan overflow flag, then CNT_NPART 64-bit partial
 // sums of the instance total (spread over addresses so the per-block atomics do not serialise)
-enum Counter : int { CNT_BIG = 0, CNT_OVERFLOW = 2, CNT_PARTIALS = 16, CNT_NPART = 64, CNT_WORDS = 16 + 2 * 64 };
+enum Counter : int { CNT_BIG = 0, CNT_OVERFLOW = 2, CNT_SCAN_TICKET = 3, CNT_PARTIALS = 16, CNT_NPART = 64,
+                     CNT_WORDS = 16 + 2 * 64 };
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }
 
@@ -94,7 +95,8 @@ struct GeomState {
     uint32_t *inst_start;  // P: first instance (expansion order) of each Gaussian
     uint32_t *big_list;    // P: Gaussians with > BIG_GAUSSIAN_TILES tiles
     uint32_t *big_slot;    // P: index of a big Gaussian in big_list (valid only for big ones)
-    uint32_t *scan_tmp;    // block sums for the instance scan
+    uint32_t *scan_tmp;    // block sums for the instance scan (multi-kernel path)
+    uint64_t *scan_status; // look-back words of the single-kernel instance scan
     SortScratch sort;      // depth sort (P keys); final order lands in sort.v[0]
     const uint32_t *order; // = sort.v[0] after the (even-pass) depth sort
 };
@@ -103,6 +105,7 @@ inline size_t carve_geom(char *base, int P, GeomState &g) {
     Carver c(base);
     uint32_t n = (uint32_t)P;
     g.counters = c.take<uint32_t>(CNT_WORDS);
+    g.scan_status = c.take<uint64_t>(div_up(n + 1, SCAN_TILE) + 1);  // cleared together with the counters
     g.rec_a = c.take<float4>(n);
     g.rec_b = c.take<float4>(n);
     g.rec_c = c.take<float2>(n);

@@ -13,6 +13,9 @@ int tuning(const char *name, int default_value);
 // out has n+1 entries; out[n] = total.  overflow_flag (device u32) is set if the total exceeds 2^32-1.
 void launch_exclusive_scan(hipStream_t s, const uint32_t *in, const uint32_t *idx, uint32_t n, uint32_t *out,
                            uint32_t *block_tmp, uint32_t *overflow_flag);
+// Same result in one launch (decoupled look-back); status (div_up(n + 1, SCAN_TILE) words) and *ticket zeroed.
+void launch_exclusive_scan_lookback(hipStream_t s, const uint32_t *in, const uint32_t *idx, uint32_t n, uint32_t *out,
+                                    uint64_t *status, uint32_t *ticket, uint32_t *overflow_flag);
 
 // LSD radix sort of n (key, value) pairs on bits [0, nbits).  Keys start in sc.k[0]; values are the
 // implicit iota 0..n-1.  After ceil(nbits/8) passes the keys are in sc.k[passes & 1] and the values in

@@ -127,6 +127,99 @@ void launch_exclusive_scan(hipStream_t s, const uint32_t *in, const uint32_t *id
     }
 }
 
+// Single-kernel exclusive scan with decoupled look-back (one launch instead of three).  Block ids come from an
+// atomic ticket so a block only waits on blocks that started before it; its first wave inspects 64
+// predecessors per round trip.  Status words: 2-bit flag | 62-bit inclusive/aggregate sum.
+constexpr uint64_t SLB_AGG = 1ull << 62, SLB_INC = 2ull << 62, SLB_MASK = (1ull << 62) - 1;
+
+template <bool GATHER>
+__global__ __launch_bounds__(256) void scan_lookback_kernel(const uint32_t *__restrict__ in,
+                                                            const uint32_t *__restrict__ idx, uint32_t n,
+                                                            uint32_t *__restrict__ out, uint64_t *__restrict__ status,
+                                                            uint32_t *__restrict__ ticket,
+                                                            uint32_t *__restrict__ overflow) {
+    constexpr int PER = SCAN_TILE / 256;
+    __shared__ uint32_t s_bid, s_w[4];
+    __shared__ unsigned long long s_excl;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) s_bid = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t bid = s_bid;
+    const uint32_t base = bid * SCAN_TILE + tid * PER;
+    uint32_t v[PER];
+    uint32_t local = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const uint32_t j = base + k;
+        v[k] = j < n ? scan_load<GATHER>(in, idx, j) : 0u;
+        local += v[k];
+    }
+    const uint32_t inc = wave_inclusive_scan(local, lane);
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    if (w == 0) {
+        const uint64_t agg = (uint64_t)s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        if (lane == 0)
+            __hip_atomic_store(status + bid, (bid == 0 ? SLB_INC : SLB_AGG) | agg, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t excl = 0;
+        int64_t look = (int64_t)bid - 1;
+        uint32_t spins = 0;
+        while (look >= 0) {
+            const int64_t q = look - lane;
+            const uint64_t sv = q >= 0 ? __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                       : SLB_INC;
+            const uint64_t flag = sv & ~SLB_MASK;
+            const uint64_t inc_mask = __ballot(flag == SLB_INC);
+            const int first = inc_mask ? __builtin_ctzll(inc_mask) : 64;
+            const uint64_t upto = first < 63 ? ((2ull << first) - 1) : ~0ull;
+            if (__ballot(flag == 0) & upto) {  // a predecessor in the window has not published yet
+                if (++spins > (1u << 24)) {
+                    if (lane == 0) atomicOr(overflow, 2u);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            uint64_t part = (lane <= first) ? (sv & SLB_MASK) : 0ull;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+            excl += part;
+            if (first < 64) break;
+            look -= 64;
+        }
+        if (lane == 0) {
+            if (bid > 0)
+                __hip_atomic_store(status + bid, SLB_INC | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_excl = excl;
+            if (base <= n && n < bid * SCAN_TILE + SCAN_TILE) {  // the block holding element n writes the total
+                const uint64_t tot = excl + agg;
+                out[n] = (uint32_t)tot;
+                if (tot > 0xffffffffull) atomicOr(overflow, 1u);
+            }
+        }
+    }
+    __syncthreads();
+    uint64_t run = s_excl + (uint64_t)(inc - local);
+    for (int i = 0; i < w; i++) run += s_w[i];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const uint32_t j = base + k;
+        if (j < n) out[j] = (uint32_t)run;
+        run += v[k];
+    }
+}
+
+void launch_exclusive_scan_lookback(hipStream_t s, const uint32_t *in, const uint32_t *idx, uint32_t n, uint32_t *out,
+                                    uint64_t *status, uint32_t *ticket, uint32_t *overflow_flag) {
+    // status (div_up(n + 1, SCAN_TILE) words) and *ticket must be zero (cleared with the forward's counters)
+    const uint32_t nb = div_up(n + 1, (uint32_t)SCAN_TILE);
+    if (idx)
+        scan_lookback_kernel<true><<<nb, 256, 0, s>>>(in, idx, n, out, status, ticket, overflow_flag);
+    else
+        scan_lookback_kernel<false><<<nb, 256, 0, s>>>(in, nullptr, n, out, status, ticket, overflow_flag);
+}
+
 // ------------------------------------------------------------------------------------------------
 // radix sort pass: histogram
 // ------------------------------------------------------------------------------------------------
