@@ -129,9 +129,10 @@ def forward_raw(means3D, sh, colors_precomp, opacities, scales, rotations, cov3D
     campos = _prep(rs.campos, device, "campos")
     M = 0 if sh_c is None else (sh_c.shape[1] if sh_c.ndim == 3 else sh_c.shape[1] // 3)
 
-    color = torch.zeros(3, H, W, dtype=torch.float32, device=device)
-    invdepth = torch.zeros(1, H, W, dtype=torch.float32, device=device)
-    radii = torch.zeros(P, dtype=torch.int32, device=device)
+    # fully written by the library (render_fwd writes every pixel, preprocess every radius; P == 0 clears)
+    color = torch.empty(3, H, W, dtype=torch.float32, device=device)
+    invdepth = torch.empty(1, H, W, dtype=torch.float32, device=device)
+    radii = torch.empty(P, dtype=torch.int32, device=device)
     bufs = _Buffers(device)
     a = _native.ForwardArgs(
         P=P, D=int(rs.sh_degree), M=M, W=W, H=H, background=_ptr(bg), means3D=_ptr(means3D_c),
