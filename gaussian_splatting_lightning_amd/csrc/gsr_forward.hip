@@ -308,59 +308,31 @@ void launch_identify_ranges(hipStream_t s, const uint32_t *keys_sorted, uint32_t
 // and the GPU runs only ~8 tile waves per SIMD, so launching heavy tiles first keeps the tail short.  One
 // workgroup: bucket histogram of the tile weights (8 instances per bucket), descending exclusive scan,
 // scatter.  Order inside a bucket is arbitrary -- it only changes which tile runs when, never a result.
+// (A 1024-bucket variant with ballot-ranked, tile-ordered buckets measured 4 % slower in render_fwd.)
 __global__ __launch_bounds__(1024) void tile_order_kernel(const uint2 *__restrict__ ranges,
-                                                          const uint32_t *__restrict__ tile_last, int use_last,
-                                                          int T, uint32_t *__restrict__ order) {
-    constexpr int NB = 1024;  // 2 instances per bucket, heaviest bucket first
-    __shared__ uint32_t hist[NB];
-    __shared__ uint32_t s_w[16];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    hist[tid] = 0;
+                                                             const uint32_t *__restrict__ tile_last, int use_last,
+                                                             int T, uint32_t *__restrict__ order) {
+    __shared__ uint32_t hist[256];
+    const int tid = threadIdx.x;
+    if (tid < 256) hist[tid] = 0;
     __syncthreads();
     auto bucket = [&](int t) -> uint32_t {
-        const uint32_t wt = use_last ? tile_last[t] : ranges[t].y - ranges[t].x;
-        return (uint32_t)(NB - 1) - min((uint32_t)(NB - 1), wt >> 1);
+        const uint32_t w = use_last ? tile_last[t] : ranges[t].y - ranges[t].x;
+        return 255u - min(255u, w >> 3);  // heaviest first
     };
-    // Tiles sharing a bucket inside a wave are aggregated by ballot (one LDS atomic per distinct bucket), so
-    // the many equally light (e.g. empty) tiles do not serialise on one counter.
-    auto ranked_add = [&](uint32_t b, bool valid, bool want_base) -> uint32_t {
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int bit = 0; bit < 10; bit++) {
-            const bool set = (b >> bit) & 1u;
-            const uint64_t m = __ballot(set);
-            peers &= set ? m : ~m;
-        }
-        const uint64_t lower = peers & lanemask_lt(lane);
-        uint32_t base = 0;
-        if (valid && lower == 0) base = atomicAdd(&hist[b], (uint32_t)__popcll(peers));
-        if (!want_base) return 0;
-        const int leader = peers ? __builtin_ctzll(peers) : 0;
-        return (uint32_t)__shfl((int)base, leader) + (uint32_t)__popcll(lower);
-    };
-    for (int t0 = 0; t0 < T; t0 += 1024) {
-        const int t = t0 + tid;
-        const bool valid = t < T;
-        ranked_add(valid ? bucket(t) : 0u, valid, false);
+    for (int t = tid; t < T; t += 1024) atomicAdd(&hist[bucket(t)], 1u);
+    __syncthreads();
+    if (tid < 64) {  // exclusive scan of the 256 buckets by one wave, 4 per lane
+        const uint32_t a = hist[4 * tid], b = hist[4 * tid + 1], c = hist[4 * tid + 2], d = hist[4 * tid + 3];
+        const uint32_t sum = a + b + c + d;
+        const uint32_t excl = wave_inclusive_scan(sum, tid) - sum;
+        hist[4 * tid] = excl;
+        hist[4 * tid + 1] = excl + a;
+        hist[4 * tid + 2] = excl + a + b;
+        hist[4 * tid + 3] = excl + a + b + c;
     }
     __syncthreads();
-    {  // exclusive scan of the 1024 bucket counts
-        const uint32_t v = hist[tid];
-        const uint32_t inc = wave_inclusive_scan(v, lane);
-        if (lane == 63) s_w[w] = inc;
-        __syncthreads();
-        uint32_t off = 0;
-        for (int i = 0; i < w; i++) off += s_w[i];
-        hist[tid] = off + inc - v;
-    }
-    __syncthreads();
-    for (int t0 = 0; t0 < T; t0 += 1024) {
-        const int t = t0 + tid;
-        const bool valid = t < T;
-        const uint32_t pos = ranked_add(valid ? bucket(t) : 0u, valid, true);
-        if (valid) order[pos] = (uint32_t)t;
-        __syncthreads();  // the next round's atomics read the bases this round advanced
-    }
+    for (int t = tid; t < T; t += 1024) order[atomicAdd(&hist[bucket(t)], 1u)] = (uint32_t)t;
 }
 
 void launch_tile_order(hipStream_t s, const uint2 *ranges, const uint32_t *tile_last, int use_last, int T,
