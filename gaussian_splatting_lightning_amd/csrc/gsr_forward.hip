@@ -311,14 +311,14 @@ void launch_identify_ranges(hipStream_t s, const uint32_t *keys_sorted, uint32_t
 // (A 1024-bucket variant with ballot-ranked, tile-ordered buckets measured 4 % slower in render_fwd.)
 __global__ __launch_bounds__(1024) void tile_order_kernel(const uint2 *__restrict__ ranges,
                                                              const uint32_t *__restrict__ tile_last, int use_last,
-                                                             int T, uint32_t *__restrict__ order) {
+                                                             int T, int shift, uint32_t *__restrict__ order) {
     __shared__ uint32_t hist[256];
     const int tid = threadIdx.x;
     if (tid < 256) hist[tid] = 0;
     __syncthreads();
     auto bucket = [&](int t) -> uint32_t {
         const uint32_t w = use_last ? tile_last[t] : ranges[t].y - ranges[t].x;
-        return 255u - min(255u, w >> 3);  // heaviest first
+        return 255u - min(255u, w >> shift);  // heaviest first
     };
     for (int t = tid; t < T; t += 1024) atomicAdd(&hist[bucket(t)], 1u);
     __syncthreads();
@@ -338,7 +338,7 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint2 *__restric
 void launch_tile_order(hipStream_t s, const uint2 *ranges, const uint32_t *tile_last, int use_last, int T,
                        uint32_t *order) {
     if (T <= 0) return;
-    tile_order_kernel<<<1, 1024, 0, s>>>(ranges, tile_last, use_last, T, order);
+    tile_order_kernel<<<1, 1024, 0, s>>>(ranges, tile_last, use_last, T, tuning("lpt_shift", 3), order);
 }
 
 // ------------------------------------------------------------------------------------------------
