@@ -341,6 +341,10 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     });
     const int lpt = tuning("lpt", 1);
     if (lpt) launch_tile_order(stream, im.ranges, nullptr, 0, (int)T, im.order_fwd);
+    // split heavy tiles combine tile_last / tile_loaded with atomicMax: start from zero (adjacent arrays)
+    GSR_HIP(hipMemsetAsync(im.tile_last, 0,
+                           (size_t)(reinterpret_cast<char *>(im.tile_loaded + T) - reinterpret_cast<char *>(im.tile_last)),
+                           stream));
     RenderFwdParams rp;
     rp.W = W; rp.H = H; rp.gx = gx; rp.gy = gy; rp.num_tiles = (int)T;
     rp.tile_order = lpt ? im.order_fwd : nullptr;

@@ -473,9 +473,131 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_fwd_v3_kernel(Rend
     }
 }
 
+// Split variant: the first 2*nsplit launch slots are the two halves (rows 0-7 / 8-15, 2 pixels per lane) of
+// the nsplit heaviest tiles of the LPT order, the rest are whole tiles.  A heavy tile then finishes in about
+// half the time, shortening the kernel's critical path.  Pixel k of half h is the whole-tile pixel 2h + k with
+// the same dy rounding, so outputs are bitwise those of the whole-tile path; the halves combine tile_last /
+// tile_loaded with atomicMax on zeroed words.
+template <int NPIX>
+__device__ __forceinline__ void composite_fwd(const RenderFwdParams &p, const int tile, const int half,
+                                              const int lane, float4 *s_a, float4 *s_b, float2 *s_c) {
+    const int tx = tile % p.gx, ty = tile / p.gx;
+    const int px = tx * BLOCK_X + (lane & 15);
+    const int py0 = ty * BLOCK_Y + (lane >> 4);
+    const float pfx = (float)px, pfy0 = (float)py0;
+    const int kbase = NPIX == 4 ? 0 : 2 * half;  // whole-tile pixel index of this wave's first pixel
+    float T[NPIX], C0[NPIX], C1[NPIX], C2[NPIX], ID[NPIX];
+    uint32_t last[NPIX];
+    bool active[NPIX];
+#pragma unroll
+    for (int k = 0; k < NPIX; k++) {
+        const int py = py0 + 4 * (kbase + k);
+        active[k] = px < p.W && py < p.H;
+        T[k] = 1.0f;
+        C0[k] = C1[k] = C2[k] = ID[k] = 0.f;
+        last[k] = 0;
+    }
+    const uint2 range = p.ranges[tile];
+    uint32_t contributor = 0;
+    uint32_t loaded_end = range.x;
+    for (uint32_t base = range.x; base < range.y; base += 64) {
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < NPIX; k++) any |= active[k];
+        if (__ballot(any) == 0) break;
+        const uint32_t s = base + lane;
+        if (s < range.y) {
+            const uint32_t u = p.sorted_u[s];
+            const uint32_t gid = p.inst_gid[u];
+            p.point_list[s] = gid;
+            p.inv[u] = s;
+            s_a[lane] = stage_rec_a(p.rec_a[gid]);
+            s_b[lane] = stage_rec_b(p.rec_b[gid]);
+            s_c[lane] = p.rec_c[gid];
+        }
+        loaded_end = min(range.y, base + 64u);
+        wave_lds_sync();
+        const int cnt = (int)min(64u, range.y - base);
+        for (int j = 0; j < cnt; j++) {
+            const float4 a = s_a[j], b = s_b[j];
+            const float2 c = s_c[j];
+            contributor++;
+            bool still = false;
+            const float dx = a.x - pfx, dy0 = a.y - pfy0;
+            const float P0 = (a.z * dx) * dx, L = a.w * dx;
+#pragma unroll
+            for (int k = 0; k < NPIX; k++) {
+                const float power2 = power2_at(b.x, dy0 - (float)(4 * (kbase + k)), P0, L);
+                const float alpha = fminf(0.99f, b.y * __builtin_amdgcn_exp2f(power2));
+                const bool ok = active[k] && !(power2 > 0.0f) && !(alpha < 1.0f / 255.0f);
+                const float test_T = T[k] * (1 - alpha);
+                const bool stop = ok && test_T < 0.0001f;
+                const bool take = ok && !stop;
+                const float wgt = take ? alpha * T[k] : 0.f;
+                C0[k] = fmaf(b.z, wgt, C0[k]);
+                C1[k] = fmaf(b.w, wgt, C1[k]);
+                C2[k] = fmaf(c.x, wgt, C2[k]);
+                ID[k] = fmaf(c.y, wgt, ID[k]);
+                T[k] = take ? test_T : T[k];
+                last[k] = take ? contributor : last[k];
+                active[k] = active[k] && !stop;
+                still |= active[k];
+            }
+            if (__ballot(still) == 0) break;
+        }
+        wave_lds_sync();
+    }
+    const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
+    const size_t HW = (size_t)p.W * p.H;
+    uint32_t mx = 0;
+#pragma unroll
+    for (int k = 0; k < NPIX; k++) {
+        const int py = py0 + 4 * (kbase + k);
+        if (px < p.W && py < p.H) {
+            const size_t pid = (size_t)py * p.W + px;
+            p.final_T[pid] = T[k];
+            p.n_contrib[pid] = last[k];
+            p.out_color[pid] = C0[k] + T[k] * bg0;
+            p.out_color[HW + pid] = C1[k] + T[k] * bg1;
+            p.out_color[2 * HW + pid] = C2[k] + T[k] * bg2;
+            if (p.out_invdepth) p.out_invdepth[pid] = ID[k];
+            mx = max(mx, last[k]);
+        }
+    }
+    mx = wave_max_u32(mx);
+    if (lane == 0) {
+        if (NPIX == 4) {
+            p.tile_last[tile] = mx;
+            p.tile_loaded[tile] = loaded_end - range.x;
+        } else {
+            atomicMax(&p.tile_last[tile], mx);
+            atomicMax(&p.tile_loaded[tile], loaded_end - range.x);
+        }
+    }
+}
+
+template <int MIN_WAVES>
+__global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_split_kernel(RenderFwdParams p, int nsplit) {
+    __shared__ float4 s_a[4][64];
+    __shared__ float4 s_b[4][64];
+    __shared__ float2 s_c[4][64];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int slot = blockIdx.x * 4 + w;
+    if (slot >= p.num_tiles + nsplit) return;
+    if (slot < 2 * nsplit)
+        composite_fwd<2>(p, (int)p.tile_order[slot >> 1], slot & 1, lane, s_a[w], s_b[w], s_c[w]);
+    else
+        composite_fwd<4>(p, (int)p.tile_order[slot - nsplit], 0, lane, s_a[w], s_b[w], s_c[w]);
+}
+
 void launch_render_fwd(hipStream_t s, const RenderFwdParams &p) {
     if (p.num_tiles <= 0) return;
     const dim3 grid(div_up(p.num_tiles, 4)), block(256);
+    const int nsplit = p.tile_order ? (int)((int64_t)p.num_tiles * tuning("fwd_split_pct", 5) / 100) : 0;
+    if (nsplit > 0) {
+        render_fwd_split_kernel<4><<<div_up(p.num_tiles + nsplit, 4), 256, 0, s>>>(p, nsplit);
+        return;
+    }
     const int pipe = tuning("fwd_pipe", 0), wpb = tuning("fwd_wpb", 4);
     if (wpb == 1) {
         const dim3 g1(p.num_tiles), b1(64);
