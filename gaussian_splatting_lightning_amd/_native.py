@@ -44,6 +44,28 @@ class BackwardArgs(ctypes.Structure):
     ]
 
 
+class AdamGroup(ctypes.Structure):
+    _fields_ = [("param", _fp), ("grad", _fp), ("exp_avg", _fp), ("exp_avg_sq", _fp), ("n", ctypes.c_int64),
+                ("lr", ctypes.c_double), ("step", ctypes.c_int64)]
+
+
+class DensifyArgs(ctypes.Structure):
+    _fields_ = [("N", ctypes.c_int64), ("opacity", _fp), ("scaling", _fp), ("max_radii2D", _fp),
+                ("xyz_grad_accum", _fp), ("xyz_grad_count", _fp),
+                ("opacity_threshold", ctypes.c_float), ("screensize_threshold", ctypes.c_float),
+                ("size_threshold", ctypes.c_float), ("grad_threshold", ctypes.c_float),
+                ("clone_size_threshold", ctypes.c_float),
+                ("apply_screensize", ctypes.c_int), ("apply_size", ctypes.c_int)]
+
+
+class DensifyField(ctypes.Structure):
+    _fields_ = [("src", _fp), ("dst", _fp), ("src_exp_avg", _fp), ("src_exp_avg_sq", _fp),
+                ("dst_exp_avg", _fp), ("dst_exp_avg_sq", _fp), ("width", ctypes.c_int), ("kind", ctypes.c_int)]
+
+
+FIELD_PLAIN, FIELD_XYZ, FIELD_SCALING, FIELD_STAT = 0, 1, 2, 3
+
+
 class StateLayout(ctypes.Structure):
     _fields_ = [(n, ctypes.c_size_t) for n in (
         "geom_rec_a", "geom_rec_b", "geom_rec_c", "geom_tiles", "geom_order", "geom_inst_off", "geom_inst_start",
@@ -57,7 +79,8 @@ EXPORTED_SYMBOLS = (
     "gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_sh_backward_views", "gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes",
     "gsr_image_buffer_bytes", "gsr_bwd_scratch_bytes", "gsr_set_profiling", "gsr_num_stages", "gsr_stage_name",
     "gsr_stage_times", "gsr_reset_stage_times", "gsr_last_error", "gsr_build_info", "gsr_state_layout_query",
-    "gsr_set_tuning", "gsr_ssim_num_partials", "gsr_ssim_forward", "gsr_ssim_backward",
+    "gsr_set_tuning", "gsr_ssim_num_partials", "gsr_ssim_forward", "gsr_ssim_backward", "gsr_adam_step",
+    "gsr_densify_workspace_bytes", "gsr_densify_classify", "gsr_densify_apply",
 )
 
 _lib = None
@@ -84,6 +107,17 @@ def load(path: str | None = None):
     lib.gsr_sh_backward_views.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _fp, _fp, _fp, _fp,
                                           ctypes.c_void_p]
     lib.gsr_sh_backward_views.restype = ctypes.c_int
+    lib.gsr_adam_step.argtypes = [ctypes.POINTER(AdamGroup), ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                  ctypes.c_double, ctypes.c_void_p]
+    lib.gsr_adam_step.restype = ctypes.c_int
+    lib.gsr_densify_workspace_bytes.argtypes = [ctypes.c_int64]
+    lib.gsr_densify_workspace_bytes.restype = ctypes.c_size_t
+    lib.gsr_densify_classify.argtypes = [ctypes.POINTER(DensifyArgs), ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p]
+    lib.gsr_densify_classify.restype = ctypes.c_int
+    lib.gsr_densify_apply.argtypes = [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.POINTER(DensifyField), ctypes.c_int, ctypes.c_void_p]
+    lib.gsr_densify_apply.restype = ctypes.c_int
     lib.gsr_ssim_num_partials.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
     lib.gsr_ssim_num_partials.restype = ctypes.c_size_t
     lib.gsr_ssim_forward.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _fp, _fp, ctypes.c_int, _fp, _fp, _fp,

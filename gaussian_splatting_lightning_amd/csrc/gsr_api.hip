@@ -7,6 +7,7 @@
 // ranges -> composite; backward: reverse composite -> big-Gaussian reduce -> preprocess backward.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -453,6 +454,117 @@ int gsr_sh_backward_views(int P, int D, int M, int V, const float *means3D, cons
     if (!means3D || !dL_dsh || (V > 0 && (!campos || !dL_dcolors_sh))) return fail(GSR_ERR_ARG, "null argument");
     hipStream_t stream = (hipStream_t)stream_ptr;
     GSR_STAGE(ST_SH_VIEWS, 0, launch_sh_backward_views(stream, P, D, M, V, means3D, campos, dL_dcolors_sh, dL_dsh));
+    return GSR_OK;
+}
+
+int gsr_adam_step(const gsr_adam_group *groups, int num_groups, double beta1, double beta2, double eps,
+                  void *stream_ptr) {
+    if (num_groups < 0 || num_groups > ADAM_MAX_GROUPS) return fail(GSR_ERR_ARG, "adam: 0..16 parameter groups");
+    if (num_groups && !groups) return fail(GSR_ERR_ARG, "adam: null groups");
+    AdamLaunch L{};
+    int64_t slices = 0;
+    int ng = 0;
+    for (int i = 0; i < num_groups; i++) {
+        const gsr_adam_group &g = groups[i];
+        if (g.n < 0 || g.step < 1) return fail(GSR_ERR_ARG, "adam: n must be >= 0 and step >= 1");
+        if (g.n == 0) continue;
+        if (!g.param || !g.grad || !g.exp_avg || !g.exp_avg_sq) return fail(GSR_ERR_ARG, "adam: null array");
+        AdamGroupDev &d = L.g[ng];
+        d.param = g.param; d.grad = g.grad; d.exp_avg = g.exp_avg; d.exp_avg_sq = g.exp_avg_sq; d.n = g.n;
+        const double bc1 = 1.0 - std::pow(beta1, (double)g.step), bc2 = 1.0 - std::pow(beta2, (double)g.step);
+        d.step_size = (float)(g.lr / bc1);
+        d.bc2_sqrt = (float)std::sqrt(bc2);
+        d.vec4 = ((((uintptr_t)g.param) | ((uintptr_t)g.grad) | ((uintptr_t)g.exp_avg) |
+                   ((uintptr_t)g.exp_avg_sq)) & 15) == 0;
+        L.slice_start[ng] = slices;
+        slices += adam_slices(g.n);
+        ng++;
+    }
+    if (slices > 0x7fffffffLL) return fail(GSR_ERR_ARG, "adam: too many elements");
+    L.num_groups = ng;
+    L.one_minus_beta1 = (float)(1.0 - beta1);
+    L.beta2 = (float)beta2;
+    L.one_minus_beta2 = (float)(1.0 - beta2);
+    L.eps = (float)eps;
+    launch_adam((hipStream_t)stream_ptr, L, slices);
+    GSR_HIP(hipGetLastError());
+    return GSR_OK;
+}
+
+// densify workspace: [dst_map 2N i32 | split_rank N i32 | block_counts 3*blocks i32 | row_class N u8]
+static size_t densify_ws(int64_t N, size_t *o_rank, size_t *o_blk, size_t *o_cls) {
+    const size_t nb = (size_t)densify_blocks(N);
+    *o_rank = align_up((size_t)N * 8, 256);
+    *o_blk = *o_rank + align_up((size_t)N * 4, 256);
+    *o_cls = *o_blk + align_up(nb * 12, 256);
+    return *o_cls + align_up((size_t)N, 256);
+}
+
+size_t gsr_densify_workspace_bytes(int64_t N) {
+    size_t a, b, c;
+    return N < 0 ? 0 : densify_ws(N, &a, &b, &c);
+}
+
+int gsr_densify_classify(const gsr_densify_args *args, void *workspace, int32_t *counts, int64_t *preserve_idx,
+                         void *stream_ptr) {
+    if (!args || args->N < 0 || args->N > 0x7fffffffLL) return fail(GSR_ERR_ARG, "densify: 0 <= N < 2^31");
+    if (!counts) return fail(GSR_ERR_ARG, "densify: null counts");
+    DensifyParams p{};
+    p.N = args->N;
+    if (p.N > 0 && (!args->opacity || !args->scaling || !args->xyz_grad_accum || !args->xyz_grad_count ||
+                    !workspace || !preserve_idx || (args->apply_screensize && !args->max_radii2D)))
+        return fail(GSR_ERR_ARG, "densify: null input");
+    size_t o_rank, o_blk, o_cls;
+    densify_ws(p.N, &o_rank, &o_blk, &o_cls);
+    char *ws = (char *)workspace;
+    p.opacity = args->opacity; p.scaling = args->scaling; p.max_radii2D = args->max_radii2D;
+    p.grad_accum = args->xyz_grad_accum; p.grad_count = args->xyz_grad_count;
+    p.opacity_threshold = args->opacity_threshold; p.screensize_threshold = args->screensize_threshold;
+    p.size_threshold = args->size_threshold; p.grad_threshold = args->grad_threshold;
+    p.clone_size_threshold = args->clone_size_threshold;
+    p.apply_screensize = args->apply_screensize; p.apply_size = args->apply_size;
+    p.dst_map = (int32_t *)ws;
+    p.split_rank = (int32_t *)(ws + o_rank);
+    p.block_counts = (int32_t *)(ws + o_blk);
+    p.row_class = (uint8_t *)(ws + o_cls);
+    p.counts = counts;
+    p.preserve_idx = preserve_idx;
+    launch_densify_classify((hipStream_t)stream_ptr, p);
+    GSR_HIP(hipGetLastError());
+    return GSR_OK;
+}
+
+int gsr_densify_apply(int64_t N, const void *workspace, const float *rotation, const float *scaling, const float *z,
+                      const gsr_densify_field *fields, int num_fields, void *stream_ptr) {
+    if (N < 0 || N > 0x7fffffffLL) return fail(GSR_ERR_ARG, "densify: 0 <= N < 2^31");
+    if (num_fields < 0 || num_fields > DENSIFY_MAX_FIELDS) return fail(GSR_ERR_ARG, "densify: 0..16 fields");
+    if (N == 0 || num_fields == 0) return GSR_OK;
+    if (!workspace || !fields || !rotation || !scaling) return fail(GSR_ERR_ARG, "densify: null input");
+    size_t o_rank, o_blk, o_cls;
+    densify_ws(N, &o_rank, &o_blk, &o_cls);
+    DensifyApply A{};
+    A.N = N;
+    A.dst_map = (const int32_t *)workspace;
+    A.split_rank = (const int32_t *)((const char *)workspace + o_rank);
+    A.z = z; A.rotation = rotation; A.scaling = scaling;
+    int64_t blocks = 0;
+    for (int i = 0; i < num_fields; i++) {
+        const gsr_densify_field &f = fields[i];
+        if (f.width <= 0 || !f.src || !f.dst) return fail(GSR_ERR_ARG, "densify: field needs src, dst, width > 0");
+        if (f.kind < GSR_FIELD_PLAIN || f.kind > GSR_FIELD_STAT) return fail(GSR_ERR_ARG, "densify: bad kind");
+        if (f.kind == GSR_FIELD_XYZ && f.width != 3) return fail(GSR_ERR_ARG, "densify: xyz field width must be 3");
+        if ((f.dst_exp_avg && !f.src_exp_avg) || (f.dst_exp_avg_sq && !f.src_exp_avg_sq))
+            return fail(GSR_ERR_ARG, "densify: moment destination without source");
+        DensifyFieldDev &d = A.f[i];
+        d.src = f.src; d.dst = f.dst; d.src_exp_avg = f.src_exp_avg; d.src_exp_avg_sq = f.src_exp_avg_sq;
+        d.dst_exp_avg = f.dst_exp_avg; d.dst_exp_avg_sq = f.dst_exp_avg_sq; d.width = f.width; d.kind = f.kind;
+        A.block_start[i] = blocks;
+        blocks += (N * f.width + 255) / 256;
+    }
+    if (blocks > 0x7fffffffLL) return fail(GSR_ERR_ARG, "densify: too many elements");
+    A.num_fields = num_fields;
+    launch_densify_apply((hipStream_t)stream_ptr, A, blocks);
+    GSR_HIP(hipGetLastError());
     return GSR_OK;
 }
 

@@ -111,6 +111,56 @@ void launch_preprocess_bwd(hipStream_t s, const PreprocessBwdParams &p);
 void launch_sh_backward_views(hipStream_t s, int P, int D, int M, int V, const float *means3D, const float *campos,
                               const float *dcolors_sh, float *dsh);
 
+// ---- fused Adam (gsr_adam.hip) ----
+constexpr int ADAM_MAX_GROUPS = 16;
+struct AdamGroupDev {
+    float *param;
+    const float *grad;
+    float *exp_avg, *exp_avg_sq;
+    int64_t n;
+    float step_size, bc2_sqrt;
+    int vec4;
+};
+struct AdamLaunch {
+    AdamGroupDev g[ADAM_MAX_GROUPS];
+    int64_t slice_start[ADAM_MAX_GROUPS];
+    int num_groups;
+    float one_minus_beta1, beta2, one_minus_beta2, eps;
+};
+int64_t adam_slices(int64_t n);
+void launch_adam(hipStream_t s, const AdamLaunch &L, int64_t total_slices);
+
+// ---- densify_and_prune (gsr_densify.hip) ----
+struct DensifyParams {
+    int64_t N;
+    const float *opacity, *scaling, *max_radii2D, *grad_accum, *grad_count;
+    float opacity_threshold, screensize_threshold, size_threshold, grad_threshold, clone_size_threshold;
+    int apply_screensize, apply_size;
+    uint8_t *row_class;      // (N)
+    int32_t *block_counts;   // (3 * blocks)
+    int32_t *counts;         // (3): kept, cloned, split
+    int32_t *dst_map;        // (2N): kept row destination | appended copy destination (-1 = none)
+    int32_t *split_rank;     // (N)
+    int64_t *preserve_idx;   // (N): first counts[0] entries valid
+};
+constexpr int DENSIFY_MAX_FIELDS = 16;
+struct DensifyFieldDev {
+    const float *src, *src_exp_avg, *src_exp_avg_sq;
+    float *dst, *dst_exp_avg, *dst_exp_avg_sq;
+    int width, kind;
+};
+struct DensifyApply {
+    DensifyFieldDev f[DENSIFY_MAX_FIELDS];
+    int64_t block_start[DENSIFY_MAX_FIELDS];
+    int num_fields;
+    int64_t N;
+    const int32_t *dst_map, *split_rank;
+    const float *z, *rotation, *scaling;
+};
+int64_t densify_blocks(int64_t N);
+void launch_densify_classify(hipStream_t s, const DensifyParams &p);
+void launch_densify_apply(hipStream_t s, const DensifyApply &A, int64_t total_blocks);
+
 // ---- fused SSIM loss (gsr_ssim.hip) ----
 size_t ssim_num_partials(int planes, int H, int W);
 void launch_ssim_forward(hipStream_t s, int planes, int H, int W, const float *img1, const float *img2, int valid,

@@ -149,6 +149,59 @@ int gsr_ssim_backward(int planes, int H, int W, const float *img1, const float *
                       const float *dL_dmean, const float *dm_dmu1, const float *dm_dsigma1_sq,
                       const float *dm_dsigma12, float *dL_dimg1, void *stream);
 
+/* Fused Adam step over up to 16 parameter groups in one launch -- replaces the torch.optim.Adam(eps=1e-15)
+ * step of the reference's six Gaussian parameter groups (gs_lightning_module.py:114-134).  All arrays are
+ * contiguous fp32 device arrays of n elements, updated in place; step is the 1-based step count of each
+ * group (torch keeps it per parameter).  No weight decay, no amsgrad, as configured by the reference. */
+typedef struct gsr_adam_group {
+    float *param;
+    const float *grad;
+    float *exp_avg, *exp_avg_sq;
+    int64_t n;
+    double lr;
+    int64_t step;
+} gsr_adam_group;
+int gsr_adam_step(const gsr_adam_group *groups, int num_groups, double beta1, double beta2, double eps, void *stream);
+
+/* densify_and_prune of gs_lightning/modules/gaussian_model.py:184-287 with the optimizer-state re-indexing of
+ * gs_lightning_module.py:213-235, in two calls:
+ *   gsr_densify_classify  classifies every row (prune / keep / clone / split) and builds the row maps;
+ *                         counts[0..2] (device) = rows kept, rows cloned, rows split.  The caller reads the
+ *                         counts back, allocates outputs of N_new = kept + cloned + split rows and draws
+ *                         z ~ N(0, 1) of shape (split, 3);
+ *   gsr_densify_apply     scatters every field (parameters, Adam moments, statistics) into the new arrays.
+ * Thresholds are absolute (the reference's *_threshold * spatial_scale already applied). */
+typedef struct gsr_densify_args {
+    int64_t N;
+    const float *opacity;       /* (N) raw (pre-sigmoid) */
+    const float *scaling;       /* (N,3) raw (log) */
+    const float *max_radii2D;   /* (N) */
+    const float *xyz_grad_accum, *xyz_grad_count;  /* (N) */
+    float opacity_threshold;    /* prune unless sigmoid(opacity) > threshold */
+    float screensize_threshold; /* with apply_screensize: prune unless max_radii2D < threshold */
+    float size_threshold;       /* with apply_size: prune unless max(exp(scaling)) < threshold */
+    float grad_threshold;       /* clone/split if accum / count >= threshold */
+    float clone_size_threshold; /* clone if max(exp(scaling)) < threshold, split otherwise */
+    int apply_screensize, apply_size;
+} gsr_densify_args;
+size_t gsr_densify_workspace_bytes(int64_t N);
+/* preserve_idx (N int64): the first counts[0] entries are the kept row indices (the reference's return value). */
+int gsr_densify_classify(const gsr_densify_args *args, void *workspace, int32_t *counts, int64_t *preserve_idx,
+                         void *stream);
+
+enum { GSR_FIELD_PLAIN = 0, GSR_FIELD_XYZ = 1, GSR_FIELD_SCALING = 2, GSR_FIELD_STAT = 3 };
+typedef struct gsr_densify_field {
+    const float *src; /* (N, width) */
+    float *dst;       /* (N_new, width) */
+    const float *src_exp_avg, *src_exp_avg_sq; /* NULL when the parameter has no optimizer state */
+    float *dst_exp_avg, *dst_exp_avg_sq;
+    int width;
+    int kind; /* XYZ: split rows move by R(q)(z*exp(scaling)); SCALING: log(exp(s)/1.6); STAT: zero on copies */
+} gsr_densify_field;
+/* rotation (N,4) raw quaternions (w,x,y,z), scaling (N,3) raw, z (split,3): the rows the split moves */
+int gsr_densify_apply(int64_t N, const void *workspace, const float *rotation, const float *scaling, const float *z,
+                      const gsr_densify_field *fields, int num_fields, void *stream);
+
 /* Buffer sizes the forward will request (host-only arithmetic; for planning and tests). */
 size_t gsr_geom_buffer_bytes(int P);
 size_t gsr_binning_buffer_bytes(int64_t R, int W, int H);

@@ -1,0 +1,175 @@
+#!/usr/bin/env python
+"""Per-step optimizer and densification cost at the cfg3 scale (1M Gaussians, SH degree 3).
+
+* Adam: GaussianAdam.step() (one fused launch over the six groups) vs torch.optim.Adam (foreach, the
+  reference's optimizer) on the same parameters.  Algorithmic bytes per element: read param, grad, exp_avg,
+  exp_avg_sq (16 B) + write param, exp_avg, exp_avg_sq (12 B) = 28 B; 59 floats per Gaussian.
+* densify_and_prune (+ optimizer-state re-indexing): gaussian_splatting_lightning_amd.densify vs the
+  reference's torch op sequence (gaussian_model.py:184-287 + gs_lightning_module.py:213-235) on the GPU.
+  Algorithmic bytes: read N rows of 59 params + 118 moments + 3 stats (180 floats) and write the N_new rows.
+Times are hipEvent averages on the current stream (host sync of the row counts included for densify).
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+NAMES = ("xyz", "features_dc", "features_rest", "opacity", "scaling", "rotation")
+SHAPES = dict(xyz=(3,), features_dc=(1, 3), features_rest=(15, 3), opacity=(1,), scaling=(3,), rotation=(4,))
+LRS = dict(xyz=1.6e-4, features_dc=2.5e-3, features_rest=1.25e-4, opacity=0.025, scaling=5e-3, rotation=1e-3)
+
+
+def timed(fn, n, torch):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n
+
+
+def make_model(N, torch, nn, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+
+    class M(nn.Module):
+        pass
+
+    m = M()
+    for k in NAMES:
+        t = torch.randn((N,) + SHAPES[k], device="cuda", generator=g)
+        if k == "scaling":
+            t = t * 1.5 - 4.5
+        if k == "opacity":
+            t = t * 2.0
+        setattr(m, f"_{k}", nn.Parameter(t))
+    cnt = torch.randint(0, 6, (N,), device="cuda", generator=g).float()
+    m.max_radii2D = torch.rand(N, device="cuda", generator=g) * 40
+    m.xyz_grad_accum = cnt * torch.rand(N, device="cuda", generator=g) * 4e-4
+    m.xyz_grad_count = cnt
+    m.spatial_scale = 1.0
+    m.use_screensize_threshold = True
+    return m
+
+
+def optimizer(m, cls):
+    return cls([{"params": [getattr(m, f"_{k}")], "lr": LRS[k], "name": k} for k in NAMES], lr=0.0, eps=1e-15)
+
+
+def reference_densify(m, opt, thr, torch, nn):
+    """gaussian_model.py:184-287 + gs_lightning_module.py:213-235 as torch ops (kornia matrix written out)."""
+    grad_t, clone_t, op_t, size_t, ss_t = thr
+    keep = (torch.sigmoid(m._opacity) > op_t).squeeze(-1)
+    keep = torch.logical_and(keep, m.max_radii2D < ss_t)
+    keep = torch.logical_and(keep, torch.max(torch.exp(m._scaling), dim=1)[0] < size_t * m.spatial_scale)
+    for k in NAMES:
+        setattr(m, f"_{k}", nn.Parameter(getattr(m, f"_{k}")[keep]))
+    m.max_radii2D, m.xyz_grad_accum, m.xyz_grad_count = (m.max_radii2D[keep], m.xyz_grad_accum[keep],
+                                                         m.xyz_grad_count[keep])
+    preserve_idx = keep.nonzero().squeeze(-1)
+    xyz_grad = m.xyz_grad_accum / m.xyz_grad_count
+    xyz_grad[xyz_grad.isnan()] = 0.0
+    bad = xyz_grad >= grad_t
+    size = torch.max(torch.exp(m._scaling), dim=1)[0]
+    small = torch.logical_and(bad, size < clone_t).nonzero().squeeze(-1)
+    large = torch.logical_and(bad, size >= clone_t).nonzero().squeeze(-1)
+
+    def add(rows):
+        n = len(rows["xyz"])
+        for k in NAMES:
+            setattr(m, f"_{k}", nn.Parameter(torch.cat([getattr(m, f"_{k}"), rows[k]], 0)))
+        m.max_radii2D = torch.cat([m.max_radii2D, torch.zeros(n, device="cuda")])
+        m.xyz_grad_accum = torch.cat([m.xyz_grad_accum, torch.zeros(n, device="cuda")])
+        m.xyz_grad_count = torch.cat([m.xyz_grad_count, torch.zeros(n, device="cuda")])
+
+    with torch.no_grad():
+        add({k: getattr(m, f"_{k}")[small].clone() for k in NAMES})
+        std = torch.exp(m._scaling)[large]
+        disp = torch.normal(mean=torch.zeros_like(m._xyz[large]), std=std)
+        q = torch.nn.functional.normalize(m._rotation)[large]
+        w, x, y, z = q.unbind(-1)
+        R = torch.stack([1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+                         2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+                         2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)], -1).view(-1, 3, 3)
+        m._xyz[large] = m._xyz[large] + torch.bmm(R, disp.unsqueeze(-1)).squeeze(-1)
+        m._scaling[large] = torch.log(torch.exp(m._scaling[large]) / 1.6)
+        add({k: getattr(m, f"_{k}")[large].clone() for k in NAMES})
+    for group in opt.param_groups:
+        k = group["name"]
+        new_p = getattr(m, f"_{k}")
+        st = opt.state.get(group["params"][0], None)
+        diff = len(new_p) - len(preserve_idx)
+        st["exp_avg"] = torch.cat([st["exp_avg"][preserve_idx], torch.zeros((diff,) + st["exp_avg"].shape[1:],
+                                                                            device="cuda")])
+        st["exp_avg_sq"] = torch.cat([st["exp_avg_sq"][preserve_idx],
+                                      torch.zeros((diff,) + st["exp_avg_sq"].shape[1:], device="cuda")])
+        del opt.state[group["params"][0]]
+        group["params"][0] = new_p
+        opt.state[new_p] = st
+
+
+def main():
+    import torch
+    from torch import nn
+    from gaussian_splatting_lightning_amd.densify import densify_and_prune
+    from gaussian_splatting_lightning_amd.optim import GaussianAdam
+    N = int(os.environ.get("GSR_TRAIN_OPS_N", 1_000_000))
+    out = {"workload": f"{N} Gaussians, SH degree 3 (59 floats each), fp32"}
+
+    # ---- Adam ----
+    res = {}
+    for name, cls in (("fused", GaussianAdam), ("torch_foreach", torch.optim.Adam)):
+        m = make_model(N, torch, nn)
+        opt = optimizer(m, cls)
+        for k in NAMES:
+            p = getattr(m, f"_{k}")
+            p.grad = torch.randn_like(p)
+        res[name] = timed(opt.step, 50, torch)
+    elems = 59 * N
+    algo = 28 * elems
+    out["adam"] = {"ms_fused": round(res["fused"], 4), "ms_torch_adam": round(res["torch_foreach"], 4),
+                   "speedup": round(res["torch_foreach"] / res["fused"], 2), "algorithmic_bytes": algo,
+                   "achieved_GBps": round(algo / (res["fused"] * 1e-3) / 1e9, 1), "hbm_peak_GBps": 8000.0,
+                   "frac": round(algo / (res["fused"] * 1e-3) / 1e9 / 8000.0, 4)}
+
+    # ---- densify_and_prune + optimizer re-indexing (fresh model per run: the op changes N) ----
+    thr = (0.0002, 0.01, 0.05, 0.4, 20.0)
+    dres = {}
+    n_new = None
+    for name in ("fused", "reference_torch"):
+        times = []
+        for rep in range(6):
+            m = make_model(N, torch, nn, seed=rep)
+            opt = optimizer(m, GaussianAdam)
+            for k in NAMES:
+                p = getattr(m, f"_{k}")
+                opt.state[p] = dict(step=torch.tensor(1.0), exp_avg=torch.randn_like(p), exp_avg_sq=torch.rand_like(p))
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            if name == "fused":
+                densify_and_prune(m, *thr, optimizer=opt)
+            else:
+                reference_densify(m, opt, thr, torch, nn)
+            e1.record()
+            torch.cuda.synchronize()
+            if rep >= 1:
+                times.append(e0.elapsed_time(e1))
+            n_new = len(m._xyz)
+        dres[name] = sum(times) / len(times)
+    algo_d = 4 * (180 * N + 180 * n_new)
+    out["densify"] = {"ms_fused": round(dres["fused"], 4), "ms_reference_torch": round(dres["reference_torch"], 4),
+                      "speedup": round(dres["reference_torch"] / dres["fused"], 2), "N_in": N, "N_out": n_new,
+                      "algorithmic_bytes": algo_d,
+                      "achieved_GBps": round(algo_d / (dres["fused"] * 1e-3) / 1e9, 1), "hbm_peak_GBps": 8000.0,
+                      "frac": round(algo_d / (dres["fused"] * 1e-3) / 1e9 / 8000.0, 4),
+                      "note": "includes the host read-back of the three row counts and output allocation"}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
