@@ -66,6 +66,16 @@ class DensifyField(ctypes.Structure):
 FIELD_PLAIN, FIELD_XYZ, FIELD_SCALING, FIELD_STAT = 0, 1, 2, 3
 
 
+class PlyColumn(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_int32), ("type", ctypes.c_int32)]
+
+
+# GSR_PLY_* type codes by PLY type name (both spellings of the PLY spec)
+PLY_TYPES = {"float": 0, "float32": 0, "double": 1, "float64": 1, "uchar": 2, "uint8": 2, "char": 3, "int8": 3,
+             "ushort": 4, "uint16": 4, "short": 5, "int16": 5, "uint": 6, "uint32": 6, "int": 7, "int32": 7}
+PLY_TYPE_SIZE = (4, 8, 1, 1, 2, 2, 4, 4)
+
+
 class StateLayout(ctypes.Structure):
     _fields_ = [(n, ctypes.c_size_t) for n in (
         "geom_rec_a", "geom_rec_b", "geom_rec_c", "geom_tiles", "geom_order", "geom_inst_off", "geom_inst_start",
@@ -80,7 +90,7 @@ EXPORTED_SYMBOLS = (
     "gsr_image_buffer_bytes", "gsr_bwd_scratch_bytes", "gsr_set_profiling", "gsr_num_stages", "gsr_stage_name",
     "gsr_stage_times", "gsr_reset_stage_times", "gsr_last_error", "gsr_build_info", "gsr_state_layout_query",
     "gsr_set_tuning", "gsr_ssim_num_partials", "gsr_ssim_forward", "gsr_ssim_backward", "gsr_adam_step",
-    "gsr_densify_workspace_bytes", "gsr_densify_classify", "gsr_densify_apply",
+    "gsr_densify_workspace_bytes", "gsr_densify_classify", "gsr_densify_apply", "gsr_ply_unpack", "gsr_ply_pack",
 )
 
 _lib = None
@@ -118,6 +128,11 @@ def load(path: str | None = None):
     lib.gsr_densify_apply.argtypes = [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.POINTER(DensifyField), ctypes.c_int, ctypes.c_void_p]
     lib.gsr_densify_apply.restype = ctypes.c_int
+    for fn in (lib.gsr_ply_unpack, lib.gsr_ply_pack):
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(PlyColumn),
+                       ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                       ctypes.c_void_p]
+        fn.restype = ctypes.c_int
     lib.gsr_ssim_num_partials.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
     lib.gsr_ssim_num_partials.restype = ctypes.c_size_t
     lib.gsr_ssim_forward.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _fp, _fp, ctypes.c_int, _fp, _fp, _fp,

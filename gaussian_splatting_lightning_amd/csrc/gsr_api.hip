@@ -568,6 +568,62 @@ int gsr_densify_apply(int64_t N, const void *workspace, const float *rotation, c
     return GSR_OK;
 }
 
+static int ply_setup(PlyLaunch &p, int64_t n, int record_bytes, int big_endian, const gsr_ply_column *columns,
+                     int num_columns, const float *const *fields, const int *widths, int num_fields, bool pack) {
+    if (n < 0 || record_bytes <= 0 || record_bytes > 48 * 1024) return fail(GSR_ERR_ARG, "ply: bad n or record size");
+    if (num_columns < 0 || num_columns > PLY_MAX_COLS) return fail(GSR_ERR_ARG, "ply: at most 128 columns");
+    if (num_fields < 0 || num_fields > PLY_MAX_FIELDS) return fail(GSR_ERR_ARG, "ply: at most 8 fields");
+    if ((num_columns && !columns) || (num_fields && (!fields || !widths))) return fail(GSR_ERR_ARG, "ply: null table");
+    int sum = 0;
+    for (int f = 0; f < num_fields; f++) {
+        if (widths[f] <= 0 || (n > 0 && !fields[f])) return fail(GSR_ERR_ARG, "ply: field needs width > 0 and data");
+        p.field[f] = const_cast<float *>(fields[f]);
+        p.width[f] = widths[f];
+        sum += widths[f];
+    }
+    if (sum != num_columns) return fail(GSR_ERR_ARG, "ply: field widths must add up to the column count");
+    static const int kSize[8] = {4, 8, 1, 1, 2, 2, 4, 4};
+    for (int c = 0; c < num_columns; c++) {
+        const gsr_ply_column &col = columns[c];
+        if (col.type < GSR_PLY_FLOAT32 || col.type > GSR_PLY_INT32) return fail(GSR_ERR_ARG, "ply: bad column type");
+        if (pack && col.type != GSR_PLY_FLOAT32) return fail(GSR_ERR_ARG, "ply: pack writes float32 columns only");
+        if (col.offset < 0 || col.offset + kSize[col.type] > record_bytes)
+            return fail(GSR_ERR_ARG, "ply: column outside the record");
+        p.cols[c] = make_int2(col.offset, col.type);
+    }
+    p.n = n;
+    p.record_bytes = record_bytes;
+    p.rows_per_block = ply_rows_per_block(record_bytes);
+    p.ncols = num_columns;
+    p.nfields = num_fields;
+    p.swap = big_endian ? 1 : 0;
+    return GSR_OK;
+}
+
+int gsr_ply_unpack(const uint8_t *records, int64_t n, int record_bytes, int big_endian, const gsr_ply_column *columns,
+                   int num_columns, float *const *fields, const int *widths, int num_fields, void *stream_ptr) {
+    PlyLaunch p{};
+    const int rc = ply_setup(p, n, record_bytes, big_endian, columns, num_columns, fields, widths, num_fields, false);
+    if (rc != GSR_OK) return rc;
+    if (n > 0 && !records) return fail(GSR_ERR_ARG, "ply: null records");
+    p.records = records;
+    launch_ply((hipStream_t)stream_ptr, p, false);
+    GSR_HIP(hipGetLastError());
+    return GSR_OK;
+}
+
+int gsr_ply_pack(uint8_t *records, int64_t n, int record_bytes, int big_endian, const gsr_ply_column *columns,
+                 int num_columns, const float *const *fields, const int *widths, int num_fields, void *stream_ptr) {
+    PlyLaunch p{};
+    const int rc = ply_setup(p, n, record_bytes, big_endian, columns, num_columns, fields, widths, num_fields, true);
+    if (rc != GSR_OK) return rc;
+    if (n > 0 && !records) return fail(GSR_ERR_ARG, "ply: null records");
+    p.records_out = records;
+    launch_ply((hipStream_t)stream_ptr, p, true);
+    GSR_HIP(hipGetLastError());
+    return GSR_OK;
+}
+
 size_t gsr_ssim_num_partials(int planes, int H, int W) {
     return (planes > 0 && H > 0 && W > 0) ? ssim_num_partials(planes, H, W) : 0;
 }

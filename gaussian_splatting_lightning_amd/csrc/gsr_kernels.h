@@ -161,6 +161,20 @@ int64_t densify_blocks(int64_t N);
 void launch_densify_classify(hipStream_t s, const DensifyParams &p);
 void launch_densify_apply(hipStream_t s, const DensifyApply &A, int64_t total_blocks);
 
+// ---- PLY records <-> fields (gsr_ply.hip) ----
+constexpr int PLY_MAX_COLS = 128, PLY_MAX_FIELDS = 8;
+struct PlyLaunch {
+    const uint8_t *records;   // unpack source
+    uint8_t *records_out;     // pack destination
+    int64_t n;
+    int record_bytes, rows_per_block, ncols, nfields, swap;
+    float *field[PLY_MAX_FIELDS];
+    int width[PLY_MAX_FIELDS];
+    int2 cols[PLY_MAX_COLS];  // (byte offset in the record, GSR_PLY_* type), destination order
+};
+int ply_rows_per_block(int record_bytes);
+void launch_ply(hipStream_t s, const PlyLaunch &p, bool pack);
+
 // ---- fused SSIM loss (gsr_ssim.hip) ----
 size_t ssim_num_partials(int planes, int H, int W);
 void launch_ssim_forward(hipStream_t s, int planes, int H, int W, const float *img1, const float *img2, int valid,

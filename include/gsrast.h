@@ -202,6 +202,23 @@ typedef struct gsr_densify_field {
 int gsr_densify_apply(int64_t N, const void *workspace, const float *rotation, const float *scaling, const float *z,
                       const gsr_densify_field *fields, int num_fields, void *stream);
 
+/* PLY vertex records <-> parameter fields (the 3DGS checkpoint of gaussian_model.py:112-171 and
+ * third_party/.../gaussian_model.py:239-314).  `records` are n fixed-size records of record_bytes each, on the
+ * device; `columns` (host array, destination order: field after field, column after column) give each
+ * column's byte offset in the record and its PLY type; fields are row-major (n, widths[f]) fp32 device
+ * arrays.  unpack converts any scalar PLY type to fp32; pack writes float32 and zero-fills record bytes no
+ * column covers (the normals of save_ply).  big_endian selects binary_big_endian records. */
+enum { GSR_PLY_FLOAT32 = 0, GSR_PLY_FLOAT64 = 1, GSR_PLY_UINT8 = 2, GSR_PLY_INT8 = 3, GSR_PLY_UINT16 = 4,
+       GSR_PLY_INT16 = 5, GSR_PLY_UINT32 = 6, GSR_PLY_INT32 = 7 };
+typedef struct gsr_ply_column {
+    int32_t offset;
+    int32_t type;
+} gsr_ply_column;
+int gsr_ply_unpack(const uint8_t *records, int64_t n, int record_bytes, int big_endian, const gsr_ply_column *columns,
+                   int num_columns, float *const *fields, const int *widths, int num_fields, void *stream);
+int gsr_ply_pack(uint8_t *records, int64_t n, int record_bytes, int big_endian, const gsr_ply_column *columns,
+                 int num_columns, const float *const *fields, const int *widths, int num_fields, void *stream);
+
 /* Buffer sizes the forward will request (host-only arithmetic; for planning and tests). */
 size_t gsr_geom_buffer_bytes(int P);
 size_t gsr_binning_buffer_bytes(int64_t R, int W, int H);
