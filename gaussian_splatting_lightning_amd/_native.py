@@ -91,6 +91,7 @@ EXPORTED_SYMBOLS = (
     "gsr_stage_times", "gsr_reset_stage_times", "gsr_last_error", "gsr_build_info", "gsr_state_layout_query",
     "gsr_set_tuning", "gsr_ssim_num_partials", "gsr_ssim_forward", "gsr_ssim_backward", "gsr_adam_step",
     "gsr_densify_workspace_bytes", "gsr_densify_classify", "gsr_densify_apply", "gsr_ply_unpack", "gsr_ply_pack",
+    "gsr_knn_workspace_bytes", "gsr_knn_mean_dist2",
 )
 
 _lib = None
@@ -133,6 +134,11 @@ def load(path: str | None = None):
                        ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int), ctypes.c_int,
                        ctypes.c_void_p]
         fn.restype = ctypes.c_int
+    lib.gsr_knn_workspace_bytes.argtypes = [ctypes.c_int64]
+    lib.gsr_knn_workspace_bytes.restype = ctypes.c_size_t
+    lib.gsr_knn_mean_dist2.argtypes = [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_void_p]
+    lib.gsr_knn_mean_dist2.restype = ctypes.c_int
     lib.gsr_ssim_num_partials.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
     lib.gsr_ssim_num_partials.restype = ctypes.c_size_t
     lib.gsr_ssim_forward.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _fp, _fp, ctypes.c_int, _fp, _fp, _fp,

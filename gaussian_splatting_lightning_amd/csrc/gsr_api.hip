@@ -624,6 +624,20 @@ int gsr_ply_pack(uint8_t *records, int64_t n, int record_bytes, int big_endian, 
     return GSR_OK;
 }
 
+size_t gsr_knn_workspace_bytes(int64_t n) { return n < 0 ? 0 : knn_workspace(n, nullptr); }
+
+int gsr_knn_mean_dist2(int64_t n, const float *points, float *out, void *workspace, void *stream_ptr) {
+    if (n < 0 || n > (int64_t)RS_ONESWEEP_MAX_N) return fail(GSR_ERR_ARG, "knn: 0 <= n < 2^30");
+    if (n == 0) return GSR_OK;
+    if (!points || !out || !workspace) return fail(GSR_ERR_ARG, "knn: null pointer");
+    KnnScratch k{};
+    k.base = workspace;
+    knn_workspace(n, &k);
+    launch_knn((hipStream_t)stream_ptr, k, points, n, out);
+    GSR_HIP(hipGetLastError());
+    return GSR_OK;
+}
+
 size_t gsr_ssim_num_partials(int planes, int H, int W) {
     return (planes > 0 && H > 0 && W > 0) ? ssim_num_partials(planes, H, W) : 0;
 }

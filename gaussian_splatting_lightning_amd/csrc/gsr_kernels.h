@@ -20,7 +20,9 @@ void launch_exclusive_scan_lookback(hipStream_t s, const uint32_t *in, const uin
 // LSD radix sort of n (key, value) pairs on bits [0, nbits).  Keys start in sc.k[0]; values are the
 // implicit iota 0..n-1.  After ceil(nbits/8) passes the keys are in sc.k[passes & 1] and the values in
 // sc.v[passes & 1].
-void launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits);
+// LSD radix sort of sc.k[0] (nbits significant bits); values are the iota permutation unless `keyed`, in which
+// case sc.v[0] holds the input values.  The result lands in buffer index (passes & 1).
+void launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bool keyed = false);
 
 // ---- forward (gsr_forward.hip) ----
 struct PreprocessParams {
@@ -174,6 +176,17 @@ struct PlyLaunch {
 };
 int ply_rows_per_block(int record_bytes);
 void launch_ply(hipStream_t s, const PlyLaunch &p, bool pack);
+
+// ---- exact 3-NN mean squared distance (gsr_knn.hip) ----
+struct KnnScratch {
+    void *base;
+    SortScratch sort;
+    uint64_t *codes, *scode;
+    float4 *spts;
+    float *partial, *box;
+};
+size_t knn_workspace(int64_t n, KnnScratch *k);  // k == nullptr: size only; else carve from k->base
+void launch_knn(hipStream_t s, KnnScratch &k, const float *pts, int64_t n, float *out);
 
 // ---- fused SSIM loss (gsr_ssim.hip) ----
 size_t ssim_num_partials(int planes, int H, int W);

@@ -518,7 +518,7 @@ __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__rest
 }
 
 template <int ITEMS>
-static void launch_radix_sort_onesweep(hipStream_t s, SortScratch &sc, uint32_t n, int passes) {
+static void launch_radix_sort_onesweep(hipStream_t s, SortScratch &sc, uint32_t n, int passes, bool keyed) {
     const uint32_t nb = div_up(n, (uint32_t)ITEMS * 256u);
     (void)hipMemsetAsync(sc.ctrl, 0, sizeof(uint32_t) * (RS_CTRL_WORDS + (size_t)passes * nb * RS_BINS), s);
     const uint32_t hb = min(div_up(n, 256u * 8u), 2048u);
@@ -527,7 +527,7 @@ static void launch_radix_sort_onesweep(hipStream_t s, SortScratch &sc, uint32_t 
     for (int p = 0; p < passes; p++) {
         const int in = p & 1, out = (p + 1) & 1;
         uint32_t *st = sc.status + (size_t)p * nb * RS_BINS;
-        if (p == 0)
+        if (p == 0 && !keyed)
             rs_onesweep_kernel<true, ITEMS><<<nb, 256, 0, s>>>(sc.k[in], nullptr, n, p, sc.ctrl, st, sc.k[out],
                                                                sc.v[out]);
         else
@@ -536,21 +536,21 @@ static void launch_radix_sort_onesweep(hipStream_t s, SortScratch &sc, uint32_t 
     }
 }
 
-void launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits) {
+void launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bool keyed) {
     if (n == 0) return;
     const uint32_t nb = div_up(n, RS_TILE);
     const int passes = radix_passes(nbits);
     // onesweep knob: bit 0 = depth-size sorts (nbits == 32), bit 1 = tile sorts
     const int os = tuning("onesweep", 1);
     if (n <= RS_ONESWEEP_MAX_N && passes <= RS_MAX_PASSES && (os & (nbits == 32 ? 1 : 2))) {
-        launch_radix_sort_onesweep<RS_ITEMS>(s, sc, n, passes);  // 8- and 32-key/thread tiles measured slower
+        launch_radix_sort_onesweep<RS_ITEMS>(s, sc, n, passes, keyed);  // 8-/32-key tiles measured slower
         return;
     }
     for (int p = 0; p < passes; p++) {
         const int shift = 8 * p, in = p & 1, out = (p + 1) & 1;
         rs_hist_kernel<<<nb, 256, 0, s>>>(sc.k[in], n, shift, sc.counts, nb);
         launch_exclusive_scan(s, sc.counts, nullptr, RS_BINS * nb, sc.counts, sc.scan_tmp, nullptr);
-        if (p == 0)
+        if (p == 0 && !keyed)
             rs_scatter_kernel<true><<<nb, 256, 0, s>>>(sc.k[in], nullptr, n, shift, sc.counts, nb, sc.k[out], sc.v[out]);
         else
             rs_scatter_kernel<false><<<nb, 256, 0, s>>>(sc.k[in], sc.v[in], n, shift, sc.counts, nb, sc.k[out],

@@ -219,6 +219,12 @@ int gsr_ply_unpack(const uint8_t *records, int64_t n, int record_bytes, int big_
 int gsr_ply_pack(uint8_t *records, int64_t n, int record_bytes, int big_endian, const gsr_ply_column *columns,
                  int num_columns, const float *const *fields, const int *widths, int num_fields, void *stream);
 
+/* Mean squared distance of every point to its 3 nearest other points -- distCUDA2 of
+ * gs_lightning/utils/math.py:9-14 (scipy KDTree query k=4, self dropped), used for the scale initialisation
+ * of gaussian_model.py:84-91.  Exact (Morton-ordered octree search); points (n,3) fp32, out (n) fp32. */
+size_t gsr_knn_workspace_bytes(int64_t n);
+int gsr_knn_mean_dist2(int64_t n, const float *points, float *out, void *workspace, void *stream);
+
 /* Buffer sizes the forward will request (host-only arithmetic; for planning and tests). */
 size_t gsr_geom_buffer_bytes(int P);
 size_t gsr_binning_buffer_bytes(int64_t R, int W, int H);

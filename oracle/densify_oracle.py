@@ -15,9 +15,11 @@ The split displacement takes `z` ~ N(0,1) of shape (n_split, 3) as an input (an 
 of shape (n, 3)): torch.normal(mean, std) draws exactly normal_(0,1) and multiplies by std (ATen
 Distributions), so the caller supplies the same draw.
 
-Parity pinning: kornia and plyfile (imported at the top of the reference module) are absent from this image,
-so the reference module cannot be imported here; tests/test_densify.py cross-checks this restatement against
-an independent torch restatement of the same lines.  Parity is therefore pinned to the restatement only.
+Parity pinning: tests/golden/densify_golden.npz holds the outputs of the reference's own
+GaussianModel.densify_and_prune run on CPU tensors (tests/golden/make_golden_train.py; kornia, plyfile and
+pycolmap are absent, so that script stands in a Quaternion.matrix() and empty plyfile/pycolmap modules, none of
+which the densify path calls except the quaternion matrix of the split).  tests/test_densify.py checks this
+restatement against that fixture and against an independent torch restatement for five threshold sets.
 """
 from __future__ import annotations
 

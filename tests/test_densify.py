@@ -306,3 +306,30 @@ def test_split_draw_equals_torch_normal():
     a = torch.normal(mean=torch.zeros_like(std), std=std, generator=torch.Generator(device="cuda").manual_seed(3))
     z = torch.empty(777, 3, device="cuda").normal_(0, 1, generator=torch.Generator(device="cuda").manual_seed(3))
     torch.testing.assert_close(a, z * std, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("case,thr", [("screensize", (0.0002, 0.01, 0.05, 0.4, 20.0)),
+                                      ("no_screensize", (0.0002, 0.01, 0.05, 0.4, None))])
+def test_oracle_matches_reference_golden(case, thr):
+    """tests/golden/densify_golden.npz: the reference's GaussianModel.densify_and_prune run on CPU tensors
+    (make_golden_train.py); the split draw is replayed as manual_seed(seed) + normal_((n_split, 3))."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "densify_golden.npz"))
+    p = {k: g[f"in_{k}"] for k in NAMES}
+    s = {k: g[f"in_{k}"] for k in ("max_radii2D", "xyz_grad_accum", "xyz_grad_count")}
+
+    def z_fn(n):
+        torch.manual_seed(int(g["seed"]))
+        return torch.empty((n, 3)).normal_().numpy()
+
+    P, S, _, keep, counts = densify_oracle.densify_and_prune(p, s, float(g["spatial_scale"]), *thr,
+                                                             use_screensize_threshold=True, z=z_fn)
+    np.testing.assert_array_equal(keep, g[f"{case}_preserve_idx"])
+    assert counts[1] > 0 and counts[2] > 0
+    for k in NAMES:
+        if k in ("xyz", "scaling"):
+            close(P[k], g[f"{case}_{k}"])
+        else:
+            np.testing.assert_array_equal(P[k], g[f"{case}_{k}"])
+    for k in S:
+        np.testing.assert_array_equal(S[k], g[f"{case}_{k}"])
