@@ -14,7 +14,7 @@ HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))
 def declared_functions():
     txt = open(HEADER).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(gsr_[a-z_]+)\s*\(", txt)) - {"gsr_alloc_fn"})
+    return sorted(set(re.findall(r"\b(gsr_[a-z0-9_]+)\s*\(", txt)) - {"gsr_alloc_fn"})
 
 
 def test_header_declares_expected_api():
