@@ -91,7 +91,7 @@ EXPORTED_SYMBOLS = (
     "gsr_stage_times", "gsr_reset_stage_times", "gsr_last_error", "gsr_build_info", "gsr_state_layout_query",
     "gsr_set_tuning", "gsr_ssim_num_partials", "gsr_ssim_forward", "gsr_ssim_backward", "gsr_adam_step",
     "gsr_densify_workspace_bytes", "gsr_densify_classify", "gsr_densify_apply", "gsr_ply_unpack", "gsr_ply_pack",
-    "gsr_knn_workspace_bytes", "gsr_knn_mean_dist2",
+    "gsr_knn_workspace_bytes", "gsr_knn_mean_dist2", "gsr_debug_wave_stamps",
 )
 
 _lib = None
@@ -168,6 +168,8 @@ def load(path: str | None = None):
     lib.gsr_state_layout_query.restype = None
     lib.gsr_set_tuning.argtypes = [ctypes.c_char_p, ctypes.c_int]
     lib.gsr_set_tuning.restype = None
+    lib.gsr_debug_wave_stamps.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    lib.gsr_debug_wave_stamps.restype = ctypes.c_int
     lib.gsr_last_error.restype = ctypes.c_char_p
     lib.gsr_build_info.restype = ctypes.c_char_p
     _lib = lib
@@ -209,3 +211,12 @@ def state_layout(P: int, R: int, W: int, H: int) -> dict:
 def set_tuning(name: str, value: int) -> None:
     """Internal A/B knob (see gsr_set_tuning)."""
     load().gsr_set_tuning(name.encode(), int(value))
+
+
+def wave_stamps(which: int, n: int):
+    """Diagnostics: (n, 4) uint32 array of per-slot (start, end, HW_ID, XCC_ID) composite-kernel stamps."""
+    import numpy as np
+    out = np.zeros((n, 4), dtype=np.uint32)
+    got = load().gsr_debug_wave_stamps(int(which), out.ctypes.data, int(n))
+    check(got if got < 0 else 0, "gsr_debug_wave_stamps")
+    return out[:got]

@@ -32,6 +32,15 @@ int gsr::tuning(const char *name, int default_value) {
     return default_value;
 }
 
+uint4 *gsr::stamp_buffer(int which) {
+    static uint4 *buf[2] = {nullptr, nullptr};
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    if (which < 0 || which > 1) return nullptr;
+    if (!buf[which] && hipMalloc(&buf[which], sizeof(uint4) * STAMP_SLOTS) == hipSuccess)
+        (void)hipMemset(buf[which], 0, sizeof(uint4) * STAMP_SLOTS);
+    return buf[which];
+}
+
 namespace {
 
 thread_local std::string g_err;
@@ -693,6 +702,15 @@ void gsr_set_tuning(const char *name, int value) {
             return;
         }
     g_tune.emplace_back(name, value);
+}
+
+int gsr_debug_wave_stamps(int which, uint32_t *host_dst, int max_slots) {
+    uint4 *b = stamp_buffer(which);
+    if (!b || !host_dst) return fail(GSR_ERR_ARG, "no stamp buffer");
+    const int n = max_slots < STAMP_SLOTS ? max_slots : STAMP_SLOTS;
+    GSR_HIP(hipDeviceSynchronize());
+    GSR_HIP(hipMemcpy(host_dst, b, sizeof(uint4) * (size_t)n, hipMemcpyDeviceToHost));
+    return n;
 }
 
 void gsr_set_profiling(int enable) {

@@ -217,9 +217,242 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_bwd_v3_kernel(Rend
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// v4: one scalar "behind" accumulator per pixel with the background folded in, strip skipping, and the next
+// batch's gathers in flight while the current batch composites.
+//   The reference keeps accum_rec (3 channels) and accum_invdepth per pixel and adds the background term
+//   -T_final / (1 - alpha) (bg . dL/dpix) to dL/dalpha.  Only the projection onto the pixel's upstream
+//   gradient enters dL/dalpha, so one scalar  D_k = (accum_rec_k + T_final / T_{k+1} bg) . dL/dpix
+//   + accum_invdepth_k dL/dinvdepth  carries all of it: at the last contributor D = bg . dL/dpix, it follows
+//   the reference's recursion  D <- D + alpha (c . dL/dpix - D)  (T_final / T_k = (1 - alpha_k) T_final /
+//   T_{k+1}), and  dL/dalpha = T_k (c . dL/dpix - D).  Per (pixel, instance) pair that is 6 VALU ops instead
+//   of 14, and 7 live registers per pixel instead of 11.
+//   STRIP: a lane's pixel k lies in the tile's 4-row strip k; strips outside the instance's alpha >= 1/255
+//   row band (strip_mask, conservative) are skipped with one scalar test instead of per-lane exec branches.
+//   PRED: inside a strip the pair update is predicated (selects) instead of nested exec-mask branches.
+//   Gathers are software-pipelined two deep: while batch b composites, the records of batch b+1 (whose
+//   Gaussian ids arrived during batch b-1) and the ids of batch b+2 are loading.
+// ------------------------------------------------------------------------------------------------
+template <bool HAS_INV, bool STRIP, bool PRED>
+__global__ __launch_bounds__(64, 5) void render_bwd_v4_kernel(RenderBwdParams p) {
+    __shared__ float4 s_a[BWD_BATCH];
+    __shared__ float4 s_b[BWD_BATCH];
+    __shared__ float2 s_c[BWD_BATCH];
+    __shared__ uint32_t s_m[BWD_BATCH];
+    __shared__ __attribute__((aligned(16))) float s_part[BWD_BATCH][PART];  // [instance][10 sums]
+    const int lane = threadIdx.x;
+    const int slot = blockIdx.x;
+    set_slot_priority(slot, p.prio_div);
+    const uint32_t t_start = p.stamps ? stamp_now() : 0u;
+    const int tile = p.tile_order ? (int)p.tile_order[slot] : slot;
+    const int tx = tile % p.gx, ty = tile / p.gx;
+    const int px = tx * BLOCK_X + (lane & 15);
+    const int py0 = ty * BLOCK_Y + (lane >> 4);
+    const float pfx = (float)px;
+    const float row0 = (float)(ty * BLOCK_Y);
+    const uint2 range = p.ranges[tile];
+    const uint32_t tl = p.tile_last[tile];
+
+    const uint32_t loaded = p.tile_loaded[tile];
+    for (uint32_t s = range.x + tl + lane; s < range.x + loaded; s += 64) {
+        const float z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        store_row(p.rows, p.rows_by_u ? p.sorted_u[s] : s, z);
+    }
+    if (tl == 0) {
+        stamp_store(p.stamps, slot, t_start, lane);
+        return;
+    }
+
+    // Pipeline prologue: ids of batches 0 and 1, records of batch 0.
+    int bend = (int)tl;
+    uint32_t nx_row = 0, nx_gid = 0, nn_row = 0, nn_gid = 0;
+    if (lane < min(BWD_BATCH, bend)) {
+        const uint32_t s_me = range.x + (uint32_t)(bend - 1 - lane);
+        nx_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
+        nx_gid = p.point_list[s_me];
+    }
+    if (lane < min(BWD_BATCH, bend - BWD_BATCH)) {
+        const uint32_t s_me = range.x + (uint32_t)(bend - BWD_BATCH - 1 - lane);
+        nn_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
+        nn_gid = p.point_list[s_me];
+    }
+    float4 nx_a = make_float4(0, 0, 0, 0), nx_b = nx_a;
+    float2 nx_c = make_float2(0, 0);
+    if (lane < min(BWD_BATCH, bend)) {
+        nx_a = p.rec_a[nx_gid];
+        nx_b = p.rec_b[nx_gid];
+        nx_c = p.rec_c[nx_gid];
+    }
+
+    const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
+    const size_t HW = (size_t)p.W * p.H;
+    float T[PIX_PER_LANE], dp0[PIX_PER_LANE], dp1[PIX_PER_LANE], dp2[PIX_PER_LANE], dinv[PIX_PER_LANE];
+    float D[PIX_PER_LANE];
+    uint32_t lastc[PIX_PER_LANE];
+    const float pfy0 = (float)py0;
+#pragma unroll
+    for (int k = 0; k < PIX_PER_LANE; k++) {
+        const int py = py0 + 4 * k;
+        const bool inside = px < p.W && py < p.H;
+        const size_t pid = inside ? (size_t)py * p.W + px : 0;
+        T[k] = inside ? p.final_T[pid] : 0.f;
+        lastc[k] = inside ? p.n_contrib[pid] : 0u;
+        dp0[k] = inside ? p.dL_dpix[pid] : 0.f;
+        dp1[k] = inside ? p.dL_dpix[HW + pid] : 0.f;
+        dp2[k] = inside ? p.dL_dpix[2 * HW + pid] : 0.f;
+        dinv[k] = (HAS_INV && inside) ? p.dL_dinvdepth[pid] : 0.f;
+        D[k] = fmaf(bg2, dp2[k], fmaf(bg1, dp1[k], bg0 * dp0[k]));
+    }
+    const float hW = 0.5f * p.W, hH = 0.5f * p.H;
+
+    for (; bend > 0; bend -= BWD_BATCH) {
+        const int cnt = min(BWD_BATCH, bend);
+        const float4 my_a = nx_a, my_b = nx_b;
+        const uint32_t my_row = nx_row;
+        if (lane < cnt) {
+            s_a[lane] = stage_rec_a(my_a);
+            s_b[lane] = stage_rec_b(my_b);
+            s_c[lane] = nx_c;
+            if (STRIP) s_m[lane] = strip_mask(my_a, my_b, row0);
+        }
+        // issue the next batch's record gathers and the batch after's ids
+        if (lane < min(BWD_BATCH, bend - BWD_BATCH)) {
+            nx_a = p.rec_a[nn_gid];
+            nx_b = p.rec_b[nn_gid];
+            nx_c = p.rec_c[nn_gid];
+        }
+        nx_row = nn_row;
+        if (lane < min(BWD_BATCH, bend - 2 * BWD_BATCH)) {
+            const uint32_t s_me = range.x + (uint32_t)(bend - 2 * BWD_BATCH - 1 - lane);
+            nn_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
+            nn_gid = p.point_list[s_me];
+        }
+        wave_lds_sync();
+        for (int j = 0; j < cnt; j++) {
+            const uint32_t idx = (uint32_t)(bend - 1 - j);
+            const float4 a = s_a[j];  // x, y, A, B
+            const float4 b = s_b[j];  // C, o, r, g
+            const float2 c = s_c[j];  // b, 1/depth
+            const uint32_t sm = STRIP ? __builtin_amdgcn_readfirstlane(s_m[j]) : 0xfu;
+            const float dx = a.x - pfx, dy0 = a.y - pfy0;
+            const float P0 = (a.z * dx) * dx, L = a.w * dx;
+            float Q0 = 0.f, Q1 = 0.f, Q2 = 0.f, w0 = 0.f, w1 = 0.f, w2 = 0.f, w3 = 0.f;
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < PIX_PER_LANE; k++) {
+                if (STRIP && !(sm & (1u << k))) continue;  // wave-uniform
+                const float dy = dy0 - (float)(4 * k);
+                if (PRED) {
+                    const float power2 = power2_at(b.x, dy, P0, L);
+                    const float G = __builtin_amdgcn_exp2f(power2);
+                    const float alpha = fminf(0.99f, b.y * G);
+                    const bool ok = idx < lastc[k] && !(power2 > 0.0f) && !(alpha < 1.0f / 255.0f);
+                    const float al = ok ? alpha : 0.f;  // al = 0 leaves T, D and the sums unchanged
+                    any |= ok;
+                    T[k] = T[k] * fast_rcp(1.f - al);
+                    const float wgt = al * T[k];
+                    float cd = fmaf(c.x, dp2[k], fmaf(b.w, dp1[k], b.z * dp0[k]));
+                    if (HAS_INV) cd = fmaf(c.y, dinv[k], cd);
+                    const float d = cd - D[k];
+                    D[k] = fmaf(al, d, D[k]);
+                    w0 = fmaf(wgt, dp0[k], w0);
+                    w1 = fmaf(wgt, dp1[k], w1);
+                    w2 = fmaf(wgt, dp2[k], w2);
+                    if (HAS_INV) w3 = fmaf(wgt, dinv[k], w3);
+                    const float q = ok ? G * (d * T[k]) : 0.f;
+                    const float qdy = q * dy;
+                    Q0 += q;
+                    Q1 += qdy;
+                    Q2 = fmaf(qdy, dy, Q2);
+                } else {
+                    if (idx >= lastc[k]) continue;
+                    const float power2 = power2_at(b.x, dy, P0, L);
+                    if (power2 > 0.0f) continue;
+                    const float G = __builtin_amdgcn_exp2f(power2);
+                    const float alpha = fminf(0.99f, b.y * G);
+                    if (alpha < 1.0f / 255.0f) continue;
+                    any = true;
+                    T[k] = T[k] * fast_rcp(1.f - alpha);
+                    const float wgt = alpha * T[k];
+                    float cd = fmaf(c.x, dp2[k], fmaf(b.w, dp1[k], b.z * dp0[k]));
+                    if (HAS_INV) cd = fmaf(c.y, dinv[k], cd);
+                    const float d = cd - D[k];
+                    D[k] = fmaf(alpha, d, D[k]);
+                    w0 = fmaf(wgt, dp0[k], w0);
+                    w1 = fmaf(wgt, dp1[k], w1);
+                    w2 = fmaf(wgt, dp2[k], w2);
+                    if (HAS_INV) w3 = fmaf(wgt, dinv[k], w3);
+                    const float q = G * (d * T[k]);
+                    const float qdy = q * dy;
+                    Q0 += q;
+                    Q1 += qdy;
+                    Q2 = fmaf(qdy, dy, Q2);
+                }
+            }
+            float *dst = s_part[j];
+            if (__ballot(any)) {
+                float m[10];
+                m[0] = Q0;
+                m[1] = Q0 * dx;
+                m[2] = Q1;
+                m[3] = m[1] * dx;
+                m[4] = Q1 * dx;
+                m[5] = Q2;
+                m[6] = w0;
+                m[7] = w1;
+                m[8] = w2;
+                m[9] = w3;
+                wave_reduce10_store(m, dst, lane);
+            } else if (lane < 10) {
+                dst[lane] = 0.f;
+            }
+        }
+        wave_lds_sync();
+        if (lane < cnt) {
+            const float4 *src = reinterpret_cast<const float4 *>(s_part[lane]);
+            const float4 u0 = src[0], u1 = src[1];
+            const float2 u2 = *reinterpret_cast<const float2 *>(s_part[lane] + 8);
+            const float S = u0.x, Sx = u0.y, Sy = u0.z, Sxx = u0.w, Sxy = u1.x, Syy = u1.y;
+            const float o = my_b.y, ca = my_a.z, cb = my_a.w, cc = my_b.x;
+            float row[10];
+            row[0] = -o * hW * (ca * Sx + cb * Sy);
+            row[1] = -o * hH * (cb * Sx + cc * Sy);
+            row[2] = -0.5f * o * Sxx;
+            row[3] = -0.5f * o * Sxy;
+            row[4] = -0.5f * o * Syy;
+            row[5] = S;
+            row[6] = u1.z;
+            row[7] = u1.w;
+            row[8] = u2.x;
+            row[9] = u2.y;
+            store_row(p.rows, my_row, row);
+        }
+        wave_lds_sync();
+    }
+    stamp_store(p.stamps, slot, t_start, lane);
+}
+
 void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
     if (p.num_tiles <= 0) return;
     const int minw = tuning("bwd_minwaves", 5), wpb = tuning("bwd_wpb", 1);
+    if (tuning("bwd_v", 4) == 4) {
+        RenderBwdParams q = p;
+        q.prio_div = tuning("prio_div", 0);
+        q.stamps = tuning("stamp", 0) ? stamp_buffer(1) : nullptr;
+        const dim3 grid(p.num_tiles), block(64);
+        const int mode = tuning("bwd_strip", 1) * 2 + tuning("bwd_pred", 0);
+#define GSR_BWD4(INV)                                                                                   \
+        do {                                                                                           \
+            if (mode == 0) render_bwd_v4_kernel<INV, false, false><<<grid, block, 0, s>>>(q);          \
+            else if (mode == 1) render_bwd_v4_kernel<INV, false, true><<<grid, block, 0, s>>>(q);      \
+            else if (mode == 2) render_bwd_v4_kernel<INV, true, false><<<grid, block, 0, s>>>(q);      \
+            else render_bwd_v4_kernel<INV, true, true><<<grid, block, 0, s>>>(q);                      \
+        } while (0)
+        if (p.dL_dinvdepth) GSR_BWD4(true);
+        else GSR_BWD4(false);
+#undef GSR_BWD4
+        return;
+    }
     const dim3 block(64 * (wpb == 1 ? 1 : 4)), grid(wpb == 1 ? p.num_tiles : div_up(p.num_tiles, 4));
 #define GSR_BWD_LAUNCH(INV, MW)                                                                        \
     do {                                                                                               \

@@ -18,6 +18,7 @@ constexpr int TILE_PIX = BLOCK_X * BLOCK_Y;
 constexpr int WAVE = 64;
 constexpr int PIX_PER_LANE = TILE_PIX / WAVE;  // one wave composites one 16x16 tile
 constexpr uint32_t BIG_GAUSSIAN_TILES = 64;   // per-Gaussian gradient rows reduced by a whole block above this
+constexpr int STAMP_SLOTS = 1 << 16;  // diagnostics: launch slots with a wave stamp (gsr_debug_wave_stamps)
 constexpr int GRAD_ROW = 12;                   // floats per instance gradient row (10 used, 48 B)
 
 // counters block at the head of the geometry buffer (zeroed every forward)
@@ -385,6 +386,26 @@ __device__ __forceinline__ float power2_at(float C, float dy, float P0, float L)
     return fmaf(dy, fmaf(C, dy, L), P0);
 }
 
+// Conservative 4-bit mask of the 4-row strips of a 16-row tile (first row row0) that hold a pixel where
+// the Gaussian can pass the compositor's alpha >= 1/255 test.  a = raw rec_a (x, y, conic a, conic b),
+// b = raw rec_b (conic c, opacity, ...).  alpha = min(0.99, o exp(power)) >= 1/255 needs
+// d^T Q d <= tau = 2 ln(255 o) (Q = [[a, b], [b, c]]), whose row extent is |dy| <= sqrt(tau (Q^-1)_yy) =
+// sqrt(tau a / (a c - b^2)).  1 % + 1 px of margin absorb the fp32 error of this bound; degenerate or
+// non-finite conics keep every strip.
+__device__ __forceinline__ uint32_t strip_mask(float4 a, float4 b, float row0) {
+    const float o255 = 255.f * b.y;
+    if (!(o255 >= 0.999f)) return o255 < 0.999f ? 0u : 0xfu;  // alpha <= o < 1/255 everywhere (NaN: keep all)
+    const float det = a.z * b.x - a.w * a.w;
+    const float tau = 2.f * __logf(fmaxf(o255, 1.f)) + 1e-3f;
+    const float e = sqrtf(tau * a.z / det) * 1.01f + 1.f;
+    if (!(det > 0.f) || !(e < 1e6f)) return 0xfu;
+    const float lo = a.y - e - row0, hi = a.y + e - row0;  // band of rows, relative to the tile
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) m |= (hi >= 4.f * k && lo <= 4.f * k + 3.f) ? (1u << k) : 0u;
+    return m;
+}
+
 // --- per-instance gradient rows (render_bwd -> big_reduce / preprocess_bwd) -------------------------
 // Row layout: [0] dmean2D.x  [1] dmean2D.y  [2] dconic.x  [3] dconic.y  [4] dconic.w  [5] dopacity
 //             [6..8] dcolor  [9] dinvdepth  [10..11] pad
@@ -448,6 +469,26 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v, int lane) {
 __device__ __forceinline__ uint64_t lanemask_lt(int lane) { return (lane == 0) ? 0ull : (~0ull >> (64 - lane)); }
 
 // Orders LDS writes before later LDS reads of other lanes of the SAME wave (no s_barrier).
+// LPT launch order puts the heaviest tiles in the first slots; with prio_div > 0 their waves also win VALU
+// issue arbitration against the lighter waves sharing their SIMD (s_setprio takes an immediate).
+__device__ __forceinline__ void set_slot_priority(int slot, int prio_div) {
+    if (prio_div <= 0) return;
+    const int lvl = slot / prio_div;
+    if (lvl == 0) __builtin_amdgcn_s_setprio(3);
+    else if (lvl == 1) __builtin_amdgcn_s_setprio(2);
+    else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
+}
+
+// Wave timeline stamp (diagnostics): 100 MHz real-time clock at start / end, HW_ID and XCC_ID registers.
+__device__ __forceinline__ uint32_t stamp_now() { return (uint32_t)__builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ void stamp_store(uint4 *stamps, int slot, uint32_t t0, int lane) {
+    if (!stamps || lane != 0 || slot >= STAMP_SLOTS) return;
+    const uint32_t t1 = stamp_now();
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+    stamps[slot] = make_uint4(t0, t1, hw, xcc);
+}
+
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

@@ -478,13 +478,20 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_fwd_v3_kernel(Rend
 // half the time, shortening the kernel's critical path.  Pixel k of half h is the whole-tile pixel 2h + k with
 // the same dy rounding, so outputs are bitwise those of the whole-tile path; the halves combine tile_last /
 // tile_loaded with atomicMax on zeroed words.
-template <int NPIX>
+// With PF the three dependent gathers of a batch (sorted_u -> inst_gid -> records) are software-pipelined
+// across batches: while batch b composites, the records of batch b+1, the Gaussian ids of batch b+2 and the
+// expansion indices of batch b+3 are loading, each from an index that arrived one batch earlier.
+// With STRIP each staged instance carries strip_mask (gsr_common.h) and a pixel row strip the instance cannot
+// reach is skipped with one scalar test (its pixels would all fail the alpha test).
+template <int NPIX, bool PF, bool STRIP>
 __device__ __forceinline__ void composite_fwd(const RenderFwdParams &p, const int tile, const int half,
-                                              const int lane, float4 *s_a, float4 *s_b, float2 *s_c) {
+                                              const int lane, float4 *s_a, float4 *s_b, float2 *s_c,
+                                              uint32_t *s_m) {
     const int tx = tile % p.gx, ty = tile / p.gx;
     const int px = tx * BLOCK_X + (lane & 15);
     const int py0 = ty * BLOCK_Y + (lane >> 4);
     const float pfx = (float)px, pfy0 = (float)py0;
+    const float row0 = (float)(ty * BLOCK_Y);
     const int kbase = NPIX == 4 ? 0 : 2 * half;  // whole-tile pixel index of this wave's first pixel
     float T[NPIX], C0[NPIX], C1[NPIX], C2[NPIX], ID[NPIX];
     uint32_t last[NPIX];
@@ -500,20 +507,62 @@ __device__ __forceinline__ void composite_fwd(const RenderFwdParams &p, const in
     const uint2 range = p.ranges[tile];
     uint32_t contributor = 0;
     uint32_t loaded_end = range.x;
+    uint32_t u1 = 0, g1 = 0, u2 = 0, g2 = 0, u3 = 0;  // PF pipeline: batch b+1 (u, id), b+2 (u, id), b+3 (u)
+    float4 ra = make_float4(0, 0, 0, 0), rb = ra;
+    float2 rc = make_float2(0, 0);
+    if (PF) {
+        const uint32_t s0 = range.x + lane;
+        if (s0 < range.y) {
+            u1 = p.sorted_u[s0];
+            g1 = p.inst_gid[u1];
+            ra = p.rec_a[g1];
+            rb = p.rec_b[g1];
+            rc = p.rec_c[g1];
+        }
+        if (s0 + 64 < range.y) {
+            u2 = p.sorted_u[s0 + 64];
+            g2 = p.inst_gid[u2];
+        }
+        if (s0 + 128 < range.y) u3 = p.sorted_u[s0 + 128];
+    }
     for (uint32_t base = range.x; base < range.y; base += 64) {
         bool any = false;
 #pragma unroll
         for (int k = 0; k < NPIX; k++) any |= active[k];
         if (__ballot(any) == 0) break;
         const uint32_t s = base + lane;
-        if (s < range.y) {
+        if (PF) {
+            if (s < range.y) {
+                p.point_list[s] = g1;
+                p.inv[u1] = s;
+                s_a[lane] = stage_rec_a(ra);
+                s_b[lane] = stage_rec_b(rb);
+                s_c[lane] = rc;
+                if (STRIP) s_m[lane] = strip_mask(ra, rb, row0);
+            }
+            if (s + 64 < range.y) {
+                ra = p.rec_a[g2];
+                rb = p.rec_b[g2];
+                rc = p.rec_c[g2];
+            }
+            uint32_t ng2 = 0, nu3 = 0;
+            if (s + 128 < range.y) ng2 = p.inst_gid[u3];
+            if (s + 192 < range.y) nu3 = p.sorted_u[s + 192];
+            u1 = u2;
+            g1 = g2;
+            u2 = u3;
+            g2 = ng2;
+            u3 = nu3;
+        } else if (s < range.y) {
             const uint32_t u = p.sorted_u[s];
             const uint32_t gid = p.inst_gid[u];
             p.point_list[s] = gid;
             p.inv[u] = s;
-            s_a[lane] = stage_rec_a(p.rec_a[gid]);
-            s_b[lane] = stage_rec_b(p.rec_b[gid]);
+            const float4 ga = p.rec_a[gid], gb = p.rec_b[gid];
+            s_a[lane] = stage_rec_a(ga);
+            s_b[lane] = stage_rec_b(gb);
             s_c[lane] = p.rec_c[gid];
+            if (STRIP) s_m[lane] = strip_mask(ga, gb, row0);
         }
         loaded_end = min(range.y, base + 64u);
         wave_lds_sync();
@@ -521,12 +570,13 @@ __device__ __forceinline__ void composite_fwd(const RenderFwdParams &p, const in
         for (int j = 0; j < cnt; j++) {
             const float4 a = s_a[j], b = s_b[j];
             const float2 c = s_c[j];
+            const uint32_t sm = STRIP ? __builtin_amdgcn_readfirstlane(s_m[j]) >> kbase : 0xfu;
             contributor++;
-            bool still = false;
             const float dx = a.x - pfx, dy0 = a.y - pfy0;
             const float P0 = (a.z * dx) * dx, L = a.w * dx;
 #pragma unroll
             for (int k = 0; k < NPIX; k++) {
+                if (STRIP && !(sm & (1u << k))) continue;  // wave-uniform: no pixel of the strip passes
                 const float power2 = power2_at(b.x, dy0 - (float)(4 * (kbase + k)), P0, L);
                 const float alpha = fminf(0.99f, b.y * __builtin_amdgcn_exp2f(power2));
                 const bool ok = active[k] && !(power2 > 0.0f) && !(alpha < 1.0f / 255.0f);
@@ -541,8 +591,10 @@ __device__ __forceinline__ void composite_fwd(const RenderFwdParams &p, const in
                 T[k] = take ? test_T : T[k];
                 last[k] = take ? contributor : last[k];
                 active[k] = active[k] && !stop;
-                still |= active[k];
             }
+            bool still = false;
+#pragma unroll
+            for (int k = 0; k < NPIX; k++) still |= active[k];
             if (__ballot(still) == 0) break;
         }
         wave_lds_sync();
@@ -576,18 +628,22 @@ __device__ __forceinline__ void composite_fwd(const RenderFwdParams &p, const in
     }
 }
 
-template <int MIN_WAVES>
+template <int MIN_WAVES, bool PF, bool STRIP>
 __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_split_kernel(RenderFwdParams p, int nsplit) {
     __shared__ float4 s_a[4][64];
     __shared__ float4 s_b[4][64];
     __shared__ float2 s_c[4][64];
+    __shared__ uint32_t s_m[4][64];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int slot = blockIdx.x * 4 + w;
     if (slot >= p.num_tiles + nsplit) return;
+    set_slot_priority(slot, p.prio_div);
+    const uint32_t t_start = p.stamps ? stamp_now() : 0u;
     if (slot < 2 * nsplit)
-        composite_fwd<2>(p, (int)p.tile_order[slot >> 1], slot & 1, lane, s_a[w], s_b[w], s_c[w]);
+        composite_fwd<2, PF, STRIP>(p, (int)p.tile_order[slot >> 1], slot & 1, lane, s_a[w], s_b[w], s_c[w], s_m[w]);
     else
-        composite_fwd<4>(p, (int)p.tile_order[slot - nsplit], 0, lane, s_a[w], s_b[w], s_c[w]);
+        composite_fwd<4, PF, STRIP>(p, (int)p.tile_order[slot - nsplit], 0, lane, s_a[w], s_b[w], s_c[w], s_m[w]);
+    stamp_store(p.stamps, slot, t_start, lane);
 }
 
 void launch_render_fwd(hipStream_t s, const RenderFwdParams &p) {
@@ -595,7 +651,15 @@ void launch_render_fwd(hipStream_t s, const RenderFwdParams &p) {
     const dim3 grid(div_up(p.num_tiles, 4)), block(256);
     const int nsplit = p.tile_order ? (int)((int64_t)p.num_tiles * tuning("fwd_split_pct", 5) / 100) : 0;
     if (nsplit > 0) {
-        render_fwd_split_kernel<4><<<div_up(p.num_tiles + nsplit, 4), 256, 0, s>>>(p, nsplit);
+        RenderFwdParams q = p;
+        q.prio_div = tuning("prio_div", 0);
+        q.stamps = tuning("stamp", 0) ? stamp_buffer(0) : nullptr;
+        const dim3 grid(div_up(p.num_tiles + nsplit, 4)), block(256);
+        const int mode = tuning("fwd_pf", 0) * 2 + tuning("fwd_strip", 0);
+        if (mode == 0) render_fwd_split_kernel<4, false, false><<<grid, block, 0, s>>>(q, nsplit);
+        else if (mode == 1) render_fwd_split_kernel<4, false, true><<<grid, block, 0, s>>>(q, nsplit);
+        else if (mode == 2) render_fwd_split_kernel<4, true, false><<<grid, block, 0, s>>>(q, nsplit);
+        else render_fwd_split_kernel<4, true, true><<<grid, block, 0, s>>>(q, nsplit);
         return;
     }
     const int pipe = tuning("fwd_pipe", 0), wpb = tuning("fwd_wpb", 4);

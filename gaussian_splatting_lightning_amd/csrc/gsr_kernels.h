@@ -7,6 +7,9 @@ namespace gsr {
 
 // Internal tuning knobs (A/B experiments in one process; defaults are the shipped configuration).
 int tuning(const char *name, int default_value);
+// Diagnostics: per-wave (start, end, HW_ID, XCC_ID) stamps of the composite kernels, one uint4 per launch
+// slot, written only when the "stamp" knob is set (buffer 0: render_fwd, 1: render_bwd).
+uint4 *stamp_buffer(int which);
 
 // ---- scan / sort (gsr_sort.hip) ----
 // Exclusive scan of n u32 values (optionally gathered through idx: v[i] = in[idx[i]]).
@@ -63,6 +66,8 @@ struct RenderFwdParams {
     const float *bg;
     float *out_color, *out_invdepth, *final_T;
     uint32_t *n_contrib, *tile_last;
+    int prio_div;  // > 0: launch slots [0, d) run at wave priority 3, [d, 2d) at 2, [2d, 3d) at 1 (set by launch)
+    uint4 *stamps; // diagnostics (set by launch), or null
 };
 void launch_render_fwd(hipStream_t s, const RenderFwdParams &p);
 
@@ -80,6 +85,8 @@ struct RenderBwdParams {
     const float *bg, *final_T, *dL_dpix, *dL_dinvdepth;
     float *rows;    // R x GRAD_ROW
     int rows_by_u;  // 1: row of an instance at its expansion index u (Gaussian-major), 0: at its sorted position
+    int prio_div;   // as RenderFwdParams::prio_div (set by launch)
+    uint4 *stamps;  // diagnostics (set by launch), or null
 };
 void launch_render_bwd(hipStream_t s, const RenderBwdParams &p);
 

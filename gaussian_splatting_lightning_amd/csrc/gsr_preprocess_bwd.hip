@@ -278,8 +278,12 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
 }
 
 // The SH coefficients (192 B per Gaussian at M = 16) are read and dL/dsh written through LDS: a wave moves
-// its 64 Gaussians' 12 KB block with coalesced float4 accesses and lanes exchange coefficient-major columns
-// (conflict-free), instead of 12 float4 accesses per lane strided by 192 B, which cost ~40 % of the kernel.
+// its 64 Gaussians' 12 KB block with coalesced float4 accesses, instead of 12 float4 accesses per lane strided
+// by 192 B, which cost ~40 % of the kernel.  In LDS each Gaussian's 48 floats sit at a 52-float stride, so
+// both the linear block copies (ds_write/read_b128 of consecutive lanes) and each lane's 12 float4 accesses
+// to its own Gaussian (52 = 4 x 13, 13 odd: 16 lanes of a b128 lane group hit 16 distinct 4-bank windows)
+// are free of bank conflicts.
+constexpr int SH_STRIDE = 52;
 template <bool LDS_SH>
 __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams p) {
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -287,43 +291,45 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         if (i < p.P) preprocess_bwd_one<false>(p, i, nullptr, nullptr);
         return;
     }
-    __shared__ float s_sh[4][48][64];
+    __shared__ __attribute__((aligned(16))) float s_sh[4][64 * SH_STRIDE];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const size_t gbase = ((size_t)blockIdx.x * 256 + (size_t)w * 64) * 48;  // first float of the wave's block
     const size_t gend = (size_t)p.P * 48;
+    float *sw = s_sh[w];
 #pragma unroll
     for (int c = 0; c < 12; c++) {
         const uint32_t f = c * 256 + lane * 4;
         if (gbase + f < gend) {
             const float4 v = *reinterpret_cast<const float4 *>(p.shs + gbase + f);
-            const uint32_t gl = f / 48, k = f % 48;
-            s_sh[w][k][gl] = v.x;
-            s_sh[w][k + 1][gl] = v.y;
-            s_sh[w][k + 2][gl] = v.z;
-            s_sh[w][k + 3][gl] = v.w;
+            *reinterpret_cast<float4 *>(sw + (f / 48) * SH_STRIDE + f % 48) = v;
         }
     }
     wave_lds_sync();
     float shv[48], dshv[48];
+    const float4 *mine = reinterpret_cast<const float4 *>(sw + lane * SH_STRIDE);
 #pragma unroll
-    for (int k = 0; k < 48; k++) {
-        shv[k] = s_sh[w][k][lane];
-        dshv[k] = 0.f;
+    for (int k = 0; k < 12; k++) {
+        const float4 v = mine[k];
+        shv[4 * k] = v.x;
+        shv[4 * k + 1] = v.y;
+        shv[4 * k + 2] = v.z;
+        shv[4 * k + 3] = v.w;
     }
+#pragma unroll
+    for (int k = 0; k < 48; k++) dshv[k] = 0.f;
     if (i < p.P) preprocess_bwd_one<true>(p, i, shv, dshv);
     if (!p.dL_dsh) return;
     wave_lds_sync();
+    float4 *mine_w = reinterpret_cast<float4 *>(sw + lane * SH_STRIDE);
 #pragma unroll
-    for (int k = 0; k < 48; k++) s_sh[w][k][lane] = dshv[k];
+    for (int k = 0; k < 12; k++) mine_w[k] = make_float4(dshv[4 * k], dshv[4 * k + 1], dshv[4 * k + 2], dshv[4 * k + 3]);
     wave_lds_sync();
 #pragma unroll
     for (int c = 0; c < 12; c++) {
         const uint32_t f = c * 256 + lane * 4;
-        if (gbase + f < gend) {
-            const uint32_t gl = f / 48, k = f % 48;
+        if (gbase + f < gend)
             *reinterpret_cast<float4 *>(p.dL_dsh + gbase + f) =
-                make_float4(s_sh[w][k][gl], s_sh[w][k + 1][gl], s_sh[w][k + 2][gl], s_sh[w][k + 3][gl]);
-        }
+                *reinterpret_cast<const float4 *>(sw + (f / 48) * SH_STRIDE + f % 48);
     }
 }
 

@@ -258,6 +258,11 @@ void gsr_reset_stage_times(void);
 /* Internal tuning knobs for A/B measurements (e.g. "bwd_occ4"); unknown names are ignored by kernels. */
 void gsr_set_tuning(const char *name, int value);
 
+/* Diagnostics: with the "stamp" knob set, the composite kernels record one (start, end, HW_ID, XCC_ID)
+ * uint32 quadruple per launch slot (start/end on the 100 MHz real-time clock).  which = 0: render_fwd,
+ * 1: render_bwd.  Copies up to max_slots quadruples to host memory; returns the count or < 0. */
+int gsr_debug_wave_stamps(int which, uint32_t *host_dst, int max_slots);
+
 const char *gsr_last_error(void);
 const char *gsr_build_info(void);
 
