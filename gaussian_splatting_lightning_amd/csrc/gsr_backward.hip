@@ -218,8 +218,8 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_bwd_v3_kernel(Rend
 }
 
 // ------------------------------------------------------------------------------------------------
-// v4: one scalar "behind" accumulator per pixel with the background folded in, strip skipping, and the next
-// batch's gathers in flight while the current batch composites.
+// v4: one scalar "behind" accumulator per pixel with the background folded in, strip skipping, and LDS
+// read-ahead.
 //   The reference keeps accum_rec (3 channels) and accum_invdepth per pixel and adds the background term
 //   -T_final / (1 - alpha) (bg . dL/dpix) to dL/dalpha.  Only the projection onto the pixel's upstream
 //   gradient enters dL/dalpha, so one scalar  D_k = (accum_rec_k + T_final / T_{k+1} bg) . dL/dpix
@@ -229,16 +229,16 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_bwd_v3_kernel(Rend
 //   of 14, and 7 live registers per pixel instead of 11.
 //   STRIP: a lane's pixel k lies in the tile's 4-row strip k; strips outside the instance's alpha >= 1/255
 //   row band (strip_mask, conservative) are skipped with one scalar test instead of per-lane exec branches.
-//   PRED: inside a strip the pair update is predicated (selects) instead of nested exec-mask branches.
-//   Gathers are software-pipelined two deep: while batch b composites, the records of batch b+1 (whose
-//   Gaussian ids arrived during batch b-1) and the ids of batch b+2 are loading.
+//   PRED 0: nested exec-mask branches (last contributor, power > 0, alpha < 1/255) around the pair update;
+//   1: the whole update predicated with selects; 2: one branch per pixel after the alpha test.
+//   LPF: the broadcast LDS reads of instance j+1 are issued before instance j's math.  (A two-deep software
+//   pipeline of the batches' global gathers was measured and gained nothing at 5 waves/SIMD.)
 // ------------------------------------------------------------------------------------------------
-template <bool HAS_INV, bool STRIP, bool PRED>
-__global__ __launch_bounds__(64, 5) void render_bwd_v4_kernel(RenderBwdParams p) {
-    __shared__ float4 s_a[BWD_BATCH];
-    __shared__ float4 s_b[BWD_BATCH];
-    __shared__ float2 s_c[BWD_BATCH];
-    __shared__ uint32_t s_m[BWD_BATCH];
+template <bool HAS_INV, bool STRIP, int PRED, bool LPF, int MIN_WAVES = 5>
+__global__ __launch_bounds__(64, MIN_WAVES) void render_bwd_v4_kernel(RenderBwdParams p) {
+    __shared__ float4 s_a[BWD_BATCH + 1];  // + 1: the LPF read-ahead of the batch's last instance
+    __shared__ float4 s_b[BWD_BATCH + 1];
+    __shared__ float2 s_c[BWD_BATCH + 1];
     __shared__ __attribute__((aligned(16))) float s_part[BWD_BATCH][PART];  // [instance][10 sums]
     const int lane = threadIdx.x;
     const int slot = blockIdx.x;
@@ -263,27 +263,7 @@ __global__ __launch_bounds__(64, 5) void render_bwd_v4_kernel(RenderBwdParams p)
         return;
     }
 
-    // Pipeline prologue: ids of batches 0 and 1, records of batch 0.
     int bend = (int)tl;
-    uint32_t nx_row = 0, nx_gid = 0, nn_row = 0, nn_gid = 0;
-    if (lane < min(BWD_BATCH, bend)) {
-        const uint32_t s_me = range.x + (uint32_t)(bend - 1 - lane);
-        nx_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
-        nx_gid = p.point_list[s_me];
-    }
-    if (lane < min(BWD_BATCH, bend - BWD_BATCH)) {
-        const uint32_t s_me = range.x + (uint32_t)(bend - BWD_BATCH - 1 - lane);
-        nn_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
-        nn_gid = p.point_list[s_me];
-    }
-    float4 nx_a = make_float4(0, 0, 0, 0), nx_b = nx_a;
-    float2 nx_c = make_float2(0, 0);
-    if (lane < min(BWD_BATCH, bend)) {
-        nx_a = p.rec_a[nx_gid];
-        nx_b = p.rec_b[nx_gid];
-        nx_c = p.rec_c[nx_gid];
-    }
-
     const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
     const size_t HW = (size_t)p.W * p.H;
     float T[PIX_PER_LANE], dp0[PIX_PER_LANE], dp1[PIX_PER_LANE], dp2[PIX_PER_LANE], dinv[PIX_PER_LANE];
@@ -307,42 +287,51 @@ __global__ __launch_bounds__(64, 5) void render_bwd_v4_kernel(RenderBwdParams p)
 
     for (; bend > 0; bend -= BWD_BATCH) {
         const int cnt = min(BWD_BATCH, bend);
-        const float4 my_a = nx_a, my_b = nx_b;
-        const uint32_t my_row = nx_row;
+        float4 my_a = make_float4(0, 0, 0, 0), my_b = my_a;
+        uint32_t my_row = 0, my_m = 0;
         if (lane < cnt) {
+            const uint32_t s_me = range.x + (uint32_t)(bend - 1 - lane);
+            my_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
+            const uint32_t gid = p.point_list[s_me];
+            my_a = p.rec_a[gid];
+            my_b = p.rec_b[gid];
             s_a[lane] = stage_rec_a(my_a);
             s_b[lane] = stage_rec_b(my_b);
-            s_c[lane] = nx_c;
-            if (STRIP) s_m[lane] = strip_mask(my_a, my_b, row0);
+            s_c[lane] = p.rec_c[gid];
+            if (STRIP) my_m = strip_mask(my_a, my_b, row0);
         }
-        // issue the next batch's record gathers and the batch after's ids
-        if (lane < min(BWD_BATCH, bend - BWD_BATCH)) {
-            nx_a = p.rec_a[nn_gid];
-            nx_b = p.rec_b[nn_gid];
-            nx_c = p.rec_c[nn_gid];
-        }
-        nx_row = nn_row;
-        if (lane < min(BWD_BATCH, bend - 2 * BWD_BATCH)) {
-            const uint32_t s_me = range.x + (uint32_t)(bend - 2 * BWD_BATCH - 1 - lane);
-            nn_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
-            nn_gid = p.point_list[s_me];
-        }
+        // strip k of instance j is live iff bit j of sk[k] (wave-uniform, scalar registers)
+        uint64_t sk[PIX_PER_LANE];
+#pragma unroll
+        for (int k = 0; k < PIX_PER_LANE; k++) sk[k] = STRIP ? __ballot((my_m >> k) & 1u) : ~0ull;
         wave_lds_sync();
+        float4 na = s_a[0], nb = s_b[0];
+        float2 nc = s_c[0];
         for (int j = 0; j < cnt; j++) {
             const uint32_t idx = (uint32_t)(bend - 1 - j);
-            const float4 a = s_a[j];  // x, y, A, B
-            const float4 b = s_b[j];  // C, o, r, g
-            const float2 c = s_c[j];  // b, 1/depth
-            const uint32_t sm = STRIP ? __builtin_amdgcn_readfirstlane(s_m[j]) : 0xfu;
+            float4 a, b;  // a: x, y, A, B; b: C, o, r, g
+            float2 c;     // b, 1/depth
+            if (LPF) {    // this instance's broadcast reads were issued during the previous one
+                a = na;
+                b = nb;
+                c = nc;
+                na = s_a[j + 1];
+                nb = s_b[j + 1];
+                nc = s_c[j + 1];
+            } else {
+                a = s_a[j];
+                b = s_b[j];
+                c = s_c[j];
+            }
             const float dx = a.x - pfx, dy0 = a.y - pfy0;
             const float P0 = (a.z * dx) * dx, L = a.w * dx;
             float Q0 = 0.f, Q1 = 0.f, Q2 = 0.f, w0 = 0.f, w1 = 0.f, w2 = 0.f, w3 = 0.f;
             bool any = false;
 #pragma unroll
             for (int k = 0; k < PIX_PER_LANE; k++) {
-                if (STRIP && !(sm & (1u << k))) continue;  // wave-uniform
+                if (STRIP && !((sk[k] >> j) & 1u)) continue;  // wave-uniform
                 const float dy = dy0 - (float)(4 * k);
-                if (PRED) {
+                if (PRED == 1) {
                     const float power2 = power2_at(b.x, dy, P0, L);
                     const float G = __builtin_amdgcn_exp2f(power2);
                     const float alpha = fminf(0.99f, b.y * G);
@@ -365,12 +354,21 @@ __global__ __launch_bounds__(64, 5) void render_bwd_v4_kernel(RenderBwdParams p)
                     Q1 += qdy;
                     Q2 = fmaf(qdy, dy, Q2);
                 } else {
-                    if (idx >= lastc[k]) continue;
-                    const float power2 = power2_at(b.x, dy, P0, L);
-                    if (power2 > 0.0f) continue;
-                    const float G = __builtin_amdgcn_exp2f(power2);
-                    const float alpha = fminf(0.99f, b.y * G);
-                    if (alpha < 1.0f / 255.0f) continue;
+                    float power2, G, alpha;
+                    if (PRED == 2) {
+                        // one exec-mask branch per pixel: the alpha test is evaluated for every lane of the strip
+                        power2 = power2_at(b.x, dy, P0, L);
+                        G = __builtin_amdgcn_exp2f(power2);
+                        alpha = fminf(0.99f, b.y * G);
+                        if (!(idx < lastc[k] && !(power2 > 0.0f) && !(alpha < 1.0f / 255.0f))) continue;
+                    } else {
+                        if (idx >= lastc[k]) continue;
+                        power2 = power2_at(b.x, dy, P0, L);
+                        if (power2 > 0.0f) continue;
+                        G = __builtin_amdgcn_exp2f(power2);
+                        alpha = fminf(0.99f, b.y * G);
+                        if (alpha < 1.0f / 255.0f) continue;
+                    }
                     any = true;
                     T[k] = T[k] * fast_rcp(1.f - alpha);
                     const float wgt = alpha * T[k];
@@ -440,13 +438,14 @@ void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
         q.prio_div = tuning("prio_div", 0);
         q.stamps = tuning("stamp", 0) ? stamp_buffer(1) : nullptr;
         const dim3 grid(p.num_tiles), block(64);
-        const int mode = tuning("bwd_strip", 1) * 2 + tuning("bwd_pred", 0);
+        const int strip = tuning("bwd_strip", 1), pred = tuning("bwd_pred", 2);
 #define GSR_BWD4(INV)                                                                                   \
         do {                                                                                           \
-            if (mode == 0) render_bwd_v4_kernel<INV, false, false><<<grid, block, 0, s>>>(q);          \
-            else if (mode == 1) render_bwd_v4_kernel<INV, false, true><<<grid, block, 0, s>>>(q);      \
-            else if (mode == 2) render_bwd_v4_kernel<INV, true, false><<<grid, block, 0, s>>>(q);      \
-            else render_bwd_v4_kernel<INV, true, true><<<grid, block, 0, s>>>(q);                      \
+            if (!strip) render_bwd_v4_kernel<INV, false, 0, false><<<grid, block, 0, s>>>(q);          \
+            else if (pred == 1) render_bwd_v4_kernel<INV, true, 1, false><<<grid, block, 0, s>>>(q);   \
+            else if (pred == 2) render_bwd_v4_kernel<INV, true, 2, false><<<grid, block, 0, s>>>(q);   \
+            else if (minw >= 6) render_bwd_v4_kernel<INV, true, 0, false, 6><<<grid, block, 0, s>>>(q); \
+            else render_bwd_v4_kernel<INV, true, 0, false><<<grid, block, 0, s>>>(q);                  \
         } while (0)
         if (p.dL_dinvdepth) GSR_BWD4(true);
         else GSR_BWD4(false);
