@@ -493,14 +493,14 @@ __device__ __forceinline__ void composite_fwd(const RenderFwdParams &p, const in
     const float pfx = (float)px, pfy0 = (float)py0;
     const float row0 = (float)(ty * BLOCK_Y);
     const int kbase = NPIX == 4 ? 0 : 2 * half;  // whole-tile pixel index of this wave's first pixel
+    // A pixel is live while T > 0: a pixel that stops (or lies outside the image) keeps -T, so the live test
+    // is one compare per pixel instead of a boolean carried in a register.
     float T[NPIX], C0[NPIX], C1[NPIX], C2[NPIX], ID[NPIX];
     uint32_t last[NPIX];
-    bool active[NPIX];
 #pragma unroll
     for (int k = 0; k < NPIX; k++) {
         const int py = py0 + 4 * (kbase + k);
-        active[k] = px < p.W && py < p.H;
-        T[k] = 1.0f;
+        T[k] = (px < p.W && py < p.H) ? 1.0f : -1.0f;
         C0[k] = C1[k] = C2[k] = ID[k] = 0.f;
         last[k] = 0;
     }
@@ -528,7 +528,7 @@ __device__ __forceinline__ void composite_fwd(const RenderFwdParams &p, const in
     for (uint32_t base = range.x; base < range.y; base += 64) {
         bool any = false;
 #pragma unroll
-        for (int k = 0; k < NPIX; k++) any |= active[k];
+        for (int k = 0; k < NPIX; k++) any |= T[k] > 0.f;
         if (__ballot(any) == 0) break;
         const uint32_t s = base + lane;
         if (PF) {
@@ -579,7 +579,7 @@ __device__ __forceinline__ void composite_fwd(const RenderFwdParams &p, const in
                 if (STRIP && !(sm & (1u << k))) continue;  // wave-uniform: no pixel of the strip passes
                 const float power2 = power2_at(b.x, dy0 - (float)(4 * (kbase + k)), P0, L);
                 const float alpha = fminf(0.99f, b.y * __builtin_amdgcn_exp2f(power2));
-                const bool ok = active[k] && !(power2 > 0.0f) && !(alpha < 1.0f / 255.0f);
+                const bool ok = T[k] > 0.f && !(power2 > 0.0f) && !(alpha < 1.0f / 255.0f);
                 const float test_T = T[k] * (1 - alpha);
                 const bool stop = ok && test_T < 0.0001f;
                 const bool take = ok && !stop;
@@ -588,13 +588,12 @@ __device__ __forceinline__ void composite_fwd(const RenderFwdParams &p, const in
                 C1[k] = fmaf(b.w, wgt, C1[k]);
                 C2[k] = fmaf(c.x, wgt, C2[k]);
                 ID[k] = fmaf(c.y, wgt, ID[k]);
-                T[k] = take ? test_T : T[k];
+                T[k] = take ? test_T : (stop ? -T[k] : T[k]);
                 last[k] = take ? contributor : last[k];
-                active[k] = active[k] && !stop;
             }
             bool still = false;
 #pragma unroll
-            for (int k = 0; k < NPIX; k++) still |= active[k];
+            for (int k = 0; k < NPIX; k++) still |= T[k] > 0.f;
             if (__ballot(still) == 0) break;
         }
         wave_lds_sync();
@@ -607,11 +606,12 @@ __device__ __forceinline__ void composite_fwd(const RenderFwdParams &p, const in
         const int py = py0 + 4 * (kbase + k);
         if (px < p.W && py < p.H) {
             const size_t pid = (size_t)py * p.W + px;
-            p.final_T[pid] = T[k];
+            const float Tk = fabsf(T[k]);
+            p.final_T[pid] = Tk;
             p.n_contrib[pid] = last[k];
-            p.out_color[pid] = C0[k] + T[k] * bg0;
-            p.out_color[HW + pid] = C1[k] + T[k] * bg1;
-            p.out_color[2 * HW + pid] = C2[k] + T[k] * bg2;
+            p.out_color[pid] = C0[k] + Tk * bg0;
+            p.out_color[HW + pid] = C1[k] + Tk * bg1;
+            p.out_color[2 * HW + pid] = C2[k] + Tk * bg2;
             if (p.out_invdepth) p.out_invdepth[pid] = ID[k];
             mx = max(mx, last[k]);
         }
