@@ -13,10 +13,12 @@ max-reduce of the radii (BASELINE.json config 4: one view per GPU).  Per-GPU wor
 weak.  value = N * Gaussians * W * H / step time (Gaussians*pixels/s, whole job).
 
 Extra fields on the one JSON line:
-  roofline      dominant kernel, achieved algorithmic bytes / its average duration from hipEvents recorded
-                around each stage on the launch stream during the timed steps (SURVEY.md §8(d) bytes);
+  roofline      dominant kernel, achieved algorithmic bytes / its average duration from a hipEvent pair
+                recorded around that kernel's stage on the launch stream during the timed steps (the only
+                events in the timed region; SURVEY.md §8(d) bytes);
   cpu_baseline  the oracle (oracle/gsr_oracle.c, C + OpenMP) on the same workload on the host cores;
-  stages_ms     average device time of every pipeline stage per step.
+  stages_ms     average device time of every pipeline stage per step, from a separate untimed pass of K steps
+                with an event pair around every stage.
 """
 from __future__ import annotations
 
@@ -122,10 +124,26 @@ def main():
         st = step()
     torch.cuda.synchronize()
 
-    # ---- timed region ----
+    # ---- per-stage breakdown (untimed): an event pair around every stage ----
     use_events = not args.no_stage_events
+    stage_avg = {}
+    if use_events:
+        _native.reset_stage_times()
+        _native.set_profiling(True)
+        for _ in range(args.steps):
+            st = step()
+        torch.cuda.synchronize()
+        _native.set_profiling(False)
+        stage_avg = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in _native.stage_times().items()}
+    # Every event is a marker packet in the stream, so the timed steps carry events around the dominant
+    # composite kernel only (its live launch time for the roofline), not around every stage.
+    dom = max(("render_fwd", "render_bwd"), key=lambda k: stage_avg.get(k, 0.0))
+
+    # ---- timed region ----
     _native.reset_stage_times()
-    _native.set_profiling(use_events)
+    if use_events:
+        _native.set_tuning("prof_mask", _native.stage_mask(dom))
+        _native.set_profiling(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -137,7 +155,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     _native.set_profiling(False)
-    stages = _native.stage_times()
+    _native.set_tuning("prof_mask", -1)
+    timed_stages = _native.stage_times()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -151,7 +170,6 @@ def main():
     nc = st.image_buffer[lay["img_n_contrib"]: lay["img_n_contrib"] + 4 * npix].view(torch.int32)
     sum_contrib = int(nc.sum(dtype=torch.int64).item())
     I = st.num_rendered
-    stage_avg = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in stages.items()}
     algo_bytes = {
         # F6 composite fwd = 8 B/T + 44 B/I + 24 B/P; B1 composite bwd adds 40 B/I of grads
         "render_fwd": 8 * T + 44 * I + 24 * npix,
@@ -160,8 +178,8 @@ def main():
         "preprocess_bwd": n * (40 + 12 * M) + 88 * n + n * (56 + 12 * M),
     }
     flops = {"render_fwd": 25.0 * sum_contrib, "render_bwd": 70.0 * sum_contrib}
-    dom = max(("render_fwd", "render_bwd"), key=lambda k: stage_avg.get(k, 0.0))
-    dom_ms = stage_avg.get(dom, 0.0)
+    tot, calls = timed_stages.get(dom, (0.0, 0))
+    dom_ms = tot / calls if calls else 0.0  # measured over the timed steps
     roofline = None
     if dom_ms > 0:
         ach = algo_bytes[dom] / (dom_ms * 1e-3) / 1e9
@@ -216,7 +234,8 @@ def main():
         "config": {"workload": cfg["desc"], "gaussians": n, "width": W, "height": H, "sh_degree": deg,
                    "views_per_step": world, "parallelism": f"dp{world} (one view per GPU, RCCL gradient exchange: {mode})",
                    "instances_per_view": I, "sum_n_contrib": sum_contrib,
-                   "stage_events": use_events},
+                   "stage_events": ("timed steps: dominant kernel only; stages_ms: separate untimed pass"
+                                    if use_events else "none")},
         "roofline": roofline, "cpu_baseline": cpu,
         "stages_ms": {k: round(v, 4) for k, v in stage_avg.items() if v > 0},
     }

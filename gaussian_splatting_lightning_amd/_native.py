@@ -202,6 +202,13 @@ def stage_times() -> dict:
     return {lib.gsr_stage_name(i).decode(): (tot[i], int(calls[i])) for i in range(n)}
 
 
+def stage_mask(*names: str) -> int:
+    """Bit mask of the named stages, for the "prof_mask" knob (-1: all stages)."""
+    lib = load()
+    idx = {lib.gsr_stage_name(i).decode(): i for i in range(lib.gsr_num_stages())}
+    return sum(1 << idx[n] for n in names)
+
+
 def state_layout(P: int, R: int, W: int, H: int) -> dict:
     out = StateLayout()
     load().gsr_state_layout_query(int(P), int(R), int(W), int(H), ctypes.byref(out))

@@ -128,7 +128,9 @@ struct StageScope {
     hipEvent_t a = nullptr;
     StageScope(hipStream_t s_, int st, bool dbg) : s(s_), stage(st), debug(dbg) {
         Profiler &p = prof();
-        if (p.enabled) {
+        // "prof_mask" (bit per Stage, default all): which stages get an event pair.  Every event adds a
+        // marker to the stream, so bench.py times its steps with events around the dominant kernel only.
+        if (p.enabled && ((tuning("prof_mask", -1) >> st) & 1)) {
             std::lock_guard<std::mutex> lk(p.mu);
             a = p.get();
             if (a) (void)hipEventRecord(a, s);
