@@ -33,9 +33,9 @@ int gsr::tuning(const char *name, int default_value) {
 }
 
 uint4 *gsr::stamp_buffer(int which) {
-    static uint4 *buf[2] = {nullptr, nullptr};
+    static uint4 *buf[4] = {nullptr, nullptr, nullptr, nullptr};
     std::lock_guard<std::mutex> lk(g_tune_mu);
-    if (which < 0 || which > 1) return nullptr;
+    if (which < 0 || which > 3) return nullptr;
     if (!buf[which] && hipMalloc(&buf[which], sizeof(uint4) * STAMP_SLOTS) == hipSuccess)
         (void)hipMemset(buf[which], 0, sizeof(uint4) * STAMP_SLOTS);
     return buf[which];

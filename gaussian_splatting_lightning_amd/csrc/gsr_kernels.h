@@ -8,7 +8,9 @@ namespace gsr {
 // Internal tuning knobs (A/B experiments in one process; defaults are the shipped configuration).
 int tuning(const char *name, int default_value);
 // Diagnostics: per-wave (start, end, HW_ID, XCC_ID) stamps of the composite kernels, one uint4 per launch
-// slot, written only when the "stamp" knob is set (buffer 0: render_fwd, 1: render_bwd).
+// slot, written only when the "stamp" knob is set (buffer 0: render_fwd, 1: render_bwd; 2: the last onesweep
+// sort pass, per block (start, ranked, looked back, end); 3: the multi-histogram, per block (start, loop done,
+// end, 0)).
 uint4 *stamp_buffer(int which);
 
 // ---- scan / sort (gsr_sort.hip) ----

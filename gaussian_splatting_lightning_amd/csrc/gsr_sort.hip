@@ -275,11 +275,17 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restr
     uint32_t key[RS_ITEMS], val[RS_ITEMS], rank[RS_ITEMS];
     const uint64_t lt = lanemask_lt(lane);
 #pragma unroll
+    for (int it = 0; it < RS_ITEMS; it++) {  // loads first (see rs_onesweep_kernel)
+        const uint32_t j = blk + w * (RS_TILE / 4) + it * 64 + lane;
+        const bool valid = j < n;
+        key[it] = valid ? keys_in[j] : 0u;
+        val[it] = IOTA_IN ? j : (valid ? vals_in[j] : 0u);
+    }
+#pragma unroll
     for (int it = 0; it < RS_ITEMS; it++) {
         const uint32_t j = blk + w * (RS_TILE / 4) + it * 64 + lane;
         const bool valid = j < n;
-        const uint32_t k = valid ? keys_in[j] : 0u;
-        const uint32_t v = IOTA_IN ? j : (valid ? vals_in[j] : 0u);
+        const uint32_t k = key[it];
         const uint32_t d = (k >> shift) & 255u;
         uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -295,8 +301,6 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restr
             r = before + (uint32_t)__popcll(lower);
             if (lower == 0) s_cnt[w][d] = before + (uint32_t)__popcll(peers);
         }
-        key[it] = k;
-        val[it] = v;
         rank[it] = r;
     }
     __syncthreads();
@@ -354,21 +358,32 @@ __device__ __forceinline__ void lb_store(uint32_t *p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+constexpr int MH_BATCH = 8;
 // Digit histograms of every pass in one read of the keys.  Keys that share a digit inside a wave are
 // aggregated by ballot (8 ballots per digit, one LDS add per distinct digit), so skewed digits -- the top
 // byte of depth keys is nearly constant -- cause no atomic serialisation.
 __global__ __launch_bounds__(256) void rs_multi_hist_kernel(const uint32_t *__restrict__ keys, uint32_t n,
-                                                            int passes, uint32_t *__restrict__ ctrl) {
+                                                            int passes, uint32_t *__restrict__ ctrl, uint4 *stamps) {
     __shared__ uint32_t h[RS_MAX_PASSES][RS_BINS];
+    const uint32_t t0 = stamps ? stamp_now() : 0u;
     const int tid = threadIdx.x, lane = tid & 63;
     for (int i = tid; i < RS_MAX_PASSES * RS_BINS; i += 256) (&h[0][0])[i] = 0;
     __syncthreads();
     const uint64_t lt = lanemask_lt(lane);
     const uint32_t stride = gridDim.x * 256;
-    for (uint32_t base = blockIdx.x * 256; base < n; base += stride) {  // uniform trip count per wave
-        const uint32_t j = base + tid;
+    // keys are loaded MH_BATCH at a time before the ballot work (one load latency per batch, not per key)
+    for (uint32_t base0 = blockIdx.x * 256; base0 < n; base0 += MH_BATCH * stride) {  // uniform per wave
+        uint32_t kb[MH_BATCH];
+#pragma unroll
+        for (int b = 0; b < MH_BATCH; b++) {
+            const uint32_t j = base0 + b * stride + tid;
+            kb[b] = j < n ? keys[j] : 0u;
+        }
+#pragma unroll
+        for (int b = 0; b < MH_BATCH; b++) {
+        const uint32_t j = base0 + b * stride + tid;
         const bool valid = j < n;
-        const uint32_t k = valid ? keys[j] : 0u;
+        const uint32_t k = kb[b];
         for (int p = 0; p < passes; p++) {
             const uint32_t d = (k >> (8 * p)) & 255u;
             uint64_t peers = __ballot(valid);
@@ -380,11 +395,17 @@ __global__ __launch_bounds__(256) void rs_multi_hist_kernel(const uint32_t *__re
             }
             if (valid && (peers & lt) == 0) atomicAdd(&h[p][d], (uint32_t)__popcll(peers));
         }
+        }
     }
     __syncthreads();
+    const uint32_t t1 = stamps ? stamp_now() : 0u;
     for (int p = 0; p < passes; p++) {
         const uint32_t c = h[p][tid];
         if (c) atomicAdd(&ctrl[RS_CTRL_HIST + p * RS_BINS + tid], c);
+    }
+    if (stamps) {
+        __syncthreads();
+        if (tid == 0 && blockIdx.x < (uint32_t)STAMP_SLOTS) stamps[blockIdx.x] = make_uint4(t0, t1, stamp_now(), 0u);
     }
 }
 
@@ -405,18 +426,20 @@ __global__ __launch_bounds__(256) void rs_hist_scan_kernel(uint32_t *__restrict_
     }
 }
 
-template <bool IOTA_IN, int ITEMS>
+template <bool IOTA_IN, int ITEMS, int LBW>
 __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__restrict__ keys_in,
                                                           const uint32_t *__restrict__ vals_in, uint32_t n,
                                                           int pass, uint32_t *__restrict__ ctrl,
                                                           uint32_t *__restrict__ status,
                                                           uint32_t *__restrict__ keys_out,
-                                                          uint32_t *__restrict__ vals_out) {
+                                                          uint32_t *__restrict__ vals_out, uint4 *stamps) {
     __shared__ uint32_t s_cnt[4][RS_BINS];  // per-wave running digit counts, then per-wave bases
     __shared__ uint32_t s_dstart[RS_BINS];  // block-local start of each digit's run
     __shared__ uint32_t s_gbase[RS_BINS];   // global start of this block's run of each digit
     __shared__ uint32_t s_wsum[4];
     __shared__ uint32_t s_bid;
+    const uint32_t t0 = stamps ? stamp_now() : 0u;
+    uint32_t t_rank = 0, t_lb = 0;
     __shared__ uint32_t s_keys[ITEMS * 256];
     __shared__ uint32_t s_vals[ITEMS * 256];
 
@@ -431,12 +454,20 @@ __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__rest
 
     uint32_t key[ITEMS], val[ITEMS], rank[ITEMS];
     const uint64_t lt = lanemask_lt(lane);
+    // all of the thread's loads are issued before the ranking: the ranking's LDS read-modify-write chain
+    // would otherwise wait one global-load latency per item (measured ~0.6 us each)
 #pragma unroll
     for (int it = 0; it < ITEMS; it++) {
         const uint32_t j = blk + w * (TILE / 4) + it * 64 + lane;
         const bool valid = j < n;
-        const uint32_t k = valid ? keys_in[j] : 0u;
-        const uint32_t v = IOTA_IN ? j : (valid ? vals_in[j] : 0u);
+        key[it] = valid ? keys_in[j] : 0u;
+        val[it] = IOTA_IN ? j : (valid ? vals_in[j] : 0u);
+    }
+#pragma unroll
+    for (int it = 0; it < ITEMS; it++) {
+        const uint32_t j = blk + w * (TILE / 4) + it * 64 + lane;
+        const bool valid = j < n;
+        const uint32_t k = key[it];
         const uint32_t d = (k >> shift) & 255u;
         uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -452,11 +483,10 @@ __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__rest
             r = before + (uint32_t)__popcll(lower);
             if (lower == 0) s_cnt[w][d] = before + (uint32_t)__popcll(peers);
         }
-        key[it] = k;
-        val[it] = v;
         rank[it] = r;
     }
     __syncthreads();
+    if (stamps) t_rank = stamp_now();
     {
         const int d = tid;
         const uint32_t c0 = s_cnt[0][d], c1 = s_cnt[1][d], c2 = s_cnt[2][d], c3 = s_cnt[3][d];
@@ -471,26 +501,47 @@ __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__rest
         if (lane == 63) s_wsum[w] = inc;
         uint32_t excl = 0;
         if (bid > 0) {
-            uint32_t look = bid - 1, spins = 0;
+            // Windowed look-back: LBW predecessors' words are loaded at once (one round-trip latency per
+            // window instead of per predecessor); published words are summed nearest first up to the first
+            // inclusive prefix, and an unpublished one is re-polled.  Positions before block 0 read as an
+            // inclusive prefix of 0.
+            int look = (int)bid - 1;
+            uint32_t spins = 0;
             while (true) {
-                const uint32_t v = lb_load(status + (size_t)look * RS_BINS + d);
-                const uint32_t f = v & ~LB_MASK;
-                if (f == 0) {
+                uint32_t v[LBW];
+#pragma unroll
+                for (int i = 0; i < LBW; i++)
+                    v[i] = (look - i >= 0) ? lb_load(status + (size_t)(look - i) * RS_BINS + d) : LB_INC;
+                bool found = false, stalled = false;
+                int used = 0;
+#pragma unroll
+                for (int i = 0; i < LBW; i++) {
+                    if (!found && !stalled) {
+                        const uint32_t f = v[i] & ~LB_MASK;
+                        if (f == 0) {
+                            stalled = true;
+                        } else {
+                            excl += v[i] & LB_MASK;
+                            used = i + 1;
+                            found = f == LB_INC;
+                        }
+                    }
+                }
+                if (found) break;
+                look -= used;
+                if (stalled) {
                     if (++spins > LB_SPIN_LIMIT) {
                         atomicOr(&ctrl[RS_CTRL_ERR], 1u);
                         break;
                     }
                     __builtin_amdgcn_s_sleep(1);
-                    continue;
                 }
-                excl += v & LB_MASK;
-                if (f == LB_INC || look == 0) break;
-                --look;
             }
             lb_store(st, LB_INC | (excl + tot));
         }
         s_gbase[d] = ctrl[RS_CTRL_HIST + pass * RS_BINS + d] + excl;
         __syncthreads();
+        if (stamps) t_lb = stamp_now();
         uint32_t woff = 0;
         for (int i = 0; i < w; i++) woff += s_wsum[i];
         s_dstart[d] = woff + inc - tot;
@@ -515,24 +566,27 @@ __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__rest
         keys_out[gpos] = k;
         vals_out[gpos] = v;
     }
+    if (stamps && tid == 0 && bid < (uint32_t)STAMP_SLOTS) stamps[bid] = make_uint4(t0, t_rank, t_lb, stamp_now());
 }
 
-template <int ITEMS>
+template <int ITEMS, int LBW>
 static void launch_radix_sort_onesweep(hipStream_t s, SortScratch &sc, uint32_t n, int passes, bool keyed) {
     const uint32_t nb = div_up(n, (uint32_t)ITEMS * 256u);
     (void)hipMemsetAsync(sc.ctrl, 0, sizeof(uint32_t) * (RS_CTRL_WORDS + (size_t)passes * nb * RS_BINS), s);
     const uint32_t hb = min(div_up(n, 256u * 8u), 2048u);
-    rs_multi_hist_kernel<<<max(hb, 1u), 256, 0, s>>>(sc.k[0], n, passes, sc.ctrl);
+    uint4 *stamps = tuning("stamp", 0) ? stamp_buffer(2) : nullptr;
+    rs_multi_hist_kernel<<<max(hb, 1u), 256, 0, s>>>(sc.k[0], n, passes, sc.ctrl,
+                                                    stamps ? stamp_buffer(3) : nullptr);
     rs_hist_scan_kernel<<<1, 256, 0, s>>>(sc.ctrl, passes);
     for (int p = 0; p < passes; p++) {
         const int in = p & 1, out = (p + 1) & 1;
         uint32_t *st = sc.status + (size_t)p * nb * RS_BINS;
         if (p == 0 && !keyed)
-            rs_onesweep_kernel<true, ITEMS><<<nb, 256, 0, s>>>(sc.k[in], nullptr, n, p, sc.ctrl, st, sc.k[out],
-                                                               sc.v[out]);
+            rs_onesweep_kernel<true, ITEMS, LBW><<<nb, 256, 0, s>>>(sc.k[in], nullptr, n, p, sc.ctrl, st, sc.k[out],
+                                                               sc.v[out], stamps);
         else
-            rs_onesweep_kernel<false, ITEMS><<<nb, 256, 0, s>>>(sc.k[in], sc.v[in], n, p, sc.ctrl, st, sc.k[out],
-                                                                sc.v[out]);
+            rs_onesweep_kernel<false, ITEMS, LBW><<<nb, 256, 0, s>>>(sc.k[in], sc.v[in], n, p, sc.ctrl, st, sc.k[out],
+                                                                sc.v[out], stamps);
     }
 }
 
@@ -543,7 +597,9 @@ void launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bo
     // onesweep knob: bit 0 = depth-size sorts (nbits == 32), bit 1 = tile sorts
     const int os = tuning("onesweep", 1);
     if (n <= RS_ONESWEEP_MAX_N && passes <= RS_MAX_PASSES && (os & (nbits == 32 ? 1 : 2))) {
-        launch_radix_sort_onesweep<RS_ITEMS>(s, sc, n, passes, keyed);  // 8-/32-key tiles measured slower
+        // 8-/32-key tiles measured slower
+        if (tuning("lbw", 16) >= 16) launch_radix_sort_onesweep<RS_ITEMS, 16>(s, sc, n, passes, keyed);
+        else launch_radix_sort_onesweep<RS_ITEMS, 1>(s, sc, n, passes, keyed);
         return;
     }
     for (int p = 0; p < passes; p++) {

@@ -260,7 +260,7 @@ void gsr_set_tuning(const char *name, int value);
 
 /* Diagnostics: with the "stamp" knob set, the composite kernels record one (start, end, HW_ID, XCC_ID)
  * uint32 quadruple per launch slot (start/end on the 100 MHz real-time clock).  which = 0: render_fwd,
- * 1: render_bwd.  Copies up to max_slots quadruples to host memory; returns the count or < 0. */
+ * 1: render_bwd, 2: radix-sort pass blocks (start, ranked, looked back, end), 3: radix histogram blocks.  Copies up to max_slots quadruples to host memory; returns the count or < 0. */
 int gsr_debug_wave_stamps(int which, uint32_t *host_dst, int max_slots);
 
 const char *gsr_last_error(void);
