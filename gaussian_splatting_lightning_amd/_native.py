@@ -79,7 +79,7 @@ PLY_TYPE_SIZE = (4, 8, 1, 1, 2, 2, 4, 4)
 class StateLayout(ctypes.Structure):
     _fields_ = [(n, ctypes.c_size_t) for n in (
         "geom_rec_a", "geom_rec_b", "geom_rec_c", "geom_tiles", "geom_order", "geom_inst_off", "geom_inst_start",
-        "geom_clamped", "geom_sorted_depth", "geom_expand_rec", "bin_point_list", "bin_inv", "bin_keys_sorted", "bin_sorted_u", "bin_inst_gid",
+        "geom_clamped", "geom_depth_key", "geom_expand_rec", "bin_point_list", "bin_inv", "bin_keys_sorted", "bin_sorted_u", "bin_inst_gid",
         "img_final_T", "img_n_contrib", "img_ranges", "img_tile_last", "img_tile_loaded")]
 
 

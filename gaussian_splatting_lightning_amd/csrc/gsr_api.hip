@@ -7,6 +7,7 @@
 // ranges -> composite; backward: reverse composite -> big-Gaussian reduce -> preprocess backward.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <mutex>
@@ -73,11 +74,15 @@ enum Stage {
     ST_BIG_REDUCE,
     ST_PREPROCESS_BWD,
     ST_SH_VIEWS,
+    ST_BK_COUNT,
+    ST_BK_SCATTER,
+    ST_SEG_SORT,
     ST_COUNT
 };
 const char *kStageNames[ST_COUNT] = {"preprocess", "depth_sort", "instance_scan", "readback",
                                      "expand",     "tile_sort",  "tile_ranges",   "render_fwd",
-                                     "render_bwd", "big_reduce", "preprocess_bwd", "sh_views"};
+                                     "render_bwd", "big_reduce", "preprocess_bwd", "sh_views",
+                                     "bucket_count", "bucket_scatter", "seg_sort"};
 
 struct Profiler {
     std::mutex mu;
@@ -241,7 +246,7 @@ void gsr_state_layout_query(int P, int64_t R, int W, int H, gsr_state_layout *ou
     out->geom_inst_start = off(g.inst_start);
     out->geom_clamped = off(g.clamped);
     out->geom_expand_rec = off(g.exp_rec);
-    out->geom_sorted_depth = off(g.sort.k[0]);
+    out->geom_depth_key = off(g.depth_key);
     out->bin_point_list = off(b.point_list);
     out->bin_inv = off(b.inv);
     out->bin_keys_sorted = off(b.keys_sorted);
@@ -310,15 +315,24 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     if (!hw || !rb_ev) return fail(GSR_ERR_HIP, "pinned host buffer / event allocation failed");
     GSR_HIP(hipMemcpyAsync(hw, g.counters, CNT_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
     GSR_HIP(hipEventRecord(rb_ev, stream));
-    GSR_STAGE(ST_DEPTH_SORT, dbg, launch_radix_sort(stream, g.sort, (uint32_t)P, 32));
-    if (tuning("scan_lookback", 1))
+    // Bucket binning (gsr_bin.hip) whenever the tile counters fit one workgroup's LDS; the radix path
+    // (depth sort, depth-ordered expansion, stable tile sort) otherwise.
+    const bool bucket = T <= BK_MAX_TILES && tuning("bucket", 1);
+    if (bucket) {
         GSR_STAGE(ST_SCAN, dbg,
-                  launch_exclusive_scan_lookback(stream, g.tiles, g.order, (uint32_t)P, g.inst_off, g.scan_status,
+                  launch_exclusive_scan_lookback(stream, g.tiles, nullptr, (uint32_t)P, g.inst_start, g.scan_status,
                                                  g.counters + CNT_SCAN_TICKET, g.counters + CNT_OVERFLOW));
-    else
-        GSR_STAGE(ST_SCAN, dbg,
-                  launch_exclusive_scan(stream, g.tiles, g.order, (uint32_t)P, g.inst_off, g.scan_tmp,
-                                        g.counters + CNT_OVERFLOW));
+    } else {
+        GSR_STAGE(ST_DEPTH_SORT, dbg, launch_radix_sort(stream, g.sort, (uint32_t)P, 32, false, g.depth_key));
+        if (tuning("scan_lookback", 1))
+            GSR_STAGE(ST_SCAN, dbg,
+                      launch_exclusive_scan_lookback(stream, g.tiles, g.order, (uint32_t)P, g.inst_off, g.scan_status,
+                                                     g.counters + CNT_SCAN_TICKET, g.counters + CNT_OVERFLOW));
+        else
+            GSR_STAGE(ST_SCAN, dbg,
+                      launch_exclusive_scan(stream, g.tiles, g.order, (uint32_t)P, g.inst_off, g.scan_tmp,
+                                            g.counters + CNT_OVERFLOW));
+    }
     GSR_STAGE(ST_READBACK, dbg, GSR_HIP(hipEventSynchronize(rb_ev)));
     uint64_t total64 = 0;
     for (int k = 0; k < CNT_NPART; k++) {
@@ -338,21 +352,46 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     carve_binning(bin, R, T, b);
     if ((uint64_t)RS_BINS * div_up(R ? R : 1, RS_TILE) + 1 > (uint64_t)SCAN_TILE * SCAN_MAX_BLOCKS)
         return fail(GSR_ERR_OVERFLOW, "too many tile instances for the single-level scan");
-    if (R > 0) {
-        ExpandParams ep;
-        ep.P = (uint32_t)P; ep.R = R; ep.gx = gx; ep.gy = gy;
-        ep.order = g.order; ep.inst_off = g.inst_off; ep.tiles = g.tiles; ep.exp_rec = g.exp_rec;
-        ep.keys_out = b.sort.k[0]; ep.inst_gid = b.inst_gid; ep.inst_start = g.inst_start;
-        GSR_STAGE(ST_EXPAND, dbg, launch_expand(stream, ep));
-        GSR_STAGE(ST_TILE_SORT, dbg, launch_radix_sort(stream, b.sort, R, tile_key_bits(T)));
-        GSR_HIP(hipMemsetAsync(b.inv, 0xff, sizeof(uint32_t) * (size_t)R, stream));
-    }
-    GSR_STAGE(ST_RANGES, dbg, {
-        GSR_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * T, stream));
-        launch_identify_ranges(stream, b.keys_sorted, R, im.ranges);
-    });
     const int lpt = tuning("lpt", 1);
-    if (lpt) launch_tile_order(stream, im.ranges, nullptr, 0, (int)T, im.order_fwd);
+    if (bucket) {
+        if (R > 0) {
+            BucketParams bp;
+            bp.P = (uint32_t)P; bp.T = T; bp.gx = gx; bp.nbig = nbig;
+            bp.nb = std::max(1u, std::min({(uint32_t)tuning("bk_blocks", 256), BK_MAX_BLOCKS, div_up(P, 1024)}));
+            bp.gper = div_up(div_up(P, bp.nb), 64) * 64;
+            bp.nb = div_up(P, bp.gper);
+            bp.tiles = g.tiles; bp.inst_start = g.inst_start; bp.depth_key = g.depth_key; bp.big_list = g.big_list;
+            bp.exp_rec = g.exp_rec;
+            bp.hist = b.bk_hist; bp.tile_cnt = b.bk_tile_cnt; bp.tile_start = b.bk_tile_start; bp.ranges = im.ranges;
+            bp.long_list = b.bk_long_list; bp.long_cnt = b.bk_long_cnt; bp.keys = b.bk_keys; bp.inst_gid = b.inst_gid;
+            GSR_STAGE(ST_BK_COUNT, dbg, launch_bucket_count(stream, bp));
+            GSR_STAGE(ST_BK_SCATTER, dbg, launch_bucket_scatter(stream, bp));
+            if (lpt) launch_tile_order(stream, im.ranges, nullptr, 0, (int)T, im.order_fwd);
+            SegSortParams sp;
+            sp.T = T; sp.ranges = im.ranges; sp.tile_order = lpt ? im.order_fwd : nullptr; sp.keys = b.bk_keys; sp.keys2 = b.bk_keys2;
+            sp.sorted_u = b.sorted_u; sp.long_list = b.bk_long_list; sp.long_cnt = b.bk_long_cnt;
+            GSR_STAGE(ST_SEG_SORT, dbg, launch_seg_sort(stream, sp));
+            GSR_HIP(hipMemsetAsync(b.inv, 0xff, sizeof(uint32_t) * (size_t)R, stream));
+        } else {
+            GSR_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * T, stream));
+            if (lpt) launch_tile_order(stream, im.ranges, nullptr, 0, (int)T, im.order_fwd);
+        }
+    } else {
+        if (R > 0) {
+            ExpandParams ep;
+            ep.P = (uint32_t)P; ep.R = R; ep.gx = gx; ep.gy = gy;
+            ep.order = g.order; ep.inst_off = g.inst_off; ep.tiles = g.tiles; ep.exp_rec = g.exp_rec;
+            ep.keys_out = b.sort.k[0]; ep.inst_gid = b.inst_gid; ep.inst_start = g.inst_start;
+            GSR_STAGE(ST_EXPAND, dbg, launch_expand(stream, ep));
+            GSR_STAGE(ST_TILE_SORT, dbg, launch_radix_sort(stream, b.sort, R, tile_key_bits(T)));
+            GSR_HIP(hipMemsetAsync(b.inv, 0xff, sizeof(uint32_t) * (size_t)R, stream));
+        }
+        GSR_STAGE(ST_RANGES, dbg, {
+            GSR_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * T, stream));
+            launch_identify_ranges(stream, b.keys_sorted, R, im.ranges);
+        });
+        if (lpt) launch_tile_order(stream, im.ranges, nullptr, 0, (int)T, im.order_fwd);
+    }
     // split heavy tiles combine tile_last / tile_loaded with atomicMax: start from zero (adjacent arrays)
     GSR_HIP(hipMemsetAsync(im.tile_last, 0,
                            (size_t)(reinterpret_cast<char *>(im.tile_loaded + T) - reinterpret_cast<char *>(im.tile_last)),

@@ -87,13 +87,14 @@ struct GeomState {
     float4 *rec_a;         // P
     float4 *rec_b;         // P
     float2 *rec_c;         // P
-    uint32_t *depth_key;   // P: float bits of view depth, 0xffffffff if culled (aliases sort.k[0])
+    uint32_t *depth_key;   // P: float bits of view depth, 0xffffffff if culled
     uint32_t *tiles;       // P: tiles touched
     uint8_t *clamped;      // P: bit c set if SH colour channel c was clamped at 0
     uint4 *exp_rec;        // P: expansion record {kept-tile mask lo, hi, rmin.x | rmin.y << 16, rect width}; mask 0 =
                            //    all tiles of the rect (area > 64 or culling off).  One 16-B gather per Gaussian.
-    uint32_t *inst_off;    // P+1: exclusive scan of tiles in depth order, [P] = total
-    uint32_t *inst_start;  // P: first instance (expansion order) of each Gaussian
+    uint32_t *inst_off;    // P+1: radix path: exclusive scan of tiles in depth order, [P] = total
+    uint32_t *inst_start;  // P+1: first instance (expansion order) of each Gaussian (bucket path: the
+                           //      exclusive scan of tiles in Gaussian order, [P] = total)
     uint32_t *big_list;    // P: Gaussians with > BIG_GAUSSIAN_TILES tiles
     uint32_t *big_slot;    // P: index of a big Gaussian in big_list (valid only for big ones)
     uint32_t *scan_tmp;    // block sums for the instance scan (multi-kernel path)
@@ -114,12 +115,12 @@ inline size_t carve_geom(char *base, int P, GeomState &g) {
     g.clamped = c.take<uint8_t>(n);
     g.exp_rec = c.take<uint4>(n);
     g.inst_off = c.take<uint32_t>((size_t)n + 1);
-    g.inst_start = c.take<uint32_t>(n);
+    g.inst_start = c.take<uint32_t>((size_t)n + 1);
+    g.depth_key = c.take<uint32_t>(n);
     g.big_list = c.take<uint32_t>(n);
     g.big_slot = c.take<uint32_t>(n);
     g.scan_tmp = c.take<uint32_t>(div_up(n + 1, SCAN_TILE) + 1);
-    carve_sort(c, g.sort, n, true);
-    g.depth_key = g.sort.k[0];  // preprocess writes the depth-sort keys in place
+    carve_sort(c, g.sort, n, true);  // radix path: depth sort, keys read from depth_key
     g.order = g.sort.v[0];
     return c.off + 256;
 }
@@ -131,14 +132,25 @@ inline int tile_key_bits(uint32_t num_tiles) {
 }
 inline int radix_passes(int bits) { return (bits + 7) / 8; }
 
+// Bucket binning (gsr_bin.hip): used when the tile count fits the LDS histogram of one workgroup.
+constexpr uint32_t BK_MAX_TILES = 32768;  // 128 KB of LDS counters (4K images: 32400 tiles)
+constexpr uint32_t BK_MAX_BLOCKS = 512;   // rows of the count matrix (carved for the maximum)
+constexpr uint32_t SEG_CAP = 512;         // longest tile the per-wave register sort takes (8 keys per lane)
+constexpr uint32_t SEG_BLOCK_CAP = 2048;  // longest tile one workgroup sorts (4 waves x 512 keys); longer: chunks
+
 struct BinningState {
     uint32_t *inst_gid;    // R: Gaussian of each instance (expansion order)
     uint32_t *point_list;  // R: Gaussian ids sorted by (tile, depth, id); written by the forward composite
                            //    for the instances it loads (every instance any pixel can reach)
     uint32_t *inv;         // R: expansion index -> sorted position, for loaded instances; else INV_NONE
-    uint32_t *keys_sorted; // R: tile id of each sorted instance
-    uint32_t *sorted_u;    // R: expansion index of each sorted instance (radix-sort values)
-    SortScratch sort;      // tile sort (R keys)
+    uint32_t *sorted_u;    // R: expansion index of each sorted instance
+    // scratch of the two binning paths (overlapping: only one runs per forward)
+    uint32_t *keys_sorted; // radix path: R tile ids of the sorted instances
+    SortScratch sort;      // radix path: tile sort (R keys); its final value buffer is sorted_u
+    unsigned long long *bk_keys;  // bucket path: R keys (depth << 32 | u) bucketed by tile
+    unsigned long long *bk_keys2; // bucket path: R, chunk-sorted keys of tiles longer than SEG_BLOCK_CAP
+    uint32_t *bk_hist;     // bucket path: BK_MAX_BLOCKS x T count matrix
+    uint32_t *bk_tile_cnt, *bk_tile_start, *bk_long_list, *bk_long_cnt;
 };
 constexpr uint32_t INV_NONE = 0xffffffffu;
 
@@ -148,11 +160,22 @@ inline size_t carve_binning(char *base, int64_t R, uint32_t num_tiles, BinningSt
     b.inst_gid = c.take<uint32_t>(n ? n : 1);
     b.point_list = c.take<uint32_t>(n ? n : 1);
     b.inv = c.take<uint32_t>(n ? n : 1);
+    b.sorted_u = c.take<uint32_t>(n ? n : 1);
+    Carver cr = c;  // radix view
     int passes = radix_passes(tile_key_bits(num_tiles));
-    carve_sort(c, b.sort, n, passes >= 2);
-    // keys and values end in slot (passes & 1)
+    carve_sort(cr, b.sort, n, passes >= 2);
+    // keys and values end in slot (passes & 1); the last pass writes its values straight into sorted_u
     b.keys_sorted = b.sort.k[passes & 1];
-    b.sorted_u = b.sort.v[passes & 1];
+    b.sort.v[passes & 1] = b.sorted_u;
+    Carver cb = c;  // bucket view
+    b.bk_keys = cb.take<unsigned long long>(n ? n : 1);
+    b.bk_keys2 = cb.take<unsigned long long>(n ? n : 1);
+    b.bk_hist = cb.take<uint32_t>((size_t)BK_MAX_BLOCKS * num_tiles + 1);
+    b.bk_tile_cnt = cb.take<uint32_t>((size_t)num_tiles + 1);
+    b.bk_tile_start = cb.take<uint32_t>((size_t)num_tiles + 1);
+    b.bk_long_list = cb.take<uint32_t>(2 * ((size_t)num_tiles + 1));
+    b.bk_long_cnt = cb.take<uint32_t>(2);
+    c.off = cr.off > cb.off ? cr.off : cb.off;
     return c.off + 256;
 }
 

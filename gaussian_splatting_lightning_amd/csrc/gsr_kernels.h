@@ -27,7 +27,9 @@ void launch_exclusive_scan_lookback(hipStream_t s, const uint32_t *in, const uin
 // sc.v[passes & 1].
 // LSD radix sort of sc.k[0] (nbits significant bits); values are the iota permutation unless `keyed`, in which
 // case sc.v[0] holds the input values.  The result lands in buffer index (passes & 1).
-void launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bool keyed = false);
+// keys0 (optional): read the first pass's keys from there instead of sc.k[0] (left unmodified).
+void launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bool keyed = false,
+                       const uint32_t *keys0 = nullptr);
 
 // ---- forward (gsr_forward.hip) ----
 struct PreprocessParams {
@@ -52,6 +54,35 @@ struct ExpandParams {
 void launch_expand(hipStream_t s, const ExpandParams &p);
 
 void launch_identify_ranges(hipStream_t s, const uint32_t *keys_sorted, uint32_t R, uint2 *ranges);
+
+// ---- bucket binning (gsr_bin.hip) ----
+struct BucketParams {
+    uint32_t P, T, nb, gper, nbig;  // Gaussians, tiles, walk blocks, Gaussians per block, big Gaussians
+    int gx;
+    const uint32_t *tiles, *inst_start, *depth_key, *big_list;
+    const uint4 *exp_rec;
+    uint32_t *hist;        // nb x T counts, then column prefixes
+    uint32_t *tile_cnt;    // T
+    uint32_t *tile_start;  // T + 1
+    uint2 *ranges;         // T
+    uint32_t *long_list;   // 2 x (T + 1): tiles of (SEG_CAP, SEG_BLOCK_CAP] instances, longer tiles
+    uint32_t *long_cnt;    // 2 counts (written by the tile scan)
+    unsigned long long *keys;  // R: depth << 32 | u, bucketed by tile
+    uint32_t *inst_gid;    // R
+};
+void launch_bucket_count(hipStream_t s, const BucketParams &p);    // walk + column prefixes + tile ranges
+void launch_bucket_scatter(hipStream_t s, const BucketParams &p);
+
+struct SegSortParams {
+    uint32_t T;
+    const uint2 *ranges;
+    const uint32_t *tile_order;  // or null
+    unsigned long long *keys;   // R bucketed keys
+    unsigned long long *keys2;  // R: chunk-sorted keys of the tiles longer than SEG_BLOCK_CAP
+    uint32_t *sorted_u;
+    const uint32_t *long_list, *long_cnt;
+};
+void launch_seg_sort(hipStream_t s, const SegSortParams &p);
 
 // Tiles ordered by descending work (range length, or tile_last when use_last) for an LPT launch order.
 void launch_tile_order(hipStream_t s, const uint2 *ranges, const uint32_t *tile_last, int use_last, int T,

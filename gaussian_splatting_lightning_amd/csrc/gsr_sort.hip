@@ -570,46 +570,50 @@ __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__rest
 }
 
 template <int ITEMS, int LBW>
-static void launch_radix_sort_onesweep(hipStream_t s, SortScratch &sc, uint32_t n, int passes, bool keyed) {
+static void launch_radix_sort_onesweep(hipStream_t s, SortScratch &sc, uint32_t n, int passes, bool keyed,
+                                       const uint32_t *keys0) {
     const uint32_t nb = div_up(n, (uint32_t)ITEMS * 256u);
     (void)hipMemsetAsync(sc.ctrl, 0, sizeof(uint32_t) * (RS_CTRL_WORDS + (size_t)passes * nb * RS_BINS), s);
     const uint32_t hb = min(div_up(n, 256u * 8u), 2048u);
     uint4 *stamps = tuning("stamp", 0) ? stamp_buffer(2) : nullptr;
-    rs_multi_hist_kernel<<<max(hb, 1u), 256, 0, s>>>(sc.k[0], n, passes, sc.ctrl,
+    rs_multi_hist_kernel<<<max(hb, 1u), 256, 0, s>>>(keys0, n, passes, sc.ctrl,
                                                     stamps ? stamp_buffer(3) : nullptr);
     rs_hist_scan_kernel<<<1, 256, 0, s>>>(sc.ctrl, passes);
     for (int p = 0; p < passes; p++) {
         const int in = p & 1, out = (p + 1) & 1;
         uint32_t *st = sc.status + (size_t)p * nb * RS_BINS;
+        const uint32_t *kin = p == 0 ? keys0 : sc.k[in];
         if (p == 0 && !keyed)
-            rs_onesweep_kernel<true, ITEMS, LBW><<<nb, 256, 0, s>>>(sc.k[in], nullptr, n, p, sc.ctrl, st, sc.k[out],
+            rs_onesweep_kernel<true, ITEMS, LBW><<<nb, 256, 0, s>>>(kin, nullptr, n, p, sc.ctrl, st, sc.k[out],
                                                                sc.v[out], stamps);
         else
-            rs_onesweep_kernel<false, ITEMS, LBW><<<nb, 256, 0, s>>>(sc.k[in], sc.v[in], n, p, sc.ctrl, st, sc.k[out],
+            rs_onesweep_kernel<false, ITEMS, LBW><<<nb, 256, 0, s>>>(kin, sc.v[in], n, p, sc.ctrl, st, sc.k[out],
                                                                 sc.v[out], stamps);
     }
 }
 
-void launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bool keyed) {
+void launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bool keyed, const uint32_t *keys0) {
     if (n == 0) return;
+    if (!keys0) keys0 = sc.k[0];
     const uint32_t nb = div_up(n, RS_TILE);
     const int passes = radix_passes(nbits);
     // onesweep knob: bit 0 = depth-size sorts (nbits == 32), bit 1 = tile sorts
     const int os = tuning("onesweep", 1);
     if (n <= RS_ONESWEEP_MAX_N && passes <= RS_MAX_PASSES && (os & (nbits == 32 ? 1 : 2))) {
         // 8-/32-key tiles measured slower
-        if (tuning("lbw", 16) >= 16) launch_radix_sort_onesweep<RS_ITEMS, 16>(s, sc, n, passes, keyed);
-        else launch_radix_sort_onesweep<RS_ITEMS, 1>(s, sc, n, passes, keyed);
+        if (tuning("lbw", 16) >= 16) launch_radix_sort_onesweep<RS_ITEMS, 16>(s, sc, n, passes, keyed, keys0);
+        else launch_radix_sort_onesweep<RS_ITEMS, 1>(s, sc, n, passes, keyed, keys0);
         return;
     }
     for (int p = 0; p < passes; p++) {
         const int shift = 8 * p, in = p & 1, out = (p + 1) & 1;
-        rs_hist_kernel<<<nb, 256, 0, s>>>(sc.k[in], n, shift, sc.counts, nb);
+        const uint32_t *kin = p == 0 ? keys0 : sc.k[in];
+        rs_hist_kernel<<<nb, 256, 0, s>>>(kin, n, shift, sc.counts, nb);
         launch_exclusive_scan(s, sc.counts, nullptr, RS_BINS * nb, sc.counts, sc.scan_tmp, nullptr);
         if (p == 0 && !keyed)
-            rs_scatter_kernel<true><<<nb, 256, 0, s>>>(sc.k[in], nullptr, n, shift, sc.counts, nb, sc.k[out], sc.v[out]);
+            rs_scatter_kernel<true><<<nb, 256, 0, s>>>(kin, nullptr, n, shift, sc.counts, nb, sc.k[out], sc.v[out]);
         else
-            rs_scatter_kernel<false><<<nb, 256, 0, s>>>(sc.k[in], sc.v[in], n, shift, sc.counts, nb, sc.k[out],
+            rs_scatter_kernel<false><<<nb, 256, 0, s>>>(kin, sc.v[in], n, shift, sc.counts, nb, sc.k[out],
                                                         sc.v[out]);
     }
 }

@@ -237,7 +237,7 @@ size_t gsr_bwd_scratch_bytes(int64_t R, int64_t num_big);
 typedef struct gsr_state_layout {
     size_t geom_rec_a, geom_rec_b, geom_rec_c; /* float4, float4, float2 per Gaussian */
     size_t geom_tiles, geom_order, geom_inst_off, geom_inst_start, geom_clamped; /* u32, u32, u32, u32, u8 */
-    size_t geom_sorted_depth; /* u32 depth bits in depth-rank order (depth of order[r]) */
+    size_t geom_depth_key;    /* u32 float bits of each Gaussian's view depth (0xffffffff: not rendered) */
     size_t geom_expand_rec;   /* uint4 {kept-tile mask lo, hi, rmin.x | rmin.y << 16, rect width} (mask 0 = all) */
     size_t bin_point_list, bin_inv, bin_keys_sorted;                  /* u32 per instance */
     size_t bin_sorted_u, bin_inst_gid;                                /* u32 per instance */

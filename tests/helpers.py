@@ -112,10 +112,7 @@ def hip_state_arrays(out: dict) -> dict:
         tiles=view(st.geom_buffer, lay["geom_tiles"], P, i32).astype(np.uint32),
         num_rendered=R)
     rec_a = view(st.geom_buffer, lay["geom_rec_a"], 4 * P, torch.float32).reshape(P, 4)
-    order = view(st.geom_buffer, lay["geom_order"], P, i32).astype(np.int64)
-    sorted_depth = view(st.geom_buffer, lay["geom_sorted_depth"], P, i32)
-    depth_bits = np.zeros(P, np.int32)
-    depth_bits[order] = sorted_depth
+    depth_bits = view(st.geom_buffer, lay["geom_depth_key"], P, i32)
     rec_b = view(st.geom_buffer, lay["geom_rec_b"], 4 * P, torch.float32).reshape(P, 4)
     res["xy"] = np.ascontiguousarray(rec_a[:, :2])
     res["conic_opacity"] = np.ascontiguousarray(np.concatenate([rec_a[:, 2:4], rec_b[:, 0:2]], 1))
