@@ -289,7 +289,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     char *img = alloc(alloc_ctx, GSR_BUF_IMAGE, carve_image(nullptr, W, H, im));
     if (!img) return fail(GSR_ERR_ALLOC, "image buffer allocation failed");
     carve_image(img, W, H, im);
-    const size_t clear_bytes = (size_t)(reinterpret_cast<char *>(g.scan_status + div_up(P + 1, SCAN_TILE) + 1) -
+    const size_t clear_bytes = (size_t)(reinterpret_cast<char *>(g.tile_status + BK_MAX_TILES / 64 + 1) -
                                         reinterpret_cast<char *>(g.counters));
     GSR_HIP(hipMemsetAsync(g.counters, 0, clear_bytes, stream));  // counters + instance-scan look-back words
 
@@ -306,6 +306,11 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     pp.view = a->viewmatrix; pp.proj = a->projmatrix; pp.campos = a->campos;
     pp.radii = a->radii;
     pp.g = g;
+    // Bucket binning (gsr_bin.hip) whenever the tile counters fit one workgroup's LDS; the radix path
+    // (depth sort, depth-ordered expansion, stable tile sort) otherwise.  The bucket path's Gaussian-order
+    // instance scan is formed by its count pass from the preprocess block totals.
+    const bool bucket = T <= BK_MAX_TILES && tuning("bucket", 1);
+    pp.block_sums = bucket ? g.block_sums : nullptr;
     GSR_STAGE(ST_PREPROCESS, dbg, launch_preprocess(stream, pp));
     // The instance total only needs the per-Gaussian tile counts, so it is read back right after the
     // preprocess: the host waits on that copy while the GPU runs the depth sort and the ordered scan, and
@@ -315,14 +320,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     if (!hw || !rb_ev) return fail(GSR_ERR_HIP, "pinned host buffer / event allocation failed");
     GSR_HIP(hipMemcpyAsync(hw, g.counters, CNT_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
     GSR_HIP(hipEventRecord(rb_ev, stream));
-    // Bucket binning (gsr_bin.hip) whenever the tile counters fit one workgroup's LDS; the radix path
-    // (depth sort, depth-ordered expansion, stable tile sort) otherwise.
-    const bool bucket = T <= BK_MAX_TILES && tuning("bucket", 1);
-    if (bucket) {
-        GSR_STAGE(ST_SCAN, dbg,
-                  launch_exclusive_scan_lookback(stream, g.tiles, nullptr, (uint32_t)P, g.inst_start, g.scan_status,
-                                                 g.counters + CNT_SCAN_TICKET, g.counters + CNT_OVERFLOW));
-    } else {
+    if (!bucket) {
         GSR_STAGE(ST_DEPTH_SORT, dbg, launch_radix_sort(stream, g.sort, (uint32_t)P, 32, false, g.depth_key));
         if (tuning("scan_lookback", 1))
             GSR_STAGE(ST_SCAN, dbg,
@@ -358,20 +356,23 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             BucketParams bp;
             bp.P = (uint32_t)P; bp.T = T; bp.gx = gx; bp.nbig = nbig;
             bp.nb = std::max(1u, std::min({(uint32_t)tuning("bk_blocks", 256), BK_MAX_BLOCKS, div_up(P, 1024)}));
-            bp.gper = div_up(div_up(P, bp.nb), 64) * 64;
+            bp.gper = div_up(div_up(P, bp.nb), 256) * 256;  // whole preprocess blocks
             bp.nb = div_up(P, bp.gper);
-            bp.tiles = g.tiles; bp.inst_start = g.inst_start; bp.depth_key = g.depth_key; bp.big_list = g.big_list;
+            bp.tiles = g.tiles; bp.inst_start = g.inst_start; bp.block_sums = g.block_sums; bp.depth_key = g.depth_key; bp.big_list = g.big_list;
             bp.exp_rec = g.exp_rec;
             bp.hist = b.bk_hist; bp.tile_cnt = b.bk_tile_cnt; bp.tile_start = b.bk_tile_start; bp.ranges = im.ranges;
-            bp.long_list = b.bk_long_list; bp.long_cnt = b.bk_long_cnt; bp.keys = b.bk_keys; bp.inst_gid = b.inst_gid;
+            bp.ticket = g.counters + CNT_COL_TICKET; bp.tile_status = g.tile_status; bp.err = g.counters + CNT_OVERFLOW;
+            bp.long_list = b.bk_long_list; bp.long_cnt = g.counters + CNT_LONG; bp.keys = b.bk_keys; bp.inst_gid = b.inst_gid; bp.inv = b.inv;
             GSR_STAGE(ST_BK_COUNT, dbg, launch_bucket_count(stream, bp));
             GSR_STAGE(ST_BK_SCATTER, dbg, launch_bucket_scatter(stream, bp));
             if (lpt) launch_tile_order(stream, im.ranges, nullptr, 0, (int)T, im.order_fwd);
             SegSortParams sp;
-            sp.T = T; sp.ranges = im.ranges; sp.tile_order = lpt ? im.order_fwd : nullptr; sp.keys = b.bk_keys; sp.keys2 = b.bk_keys2;
-            sp.sorted_u = b.sorted_u; sp.long_list = b.bk_long_list; sp.long_cnt = b.bk_long_cnt;
+            // the long tiles lead the LPT order only while SEG_CAP + 1 is a multiple of the bucket width
+            sp.T = T; sp.ranges = im.ranges;
+            sp.tile_order = (lpt && (((SEG_CAP + 1) >> tuning("lpt_shift", 3)) << tuning("lpt_shift", 3)) == SEG_CAP + 1)
+                                ? im.order_fwd : nullptr; sp.keys = b.bk_keys; sp.keys2 = b.bk_keys2;
+            sp.sorted_u = b.sorted_u; sp.long_list = b.bk_long_list; sp.long_cnt = g.counters + CNT_LONG;
             GSR_STAGE(ST_SEG_SORT, dbg, launch_seg_sort(stream, sp));
-            GSR_HIP(hipMemsetAsync(b.inv, 0xff, sizeof(uint32_t) * (size_t)R, stream));
         } else {
             GSR_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * T, stream));
             if (lpt) launch_tile_order(stream, im.ranges, nullptr, 0, (int)T, im.order_fwd);

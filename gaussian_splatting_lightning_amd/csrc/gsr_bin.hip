@@ -6,7 +6,7 @@
 //   1. bk_count    each block walks a contiguous Gaussian range (plus a share of the big Gaussians) and
 //                  histograms its instances per tile in LDS: one row of the (blocks x tiles) count matrix;
 //   2. bk_columns  exclusive prefix of every tile column over the blocks, and the tile totals;
-//   3. bk_tscan    exclusive scan of the tile totals -> tile ranges (one workgroup);
+//   3.             step 2 also scans the tile totals (decoupled look-back) -> tile ranges;
 //   4. bk_scatter  the same walk again: each instance takes the next free slot of its tile's bucket
 //                  (LDS counters seeded from the prefixes) and stores key = depth bits << 32 | u, where u is
 //                  its Gaussian-major expansion index (u increases with the Gaussian index);
@@ -16,7 +16,7 @@
 //                  and the result is exactly the reference's (tile, depth, index) order.  Tiles above
 //                  SEG_CAP instances are sorted by a whole workgroup (seg_block: four waves' registers, the
 //                  cross-wave stages through LDS); tiles above SEG_BLOCK_CAP in SEG_BLOCK_CAP-key chunks that
-//                  seg_merge places by merge ranks (binary search of every key in the other chunks).
+//                  seg_huge sorts (in LDS up to 8192 keys, else in chunks placed by merge ranks) (binary search of every key in the other chunks).
 // Everything is integer work; nothing depends on scheduling, so the result is deterministic.
 #include <algorithm>
 
@@ -58,6 +58,49 @@ __device__ __forceinline__ uint32_t rect_tile(uint32_t c, uint32_t rx, uint32_t 
     return (ry + cy) * gx + rx + (c - cy * w);
 }
 
+// Gaussian-order exclusive scan of the kept-tile counts over [g_lo, g_hi) (the instances' Gaussian-major
+// expansion offsets u): the preprocess block totals before g_lo (a multiple of 256) give the base, then a
+// workgroup scan of the range, 4 Gaussians per thread per round.  The workgroup holding the last Gaussian
+// also writes the total.  s_tmp: >= BKW + 1 words of scratch LDS.
+template <int BKW>
+__device__ void bk_instance_offsets(const BucketParams &p, uint32_t g_lo, uint32_t g_hi, uint32_t *s_tmp) {
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    uint32_t acc = 0;
+    for (uint32_t k = tid; k < g_lo / 256; k += 64 * BKW) acc += p.block_sums[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += (uint32_t)__shfl_xor((int)acc, o);
+    if (lane == 0) s_tmp[w] = acc;
+    __syncthreads();
+    uint32_t base = 0;
+    for (int k = 0; k < BKW; k++) base += s_tmp[k];
+    __syncthreads();
+    for (uint32_t r0 = g_lo; r0 < g_hi; r0 += 4 * 64 * BKW) {
+        const uint32_t g = r0 + 4 * (uint32_t)tid;
+        uint32_t v[4], loc = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            v[k] = g + k < g_hi ? p.tiles[g + k] : 0u;
+            loc += v[k];
+        }
+        const uint32_t inc = wave_inclusive_scan(loc, lane);
+        if (lane == 63) s_tmp[w] = inc;
+        __syncthreads();
+        uint32_t run = base + inc - loc, all = 0;
+        for (int k = 0; k < BKW; k++) {
+            if (k < w) run += s_tmp[k];
+            all += s_tmp[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (g + k < g_hi) p.inst_start[g + k] = run;
+            run += v[k];
+        }
+        base += all;
+        __syncthreads();
+    }
+    if (g_hi == p.P && tid == 0) p.inst_start[p.P] = base;
+}
+
 template <bool SCATTER, int BKW>  // BKW: waves per workgroup
 __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
     extern __shared__ uint32_t s_tab[];   // T entries: tile counts (count) / next free bucket slot (scatter)
@@ -73,8 +116,9 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
         for (uint32_t t = tid; t < T; t += 64 * BKW) s_tab[t] = 0u;
     }
     s_own[w][lane] = -1;
-    __syncthreads();
     const uint32_t g_lo = b * p.gper, g_hi = min(p.P, g_lo + p.gper);
+    if (!SCATTER) bk_instance_offsets<BKW>(p, g_lo, g_hi, reinterpret_cast<uint32_t *>(&s_aux[0][0]));
+    __syncthreads();
     uint32_t g = g_lo + (uint32_t)w * 64 + lane;
     uint32_t n_kept = 0, n_u = 0, n_dep = 0;
     uint4 n_e = make_uint4(0, 0, 0, 0);
@@ -131,6 +175,7 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
                         const uint32_t slot = atomicAdd(&s_tab[tile], 1u);
                         p.keys[slot] = ((unsigned long long)x.z << 32) | ui;
                         p.inst_gid[ui] = g0 + (uint32_t)o;
+                        p.inv[ui] = INV_NONE;
                     }
                 }
             }
@@ -152,6 +197,7 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
                 const uint32_t slot = atomicAdd(&s_tab[tile], 1u);
                 p.keys[slot] = dk | (u0 + c);
                 p.inst_gid[u0 + c] = gb;
+                p.inv[u0 + c] = INV_NONE;
             }
         }
     }
@@ -163,14 +209,23 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// step 2: column prefixes of the count matrix.  A workgroup owns 64 tile columns (one per lane); its four
-// waves own four contiguous quarters of the block rows.
+// steps 2 and 3: column prefixes of the count matrix, tile totals, and the tile starts / ranges from a
+// decoupled look-back over the workgroups in tile order.  A workgroup owns 64 tile columns (one per lane); its
+// four waves own four contiguous quarters of the block rows.  Workgroup ids come from an atomic ticket, so a
+// workgroup only waits on workgroups that started before it.  The long tiles are appended to two lists for
+// the workgroup sorts: list 0 holds tiles of (SEG_CAP, SEG_BLOCK_CAP] instances, list 1 longer ones.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void bk_columns_kernel(uint32_t *__restrict__ hist, uint32_t nb, uint32_t T,
-                                                         uint32_t *__restrict__ tile_cnt) {
+__global__ __launch_bounds__(256) void bk_columns_kernel(BucketParams p) {
     __shared__ uint32_t s_sum[4][64];
+    __shared__ uint32_t s_bid;
+    __shared__ unsigned long long s_excl;
+    uint32_t *__restrict__ hist = p.hist;
+    const uint32_t nb = p.nb, T = p.T;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const uint32_t t = blockIdx.x * 64 + lane;
+    if (tid == 0) s_bid = atomicAdd(p.ticket, 1u);
+    __syncthreads();
+    const uint32_t bid = s_bid;
+    const uint32_t t = bid * 64 + lane;
     const uint32_t q = (nb + 3) / 4, r0 = min(nb, w * q), r1 = min(nb, r0 + q);
     uint32_t sum = 0;
     if (t < T) {
@@ -186,6 +241,31 @@ __global__ __launch_bounds__(256) void bk_columns_kernel(uint32_t *__restrict__ 
     }
     s_sum[w][lane] = sum;
     __syncthreads();
+    const uint32_t tot = s_sum[0][lane] + s_sum[1][lane] + s_sum[2][lane] + s_sum[3][lane];  // tile total
+    if (w == 0) {
+        const uint32_t inc = wave_inclusive_scan(tot, lane);
+        const uint64_t excl = wave_lookback(p.tile_status, bid, (uint64_t)__builtin_amdgcn_readlane((int)inc, 63),
+                                            lane, p.err);
+        if (t < T) {
+            const uint32_t st = (uint32_t)(excl + inc - tot);
+            p.tile_start[t] = st;
+            p.ranges[t] = tot ? make_uint2(st, st + tot) : make_uint2(0, 0);  // empty: (0, 0), as the reference
+            p.tile_cnt[t] = tot;
+            if (t == T - 1) p.tile_start[T] = st + tot;
+        }
+        const bool l0 = t < T && tot > SEG_CAP && tot <= SEG_BLOCK_CAP, l1 = t < T && tot > SEG_BLOCK_CAP;
+        const uint64_t m0 = __ballot(l0), m1 = __ballot(l1);
+        uint32_t b0 = 0, b1 = 0;
+        if (lane == 0) {
+            if (m0) b0 = atomicAdd(&p.long_cnt[0], (uint32_t)__popcll(m0));
+            if (m1) b1 = atomicAdd(&p.long_cnt[1], (uint32_t)__popcll(m1));
+        }
+        b0 = __builtin_amdgcn_readfirstlane(b0);
+        b1 = __builtin_amdgcn_readfirstlane(b1);
+        const uint64_t lt = lanemask_lt(lane);
+        if (l0) p.long_list[b0 + __popcll(m0 & lt)] = t;
+        if (l1) p.long_list[(T + 1) + b1 + __popcll(m1 & lt)] = t;
+    }
     uint32_t run = 0;
     for (int i = 0; i < w; i++) run += s_sum[i][lane];
     if (t < T) {
@@ -205,49 +285,7 @@ __global__ __launch_bounds__(256) void bk_columns_kernel(uint32_t *__restrict__ 
             hist[(size_t)r * T + t] = run;
             run += v;
         }
-        if (w == 3) tile_cnt[t] = run;
     }
-}
-
-// ------------------------------------------------------------------------------------------------
-// step 3: tile starts and ranges (one workgroup, T <= BK_MAX_TILES), and the lists of the long tiles that the
-// per-wave sort leaves to seg_block: list 0 holds tiles of (SEG_CAP, SEG_BLOCK_CAP] instances, list 1 longer ones.
-// ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void bk_tscan_kernel(const uint32_t *__restrict__ tile_cnt, uint32_t T,
-                                                        uint32_t *__restrict__ tile_start, uint2 *__restrict__ ranges,
-                                                        uint32_t *__restrict__ long_list, uint32_t *__restrict__ long_cnt) {
-    __shared__ uint32_t s_w[16], s_n[2];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (tid < 2) s_n[tid] = 0u;
-    // wave w scans tiles [w * span, (w + 1) * span), 64 at a time (coalesced)
-    const uint32_t span = (T + 16 * 64 - 1) / (16 * 64) * 64;
-    const uint32_t t0 = (uint32_t)w * span, t1 = min(T, t0 + span);
-    uint32_t sum = 0;
-    for (uint32_t t = t0 + lane; t < t1; t += 64) sum += tile_cnt[t];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) sum += (uint32_t)__shfl_xor((int)sum, o);
-    if (lane == 0) s_w[w] = sum;
-    __syncthreads();
-    uint32_t run = 0;
-    for (int i = 0; i < w; i++) run += s_w[i];
-    for (uint32_t tb = t0; tb < t1; tb += 64) {
-        const uint32_t t = tb + lane;
-        const uint32_t v = t < t1 ? tile_cnt[t] : 0u;
-        const uint32_t inc = wave_inclusive_scan(v, lane);
-        if (t < t1) {
-            const uint32_t st = run + inc - v;
-            tile_start[t] = st;
-            ranges[t] = v ? make_uint2(st, st + v) : make_uint2(0, 0);  // empty: (0, 0), as the reference
-            if (v > SEG_CAP) {
-                const int which = v > SEG_BLOCK_CAP;
-                long_list[which * (T + 1) + atomicAdd(&s_n[which], 1u)] = t;
-            }
-        }
-        run += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-    }
-    if (w == 15 && lane == 0) tile_start[T] = run;
-    __syncthreads();
-    if (tid < 2) long_cnt[tid] = s_n[tid];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -355,102 +393,104 @@ __global__ __launch_bounds__(256) void seg_sort_kernel(SegSortParams p) {
     else seg_sort_wave<8>(p.keys, rg.x, n, p.sorted_u, lane);
 }
 
-// Workgroup sort of up to SEG_BLOCK_CAP keys: wave w sorts keys [512 w, 512 w + 512) in registers (as
+// Workgroup sort of up to 16 x 512 keys in LDS: the waves sort 512-key chunks in registers (as
 // seg_sort_wave<8>) into LDS, padded with all-ones keys; then every key's position is its index in its chunk
 // plus its rank in each other chunk (branchless binary searches, 8 keys per thread interleaved).
 constexpr uint32_t SB_CHUNK = 512;
-__device__ __forceinline__ void seg_block_sort(const unsigned long long *__restrict__ keys, uint32_t start,
-                                               uint32_t n, uint32_t *__restrict__ sorted_u,
-                                               unsigned long long *__restrict__ keys_out,
-                                               unsigned long long *__restrict__ s_x, int w, int lane) {
+__device__ __forceinline__ void seg_lds_sort(const unsigned long long *__restrict__ keys, uint32_t start, uint32_t n,
+                                             uint32_t *__restrict__ sorted_u, unsigned long long *__restrict__ keys_out,
+                                             unsigned long long *__restrict__ s_x, int w, int lane) {
     const uint32_t nch = (n + SB_CHUNK - 1) / SB_CHUNK;
-    if ((uint32_t)w < nch) {
-        const uint32_t c0 = (uint32_t)w * SB_CHUNK;
+    for (uint32_t c = (uint32_t)w; c < nch; c += 4) {
+        const uint32_t c0 = c * SB_CHUNK;
         seg_sort_wave_to_lds<8>(keys, start + c0, min(SB_CHUNK, n - c0), s_x + c0, lane);
     }
     __syncthreads();
-    constexpr int PER = SEG_BLOCK_CAP / 256;
-    unsigned long long key[PER];
-    uint32_t pos[PER];
+    constexpr int PER = 8;
+    for (uint32_t e0 = 0; e0 < n; e0 += 256 * PER) {
+        unsigned long long key[PER];
+        uint32_t pos[PER];
 #pragma unroll
-    for (int i = 0; i < PER; i++) {
-        const uint32_t e = threadIdx.x + 256u * i;
-        key[i] = e < n ? s_x[e] : ~0ull;
-        pos[i] = e & (SB_CHUNK - 1);
-    }
-    for (uint32_t c2 = 0; c2 < nch; c2++) {
-        const unsigned long long *ch = s_x + c2 * SB_CHUNK;
-        uint32_t idx[PER];
+        for (int i = 0; i < PER; i++) {
+            const uint32_t e = e0 + threadIdx.x + 256u * i;
+            key[i] = e < n ? s_x[e] : ~0ull;
+            pos[i] = e & (SB_CHUNK - 1);
+        }
+        for (uint32_t c2 = 0; c2 < nch; c2++) {
+            const unsigned long long *ch = s_x + c2 * SB_CHUNK;
+            uint32_t idx[PER];
 #pragma unroll
-        for (int i = 0; i < PER; i++) idx[i] = 0;
+            for (int i = 0; i < PER; i++) idx[i] = 0;
 #pragma unroll
-        for (uint32_t step = SB_CHUNK / 2; step; step >>= 1) {
+            for (uint32_t step = SB_CHUNK / 2; step; step >>= 1) {
 #pragma unroll
-            for (int i = 0; i < PER; i++)
-                if (ch[idx[i] + step - 1] < key[i]) idx[i] += step;
+                for (int i = 0; i < PER; i++)
+                    if (ch[idx[i] + step - 1] < key[i]) idx[i] += step;
+            }
+#pragma unroll
+            for (int i = 0; i < PER; i++) {
+                const uint32_t e = e0 + threadIdx.x + 256u * i;
+                // the last probe decides between idx and idx + 1 (lower bound over 512 entries)
+                const uint32_t lb = idx[i] + (ch[idx[i]] < key[i] ? 1u : 0u);
+                if (e / SB_CHUNK != c2) pos[i] += lb;
+            }
         }
 #pragma unroll
         for (int i = 0; i < PER; i++) {
-            const uint32_t e = threadIdx.x + 256u * i;
-            // the last probe decides between idx and idx + 1 (lower bound over 512 entries)
-            const uint32_t lb = idx[i] + (ch[idx[i]] < key[i] ? 1u : 0u);
-            if ((e >> 9) != c2) pos[i] += lb;
+            const uint32_t e = e0 + threadIdx.x + 256u * i;
+            if (e >= n) continue;
+            if (keys_out) keys_out[start + pos[i]] = key[i];
+            else sorted_u[start + pos[i]] = (uint32_t)key[i];
         }
-    }
-#pragma unroll
-    for (int i = 0; i < PER; i++) {
-        const uint32_t e = threadIdx.x + 256u * i;
-        if (e >= n) continue;
-        if (keys_out) keys_out[start + pos[i]] = key[i];
-        else sorted_u[start + pos[i]] = (uint32_t)key[i];
     }
     __syncthreads();  // s_x is reused by the next chunk / tile
 }
 
-// Long tiles, one workgroup each (the workgroups loop over the device-side lists, so every wave reaches the
-// exit): list 0 sorted whole, list 1 in SEG_BLOCK_CAP-key chunks for seg_merge (each chunk written back
-// sorted, into a second key buffer).
+// Tiles of (SEG_CAP, SEG_BLOCK_CAP] instances, one workgroup each; the workgroups loop over the tiles (their
+// count is only known on the device), so every wave reaches the exit.  With the LPT order the long tiles are
+// exactly its first long_cnt[0] + long_cnt[1] slots (SEG_CAP + 1 is a multiple of the LPT bucket width), taken
+// longest first; tiles above SEG_BLOCK_CAP among them are left to seg_huge.
 __global__ __launch_bounds__(256) void seg_block_kernel(SegSortParams p) {
     __shared__ unsigned long long s_x[SEG_BLOCK_CAP];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t n0 = p.long_cnt[0], n1 = p.long_cnt[1];
-    for (uint32_t i = blockIdx.x; i < n0 + n1; i += gridDim.x) {
-        const bool chunked = i >= n0;
-        const uint32_t tile = chunked ? p.long_list[p.T + 1 + (i - n0)] : p.long_list[i];
+    const uint32_t n0 = p.long_cnt[0], nl = p.tile_order ? n0 + p.long_cnt[1] : n0;
+    for (uint32_t i = blockIdx.x; i < nl; i += gridDim.x) {
+        const uint32_t tile = p.tile_order ? p.tile_order[i] : p.long_list[i];
         const uint2 rg = p.ranges[tile];
         const uint32_t n = rg.y - rg.x;
-        for (uint32_t c0 = 0; c0 < n; c0 += SEG_BLOCK_CAP)
-            seg_block_sort(p.keys, rg.x + c0, min(SEG_BLOCK_CAP, n - c0), p.sorted_u,
-                           chunked ? p.keys2 : nullptr, s_x, w, lane);
+        if (n <= SEG_CAP || n > SEG_BLOCK_CAP) continue;  // workgroup-uniform
+        seg_lds_sort(p.keys, rg.x, n, p.sorted_u, nullptr, s_x, w, lane);
     }
 }
 
-// Merge ranks of the chunk-sorted tiles of list 1: an element's sorted position is its index in its chunk plus
-// the number of smaller keys in every other chunk (keys are unique).  One workgroup per tile; the tile's keys
-// are staged in LDS when they fit, else searched in global memory.
-constexpr uint32_t MERGE_LDS_KEYS = 8192;
-__global__ __launch_bounds__(256) void seg_merge_kernel(SegSortParams p) {
-    constexpr uint32_t CAP = SEG_BLOCK_CAP;
-    __shared__ unsigned long long s_k[MERGE_LDS_KEYS];
+// Tiles above SEG_BLOCK_CAP instances (list 1), one workgroup each: sorted in LDS (dynamic, lds_keys keys)
+// when they fit, else in SEG_BLOCK_CAP-key chunks written to keys2 and placed by merge ranks searched in global
+// memory (the workgroup's own stores, ordered by a device-scope fence).
+__global__ __launch_bounds__(256) void seg_huge_kernel(SegSortParams p, uint32_t lds_keys) {
+    extern __shared__ unsigned long long s_k[];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t nh = p.long_cnt[1];
     for (uint32_t h = blockIdx.x; h < nh; h += gridDim.x) {
         const uint2 rg = p.ranges[p.long_list[p.T + 1 + h]];
         const uint32_t n = rg.y - rg.x;
-        const bool in_lds = n <= MERGE_LDS_KEYS;
-        __syncthreads();  // the previous tile's readers are done with s_k
-        if (in_lds)
-            for (uint32_t e = threadIdx.x; e < n; e += 256) s_k[e] = p.keys2[rg.x + e];
+        if (n <= lds_keys) {
+            seg_lds_sort(p.keys, rg.x, n, p.sorted_u, nullptr, s_k, w, lane);
+            continue;
+        }
+        for (uint32_t c0 = 0; c0 < n; c0 += SEG_BLOCK_CAP)
+            seg_lds_sort(p.keys, rg.x + c0, min(SEG_BLOCK_CAP, n - c0), nullptr, p.keys2, s_k, w, lane);
+        __threadfence();
         __syncthreads();
-        const unsigned long long *kk = in_lds ? s_k : p.keys2 + rg.x;
-        const uint32_t nch = (n + CAP - 1) / CAP;
+        const unsigned long long *kk = p.keys2 + rg.x;
+        const uint32_t nch = (n + SEG_BLOCK_CAP - 1) / SEG_BLOCK_CAP;
         for (uint32_t e = threadIdx.x; e < n; e += 256) {
             const unsigned long long key = kk[e];
-            const uint32_t c = e / CAP;
-            uint32_t pos = e - c * CAP;
+            const uint32_t c = e / SEG_BLOCK_CAP;
+            uint32_t pos = e - c * SEG_BLOCK_CAP;
             for (uint32_t c2 = 0; c2 < nch; c2++) {
                 if (c2 == c) continue;
-                const unsigned long long *ch = kk + c2 * CAP;
-                uint32_t lo = 0, hi = min(CAP, n - c2 * CAP);  // first index with ch[i] >= key
+                const unsigned long long *ch = kk + c2 * SEG_BLOCK_CAP;
+                uint32_t lo = 0, hi = min(SEG_BLOCK_CAP, n - c2 * SEG_BLOCK_CAP);  // first index with ch[i] >= key
                 while (lo < hi) {
                     const uint32_t mid = (lo + hi) >> 1;
                     if (ch[mid] < key) lo = mid + 1; else hi = mid;
@@ -459,6 +499,7 @@ __global__ __launch_bounds__(256) void seg_merge_kernel(SegSortParams p) {
             }
             p.sorted_u[rg.x + pos] = (uint32_t)key;
         }
+        __syncthreads();
     }
 }
 
@@ -484,17 +525,17 @@ static void launch_walk(hipStream_t s, const BucketParams &p) {
 
 void launch_bucket_count(hipStream_t s, const BucketParams &p) {
     launch_walk<false>(s, p);
-    bk_columns_kernel<<<div_up(p.T, 64), 256, 0, s>>>(p.hist, p.nb, p.T, p.tile_cnt);
-    bk_tscan_kernel<<<1, 1024, 0, s>>>(p.tile_cnt, p.T, p.tile_start, p.ranges, p.long_list, p.long_cnt);
+    bk_columns_kernel<<<div_up(p.T, 64), 256, 0, s>>>(p);
 }
 
 void launch_bucket_scatter(hipStream_t s, const BucketParams &p) { launch_walk<true>(s, p); }
 
 void launch_seg_sort(hipStream_t s, const SegSortParams &p) {
     if (p.T == 0) return;
-    seg_block_kernel<<<std::min(p.T, 1024u), 256, 0, s>>>(p);  // the longest tiles first
+    seg_block_kernel<<<std::min(p.T, 1280u), 256, 0, s>>>(p);  // the longest tiles first
     seg_sort_kernel<<<div_up(p.T, 4), 256, 0, s>>>(p);
-    seg_merge_kernel<<<256, 256, 0, s>>>(p);
+    constexpr uint32_t HUGE_LDS_KEYS = 8192;  // 64 KB
+    seg_huge_kernel<<<128, 256, HUGE_LDS_KEYS * sizeof(unsigned long long), s>>>(p, HUGE_LDS_KEYS);
 }
 
 }  // namespace gsr

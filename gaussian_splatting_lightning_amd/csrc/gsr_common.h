@@ -24,7 +24,7 @@ constexpr int GRAD_ROW = 12;                   // floats per instance gradient r
 // counters block at the head of the geometry buffer (zeroed every forward)
 // counters: [CNT_BIG] big-Gaussian count, [CNT_OVERFLOW] scan overflow flag, then CNT_NPART 64-bit partial
 // sums of the instance total (spread over addresses so the per-block atomics do not serialise)
-enum Counter : int { CNT_BIG = 0, CNT_OVERFLOW = 2, CNT_SCAN_TICKET = 3, CNT_PARTIALS = 16, CNT_NPART = 64,
+enum Counter : int { CNT_BIG = 0, CNT_OVERFLOW = 2, CNT_SCAN_TICKET = 3, CNT_COL_TICKET = 4, CNT_LONG = 6, CNT_PARTIALS = 16, CNT_NPART = 64,
                      CNT_WORDS = 16 + 2 * 64 };
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }
@@ -82,6 +82,13 @@ inline void carve_sort(Carver &c, SortScratch &s, uint32_t n, bool need_v0) {
     s.status = s.ctrl + RS_CTRL_WORDS;
 }
 
+// Bucket binning (gsr_bin.hip): used when the tile count fits the LDS histogram of one workgroup.
+constexpr uint32_t BK_MAX_TILES = 32768;  // 128 KB of LDS counters (4K images: 32400 tiles)
+constexpr uint32_t BK_MAX_BLOCKS = 512;   // rows of the count matrix (carved for the maximum)
+constexpr uint32_t SEG_CAP = 511;         // longest tile the per-wave register sort takes (8 keys per lane);
+                                          // SEG_CAP + 1 is a multiple of the LPT bucket width (seg_block)
+constexpr uint32_t SEG_BLOCK_CAP = 2048;  // longest tile one workgroup sorts (4 waves x 512 keys); longer: chunks
+
 struct GeomState {
     uint32_t *counters;    // CNT_WORDS
     float4 *rec_a;         // P
@@ -95,10 +102,12 @@ struct GeomState {
     uint32_t *inst_off;    // P+1: radix path: exclusive scan of tiles in depth order, [P] = total
     uint32_t *inst_start;  // P+1: first instance (expansion order) of each Gaussian (bucket path: the
                            //      exclusive scan of tiles in Gaussian order, [P] = total)
+    uint32_t *block_sums;  // div_up(P, 256): kept-tile totals of the preprocess blocks (bucket path)
     uint32_t *big_list;    // P: Gaussians with > BIG_GAUSSIAN_TILES tiles
     uint32_t *big_slot;    // P: index of a big Gaussian in big_list (valid only for big ones)
     uint32_t *scan_tmp;    // block sums for the instance scan (multi-kernel path)
     uint64_t *scan_status; // look-back words of the single-kernel instance scan
+    uint64_t *tile_status; // look-back words of the bucket path's tile scan
     SortScratch sort;      // depth sort (P keys); final order lands in sort.v[0]
     const uint32_t *order; // = sort.v[0] after the (even-pass) depth sort
 };
@@ -108,6 +117,7 @@ inline size_t carve_geom(char *base, int P, GeomState &g) {
     uint32_t n = (uint32_t)P;
     g.counters = c.take<uint32_t>(CNT_WORDS);
     g.scan_status = c.take<uint64_t>(div_up(n + 1, SCAN_TILE) + 1);  // cleared together with the counters
+    g.tile_status = c.take<uint64_t>(BK_MAX_TILES / 64 + 1);         // cleared together with the counters
     g.rec_a = c.take<float4>(n);
     g.rec_b = c.take<float4>(n);
     g.rec_c = c.take<float2>(n);
@@ -117,6 +127,7 @@ inline size_t carve_geom(char *base, int P, GeomState &g) {
     g.inst_off = c.take<uint32_t>((size_t)n + 1);
     g.inst_start = c.take<uint32_t>((size_t)n + 1);
     g.depth_key = c.take<uint32_t>(n);
+    g.block_sums = c.take<uint32_t>(div_up(n, 256) + 1);
     g.big_list = c.take<uint32_t>(n);
     g.big_slot = c.take<uint32_t>(n);
     g.scan_tmp = c.take<uint32_t>(div_up(n + 1, SCAN_TILE) + 1);
@@ -132,12 +143,6 @@ inline int tile_key_bits(uint32_t num_tiles) {
 }
 inline int radix_passes(int bits) { return (bits + 7) / 8; }
 
-// Bucket binning (gsr_bin.hip): used when the tile count fits the LDS histogram of one workgroup.
-constexpr uint32_t BK_MAX_TILES = 32768;  // 128 KB of LDS counters (4K images: 32400 tiles)
-constexpr uint32_t BK_MAX_BLOCKS = 512;   // rows of the count matrix (carved for the maximum)
-constexpr uint32_t SEG_CAP = 512;         // longest tile the per-wave register sort takes (8 keys per lane)
-constexpr uint32_t SEG_BLOCK_CAP = 2048;  // longest tile one workgroup sorts (4 waves x 512 keys); longer: chunks
-
 struct BinningState {
     uint32_t *inst_gid;    // R: Gaussian of each instance (expansion order)
     uint32_t *point_list;  // R: Gaussian ids sorted by (tile, depth, id); written by the forward composite
@@ -150,7 +155,7 @@ struct BinningState {
     unsigned long long *bk_keys;  // bucket path: R keys (depth << 32 | u) bucketed by tile
     unsigned long long *bk_keys2; // bucket path: R, chunk-sorted keys of tiles longer than SEG_BLOCK_CAP
     uint32_t *bk_hist;     // bucket path: BK_MAX_BLOCKS x T count matrix
-    uint32_t *bk_tile_cnt, *bk_tile_start, *bk_long_list, *bk_long_cnt;
+    uint32_t *bk_tile_cnt, *bk_tile_start, *bk_long_list;
 };
 constexpr uint32_t INV_NONE = 0xffffffffu;
 
@@ -174,7 +179,6 @@ inline size_t carve_binning(char *base, int64_t R, uint32_t num_tiles, BinningSt
     b.bk_tile_cnt = cb.take<uint32_t>((size_t)num_tiles + 1);
     b.bk_tile_start = cb.take<uint32_t>((size_t)num_tiles + 1);
     b.bk_long_list = cb.take<uint32_t>(2 * ((size_t)num_tiles + 1));
-    b.bk_long_cnt = cb.take<uint32_t>(2);
     c.off = cr.off > cb.off ? cr.off : cb.off;
     return c.off + 256;
 }
@@ -490,6 +494,47 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v, int lane) {
 }
 
 __device__ __forceinline__ uint64_t lanemask_lt(int lane) { return (lane == 0) ? 0ull : (~0ull >> (64 - lane)); }
+
+// Decoupled look-back by one whole wave: publishes the block's aggregate, then sums predecessors' words 64 at a
+// time (nearest first) up to the first inclusive prefix, and publishes its own inclusive prefix.  Returns the
+// block's exclusive prefix (every lane).  Status words: 2-bit flag | 62-bit value, zero = not yet published.
+// Block ids must follow start order (atomic ticket).  A chain that never completes sets bit 1 of *err.
+constexpr uint64_t SLB_AGG = 1ull << 62, SLB_INC = 2ull << 62, SLB_MASK = (1ull << 62) - 1;
+__device__ __forceinline__ uint64_t wave_lookback(uint64_t *status, uint32_t bid, uint64_t agg, int lane,
+                                                  uint32_t *err) {
+    if (lane == 0)
+        __hip_atomic_store(status + bid, (bid == 0 ? SLB_INC : SLB_AGG) | agg, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t excl = 0;
+    int64_t look = (int64_t)bid - 1;
+    uint32_t spins = 0;
+    while (look >= 0) {
+        const int64_t q = look - lane;
+        const uint64_t sv =
+            q >= 0 ? __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : SLB_INC;
+        const uint64_t flag = sv & ~SLB_MASK;
+        const uint64_t inc_mask = __ballot(flag == SLB_INC);
+        const int first = inc_mask ? __builtin_ctzll(inc_mask) : 64;
+        const uint64_t upto = first < 63 ? ((2ull << first) - 1) : ~0ull;
+        if (__ballot(flag == 0) & upto) {  // a predecessor in the window has not published yet
+            if (++spins > (1u << 24)) {
+                if (lane == 0) atomicOr(err, 2u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        uint64_t part = (lane <= first) ? (sv & SLB_MASK) : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+        excl += part;
+        if (first < 64) break;
+        look -= 64;
+    }
+    if (lane == 0 && bid > 0)
+        __hip_atomic_store(status + bid, SLB_INC | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
 
 // Orders LDS writes before later LDS reads of other lanes of the SAME wave (no s_barrier).
 // LPT launch order puts the heaviest tiles in the first slots; with prio_div > 0 their waves also win VALU

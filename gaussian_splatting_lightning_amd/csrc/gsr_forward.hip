@@ -106,12 +106,16 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
 // Exact tile culling is balanced across the wave: the (Gaussian, tile) pairs of all 64 lanes' rects are
 // enumerated jointly (prefix sum of the rect areas, each lane takes every 64th pair, owner found by binary
 // search), so a wave costs ceil(sum of areas / 64) tile tests instead of its largest rect.
+//
+// With p.block_sums (bucket binning) every block also stores its kept-tile total, from which the bucket count
+// pass forms the Gaussian-order instance offsets.
 __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessParams p) {
     __shared__ CullGauss s_cg[4][64];
     __shared__ int4 s_rect[4][64];        // rx, ry, rw, start of the lane's pairs
     __shared__ unsigned long long s_mask[4][64];
     __shared__ uint32_t s_w[4];
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t bid = blockIdx.x;
+    const int i = (int)bid * 256 + threadIdx.x;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     CullIn ci;
     ci.need = false;
@@ -160,8 +164,8 @@ __global__ __launch_bounds__(256) void preprocess_kernel(PreprocessParams p) {
     if (threadIdx.x == 0) {
         const unsigned long long tot = (unsigned long long)s_w[0] + s_w[1] + s_w[2] + s_w[3];
         if (tot)
-            atomicAdd(reinterpret_cast<unsigned long long *>(p.g.counters + CNT_PARTIALS) + (blockIdx.x % CNT_NPART),
-                      tot);
+            atomicAdd(reinterpret_cast<unsigned long long *>(p.g.counters + CNT_PARTIALS) + (bid % CNT_NPART), tot);
+        if (p.block_sums) p.block_sums[bid] = (uint32_t)tot;  // <= 256 * 2^16 tiles
     }
 }
 

@@ -41,6 +41,7 @@ struct PreprocessParams {
     const float *view, *proj, *campos;
     int *radii;
     GeomState g;
+    uint32_t *block_sums;  // optional: kept-tile total of every 256-Gaussian block
 };
 void launch_preprocess(hipStream_t s, const PreprocessParams &p);
 
@@ -59,16 +60,22 @@ void launch_identify_ranges(hipStream_t s, const uint32_t *keys_sorted, uint32_t
 struct BucketParams {
     uint32_t P, T, nb, gper, nbig;  // Gaussians, tiles, walk blocks, Gaussians per block, big Gaussians
     int gx;
-    const uint32_t *tiles, *inst_start, *depth_key, *big_list;
+    const uint32_t *tiles, *depth_key, *big_list;
+    const uint32_t *block_sums;  // preprocess block totals (256 Gaussians each)
+    uint32_t *inst_start;  // P + 1: written by the count pass (Gaussian-order exclusive scan of tiles)
     const uint4 *exp_rec;
     uint32_t *hist;        // nb x T counts, then column prefixes
     uint32_t *tile_cnt;    // T
     uint32_t *tile_start;  // T + 1
     uint2 *ranges;         // T
     uint32_t *long_list;   // 2 x (T + 1): tiles of (SEG_CAP, SEG_BLOCK_CAP] instances, longer tiles
-    uint32_t *long_cnt;    // 2 counts (written by the tile scan)
+    uint32_t *long_cnt;    // 2 counts (zeroed)
+    uint32_t *ticket;      // zeroed: column-pass workgroup ticket
+    uint64_t *tile_status; // zeroed: div_up(T, 64) look-back words of the column pass
+    uint32_t *err;         // look-back failure flag
     unsigned long long *keys;  // R: depth << 32 | u, bucketed by tile
     uint32_t *inst_gid;    // R
+    uint32_t *inv;         // R: reset to INV_NONE by the scatter (the forward composite fills it)
 };
 void launch_bucket_count(hipStream_t s, const BucketParams &p);    // walk + column prefixes + tile ranges
 void launch_bucket_scatter(hipStream_t s, const BucketParams &p);

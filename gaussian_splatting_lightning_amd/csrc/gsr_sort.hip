@@ -130,7 +130,6 @@ void launch_exclusive_scan(hipStream_t s, const uint32_t *in, const uint32_t *id
 // Single-kernel exclusive scan with decoupled look-back (one launch instead of three).  Block ids come from an
 // atomic ticket so a block only waits on blocks that started before it; its first wave inspects 64
 // predecessors per round trip.  Status words: 2-bit flag | 62-bit inclusive/aggregate sum.
-constexpr uint64_t SLB_AGG = 1ull << 62, SLB_INC = 2ull << 62, SLB_MASK = (1ull << 62) - 1;
 
 template <bool GATHER>
 __global__ __launch_bounds__(256) void scan_lookback_kernel(const uint32_t *__restrict__ in,

@@ -49,10 +49,12 @@ def compare_forward(inp, hip, oracle_out):
     assert np.sum(hs["inv"] != 0xFFFFFFFF) == loaded.sum()
     assert abs(hs["num_rendered"] - run.num_rendered) <= 1e-4 * run.num_rendered + 2
     ft, nc = run.image_state()
-    assert np.mean(hs["n_contrib"] == nc) >= 0.999
-    assert close_fraction(hip["color"], color, 1e-5) >= 0.999
+    # threshold flips: at most 0.1 % of the pixels (and at least 3 allowed, for tiny images)
+    flips = max(3, int(1e-3 * W * H))
+    assert np.sum(hs["n_contrib"] != nc) <= flips
+    assert np.sum(np.any(np.abs(hip["color"] - color) > 1e-5, axis=0)) <= flips
     assert np.abs(hip["color"] - color).max() <= 2e-2
-    assert close_fraction(hip["invdepth"], invd, 1e-5, 1e-5) >= 0.999
+    assert np.sum(np.abs(hip["invdepth"] - invd) > 1e-5 + 1e-5 * np.abs(invd)) <= flips
     return run
 
 
@@ -389,19 +391,23 @@ def test_composite_variants_are_bitwise_identical(gpu_device, knobs):
             assert np.array_equal(ref["grads"][k], alt["grads"][k]), k
 
 
-def test_long_tiles_and_depth_ties(gpu_device):
-    """Bucket binning on tiles beyond one wave's register sort (> 512, > 1024 and > 2048 instances: seg_long and the
-    chunked merge) and on exact depth ties (duplicated Gaussians: the (tile, depth, index) order falls back to
-    the Gaussian index, as the reference's stable radix sort does)."""
-    inp = scene_inputs(60_000, 96, 64, sh_degree=1, seed=23)
+@pytest.mark.parametrize("n,W,H", [(60_000, 96, 64), (50_000, 32, 32)])
+def test_long_tiles_and_depth_ties(gpu_device, n, W, H):
+    """Bucket binning on tiles beyond one wave's register sort (> 511 instances: seg_block; > 2048: seg_huge in
+    LDS; > 8192: seg_huge's chunks placed by merge ranks) and on exact depth ties (duplicated Gaussians: the
+    (tile, depth, index) order falls back to the Gaussian index, as the reference's stable radix sort does)."""
+    inp = scene_inputs(n, W, H, sh_degree=1, seed=23)
     for k in ("means3D", "scales", "rotations", "opacities", "shs"):
         inp[k][1000:1200] = inp[k][1000]
         inp[k][5000:5300] = inp[k][5001]
-    dc, di = upstream(96, 64, 23)
+    dc, di = upstream(W, H, 23)
     hip = run_hip(inp, gpu_device, dc, di)
     run = compare_forward(inp, hip, run_oracle(inp))
     n_tile = np.diff(hip_state_arrays(hip)["ranges"], axis=1)[:, 0]
-    assert n_tile.max() > 2048 and np.any((n_tile > 1024) & (n_tile <= 2048))
+    if W > 32:
+        assert n_tile.max() > 2048 and np.any((n_tile > 511) & (n_tile <= 2048))
+    else:
+        assert n_tile.max() > 8192
     compare_backward(hip, run, dc, di, 1e-3)
 
 
