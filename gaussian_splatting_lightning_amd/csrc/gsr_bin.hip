@@ -377,22 +377,6 @@ __device__ __forceinline__ void seg_sort_wave_to_lds(const unsigned long long *k
     seg_sort_wave_impl<E>(keys, start, n, nullptr, lds_out, lane);
 }
 
-// One wave per tile of at most SEG_CAP instances (longer ones are in the long lists).  Launch slots follow
-// the LPT order, so the longest tiles start first.
-__global__ __launch_bounds__(256) void seg_sort_kernel(SegSortParams p) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t slot = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (slot >= p.T) return;
-    const uint32_t tile = p.tile_order ? p.tile_order[slot] : slot;
-    const uint2 rg = p.ranges[tile];
-    const uint32_t n = rg.y - rg.x;
-    if (n == 0 || n > SEG_CAP) return;
-    if (n <= 64u) seg_sort_wave<1>(p.keys, rg.x, n, p.sorted_u, lane);
-    else if (n <= 128u) seg_sort_wave<2>(p.keys, rg.x, n, p.sorted_u, lane);
-    else if (n <= 256u) seg_sort_wave<4>(p.keys, rg.x, n, p.sorted_u, lane);
-    else seg_sort_wave<8>(p.keys, rg.x, n, p.sorted_u, lane);
-}
-
 // Workgroup sort of up to 16 x 512 keys in LDS: the waves sort 512-key chunks in registers (as
 // seg_sort_wave<8>) into LDS, padded with all-ones keys; then every key's position is its index in its chunk
 // plus its rank in each other chunk (branchless binary searches, 8 keys per thread interleaved).
@@ -446,20 +430,36 @@ __device__ __forceinline__ void seg_lds_sort(const unsigned long long *__restric
     __syncthreads();  // s_x is reused by the next chunk / tile
 }
 
-// Tiles of (SEG_CAP, SEG_BLOCK_CAP] instances, one workgroup each; the workgroups loop over the tiles (their
-// count is only known on the device), so every wave reaches the exit.  With the LPT order the long tiles are
-// exactly its first long_cnt[0] + long_cnt[1] slots (SEG_CAP + 1 is a multiple of the LPT bucket width), taken
-// longest first; tiles above SEG_BLOCK_CAP among them are left to seg_huge.
-__global__ __launch_bounds__(256) void seg_block_kernel(SegSortParams p) {
+// Every tile up to SEG_BLOCK_CAP instances, in one persistent launch (the workgroups loop over the tiles, whose
+// counts are only known on the device, so every wave reaches the exit):
+//   1. tiles of (SEG_CAP, SEG_BLOCK_CAP] instances, one workgroup each (seg_lds_sort).  With the LPT order
+//      they are exactly its first long_cnt[0] + long_cnt[1] slots (SEG_CAP + 1 is a multiple of the LPT
+//      bucket width), taken longest first; tiles above SEG_BLOCK_CAP among them are left to seg_huge;
+//   2. then the short tiles, one wave each (seg_sort_wave), again longest first.
+__global__ __launch_bounds__(256) void seg_sort_kernel(SegSortParams p) {
     __shared__ unsigned long long s_x[SEG_BLOCK_CAP];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t n0 = p.long_cnt[0], nl = p.tile_order ? n0 + p.long_cnt[1] : n0;
+    const uint32_t n0 = p.long_cnt[0], nlong = n0 + p.long_cnt[1];
+    const uint32_t nl = p.tile_order ? nlong : n0;
     for (uint32_t i = blockIdx.x; i < nl; i += gridDim.x) {
         const uint32_t tile = p.tile_order ? p.tile_order[i] : p.long_list[i];
         const uint2 rg = p.ranges[tile];
         const uint32_t n = rg.y - rg.x;
         if (n <= SEG_CAP || n > SEG_BLOCK_CAP) continue;  // workgroup-uniform
         seg_lds_sort(p.keys, rg.x, n, p.sorted_u, nullptr, s_x, w, lane);
+    }
+    const uint32_t s0 = p.tile_order ? nlong : 0u;
+    // waves in the order workgroups finished phase 1 would be better balanced, but a shared work counter
+    // serialises ~10^4 device-scope atomics (measured 2x slower): a static round robin instead
+    for (uint32_t j = s0 + blockIdx.x * 4 + (uint32_t)w; j < p.T; j += gridDim.x * 4) {
+        const uint32_t tile = p.tile_order ? p.tile_order[j] : j;
+        const uint2 rg = p.ranges[tile];
+        const uint32_t n = rg.y - rg.x;
+        if (n == 0 || n > SEG_CAP) continue;  // wave-uniform
+        if (n <= 64u) seg_sort_wave<1>(p.keys, rg.x, n, p.sorted_u, lane);
+        else if (n <= 128u) seg_sort_wave<2>(p.keys, rg.x, n, p.sorted_u, lane);
+        else if (n <= 256u) seg_sort_wave<4>(p.keys, rg.x, n, p.sorted_u, lane);
+        else seg_sort_wave<8>(p.keys, rg.x, n, p.sorted_u, lane);
     }
 }
 
@@ -532,8 +532,7 @@ void launch_bucket_scatter(hipStream_t s, const BucketParams &p) { launch_walk<t
 
 void launch_seg_sort(hipStream_t s, const SegSortParams &p) {
     if (p.T == 0) return;
-    seg_block_kernel<<<std::min(p.T, 1280u), 256, 0, s>>>(p);  // the longest tiles first
-    seg_sort_kernel<<<div_up(p.T, 4), 256, 0, s>>>(p);
+    seg_sort_kernel<<<std::min(div_up(p.T, 4), (uint32_t)tuning("seg_grid", 1536)), 256, 0, s>>>(p);
     constexpr uint32_t HUGE_LDS_KEYS = 8192;  // 64 KB
     seg_huge_kernel<<<128, 256, HUGE_LDS_KEYS * sizeof(unsigned long long), s>>>(p, HUGE_LDS_KEYS);
 }
