@@ -361,6 +361,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             bp.tiles = g.tiles; bp.inst_start = g.inst_start; bp.block_sums = g.block_sums; bp.depth_key = g.depth_key; bp.big_list = g.big_list;
             bp.exp_rec = g.exp_rec;
             bp.hist = b.bk_hist; bp.tile_cnt = b.bk_tile_cnt; bp.tile_start = b.bk_tile_start; bp.ranges = im.ranges;
+            bp.tile_last = im.tile_last; bp.tile_loaded = im.tile_loaded;
             bp.ticket = g.counters + CNT_COL_TICKET; bp.tile_status = g.tile_status; bp.err = g.counters + CNT_OVERFLOW;
             bp.long_list = b.bk_long_list; bp.long_cnt = g.counters + CNT_LONG; bp.keys = b.bk_keys; bp.inst_gid = b.inst_gid; bp.inv = b.inv;
             GSR_STAGE(ST_BK_COUNT, dbg, launch_bucket_count(stream, bp));
@@ -393,10 +394,13 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
         });
         if (lpt) launch_tile_order(stream, im.ranges, nullptr, 0, (int)T, im.order_fwd);
     }
-    // split heavy tiles combine tile_last / tile_loaded with atomicMax: start from zero (adjacent arrays)
-    GSR_HIP(hipMemsetAsync(im.tile_last, 0,
-                           (size_t)(reinterpret_cast<char *>(im.tile_loaded + T) - reinterpret_cast<char *>(im.tile_last)),
-                           stream));
+    // split heavy tiles combine tile_last / tile_loaded with atomicMax: start from zero (adjacent arrays; the
+    // bucket path's column pass clears them)
+    if (!bucket || R == 0)
+        GSR_HIP(hipMemsetAsync(im.tile_last, 0,
+                               (size_t)(reinterpret_cast<char *>(im.tile_loaded + T) -
+                                        reinterpret_cast<char *>(im.tile_last)),
+                               stream));
     RenderFwdParams rp;
     rp.W = W; rp.H = H; rp.gx = gx; rp.gy = gy; rp.num_tiles = (int)T;
     rp.tile_order = lpt ? im.order_fwd : nullptr;

@@ -251,6 +251,8 @@ __global__ __launch_bounds__(256) void bk_columns_kernel(BucketParams p) {
             p.tile_start[t] = st;
             p.ranges[t] = tot ? make_uint2(st, st + tot) : make_uint2(0, 0);  // empty: (0, 0), as the reference
             p.tile_cnt[t] = tot;
+            p.tile_last[t] = 0u;
+            p.tile_loaded[t] = 0u;
             if (t == T - 1) p.tile_start[T] = st + tot;
         }
         const bool l0 = t < T && tot > SEG_CAP && tot <= SEG_BLOCK_CAP, l1 = t < T && tot > SEG_BLOCK_CAP;

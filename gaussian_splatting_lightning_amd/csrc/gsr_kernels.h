@@ -73,6 +73,7 @@ struct BucketParams {
     uint32_t *ticket;      // zeroed: column-pass workgroup ticket
     uint64_t *tile_status; // zeroed: div_up(T, 64) look-back words of the column pass
     uint32_t *err;         // look-back failure flag
+    uint32_t *tile_last, *tile_loaded;  // T each: cleared by the column pass for the forward composite
     unsigned long long *keys;  // R: depth << 32 | u, bucketed by tile
     uint32_t *inst_gid;    // R
     uint32_t *inv;         // R: reset to INV_NONE by the scatter (the forward composite fills it)

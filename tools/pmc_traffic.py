@@ -17,6 +17,8 @@ from pmc_summary import load, short  # noqa: E402
 STAGE_OF = {
     "render_fwd": "render_fwd", "render_bwd": "render_bwd", "preprocess_kernel": "preprocess",
     "preprocess_bwd": "preprocess_bwd", "expand_kernel": "expand", "big_reduce": "big_reduce",
+    "bk_walk_kernel<false": "bucket_count_walk", "bk_walk_kernel<true": "bucket_scatter",
+    "bk_columns": "bucket_columns", "seg_sort_kernel": "seg_sort",
 }
 
 
