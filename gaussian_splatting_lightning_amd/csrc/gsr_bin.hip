@@ -536,7 +536,7 @@ void launch_seg_sort(hipStream_t s, const SegSortParams &p) {
     if (p.T == 0) return;
     seg_sort_kernel<<<std::min(div_up(p.T, 4), (uint32_t)tuning("seg_grid", 1536)), 256, 0, s>>>(p);
     constexpr uint32_t HUGE_LDS_KEYS = 8192;  // 64 KB
-    seg_huge_kernel<<<128, 256, HUGE_LDS_KEYS * sizeof(unsigned long long), s>>>(p, HUGE_LDS_KEYS);
+    seg_huge_kernel<<<512, 256, HUGE_LDS_KEYS * sizeof(unsigned long long), s>>>(p, HUGE_LDS_KEYS);
 }
 
 }  // namespace gsr

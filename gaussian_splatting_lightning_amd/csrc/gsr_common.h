@@ -85,6 +85,7 @@ inline void carve_sort(Carver &c, SortScratch &s, uint32_t n, bool need_v0) {
 // Bucket binning (gsr_bin.hip): used when the tile count fits the LDS histogram of one workgroup.
 constexpr uint32_t BK_MAX_TILES = 32768;  // 128 KB of LDS counters (4K images: 32400 tiles)
 constexpr uint32_t BK_MAX_BLOCKS = 512;   // rows of the count matrix (carved for the maximum)
+constexpr uint32_t BK_MAX_MEAN = 1024;    // default path choice: mean instances per tile up to this
 constexpr uint32_t SEG_CAP = 511;         // longest tile the per-wave register sort takes (8 keys per lane);
                                           // SEG_CAP + 1 is a multiple of the LPT bucket width (seg_block)
 constexpr uint32_t SEG_BLOCK_CAP = 2048;  // longest tile one workgroup sorts (4 waves x 512 keys); longer: chunks

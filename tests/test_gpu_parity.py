@@ -401,7 +401,12 @@ def test_long_tiles_and_depth_ties(gpu_device, n, W, H):
         inp[k][1000:1200] = inp[k][1000]
         inp[k][5000:5300] = inp[k][5001]
     dc, di = upstream(W, H, 23)
-    hip = run_hip(inp, gpu_device, dc, di)
+    from gaussian_splatting_lightning_amd import _native
+    try:
+        _native.set_tuning("bucket", 2)  # bucket binning even for these long tiles (the default picks radix)
+        hip = run_hip(inp, gpu_device, dc, di)
+    finally:
+        _native.set_tuning("bucket", 1)
     run = compare_forward(inp, hip, run_oracle(inp))
     n_tile = np.diff(hip_state_arrays(hip)["ranges"], axis=1)[:, 0]
     if W > 32:
@@ -418,8 +423,9 @@ def test_binning_paths_are_bitwise_identical(gpu_device, W, H):
     from gaussian_splatting_lightning_amd import _native
     inp = scene_inputs(200_000 if W > 100 else 60_000, W, H, sh_degree=3, seed=6, stress_fraction=0.01)
     dc, di = upstream(W, H, 6)
-    ref = run_hip(inp, gpu_device, dc, di)
     try:
+        _native.set_tuning("bucket", 2)
+        ref = run_hip(inp, gpu_device, dc, di)
         _native.set_tuning("bucket", 0)
         alt = run_hip(inp, gpu_device, dc, di)
     finally:
