@@ -55,10 +55,13 @@ __device__ __forceinline__ void cov3d_backward(float3 scale, float mod, float4 r
 // to dsh_out (zeros when not visible) for the cooperative store; otherwise SH is read / written directly.
 template <bool LDS>
 __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p, const int i, const float *sh_in,
-                                                   float *dsh_out) {
+                                                   float *dsh_out, bool have_gs, const float (&gs_in)[10]) {
     const bool vis = p.radii[i] > 0;
     float gs[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    if (vis) {
+    if (vis && have_gs && p.tiles[i] <= BIG_GAUSSIAN_TILES) {
+#pragma unroll
+        for (int k = 0; k < 10; k++) gs[k] = gs_in[k];
+    } else if (vis) {
         const uint32_t start = p.inst_start[i], cnt = p.tiles[i];
         if (cnt > BIG_GAUSSIAN_TILES) {
             add_row(p.bigsum, p.big_slot[i], gs);
@@ -288,7 +291,8 @@ template <bool LDS_SH>
 __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams p) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (!LDS_SH) {
-        if (i < p.P) preprocess_bwd_one<false>(p, i, nullptr, nullptr);
+        const float none[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        if (i < p.P) preprocess_bwd_one<false>(p, i, nullptr, nullptr, false, none);
         return;
     }
     __shared__ __attribute__((aligned(16))) float s_sh[4][64 * SH_STRIDE];
@@ -296,6 +300,75 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
     const size_t gbase = ((size_t)blockIdx.x * 256 + (size_t)w * 64) * 48;  // first float of the wave's block
     const size_t gend = (size_t)p.P * 48;
     float *sw = s_sh[w];
+    // Gradient rows of the wave's 64 Gaussians (rows_by_u: each Gaussian's rows are contiguous), gathered
+    // jointly: the (Gaussian, row) pairs of all lanes are enumerated in order, every lane loads the inv words of
+    // pairs l, l + 64, ... of a chunk, then the rows the composite wrote (others read as zero) into the LDS that later
+    // stages the SH block, then each lane sums its own Gaussian's rows in row order.  Divergent per-lane
+    // loops of dependent loads cost ~40 % of the kernel otherwise.  Gaussians above BIG_GAUSSIAN_TILES rows
+    // take their block-reduced sum in preprocess_bwd_one.
+    float gs[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (p.rows_by_u) {
+        const bool vis = i < p.P && p.radii[i] > 0;
+        const uint32_t cnt = vis ? p.tiles[i] : 0u;
+        const uint32_t len = cnt <= BIG_GAUSSIAN_TILES ? cnt : 0u;
+        const uint32_t incl = wave_inclusive_scan(len, lane);
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        const uint32_t pst = incl - len;
+        constexpr uint32_t CH = 320, PER = CH / 64;  // pairs per chunk: 10 floats each fit the SH staging
+        // (first pair, first expansion index) of each lane's Gaussian, in the staging area's last 512 B
+        uint2 *s_meta = reinterpret_cast<uint2 *>(sw + CH * 10);
+        static_assert(CH * 10 + 128 <= 64 * SH_STRIDE, "row chunk + meta fit the SH staging");
+        s_meta[lane] = make_uint2(pst, len ? p.inst_start[i] : 0u);
+        wave_lds_sync();
+        for (uint32_t c0 = 0; c0 < total; c0 += CH) {
+            float4 ra[PER], rb[PER];
+            float2 rc[PER];
+            uint32_t sidx[PER];
+            uint32_t uu[PER];
+#pragma unroll
+            for (uint32_t r = 0; r < PER; r++) {  // all inv words of the chunk first ...
+                const uint32_t j = c0 + r * 64 + lane;
+                sidx[r] = INV_NONE;
+                uu[r] = 0;
+                if (j < total) {
+                    int o = 0;
+#pragma unroll
+                    for (int step = 32; step; step >>= 1)
+                        if (s_meta[o + step].x <= j) o += step;
+                    const uint2 m = s_meta[o];
+                    uu[r] = m.y + (j - m.x);
+                    sidx[r] = p.inv[uu[r]];
+                }
+            }
+#pragma unroll
+            for (uint32_t r = 0; r < PER; r++) {  // ... then only the rows the composite wrote
+                ra[r] = rb[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+                rc[r] = make_float2(0.f, 0.f);
+                if (sidx[r] != INV_NONE) {
+                    const float4 *src = reinterpret_cast<const float4 *>(p.rows + (size_t)uu[r] * GRAD_ROW);
+                    ra[r] = src[0];
+                    rb[r] = src[1];
+                    rc[r] = *reinterpret_cast<const float2 *>(src + 2);
+                }
+            }
+#pragma unroll
+            for (uint32_t r = 0; r < PER; r++) {
+                const uint32_t q = r * 64 + lane;  // pair within the chunk
+                float *d = sw + q * 10;
+                d[0] = ra[r].x; d[1] = ra[r].y; d[2] = ra[r].z; d[3] = ra[r].w;
+                d[4] = rb[r].x; d[5] = rb[r].y; d[6] = rb[r].z; d[7] = rb[r].w;
+                d[8] = rc[r].x; d[9] = rc[r].y;
+            }
+            wave_lds_sync();
+            const uint32_t lo = max(pst, c0), hi = min(pst + len, c0 + CH);
+            for (uint32_t j = lo; j < hi; j++) {
+                const float *d = sw + (j - c0) * 10;
+#pragma unroll
+                for (int k = 0; k < 10; k++) gs[k] += d[k];
+            }
+            wave_lds_sync();
+        }
+    }
 #pragma unroll
     for (int c = 0; c < 12; c++) {
         const uint32_t f = c * 256 + lane * 4;
@@ -317,7 +390,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
     }
 #pragma unroll
     for (int k = 0; k < 48; k++) dshv[k] = 0.f;
-    if (i < p.P) preprocess_bwd_one<true>(p, i, shv, dshv);
+    if (i < p.P) preprocess_bwd_one<true>(p, i, shv, dshv, p.rows_by_u != 0, gs);
     if (!p.dL_dsh) return;
     wave_lds_sync();
     float4 *mine_w = reinterpret_cast<float4 *>(sw + lane * SH_STRIDE);
