@@ -107,6 +107,10 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
         p.dL_dcolors[3 * i + 2] = gs[8];
     }
     const int ncoef = p.M * 3;
+    if (LDS && (!vis || !p.shs)) {
+#pragma unroll
+        for (int k = 0; k < 48; k++) dsh_out[k] = 0.f;
+    }
     if (!vis) {
         if (p.dL_dopacity) p.dL_dopacity[i] = 0.f;
         if (p.dL_dmeans3D) { p.dL_dmeans3D[3 * i] = 0.f; p.dL_dmeans3D[3 * i + 1] = 0.f; p.dL_dmeans3D[3 * i + 2] = 0.f; }
@@ -230,10 +234,8 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
         float *dsh = p.dL_dsh ? p.dL_dsh + (size_t)i * ncoef : nullptr;  // null only with dL_dcolors_sh (API)
         const float *shp = p.shs + (size_t)i * ncoef;
         if (LDS) {
-            // LDS-staged: coefficients already in registers, dL/dsh handed back for the coalesced store
-#pragma unroll
-            for (int k = 0; k < 48; k++) dsh_out[k] = 0.f;
-            dm = dm + sh_backward_dispatch(p.D, sh_in, mean - campos, dRGB, dsh_out);
+            // LDS-staged block (M = 16): dL/dsh replaces the coefficients in place for the coalesced store
+            dm = dm + sh_backward_inplace_dispatch(p.D, dsh_out, mean - campos, dRGB);
         } else if (p.sh_vec16) {
             // 16 coefficients x 3 = 192 B per Gaussian: 12 float4 loads and stores per lane
             float shv[48], dshv[48];
@@ -378,24 +380,9 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         }
     }
     wave_lds_sync();
-    float shv[48], dshv[48];
-    const float4 *mine = reinterpret_cast<const float4 *>(sw + lane * SH_STRIDE);
-#pragma unroll
-    for (int k = 0; k < 12; k++) {
-        const float4 v = mine[k];
-        shv[4 * k] = v.x;
-        shv[4 * k + 1] = v.y;
-        shv[4 * k + 2] = v.z;
-        shv[4 * k + 3] = v.w;
-    }
-#pragma unroll
-    for (int k = 0; k < 48; k++) dshv[k] = 0.f;
-    if (i < p.P) preprocess_bwd_one<true>(p, i, shv, dshv, p.rows_by_u != 0, gs);
+    // each lane's 48 coefficients are read and replaced by dL/dsh in its LDS slot
+    if (i < p.P) preprocess_bwd_one<true>(p, i, nullptr, sw + lane * SH_STRIDE, p.rows_by_u != 0, gs);
     if (!p.dL_dsh) return;
-    wave_lds_sync();
-    float4 *mine_w = reinterpret_cast<float4 *>(sw + lane * SH_STRIDE);
-#pragma unroll
-    for (int k = 0; k < 12; k++) mine_w[k] = make_float4(dshv[4 * k], dshv[4 * k + 1], dshv[4 * k + 2], dshv[4 * k + 3]);
     wave_lds_sync();
 #pragma unroll
     for (int c = 0; c < 12; c++) {

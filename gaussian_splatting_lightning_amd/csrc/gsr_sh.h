@@ -112,6 +112,71 @@ __device__ __forceinline__ float3 sh_backward(const float *__restrict__ sh, floa
     return dnormvdv(dir_orig, dL_ddir);
 }
 
+// sh_backward on one buffer: reads the coefficients, then overwrites them with dL/dsh (zeros above the degree,
+// up to 16 coefficients).  For an LDS-staged block, so the coefficients never occupy registers all at once.
+template <int DEG>
+__device__ __forceinline__ float3 sh_backward_inplace(float *sh_io, float3 dir_orig, float3 dRGB) {
+    const float len = sqrtf(dot3(dir_orig, dir_orig));
+    const float3 dir = make_float3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
+    float3 dx = make_float3(0, 0, 0), dy = dx, dz = dx;
+    const float x = dir.x, y = dir.y, z = dir.z;
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    const float *sh = sh_io;
+    if (DEG > 0) {
+        dx = -GSR_SH_C1 * f3(sh + 9);
+        dy = -GSR_SH_C1 * f3(sh + 3);
+        dz = GSR_SH_C1 * f3(sh + 6);
+        if (DEG > 1) {
+            const float3 s4 = f3(sh + 12), s5 = f3(sh + 15), s6 = f3(sh + 18), s7 = f3(sh + 21), s8 = f3(sh + 24);
+            dx = dx + (SH_C2[0] * y) * s4 + (SH_C2[2] * 2.f * -x) * s6 + (SH_C2[3] * z) * s7 + (SH_C2[4] * 2.f * x) * s8;
+            dy = dy + (SH_C2[0] * x) * s4 + (SH_C2[1] * z) * s5 + (SH_C2[2] * 2.f * -y) * s6 + (SH_C2[4] * 2.f * -y) * s8;
+            dz = dz + (SH_C2[1] * y) * s5 + (SH_C2[2] * 2.f * 2.f * z) * s6 + (SH_C2[3] * x) * s7;
+            if (DEG > 2) {
+                const float3 s9 = f3(sh + 27), s10 = f3(sh + 30), s11 = f3(sh + 33), s12 = f3(sh + 36),
+                             s13 = f3(sh + 39), s14 = f3(sh + 42), s15 = f3(sh + 45);
+                dx = dx + (SH_C3[0] * 3.f * 2.f * xy) * s9 + (SH_C3[1] * yz) * s10 + (SH_C3[2] * -2.f * xy) * s11 +
+                     (SH_C3[3] * -3.f * 2.f * xz) * s12 + (SH_C3[4] * (-3.f * xx + 4.f * zz - yy)) * s13 +
+                     (SH_C3[5] * 2.f * xz) * s14 + (SH_C3[6] * 3.f * (xx - yy)) * s15;
+                dy = dy + (SH_C3[0] * 3.f * (xx - yy)) * s9 + (SH_C3[1] * xz) * s10 +
+                     (SH_C3[2] * (-3.f * yy + 4.f * zz - xx)) * s11 + (SH_C3[3] * -3.f * 2.f * yz) * s12 +
+                     (SH_C3[4] * -2.f * xy) * s13 + (SH_C3[5] * -2.f * yz) * s14 + (SH_C3[6] * -3.f * 2.f * xy) * s15;
+                dz = dz + (SH_C3[1] * xy) * s10 + (SH_C3[2] * 4.f * 2.f * yz) * s11 +
+                     (SH_C3[3] * 3.f * (2.f * zz - xx - yy)) * s12 + (SH_C3[4] * 4.f * 2.f * xz) * s13 +
+                     (SH_C3[5] * (xx - yy)) * s14;
+            }
+        }
+    }
+    // every read precedes the first write (the compiler cannot reorder them: same buffer)
+    float *dsh = sh_io;
+    const float3 zero = make_float3(0, 0, 0);
+    st3(dsh, GSR_SH_C0 * dRGB);
+    st3(dsh + 3, DEG > 0 ? (-GSR_SH_C1 * y) * dRGB : zero);
+    st3(dsh + 6, DEG > 0 ? (GSR_SH_C1 * z) * dRGB : zero);
+    st3(dsh + 9, DEG > 0 ? (-GSR_SH_C1 * x) * dRGB : zero);
+    st3(dsh + 12, DEG > 1 ? (SH_C2[0] * xy) * dRGB : zero);
+    st3(dsh + 15, DEG > 1 ? (SH_C2[1] * yz) * dRGB : zero);
+    st3(dsh + 18, DEG > 1 ? (SH_C2[2] * (2.f * zz - xx - yy)) * dRGB : zero);
+    st3(dsh + 21, DEG > 1 ? (SH_C2[3] * xz) * dRGB : zero);
+    st3(dsh + 24, DEG > 1 ? (SH_C2[4] * (xx - yy)) * dRGB : zero);
+    st3(dsh + 27, DEG > 2 ? (SH_C3[0] * y * (3.f * xx - yy)) * dRGB : zero);
+    st3(dsh + 30, DEG > 2 ? (SH_C3[1] * xy * z) * dRGB : zero);
+    st3(dsh + 33, DEG > 2 ? (SH_C3[2] * y * (4.f * zz - xx - yy)) * dRGB : zero);
+    st3(dsh + 36, DEG > 2 ? (SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy)) * dRGB : zero);
+    st3(dsh + 39, DEG > 2 ? (SH_C3[4] * x * (4.f * zz - xx - yy)) * dRGB : zero);
+    st3(dsh + 42, DEG > 2 ? (SH_C3[5] * z * (xx - yy)) * dRGB : zero);
+    st3(dsh + 45, DEG > 2 ? (SH_C3[6] * x * (xx - 3.f * yy)) * dRGB : zero);
+    const float3 dL_ddir = make_float3(dot3(dx, dRGB), dot3(dy, dRGB), dot3(dz, dRGB));
+    return dnormvdv(dir_orig, dL_ddir);
+}
+__device__ __forceinline__ float3 sh_backward_inplace_dispatch(int deg, float *sh_io, float3 dir_orig, float3 dRGB) {
+    switch (deg) {
+        case 0: return sh_backward_inplace<0>(sh_io, dir_orig, dRGB);
+        case 1: return sh_backward_inplace<1>(sh_io, dir_orig, dRGB);
+        case 2: return sh_backward_inplace<2>(sh_io, dir_orig, dRGB);
+        default: return sh_backward_inplace<3>(sh_io, dir_orig, dRGB);
+    }
+}
+
 // SH basis values b[0..(DEG+1)^2) at unit direction (x,y,z); b[k] * dRGB is sh_backward's dL/dsh[k].
 template <int DEG>
 __device__ __forceinline__ void sh_basis(float x, float y, float z, float *b) {
