@@ -64,6 +64,43 @@ __device__ __forceinline__ void wave_reduce10_store(const float m[10], float *__
     if ((lane & 31) == 0) dst[8 + (lane >> 5)] = c8;
 }
 
+// Two instances' 10 values (20) through the same transposing reduction: the register count halves at each
+// exchange level, so the pair costs ~58 VALU ops instead of 2 x ~40.  After the bit-5/4 swaps b[k] holds value
+// 4 k + 2 b4 + b5; the bit-3 exchange pairs (b0, b1) and (b2, b3) into values 8 m + 4 b3 + 2 b4 + b5, and b4 sums
+// alone into 16 + 2 b4 + b5.  Value v < 10 is instance 0's, v >= 10 instance 1's (the next PART-float row).
+__device__ __forceinline__ void wave_reduce20_store(const float m0[10], const float m1[10], float *__restrict__ dst,
+                                                    int lane) {
+    float a[10];
+#pragma unroll
+    for (int i = 0; i < 5; i++) a[i] = sum_swap32(m0[2 * i], m0[2 * i + 1]);
+#pragma unroll
+    for (int i = 0; i < 5; i++) a[5 + i] = sum_swap32(m1[2 * i], m1[2 * i + 1]);
+    float bb[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) bb[k] = sum_swap16(a[2 * k], a[2 * k + 1]);
+    const bool hi3 = (lane & 8) != 0;
+    float c[3];
+#pragma unroll
+    for (int m = 0; m < 2; m++) {
+        const float keep = hi3 ? bb[2 * m + 1] : bb[2 * m], send = hi3 ? bb[2 * m] : bb[2 * m + 1];
+        c[m] = keep + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send), 0x128, 0xf, 0xf, false));
+    }
+    c[2] = dpp_add<0x128>(bb[4]);  // row_ror:8 (= lane ^ 8)
+#pragma unroll
+    for (int m = 0; m < 3; m++) {
+        c[m] = dpp_add<0xB1>(c[m]);   // quad_perm [1,0,3,2]
+        c[m] = dpp_add<0x4E>(c[m]);   // quad_perm [2,3,0,1]
+        c[m] = dpp_add<0x141>(c[m]);  // row_half_mirror
+    }
+    const int low = ((lane >> 1) & 4) | ((lane >> 3) & 2) | (lane >> 5);  // 4 b3 + 2 b4 + b5
+    if ((lane & 7) == 0) {
+        dst[low] = c[0];                                // values 0..7
+        const int v = 8 + low;                          // values 8..15
+        dst[v < 10 ? v : v - 10 + PART] = c[1];
+    }
+    if ((lane & 15) == 0) dst[16 + low - 10 + PART] = c[2];  // values 16..19 (b3 = 0 here)
+}
+
 template <bool HAS_INV, int MIN_WAVES, int WPB>
 __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_bwd_v3_kernel(RenderBwdParams p) {
     __shared__ float4 s_a[WPB][BWD_BATCH];
@@ -234,7 +271,7 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_bwd_v3_kernel(Rend
 //   LPF: the broadcast LDS reads of instance j+1 are issued before instance j's math.  (A two-deep software
 //   pipeline of the batches' global gathers was measured and gained nothing at 5 waves/SIMD.)
 // ------------------------------------------------------------------------------------------------
-template <bool HAS_INV, bool STRIP, int PRED, bool LPF, int MIN_WAVES = 5>
+template <bool HAS_INV, bool STRIP, int PRED, bool LPF, int MIN_WAVES = 5, bool PAIR = false>
 __global__ __launch_bounds__(64, MIN_WAVES) void render_bwd_v4_kernel(RenderBwdParams p) {
     __shared__ float4 s_a[BWD_BATCH + 1];  // + 1: the LPF read-ahead of the batch's last instance
     __shared__ float4 s_b[BWD_BATCH + 1];
@@ -307,7 +344,8 @@ __global__ __launch_bounds__(64, MIN_WAVES) void render_bwd_v4_kernel(RenderBwdP
         wave_lds_sync();
         float4 na = s_a[0], nb = s_b[0];
         float2 nc = s_c[0];
-        for (int j = 0; j < cnt; j++) {
+        // one instance's pass over the lane's pixels: updates T / D, returns the 10 per-lane sums in m
+        auto pass = [&](const int j, float m[10]) -> bool {
             const uint32_t idx = (uint32_t)(bend - 1 - j);
             float4 a, b;  // a: x, y, A, B; b: C, o, r, g
             float2 c;     // b, 1/depth
@@ -387,20 +425,33 @@ __global__ __launch_bounds__(64, MIN_WAVES) void render_bwd_v4_kernel(RenderBwdP
                     Q2 = fmaf(qdy, dy, Q2);
                 }
             }
+            m[0] = Q0;
+            m[1] = Q0 * dx;
+            m[2] = Q1;
+            m[3] = m[1] * dx;
+            m[4] = Q1 * dx;
+            m[5] = Q2;
+            m[6] = w0;
+            m[7] = w1;
+            m[8] = w2;
+            m[9] = w3;
+            return any;
+        };
+        for (int j = 0; j < cnt; j += PAIR ? 2 : 1) {
+            float m0[10];
+            const bool any0 = pass(j, m0);
             float *dst = s_part[j];
-            if (__ballot(any)) {
-                float m[10];
-                m[0] = Q0;
-                m[1] = Q0 * dx;
-                m[2] = Q1;
-                m[3] = m[1] * dx;
-                m[4] = Q1 * dx;
-                m[5] = Q2;
-                m[6] = w0;
-                m[7] = w1;
-                m[8] = w2;
-                m[9] = w3;
-                wave_reduce10_store(m, dst, lane);
+            if (PAIR && j + 1 < cnt) {
+                float m1[10];
+                const bool any1 = pass(j + 1, m1);
+                if (__ballot(any0 || any1)) {
+                    wave_reduce20_store(m0, m1, dst, lane);
+                } else if (lane < 10) {
+                    dst[lane] = 0.f;
+                    dst[PART + lane] = 0.f;
+                }
+            } else if (__ballot(any0)) {
+                wave_reduce10_store(m0, dst, lane);
             } else if (lane < 10) {
                 dst[lane] = 0.f;
             }
@@ -438,11 +489,12 @@ void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
         q.prio_div = tuning("prio_div", 0);
         q.stamps = tuning("stamp", 0) ? stamp_buffer(1) : nullptr;
         const dim3 grid(p.num_tiles), block(64);
-        const int strip = tuning("bwd_strip", 1), pred = tuning("bwd_pred", 2);
+        const int strip = tuning("bwd_strip", 1), pred = tuning("bwd_pred", 2), pair = tuning("bwd_pair", 1);
 #define GSR_BWD4(INV)                                                                                   \
         do {                                                                                           \
             if (!strip) render_bwd_v4_kernel<INV, false, 0, false><<<grid, block, 0, s>>>(q);          \
             else if (pred == 1) render_bwd_v4_kernel<INV, true, 1, false><<<grid, block, 0, s>>>(q);   \
+            else if (pred == 2 && pair) render_bwd_v4_kernel<INV, true, 2, false, 5, true><<<grid, block, 0, s>>>(q); \
             else if (pred == 2) render_bwd_v4_kernel<INV, true, 2, false><<<grid, block, 0, s>>>(q);   \
             else if (minw >= 6) render_bwd_v4_kernel<INV, true, 0, false, 6><<<grid, block, 0, s>>>(q); \
             else render_bwd_v4_kernel<INV, true, 0, false><<<grid, block, 0, s>>>(q);                  \

@@ -365,7 +365,8 @@ def test_densify_stats_from_backward(gpu_device):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knobs", [{"fwd_strip": 1}, {"bwd_strip": 0}, {"bwd_pred": 0}, {"bwd_pred": 1}, {"bwd_v": 3}])
+@pytest.mark.parametrize("knobs", [{"fwd_strip": 1}, {"bwd_strip": 0}, {"bwd_pred": 0}, {"bwd_pred": 1}, {"bwd_v": 3},
+                                   {"bwd_pair": 0}])
 def test_composite_variants_are_bitwise_identical(gpu_device, knobs):
     """Strip skipping only skips rows where every pixel fails alpha >= 1/255, and the predicated backward
     body performs the same operations as the branchy one: outputs and gradients must match bit for bit
@@ -381,7 +382,7 @@ def test_composite_variants_are_bitwise_identical(gpu_device, knobs):
         alt = run_hip(inp, gpu_device, dc, di)
     finally:
         for k in knobs:
-            _native.set_tuning(k, {"fwd_strip": 0, "bwd_strip": 1, "bwd_pred": 2, "bwd_v": 4}[k])
+            _native.set_tuning(k, {"fwd_strip": 0, "bwd_strip": 1, "bwd_pred": 2, "bwd_v": 4, "bwd_pair": 1}[k])
     for k in ("color", "invdepth", "radii"):
         assert np.array_equal(ref[k], alt[k]), k
     for k in GRADS:
