@@ -438,3 +438,12 @@ def test_binning_paths_are_bitwise_identical(gpu_device, W, H):
         assert np.array_equal(ref[k], alt[k]), k
     for k in GRADS:
         assert np.array_equal(ref["grads"][k], alt["grads"][k]), k
+
+
+def test_beyond_lpt_and_bucket_tile_limits(gpu_device):
+    """More than 32768 tiles (8K-class image): the radix binning path."""
+    inp = scene_inputs(3000, 4160, 2336, sh_degree=1, seed=31)
+    dc, di = upstream(4160, 2336, 31)
+    hip = run_hip(inp, gpu_device, dc, di)
+    run = compare_forward(inp, hip, run_oracle(inp))
+    compare_backward(hip, run, dc, di, 1e-3)
