@@ -377,6 +377,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             sp.tile_order = (lpt && (((SEG_CAP + 1) >> tuning("lpt_shift", 3)) << tuning("lpt_shift", 3)) == SEG_CAP + 1)
                                 ? im.order_fwd : nullptr; sp.keys = b.bk_keys; sp.keys2 = b.bk_keys2;
             sp.sorted_u = b.sorted_u; sp.long_list = b.bk_long_list; sp.long_cnt = g.counters + CNT_LONG;
+            sp.tie_list = b.bk_tie_list; sp.tie_cnt = g.counters + CNT_TIES;
             GSR_STAGE(ST_SEG_SORT, dbg, launch_seg_sort(stream, sp));
         } else {
             GSR_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * T, stream));

@@ -368,58 +368,222 @@ __device__ __forceinline__ void seg_sort_wave_impl(const unsigned long long *__r
     }
 }
 
+// 32-bit form of the same network.  Within one sort the keys are ranked by a 32-bit proxy
+//   k32 = ((depth bits - min depth bits) >> sh) << IDXB | index,   IDXB = log2(64 E),
+// with sh chosen so the depth offsets fit 32 - IDXB bits: unique keys, compare-exchanges are v_min/v_max
+// pairs and lane exchanges one ds_bpermute (about 2.5x fewer VALU ops than 64-bit keys).  The proxy orders
+// exactly like (depth, u) unless two keys share a quantised depth (~8 % of 512-key sorts at cfg 3).  Such ties
+// (a ballot over adjacent sorted keys) are put in order after the gather by odd-even transposition passes on
+// the full keys: keys of different quantised depth are already ordered, so only the tie runs move.  After
+// TIE_PASSES pass pairs without convergence the sort returns false and the caller hands the tile to the 64-bit
+// sort.  Descending merge halves run on complemented keys, so
+// every stage of a merge level is an ascending min / max.  scratch: 64 E keys of LDS (the full keys, gathered
+// back by index after the sort).
 template <int E>
-__device__ __forceinline__ void seg_sort_wave(const unsigned long long *keys, uint32_t start, uint32_t n,
-                                              uint32_t *sorted_u, int lane) {
-    seg_sort_wave_impl<E>(keys, start, n, sorted_u, nullptr, lane);
+__device__ __forceinline__ bool seg_sort_wave32(const unsigned long long *__restrict__ keys, uint32_t start, uint32_t n,
+                                                unsigned long long *__restrict__ scratch, int lane,
+                                                unsigned long long (&out)[E]) {
+    constexpr int LOGE = (E >= 8) ? 3 : (E >= 4) ? 2 : (E >= 2) ? 1 : 0;
+    constexpr int IDXB = LOGE + 6;
+    const uint32_t base = (uint32_t)lane * E;
+    unsigned long long x64[E];
+    uint32_t dmin = 0xffffffffu, dmax = 0u;
+#pragma unroll
+    for (int r = 0; r < E; r++) {
+        const bool valid = base + r < n;
+        x64[r] = valid ? keys[start + base + r] : ~0ull;
+        scratch[base + r] = x64[r];
+        const uint32_t d = (uint32_t)(x64[r] >> 32);
+        if (valid) {
+            dmin = min(dmin, d);
+            dmax = max(dmax, d);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        dmin = min(dmin, (uint32_t)__shfl_xor((int)dmin, o));
+        dmax = max(dmax, (uint32_t)__shfl_xor((int)dmax, o));
+    }
+    const uint32_t range = dmax - dmin;
+    const int bits = range ? 32 - __builtin_clz(range) : 0;
+    const int sh = bits > 32 - IDXB ? bits - (32 - IDXB) : 0;
+    uint32_t x[E];
+#pragma unroll
+    for (int r = 0; r < E; r++)
+        x[r] = (base + r < n) ? ((((uint32_t)(x64[r] >> 32) - dmin) >> sh) << IDXB) | (base + r) : 0xffffffffu;
+    // merge levels k < E: registers only, compile-time directions
+#pragma unroll
+    for (int lk = 1; lk < LOGE; lk++) {
+#pragma unroll
+        for (int lj = lk - 1; lj >= 0; lj--) {
+#pragma unroll
+            for (int r = 0; r < E; r++) {
+                if (r & (1 << lj)) continue;
+                const uint32_t a = x[r], c = x[r | (1 << lj)];
+                const uint32_t lo = min(a, c), hi = max(a, c);
+                const bool asc = (r & (1 << lk)) == 0;
+                x[r] = asc ? lo : hi;
+                x[r | (1 << lj)] = asc ? hi : lo;
+            }
+        }
+    }
+    for (int lk = LOGE > 1 ? LOGE : 1; lk <= LOGE + 6; lk++) {
+        const uint32_t flip = (base & (1u << lk)) ? 0xffffffffu : 0u;  // descending half: complemented keys
+#pragma unroll
+        for (int r = 0; r < E; r++) x[r] ^= flip;
+        for (int lj = lk - 1; lj >= LOGE; lj--) {
+            const int lm = 1 << (lj - LOGE);
+            const bool lower = (lane & lm) == 0;
+            const int addr = (lane ^ lm) << 2;
+            uint32_t y[E];
+#pragma unroll
+            for (int r = 0; r < E; r++) y[r] = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)x[r]);
+#pragma unroll
+            for (int r = 0; r < E; r++) x[r] = lower ? min(x[r], y[r]) : max(x[r], y[r]);
+        }
+#pragma unroll
+        for (int lj = LOGE - 1; lj >= 0; lj--) {
+#pragma unroll
+            for (int r = 0; r < E; r++) {
+                if (r & (1 << lj)) continue;
+                const uint32_t a = x[r], c = x[r | (1 << lj)];
+                x[r] = min(a, c);
+                x[r | (1 << lj)] = max(a, c);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < E; r++) x[r] ^= flip;
+    }
+    // ties of the quantised depth between adjacent sorted keys (both real)
+    const uint32_t next0 = (uint32_t)__shfl_down((int)x[0], 1);
+    bool tie = false;
+#pragma unroll
+    for (int r = 0; r < E; r++) {
+        const uint32_t nx = r + 1 < E ? x[r + 1] : next0;
+        const bool both = base + r + 1 < n && (r + 1 < E || lane < 63);
+        tie |= both && (x[r] >> IDXB) == (nx >> IDXB);
+    }
+    const bool any_tie = __ballot(tie) != 0;
+    wave_lds_sync();  // scratch written by every lane above
+#pragma unroll
+    for (int r = 0; r < E; r++) out[r] = scratch[x[r] & ((1u << IDXB) - 1u)];
+    if (!any_tie) return true;
+    constexpr int TIE_PASSES = 8;
+    for (int it = 0; it < TIE_PASSES; it++) {
+        bool sw = false;
+        auto ce = [&](unsigned long long &a, unsigned long long &b) {
+            const bool s = b < a;
+            const unsigned long long lo = s ? b : a, hi = s ? a : b;
+            a = lo;
+            b = hi;
+            sw |= s;
+        };
+        // even phase: pairs (2m, 2m + 1)
+        if (E == 1) {
+            const unsigned long long y = __shfl_xor(out[0], 1);
+            const bool lower = (lane & 1) == 0;
+            const unsigned long long v = lower ? (y < out[0] ? y : out[0]) : (y > out[0] ? y : out[0]);
+            sw |= v != out[0];
+            out[0] = v;
+        } else {
+#pragma unroll
+            for (int r = 0; r + 1 < E; r += 2) ce(out[r], out[r + 1]);
+        }
+        // odd phase: pairs (2m + 1, 2m + 2); the pair across lanes l, l + 1 is (l E + E - 1, (l + 1) E)
+#pragma unroll
+        for (int r = 1; r + 1 < E; r += 2) ce(out[r], out[r + 1]);
+        const unsigned long long nx = __shfl_down(out[0], 1), pv = __shfl_up(out[E - 1], 1);
+        // E == 1: lane l is one element, in the pair (l, l + 1) when l is odd, (l - 1, l) when even
+        const bool low_end = E > 1 || (lane & 1), high_end = E > 1 || !(lane & 1);
+        if (low_end && lane < 63 && nx < out[E - 1]) {
+            out[E - 1] = nx;
+            sw = true;
+        }
+        if (high_end && lane > 0 && out[0] < pv) {
+            out[0] = pv;
+            sw = true;
+        }
+        if (!__ballot(sw)) return true;
+    }
+    return false;
 }
-template <int E>
-__device__ __forceinline__ void seg_sort_wave_to_lds(const unsigned long long *keys, uint32_t start, uint32_t n,
+
+// Wrappers.  P32: the proxy-key sort, false on a tie (nothing written; seg_huge sorts the tile again on its
+// 64-bit keys).  P32 = false: the 64-bit network.  The two live in separate kernels (seg_sort / seg_huge), so
+// the common kernel carries only the 32-bit network's registers.
+template <int E, bool P32>
+__device__ __forceinline__ bool seg_sort_wave(const unsigned long long *keys, uint32_t start, uint32_t n,
+                                              uint32_t *sorted_u, int lane, unsigned long long *scratch) {
+    if (!P32) {
+        seg_sort_wave_impl<E>(keys, start, n, sorted_u, nullptr, lane);
+        return true;
+    }
+    unsigned long long y[E];
+    if (!seg_sort_wave32<E>(keys, start, n, scratch, lane, y)) return false;
+    const uint32_t base = (uint32_t)lane * E;
+#pragma unroll
+    for (int r = 0; r < E; r++)
+        if (base + r < n) sorted_u[start + base + r] = (uint32_t)y[r];
+    return true;
+}
+// sorted (padded) keys into lds_out, which is also the scratch
+template <int E, bool P32>
+__device__ __forceinline__ bool seg_sort_wave_to_lds(const unsigned long long *keys, uint32_t start, uint32_t n,
                                                      unsigned long long *lds_out, int lane) {
-    seg_sort_wave_impl<E>(keys, start, n, nullptr, lds_out, lane);
+    if (!P32) {
+        seg_sort_wave_impl<E>(keys, start, n, nullptr, lds_out, lane);
+        return true;
+    }
+    unsigned long long y[E];
+    if (!seg_sort_wave32<E>(keys, start, n, lds_out, lane, y)) return false;
+    wave_lds_sync();  // every lane's gathers done before the scratch is overwritten
+    const uint32_t base = (uint32_t)lane * E;
+#pragma unroll
+    for (int r = 0; r < E; r++) lds_out[base + r] = y[r];
+    return true;
 }
 
 // Workgroup sort of up to 16 x 512 keys in LDS: the waves sort 512-key chunks in registers (as
 // seg_sort_wave<8>) into LDS, padded with all-ones keys; then every key's position is its index in its chunk
-// plus its rank in each other chunk (branchless binary searches, 8 keys per thread interleaved).
+// plus its lower bound in each other chunk (seg_merge_ranks).
 constexpr uint32_t SB_CHUNK = 512;
-__device__ __forceinline__ void seg_lds_sort(const unsigned long long *__restrict__ keys, uint32_t start, uint32_t n,
-                                             uint32_t *__restrict__ sorted_u, unsigned long long *__restrict__ keys_out,
-                                             unsigned long long *__restrict__ s_x, int w, int lane) {
-    const uint32_t nch = (n + SB_CHUNK - 1) / SB_CHUNK;
-    for (uint32_t c = (uint32_t)w; c < nch; c += 4) {
-        const uint32_t c0 = c * SB_CHUNK;
-        seg_sort_wave_to_lds<8>(keys, start + c0, min(SB_CHUNK, n - c0), s_x + c0, lane);
-    }
-    __syncthreads();
-    constexpr int PER = 8;
+constexpr uint32_t SB_WAVE_SCRATCH = SEG_BLOCK_CAP / 4;  // a wave's share of the workgroup's key LDS
+
+// Merge ranks: branchless binary searches over the padded 512-key chunks, PER keys per thread interleaved.
+// Key slot i of a thread lies in chunk e0 / 512 + i / 2, and visits the other chunks by rotation (own + d), so
+// no search is spent on a key's own chunk; slots past n search harmlessly (chunk 0) and are not written.
+template <int PER>
+__device__ __forceinline__ void seg_merge_ranks(const unsigned long long *__restrict__ s_x, uint32_t n, uint32_t nch,
+                                                uint32_t start, uint32_t *__restrict__ sorted_u,
+                                                unsigned long long *__restrict__ keys_out) {
+    const uint32_t span = nch * SB_CHUNK;
     for (uint32_t e0 = 0; e0 < n; e0 += 256 * PER) {
         unsigned long long key[PER];
-        uint32_t pos[PER];
+        uint32_t pos[PER], own[PER];
 #pragma unroll
         for (int i = 0; i < PER; i++) {
             const uint32_t e = e0 + threadIdx.x + 256u * i;
             key[i] = e < n ? s_x[e] : ~0ull;
             pos[i] = e & (SB_CHUNK - 1);
+            own[i] = e < n ? (e & ~(SB_CHUNK - 1)) : 0u;
         }
-        for (uint32_t c2 = 0; c2 < nch; c2++) {
-            const unsigned long long *ch = s_x + c2 * SB_CHUNK;
-            uint32_t idx[PER];
+        for (uint32_t d = SB_CHUNK; d < span; d += SB_CHUNK) {
+            uint32_t lo[PER], idx[PER];
 #pragma unroll
-            for (int i = 0; i < PER; i++) idx[i] = 0;
+            for (int i = 0; i < PER; i++) {
+                lo[i] = own[i] + d;
+                if (lo[i] >= span) lo[i] -= span;
+                idx[i] = lo[i];
+            }
 #pragma unroll
             for (uint32_t step = SB_CHUNK / 2; step; step >>= 1) {
 #pragma unroll
                 for (int i = 0; i < PER; i++)
-                    if (ch[idx[i] + step - 1] < key[i]) idx[i] += step;
+                    if (s_x[idx[i] + step - 1] < key[i]) idx[i] += step;
             }
 #pragma unroll
-            for (int i = 0; i < PER; i++) {
-                const uint32_t e = e0 + threadIdx.x + 256u * i;
-                // the last probe decides between idx and idx + 1 (lower bound over 512 entries)
-                const uint32_t lb = idx[i] + (ch[idx[i]] < key[i] ? 1u : 0u);
-                if (e / SB_CHUNK != c2) pos[i] += lb;
-            }
+            for (int i = 0; i < PER; i++)  // the last probe decides between idx and idx + 1
+                pos[i] += idx[i] - lo[i] + (s_x[idx[i]] < key[i] ? 1u : 0u);
         }
 #pragma unroll
         for (int i = 0; i < PER; i++) {
@@ -429,18 +593,48 @@ __device__ __forceinline__ void seg_lds_sort(const unsigned long long *__restric
             else sorted_u[start + pos[i]] = (uint32_t)key[i];
         }
     }
+}
+
+// With P32 a chunk sort that meets a tie stores tag into *s_flag and the whole sort returns false (uniform over
+// the workgroup, nothing written); a workgroup's calls use distinct tags, so the flag is never cleared.
+template <bool P32>
+__device__ __forceinline__ bool seg_lds_sort(const unsigned long long *__restrict__ keys, uint32_t start, uint32_t n,
+                                             uint32_t *__restrict__ sorted_u, unsigned long long *__restrict__ keys_out,
+                                             unsigned long long *__restrict__ s_x, int w, int lane, uint32_t *s_flag,
+                                             uint32_t tag, uint32_t *t_mid = nullptr) {
+    const uint32_t nch = (n + SB_CHUNK - 1) / SB_CHUNK;
+    for (uint32_t c = (uint32_t)w; c < nch; c += 4) {
+        const uint32_t c0 = c * SB_CHUNK;
+        if (!seg_sort_wave_to_lds<8, P32>(keys, start + c0, min(SB_CHUNK, n - c0), s_x + c0, lane) && lane == 0)
+            *s_flag = tag;
+    }
+    __syncthreads();
+    if (P32 && *s_flag == tag) {
+        __syncthreads();  // every thread has read the flag before the LDS is reused
+        return false;
+    }
+    if (t_mid) *t_mid = stamp_now();
+    if (n <= 256u * 4u) seg_merge_ranks<4>(s_x, n, nch, start, sorted_u, keys_out);
+    else seg_merge_ranks<8>(s_x, n, nch, start, sorted_u, keys_out);
     __syncthreads();  // s_x is reused by the next chunk / tile
+    return true;
 }
 
 // Every tile up to SEG_BLOCK_CAP instances, in one persistent launch (the workgroups loop over the tiles, whose
-// counts are only known on the device, so every wave reaches the exit):
+// counts are only known on the device, so every wave reaches the exit), on 32-bit proxy keys (P32, else on
+// the 64-bit keys: the A/B reference, knob "seg32"):
 //   1. tiles of (SEG_CAP, SEG_BLOCK_CAP] instances, one workgroup each (seg_lds_sort).  With the LPT order
 //      they are exactly its first long_cnt[0] + long_cnt[1] slots (SEG_CAP + 1 is a multiple of the LPT
 //      bucket width), taken longest first; tiles above SEG_BLOCK_CAP among them are left to seg_huge;
 //   2. then the short tiles, one wave each (seg_sort_wave), again longest first.
+// A tile whose proxy keys tie is appended to tie_list for seg_huge.
+template <bool P32>
 __global__ __launch_bounds__(256) void seg_sort_kernel(SegSortParams p) {
     __shared__ unsigned long long s_x[SEG_BLOCK_CAP];
+    __shared__ uint32_t s_flag;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_flag = 0u;
+    __syncthreads();
     const uint32_t n0 = p.long_cnt[0], nlong = n0 + p.long_cnt[1];
     const uint32_t nl = p.tile_order ? nlong : n0;
     for (uint32_t i = blockIdx.x; i < nl; i += gridDim.x) {
@@ -448,7 +642,14 @@ __global__ __launch_bounds__(256) void seg_sort_kernel(SegSortParams p) {
         const uint2 rg = p.ranges[tile];
         const uint32_t n = rg.y - rg.x;
         if (n <= SEG_CAP || n > SEG_BLOCK_CAP) continue;  // workgroup-uniform
-        seg_lds_sort(p.keys, rg.x, n, p.sorted_u, nullptr, s_x, w, lane);
+        const uint32_t t0 = p.stamps ? stamp_now() : 0u;
+        uint32_t t1 = 0;
+        if (!seg_lds_sort<P32>(p.keys, rg.x, n, p.sorted_u, nullptr, s_x, w, lane, &s_flag, i + 1u,
+                               p.stamps ? &t1 : nullptr)) {
+            if (threadIdx.x == 0) p.tie_list[atomicAdd(p.tie_cnt, 1u)] = tile;
+            continue;
+        }
+        if (p.stamps && threadIdx.x == 0 && i < (uint32_t)STAMP_SLOTS) p.stamps[i] = make_uint4(t0, t1, stamp_now(), n);
     }
     const uint32_t s0 = p.tile_order ? nlong : 0u;
     // waves in the order workgroups finished phase 1 would be better balanced, but a shared work counter
@@ -458,29 +659,44 @@ __global__ __launch_bounds__(256) void seg_sort_kernel(SegSortParams p) {
         const uint2 rg = p.ranges[tile];
         const uint32_t n = rg.y - rg.x;
         if (n == 0 || n > SEG_CAP) continue;  // wave-uniform
-        if (n <= 64u) seg_sort_wave<1>(p.keys, rg.x, n, p.sorted_u, lane);
-        else if (n <= 128u) seg_sort_wave<2>(p.keys, rg.x, n, p.sorted_u, lane);
-        else if (n <= 256u) seg_sort_wave<4>(p.keys, rg.x, n, p.sorted_u, lane);
-        else seg_sort_wave<8>(p.keys, rg.x, n, p.sorted_u, lane);
+        unsigned long long *scratch = s_x + w * SB_WAVE_SCRATCH;
+        bool ok;
+        if (n <= 64u) ok = seg_sort_wave<1, P32>(p.keys, rg.x, n, p.sorted_u, lane, scratch);
+        else if (n <= 128u) ok = seg_sort_wave<2, P32>(p.keys, rg.x, n, p.sorted_u, lane, scratch);
+        else if (n <= 256u) ok = seg_sort_wave<4, P32>(p.keys, rg.x, n, p.sorted_u, lane, scratch);
+        else ok = seg_sort_wave<8, P32>(p.keys, rg.x, n, p.sorted_u, lane, scratch);
+        if (!ok && lane == 0) p.tie_list[atomicAdd(p.tie_cnt, 1u)] = tile;
     }
 }
 
-// Tiles above SEG_BLOCK_CAP instances (list 1), one workgroup each: sorted in LDS (dynamic, lds_keys keys)
-// when they fit, else in SEG_BLOCK_CAP-key chunks written to keys2 and placed by merge ranks searched in global
-// memory (the workgroup's own stores, ordered by a device-scope fence).
+// On the full 64-bit keys, one workgroup per tile: the tiles above SEG_BLOCK_CAP instances (list 1), then the
+// tiles seg_sort handed over after a proxy-key tie.  A short tie tile is sorted by wave 0 in registers; the
+// others in LDS (dynamic, lds_keys keys) when they fit, else in SEG_BLOCK_CAP-key chunks written to keys2 and
+// placed by merge ranks searched in global memory (the workgroup's own stores, ordered by a device-scope fence).
 __global__ __launch_bounds__(256) void seg_huge_kernel(SegSortParams p, uint32_t lds_keys) {
     extern __shared__ unsigned long long s_k[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t nh = p.long_cnt[1];
-    for (uint32_t h = blockIdx.x; h < nh; h += gridDim.x) {
-        const uint2 rg = p.ranges[p.long_list[p.T + 1 + h]];
+    const uint32_t nh = p.long_cnt[1], nt = *p.tie_cnt;
+    for (uint32_t h = blockIdx.x; h < nh + nt; h += gridDim.x) {
+        const uint32_t tile = h < nh ? p.long_list[p.T + 1 + h] : p.tie_list[h - nh];
+        const uint2 rg = p.ranges[tile];
         const uint32_t n = rg.y - rg.x;
+        if (n <= SEG_CAP) {  // workgroup-uniform; waves 1-3 go on to the next tile
+            if (w == 0) {
+                if (n <= 64u) seg_sort_wave<1, false>(p.keys, rg.x, n, p.sorted_u, lane, nullptr);
+                else if (n <= 128u) seg_sort_wave<2, false>(p.keys, rg.x, n, p.sorted_u, lane, nullptr);
+                else if (n <= 256u) seg_sort_wave<4, false>(p.keys, rg.x, n, p.sorted_u, lane, nullptr);
+                else seg_sort_wave<8, false>(p.keys, rg.x, n, p.sorted_u, lane, nullptr);
+            }
+            continue;
+        }
         if (n <= lds_keys) {
-            seg_lds_sort(p.keys, rg.x, n, p.sorted_u, nullptr, s_k, w, lane);
+            seg_lds_sort<false>(p.keys, rg.x, n, p.sorted_u, nullptr, s_k, w, lane, nullptr, 0u);
             continue;
         }
         for (uint32_t c0 = 0; c0 < n; c0 += SEG_BLOCK_CAP)
-            seg_lds_sort(p.keys, rg.x + c0, min(SEG_BLOCK_CAP, n - c0), nullptr, p.keys2, s_k, w, lane);
+            seg_lds_sort<false>(p.keys, rg.x + c0, min(SEG_BLOCK_CAP, n - c0), nullptr, p.keys2, s_k, w, lane,
+                                nullptr, 0u);
         __threadfence();
         __syncthreads();
         const unsigned long long *kk = p.keys2 + rg.x;
@@ -532,9 +748,13 @@ void launch_bucket_count(hipStream_t s, const BucketParams &p) {
 
 void launch_bucket_scatter(hipStream_t s, const BucketParams &p) { launch_walk<true>(s, p); }
 
-void launch_seg_sort(hipStream_t s, const SegSortParams &p) {
-    if (p.T == 0) return;
-    seg_sort_kernel<<<std::min(div_up(p.T, 4), (uint32_t)tuning("seg_grid", 1536)), 256, 0, s>>>(p);
+void launch_seg_sort(hipStream_t s, const SegSortParams &p0) {
+    if (p0.T == 0) return;
+    SegSortParams p = p0;
+    p.stamps = tuning("stamp", 0) ? stamp_buffer(2) : nullptr;
+    const uint32_t grid = std::min(div_up(p.T, 4), (uint32_t)tuning("seg_grid", 1536));
+    if (tuning("seg32", 1)) seg_sort_kernel<true><<<grid, 256, 0, s>>>(p);
+    else seg_sort_kernel<false><<<grid, 256, 0, s>>>(p);
     constexpr uint32_t HUGE_LDS_KEYS = 8192;  // 64 KB
     seg_huge_kernel<<<512, 256, HUGE_LDS_KEYS * sizeof(unsigned long long), s>>>(p, HUGE_LDS_KEYS);
 }

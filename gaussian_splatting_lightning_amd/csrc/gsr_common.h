@@ -24,7 +24,7 @@ constexpr int GRAD_ROW = 12;                   // floats per instance gradient r
 // counters block at the head of the geometry buffer (zeroed every forward)
 // counters: [CNT_BIG] big-Gaussian count, [CNT_OVERFLOW] scan overflow flag, then CNT_NPART 64-bit partial
 // sums of the instance total (spread over addresses so the per-block atomics do not serialise)
-enum Counter : int { CNT_BIG = 0, CNT_OVERFLOW = 2, CNT_SCAN_TICKET = 3, CNT_COL_TICKET = 4, CNT_LONG = 6, CNT_PARTIALS = 16, CNT_NPART = 64,
+enum Counter : int { CNT_BIG = 0, CNT_OVERFLOW = 2, CNT_SCAN_TICKET = 3, CNT_COL_TICKET = 4, CNT_LONG = 6, CNT_TIES = 8, CNT_PARTIALS = 16, CNT_NPART = 64,
                      CNT_WORDS = 16 + 2 * 64 };
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }
@@ -157,6 +157,7 @@ struct BinningState {
     unsigned long long *bk_keys2; // bucket path: R, chunk-sorted keys of tiles longer than SEG_BLOCK_CAP
     uint32_t *bk_hist;     // bucket path: BK_MAX_BLOCKS x T count matrix
     uint32_t *bk_tile_cnt, *bk_tile_start, *bk_long_list;
+    uint32_t *bk_tie_list;  // bucket path: tiles whose 32-bit proxy-key sort met a depth tie
 };
 constexpr uint32_t INV_NONE = 0xffffffffu;
 
@@ -180,6 +181,7 @@ inline size_t carve_binning(char *base, int64_t R, uint32_t num_tiles, BinningSt
     b.bk_tile_cnt = cb.take<uint32_t>((size_t)num_tiles + 1);
     b.bk_tile_start = cb.take<uint32_t>((size_t)num_tiles + 1);
     b.bk_long_list = cb.take<uint32_t>(2 * ((size_t)num_tiles + 1));
+    b.bk_tie_list = cb.take<uint32_t>((size_t)num_tiles + 1);
     c.off = cr.off > cb.off ? cr.off : cb.off;
     return c.off + 256;
 }

@@ -447,3 +447,22 @@ def test_beyond_lpt_and_bucket_tile_limits(gpu_device):
     hip = run_hip(inp, gpu_device, dc, di)
     run = compare_forward(inp, hip, run_oracle(inp))
     compare_backward(hip, run, dc, di, 1e-3)
+
+
+@pytest.mark.parametrize("bucket", [0, 1])
+def test_debug_mode_is_bitwise_identical(gpu_device, bucket):
+    """debug=True synchronises and checks after every stage (notes/rasterizer_note.h:44-53) on both binning
+    paths; outputs and gradients are those of the asynchronous run."""
+    from gaussian_splatting_lightning_amd import _native
+    inp = scene_inputs(20_000, 320, 240, sh_degree=2, seed=41)
+    dc, di = upstream(320, 240, 41)
+    try:
+        _native.set_tuning("bucket", bucket)
+        a = run_hip(inp, gpu_device, dc, di)
+        b = run_hip(inp, gpu_device, dc, di, debug=True)
+    finally:
+        _native.set_tuning("bucket", 1)
+    for k in ("color", "invdepth", "radii"):
+        assert np.array_equal(a[k], b[k]), k
+    for k in GRADS:
+        assert np.array_equal(a["grads"][k], b["grads"][k]), k
