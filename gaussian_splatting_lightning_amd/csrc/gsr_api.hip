@@ -310,13 +310,31 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     pp.block_sums = g.block_sums;
     GSR_STAGE(ST_PREPROCESS, dbg, launch_preprocess(stream, pp));
     // The instance total only needs the per-Gaussian tile counts, so it is read back right after the
-    // preprocess: the host waits on that copy while the GPU runs the depth sort and the ordered scan, and
-    // the binning launches are queued before the GPU drains (no idle gap at the only host sync).
+    // preprocess.  The bucket path's count pass needs no total either: whenever the tile count admits that
+    // path it is queued right behind the copy, so the GPU runs it while the host waits (its scratch is in the
+    // image buffer; if the total then selects the radix path, its results are simply unused).
     uint32_t *hw = pinned_words();
     hipEvent_t rb_ev = readback_event();
     if (!hw || !rb_ev) return fail(GSR_ERR_HIP, "pinned host buffer / event allocation failed");
     GSR_HIP(hipMemcpyAsync(hw, g.counters, CNT_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
     GSR_HIP(hipEventRecord(rb_ev, stream));
+    const int bk = tuning("bucket", 1);
+    const bool bk_possible = bk == 2 ? T <= BK_MAX_TILES : bk == 1 && T <= BK_MAX_TILES / 2;
+    const int lpt = tuning("lpt", 1);
+    BucketParams bp = {};
+    if (bk_possible) {
+        bp.P = (uint32_t)P; bp.T = T; bp.gx = gx; bp.nbig = g.counters + CNT_BIG;
+        bp.nb = std::max(1u, std::min({(uint32_t)tuning("bk_blocks", 256), BK_MAX_BLOCKS, div_up(P, 1024)}));
+        bp.gper = div_up(div_up(P, bp.nb), 256) * 256;  // whole preprocess blocks
+        bp.nb = div_up(P, bp.gper);
+        bp.tiles = g.tiles; bp.inst_start = g.inst_start; bp.block_sums = g.block_sums; bp.depth_key = g.depth_key;
+        bp.big_list = g.big_list; bp.exp_rec = g.exp_rec;
+        bp.hist = im.bk_hist; bp.tile_cnt = im.bk_tile_cnt; bp.tile_start = im.bk_tile_start; bp.ranges = im.ranges;
+        bp.tile_last = im.tile_last; bp.tile_loaded = im.tile_loaded;
+        bp.ticket = g.counters + CNT_COL_TICKET; bp.tile_status = g.tile_status; bp.err = g.counters + CNT_OVERFLOW;
+        bp.long_list = im.bk_long_list; bp.long_cnt = g.counters + CNT_LONG;
+        GSR_STAGE(ST_BK_COUNT, dbg, launch_bucket_count(stream, bp));
+    }
     GSR_STAGE(ST_READBACK, dbg, GSR_HIP(hipEventSynchronize(rb_ev)));
     uint64_t total64 = 0;
     for (int k = 0; k < CNT_NPART; k++) {
@@ -333,9 +351,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     // the tiles are short (per-tile sorts cost n log^2 n): at 1M Gaussians / 1080p (517 instances per tile) it
     // takes 0.20 ms against the radix path's 0.30; at 5M / 4K stress (1240 per tile) 4.4 ms against 1.4.
     // Otherwise the radix path: depth sort, depth-ordered expansion, stable tile sort.
-    const int bk = tuning("bucket", 1);
-    const bool bucket = bk == 2 ? T <= BK_MAX_TILES
-                                : bk == 1 && T <= BK_MAX_TILES / 2 && (uint64_t)R <= (uint64_t)BK_MAX_MEAN * T;
+    const bool bucket = bk_possible && (bk == 2 || (uint64_t)R <= (uint64_t)BK_MAX_MEAN * T);
     if (!bucket) {
         GSR_STAGE(ST_DEPTH_SORT, dbg, launch_radix_sort(stream, g.sort, (uint32_t)P, 32, false, g.depth_key));
         if (tuning("scan_lookback", 1))
@@ -354,30 +370,19 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     carve_binning(bin, R, T, b);
     if ((uint64_t)RS_BINS * div_up(R ? R : 1, RS_TILE) + 1 > (uint64_t)SCAN_TILE * SCAN_MAX_BLOCKS)
         return fail(GSR_ERR_OVERFLOW, "too many tile instances for the single-level scan");
-    const int lpt = tuning("lpt", 1);
     if (bucket) {
         if (R > 0) {
-            BucketParams bp;
-            bp.P = (uint32_t)P; bp.T = T; bp.gx = gx; bp.nbig = nbig;
-            bp.nb = std::max(1u, std::min({(uint32_t)tuning("bk_blocks", 256), BK_MAX_BLOCKS, div_up(P, 1024)}));
-            bp.gper = div_up(div_up(P, bp.nb), 256) * 256;  // whole preprocess blocks
-            bp.nb = div_up(P, bp.gper);
-            bp.tiles = g.tiles; bp.inst_start = g.inst_start; bp.block_sums = g.block_sums; bp.depth_key = g.depth_key; bp.big_list = g.big_list;
-            bp.exp_rec = g.exp_rec;
-            bp.hist = b.bk_hist; bp.tile_cnt = b.bk_tile_cnt; bp.tile_start = b.bk_tile_start; bp.ranges = im.ranges;
-            bp.tile_last = im.tile_last; bp.tile_loaded = im.tile_loaded;
-            bp.ticket = g.counters + CNT_COL_TICKET; bp.tile_status = g.tile_status; bp.err = g.counters + CNT_OVERFLOW;
-            bp.long_list = b.bk_long_list; bp.long_cnt = g.counters + CNT_LONG; bp.keys = b.bk_keys; bp.inst_gid = b.inst_gid; bp.inv = b.inv;
-            GSR_STAGE(ST_BK_COUNT, dbg, launch_bucket_count(stream, bp));
-            GSR_STAGE(ST_BK_SCATTER, dbg, launch_bucket_scatter(stream, bp));
-            if (lpt) launch_tile_order(stream, im.ranges, nullptr, 0, (int)T, im.order_fwd);
+            bp.keys = b.bk_keys; bp.inst_gid = b.inst_gid; bp.inv = b.inv;
+            bp.order = lpt ? im.order_fwd : nullptr;
+            bp.lpt_shift = tuning("lpt_shift", 3);
+            GSR_STAGE(ST_BK_SCATTER, dbg, launch_bucket_scatter(stream, bp));  // and the forward LPT order
             SegSortParams sp;
             // the long tiles lead the LPT order only while SEG_CAP + 1 is a multiple of the bucket width
             sp.T = T; sp.ranges = im.ranges;
             sp.tile_order = (lpt && (((SEG_CAP + 1) >> tuning("lpt_shift", 3)) << tuning("lpt_shift", 3)) == SEG_CAP + 1)
                                 ? im.order_fwd : nullptr; sp.keys = b.bk_keys; sp.keys2 = b.bk_keys2;
-            sp.sorted_u = b.sorted_u; sp.long_list = b.bk_long_list; sp.long_cnt = g.counters + CNT_LONG;
-            sp.tie_list = b.bk_tie_list; sp.tie_cnt = g.counters + CNT_TIES;
+            sp.sorted_u = b.sorted_u; sp.long_list = im.bk_long_list; sp.long_cnt = g.counters + CNT_LONG;
+            sp.tie_list = im.bk_tie_list; sp.tie_cnt = g.counters + CNT_TIES;
             GSR_STAGE(ST_SEG_SORT, dbg, launch_seg_sort(stream, sp));
         } else {
             GSR_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * T, stream));

@@ -109,6 +109,10 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
     __shared__ int s_own[BKW][64];        // lane whose cell run starts at this pair of the step, else -1
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const uint32_t b = blockIdx.x, T = p.T, gx = (uint32_t)p.gx;
+    if (SCATTER && b == p.nb) {  // the extra workgroup: the forward LPT order (the column pass wrote the ranges)
+        lpt_order_block(p.ranges, nullptr, 0, (int)T, p.lpt_shift, p.order, reinterpret_cast<uint32_t *>(&s_own[0][0]));
+        return;
+    }
     if (SCATTER) {
         const uint32_t *hrow = p.hist + (size_t)b * T;
         for (uint32_t t = tid; t < T; t += 64 * BKW) s_tab[t] = p.tile_start[t] + hrow[t];
@@ -182,7 +186,8 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
         }
         wave_lds_sync();
     }
-    for (uint32_t bi = b; bi < p.nbig; bi += p.nb) {
+    const uint32_t nbig = *p.nbig;
+    for (uint32_t bi = b; bi < nbig; bi += p.nb) {
         const uint32_t gb = p.big_list[bi];
         const uint4 e = p.exp_rec[gb];
         const uint32_t area = p.tiles[gb];
@@ -726,27 +731,28 @@ __global__ __launch_bounds__(256) void seg_huge_kernel(SegSortParams p, uint32_t
 // ------------------------------------------------------------------------------------------------
 // 16 waves per workgroup, or 8 when the tile counters leave too little LDS for 16 waves' staging.
 template <bool SCATTER>
-static void launch_walk(hipStream_t s, const BucketParams &p) {
+static void launch_walk(hipStream_t s, const BucketParams &p, uint32_t grid) {
     const size_t lds = sizeof(uint32_t) * p.T;
     if (lds + 40 * 1024 <= 160 * 1024) {
         if (lds > 65536)
             (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&bk_walk_kernel<SCATTER, 16>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        bk_walk_kernel<SCATTER, 16><<<p.nb, 64 * 16, lds, s>>>(p);
+        bk_walk_kernel<SCATTER, 16><<<grid, 64 * 16, lds, s>>>(p);
     } else {
         if (lds > 65536)
             (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&bk_walk_kernel<SCATTER, 8>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        bk_walk_kernel<SCATTER, 8><<<p.nb, 64 * 8, lds, s>>>(p);
+        bk_walk_kernel<SCATTER, 8><<<grid, 64 * 8, lds, s>>>(p);
     }
 }
 
 void launch_bucket_count(hipStream_t s, const BucketParams &p) {
-    launch_walk<false>(s, p);
+    launch_walk<false>(s, p, p.nb);
     bk_columns_kernel<<<div_up(p.T, 64), 256, 0, s>>>(p);
 }
 
-void launch_bucket_scatter(hipStream_t s, const BucketParams &p) { launch_walk<true>(s, p); }
+// plus one workgroup for the forward LPT order when p.order is set
+void launch_bucket_scatter(hipStream_t s, const BucketParams &p) { launch_walk<true>(s, p, p.nb + (p.order ? 1u : 0u)); }
 
 void launch_seg_sort(hipStream_t s, const SegSortParams &p0) {
     if (p0.T == 0) return;

@@ -155,9 +155,6 @@ struct BinningState {
     SortScratch sort;      // radix path: tile sort (R keys); its final value buffer is sorted_u
     unsigned long long *bk_keys;  // bucket path: R keys (depth << 32 | u) bucketed by tile
     unsigned long long *bk_keys2; // bucket path: R, chunk-sorted keys of tiles longer than SEG_BLOCK_CAP
-    uint32_t *bk_hist;     // bucket path: BK_MAX_BLOCKS x T count matrix
-    uint32_t *bk_tile_cnt, *bk_tile_start, *bk_long_list;
-    uint32_t *bk_tie_list;  // bucket path: tiles whose 32-bit proxy-key sort met a depth tie
 };
 constexpr uint32_t INV_NONE = 0xffffffffu;
 
@@ -177,11 +174,6 @@ inline size_t carve_binning(char *base, int64_t R, uint32_t num_tiles, BinningSt
     Carver cb = c;  // bucket view
     b.bk_keys = cb.take<unsigned long long>(n ? n : 1);
     b.bk_keys2 = cb.take<unsigned long long>(n ? n : 1);
-    b.bk_hist = cb.take<uint32_t>((size_t)BK_MAX_BLOCKS * num_tiles + 1);
-    b.bk_tile_cnt = cb.take<uint32_t>((size_t)num_tiles + 1);
-    b.bk_tile_start = cb.take<uint32_t>((size_t)num_tiles + 1);
-    b.bk_long_list = cb.take<uint32_t>(2 * ((size_t)num_tiles + 1));
-    b.bk_tie_list = cb.take<uint32_t>((size_t)num_tiles + 1);
     c.off = cr.off > cb.off ? cr.off : cb.off;
     return c.off + 256;
 }
@@ -194,6 +186,13 @@ struct ImageState {
     uint32_t *tile_loaded; // T: instances of the tile the forward composite gathered (>= tile_last)
     uint32_t *order_fwd;   // tiles in descending forward work (instances in range), LPT launch order
     uint32_t *order_bwd;   // tiles in descending backward work (tile_last)
+    // bucket path count-pass scratch (gsr_bin.hip), here rather than in the binning buffer so that the pass
+    // can run before the instance total (the binning buffer's size) reaches the host
+    uint32_t *bk_hist;       // BK_MAX_BLOCKS x T count matrix (empty above BK_MAX_TILES)
+    uint32_t *bk_tile_cnt;   // T
+    uint32_t *bk_tile_start; // T + 1
+    uint32_t *bk_long_list;  // 2 x (T + 1): tiles of (SEG_CAP, SEG_BLOCK_CAP] instances, longer tiles
+    uint32_t *bk_tie_list;   // T + 1: tiles whose 32-bit proxy-key sort did not converge
 };
 
 inline size_t carve_image(char *base, int W, int H, ImageState &im) {
@@ -207,6 +206,12 @@ inline size_t carve_image(char *base, int W, int H, ImageState &im) {
     im.tile_loaded = c.take<uint32_t>((size_t)gx * gy + 1);
     im.order_fwd = c.take<uint32_t>((size_t)gx * gy + 1);
     im.order_bwd = c.take<uint32_t>((size_t)gx * gy + 1);
+    const size_t nt = (size_t)gx * gy;
+    im.bk_hist = c.take<uint32_t>((nt <= BK_MAX_TILES ? (size_t)BK_MAX_BLOCKS * nt : 0) + 1);
+    im.bk_tile_cnt = c.take<uint32_t>(nt + 1);
+    im.bk_tile_start = c.take<uint32_t>(nt + 1);
+    im.bk_long_list = c.take<uint32_t>(2 * (nt + 1));
+    im.bk_tie_list = c.take<uint32_t>(nt + 1);
     return c.off + 256;
 }
 
@@ -539,7 +544,6 @@ __device__ __forceinline__ uint64_t wave_lookback(uint64_t *status, uint32_t bid
     return excl;
 }
 
-// Orders LDS writes before later LDS reads of other lanes of the SAME wave (no s_barrier).
 // LPT launch order puts the heaviest tiles in the first slots; with prio_div > 0 their waves also win VALU
 // issue arbitration against the lighter waves sharing their SIMD (s_setprio takes an immediate).
 __device__ __forceinline__ void set_slot_priority(int slot, int prio_div) {
@@ -560,10 +564,40 @@ __device__ __forceinline__ void stamp_store(uint4 *stamps, int slot, uint32_t t0
     stamps[slot] = make_uint4(t0, t1, hw, xcc);
 }
 
+// Orders LDS writes before later LDS reads of other lanes of the SAME wave (no s_barrier).
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// LPT (longest-processing-time-first) tile order by one workgroup of any multiple of 64 threads: histogram of the
+// tile weights (range length, or tile_last when use_last) in 2^shift-instance buckets, heaviest first, exclusive
+// scan by one wave, scatter.  Order inside a bucket is arbitrary -- it only changes which tile runs when, never
+// a result.  hist: 256 words of LDS.  Run by tile_order_kernel and by the bucket scatter's extra workgroup.
+__device__ __forceinline__ void lpt_order_block(const uint2 *__restrict__ ranges, const uint32_t *__restrict__ tile_last,
+                                                int use_last, int T, int shift, uint32_t *__restrict__ order,
+                                                uint32_t *hist) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    auto bucket = [&](int t) -> uint32_t {
+        const uint32_t w = use_last ? tile_last[t] : ranges[t].y - ranges[t].x;
+        return 255u - min(255u, w >> shift);  // heaviest first
+    };
+    for (int k = tid; k < 256; k += nt) hist[k] = 0;
+    __syncthreads();
+    for (int t = tid; t < T; t += nt) atomicAdd(&hist[bucket(t)], 1u);
+    __syncthreads();
+    if (tid < 64) {  // exclusive scan of the 256 buckets by one wave, 4 per lane
+        const uint32_t a = hist[4 * tid], b = hist[4 * tid + 1], c = hist[4 * tid + 2], d = hist[4 * tid + 3];
+        const uint32_t sum = a + b + c + d;
+        const uint32_t excl = wave_inclusive_scan(sum, tid) - sum;
+        hist[4 * tid] = excl;
+        hist[4 * tid + 1] = excl + a;
+        hist[4 * tid + 2] = excl + a + b;
+        hist[4 * tid + 3] = excl + a + b + c;
+    }
+    __syncthreads();
+    for (int t = tid; t < T; t += nt) order[atomicAdd(&hist[bucket(t)], 1u)] = (uint32_t)t;
 }
 
 #endif  // __HIPCC__

@@ -317,26 +317,7 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint2 *__restric
                                                              const uint32_t *__restrict__ tile_last, int use_last,
                                                              int T, int shift, uint32_t *__restrict__ order) {
     __shared__ uint32_t hist[256];
-    const int tid = threadIdx.x;
-    if (tid < 256) hist[tid] = 0;
-    __syncthreads();
-    auto bucket = [&](int t) -> uint32_t {
-        const uint32_t w = use_last ? tile_last[t] : ranges[t].y - ranges[t].x;
-        return 255u - min(255u, w >> shift);  // heaviest first
-    };
-    for (int t = tid; t < T; t += 1024) atomicAdd(&hist[bucket(t)], 1u);
-    __syncthreads();
-    if (tid < 64) {  // exclusive scan of the 256 buckets by one wave, 4 per lane
-        const uint32_t a = hist[4 * tid], b = hist[4 * tid + 1], c = hist[4 * tid + 2], d = hist[4 * tid + 3];
-        const uint32_t sum = a + b + c + d;
-        const uint32_t excl = wave_inclusive_scan(sum, tid) - sum;
-        hist[4 * tid] = excl;
-        hist[4 * tid + 1] = excl + a;
-        hist[4 * tid + 2] = excl + a + b;
-        hist[4 * tid + 3] = excl + a + b + c;
-    }
-    __syncthreads();
-    for (int t = tid; t < T; t += 1024) order[atomicAdd(&hist[bucket(t)], 1u)] = (uint32_t)t;
+    lpt_order_block(ranges, tile_last, use_last, T, shift, order, hist);
 }
 
 void launch_tile_order(hipStream_t s, const uint2 *ranges, const uint32_t *tile_last, int use_last, int T,

@@ -58,7 +58,8 @@ void launch_identify_ranges(hipStream_t s, const uint32_t *keys_sorted, uint32_t
 
 // ---- bucket binning (gsr_bin.hip) ----
 struct BucketParams {
-    uint32_t P, T, nb, gper, nbig;  // Gaussians, tiles, walk blocks, Gaussians per block, big Gaussians
+    uint32_t P, T, nb, gper;  // Gaussians, tiles, walk blocks, Gaussians per block
+    const uint32_t *nbig;     // big-Gaussian count (device word written by the preprocess)
     int gx;
     const uint32_t *tiles, *depth_key, *big_list;
     const uint32_t *block_sums;  // preprocess block totals (256 Gaussians each)
@@ -77,6 +78,8 @@ struct BucketParams {
     unsigned long long *keys;  // R: depth << 32 | u, bucketed by tile
     uint32_t *inst_gid;    // R
     uint32_t *inv;         // R: reset to INV_NONE by the scatter (the forward composite fills it)
+    uint32_t *order;       // scatter: an extra workgroup writes the forward LPT order here (or null: none)
+    int lpt_shift;
 };
 void launch_bucket_count(hipStream_t s, const BucketParams &p);    // walk + column prefixes + tile ranges
 void launch_bucket_scatter(hipStream_t s, const BucketParams &p);

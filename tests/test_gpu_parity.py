@@ -417,6 +417,30 @@ def test_long_tiles_and_depth_ties(gpu_device, n, W, H):
     compare_backward(hip, run, dc, di, 1e-3)
 
 
+def test_dense_tiles_fall_back_to_radix_after_speculative_count(gpu_device):
+    """Default path choice on tiles averaging more than 1024 instances: the bucket count pass has already run
+    (it is queued before the instance total is known), then the total selects the radix path, whose outputs must
+    not depend on what the count pass left behind."""
+    from gaussian_splatting_lightning_amd import _native
+    W, H = 96, 64
+    inp = scene_inputs(60_000, W, H, sh_degree=1, seed=29)
+    dc, di = upstream(W, H, 29)
+    hip = run_hip(inp, gpu_device, dc, di)
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+    assert hip["state"].num_rendered > 1024 * T  # the radix path was chosen
+    run = compare_forward(inp, hip, run_oracle(inp))
+    compare_backward(hip, run, dc, di, 1e-3)
+    try:
+        _native.set_tuning("bucket", 2)
+        forced = run_hip(inp, gpu_device, dc, di)
+    finally:
+        _native.set_tuning("bucket", 1)
+    for k in ("color", "invdepth", "radii"):
+        assert np.array_equal(hip[k], forced[k]), k
+    for k in GRADS:
+        assert np.array_equal(hip["grads"][k], forced["grads"][k]), k
+
+
 @pytest.mark.parametrize("W,H", [(1280, 720), (96, 64)])
 def test_binning_paths_are_bitwise_identical(gpu_device, W, H):
     """The bucket binning (per-tile sorts) and the radix binning (depth sort + stable tile sort) produce the
