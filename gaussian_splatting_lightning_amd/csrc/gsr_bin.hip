@@ -10,13 +10,14 @@
 //   4. bk_scatter  the same walk again: each instance takes the next free slot of its tile's bucket
 //                  (LDS counters seeded from the prefixes) and stores key = depth bits << 32 | u, where u is
 //                  its Gaussian-major expansion index (u increases with the Gaussian index);
-//   5. seg_sort    one wave per tile sorts the bucket by key in registers (bitonic network, 64-bit keys)
-//                  and writes the expansion index of every sorted position.  Keys are unique inside a tile
-//                  (one instance per Gaussian), so the order inside a bucket after step 4 does not matter
-//                  and the result is exactly the reference's (tile, depth, index) order.  Tiles above
-//                  SEG_CAP instances are sorted by a whole workgroup (seg_block: four waves' registers, the
-//                  cross-wave stages through LDS); tiles above SEG_BLOCK_CAP in SEG_BLOCK_CAP-key chunks that
-//                  seg_huge sorts (in LDS up to 8192 keys, else in chunks placed by merge ranks) (binary search of every key in the other chunks).
+//   5. seg_sort    one wave per tile sorts the bucket by key in registers (bitonic network on 32-bit proxy
+//                  keys, ties repaired on the full keys) and writes the expansion index of every sorted
+//                  position.  Keys are unique inside a tile (one instance per Gaussian), so the order inside
+//                  a bucket after step 4 does not matter and the result is exactly the reference's (tile,
+//                  depth, index) order.  Tiles above SEG_CAP instances are sorted by a whole workgroup (four
+//                  waves sort 512-key chunks, then merge ranks through LDS); tiles above SEG_BLOCK_CAP, and
+//                  tiles whose ties did not resolve, by seg_huge on the 64-bit keys (in LDS up to 8192
+//                  keys, else in chunks placed by merge ranks).
 // Everything is integer work; nothing depends on scheduling, so the result is deterministic.
 #include <algorithm>
 
