@@ -465,8 +465,10 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
         rp.W = W; rp.H = H; rp.gx = gx; rp.gy = gy; rp.num_tiles = (int)T;
         rp.ranges = im.ranges; rp.point_list = b.point_list; rp.n_contrib = im.n_contrib;
         const int lpt = tuning("lpt", 1);
-        if (lpt) launch_tile_order(stream, im.ranges, im.tile_last, 1, (int)T, im.order_bwd);
-        rp.tile_order = lpt ? im.order_bwd : nullptr;
+        // "bwd_order" 0: reuse the forward's order (range lengths) and skip the tile_last ordering launch
+        const bool own_order = lpt && tuning("bwd_order", 1);
+        if (own_order) launch_tile_order(stream, im.ranges, im.tile_last, 1, (int)T, im.order_bwd);
+        rp.tile_order = lpt ? (own_order ? im.order_bwd : im.order_fwd) : nullptr;
         rp.tile_last = im.tile_last; rp.tile_loaded = im.tile_loaded;
         rp.rec_a = g.rec_a; rp.rec_b = g.rec_b; rp.rec_c = g.rec_c;
         rp.bg = a->background; rp.final_T = im.final_T; rp.dL_dpix = a->dL_dpix; rp.dL_dinvdepth = a->dL_dinvdepth;
