@@ -477,7 +477,7 @@ __device__ __forceinline__ void composite_fwd(const RenderFwdParams &p, const in
     const int py0 = ty * BLOCK_Y + (lane >> 4);
     const float pfx = (float)px, pfy0 = (float)py0;
     const float row0 = (float)(ty * BLOCK_Y);
-    const int kbase = NPIX == 4 ? 0 : 2 * half;  // whole-tile pixel index of this wave's first pixel
+    const int kbase = NPIX == 4 ? 0 : NPIX * half;  // whole-tile pixel index of this wave's first pixel
     // A pixel is live while T > 0: a pixel that stops (or lies outside the image) keeps -T, so the live test
     // is one compare per pixel instead of a boolean carried in a register.
     float T[NPIX], C0[NPIX], C1[NPIX], C2[NPIX], ID[NPIX];
@@ -631,8 +631,44 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_split_kernel(Render
     stamp_store(p.stamps, slot, t_start, lane);
 }
 
+// Every tile in 4 / NPIX parts (row strips {NPIX * part .. NPIX * part + NPIX - 1} of each lane's column), one
+// wave each, consecutive slots: 2 or 4 times the waves of whole tiles, each with fewer registers, so the SIMDs
+// stay fuller to the end of the launch.  Parts combine tile_last / tile_loaded with atomicMax on zeroed words.
+template <int NPIX, int MIN_WAVES>
+__global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_part_kernel(RenderFwdParams p) {
+    __shared__ float4 s_a[4][64];
+    __shared__ float4 s_b[4][64];
+    __shared__ float2 s_c[4][64];
+    __shared__ uint32_t s_m[4][64];
+    constexpr int PARTS = 4 / NPIX;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int slot = blockIdx.x * 4 + w;
+    if (slot >= p.num_tiles * PARTS) return;
+    const uint32_t t_start = p.stamps ? stamp_now() : 0u;
+    const int tile = p.tile_order ? (int)p.tile_order[slot / PARTS] : slot / PARTS;
+    composite_fwd<NPIX, false, false>(p, tile, slot % PARTS, lane, s_a[w], s_b[w], s_c[w], s_m[w]);
+    stamp_store(p.stamps, slot, t_start, lane);
+}
+
 void launch_render_fwd(hipStream_t s, const RenderFwdParams &p) {
     if (p.num_tiles <= 0) return;
+    // "fwd_parts" 1, 2 or 4; 0 (default): 4 or 2 when that many part-waves still fit the GPU's ~8 resident waves
+    // per SIMD, twice over (small images, where one heavy tile's latency sets the kernel time), else whole tiles with
+    // only the heaviest split in two
+    int parts = tuning("fwd_parts", 0);
+    if (parts == 0) parts = p.num_tiles * 4 <= tuning("fwd_part_slots", 16384) ? 4
+                            : p.num_tiles * 2 <= tuning("fwd_part_slots", 16384) ? 2 : 1;
+    if (parts == 2 || parts == 4) {
+        RenderFwdParams q = p;
+        q.stamps = tuning("stamp", 0) ? stamp_buffer(0) : nullptr;
+        const dim3 grid(div_up(p.num_tiles * parts, 4)), block(256);
+        const int mw = tuning("fwd_part_waves", 8);
+        if (parts == 2 && mw >= 8) render_fwd_part_kernel<2, 8><<<grid, block, 0, s>>>(q);
+        else if (parts == 2) render_fwd_part_kernel<2, 4><<<grid, block, 0, s>>>(q);
+        else if (mw >= 8) render_fwd_part_kernel<1, 8><<<grid, block, 0, s>>>(q);
+        else render_fwd_part_kernel<1, 4><<<grid, block, 0, s>>>(q);
+        return;
+    }
     const dim3 grid(div_up(p.num_tiles, 4)), block(256);
     const int nsplit = p.tile_order ? (int)((int64_t)p.num_tiles * tuning("fwd_split_pct", 5) / 100) : 0;
     if (nsplit > 0) {

@@ -365,13 +365,14 @@ def test_densify_stats_from_backward(gpu_device):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knobs", [{"fwd_strip": 1}, {"bwd_strip": 0}, {"bwd_pred": 0}, {"bwd_pred": 1}, {"bwd_v": 3},
-                                   {"bwd_pair": 0}])
+@pytest.mark.parametrize("knobs", [{"fwd_strip": 1, "fwd_parts": 1}, {"fwd_parts": 2}, {"bwd_strip": 0},
+                                   {"bwd_pred": 0}, {"bwd_pred": 1}, {"bwd_v": 3}, {"bwd_pair": 0}])
 def test_composite_variants_are_bitwise_identical(gpu_device, knobs):
     """Strip skipping only skips rows where every pixel fails alpha >= 1/255, and the predicated backward
-    body performs the same operations as the branchy one: outputs and gradients must match bit for bit
-    (including a non-zero background and a 5 % share of split heavy tiles).  The v3 backward keeps the
-    per-channel accumulators: gradients agree to rounding only."""
+    body performs the same operations as the branchy one, and a tile composited in 4 or 2 row-strip parts
+    (the default at this size) or whole (with a 5 % share of split heavy tiles) gives the same pixels and
+    contributor counts: outputs and gradients must match bit for bit (with a non-zero background).  The v3
+    backward keeps the per-channel accumulators: gradients agree to rounding only."""
     from gaussian_splatting_lightning_amd import _native
     inp = scene_inputs(200_000, 1280, 720, sh_degree=3, seed=4, bg=(0.3, 0.6, 0.9))
     dc, di = upstream(1280, 720, 4)
@@ -382,7 +383,8 @@ def test_composite_variants_are_bitwise_identical(gpu_device, knobs):
         alt = run_hip(inp, gpu_device, dc, di)
     finally:
         for k in knobs:
-            _native.set_tuning(k, {"fwd_strip": 0, "bwd_strip": 1, "bwd_pred": 2, "bwd_v": 4, "bwd_pair": 1}[k])
+            _native.set_tuning(k, {"fwd_strip": 0, "fwd_parts": 0, "bwd_strip": 1, "bwd_pred": 2, "bwd_v": 4,
+                                   "bwd_pair": 1}[k])
     for k in ("color", "invdepth", "radii"):
         assert np.array_equal(ref[k], alt[k]), k
     for k in GRADS:
