@@ -481,6 +481,170 @@ __global__ __launch_bounds__(64, MIN_WAVES) void render_bwd_v4_kernel(RenderBwdP
     stamp_store(p.stamps, slot, t_start, lane);
 }
 
+// Parts variant for small images: PARTS waves of one workgroup share one tile, wave w compositing the lane's
+// pixels of row strips [w NP, w NP + NP) (NP = 4 / PARTS).  With few tiles (800x800: 2500 tiles for 1024
+// SIMDs) one heavy tile's serial walk sets the kernel time; splitting its pixels shortens that walk.  Per batch
+// of BWD_BATCH instances: wave 0 stages the records, every wave reduces its own per-instance sums into its
+// s_part plane, and after a barrier wave 0 adds the planes in part order and writes the gradient row.  The
+// per-instance reductions are repeated PARTS times, so it pays only where latency, not issue, is the limit.
+template <bool HAS_INV, int PARTS>
+__global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdParams p) {
+    constexpr int NP = PIX_PER_LANE / PARTS;
+    __shared__ float4 s_a[BWD_BATCH];
+    __shared__ float4 s_b[BWD_BATCH];
+    __shared__ float2 s_c[BWD_BATCH];
+    __shared__ uint32_t s_m[BWD_BATCH];
+    __shared__ __attribute__((aligned(16))) float s_part[PARTS][BWD_BATCH][PART];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int slot = blockIdx.x;
+    const int tile = p.tile_order ? (int)p.tile_order[slot] : slot;
+    const int tx = tile % p.gx, ty = tile / p.gx;
+    const int px = tx * BLOCK_X + (lane & 15);
+    const int py0 = ty * BLOCK_Y + (lane >> 4);
+    const float pfx = (float)px;
+    const float row0 = (float)(ty * BLOCK_Y);
+    const uint2 range = p.ranges[tile];
+    const uint32_t tl = p.tile_last[tile];
+    const uint32_t loaded = p.tile_loaded[tile];
+    for (uint32_t s = range.x + tl + threadIdx.x; s < range.x + loaded; s += 64 * PARTS) {
+        const float z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        store_row(p.rows, p.rows_by_u ? p.sorted_u[s] : s, z);
+    }
+    if (tl == 0) return;  // workgroup-uniform
+
+    const int kbase = w * NP;
+    const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
+    const size_t HW = (size_t)p.W * p.H;
+    float T[NP], dp0[NP], dp1[NP], dp2[NP], dinv[NP], D[NP];
+    uint32_t lastc[NP];
+    const float pfy0 = (float)py0;
+#pragma unroll
+    for (int k = 0; k < NP; k++) {
+        const int py = py0 + 4 * (kbase + k);
+        const bool inside = px < p.W && py < p.H;
+        const size_t pid = inside ? (size_t)py * p.W + px : 0;
+        T[k] = inside ? p.final_T[pid] : 0.f;
+        lastc[k] = inside ? p.n_contrib[pid] : 0u;
+        dp0[k] = inside ? p.dL_dpix[pid] : 0.f;
+        dp1[k] = inside ? p.dL_dpix[HW + pid] : 0.f;
+        dp2[k] = inside ? p.dL_dpix[2 * HW + pid] : 0.f;
+        dinv[k] = (HAS_INV && inside) ? p.dL_dinvdepth[pid] : 0.f;
+        D[k] = fmaf(bg2, dp2[k], fmaf(bg1, dp1[k], bg0 * dp0[k]));
+    }
+    const float hW = 0.5f * p.W, hH = 0.5f * p.H;
+
+    for (int bend = (int)tl; bend > 0; bend -= BWD_BATCH) {
+        const int cnt = min(BWD_BATCH, bend);
+        float4 my_a = make_float4(0, 0, 0, 0), my_b = my_a;
+        uint32_t my_row = 0;
+        if (w == 0 && lane < cnt) {
+            const uint32_t s_me = range.x + (uint32_t)(bend - 1 - lane);
+            my_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
+            const uint32_t gid = p.point_list[s_me];
+            my_a = p.rec_a[gid];
+            my_b = p.rec_b[gid];
+            s_a[lane] = stage_rec_a(my_a);
+            s_b[lane] = stage_rec_b(my_b);
+            s_c[lane] = p.rec_c[gid];
+            s_m[lane] = strip_mask(my_a, my_b, row0);
+        }
+        __syncthreads();
+        // strip k of instance j is live iff bit j of sk[k] (wave-uniform)
+        const uint32_t mm = lane < cnt ? s_m[lane] : 0u;
+        uint64_t sk[NP];
+#pragma unroll
+        for (int k = 0; k < NP; k++) sk[k] = __ballot((mm >> (kbase + k)) & 1u);
+        auto pass = [&](const int j, float m[10]) -> bool {
+            const uint32_t idx = (uint32_t)(bend - 1 - j);
+            const float4 a = s_a[j], b = s_b[j];  // a: x, y, A, B; b: C, o, r, g
+            const float2 c = s_c[j];              // b, 1/depth
+            const float dx = a.x - pfx, dy0 = a.y - pfy0;
+            const float P0 = (a.z * dx) * dx, L = a.w * dx;
+            float Q0 = 0.f, Q1 = 0.f, Q2 = 0.f, w0 = 0.f, w1 = 0.f, w2 = 0.f, w3 = 0.f;
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < NP; k++) {
+                if (!((sk[k] >> j) & 1u)) continue;  // wave-uniform
+                const float dy = dy0 - (float)(4 * (kbase + k));
+                const float power2 = power2_at(b.x, dy, P0, L);
+                const float G = __builtin_amdgcn_exp2f(power2);
+                const float alpha = fminf(0.99f, b.y * G);
+                if (!(idx < lastc[k] && !(power2 > 0.0f) && !(alpha < 1.0f / 255.0f))) continue;
+                any = true;
+                T[k] = T[k] * fast_rcp(1.f - alpha);
+                const float wgt = alpha * T[k];
+                float cd = fmaf(c.x, dp2[k], fmaf(b.w, dp1[k], b.z * dp0[k]));
+                if (HAS_INV) cd = fmaf(c.y, dinv[k], cd);
+                const float d = cd - D[k];
+                D[k] = fmaf(alpha, d, D[k]);
+                w0 = fmaf(wgt, dp0[k], w0);
+                w1 = fmaf(wgt, dp1[k], w1);
+                w2 = fmaf(wgt, dp2[k], w2);
+                if (HAS_INV) w3 = fmaf(wgt, dinv[k], w3);
+                const float q = G * (d * T[k]);
+                const float qdy = q * dy;
+                Q0 += q;
+                Q1 += qdy;
+                Q2 = fmaf(qdy, dy, Q2);
+            }
+            m[0] = Q0;
+            m[1] = Q0 * dx;
+            m[2] = Q1;
+            m[3] = m[1] * dx;
+            m[4] = Q1 * dx;
+            m[5] = Q2;
+            m[6] = w0;
+            m[7] = w1;
+            m[8] = w2;
+            m[9] = w3;
+            return any;
+        };
+        for (int j = 0; j < cnt; j += 2) {
+            float m0[10];
+            const bool any0 = pass(j, m0);
+            float *dst = s_part[w][j];
+            if (j + 1 < cnt) {
+                float m1[10];
+                const bool any1 = pass(j + 1, m1);
+                if (__ballot(any0 || any1)) {
+                    wave_reduce20_store(m0, m1, dst, lane);
+                } else if (lane < 10) {
+                    dst[lane] = 0.f;
+                    dst[PART + lane] = 0.f;
+                }
+            } else if (__ballot(any0)) {
+                wave_reduce10_store(m0, dst, lane);
+            } else if (lane < 10) {
+                dst[lane] = 0.f;
+            }
+        }
+        __syncthreads();
+        if (w == 0 && lane < cnt) {
+            float u[10];
+#pragma unroll
+            for (int v = 0; v < 10; v++) u[v] = s_part[0][lane][v];
+#pragma unroll
+            for (int q = 1; q < PARTS; q++)
+#pragma unroll
+                for (int v = 0; v < 10; v++) u[v] += s_part[q][lane][v];
+            const float o = my_b.y, ca = my_a.z, cb = my_a.w, cc = my_b.x;
+            float row[10];
+            row[0] = -o * hW * (ca * u[1] + cb * u[2]);
+            row[1] = -o * hH * (cb * u[1] + cc * u[2]);
+            row[2] = -0.5f * o * u[3];
+            row[3] = -0.5f * o * u[4];
+            row[4] = -0.5f * o * u[5];
+            row[5] = u[0];
+            row[6] = u[6];
+            row[7] = u[7];
+            row[8] = u[8];
+            row[9] = u[9];
+            store_row(p.rows, my_row, row);
+        }
+        __syncthreads();  // the next batch overwrites the staged records and the sums
+    }
+}
+
 void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
     if (p.num_tiles <= 0) return;
     const int minw = tuning("bwd_minwaves", 5), wpb = tuning("bwd_wpb", 1);
@@ -488,6 +652,21 @@ void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
         RenderBwdParams q = p;
         q.prio_div = tuning("prio_div", 0);
         q.stamps = tuning("stamp", 0) ? stamp_buffer(1) : nullptr;
+        // "bwd_parts" 1, 2 or 4; 0 (default): 4 or 2 while that many part-waves fit within bwd_part_slots
+        int parts = tuning("bwd_parts", 0);
+        const int slots = tuning("bwd_part_slots", 8192);  // 1024 SIMDs x 8: 800x800 (2500 tiles) takes 2 parts
+        if (parts == 0) parts = p.num_tiles * 4 <= slots ? 4 : p.num_tiles * 2 <= slots ? 2 : 1;
+        if (parts == 2 || parts == 4) {
+            const dim3 grid(p.num_tiles), block(64 * parts);
+            if (p.dL_dinvdepth) {
+                if (parts == 2) render_bwd_parts_kernel<true, 2><<<grid, block, 0, s>>>(q);
+                else render_bwd_parts_kernel<true, 4><<<grid, block, 0, s>>>(q);
+            } else {
+                if (parts == 2) render_bwd_parts_kernel<false, 2><<<grid, block, 0, s>>>(q);
+                else render_bwd_parts_kernel<false, 4><<<grid, block, 0, s>>>(q);
+            }
+            return;
+        }
         const dim3 grid(p.num_tiles), block(64);
         const int strip = tuning("bwd_strip", 1), pred = tuning("bwd_pred", 2), pair = tuning("bwd_pair", 1);
 #define GSR_BWD4(INV)                                                                                   \
