@@ -634,8 +634,8 @@ __device__ __forceinline__ bool seg_lds_sort(const unsigned long long *__restric
 //      bucket width), taken longest first; tiles above SEG_BLOCK_CAP among them are left to seg_huge;
 //   2. then the short tiles, one wave each (seg_sort_wave), again longest first.
 // A tile whose proxy keys tie is appended to tie_list for seg_huge.
-template <bool P32>
-__global__ __launch_bounds__(256) void seg_sort_kernel(SegSortParams p) {
+template <bool P32, int MIN_WAVES = 1>
+__global__ __launch_bounds__(256, MIN_WAVES) void seg_sort_kernel(SegSortParams p) {
     __shared__ unsigned long long s_x[SEG_BLOCK_CAP];
     __shared__ uint32_t s_flag;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -760,7 +760,10 @@ void launch_seg_sort(hipStream_t s, const SegSortParams &p0) {
     SegSortParams p = p0;
     p.stamps = tuning("stamp", 0) ? stamp_buffer(2) : nullptr;
     const uint32_t grid = std::min(div_up(p.T, 4), (uint32_t)tuning("seg_grid", 1536));
-    if (tuning("seg32", 1)) seg_sort_kernel<true><<<grid, 256, 0, s>>>(p);
+    const int minw = tuning("seg_minw", 6);  // 80 VGPRs: 0.053 vs 0.060 ms at 4 waves/SIMD
+    if (tuning("seg32", 1) && minw >= 6) seg_sort_kernel<true, 6><<<grid, 256, 0, s>>>(p);
+    else if (tuning("seg32", 1) && minw == 5) seg_sort_kernel<true, 5><<<grid, 256, 0, s>>>(p);
+    else if (tuning("seg32", 1)) seg_sort_kernel<true><<<grid, 256, 0, s>>>(p);
     else seg_sort_kernel<false><<<grid, 256, 0, s>>>(p);
     constexpr uint32_t HUGE_LDS_KEYS = 8192;  // 64 KB
     seg_huge_kernel<<<512, 256, HUGE_LDS_KEYS * sizeof(unsigned long long), s>>>(p, HUGE_LDS_KEYS);
