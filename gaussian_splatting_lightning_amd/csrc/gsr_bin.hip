@@ -761,7 +761,8 @@ void launch_seg_sort(hipStream_t s, const SegSortParams &p0) {
     p.stamps = tuning("stamp", 0) ? stamp_buffer(2) : nullptr;
     const uint32_t grid = std::min(div_up(p.T, 4), (uint32_t)tuning("seg_grid", 1536));
     const int minw = tuning("seg_minw", 6);  // 80 VGPRs: 0.053 vs 0.060 ms at 4 waves/SIMD
-    if (tuning("seg32", 1) && minw >= 6) seg_sort_kernel<true, 6><<<grid, 256, 0, s>>>(p);
+    if (tuning("seg32", 1) && minw >= 7) seg_sort_kernel<true, 7><<<grid, 256, 0, s>>>(p);
+    else if (tuning("seg32", 1) && minw == 6) seg_sort_kernel<true, 6><<<grid, 256, 0, s>>>(p);
     else if (tuning("seg32", 1) && minw == 5) seg_sort_kernel<true, 5><<<grid, 256, 0, s>>>(p);
     else if (tuning("seg32", 1)) seg_sort_kernel<true><<<grid, 256, 0, s>>>(p);
     else seg_sort_kernel<false><<<grid, 256, 0, s>>>(p);
