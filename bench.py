@@ -13,9 +13,10 @@ max-reduce of the radii (BASELINE.json config 4: one view per GPU).  Per-GPU wor
 weak.  value = N * Gaussians * W * H / step time (Gaussians*pixels/s, whole job).
 
 Extra fields on the one JSON line:
-  roofline      dominant kernel, achieved algorithmic bytes / its average duration from a hipEvent pair
-                recorded around that kernel's stage on the launch stream during the timed steps (the only
-                events in the timed region; SURVEY.md §8(d) bytes);
+  roofline      dominant kernel (a composite pass, fp32-VALU-bound): algorithmic flops / its average duration
+                from a hipEvent pair recorded around that kernel's stage on the launch stream during the timed
+                steps (the only events in the timed region; SURVEY.md §8(d) flops), with the same launch's
+                algorithmic-bytes HBM figure and PMC traffic beside it;
   cpu_baseline  the oracle (oracle/gsr_oracle.c, C + OpenMP) on the same workload on the host cores;
   stages_ms     average device time of every pipeline stage per step, from a separate untimed pass of K steps
                 with an event pair around every stage.
@@ -192,13 +193,19 @@ def main():
                 traffic = e.get("hbm_bytes_per_launch") if e else None
             except Exception:  # noqa: BLE001
                 traffic = None
-        roofline = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "algorithmic_bytes_per_launch": algo_bytes[dom], "avg_launch_ms": round(dom_ms, 4),
-                    "valu_tflops_est": round(flops[dom] / (dom_ms * 1e-3) / 1e12, 2),
-                    "valu_frac_est": round(flops[dom] / (dom_ms * 1e-3) / 1e12 / FP32_VALU_PEAK_TF, 4),
-                    "note": "composite is VALU-bound by construction (SURVEY §8(d)); valu_* uses 25/70 flop per "
-                            "evaluated (pixel, Gaussian) pair x sum(n_contrib)"}
+        # The composite passes are VALU-bound by construction (~145 flop per byte against the
+        # 20 flop/B ridge), so the headline roofline is the fp32 VALU one: algorithmic flops (25 / 70 per
+        # evaluated (pixel, Gaussian) pair x sum(n_contrib)) over the live launch time.  The HBM figure of the
+        # same launch (SURVEY's algorithmic bytes, PMC traffic) is kept beside it.
+        tflops = flops[dom] / (dom_ms * 1e-3) / 1e12
+        roofline = {"kernel": dom, "bound": "valu", "achieved": round(tflops, 2), "peak": FP32_VALU_PEAK_TF,
+                    "unit": "TFLOP/s", "frac": round(tflops / FP32_VALU_PEAK_TF, 4), "traffic": traffic,
+                    "algorithmic_flops_per_launch": flops[dom], "avg_launch_ms": round(dom_ms, 4),
+                    "hbm": {"achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": algo_bytes[dom]},
+                    "note": "fp32 VALU bound (no MFMA work on this path); flops = 25 (fwd) / 70 (bwd) per pair x "
+                            "sum(n_contrib) (SURVEY §8(d)); traffic = PMC HBM bytes per launch "
+                            "(profiles/pmc_traffic.json)"}
 
     # ---- CPU baseline: the oracle on the same workload, rank 0 at N=1 only ----
     cpu = None
@@ -236,6 +243,8 @@ def main():
                    "instances_per_view": I, "sum_n_contrib": sum_contrib,
                    "stage_events": ("timed steps: dominant kernel only; stages_ms: separate untimed pass"
                                     if use_events else "none")},
+        **({"multi_gpu_note": "the RCCL exchange cannot be rehearsed on a 1-GPU box (RCCL rejects two ranks on one "
+                              "device); gloo world-size-2 tests cover its logic (DESIGN.md §6)"} if world > 1 else {}),
         "roofline": roofline, "cpu_baseline": cpu,
         "stages_ms": {k: round(v, 4) for k, v in stage_avg.items() if v > 0},
     }

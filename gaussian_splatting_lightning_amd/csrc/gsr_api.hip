@@ -171,18 +171,63 @@ struct StageScope {
         if (rc_ != GSR_OK) return rc_;                  \
     } while (0)
 
-hipEvent_t readback_event() {
-    thread_local hipEvent_t e = nullptr;
-    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
-    return e;
+// Every entry point runs with the device of its stream current (the caller's current device may differ, e.g. a
+// thread rendering on cuda:1 after cuda:0), so scratch events, pinned words and launches all belong to the
+// stream's device.  The null stream means the current device.
+struct StreamDeviceGuard {
+    int prev = -1, dev = -1;
+    explicit StreamDeviceGuard(hipStream_t s) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        dev = prev;
+        if (s && hipStreamGetDevice(s, &dev) != hipSuccess) dev = prev;
+        if (dev != prev && dev >= 0) (void)hipSetDevice(dev);
+        (void)hipGetLastError();
+    }
+    ~StreamDeviceGuard() {
+        if (prev >= 0 && dev != prev) (void)hipSetDevice(prev);
+    }
+};
+
+constexpr int kMaxDevices = 64;
+
+// The readback event and pinned words are per thread AND per device: an event recorded on a stream of
+// another device is an invalid handle.
+hipEvent_t readback_event(int dev) {
+    thread_local hipEvent_t e[kMaxDevices] = {};
+    if (dev < 0 || dev >= kMaxDevices) return nullptr;
+    if (!e[dev] && hipEventCreateWithFlags(&e[dev], hipEventDisableTiming) != hipSuccess) e[dev] = nullptr;
+    return e[dev];
 }
 
-uint32_t *pinned_words() {
-    thread_local uint32_t *p = nullptr;
-    if (!p) {
-        if (hipHostMalloc((void **)&p, 4096, hipHostMallocDefault) != hipSuccess) p = nullptr;
+uint32_t *pinned_words(int dev) {
+    thread_local uint32_t *p[kMaxDevices] = {};
+    if (dev < 0 || dev >= kMaxDevices) return nullptr;
+    if (!p[dev]) {
+        if (hipHostMalloc((void **)&p[dev], 4096, hipHostMallocDefault) != hipSuccess) p[dev] = nullptr;
     }
-    return p;
+    return p[dev];
+}
+
+// The decoupled look-backs (instance scan, bucket tile scan, onesweep sorts) stop spinning after ~2^24 polls and
+// set a flag instead of hanging the GPU.  A chain only breaks if a predecessor never publishes, which the ticket
+// order rules out short of a preempted or killed wave; a broken chain can only under-count a prefix, so every
+// derived offset stays inside its buffer and the failure is wrong output, never a fault.  With debug set the
+// forward reads the flags back (it is synchronising anyway) and fails instead of returning such output.
+int check_lookback_flags(hipStream_t s, int dev, const uint32_t *counters, const uint32_t *depth_ctrl,
+                         const uint32_t *tile_ctrl) {
+    uint32_t *hw = pinned_words(dev);
+    if (!hw) return fail(GSR_ERR_HIP, "pinned host buffer allocation failed");
+    GSR_HIP(hipMemcpyAsync(hw, counters + CNT_OVERFLOW, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if (depth_ctrl)
+        GSR_HIP(hipMemcpyAsync(hw + 1, depth_ctrl + RS_CTRL_ERR, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if (tile_ctrl)
+        GSR_HIP(hipMemcpyAsync(hw + 2, tile_ctrl + RS_CTRL_ERR, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    GSR_HIP(hipStreamSynchronize(s));
+    const uint32_t c = hw[0], d = depth_ctrl ? hw[1] : 0u, t = tile_ctrl ? hw[2] : 0u;
+    if (c & 2u) return fail(GSR_ERR_HIP, "instance/tile scan look-back did not complete (spin limit)");
+    if (c & 1u) return fail(GSR_ERR_OVERFLOW, "instance scan overflow");
+    if (d | t) return fail(GSR_ERR_HIP, "radix sort look-back did not complete (spin limit)");
+    return GSR_OK;
 }
 
 int check_common(int P, int D, int M, int W, int H, const float *means3D, const float *opac,
@@ -268,6 +313,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     if (rc) return rc;
     if (!a->out_color || (a->P > 0 && !a->radii)) return fail(GSR_ERR_ARG, "out_color and radii are required");
     hipStream_t stream = (hipStream_t)stream_ptr;
+    StreamDeviceGuard device_guard(stream);
     const bool dbg = a->debug != 0;
     const int P = a->P, W = a->W, H = a->H;
     const int gx = (W + BLOCK_X - 1) / BLOCK_X, gy = (H + BLOCK_Y - 1) / BLOCK_Y;
@@ -313,8 +359,8 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     // preprocess.  The bucket path's count pass needs no total either: whenever the tile count admits that
     // path it is queued right behind the copy, so the GPU runs it while the host waits (its scratch is in the
     // image buffer; if the total then selects the radix path, its results are simply unused).
-    uint32_t *hw = pinned_words();
-    hipEvent_t rb_ev = readback_event();
+    uint32_t *hw = pinned_words(device_guard.dev);
+    hipEvent_t rb_ev = readback_event(device_guard.dev);
     if (!hw || !rb_ev) return fail(GSR_ERR_HIP, "pinned host buffer / event allocation failed");
     GSR_HIP(hipMemcpyAsync(hw, g.counters, CNT_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
     GSR_HIP(hipEventRecord(rb_ev, stream));
@@ -421,6 +467,12 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     rp.out_color = a->out_color; rp.out_invdepth = a->out_invdepth; rp.final_T = im.final_T;
     rp.n_contrib = im.n_contrib; rp.tile_last = im.tile_last;
     GSR_STAGE(ST_RENDER_FWD, dbg, launch_render_fwd(stream, rp));
+    if (dbg) {  // onesweep control blocks exist only for the sorts that ran on the onesweep path
+        const int os = tuning("onesweep", 1);
+        return check_lookback_flags(stream, device_guard.dev, g.counters,
+                                    (!bucket && (os & 1)) ? g.sort.ctrl : nullptr,
+                                    (!bucket && R > 0 && (os & 2)) ? b.sort.ctrl : nullptr);
+    }
     return GSR_OK;
 }
 
@@ -438,6 +490,7 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
         return fail(GSR_ERR_ARG, "dL_dsh (or dL_dcolors_sh) is required when shs are given");
     if (a->R < 0 || a->R > 0xffffffffLL) return fail(GSR_ERR_ARG, "bad num_rendered");
     hipStream_t stream = (hipStream_t)stream_ptr;
+    StreamDeviceGuard device_guard(stream);
     const bool dbg = a->debug != 0;
     const int P = a->P, W = a->W, H = a->H;
     const int gx = (W + BLOCK_X - 1) / BLOCK_X, gy = (H + BLOCK_Y - 1) / BLOCK_Y;
@@ -520,6 +573,7 @@ int gsr_sh_backward_views(int P, int D, int M, int V, const float *means3D, cons
     if (P == 0) return GSR_OK;
     if (!means3D || !dL_dsh || (V > 0 && (!campos || !dL_dcolors_sh))) return fail(GSR_ERR_ARG, "null argument");
     hipStream_t stream = (hipStream_t)stream_ptr;
+    StreamDeviceGuard device_guard(stream);
     GSR_STAGE(ST_SH_VIEWS, 0, launch_sh_backward_views(stream, P, D, M, V, means3D, campos, dL_dcolors_sh, dL_dsh));
     return GSR_OK;
 }
@@ -553,6 +607,7 @@ int gsr_adam_step(const gsr_adam_group *groups, int num_groups, double beta1, do
     L.beta2 = (float)beta2;
     L.one_minus_beta2 = (float)(1.0 - beta2);
     L.eps = (float)eps;
+    StreamDeviceGuard device_guard((hipStream_t)stream_ptr);
     launch_adam((hipStream_t)stream_ptr, L, slices);
     GSR_HIP(hipGetLastError());
     return GSR_OK;
@@ -596,6 +651,7 @@ int gsr_densify_classify(const gsr_densify_args *args, void *workspace, int32_t 
     p.row_class = (uint8_t *)(ws + o_cls);
     p.counts = counts;
     p.preserve_idx = preserve_idx;
+    StreamDeviceGuard device_guard((hipStream_t)stream_ptr);
     launch_densify_classify((hipStream_t)stream_ptr, p);
     GSR_HIP(hipGetLastError());
     return GSR_OK;
@@ -630,6 +686,7 @@ int gsr_densify_apply(int64_t N, const void *workspace, const float *rotation, c
     }
     if (blocks > 0x7fffffffLL) return fail(GSR_ERR_ARG, "densify: too many elements");
     A.num_fields = num_fields;
+    StreamDeviceGuard device_guard((hipStream_t)stream_ptr);
     launch_densify_apply((hipStream_t)stream_ptr, A, blocks);
     GSR_HIP(hipGetLastError());
     return GSR_OK;
@@ -674,6 +731,7 @@ int gsr_ply_unpack(const uint8_t *records, int64_t n, int record_bytes, int big_
     if (rc != GSR_OK) return rc;
     if (n > 0 && !records) return fail(GSR_ERR_ARG, "ply: null records");
     p.records = records;
+    StreamDeviceGuard device_guard((hipStream_t)stream_ptr);
     launch_ply((hipStream_t)stream_ptr, p, false);
     GSR_HIP(hipGetLastError());
     return GSR_OK;
@@ -686,6 +744,7 @@ int gsr_ply_pack(uint8_t *records, int64_t n, int record_bytes, int big_endian, 
     if (rc != GSR_OK) return rc;
     if (n > 0 && !records) return fail(GSR_ERR_ARG, "ply: null records");
     p.records_out = records;
+    StreamDeviceGuard device_guard((hipStream_t)stream_ptr);
     launch_ply((hipStream_t)stream_ptr, p, true);
     GSR_HIP(hipGetLastError());
     return GSR_OK;
@@ -700,6 +759,7 @@ int gsr_knn_mean_dist2(int64_t n, const float *points, float *out, void *workspa
     KnnScratch k{};
     k.base = workspace;
     knn_workspace(n, &k);
+    StreamDeviceGuard device_guard((hipStream_t)stream_ptr);
     launch_knn((hipStream_t)stream_ptr, k, points, n, out);
     GSR_HIP(hipGetLastError());
     return GSR_OK;
@@ -718,6 +778,7 @@ int gsr_ssim_forward(int planes, int H, int W, const float *img1, const float *i
     if ((dm_dmu1 == nullptr) != (dm_dsigma1_sq == nullptr) || (dm_dmu1 == nullptr) != (dm_dsigma12 == nullptr))
         return fail(GSR_ERR_ARG, "ssim: derivative maps must be all given or all NULL");
     hipStream_t s = (hipStream_t)stream_ptr;
+    StreamDeviceGuard device_guard(s);
     launch_ssim_forward(s, planes, H, W, img1, img2, valid_padding, partial_sums, dm_dmu1, dm_dsigma1_sq, dm_dsigma12);
     GSR_HIP(hipGetLastError());
     return GSR_OK;
@@ -733,6 +794,7 @@ int gsr_ssim_backward(int planes, int H, int W, const float *img1, const float *
     const int64_t counted = (int64_t)planes * (valid_padding ? (int64_t)(H - 10) * (W - 10) : (int64_t)H * W);
     if (counted <= 0) return fail(GSR_ERR_ARG, "ssim: image smaller than the valid window");
     hipStream_t s = (hipStream_t)stream_ptr;
+    StreamDeviceGuard device_guard(s);
     launch_ssim_backward(s, planes, H, W, img1, img2, valid_padding, dL_dmean, (float)(1.0 / (double)counted), dm_dmu1,
                          dm_dsigma1_sq, dm_dsigma12, dL_dimg1);
     GSR_HIP(hipGetLastError());
@@ -746,6 +808,7 @@ int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const
     if (P == 0) return GSR_OK;
     if (!means3D || !viewmatrix || !present) return fail(GSR_ERR_ARG, "null argument");
     hipStream_t s = (hipStream_t)stream_ptr;
+    StreamDeviceGuard device_guard(s);
     launch_mark_visible(s, P, means3D, viewmatrix, present);
     GSR_HIP(hipGetLastError());
     return GSR_OK;

@@ -143,7 +143,9 @@ def forward_raw(means3D, sh, colors_precomp, opacities, scales, rotations, cov3D
         antialiasing=int(bool(rs.antialiasing)), debug=int(bool(rs.debug)), out_color=color.data_ptr(),
         out_invdepth=invdepth.data_ptr(), radii=radii.data_ptr())
     num_rendered = ctypes.c_int64(0)
-    rc = lib.gsr_forward(ctypes.byref(a), bufs.callback, None, _stream_handle(device), ctypes.byref(num_rendered))
+    with torch.cuda.device(device):  # the library also switches to its stream's device (gsr_api.hip)
+        rc = lib.gsr_forward(ctypes.byref(a), bufs.callback, None, _stream_handle(device),
+                             ctypes.byref(num_rendered))
     _native.check(rc, "rasterize_gaussians")
     state = ForwardState(means3D_c, sh_c, col_c, op_c, sc_c, rot_c, cov_c, radii, bg, view, proj, campos,
                          bufs.get(_native.GSR_BUF_GEOM), bufs.get(_native.GSR_BUF_BINNING),
@@ -209,7 +211,8 @@ def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_
         dL_dmeans3D=dmeans3D.data_ptr(), dL_dcov3D=_ptr(dcov), dL_dsh=_ptr(dsh),
         dL_dscales=dscales.data_ptr(), dL_drotations=drot.data_ptr(), dL_dcolors_sh=_ptr(dcsh),
         densify_stats=_ptr(dstats))
-    rc = lib.gsr_backward(ctypes.byref(a), bufs.callback, None, _stream_handle(device))
+    with torch.cuda.device(device):
+        rc = lib.gsr_backward(ctypes.byref(a), bufs.callback, None, _stream_handle(device))
     _native.check(rc, "rasterize_gaussians_backward")
     return dict(
         means3D=dmeans3D, means2D=dmeans2D,
@@ -275,8 +278,9 @@ def sh_backward_views(means3D: torch.Tensor, campos: torch.Tensor, dcolors_sh: t
         out = torch.empty(P, M, 3, dtype=torch.float32, device=device)
     elif tuple(out.shape) != (P, M, 3) or out.dtype != torch.float32 or not out.is_contiguous():
         raise RuntimeError(f"out must be a contiguous float32 tensor of shape {(P, M, 3)}")
-    rc = lib.gsr_sh_backward_views(P, int(sh_degree), int(M), V, _ptr(m), _ptr(c), _ptr(d), out.data_ptr(),
-                                   _stream_handle(device))
+    with torch.cuda.device(device):
+        rc = lib.gsr_sh_backward_views(P, int(sh_degree), int(M), V, _ptr(m), _ptr(c), _ptr(d), out.data_ptr(),
+                                       _stream_handle(device))
     _native.check(rc, "sh_backward_views")
     return out
 
@@ -290,7 +294,9 @@ def mark_visible(positions: torch.Tensor, viewmatrix: torch.Tensor, projmatrix: 
     P = positions.shape[0]
     present = torch.zeros(P, dtype=torch.bool, device=device)
     if P:
-        rc = lib.gsr_mark_visible(P, _ptr(pos), _ptr(view), _ptr(proj), present.data_ptr(), _stream_handle(device))
+        with torch.cuda.device(device):
+            rc = lib.gsr_mark_visible(P, _ptr(pos), _ptr(view), _ptr(proj), present.data_ptr(),
+                                      _stream_handle(device))
         _native.check(rc, "mark_visible")
     return present
 

@@ -496,3 +496,20 @@ def test_debug_mode_is_bitwise_identical(gpu_device, bucket):
         assert np.array_equal(a[k], b[k]), k
     for k in GRADS:
         assert np.array_equal(a["grads"][k], b["grads"][k]), k
+
+
+@pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2, reason="needs two HIP devices")
+def test_render_on_non_current_device():
+    """Inputs on cuda:1 while cuda:0 is current (and the reverse afterwards): the library runs on its stream's
+    device (per-device readback event and pinned words), so results equal those of a cuda:0 run."""
+    inp = scene_inputs(5000, 160, 120, sh_degree=1, seed=51)
+    dc, di = upstream(160, 120, 51)
+    d0, d1 = torch.device("cuda", 0), torch.device("cuda", 1)
+    torch.cuda.set_device(d0)
+    a = run_hip(inp, d0, dc, di)
+    b = run_hip(inp, d1, dc, di)
+    c = run_hip(inp, d0, dc, di)
+    for k in ("color", "invdepth", "radii"):
+        assert np.array_equal(a[k], b[k]) and np.array_equal(a[k], c[k]), k
+    for k in GRADS:
+        assert np.array_equal(a["grads"][k], b["grads"][k]), k
