@@ -335,7 +335,7 @@ __global__ __launch_bounds__(64, MIN_WAVES) void render_bwd_v4_kernel(RenderBwdP
             s_a[lane] = stage_rec_a(my_a);
             s_b[lane] = stage_rec_b(my_b);
             s_c[lane] = p.rec_c[gid];
-            if (STRIP) my_m = strip_mask(my_a, my_b, row0);
+            if (STRIP) my_m = cell_mask(p.strip_exact, my_a, my_b, row0, (float)(tx * BLOCK_X));
         }
         // strip k of instance j is live iff bit j of sk[k] (wave-uniform, scalar registers)
         uint64_t sk[PIX_PER_LANE];
@@ -546,7 +546,7 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
             s_a[lane] = stage_rec_a(my_a);
             s_b[lane] = stage_rec_b(my_b);
             s_c[lane] = p.rec_c[gid];
-            s_m[lane] = strip_mask(my_a, my_b, row0);
+            s_m[lane] = cell_mask(p.strip_exact, my_a, my_b, row0, (float)(tx * BLOCK_X));
         }
         __syncthreads();
         // strip k of instance j is live iff bit j of sk[k] (wave-uniform)
@@ -650,6 +650,7 @@ void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
     const int minw = tuning("bwd_minwaves", 5), wpb = tuning("bwd_wpb", 1);
     if (tuning("bwd_v", 4) == 4) {
         RenderBwdParams q = p;
+        q.strip_exact = tuning("strip_exact", 1);
         q.prio_div = tuning("prio_div", 0);
         q.stamps = tuning("stamp", 0) ? stamp_buffer(1) : nullptr;
         // "bwd_parts" 1, 2 or 4; 0 (default): 4 or 2 while that many part-waves fit within bwd_part_slots

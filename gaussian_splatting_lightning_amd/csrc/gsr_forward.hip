@@ -523,7 +523,7 @@ __device__ __forceinline__ void composite_fwd(const RenderFwdParams &p, const in
                 s_a[lane] = stage_rec_a(ra);
                 s_b[lane] = stage_rec_b(rb);
                 s_c[lane] = rc;
-                if (STRIP) s_m[lane] = strip_mask(ra, rb, row0);
+                if (STRIP) s_m[lane] = cell_mask(p.strip_exact, ra, rb, row0, (float)(tx * BLOCK_X));
             }
             if (s + 64 < range.y) {
                 ra = p.rec_a[g2];
@@ -547,7 +547,7 @@ __device__ __forceinline__ void composite_fwd(const RenderFwdParams &p, const in
             s_a[lane] = stage_rec_a(ga);
             s_b[lane] = stage_rec_b(gb);
             s_c[lane] = p.rec_c[gid];
-            if (STRIP) s_m[lane] = strip_mask(ga, gb, row0);
+            if (STRIP) s_m[lane] = cell_mask(p.strip_exact, ga, gb, row0, (float)(tx * BLOCK_X));
         }
         loaded_end = min(range.y, base + 64u);
         wave_lds_sync();
@@ -634,7 +634,7 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_split_kernel(Render
 // Every tile in 4 / NPIX parts (row strips {NPIX * part .. NPIX * part + NPIX - 1} of each lane's column), one
 // wave each, consecutive slots: 2 or 4 times the waves of whole tiles, each with fewer registers, so the SIMDs
 // stay fuller to the end of the launch.  Parts combine tile_last / tile_loaded with atomicMax on zeroed words.
-template <int NPIX, int MIN_WAVES>
+template <int NPIX, int MIN_WAVES, bool STRIP>
 __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_part_kernel(RenderFwdParams p) {
     __shared__ float4 s_a[4][64];
     __shared__ float4 s_b[4][64];
@@ -646,12 +646,14 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_part_kernel(RenderF
     if (slot >= p.num_tiles * PARTS) return;
     const uint32_t t_start = p.stamps ? stamp_now() : 0u;
     const int tile = p.tile_order ? (int)p.tile_order[slot / PARTS] : slot / PARTS;
-    composite_fwd<NPIX, false, false>(p, tile, slot % PARTS, lane, s_a[w], s_b[w], s_c[w], s_m[w]);
+    composite_fwd<NPIX, false, STRIP>(p, tile, slot % PARTS, lane, s_a[w], s_b[w], s_c[w], s_m[w]);
     stamp_store(p.stamps, slot, t_start, lane);
 }
 
-void launch_render_fwd(hipStream_t s, const RenderFwdParams &p) {
-    if (p.num_tiles <= 0) return;
+void launch_render_fwd(hipStream_t s, const RenderFwdParams &p0) {
+    if (p0.num_tiles <= 0) return;
+    RenderFwdParams p = p0;
+    p.strip_exact = tuning("strip_exact", 1);
     // "fwd_parts" 1, 2 or 4; 0 (default): 4 or 2 when that many part-waves still fit the GPU's ~8 resident waves
     // per SIMD, twice over (small images, where one heavy tile's latency sets the kernel time), else whole tiles with
     // only the heaviest split in two
@@ -663,10 +665,18 @@ void launch_render_fwd(hipStream_t s, const RenderFwdParams &p) {
         q.stamps = tuning("stamp", 0) ? stamp_buffer(0) : nullptr;
         const dim3 grid(div_up(p.num_tiles * parts, 4)), block(256);
         const int mw = tuning("fwd_part_waves", 8);
-        if (parts == 2 && mw >= 8) render_fwd_part_kernel<2, 8><<<grid, block, 0, s>>>(q);
-        else if (parts == 2) render_fwd_part_kernel<2, 4><<<grid, block, 0, s>>>(q);
-        else if (mw >= 8) render_fwd_part_kernel<1, 8><<<grid, block, 0, s>>>(q);
-        else render_fwd_part_kernel<1, 4><<<grid, block, 0, s>>>(q);
+        // "fwd_strip_parts" 1 (default): skip an instance's 4-row strips that no pixel can pass (cell_mask)
+        const bool strip = tuning("fwd_strip_parts", 1) != 0;
+#define GSR_FWD_PART(NP, MW)                                                                            \
+        do {                                                                                           \
+            if (strip) render_fwd_part_kernel<NP, MW, true><<<grid, block, 0, s>>>(q);                 \
+            else render_fwd_part_kernel<NP, MW, false><<<grid, block, 0, s>>>(q);                      \
+        } while (0)
+        if (parts == 2 && mw >= 8) GSR_FWD_PART(2, 8);
+        else if (parts == 2) GSR_FWD_PART(2, 4);
+        else if (mw >= 8) GSR_FWD_PART(1, 8);
+        else GSR_FWD_PART(1, 4);
+#undef GSR_FWD_PART
         return;
     }
     const dim3 grid(div_up(p.num_tiles, 4)), block(256);

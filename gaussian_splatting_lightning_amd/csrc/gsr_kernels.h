@@ -114,6 +114,7 @@ struct RenderFwdParams {
     uint32_t *n_contrib, *tile_last;
     int prio_div;  // > 0: launch slots [0, d) run at wave priority 3, [d, 2d) at 2, [2d, 3d) at 1 (set by launch)
     uint4 *stamps; // diagnostics (set by launch), or null
+    int strip_exact;  // strip skipping mask: 1 strip_mask_exact (column-band extent), 0 strip_mask (set by launch)
 };
 void launch_render_fwd(hipStream_t s, const RenderFwdParams &p);
 
@@ -133,6 +134,7 @@ struct RenderBwdParams {
     int rows_by_u;  // 1: row of an instance at its expansion index u (Gaussian-major), 0: at its sorted position
     int prio_div;   // as RenderFwdParams::prio_div (set by launch)
     uint4 *stamps;  // diagnostics (set by launch), or null
+    int strip_exact;  // as RenderFwdParams::strip_exact (set by launch)
 };
 void launch_render_bwd(hipStream_t s, const RenderBwdParams &p);
 

@@ -23,6 +23,35 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def strip_mask_exact(x, y, A, B, C, o, row0, col0):
+    """numpy fp32 restatement of gsr_common.h strip_mask_exact (vectorised over instances): (n,) -> (n, 4) bool."""
+    f = np.float32
+    x, y, A, B, C, o = (np.asarray(v, f) for v in (x, y, A, B, C, o))
+    with np.errstate(all="ignore"):
+        o255 = f(255) * o
+        det = A * C - B * B
+        hd = f(0.5) * (A - C)
+        lmin = f(0.5) * (A + C) - np.sqrt(hd * hd + B * B)
+        eps = f(1e-5) * (np.abs(A) + np.abs(B) + np.abs(C)) / lmin
+        tau = (f(2) * np.log(np.maximum(o255 * f(1.00001), f(1))) + f(1e-3)) / (f(1) - eps)
+        V = np.sqrt(tau * A / det)
+        uL = f(col0) - x
+        uR = uL + f(15)
+        ut = -B * V / A
+        ic, ctau = f(1) / C, C * tau
+        u = np.minimum(np.maximum(ut, uL), uR)
+        vmax = np.where((ut >= uL) & (ut <= uR), V, (-B * u + np.sqrt(np.maximum(ctau - det * u * u, 0))) * ic)
+        u = np.minimum(np.maximum(-ut, uL), uR)
+        vmin = np.where((-ut >= uL) & (-ut <= uR), -V, (-B * u - np.sqrt(np.maximum(ctau - det * u * u, 0))) * ic)
+        mg = f(1e-2) * V + f(1e-3) * (np.abs(uL) + np.abs(uR)) + f(0.0625)
+        lo, hi = y + vmin - mg - f(row0), y + vmax + mg - f(row0)
+        m = np.stack([(hi >= 4 * k) & (lo <= 4 * k + 3) for k in range(4)], 1)
+        keep_all = ~((det > 0) & (lmin > 0) & (eps < 1e-2) & (V < 1e6)) | np.isnan(o255)
+    m[keep_all] = True
+    m[o255 < 0.999] = False
+    return m
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg2")
@@ -52,7 +81,7 @@ def main():
     ly, lx = ly.reshape(-1), lx.reshape(-1)
     strip_of = ly // 4
     quad_of = (ly // 8) * 2 + (lx // 8)
-    tot = dict(pairs=0, strip_band=0, quad_box=0, quad_exact=0, strip_exact=0, quad_active=0, strip_active=0,
+    tot = dict(strip_fn=0, strip_fn_miss=0, pairs=0, strip_band=0, quad_box=0, quad_exact=0, strip_exact=0, quad_active=0, strip_active=0,
                active_pairs=0, fwd_pairs_tile=0)
     for t in tiles:
         tx, ty = t % gx, t // gx
@@ -90,13 +119,18 @@ def main():
             tot["quad_box"] += int(((hi_y >= y0) & (lo_y <= y0 + 7) & (hi_x >= x0) & (lo_x <= x0 + 7)).sum())
             tot["quad_exact"] += int(ok[:, quad_of == q].any(1).sum())
             tot["quad_active"] += int(act[:, quad_of == q].any(1).sum())
+        sm = strip_mask_exact(m[:, 0], m[:, 1], c[:, 0], c[:, 1], c[:, 2], c[:, 3], r0y, r0x)
+        tot["strip_fn"] += int(sm.sum())
+        for k in range(4):
+            tot["strip_fn_miss"] += int((ok[:, strip_of == k].any(1) & ~sm[:, k]).sum())
         for k in range(4):
             tot["strip_exact"] += int(ok[:, strip_of == k].any(1).sum())
             tot["strip_active"] += int(act[:, strip_of == k].any(1).sum())
     cells = tot["pairs"] // 64
     print(f"{args.config}: tiles {len(tiles)}, walked (tile, instance) pairs {tot['pairs'] // 256}, "
           f"active pixel pairs {tot['active_pairs']} ({tot['active_pairs'] / tot['pairs']:.3f} of walked)")
-    for k in ("strip_band", "strip_exact", "strip_active", "quad_box", "quad_exact", "quad_active"):
+    print(f"  strip_mask_exact: misses {tot['strip_fn_miss']} (must be 0)")
+    for k in ("strip_band", "strip_fn", "strip_exact", "strip_active", "quad_box", "quad_exact", "quad_active"):
         print(f"  {k:12s} live cells {tot[k]:>12d}  {tot[k] / cells:.3f} of all, "
               f"active-pixel density {tot['active_pairs'] / max(tot[k] * 64, 1):.3f}")
 
