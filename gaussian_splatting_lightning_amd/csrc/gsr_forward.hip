@@ -650,6 +650,131 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_part_kernel(RenderF
     stamp_store(p.stamps, slot, t_start, lane);
 }
 
+// v5: the row-strip part kernel with every piece of per-instance control wave-uniform.  The wave index is
+// read back as a scalar, so the tile, its range, the batch count and the contributor counter live in SGPRs;
+// each batch's strip masks (cell_mask) are ballots (one 64-bit word per pixel strip, bit j = instance j can
+// reach the strip), so a dead strip is skipped by one scalar bit test; the records of a batch sit in one LDS
+// array of 48-byte entries, read with immediate offsets from a single address.  Per instance this leaves the
+// dx / quadratic-form setup and the liveness ballot on the VALU (round-1 part kernel: ~19 VALU of per-instance
+// overhead besides the pixels).  The pixel update is that of composite_fwd, so outputs are bitwise identical.
+struct alignas(16) FwdRec {
+    float4 a;  // x, y, A, B (stage_rec_a)
+    float4 b;  // C, o, r, g (stage_rec_b)
+    float2 c;  // b, 1/depth
+    float2 pad;
+};
+
+template <int NPIX, int MIN_WAVES>
+__global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v5_kernel(RenderFwdParams p) {
+    constexpr int PARTS = 4 / NPIX;
+    __shared__ FwdRec s_rec[4][64];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int slot = blockIdx.x * 4 + w;
+    if (slot >= p.num_tiles * PARTS) return;
+    const int half = slot % PARTS;
+    const int tile = __builtin_amdgcn_readfirstlane(p.tile_order ? (int)p.tile_order[slot / PARTS] : slot / PARTS);
+    const uint32_t t_start = p.stamps ? stamp_now() : 0u;
+    const int tx = tile % p.gx, ty = tile / p.gx;
+    const int px = tx * BLOCK_X + (lane & 15);
+    const int py0 = ty * BLOCK_Y + (lane >> 4);
+    const float pfx = (float)px, pfy0 = (float)py0;
+    const float row0 = (float)(ty * BLOCK_Y), col0 = (float)(tx * BLOCK_X);
+    const int kbase = NPIX * half;  // whole-tile pixel index of this wave's first pixel
+    float T[NPIX], C0[NPIX], C1[NPIX], C2[NPIX], ID[NPIX];
+    uint32_t last[NPIX];
+#pragma unroll
+    for (int k = 0; k < NPIX; k++) {
+        const int py = py0 + 4 * (kbase + k);
+        T[k] = (px < p.W && py < p.H) ? 1.0f : -1.0f;  // live while T > 0 (composite_fwd)
+        C0[k] = C1[k] = C2[k] = ID[k] = 0.f;
+        last[k] = 0;
+    }
+    const uint2 rg = p.ranges[tile];
+    const uint32_t r0 = __builtin_amdgcn_readfirstlane(rg.x), r1 = __builtin_amdgcn_readfirstlane(rg.y);
+    uint32_t contributor = 0;
+    uint32_t loaded_end = r0;
+    FwdRec *sr = s_rec[w];
+    for (uint32_t base = r0; base < r1; base += 64) {
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < NPIX; k++) any |= T[k] > 0.f;
+        if (__ballot(any) == 0) break;
+        const uint32_t s = base + lane;
+        uint32_t m = 0;
+        if (s < r1) {
+            const uint32_t u = p.sorted_u[s];
+            const uint32_t gid = p.inst_gid[u];
+            p.point_list[s] = gid;
+            p.inv[u] = s;
+            const float4 ga = p.rec_a[gid], gb = p.rec_b[gid];
+            sr[lane].a = stage_rec_a(ga);
+            sr[lane].b = stage_rec_b(gb);
+            sr[lane].c = p.rec_c[gid];
+            m = cell_mask(p.strip_exact, ga, gb, row0, col0) >> kbase;
+        }
+        uint64_t sk[NPIX];
+#pragma unroll
+        for (int k = 0; k < NPIX; k++) sk[k] = __ballot((m >> k) & 1u);
+        loaded_end = min(r1, base + 64u);
+        wave_lds_sync();
+        const uint32_t cnt = min(64u, r1 - base);
+        for (uint32_t j = 0; j < cnt; j++) {
+            const float4 a = sr[j].a, b = sr[j].b;
+            const float2 c = sr[j].c;
+            contributor++;
+            const float dx = a.x - pfx, dy0 = a.y - pfy0;
+            const float P0 = (a.z * dx) * dx, L = a.w * dx;
+#pragma unroll
+            for (int k = 0; k < NPIX; k++) {
+                if (!((sk[k] >> j) & 1u)) continue;  // wave-uniform: no pixel of the strip passes
+                const float power2 = power2_at(b.x, dy0 - (float)(4 * (kbase + k)), P0, L);
+                const float alpha = fminf(0.99f, b.y * __builtin_amdgcn_exp2f(power2));
+                const bool ok = T[k] > 0.f && !(power2 > 0.0f) && !(alpha < 1.0f / 255.0f);
+                const float test_T = T[k] * (1 - alpha);
+                const bool stop = ok && test_T < 0.0001f;
+                const bool take = ok && !stop;
+                const float wgt = take ? alpha * T[k] : 0.f;
+                C0[k] = fmaf(b.z, wgt, C0[k]);
+                C1[k] = fmaf(b.w, wgt, C1[k]);
+                C2[k] = fmaf(c.x, wgt, C2[k]);
+                ID[k] = fmaf(c.y, wgt, ID[k]);
+                T[k] = take ? test_T : (stop ? -T[k] : T[k]);
+                last[k] = take ? contributor : last[k];
+            }
+            uint64_t live = 0;
+#pragma unroll
+            for (int k = 0; k < NPIX; k++) live |= __ballot(T[k] > 0.f);
+            if (live == 0) break;
+        }
+        wave_lds_sync();
+    }
+    const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
+    const size_t HW = (size_t)p.W * p.H;
+    uint32_t mx = 0;
+#pragma unroll
+    for (int k = 0; k < NPIX; k++) {
+        const int py = py0 + 4 * (kbase + k);
+        if (px < p.W && py < p.H) {
+            const size_t pid = (size_t)py * p.W + px;
+            const float Tk = fabsf(T[k]);
+            p.final_T[pid] = Tk;
+            p.n_contrib[pid] = last[k];
+            p.out_color[pid] = C0[k] + Tk * bg0;
+            p.out_color[HW + pid] = C1[k] + Tk * bg1;
+            p.out_color[2 * HW + pid] = C2[k] + Tk * bg2;
+            if (p.out_invdepth) p.out_invdepth[pid] = ID[k];
+            mx = max(mx, last[k]);
+        }
+    }
+    mx = wave_max_u32(mx);
+    if (lane == 0) {
+        atomicMax(&p.tile_last[tile], mx);
+        atomicMax(&p.tile_loaded[tile], loaded_end - r0);
+    }
+    stamp_store(p.stamps, slot, t_start, lane);
+}
+
 void launch_render_fwd(hipStream_t s, const RenderFwdParams &p0) {
     if (p0.num_tiles <= 0) return;
     RenderFwdParams p = p0;
@@ -665,7 +790,15 @@ void launch_render_fwd(hipStream_t s, const RenderFwdParams &p0) {
         q.stamps = tuning("stamp", 0) ? stamp_buffer(0) : nullptr;
         const dim3 grid(div_up(p.num_tiles * parts, 4)), block(256);
         const int mw = tuning("fwd_part_waves", 8);
-        // "fwd_strip_parts" 1 (default): skip an instance's 4-row strips that no pixel can pass (cell_mask)
+        // "fwd_v" 5 (default): render_fwd_v5_kernel (wave-uniform control, always strip skipping); 4: the
+        // composite_fwd part kernel, with "fwd_strip_parts" 1 skipping dead strips (cell_mask)
+        if (tuning("fwd_v", 5) == 5) {
+            if (parts == 2 && mw >= 8) render_fwd_v5_kernel<2, 8><<<grid, block, 0, s>>>(q);
+            else if (parts == 2) render_fwd_v5_kernel<2, 4><<<grid, block, 0, s>>>(q);
+            else if (mw >= 8) render_fwd_v5_kernel<1, 8><<<grid, block, 0, s>>>(q);
+            else render_fwd_v5_kernel<1, 4><<<grid, block, 0, s>>>(q);
+            return;
+        }
         const bool strip = tuning("fwd_strip_parts", 1) != 0;
 #define GSR_FWD_PART(NP, MW)                                                                            \
         do {                                                                                           \
