@@ -52,7 +52,7 @@ __device__ __forceinline__ void wave_reduce10_store(const float m[10], float *__
     float c8 = sum_swap16(a4, a4);        // value 8 + b5
     const bool hi3 = (lane & 8) != 0;
     const float keep = hi3 ? b1 : b0, send = hi3 ? b0 : b1;
-    float c0 = keep + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send), 0x128, 0xf, 0xf, false));
+    float c0 = dpp_xadd<0x128>(keep, send);
     c8 = dpp_add<0x128>(c8);  // row_ror:8 (= lane ^ 8)
     c0 = dpp_add<0xB1>(c0);   // quad_perm [1,0,3,2]
     c8 = dpp_add<0xB1>(c8);
@@ -83,7 +83,7 @@ __device__ __forceinline__ void wave_reduce20_store(const float m0[10], const fl
 #pragma unroll
     for (int m = 0; m < 2; m++) {
         const float keep = hi3 ? bb[2 * m + 1] : bb[2 * m], send = hi3 ? bb[2 * m] : bb[2 * m + 1];
-        c[m] = keep + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send), 0x128, 0xf, 0xf, false));
+        c[m] = dpp_xadd<0x128>(keep, send);
     }
     c[2] = dpp_add<0x128>(bb[4]);  // row_ror:8 (= lane ^ 8)
 #pragma unroll
@@ -645,10 +645,195 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
     }
 }
 
+// v5: v4's pair-reduced update (PRED 2) with the per-instance control on the scalar unit.
+//   render_bwd is VALU-issue-bound (SQ_INSTS_VALU x issue cost ~ 80 % of its cycles at cfg 3), so every saved
+//   vector instruction counts:
+//   * strip liveness by contributor count: a pixel takes part in instance idx only while idx < n_contrib, so strip
+//     k is dead for every idx >= its lanes' largest n_contrib (smax[k]); those batch bits are cleared from the
+//     strip mask with scalar ops, and for idx < the strips' smallest n_contrib (smin[k]) the per-lane
+//     `idx < n_contrib` compare is skipped (a scalar bit test selects the variant);
+//   * the staged records are one 48-byte FwdRec array.
+//   The pixel update is v4's, so gradients are bitwise those of v4.
+template <bool HAS_INV, bool LASTC>
+__global__ __launch_bounds__(64, 5) void render_bwd_v5_kernel(RenderBwdParams p) {
+    __shared__ FwdRec s_rec[BWD_BATCH];
+    __shared__ __attribute__((aligned(16))) float s_part[BWD_BATCH][PART];  // [instance][10 sums]
+    const int lane = threadIdx.x;
+    const int slot = blockIdx.x;
+    const uint32_t t_start = p.stamps ? stamp_now() : 0u;
+    const int tile = __builtin_amdgcn_readfirstlane(p.tile_order ? (int)p.tile_order[slot] : slot);
+    const int tx = tile % p.gx, ty = tile / p.gx;
+    const int px = tx * BLOCK_X + (lane & 15);
+    const int py0 = ty * BLOCK_Y + (lane >> 4);
+    const float pfx = (float)px, pfy0 = (float)py0;
+    const float row0 = (float)(ty * BLOCK_Y), col0 = (float)(tx * BLOCK_X);
+    const uint2 range = p.ranges[tile];
+    const uint32_t r0 = __builtin_amdgcn_readfirstlane(range.x);
+    const uint32_t tl = __builtin_amdgcn_readfirstlane(p.tile_last[tile]);
+    const uint32_t loaded = __builtin_amdgcn_readfirstlane(p.tile_loaded[tile]);
+    for (uint32_t s = r0 + tl + lane; s < r0 + loaded; s += 64) {
+        const float z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        store_row(p.rows, p.rows_by_u ? p.sorted_u[s] : s, z);
+    }
+    if (tl == 0) {
+        stamp_store(p.stamps, slot, t_start, lane);
+        return;
+    }
+
+    const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
+    const size_t HW = (size_t)p.W * p.H;
+    float T[PIX_PER_LANE], dp0[PIX_PER_LANE], dp1[PIX_PER_LANE], dp2[PIX_PER_LANE], dinv[PIX_PER_LANE];
+    float D[PIX_PER_LANE];
+    uint32_t lastc[PIX_PER_LANE], smax[PIX_PER_LANE], smin[PIX_PER_LANE];
+#pragma unroll
+    for (int k = 0; k < PIX_PER_LANE; k++) {
+        const int py = py0 + 4 * k;
+        const bool inside = px < p.W && py < p.H;
+        const size_t pid = inside ? (size_t)py * p.W + px : 0;
+        T[k] = inside ? p.final_T[pid] : 0.f;
+        lastc[k] = inside ? p.n_contrib[pid] : 0u;
+        dp0[k] = inside ? p.dL_dpix[pid] : 0.f;
+        dp1[k] = inside ? p.dL_dpix[HW + pid] : 0.f;
+        dp2[k] = inside ? p.dL_dpix[2 * HW + pid] : 0.f;
+        dinv[k] = (HAS_INV && inside) ? p.dL_dinvdepth[pid] : 0.f;
+        D[k] = fmaf(bg2, dp2[k], fmaf(bg1, dp1[k], bg0 * dp0[k]));
+        if (LASTC) {
+            smax[k] = __builtin_amdgcn_readfirstlane(wave_max_u32(lastc[k]));
+            smin[k] = __builtin_amdgcn_readfirstlane(wave_min_u32(lastc[k]));
+        }
+    }
+    const float hW = 0.5f * p.W, hH = 0.5f * p.H;
+
+    for (int bend = (int)tl; bend > 0; bend -= BWD_BATCH) {
+        const int cnt = min(BWD_BATCH, bend);
+        float4 my_a = make_float4(0, 0, 0, 0), my_b = my_a;
+        uint32_t my_row = 0, my_m = 0;
+        if (lane < cnt) {
+            const uint32_t s_me = r0 + (uint32_t)(bend - 1 - lane);
+            my_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
+            const uint32_t gid = p.point_list[s_me];
+            my_a = p.rec_a[gid];
+            my_b = p.rec_b[gid];
+            s_rec[lane].a = stage_rec_a(my_a);
+            s_rec[lane].b = stage_rec_b(my_b);
+            s_rec[lane].c = p.rec_c[gid];
+            my_m = cell_mask(p.strip_exact, my_a, my_b, row0, col0);
+        }
+        // sk[k] bit j: strip k of instance j (idx = bend - 1 - j) may hold a contributing pixel;
+        // nd[k] bit j: some lane of strip k may have n_contrib <= idx (the per-lane compare is needed)
+        uint64_t sk[PIX_PER_LANE], nd[PIX_PER_LANE];
+#pragma unroll
+        for (int k = 0; k < PIX_PER_LANE; k++) {
+            sk[k] = __ballot((my_m >> k) & 1u);
+            if (LASTC) {
+                const int lo = bend - (int)smax[k];  // j < lo: idx >= smax, no lane of the strip contributes
+                const int hi = bend - (int)smin[k];  // j < hi: idx >= smin, some lane may not contribute
+                sk[k] &= lo <= 0 ? ~0ull : lo >= 64 ? 0ull : ~0ull << lo;
+                nd[k] = hi <= 0 ? 0ull : hi >= 64 ? ~0ull : (1ull << hi) - 1ull;
+            } else {
+                nd[k] = ~0ull;
+            }
+        }
+        wave_lds_sync();
+        // one instance's pass over the lane's pixels: updates T / D, returns the 10 per-lane sums in m and the
+        // ballot of the lanes that contributed
+        auto pass = [&](const int j, float m[10]) -> bool {
+            const uint32_t idx = (uint32_t)(bend - 1 - j);
+            const FwdRec &r = s_rec[j];
+            const float4 a = r.a, b = r.b;  // a: x, y, A, B; b: C, o, r, g
+            const float2 c = r.c;           // b, 1/depth
+            const float dx = a.x - pfx, dy0 = a.y - pfy0;
+            const float P0 = (a.z * dx) * dx, L = a.w * dx;
+            float Q0 = 0.f, Q1 = 0.f, Q2 = 0.f, w0 = 0.f, w1 = 0.f, w2 = 0.f, w3 = 0.f;
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < PIX_PER_LANE; k++) {
+                if (!((sk[k] >> j) & 1u)) continue;  // wave-uniform
+                const float dy = dy0 - (float)(4 * k);
+                const float power2 = power2_at(b.x, dy, P0, L);
+                const float G = __builtin_amdgcn_exp2f(power2);
+                const float alpha = fminf(0.99f, b.y * G);
+                const bool need = (nd[k] >> j) & 1u;  // wave-uniform
+                const bool ok = !(power2 > 0.0f) & !(alpha < 1.0f / 255.0f) & (!need | (idx < lastc[k]));
+                if (!ok) continue;
+                any = true;
+                T[k] = T[k] * fast_rcp(1.f - alpha);
+                const float wgt = alpha * T[k];
+                float cd = fmaf(c.x, dp2[k], fmaf(b.w, dp1[k], b.z * dp0[k]));
+                if (HAS_INV) cd = fmaf(c.y, dinv[k], cd);
+                const float d = cd - D[k];
+                D[k] = fmaf(alpha, d, D[k]);
+                w0 = fmaf(wgt, dp0[k], w0);
+                w1 = fmaf(wgt, dp1[k], w1);
+                w2 = fmaf(wgt, dp2[k], w2);
+                if (HAS_INV) w3 = fmaf(wgt, dinv[k], w3);
+                const float q = G * (d * T[k]);
+                const float qdy = q * dy;
+                Q0 += q;
+                Q1 += qdy;
+                Q2 = fmaf(qdy, dy, Q2);
+            }
+            m[0] = Q0;
+            m[1] = Q0 * dx;
+            m[2] = Q1;
+            m[3] = m[1] * dx;
+            m[4] = Q1 * dx;
+            m[5] = Q2;
+            m[6] = w0;
+            m[7] = w1;
+            m[8] = w2;
+            m[9] = w3;
+            return any;
+        };
+        for (int j = 0; j < cnt; j += 2) {
+            float m0[10];
+            const bool any0 = pass(j, m0);
+            float *dst = s_part[j];
+            if (j + 1 < cnt) {
+                float m1[10];
+                const bool any1 = pass(j + 1, m1);
+                if (__ballot(any0 || any1)) {
+                    wave_reduce20_store(m0, m1, dst, lane);
+                } else if (lane < 10) {
+                    dst[lane] = 0.f;
+                    dst[PART + lane] = 0.f;
+                }
+            } else if (__ballot(any0)) {
+                wave_reduce10_store(m0, dst, lane);
+            } else if (lane < 10) {
+                dst[lane] = 0.f;
+            }
+        }
+        wave_lds_sync();
+        if (lane < cnt) {
+            const float4 *src = reinterpret_cast<const float4 *>(s_part[lane]);
+            const float4 u0 = src[0], u1 = src[1];
+            const float2 u2 = *reinterpret_cast<const float2 *>(s_part[lane] + 8);
+            const float S = u0.x, Sx = u0.y, Sy = u0.z, Sxx = u0.w, Sxy = u1.x, Syy = u1.y;
+            const float o = my_b.y, ca = my_a.z, cb = my_a.w, cc = my_b.x;
+            float row[10];
+            row[0] = -o * hW * (ca * Sx + cb * Sy);
+            row[1] = -o * hH * (cb * Sx + cc * Sy);
+            row[2] = -0.5f * o * Sxx;
+            row[3] = -0.5f * o * Sxy;
+            row[4] = -0.5f * o * Syy;
+            row[5] = S;
+            row[6] = u1.z;
+            row[7] = u1.w;
+            row[8] = u2.x;
+            row[9] = u2.y;
+            store_row(p.rows, my_row, row);
+        }
+        wave_lds_sync();
+    }
+    stamp_store(p.stamps, slot, t_start, lane);
+}
+
 void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
     if (p.num_tiles <= 0) return;
     const int minw = tuning("bwd_minwaves", 5), wpb = tuning("bwd_wpb", 1);
-    if (tuning("bwd_v", 4) == 4) {
+    const int bv = tuning("bwd_v", 5);
+    if (bv == 5 || bv == 4) {
         RenderBwdParams q = p;
         q.strip_exact = tuning("strip_exact", 1);
         q.prio_div = tuning("prio_div", 0);
@@ -669,6 +854,17 @@ void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
             return;
         }
         const dim3 grid(p.num_tiles), block(64);
+        if (bv == 5) {  // "bwd_lastc" 1 (default): strip liveness and compare skipping by n_contrib bounds
+            const bool lc = tuning("bwd_lastc", 1) != 0;
+            if (p.dL_dinvdepth) {
+                if (lc) render_bwd_v5_kernel<true, true><<<grid, block, 0, s>>>(q);
+                else render_bwd_v5_kernel<true, false><<<grid, block, 0, s>>>(q);
+            } else {
+                if (lc) render_bwd_v5_kernel<false, true><<<grid, block, 0, s>>>(q);
+                else render_bwd_v5_kernel<false, false><<<grid, block, 0, s>>>(q);
+            }
+            return;
+        }
         const int strip = tuning("bwd_strip", 1), pred = tuning("bwd_pred", 2), pair = tuning("bwd_pair", 1);
 #define GSR_BWD4(INV)                                                                                   \
         do {                                                                                           \

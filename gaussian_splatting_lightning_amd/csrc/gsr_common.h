@@ -417,6 +417,15 @@ __device__ __forceinline__ float4 stage_rec_a(float4 a) {  // (x, y, conic.x, co
 __device__ __forceinline__ float4 stage_rec_b(float4 b) {  // (conic.z, o, r, g) -> (C, o, r, g)
     return make_float4(b.x * NEG_HALF_LOG2E, b.y, b.z, b.w);
 }
+// One staged compositing record in LDS (48 B): both composite passes read a batch's instances from an array
+// of these with immediate offsets from one address.
+struct alignas(16) FwdRec {
+    float4 a;  // x, y, A, B (stage_rec_a)
+    float4 b;  // C, o, r, g (stage_rec_b)
+    float2 c;  // b, 1/depth
+    float2 pad;
+};
+
 __device__ __forceinline__ float power2_at(float C, float dy, float P0, float L) {
     return fmaf(dy, fmaf(C, dy, L), P0);
 }
@@ -514,12 +523,19 @@ __device__ __forceinline__ float dpp_mov(float old, float v) {
                                                       BANK_MASK, BOUND));
 }
 
-// v + (v moved across lanes by DPP CTRL).  No `old` operand: lanes outside ROW_MASK/BANK_MASK receive an
-// undefined value, so callers only read lanes the pattern fully defines.  Without an old value the compiler
-// folds the move into the add (v_add_f32_dpp) instead of zero-initialising a temporary first.
+// keep + (v moved across lanes by DPP CTRL).  With full row/bank masks and a pattern that defines every lane
+// (quad_perm, row_ror, row_mirror, row_half_mirror) bound_ctrl does not change the result, and it is what lets
+// the compiler fold the move into the add (one v_add_f32_dpp instead of v_mov_b32_dpp + v_add_f32).  Partial
+// masks keep the plain move: lanes outside ROW_MASK/BANK_MASK then receive an undefined value, so callers only
+// read lanes the pattern fully defines.
+template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf>
+__device__ __forceinline__ float dpp_xadd(float keep, float v) {
+    constexpr bool FULL = ROW_MASK == 0xf && BANK_MASK == 0xf;
+    return keep + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, ROW_MASK, BANK_MASK, FULL));
+}
 template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf>
 __device__ __forceinline__ float dpp_add(float v) {
-    return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, ROW_MASK, BANK_MASK, false));
+    return dpp_xadd<CTRL, ROW_MASK, BANK_MASK>(v, v);
 }
 
 // Sum over the 64 lanes (every lane must be active); the result is returned wave-uniform.
@@ -536,6 +552,11 @@ __device__ __forceinline__ float wave_sum(float v) {
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
     return v;
 }
 

@@ -657,12 +657,6 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_part_kernel(RenderF
 // array of 48-byte entries, read with immediate offsets from a single address.  Per instance this leaves the
 // dx / quadratic-form setup and the liveness ballot on the VALU (round-1 part kernel: ~19 VALU of per-instance
 // overhead besides the pixels).  The pixel update is that of composite_fwd, so outputs are bitwise identical.
-struct alignas(16) FwdRec {
-    float4 a;  // x, y, A, B (stage_rec_a)
-    float4 b;  // C, o, r, g (stage_rec_b)
-    float2 c;  // b, 1/depth
-    float2 pad;
-};
 
 template <int NPIX, int MIN_WAVES>
 __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v5_kernel(RenderFwdParams p) {

@@ -367,15 +367,16 @@ def test_densify_stats_from_backward(gpu_device):
 @pytest.mark.gpu
 @pytest.mark.parametrize("knobs", [{"fwd_strip": 1, "fwd_parts": 1}, {"fwd_parts": 2}, {"fwd_v": 4},
                                    {"fwd_v": 4, "fwd_parts": 2, "fwd_strip_parts": 0}, {"strip_exact": 0},
-                                   {"bwd_strip": 0},
-                                   {"bwd_pred": 0}, {"bwd_pred": 1}, {"bwd_v": 3}, {"bwd_pair": 0},
-                                   {"bwd_parts": 2}, {"bwd_parts": 4}])
+                                   {"bwd_v": 4}, {"bwd_lastc": 0}, {"bwd_v": 4, "bwd_strip": 0},
+                                   {"bwd_v": 4, "bwd_pred": 0}, {"bwd_v": 4, "bwd_pred": 1}, {"bwd_v": 3},
+                                   {"bwd_v": 4, "bwd_pair": 0}, {"bwd_parts": 2}, {"bwd_parts": 4}])
 def test_composite_variants_are_bitwise_identical(gpu_device, knobs):
     """Strip skipping (row-band or exact column-band masks) only skips rows where every pixel fails
     alpha >= 1/255, the wave-uniform v5 forward performs composite_fwd's pixel update, and the predicated backward
     body performs the same operations as the branchy one, and a tile composited in 4 or 2 row-strip parts
     (the default at this size) or whole (with a 5 % share of split heavy tiles) gives the same pixels and
-    contributor counts: outputs and gradients must match bit for bit (with a non-zero background).  The v3
+    contributor counts, and the v5 backward's n_contrib strip bounds only skip strips and compares that cannot
+    contribute: outputs and gradients must match bit for bit (with a non-zero background).  The v3
     backward keeps the per-channel accumulators, and the parts backward adds its waves' per-instance sums:
     gradients agree to rounding only."""
     from gaussian_splatting_lightning_amd import _native
@@ -389,14 +390,14 @@ def test_composite_variants_are_bitwise_identical(gpu_device, knobs):
         alt = run_hip(inp, gpu_device, dc, di)
     finally:
         for k in knobs:
-            _native.set_tuning(k, {"fwd_strip": 0, "fwd_parts": 0, "bwd_strip": 1, "bwd_pred": 2, "bwd_v": 4,
+            _native.set_tuning(k, {"fwd_strip": 0, "fwd_parts": 0, "bwd_strip": 1, "bwd_pred": 2, "bwd_v": 5,
                                    "bwd_pair": 1, "bwd_parts": 0, "fwd_v": 5, "fwd_strip_parts": 1,
-                                   "strip_exact": 1}[k])
+                                   "strip_exact": 1, "bwd_lastc": 1}[k])
         _native.set_tuning("bwd_parts", 0)
     for k in ("color", "invdepth", "radii"):
         assert np.array_equal(ref[k], alt[k]), k
     for k in GRADS:
-        if "bwd_v" in knobs or "bwd_parts" in knobs:
+        if knobs.get("bwd_v") == 3 or "bwd_parts" in knobs:
             assert rel_l2(alt["grads"][k], ref["grads"][k]) <= 1e-5, k
         else:
             assert np.array_equal(ref["grads"][k], alt["grads"][k]), k

@@ -82,7 +82,7 @@ def main():
     strip_of = ly // 4
     quad_of = (ly // 8) * 2 + (lx // 8)
     tot = dict(strip_fn=0, strip_fn_miss=0, pairs=0, strip_band=0, quad_box=0, quad_exact=0, strip_exact=0, quad_active=0, strip_active=0,
-               active_pairs=0, fwd_pairs_tile=0)
+               active_pairs=0, fwd_pairs_tile=0, strip_fn_lastc=0, need_cmp=0, inst_dead=0)
     for t in tiles:
         tx, ty = t % gx, t // gx
         px, py = tx * 16 + lx, ty * 16 + ly
@@ -121,6 +121,14 @@ def main():
             tot["quad_active"] += int(act[:, quad_of == q].any(1).sum())
         sm = strip_mask_exact(m[:, 0], m[:, 1], c[:, 0], c[:, 1], c[:, 2], c[:, 3], r0y, r0x)
         tot["strip_fn"] += int(sm.sum())
+        tot["inst_dead"] += int((~act.any(1)).sum())
+        idx = np.arange(last)
+        for k in range(4):
+            lc = ncp[strip_of == k]
+            smax, smin = int(lc.max()), int(lc.min())
+            live = sm[:, k] & (idx < smax)
+            tot["strip_fn_lastc"] += int(live.sum())
+            tot["need_cmp"] += int((live & (idx >= smin)).sum())
         for k in range(4):
             tot["strip_fn_miss"] += int((ok[:, strip_of == k].any(1) & ~sm[:, k]).sum())
         for k in range(4):
@@ -130,7 +138,9 @@ def main():
     print(f"{args.config}: tiles {len(tiles)}, walked (tile, instance) pairs {tot['pairs'] // 256}, "
           f"active pixel pairs {tot['active_pairs']} ({tot['active_pairs'] / tot['pairs']:.3f} of walked)")
     print(f"  strip_mask_exact: misses {tot['strip_fn_miss']} (must be 0)")
-    for k in ("strip_band", "strip_fn", "strip_exact", "strip_active", "quad_box", "quad_exact", "quad_active"):
+    print(f"  walked instances contributing to no pixel: {tot['inst_dead'] / (tot['pairs'] // 256):.3f}; "
+          f"strip evaluations needing the n_contrib compare: {tot['need_cmp'] / max(tot['strip_fn_lastc'], 1):.3f}")
+    for k in ("strip_band", "strip_fn", "strip_fn_lastc", "strip_exact", "strip_active", "quad_box", "quad_exact", "quad_active"):
         print(f"  {k:12s} live cells {tot[k]:>12d}  {tot[k] / cells:.3f} of all, "
               f"active-pixel density {tot['active_pairs'] / max(tot[k] * 64, 1):.3f}")
 
