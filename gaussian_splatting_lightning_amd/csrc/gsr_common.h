@@ -417,6 +417,17 @@ __device__ __forceinline__ float4 stage_rec_a(float4 a) {  // (x, y, conic.x, co
 __device__ __forceinline__ float4 stage_rec_b(float4 b) {  // (conic.z, o, r, g) -> (C, o, r, g)
     return make_float4(b.x * NEG_HALF_LOG2E, b.y, b.z, b.w);
 }
+// Per-lane select by a wave lane mask held in scalar registers (e.g. from __builtin_amdgcn_fcmpf): one
+// v_cndmask_b32 that reads the mask directly, where `cond ? a : b` on a bool rebuilt from a mask would first
+// materialise it in a vector register.  Lanes outside exec are left undefined, as any VALU result.
+__device__ __forceinline__ float select_mask(uint64_t mask, float a, float b) {
+    float r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(mask));
+    return r;
+}
+// LLVM CmpInst predicates for __builtin_amdgcn_fcmpf
+constexpr int FCMP_OLT = 4, FCMP_OLE = 5, FCMP_UGE = 11;
+
 // One staged compositing record in LDS (48 B): both composite passes read a batch's instances from an array
 // of these with immediate offsets from one address.
 struct alignas(16) FwdRec {

@@ -769,6 +769,136 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v5_kernel(RenderFwd
     stamp_store(p.stamps, slot, t_start, lane);
 }
 
+// v6: v5 with a pixel's termination kept off the per-pair path.
+//   v5 marks a finished pixel by negating T and tests T > 0 for every (pixel, instance) pair, negates T with a
+//   select per pair, and ballots T > 0 after every instance.  Here a finished (or off-image) pixel gets a NaN row
+//   offset, so its exponent is NaN and the ordered `power2 <= 0` test already rejects it; T is never negated;
+//   the stop test's ballot guards a rare branch that retires the pixel and clears its lane from the strip's
+//   live mask (scalar), so a strip whose pixels have all finished is skipped like a dead cell, and the wave
+//   stops when no strip is live without any per-instance vector compare.  Same arithmetic on every pair that
+//   v5 evaluates with effect, so the same bits.
+template <int NPIX, int MIN_WAVES>
+__global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwdParams p) {
+    constexpr int PARTS = 4 / NPIX;
+    __shared__ FwdRec s_rec[4][64];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int slot = blockIdx.x * 4 + w;
+    if (slot >= p.num_tiles * PARTS) return;
+    const int half = slot % PARTS;
+    const int tile = __builtin_amdgcn_readfirstlane(p.tile_order ? (int)p.tile_order[slot / PARTS] : slot / PARTS);
+    const uint32_t t_start = p.stamps ? stamp_now() : 0u;
+    const int tx = tile % p.gx, ty = tile / p.gx;
+    const int px = tx * BLOCK_X + (lane & 15);
+    const int py0 = ty * BLOCK_Y + (lane >> 4);
+    const float pfx = (float)px, pfy0 = (float)py0;
+    const float row0 = (float)(ty * BLOCK_Y), col0 = (float)(tx * BLOCK_X);
+    const int kbase = NPIX * half;  // whole-tile pixel index of this wave's first pixel
+    float T[NPIX], C0[NPIX], C1[NPIX], C2[NPIX], ID[NPIX], off[NPIX];
+    uint32_t last[NPIX];
+    uint64_t livek[NPIX];  // lanes whose pixel k still composites (wave-uniform)
+#pragma unroll
+    for (int k = 0; k < NPIX; k++) {
+        const int py = py0 + 4 * (kbase + k);
+        const bool inside = px < p.W && py < p.H;
+        off[k] = inside ? (float)(4 * (kbase + k)) : __builtin_nanf("");
+        livek[k] = __ballot(inside);
+        T[k] = 1.0f;
+        C0[k] = C1[k] = C2[k] = ID[k] = 0.f;
+        last[k] = 0;
+    }
+    const uint2 rg = p.ranges[tile];
+    const uint32_t r0 = __builtin_amdgcn_readfirstlane(rg.x), r1 = __builtin_amdgcn_readfirstlane(rg.y);
+    uint32_t contributor = 0;
+    uint32_t loaded_end = r0;
+    FwdRec *sr = s_rec[w];
+    for (uint32_t base = r0; base < r1; base += 64) {
+        uint64_t anylive = 0;
+#pragma unroll
+        for (int k = 0; k < NPIX; k++) anylive |= livek[k];
+        if (anylive == 0) break;
+        const uint32_t s = base + lane;
+        uint32_t m = 0;
+        if (s < r1) {
+            const uint32_t u = p.sorted_u[s];
+            const uint32_t gid = p.inst_gid[u];
+            p.point_list[s] = gid;
+            p.inv[u] = s;
+            const float4 ga = p.rec_a[gid], gb = p.rec_b[gid];
+            sr[lane].a = stage_rec_a(ga);
+            sr[lane].b = stage_rec_b(gb);
+            sr[lane].c = p.rec_c[gid];
+            m = cell_mask(p.strip_exact, ga, gb, row0, col0) >> kbase;
+        }
+        uint64_t sk[NPIX];
+#pragma unroll
+        for (int k = 0; k < NPIX; k++) sk[k] = __ballot((m >> k) & 1u);
+        loaded_end = min(r1, base + 64u);
+        wave_lds_sync();
+        const uint32_t cnt = min(64u, r1 - base);
+        for (uint32_t j = 0; j < cnt; j++) {
+            const float4 a = sr[j].a, b = sr[j].b;
+            const float2 c = sr[j].c;
+            contributor++;
+            const float dx = a.x - pfx, dy0 = a.y - pfy0;
+            const float P0 = (a.z * dx) * dx, L = a.w * dx;
+#pragma unroll
+            for (int k = 0; k < NPIX; k++) {
+                if (!((sk[k] >> j) & 1u) || livek[k] == 0) continue;  // wave-uniform
+                const float power2 = power2_at(b.x, dy0 - off[k], P0, L);
+                const float alpha = fminf(0.99f, b.y * __builtin_amdgcn_exp2f(power2));
+                const float test_T = T[k] * (1 - alpha);
+                // lane masks straight from the compares (scalar registers): ok = power2 <= 0 (ordered, so false
+                // for a retired pixel's NaN exponent; power2 is never NaN otherwise) and !(alpha < 1/255)
+                const uint64_t ok = __builtin_amdgcn_fcmpf(power2, 0.0f, FCMP_OLE) &
+                                    __builtin_amdgcn_fcmpf(alpha, 1.0f / 255.0f, FCMP_UGE);
+                const uint64_t low = __builtin_amdgcn_fcmpf(test_T, 0.0001f, FCMP_OLT);
+                const uint64_t take = ok & ~low, stop = ok & low;
+                const float wgt = select_mask(take, alpha * T[k], 0.f);
+                C0[k] = fmaf(b.z, wgt, C0[k]);
+                C1[k] = fmaf(b.w, wgt, C1[k]);
+                C2[k] = fmaf(c.x, wgt, C2[k]);
+                ID[k] = fmaf(c.y, wgt, ID[k]);
+                T[k] = select_mask(take, test_T, T[k]);
+                last[k] = __float_as_uint(select_mask(take, __uint_as_float(contributor), __uint_as_float(last[k])));
+                if (stop) {  // rare: some pixels of the strip reach T < 1e-4 and retire
+                    off[k] = select_mask(stop, __builtin_nanf(""), off[k]);
+                    livek[k] &= ~stop;
+                }
+            }
+            uint64_t anylive = 0;
+#pragma unroll
+            for (int k = 0; k < NPIX; k++) anylive |= livek[k];
+            if (anylive == 0) break;
+        }
+        wave_lds_sync();
+    }
+    const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
+    const size_t HW = (size_t)p.W * p.H;
+    uint32_t mx = 0;
+#pragma unroll
+    for (int k = 0; k < NPIX; k++) {
+        const int py = py0 + 4 * (kbase + k);
+        if (px < p.W && py < p.H) {
+            const size_t pid = (size_t)py * p.W + px;
+            const float Tk = T[k];
+            p.final_T[pid] = Tk;
+            p.n_contrib[pid] = last[k];
+            p.out_color[pid] = C0[k] + Tk * bg0;
+            p.out_color[HW + pid] = C1[k] + Tk * bg1;
+            p.out_color[2 * HW + pid] = C2[k] + Tk * bg2;
+            if (p.out_invdepth) p.out_invdepth[pid] = ID[k];
+            mx = max(mx, last[k]);
+        }
+    }
+    mx = wave_max_u32(mx);
+    if (lane == 0) {
+        atomicMax(&p.tile_last[tile], mx);
+        atomicMax(&p.tile_loaded[tile], loaded_end - r0);
+    }
+    stamp_store(p.stamps, slot, t_start, lane);
+}
+
 void launch_render_fwd(hipStream_t s, const RenderFwdParams &p0) {
     if (p0.num_tiles <= 0) return;
     RenderFwdParams p = p0;
@@ -786,7 +916,15 @@ void launch_render_fwd(hipStream_t s, const RenderFwdParams &p0) {
         const int mw = tuning("fwd_part_waves", 8);
         // "fwd_v" 5 (default): render_fwd_v5_kernel (wave-uniform control, always strip skipping); 4: the
         // composite_fwd part kernel, with "fwd_strip_parts" 1 skipping dead strips (cell_mask)
-        if (tuning("fwd_v", 5) == 5) {
+        const int fv = tuning("fwd_v", 6);
+        if (fv == 6) {  // render_fwd_v6_kernel: retired pixels off the per-pair path
+            if (parts == 2 && mw >= 8) render_fwd_v6_kernel<2, 8><<<grid, block, 0, s>>>(q);
+            else if (parts == 2) render_fwd_v6_kernel<2, 4><<<grid, block, 0, s>>>(q);
+            else if (mw >= 8) render_fwd_v6_kernel<1, 8><<<grid, block, 0, s>>>(q);
+            else render_fwd_v6_kernel<1, 4><<<grid, block, 0, s>>>(q);
+            return;
+        }
+        if (fv == 5) {
             if (parts == 2 && mw >= 8) render_fwd_v5_kernel<2, 8><<<grid, block, 0, s>>>(q);
             else if (parts == 2) render_fwd_v5_kernel<2, 4><<<grid, block, 0, s>>>(q);
             else if (mw >= 8) render_fwd_v5_kernel<1, 8><<<grid, block, 0, s>>>(q);
