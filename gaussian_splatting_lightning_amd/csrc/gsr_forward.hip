@@ -813,10 +813,6 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
     uint32_t loaded_end = r0;
     FwdRec *sr = s_rec[w];
     for (uint32_t base = r0; base < r1; base += 64) {
-        uint64_t anylive = 0;
-#pragma unroll
-        for (int k = 0; k < NPIX; k++) anylive |= livek[k];
-        if (anylive == 0) break;
         const uint32_t s = base + lane;
         uint32_t m = 0;
         if (s < r1) {
@@ -832,11 +828,12 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
         }
         uint64_t sk[NPIX];
 #pragma unroll
-        for (int k = 0; k < NPIX; k++) sk[k] = __ballot((m >> k) & 1u);
+        for (int k = 0; k < NPIX; k++) sk[k] = livek[k] ? __ballot((m >> k) & 1u) : 0ull;  // finished strips: none
         loaded_end = min(r1, base + 64u);
         wave_lds_sync();
-        const uint32_t cnt = min(64u, r1 - base);
-        for (uint32_t j = 0; j < cnt; j++) {
+        uint32_t cnt = min(64u, r1 - base);
+        uint64_t bit = 1;  // 1 << j
+        for (uint32_t j = 0; j < cnt; j++, bit <<= 1) {
             const float4 a = sr[j].a, b = sr[j].b;
             const float2 c = sr[j].c;
             contributor++;
@@ -844,7 +841,7 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
             const float P0 = (a.z * dx) * dx, L = a.w * dx;
 #pragma unroll
             for (int k = 0; k < NPIX; k++) {
-                if (!((sk[k] >> j) & 1u) || livek[k] == 0) continue;  // wave-uniform
+                if (!(sk[k] & bit)) continue;  // wave-uniform
                 const float power2 = power2_at(b.x, dy0 - off[k], P0, L);
                 const float alpha = fminf(0.99f, b.y * __builtin_amdgcn_exp2f(power2));
                 const float test_T = T[k] * (1 - alpha);
@@ -864,14 +861,21 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
                 if (stop) {  // rare: some pixels of the strip reach T < 1e-4 and retire
                     off[k] = select_mask(stop, __builtin_nanf(""), off[k]);
                     livek[k] &= ~stop;
+                    if (livek[k] == 0) {  // the whole strip finished: skip it for the rest of the batch
+                        sk[k] = 0;
+                        uint64_t anylive = 0;
+#pragma unroll
+                        for (int q = 0; q < NPIX; q++) anylive |= livek[q];
+                        if (anylive == 0) cnt = j + 1;  // every pixel of the wave finished: end the walk
+                    }
                 }
             }
-            uint64_t anylive = 0;
-#pragma unroll
-            for (int k = 0; k < NPIX; k++) anylive |= livek[k];
-            if (anylive == 0) break;
         }
         wave_lds_sync();
+        uint64_t anylive = 0;
+#pragma unroll
+        for (int k = 0; k < NPIX; k++) anylive |= livek[k];
+        if (anylive == 0) break;
     }
     const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
     const size_t HW = (size_t)p.W * p.H;
