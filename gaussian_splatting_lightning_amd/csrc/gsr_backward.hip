@@ -829,11 +829,186 @@ __global__ __launch_bounds__(64, 5) void render_bwd_v5_kernel(RenderBwdParams p)
     stamp_store(p.stamps, slot, t_start, lane);
 }
 
+// v6: v5 with the per-pair control on scalar masks, no exec branching.
+//   render_bwd is bound by the issue of its vector AND scalar instructions (the scalar unit is shared by the CU's
+//   four SIMDs: ~1.8 ns per SALU instruction per SIMD against ~1.3 ns per VALU one, tools/probes/valu_rate_probe.hip).
+//   v5's exec branch per live strip costs ~7 scalar instructions (mask merges, saveexec, the branch, the exec
+//   restore, the contributor flag) and its contributor ballot two vector ones per instance.  Here the three tests
+//   are compares into scalar masks (uicmp / fcmpf builtins), the update is predicated by two selects on the mask
+//   (alpha and q forced to 0: every accumulator is then bitwise unchanged), and the instance's "any lane
+//   contributed" test is the OR of the masks.  Gradients are bitwise those of v4 / v5.
+//   Measured at cfg 3: SALU 56 M -> 45 M but VALU 192 M -> 206 M (the selects, and the rcp no longer skipped when
+//   no lane contributes): 0.341 against v5's 0.327 ms, so v5 stays the default ("bwd_v" 6 selects this one).
+//   The backward is VALU-bound; the scalar cost decides only in the forward (render_fwd_v6_kernel).
+template <bool HAS_INV>
+__global__ __launch_bounds__(64, 5) void render_bwd_v6_kernel(RenderBwdParams p) {
+    __shared__ FwdRec s_rec[BWD_BATCH];
+    __shared__ __attribute__((aligned(16))) float s_part[BWD_BATCH][PART];  // [instance][10 sums]
+    const int lane = threadIdx.x;
+    const int slot = blockIdx.x;
+    const uint32_t t_start = p.stamps ? stamp_now() : 0u;
+    const int tile = __builtin_amdgcn_readfirstlane(p.tile_order ? (int)p.tile_order[slot] : slot);
+    const int tx = tile % p.gx, ty = tile / p.gx;
+    const int px = tx * BLOCK_X + (lane & 15);
+    const int py0 = ty * BLOCK_Y + (lane >> 4);
+    const float pfx = (float)px, pfy0 = (float)py0;
+    const float row0 = (float)(ty * BLOCK_Y), col0 = (float)(tx * BLOCK_X);
+    const uint2 range = p.ranges[tile];
+    const uint32_t r0 = __builtin_amdgcn_readfirstlane(range.x);
+    const uint32_t tl = __builtin_amdgcn_readfirstlane(p.tile_last[tile]);
+    const uint32_t loaded = __builtin_amdgcn_readfirstlane(p.tile_loaded[tile]);
+    for (uint32_t s = r0 + tl + lane; s < r0 + loaded; s += 64) {
+        const float z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        store_row(p.rows, p.rows_by_u ? p.sorted_u[s] : s, z);
+    }
+    if (tl == 0) {
+        stamp_store(p.stamps, slot, t_start, lane);
+        return;
+    }
+
+    const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
+    const size_t HW = (size_t)p.W * p.H;
+    float T[PIX_PER_LANE], dp0[PIX_PER_LANE], dp1[PIX_PER_LANE], dp2[PIX_PER_LANE], dinv[PIX_PER_LANE];
+    float D[PIX_PER_LANE];
+    uint32_t lastc[PIX_PER_LANE];
+#pragma unroll
+    for (int k = 0; k < PIX_PER_LANE; k++) {
+        const int py = py0 + 4 * k;
+        const bool inside = px < p.W && py < p.H;
+        const size_t pid = inside ? (size_t)py * p.W + px : 0;
+        T[k] = inside ? p.final_T[pid] : 0.f;
+        lastc[k] = inside ? p.n_contrib[pid] : 0u;
+        dp0[k] = inside ? p.dL_dpix[pid] : 0.f;
+        dp1[k] = inside ? p.dL_dpix[HW + pid] : 0.f;
+        dp2[k] = inside ? p.dL_dpix[2 * HW + pid] : 0.f;
+        dinv[k] = (HAS_INV && inside) ? p.dL_dinvdepth[pid] : 0.f;
+        D[k] = fmaf(bg2, dp2[k], fmaf(bg1, dp1[k], bg0 * dp0[k]));
+    }
+    const float hW = 0.5f * p.W, hH = 0.5f * p.H;
+
+    for (int bend = (int)tl; bend > 0; bend -= BWD_BATCH) {
+        const int cnt = min(BWD_BATCH, bend);
+        float4 my_a = make_float4(0, 0, 0, 0), my_b = my_a;
+        uint32_t my_row = 0, my_m = 0;
+        if (lane < cnt) {
+            const uint32_t s_me = r0 + (uint32_t)(bend - 1 - lane);
+            my_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
+            const uint32_t gid = p.point_list[s_me];
+            my_a = p.rec_a[gid];
+            my_b = p.rec_b[gid];
+            s_rec[lane].a = stage_rec_a(my_a);
+            s_rec[lane].b = stage_rec_b(my_b);
+            s_rec[lane].c = p.rec_c[gid];
+            my_m = cell_mask(p.strip_exact, my_a, my_b, row0, col0);
+        }
+        // sk[k] bit j: strip k of instance j (idx = bend - 1 - j) may hold a contributing pixel (the batch's 32
+        // instances fit the low half of the ballot)
+        uint32_t sk[PIX_PER_LANE];
+#pragma unroll
+        for (int k = 0; k < PIX_PER_LANE; k++) sk[k] = (uint32_t)__ballot((my_m >> k) & 1u);
+        wave_lds_sync();
+        // one instance's pass over the lane's pixels: updates T / D, returns the 10 per-lane sums in m and the
+        // ballot of the lanes that contributed
+        auto pass = [&](const int j, float m[10]) -> uint64_t {
+            const uint32_t idx = (uint32_t)(bend - 1 - j);
+            const FwdRec &r = s_rec[j];
+            const float4 a = r.a, b = r.b;  // a: x, y, A, B; b: C, o, r, g
+            const float2 c = r.c;           // b, 1/depth
+            const float dx = a.x - pfx, dy0 = a.y - pfy0;
+            const float P0 = (a.z * dx) * dx, L = a.w * dx;
+            float Q0 = 0.f, Q1 = 0.f, Q2 = 0.f, w0 = 0.f, w1 = 0.f, w2 = 0.f, w3 = 0.f;
+            uint64_t any = 0;
+#pragma unroll
+            for (int k = 0; k < PIX_PER_LANE; k++) {
+                if (!((sk[k] >> j) & 1u)) continue;  // wave-uniform
+                const float dy = dy0 - (float)(4 * k);
+                const float power2 = power2_at(b.x, dy, P0, L);
+                const float G = __builtin_amdgcn_exp2f(power2);
+                const float alpha = fminf(0.99f, b.y * G);
+                // the contributing lanes, as a scalar mask: idx < n_contrib, !(power2 > 0), !(alpha < 1/255)
+                const uint64_t ok = __builtin_amdgcn_uicmp(idx, lastc[k], ICMP_ULT) &
+                                    __builtin_amdgcn_fcmpf(power2, 0.0f, FCMP_ULE) &
+                                    __builtin_amdgcn_fcmpf(alpha, 1.0f / 255.0f, FCMP_UGE);
+                any |= ok;
+                // predicated update: al = 0 leaves T, D and every sum bitwise unchanged (rcp(1) = 1, x + 0 = x)
+                const float al = select_mask(ok, alpha, 0.f);
+                T[k] = T[k] * fast_rcp(1.f - al);
+                const float wgt = al * T[k];
+                float cd = fmaf(c.x, dp2[k], fmaf(b.w, dp1[k], b.z * dp0[k]));
+                if (HAS_INV) cd = fmaf(c.y, dinv[k], cd);
+                const float d = cd - D[k];
+                D[k] = fmaf(al, d, D[k]);
+                w0 = fmaf(wgt, dp0[k], w0);
+                w1 = fmaf(wgt, dp1[k], w1);
+                w2 = fmaf(wgt, dp2[k], w2);
+                if (HAS_INV) w3 = fmaf(wgt, dinv[k], w3);
+                const float q = select_mask(ok, G * (d * T[k]), 0.f);
+                const float qdy = q * dy;
+                Q0 += q;
+                Q1 += qdy;
+                Q2 = fmaf(qdy, dy, Q2);
+            }
+            m[0] = Q0;
+            m[1] = Q0 * dx;
+            m[2] = Q1;
+            m[3] = m[1] * dx;
+            m[4] = Q1 * dx;
+            m[5] = Q2;
+            m[6] = w0;
+            m[7] = w1;
+            m[8] = w2;
+            m[9] = w3;
+            return any;
+        };
+        for (int j = 0; j < cnt; j += 2) {
+            float m0[10];
+            const uint64_t any0 = pass(j, m0);
+            float *dst = s_part[j];
+            if (j + 1 < cnt) {
+                float m1[10];
+                const uint64_t any1 = pass(j + 1, m1);
+                if (any0 | any1) {
+                    wave_reduce20_store(m0, m1, dst, lane);
+                } else if (lane < 10) {
+                    dst[lane] = 0.f;
+                    dst[PART + lane] = 0.f;
+                }
+            } else if (any0) {
+                wave_reduce10_store(m0, dst, lane);
+            } else if (lane < 10) {
+                dst[lane] = 0.f;
+            }
+        }
+        wave_lds_sync();
+        if (lane < cnt) {
+            const float4 *src = reinterpret_cast<const float4 *>(s_part[lane]);
+            const float4 u0 = src[0], u1 = src[1];
+            const float2 u2 = *reinterpret_cast<const float2 *>(s_part[lane] + 8);
+            const float S = u0.x, Sx = u0.y, Sy = u0.z, Sxx = u0.w, Sxy = u1.x, Syy = u1.y;
+            const float o = my_b.y, ca = my_a.z, cb = my_a.w, cc = my_b.x;
+            float row[10];
+            row[0] = -o * hW * (ca * Sx + cb * Sy);
+            row[1] = -o * hH * (cb * Sx + cc * Sy);
+            row[2] = -0.5f * o * Sxx;
+            row[3] = -0.5f * o * Sxy;
+            row[4] = -0.5f * o * Syy;
+            row[5] = S;
+            row[6] = u1.z;
+            row[7] = u1.w;
+            row[8] = u2.x;
+            row[9] = u2.y;
+            store_row(p.rows, my_row, row);
+        }
+        wave_lds_sync();
+    }
+    stamp_store(p.stamps, slot, t_start, lane);
+}
+
 void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
     if (p.num_tiles <= 0) return;
     const int minw = tuning("bwd_minwaves", 5), wpb = tuning("bwd_wpb", 1);
-    const int bv = tuning("bwd_v", 5);
-    if (bv == 5 || bv == 4) {
+    const int bv = tuning("bwd_v", 5);  // 6 measured slower: 0.341 vs 0.327 ms (+7 % VALU, -20 % SALU)
+    if (bv >= 4) {
         RenderBwdParams q = p;
         q.strip_exact = tuning("strip_exact", 1);
         q.prio_div = tuning("prio_div", 0);
@@ -854,6 +1029,11 @@ void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
             return;
         }
         const dim3 grid(p.num_tiles), block(64);
+        if (bv == 6) {
+            if (p.dL_dinvdepth) render_bwd_v6_kernel<true><<<grid, block, 0, s>>>(q);
+            else render_bwd_v6_kernel<false><<<grid, block, 0, s>>>(q);
+            return;
+        }
         if (bv == 5) {  // "bwd_lastc" 1: strip liveness and compare skipping by n_contrib bounds (measured 2.5 % slower: SALU)
             const bool lc = tuning("bwd_lastc", 0) != 0;
             if (p.dL_dinvdepth) {

@@ -425,8 +425,8 @@ __device__ __forceinline__ float select_mask(uint64_t mask, float a, float b) {
     asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(mask));
     return r;
 }
-// LLVM CmpInst predicates for __builtin_amdgcn_fcmpf
-constexpr int FCMP_OLT = 4, FCMP_OLE = 5, FCMP_UGE = 11;
+// LLVM CmpInst predicates for __builtin_amdgcn_fcmpf / __builtin_amdgcn_uicmp
+constexpr int FCMP_OLT = 4, FCMP_OLE = 5, FCMP_UGE = 11, FCMP_ULE = 13, ICMP_ULT = 36;
 
 // One staged compositing record in LDS (48 B): both composite passes read a batch's instances from an array
 // of these with immediate offsets from one address.

@@ -368,7 +368,8 @@ def test_densify_stats_from_backward(gpu_device):
 @pytest.mark.parametrize("knobs", [{"fwd_strip": 1, "fwd_parts": 1}, {"fwd_parts": 2}, {"fwd_v": 4}, {"fwd_v": 5},
                                    {"fwd_v": 5, "fwd_parts": 4}, {"fwd_parts": 4}, {"fwd_parts": 1},
                                    {"fwd_v": 4, "fwd_parts": 2, "fwd_strip_parts": 0}, {"strip_exact": 0},
-                                   {"bwd_v": 4}, {"bwd_lastc": 0}, {"bwd_v": 4, "bwd_strip": 0},
+                                   {"bwd_v": 4}, {"bwd_v": 6}, {"bwd_lastc": 1},
+                                   {"bwd_v": 4, "bwd_strip": 0},
                                    {"bwd_v": 4, "bwd_pred": 0}, {"bwd_v": 4, "bwd_pred": 1}, {"bwd_v": 3},
                                    {"bwd_v": 4, "bwd_pair": 0}, {"bwd_parts": 2}, {"bwd_parts": 4}])
 def test_composite_variants_are_bitwise_identical(gpu_device, knobs):
@@ -377,8 +378,9 @@ def test_composite_variants_are_bitwise_identical(gpu_device, knobs):
     pixels by a NaN row offset instead of a negated T), and the predicated backward
     body performs the same operations as the branchy one, and a tile composited in 4 or 2 row-strip parts
     (the default at this size) or whole (with a 5 % share of split heavy tiles) gives the same pixels and
-    contributor counts, and the v5 backward's n_contrib strip bounds only skip strips and compares that cannot
-    contribute: outputs and gradients must match bit for bit (with a non-zero background).  The v3
+    contributor counts, the v5 backward's n_contrib strip bounds only skip strips and compares that cannot
+    contribute, and the v6 backward's select-predicated update leaves every accumulator bitwise unchanged on the
+    lanes it masks: outputs and gradients must match bit for bit (with a non-zero background).  The v3
     backward keeps the per-channel accumulators, and the parts backward adds its waves' per-instance sums:
     gradients agree to rounding only."""
     from gaussian_splatting_lightning_amd import _native
@@ -394,7 +396,7 @@ def test_composite_variants_are_bitwise_identical(gpu_device, knobs):
         for k in knobs:
             _native.set_tuning(k, {"fwd_strip": 0, "fwd_parts": 0, "bwd_strip": 1, "bwd_pred": 2, "bwd_v": 5,
                                    "bwd_pair": 1, "bwd_parts": 0, "fwd_v": 6, "fwd_strip_parts": 1,
-                                   "strip_exact": 1, "bwd_lastc": 1}[k])
+                                   "strip_exact": 1, "bwd_lastc": 0}[k])
         _native.set_tuning("bwd_parts", 0)
     for k in ("color", "invdepth", "radii"):
         assert np.array_equal(ref[k], alt[k]), k
