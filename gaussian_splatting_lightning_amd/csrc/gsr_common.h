@@ -98,6 +98,7 @@ struct GeomState {
     uint32_t *depth_key;   // P: float bits of view depth, 0xffffffff if culled
     uint32_t *tiles;       // P: tiles touched
     uint8_t *clamped;      // P: bit c set if SH colour channel c was clamped at 0
+    float *sh_jac;         // 9 x P: d rgb / d (unit view direction), planes [axis][channel] (SH degree > 0 only)
     uint4 *exp_rec;        // P: expansion record {kept-tile mask lo, hi, rmin.x | rmin.y << 16, rect width}; mask 0 =
                            //    all tiles of the rect (area > 64 or culling off).  One 16-B gather per Gaussian.
     uint32_t *inst_off;    // P+1: radix path: exclusive scan of tiles in depth order, [P] = total
@@ -124,6 +125,7 @@ inline size_t carve_geom(char *base, int P, GeomState &g) {
     g.rec_c = c.take<float2>(n);
     g.tiles = c.take<uint32_t>(n);
     g.clamped = c.take<uint8_t>(n);
+    g.sh_jac = c.take<float>((size_t)9 * n);
     g.exp_rec = c.take<uint4>(n);
     g.inst_off = c.take<uint32_t>((size_t)n + 1);
     g.inst_start = c.take<uint32_t>((size_t)n + 1);

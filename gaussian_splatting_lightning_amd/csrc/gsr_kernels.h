@@ -157,6 +157,7 @@ struct PreprocessBwdParams {
     const uint32_t *tiles, *inst_start, *inv, *big_slot;
     int rows_by_u;
     const uint8_t *clamped;
+    const float *sh_jac;  // 9 x P direction Jacobian of the colour, from the forward (SH degree > 0)
     const float *rows, *bigsum;
     float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales, *dL_drot;
     float *dL_dcolors_sh;  // clamp-masked colour gradient (may be null)

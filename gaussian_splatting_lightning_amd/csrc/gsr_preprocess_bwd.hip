@@ -222,6 +222,9 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
     dm.y += (pm[4] * m_w - pm[7] * mul1) * g2x + (pm[5] * m_w - pm[7] * mul2) * g2y;
     dm.z += (pm[8] * m_w - pm[11] * mul1) * g2x + (pm[9] * m_w - pm[11] * mul2) * g2y;
     // ---- SH backward ----
+    // dL/dsh = basis(dir) (x) dRGB needs only the direction; the direction term of dL/dmeans3D uses the colour's
+    // direction Jacobian the forward stored (sh_jac), so the 48 coefficients are not read here.  (The backward's
+    // shs are the forward's, as in the autograd function and the upstream API.)
     if (p.shs && p.M > 0) {
         const uint8_t cl = p.clamped[i];
         const float3 dRGB = make_float3((cl & 1) ? 0.f : gs[6], (cl & 2) ? 0.f : gs[7], (cl & 4) ? 0.f : gs[8]);
@@ -231,36 +234,29 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
             p.dL_dcolors_sh[3 * i + 1] = dRGB.y;
             p.dL_dcolors_sh[3 * i + 2] = dRGB.z;
         }
+        float3 jx = make_float3(0, 0, 0), jy = jx, jz = jx;
+        if (p.D > 0) {
+            const size_t n = (size_t)p.P;
+            const float *J = p.sh_jac + i;
+            jx = make_float3(J[0], J[n], J[2 * n]);
+            jy = make_float3(J[3 * n], J[4 * n], J[5 * n]);
+            jz = make_float3(J[6 * n], J[7 * n], J[8 * n]);
+        }
         float *dsh = p.dL_dsh ? p.dL_dsh + (size_t)i * ncoef : nullptr;  // null only with dL_dcolors_sh (API)
-        const float *shp = p.shs + (size_t)i * ncoef;
         if (LDS) {
-            // LDS-staged block (M = 16): dL/dsh replaces the coefficients in place for the coalesced store
-            dm = dm + sh_backward_inplace_dispatch(p.D, dsh_out, mean - campos, dRGB);
-        } else if (p.sh_vec16) {
-            // 16 coefficients x 3 = 192 B per Gaussian: 12 float4 loads and stores per lane
-            float shv[48], dshv[48];
-            const float4 *s4 = reinterpret_cast<const float4 *>(shp);
-#pragma unroll
-            for (int k = 0; k < 12; k++) {
-                const float4 q = s4[k];
-                shv[4 * k] = q.x; shv[4 * k + 1] = q.y; shv[4 * k + 2] = q.z; shv[4 * k + 3] = q.w;
-            }
-#pragma unroll
-            for (int k = 0; k < 48; k++) dshv[k] = 0.f;
-            dm = dm + sh_backward_dispatch(p.D, shv, mean - campos, dRGB, dshv);
-            if (dsh) {
+            // LDS-staged block (M = 16): dL/dsh goes to the lane's slot for the coalesced store
+            dm = dm + sh_backward_jac_dispatch(p.D, mean - campos, dRGB, jx, jy, jz, dsh_out);
+        } else {
+            float dshv[48];
+            dm = dm + sh_backward_jac_dispatch(p.D, mean - campos, dRGB, jx, jy, jz, dshv);
+            if (dsh && p.sh_vec16) {
                 float4 *d4 = reinterpret_cast<float4 *>(dsh);
 #pragma unroll
                 for (int k = 0; k < 12; k++)
                     d4[k] = make_float4(dshv[4 * k], dshv[4 * k + 1], dshv[4 * k + 2], dshv[4 * k + 3]);
+            } else if (dsh) {
+                for (int k = 0; k < ncoef; k++) dsh[k] = k < 48 ? dshv[k] : 0.f;
             }
-        } else if (dsh) {
-            dm = dm + sh_backward_dispatch(p.D, shp, mean - campos, dRGB, dsh);
-            const int used = (p.D + 1) * (p.D + 1) * 3;
-            for (int k = used; k < ncoef; k++) dsh[k] = 0.f;
-        } else {
-            float dtmp[48];  // dL/dsh discarded (compact multi-view mode); only the direction term is kept
-            dm = dm + sh_backward_dispatch(p.D, shp, mean - campos, dRGB, dtmp);
         }
     }
     if (p.dL_dmeans3D) {
@@ -282,12 +278,11 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
     }
 }
 
-// The SH coefficients (192 B per Gaussian at M = 16) are read and dL/dsh written through LDS: a wave moves
-// its 64 Gaussians' 12 KB block with coalesced float4 accesses, instead of 12 float4 accesses per lane strided
-// by 192 B, which cost ~40 % of the kernel.  In LDS each Gaussian's 48 floats sit at a 52-float stride, so
-// both the linear block copies (ds_write/read_b128 of consecutive lanes) and each lane's 12 float4 accesses
-// to its own Gaussian (52 = 4 x 13, 13 odd: 16 lanes of a b128 lane group hit 16 distinct 4-bank windows)
-// are free of bank conflicts.
+// dL/dsh (192 B per Gaussian at M = 16) is written through LDS: a wave moves its 64 Gaussians' 12 KB block
+// with coalesced float4 stores, instead of 12 float4 stores per lane strided by 192 B.  In LDS each Gaussian's
+// 48 floats sit at a 52-float stride, so both the linear block copy (ds_read_b128 of consecutive lanes) and
+// each lane's 12 float4 writes to its own Gaussian (52 = 4 x 13, 13 odd: 16 lanes of a b128 lane group hit 16
+// distinct 4-bank windows) are free of bank conflicts.  The coefficients themselves are not read (sh_jac).
 constexpr int SH_STRIDE = 52;
 template <bool LDS_SH>
 __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams p) {
@@ -371,16 +366,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
             wave_lds_sync();
         }
     }
-#pragma unroll
-    for (int c = 0; c < 12; c++) {
-        const uint32_t f = c * 256 + lane * 4;
-        if (gbase + f < gend) {
-            const float4 v = *reinterpret_cast<const float4 *>(p.shs + gbase + f);
-            *reinterpret_cast<float4 *>(sw + (f / 48) * SH_STRIDE + f % 48) = v;
-        }
-    }
-    wave_lds_sync();
-    // each lane's 48 coefficients are read and replaced by dL/dsh in its LDS slot
+    // each lane writes its Gaussian's dL/dsh into its LDS slot (the row chunks above are done with the area)
     if (i < p.P) preprocess_bwd_one<true>(p, i, nullptr, sw + lane * SH_STRIDE, p.rows_by_u != 0, gs);
     if (!p.dL_dsh) return;
     wave_lds_sync();

@@ -45,6 +45,54 @@ __device__ __forceinline__ float3 sh_dispatch(int deg, const float *__restrict__
     }
 }
 
+// Colour and its Jacobian with respect to the unit view direction, in one pass over the coefficients:
+// jx = d rgb / d dir.x (one float3 over the colour channels), likewise jy, jz.  The forward stores the Jacobian
+// (9 floats per Gaussian) so the backward forms dL/ddir = (jx . dRGB, jy . dRGB, jz . dRGB) without reading
+// the 48 coefficients again; the expressions are sh_backward's, so the product is bitwise the same.
+template <int DEG>
+__device__ __forceinline__ float3 sh_eval_jac(const float *__restrict__ sh, float3 dir, float3 &jx, float3 &jy,
+                                              float3 &jz) {
+    const float3 res = sh_eval<DEG>(sh, dir);
+    jx = jy = jz = make_float3(0, 0, 0);
+    const float x = dir.x, y = dir.y, z = dir.z;
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    if (DEG > 0) {
+        jx = -GSR_SH_C1 * f3(sh + 9);
+        jy = -GSR_SH_C1 * f3(sh + 3);
+        jz = GSR_SH_C1 * f3(sh + 6);
+        if (DEG > 1) {
+            const float3 s4 = f3(sh + 12), s5 = f3(sh + 15), s6 = f3(sh + 18), s7 = f3(sh + 21), s8 = f3(sh + 24);
+            jx = jx + (SH_C2[0] * y) * s4 + (SH_C2[2] * 2.f * -x) * s6 + (SH_C2[3] * z) * s7 + (SH_C2[4] * 2.f * x) * s8;
+            jy = jy + (SH_C2[0] * x) * s4 + (SH_C2[1] * z) * s5 + (SH_C2[2] * 2.f * -y) * s6 + (SH_C2[4] * 2.f * -y) * s8;
+            jz = jz + (SH_C2[1] * y) * s5 + (SH_C2[2] * 2.f * 2.f * z) * s6 + (SH_C2[3] * x) * s7;
+            if (DEG > 2) {
+                const float3 s9 = f3(sh + 27), s10 = f3(sh + 30), s11 = f3(sh + 33), s12 = f3(sh + 36),
+                             s13 = f3(sh + 39), s14 = f3(sh + 42), s15 = f3(sh + 45);
+                jx = jx + (SH_C3[0] * 3.f * 2.f * xy) * s9 + (SH_C3[1] * yz) * s10 + (SH_C3[2] * -2.f * xy) * s11 +
+                     (SH_C3[3] * -3.f * 2.f * xz) * s12 + (SH_C3[4] * (-3.f * xx + 4.f * zz - yy)) * s13 +
+                     (SH_C3[5] * 2.f * xz) * s14 + (SH_C3[6] * 3.f * (xx - yy)) * s15;
+                jy = jy + (SH_C3[0] * 3.f * (xx - yy)) * s9 + (SH_C3[1] * xz) * s10 +
+                     (SH_C3[2] * (-3.f * yy + 4.f * zz - xx)) * s11 + (SH_C3[3] * -3.f * 2.f * yz) * s12 +
+                     (SH_C3[4] * -2.f * xy) * s13 + (SH_C3[5] * -2.f * yz) * s14 + (SH_C3[6] * -3.f * 2.f * xy) * s15;
+                jz = jz + (SH_C3[1] * xy) * s10 + (SH_C3[2] * 4.f * 2.f * yz) * s11 +
+                     (SH_C3[3] * 3.f * (2.f * zz - xx - yy)) * s12 + (SH_C3[4] * 4.f * 2.f * xz) * s13 +
+                     (SH_C3[5] * (xx - yy)) * s14;
+            }
+        }
+    }
+    return res;
+}
+
+__device__ __forceinline__ float3 sh_eval_jac_dispatch(int deg, const float *__restrict__ sh, float3 dir, float3 &jx,
+                                                       float3 &jy, float3 &jz) {
+    switch (deg) {
+        case 0: return sh_eval_jac<0>(sh, dir, jx, jy, jz);
+        case 1: return sh_eval_jac<1>(sh, dir, jx, jy, jz);
+        case 2: return sh_eval_jac<2>(sh, dir, jx, jy, jz);
+        default: return sh_eval_jac<3>(sh, dir, jx, jy, jz);
+    }
+}
+
 __device__ __forceinline__ float3 dnormvdv(float3 v, float3 dv) {
     const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
     const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
@@ -174,6 +222,45 @@ __device__ __forceinline__ float3 sh_backward_inplace_dispatch(int deg, float *s
         case 1: return sh_backward_inplace<1>(sh_io, dir_orig, dRGB);
         case 2: return sh_backward_inplace<2>(sh_io, dir_orig, dRGB);
         default: return sh_backward_inplace<3>(sh_io, dir_orig, dRGB);
+    }
+}
+
+// The backward from the forward's direction Jacobian: writes dL/dsh[0..48) (zeros above the degree; the same
+// values as sh_backward_inplace) and returns dL/dmean through the view direction.  No coefficient is read.
+template <int DEG>
+__device__ __forceinline__ float3 sh_backward_jac(float3 dir_orig, float3 dRGB, float3 jx, float3 jy, float3 jz,
+                                                  float *__restrict__ dsh) {
+    const float len = sqrtf(dot3(dir_orig, dir_orig));
+    const float3 dir = make_float3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
+    const float x = dir.x, y = dir.y, z = dir.z;
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    const float3 zero = make_float3(0, 0, 0);
+    st3(dsh, GSR_SH_C0 * dRGB);
+    st3(dsh + 3, DEG > 0 ? (-GSR_SH_C1 * y) * dRGB : zero);
+    st3(dsh + 6, DEG > 0 ? (GSR_SH_C1 * z) * dRGB : zero);
+    st3(dsh + 9, DEG > 0 ? (-GSR_SH_C1 * x) * dRGB : zero);
+    st3(dsh + 12, DEG > 1 ? (SH_C2[0] * xy) * dRGB : zero);
+    st3(dsh + 15, DEG > 1 ? (SH_C2[1] * yz) * dRGB : zero);
+    st3(dsh + 18, DEG > 1 ? (SH_C2[2] * (2.f * zz - xx - yy)) * dRGB : zero);
+    st3(dsh + 21, DEG > 1 ? (SH_C2[3] * xz) * dRGB : zero);
+    st3(dsh + 24, DEG > 1 ? (SH_C2[4] * (xx - yy)) * dRGB : zero);
+    st3(dsh + 27, DEG > 2 ? (SH_C3[0] * y * (3.f * xx - yy)) * dRGB : zero);
+    st3(dsh + 30, DEG > 2 ? (SH_C3[1] * xy * z) * dRGB : zero);
+    st3(dsh + 33, DEG > 2 ? (SH_C3[2] * y * (4.f * zz - xx - yy)) * dRGB : zero);
+    st3(dsh + 36, DEG > 2 ? (SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy)) * dRGB : zero);
+    st3(dsh + 39, DEG > 2 ? (SH_C3[4] * x * (4.f * zz - xx - yy)) * dRGB : zero);
+    st3(dsh + 42, DEG > 2 ? (SH_C3[5] * z * (xx - yy)) * dRGB : zero);
+    st3(dsh + 45, DEG > 2 ? (SH_C3[6] * x * (xx - 3.f * yy)) * dRGB : zero);
+    const float3 dL_ddir = make_float3(dot3(jx, dRGB), dot3(jy, dRGB), dot3(jz, dRGB));
+    return dnormvdv(dir_orig, dL_ddir);
+}
+__device__ __forceinline__ float3 sh_backward_jac_dispatch(int deg, float3 dir_orig, float3 dRGB, float3 jx, float3 jy,
+                                                           float3 jz, float *dsh) {
+    switch (deg) {
+        case 0: return sh_backward_jac<0>(dir_orig, dRGB, jx, jy, jz, dsh);
+        case 1: return sh_backward_jac<1>(dir_orig, dRGB, jx, jy, jz, dsh);
+        case 2: return sh_backward_jac<2>(dir_orig, dRGB, jx, jy, jz, dsh);
+        default: return sh_backward_jac<3>(dir_orig, dRGB, jx, jy, jz, dsh);
     }
 }
 
