@@ -51,11 +51,12 @@ __device__ __forceinline__ void cov3d_backward(float3 scale, float mod, float4 r
              4 * z * (dMt[1][1] + dMt[0][0]);
 }
 
-// One Gaussian.  With sh_in (the LDS-staged path) its 48 SH coefficients come from registers and dL/dsh goes
-// to dsh_out (zeros when not visible) for the cooperative store; otherwise SH is read / written directly.
+// One Gaussian.  In the LDS-staged path (LDS) dL/dsh is not written here: the Gaussian's clamp-masked colour
+// gradient and view direction go to dRGB_out / dir_out (dRGB zero when not visible) for the kernel's staged
+// coalesced store; otherwise dL/dsh is written directly.
 template <bool LDS>
-__device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p, const int i, const float *sh_in,
-                                                   float *dsh_out, bool have_gs, const float (&gs_in)[10]) {
+__device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p, const int i, bool have_gs,
+                                                   const float (&gs_in)[10], float3 &dRGB_out, float3 &dir_out) {
     const bool vis = p.radii[i] > 0;
     float gs[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (vis && have_gs && p.tiles[i] <= BIG_GAUSSIAN_TILES) {
@@ -107,10 +108,8 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
         p.dL_dcolors[3 * i + 2] = gs[8];
     }
     const int ncoef = p.M * 3;
-    if (LDS && (!vis || !p.shs)) {
-#pragma unroll
-        for (int k = 0; k < 48; k++) dsh_out[k] = 0.f;
-    }
+    dRGB_out = make_float3(0.f, 0.f, 0.f);
+    dir_out = make_float3(1.f, 0.f, 0.f);
     if (!vis) {
         if (p.dL_dopacity) p.dL_dopacity[i] = 0.f;
         if (p.dL_dmeans3D) { p.dL_dmeans3D[3 * i] = 0.f; p.dL_dmeans3D[3 * i + 1] = 0.f; p.dL_dmeans3D[3 * i + 2] = 0.f; }
@@ -244,8 +243,10 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
         }
         float *dsh = p.dL_dsh ? p.dL_dsh + (size_t)i * ncoef : nullptr;  // null only with dL_dcolors_sh (API)
         if (LDS) {
-            // LDS-staged block (M = 16): dL/dsh goes to the lane's slot for the coalesced store
-            dm = dm + sh_backward_jac_dispatch(p.D, mean - campos, dRGB, jx, jy, jz, dsh_out);
+            // LDS-staged block (M = 16): the kernel writes dL/dsh = basis (x) dRGB through LDS
+            dm = dm + sh_dir_grad(mean - campos, dRGB, jx, jy, jz);
+            dRGB_out = dRGB;
+            dir_out = mean - campos;
         } else {
             float dshv[48];
             dm = dm + sh_backward_jac_dispatch(p.D, mean - campos, dRGB, jx, jy, jz, dshv);
@@ -278,21 +279,25 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
     }
 }
 
-// dL/dsh (192 B per Gaussian at M = 16) is written through LDS: a wave moves its 64 Gaussians' 12 KB block
-// with coalesced float4 stores, instead of 12 float4 stores per lane strided by 192 B.  In LDS each Gaussian's
-// 48 floats sit at a 52-float stride, so both the linear block copy (ds_read_b128 of consecutive lanes) and
-// each lane's 12 float4 writes to its own Gaussian (52 = 4 x 13, 13 odd: 16 lanes of a b128 lane group hit 16
-// distinct 4-bank windows) are free of bank conflicts.  The coefficients themselves are not read (sh_jac).
+// dL/dsh (192 B per Gaussian at M = 16) is written through LDS: each half of a wave's 64 Gaussians writes its
+// products basis (x) dRGB into a 32-Gaussian staging area, then the wave stores that 6 KB block with coalesced
+// float4 stores (instead of 12 float4 stores per lane strided by 192 B).  In LDS each Gaussian's 48 floats sit
+// at a 52-float stride, so both the linear block copy (ds_read_b128 of consecutive lanes) and each lane's float4
+// writes to its own Gaussian (52 = 4 x 13, 13 odd: 16 lanes of a b128 lane group hit 16 distinct 4-bank windows)
+// are free of bank conflicts.  The coefficients themselves are not read (sh_jac).  A half-wave staging area
+// (6.5 KB, shared with the row-gather chunks) keeps the block at 26 KB of LDS: six blocks, the VGPR limit, per CU.
 constexpr int SH_STRIDE = 52;
+constexpr int PBWD_STAGE = 32 * SH_STRIDE;  // floats of LDS per wave
 template <bool LDS_SH>
 __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams p) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (!LDS_SH) {
         const float none[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        if (i < p.P) preprocess_bwd_one<false>(p, i, nullptr, nullptr, false, none);
+        float3 d3, v3;
+        if (i < p.P) preprocess_bwd_one<false>(p, i, false, none, d3, v3);
         return;
     }
-    __shared__ __attribute__((aligned(16))) float s_sh[4][64 * SH_STRIDE];
+    __shared__ __attribute__((aligned(16))) float s_sh[4][PBWD_STAGE];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const size_t gbase = ((size_t)blockIdx.x * 256 + (size_t)w * 64) * 48;  // first float of the wave's block
     const size_t gend = (size_t)p.P * 48;
@@ -300,7 +305,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
     // Gradient rows of the wave's 64 Gaussians (rows_by_u: each Gaussian's rows are contiguous), gathered
     // jointly: the (Gaussian, row) pairs of all lanes are enumerated in order, every lane loads the inv words of
     // pairs l, l + 64, ... of a chunk, then the rows the composite wrote (others read as zero) into the LDS that later
-    // stages the SH block, then each lane sums its own Gaussian's rows in row order.  Divergent per-lane
+    // stages dL/dsh, then each lane sums its own Gaussian's rows in row order.  Divergent per-lane
     // loops of dependent loads cost ~40 % of the kernel otherwise.  Gaussians above BIG_GAUSSIAN_TILES rows
     // take their block-reduced sum in preprocess_bwd_one.
     float gs[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -311,10 +316,10 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         const uint32_t incl = wave_inclusive_scan(len, lane);
         const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         const uint32_t pst = incl - len;
-        constexpr uint32_t CH = 320, PER = CH / 64;  // pairs per chunk: 10 floats each fit the SH staging
-        // (first pair, first expansion index) of each lane's Gaussian, in the staging area's last 512 B
+        constexpr uint32_t CH = 128, PER = CH / 64;  // pairs per chunk: 10 floats each fit the staging area
+        // (first pair, first expansion index) of each lane's Gaussian, behind the chunk
         uint2 *s_meta = reinterpret_cast<uint2 *>(sw + CH * 10);
-        static_assert(CH * 10 + 128 <= 64 * SH_STRIDE, "row chunk + meta fit the SH staging");
+        static_assert(CH * 10 + 128 <= PBWD_STAGE, "row chunk + meta fit the staging area");
         s_meta[lane] = make_uint2(pst, len ? p.inst_start[i] : 0u);
         wave_lds_sync();
         for (uint32_t c0 = 0; c0 < total; c0 += CH) {
@@ -366,16 +371,22 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
             wave_lds_sync();
         }
     }
-    // each lane writes its Gaussian's dL/dsh into its LDS slot (the row chunks above are done with the area)
-    if (i < p.P) preprocess_bwd_one<true>(p, i, nullptr, sw + lane * SH_STRIDE, p.rows_by_u != 0, gs);
+    float3 dRGB = make_float3(0.f, 0.f, 0.f), dir = make_float3(1.f, 0.f, 0.f);
+    if (i < p.P) preprocess_bwd_one<true>(p, i, p.rows_by_u != 0, gs, dRGB, dir);
     if (!p.dL_dsh) return;
-    wave_lds_sync();
 #pragma unroll
-    for (int c = 0; c < 12; c++) {
-        const uint32_t f = c * 256 + lane * 4;
-        if (gbase + f < gend)
-            *reinterpret_cast<float4 *>(p.dL_dsh + gbase + f) =
-                *reinterpret_cast<const float4 *>(sw + (f / 48) * SH_STRIDE + f % 48);
+    for (int h = 0; h < 2; h++) {
+        wave_lds_sync();  // the area's previous contents (row chunks or the other half) are consumed
+        if ((lane >> 5) == h) sh_dsh_dispatch(p.D, dir, dRGB, sw + (lane & 31) * SH_STRIDE);
+        wave_lds_sync();
+#pragma unroll
+        for (int c = 0; c < 6; c++) {  // 32 Gaussians x 48 floats = 384 float4, 6 per lane
+            const uint32_t f = c * 256 + lane * 4;
+            const size_t go = gbase + (size_t)h * 1536 + f;
+            if (go < gend)
+                *reinterpret_cast<float4 *>(p.dL_dsh + go) =
+                    *reinterpret_cast<const float4 *>(sw + (f / 48) * SH_STRIDE + f % 48);
+        }
     }
 }
 

@@ -225,11 +225,10 @@ __device__ __forceinline__ float3 sh_backward_inplace_dispatch(int deg, float *s
     }
 }
 
-// The backward from the forward's direction Jacobian: writes dL/dsh[0..48) (zeros above the degree; the same
-// values as sh_backward_inplace) and returns dL/dmean through the view direction.  No coefficient is read.
+// dL/dsh = basis(dir) (x) dRGB at the normalised direction of dir_orig: dsh[0..48), zeros above the degree (the
+// same values as sh_backward_inplace writes).
 template <int DEG>
-__device__ __forceinline__ float3 sh_backward_jac(float3 dir_orig, float3 dRGB, float3 jx, float3 jy, float3 jz,
-                                                  float *__restrict__ dsh) {
+__device__ __forceinline__ void sh_dsh(float3 dir_orig, float3 dRGB, float *__restrict__ dsh) {
     const float len = sqrtf(dot3(dir_orig, dir_orig));
     const float3 dir = make_float3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
     const float x = dir.x, y = dir.y, z = dir.z;
@@ -251,8 +250,29 @@ __device__ __forceinline__ float3 sh_backward_jac(float3 dir_orig, float3 dRGB, 
     st3(dsh + 39, DEG > 2 ? (SH_C3[4] * x * (4.f * zz - xx - yy)) * dRGB : zero);
     st3(dsh + 42, DEG > 2 ? (SH_C3[5] * z * (xx - yy)) * dRGB : zero);
     st3(dsh + 45, DEG > 2 ? (SH_C3[6] * x * (xx - 3.f * yy)) * dRGB : zero);
+}
+__device__ __forceinline__ void sh_dsh_dispatch(int deg, float3 dir_orig, float3 dRGB, float *dsh) {
+    switch (deg) {
+        case 0: sh_dsh<0>(dir_orig, dRGB, dsh); break;
+        case 1: sh_dsh<1>(dir_orig, dRGB, dsh); break;
+        case 2: sh_dsh<2>(dir_orig, dRGB, dsh); break;
+        default: sh_dsh<3>(dir_orig, dRGB, dsh); break;
+    }
+}
+
+// The direction term of dL/dmean from the forward's colour Jacobian: dL/ddir = (jx . dRGB, jy . dRGB, jz . dRGB)
+// through the normalisation (sh_backward's last two lines); no coefficient is read.
+__device__ __forceinline__ float3 sh_dir_grad(float3 dir_orig, float3 dRGB, float3 jx, float3 jy, float3 jz) {
     const float3 dL_ddir = make_float3(dot3(jx, dRGB), dot3(jy, dRGB), dot3(jz, dRGB));
     return dnormvdv(dir_orig, dL_ddir);
+}
+
+// Both: the non-staged backward path (dL/dsh into registers or global memory).
+template <int DEG>
+__device__ __forceinline__ float3 sh_backward_jac(float3 dir_orig, float3 dRGB, float3 jx, float3 jy, float3 jz,
+                                                  float *__restrict__ dsh) {
+    sh_dsh<DEG>(dir_orig, dRGB, dsh);
+    return sh_dir_grad(dir_orig, dRGB, jx, jy, jz);
 }
 __device__ __forceinline__ float3 sh_backward_jac_dispatch(int deg, float3 dir_orig, float3 dRGB, float3 jx, float3 jy,
                                                            float3 jz, float *dsh) {
