@@ -11,6 +11,8 @@
 #include <cmath>
 #include <cstring>
 #include <mutex>
+
+#include <immintrin.h>
 #include <string>
 #include <vector>
 
@@ -199,11 +201,54 @@ hipEvent_t readback_event(int dev) {
     return e[dev];
 }
 
+// Instance total of the last forward on this thread and device (the binning buffer's pre-wait size hint).
+int64_t &readback_hint(int dev) {
+    thread_local int64_t h[kMaxDevices] = {};
+    static int64_t none = 0;
+    if (dev < 0 || dev >= kMaxDevices) return none = 0;
+    return h[dev];
+}
+
+// Sequence number of the next preprocess readback on this thread and device (never 0: the buffer starts zeroed).
+uint32_t next_readback_seq(int dev) {
+    thread_local uint32_t seq[kMaxDevices] = {};
+    if (dev < 0 || dev >= kMaxDevices) return 1u;
+    if (++seq[dev] == 0u) seq[dev] = 1u;
+    return seq[dev];
+}
+
+// Spin until the preprocess's last workgroup has published {total lo, hi, big count, seq} at hw[CNT_WORDS] (one
+// 16-B store, read here with one 16-B load: aligned 16-B SSE loads are single-copy atomic on AVX-capable x86).
+// Every 4096 polls the stream is queried, so a failed launch or a kernel fault returns an error instead of
+// spinning forever.
+int wait_readback(const uint32_t *hw, uint32_t seq, hipStream_t s, uint64_t *total, uint32_t *nbig) {
+    const __m128i *src = reinterpret_cast<const __m128i *>(hw + CNT_WORDS);
+    for (uint64_t it = 1;; it++) {
+        const __m128i v = _mm_load_si128((const __m128i *)(volatile const void *)src);
+        alignas(16) uint32_t w[4];
+        _mm_store_si128(reinterpret_cast<__m128i *>(w), v);
+        if (w[3] == seq) {
+            *total = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+            *nbig = w[2];
+            return GSR_OK;
+        }
+        if ((it & 4095) == 0) {
+            const hipError_t e = hipStreamQuery(s);
+            if (e != hipSuccess && e != hipErrorNotReady) return fail(GSR_ERR_HIP, hipGetErrorString(e));
+            if (e == hipSuccess && __atomic_load_n(hw + CNT_WORDS + 3, __ATOMIC_ACQUIRE) != seq)
+                return fail(GSR_ERR_HIP, "preprocess finished without publishing its counters");
+        }
+        _mm_pause();
+    }
+}
+
 uint32_t *pinned_words(int dev) {
     thread_local uint32_t *p[kMaxDevices] = {};
     if (dev < 0 || dev >= kMaxDevices) return nullptr;
     if (!p[dev]) {
-        if (hipHostMalloc((void **)&p[dev], 4096, hipHostMallocDefault) != hipSuccess) p[dev] = nullptr;
+        // coherent (fine-grained) pinned memory: the preprocess writes the counters here directly
+        if (hipHostMalloc((void **)&p[dev], 4096, hipHostMallocCoherent) != hipSuccess) p[dev] = nullptr;
+        else memset(p[dev], 0, 4096);
     }
     return p[dev];
 }
@@ -335,9 +380,11 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     char *img = alloc(alloc_ctx, GSR_BUF_IMAGE, carve_image(nullptr, W, H, im));
     if (!img) return fail(GSR_ERR_ALLOC, "image buffer allocation failed");
     carve_image(img, W, H, im);
-    const size_t clear_bytes = (size_t)(reinterpret_cast<char *>(g.tile_status + BK_MAX_TILES / 64 + 1) -
-                                        reinterpret_cast<char *>(g.counters));
-    GSR_HIP(hipMemsetAsync(g.counters, 0, clear_bytes, stream));  // counters + instance-scan look-back words
+    // counters + instance-scan and tile-scan look-back words; rounded up to the carver's 256-B alignment (the
+    // next array starts there) so the memset is one aligned fill kernel, not an aligned fill plus a tail
+    const size_t clear_bytes = align_up((size_t)(reinterpret_cast<char *>(g.tile_status + BK_MAX_TILES / 64 + 1) -
+                                                 reinterpret_cast<char *>(g.counters)), 256);
+    GSR_HIP(hipMemsetAsync(g.counters, 0, clear_bytes, stream));
 
     PreprocessParams pp;
     pp.P = P; pp.D = a->D; pp.M = a->M; pp.W = W; pp.H = H; pp.gx = gx; pp.gy = gy;
@@ -354,16 +401,24 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     pp.g = g;
     // The bucket path's Gaussian-order instance scan is formed by its count pass from these block totals.
     pp.block_sums = g.block_sums;
-    GSR_STAGE(ST_PREPROCESS, dbg, launch_preprocess(stream, pp));
     // The instance total only needs the per-Gaussian tile counts, so it is read back right after the
-    // preprocess.  The bucket path's count pass needs no total either: whenever the tile count admits that
-    // path it is queued right behind the copy, so the GPU runs it while the host waits (its scratch is in the
-    // image buffer; if the total then selects the radix path, its results are simply unused).
+    // preprocess: its last workgroup writes the counters into pinned host memory and then a sequence word the
+    // host polls ("rb_spin" 1, default; 0: a copy plus an event, one more kernel and a barrier on the stream).
+    // The bucket path's count pass needs no total either: whenever the tile count admits that path it is queued
+    // right behind the preprocess, so the GPU runs it while the host waits (its scratch is in the image buffer;
+    // if the total then selects the radix path, its results are simply unused).
     uint32_t *hw = pinned_words(device_guard.dev);
     hipEvent_t rb_ev = readback_event(device_guard.dev);
     if (!hw || !rb_ev) return fail(GSR_ERR_HIP, "pinned host buffer / event allocation failed");
-    GSR_HIP(hipMemcpyAsync(hw, g.counters, CNT_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-    GSR_HIP(hipEventRecord(rb_ev, stream));
+    const bool rb_spin = tuning("rb_spin", 1) != 0 && !dbg;
+    const uint32_t seq = next_readback_seq(device_guard.dev);
+    pp.host_words = rb_spin ? hw : nullptr;
+    pp.seq = seq;
+    GSR_STAGE(ST_PREPROCESS, dbg, launch_preprocess(stream, pp));
+    if (!rb_spin) {
+        GSR_HIP(hipMemcpyAsync(hw, g.counters, CNT_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        GSR_HIP(hipEventRecord(rb_ev, stream));
+    }
     const int bk = tuning("bucket", 1);
     const bool bk_possible = bk == 2 ? T <= BK_MAX_TILES : bk == 1 && T <= BK_MAX_TILES / 2;
     const int lpt = tuning("lpt", 1);
@@ -381,17 +436,39 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
         bp.long_list = im.bk_long_list; bp.long_cnt = g.counters + CNT_LONG;
         GSR_STAGE(ST_BK_COUNT, dbg, launch_bucket_count(stream, bp));
     }
-    GSR_STAGE(ST_READBACK, dbg, GSR_HIP(hipEventSynchronize(rb_ev)));
+    // The binning buffer's size depends on the instance total.  Requesting it through the caller's allocator
+    // (a Python callback from rasterizer.py) after the readback put ~40 us of host work between the preprocess and
+    // the next launch, longer than the queued count passes cover; so with a total from an earlier call on this
+    // thread and device the buffer is requested before the wait, 25 % larger, and only re-requested when the
+    // total exceeds it ("bin_prealloc" 0: always after the wait).
+    BinningState b;
+    char *bin = nullptr;
+    int64_t bin_cap = -1;
+    int64_t &r_hint = readback_hint(device_guard.dev);
+    if (r_hint > 0 && tuning("bin_prealloc", 1)) {
+        bin_cap = std::min<int64_t>(r_hint + r_hint / 4 + 4096, 0xffffffffLL);
+        bin = alloc(alloc_ctx, GSR_BUF_BINNING, carve_binning(nullptr, bin_cap, T, b));
+        if (!bin) return fail(GSR_ERR_ALLOC, "binning buffer allocation failed");
+    }
     uint64_t total64 = 0;
-    for (int k = 0; k < CNT_NPART; k++) {
-        uint64_t part;
-        memcpy(&part, hw + CNT_PARTIALS + 2 * k, sizeof(part));
-        total64 += part;
+    uint32_t nbig = 0;
+    if (rb_spin) {
+        GSR_STAGE(ST_READBACK, dbg, {
+            const int rc = wait_readback(hw, seq, stream, &total64, &nbig);
+            if (rc) return rc;
+        });
+    } else {
+        GSR_STAGE(ST_READBACK, dbg, GSR_HIP(hipEventSynchronize(rb_ev)));
+        for (int k = 0; k < CNT_NPART; k++) {
+            uint64_t part;
+            memcpy(&part, hw + CNT_PARTIALS + 2 * k, sizeof(part));
+            total64 += part;
+        }
+        nbig = hw[CNT_BIG];
     }
     if (total64 > 0xffffffffull) return fail(GSR_ERR_OVERFLOW, "more than 2^32-1 tile instances");
     const uint32_t R = (uint32_t)total64;
     *num_rendered = R;
-    const uint32_t nbig = hw[CNT_BIG];
     a->num_big_out = nbig;
     // Bucket binning (gsr_bin.hip) while the tile counters fit a workgroup's LDS with room for two per CU and
     // the tiles are short (per-tile sorts cost n log^2 n): at 1M Gaussians / 1080p (517 instances per tile) it
@@ -410,10 +487,12 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
                                             g.counters + CNT_OVERFLOW));
     }
 
-    BinningState b;
-    char *bin = alloc(alloc_ctx, GSR_BUF_BINNING, carve_binning(nullptr, R, T, b));
-    if (!bin) return fail(GSR_ERR_ALLOC, "binning buffer allocation failed");
-    carve_binning(bin, R, T, b);
+    r_hint = R;
+    if (!bin || (int64_t)R > bin_cap) {
+        bin = alloc(alloc_ctx, GSR_BUF_BINNING, carve_binning(nullptr, R, T, b));
+        if (!bin) return fail(GSR_ERR_ALLOC, "binning buffer allocation failed");
+    }
+    carve_binning(bin, R, T, b);  // offsets from R: a larger buffer only has unused space at the end
     if ((uint64_t)RS_BINS * div_up(R ? R : 1, RS_TILE) + 1 > (uint64_t)SCAN_TILE * SCAN_MAX_BLOCKS)
         return fail(GSR_ERR_OVERFLOW, "too many tile instances for the single-level scan");
     if (bucket) {

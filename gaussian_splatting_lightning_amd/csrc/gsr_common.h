@@ -24,7 +24,7 @@ constexpr int GRAD_ROW = 12;                   // floats per instance gradient r
 // counters block at the head of the geometry buffer (zeroed every forward)
 // counters: [CNT_BIG] big-Gaussian count, [CNT_OVERFLOW] scan overflow flag, then CNT_NPART 64-bit partial
 // sums of the instance total (spread over addresses so the per-block atomics do not serialise)
-enum Counter : int { CNT_BIG = 0, CNT_OVERFLOW = 2, CNT_SCAN_TICKET = 3, CNT_COL_TICKET = 4, CNT_LONG = 6, CNT_TIES = 8, CNT_PARTIALS = 16, CNT_NPART = 64,
+enum Counter : int { CNT_BIG = 0, CNT_OVERFLOW = 2, CNT_SCAN_TICKET = 3, CNT_COL_TICKET = 4, CNT_LONG = 6, CNT_TIES = 8, CNT_PRE_DONE = 10, CNT_PARTIALS = 16, CNT_NPART = 64,
                      CNT_WORDS = 16 + 2 * 64 };
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }

@@ -182,11 +182,45 @@ __global__ __launch_bounds__(256, GSR_PRE_MINW) void preprocess_kernel(Preproces
     for (int o = 32; o > 0; o >>= 1) kept += (uint32_t)__shfl_xor((int)kept, o);
     if (lane == 0) s_w[w] = kept;
     __syncthreads();
+    __shared__ uint32_t s_last;
     if (threadIdx.x == 0) {
         const unsigned long long tot = (unsigned long long)s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        unsigned long long old = 0;
         if (tot)
-            atomicAdd(reinterpret_cast<unsigned long long *>(p.g.counters + CNT_PARTIALS) + (bid % CNT_NPART), tot);
+            old = atomicAdd(reinterpret_cast<unsigned long long *>(p.g.counters + CNT_PARTIALS) + (bid % CNT_NPART), tot);
         if (p.block_sums) p.block_sums[bid] = (uint32_t)tot;  // <= 256 * 2^16 tiles
+        if (p.host_words) {
+            // The workgroup's counter atomics have all returned before its ticket is taken (the big-slot ones before
+            // the barrier, the partial sum here: its result is waited for), so the workgroup that draws the last
+            // ticket sees every count.  No fence: an agent-scope release writes back the XCD's L2, ~60 ns per
+            // workgroup, which over 3906 workgroups tripled the kernel.
+            asm volatile("" ::"v"(old));
+            s_last = atomicAdd(&p.g.counters[CNT_PRE_DONE], 1u) == gridDim.x - 1;
+        }
+    }
+    if (!p.host_words) return;
+    __syncthreads();
+    if (!s_last) return;
+    // The last workgroup publishes {instance total lo, hi, big count, seq} to pinned host memory in ONE 16-B store
+    // (the host reads it with one 16-B load and trusts it when the sequence word matches), so no release fence is
+    // needed: a system-scope release writes back the L2 first and delayed the host's view by ~35 us.
+    if (threadIdx.x >= 64) return;
+    const unsigned long long part = __hip_atomic_load(
+        reinterpret_cast<unsigned long long *>(p.g.counters + CNT_PARTIALS) + threadIdx.x, __ATOMIC_RELAXED,
+        __HIP_MEMORY_SCOPE_AGENT);  // CNT_NPART == 64: one partial per lane
+    const unsigned long long lo = (uint32_t)part, hi = part >> 32;
+    unsigned long long slo = lo, shi = hi;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        slo += (unsigned long long)__shfl_xor((long long)slo, o);
+        shi += (unsigned long long)__shfl_xor((long long)shi, o);
+    }
+    if (threadIdx.x == 0) {
+        const unsigned long long total = slo + (shi << 32);
+        const uint32_t nbig = __hip_atomic_load(&p.g.counters[CNT_BIG], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 v = {(uint32_t)total, (uint32_t)(total >> 32), nbig, p.seq};
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p.host_words + CNT_WORDS));
     }
 }
 

@@ -42,6 +42,10 @@ struct PreprocessParams {
     int *radii;
     GeomState g;
     uint32_t *block_sums;  // optional: kept-tile total of every 256-Gaussian block
+    // optional: pinned host words; the last preprocess workgroup writes {instance total lo, hi, big count, seq}
+    // to host_words[CNT_WORDS .. +4) in one 16-B store (the forward's readback without a copy or an event)
+    uint32_t *host_words;
+    uint32_t seq;
 };
 void launch_preprocess(hipStream_t s, const PreprocessParams &p);
 
