@@ -965,9 +965,18 @@ void launch_render_fwd(hipStream_t s, const RenderFwdParams &p0) {
     // "fwd_parts" 1, 2 or 4; 0 (default): 4 or 2 when that many part-waves still fit the GPU's ~8 resident waves
     // per SIMD, twice over (small images, where one heavy tile's latency sets the kernel time), else whole tiles with
     // only the heaviest split in two
+    // (measured at 1080p, 8160 tiles: whole tiles with render_fwd_v6 0.175 ms against 0.196 in 2 parts; at 800x800,
+    // 2500 tiles: 4 parts 0.073, 2 parts 0.092, whole 0.126)
     int parts = tuning("fwd_parts", 0);
-    if (parts == 0) parts = p.num_tiles * 4 <= tuning("fwd_part_slots", 16384) ? 4
-                            : p.num_tiles * 2 <= tuning("fwd_part_slots", 16384) ? 2 : 1;
+    if (parts == 0) parts = p.num_tiles * 4 <= tuning("fwd_part_slots", 16384) ? 4 : 1;
+    if (parts == 1 && tuning("fwd_v", 6) == 6 && tuning("fwd_whole_v6", 1)) {  // whole tiles, v6 (4 pixels / lane)
+        RenderFwdParams q = p;
+        q.stamps = tuning("stamp", 0) ? stamp_buffer(0) : nullptr;
+        const dim3 grid(div_up(p.num_tiles, 4)), block(256);
+        if (tuning("fwd_part_waves", 8) >= 6) render_fwd_v6_kernel<4, 6><<<grid, block, 0, s>>>(q);
+        else render_fwd_v6_kernel<4, 4><<<grid, block, 0, s>>>(q);
+        return;
+    }
     if (parts == 2 || parts == 4) {
         RenderFwdParams q = p;
         q.stamps = tuning("stamp", 0) ? stamp_buffer(0) : nullptr;
