@@ -37,6 +37,8 @@ if REPO not in sys.path:
 METRIC = "rasterizer fwd+bwd ms & Gaussians·pixels/s @ 1M gauss, 1080p; 1/2/4/8-GPU"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
 FP32_VALU_PEAK_TF = 157.3  # MI355X_MICROARCH.md chip table (spec)
+VALU_ISSUE_NS = 1.29   # per wave-instruction per SIMD, every SIMD issuing fp32 FMA (tools/probes/valu_rate_probe.hip)
+TRANS_EXTRA_NS = 2.2   # v_exp / v_rcp cost ~3.5 ns on the same pipe
 PY_REFERENCE_CFG3_S = 730.0  # reference Python rasterizer, cfg 3 fwd+bwd, 8-core Xeon
 
 CONFIGS = {
@@ -198,11 +200,27 @@ def main():
         # evaluated (pixel, Gaussian) pair x sum(n_contrib)) over the live launch time.  The HBM figure of the
         # same launch (SURVEY's algorithmic bytes, PMC traffic) is kept beside it.
         tflops = flops[dom] / (dom_ms * 1e-3) / 1e12
+        # VALU issue utilisation of the same launch: PMC wave-instruction counts (profiles/pmc_insts.json, same
+        # config) x the per-SIMD issue costs tools/probes/valu_rate_probe.hip measured with every SIMD issuing
+        # (1.29 ns per VALU, +2.2 ns per transcendental), over the live launch time
+        issue = None
+        ins_path = os.path.join(REPO, "profiles", "pmc_insts.json")
+        if os.path.exists(ins_path):
+            try:
+                e = json.load(open(ins_path)).get(args.config, {}).get(dom)
+                if e:
+                    busy_ms = (e["valu"] * VALU_ISSUE_NS + (e.get("trans") or 0) * TRANS_EXTRA_NS) / 1024 * 1e-6
+                    issue = {"valu_insts": e["valu"], "salu_insts": e.get("salu"), "trans_insts": e.get("trans"),
+                             "valu_busy_ms": round(busy_ms, 4), "frac": round(busy_ms / dom_ms, 4),
+                             "note": "VALU issue time per SIMD / launch time (profiles/pmc_insts.json)"}
+            except Exception:  # noqa: BLE001
+                issue = None
         roofline = {"kernel": dom, "bound": "valu", "achieved": round(tflops, 2), "peak": FP32_VALU_PEAK_TF,
                     "unit": "TFLOP/s", "frac": round(tflops / FP32_VALU_PEAK_TF, 4), "traffic": traffic,
                     "algorithmic_flops_per_launch": flops[dom], "avg_launch_ms": round(dom_ms, 4),
                     "hbm": {"achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": algo_bytes[dom]},
+                    "valu_issue": issue,
                     "note": "fp32 VALU bound (no MFMA work on this path); flops = 25 (fwd) / 70 (bwd) per pair x "
                             "sum(n_contrib) (SURVEY §8(d)); traffic = PMC HBM bytes per launch "
                             "(profiles/pmc_traffic.json)"}
