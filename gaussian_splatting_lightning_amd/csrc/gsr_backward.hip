@@ -101,6 +101,75 @@ __device__ __forceinline__ void wave_reduce20_store(const float m0[10], const fl
     if ((lane & 15) == 0) dst[16 + low - 10 + PART] = c[2];  // values 16..19 (b3 = 0 here)
 }
 
+__device__ constexpr float kZero8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+// The composite passes hand over one instance's raw per-lane sums r = (Q0 = Σq, Q1 = Σq·dy, Q2 = Σq·dy², w0..w3,
+// dx); the six moments need dx, which is the same for the lanes l, l ^ 16, l ^ 32 and l ^ 48 (one pixel column).
+// One instance: the moments on the lane, then the 10-value reduction.
+__device__ __forceinline__ void wave_reduce_one_store(const float r[8], float *__restrict__ dst, int lane) {
+    const float dx = r[7];
+    float m[10];
+    m[0] = r[0];
+    m[1] = r[0] * dx;
+    m[2] = r[1];
+    m[3] = m[1] * dx;
+    m[4] = r[1] * dx;
+    m[5] = r[2];
+#pragma unroll
+    for (int i = 0; i < 4; i++) m[6 + i] = r[3 + i];
+    wave_reduce10_store(m, dst, lane);
+}
+
+// Two instances: the bit-5 exchange pairs each raw sum of instance 0 with the same sum of instance 1 (7 swaps, not
+// the 10 of two moment sets), so every register then holds one quantity (instance b5's) and the moments are formed
+// once for both instances, on sums already reduced over lane bit 5, with the lane's dx of its instance.  The
+// remaining levels are wave_reduce20_store's: after the bit-4 swaps bb[k] holds value 2 k + b4, the bit-3 exchange
+// makes value 4 m + 2 b3 + b4 (m = 0, 1) and 8 + b4; values are in gradient-row order
+// (S, Sx, Sy, Sxx, Sxy, Syy, w0..w3) of instance b5 (the next PART-float row for instance 1).
+// BOTH = false reduces instance 0 alone through the same operation tree (r1 all zero, only its row stored), so an
+// instance's gradient bits do not depend on whether it was paired.
+template <bool BOTH = true>
+__device__ __forceinline__ void wave_reduce_pair_store(const float r0[8], const float r1[8], float *__restrict__ dst,
+                                                       int lane) {
+    const bool hi5 = (lane & 32) != 0;
+    const float dx = hi5 ? r1[7] : r0[7];
+    const float s0 = sum_swap32(r0[0], r1[0]), s1 = sum_swap32(r0[1], r1[1]), s2 = sum_swap32(r0[2], r1[2]);
+    float R[10];
+    R[0] = s0;
+    R[1] = s0 * dx;
+    R[2] = s1;
+    R[3] = R[1] * dx;
+    R[4] = s1 * dx;
+    R[5] = s2;
+#pragma unroll
+    for (int i = 0; i < 4; i++) R[6 + i] = sum_swap32(r0[3 + i], r1[3 + i]);
+    float bb[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) bb[k] = sum_swap16(R[2 * k], R[2 * k + 1]);
+    const bool hi3 = (lane & 8) != 0;
+    float c[3];
+#pragma unroll
+    for (int m = 0; m < 2; m++) {
+        const float keep = hi3 ? bb[2 * m + 1] : bb[2 * m], send = hi3 ? bb[2 * m] : bb[2 * m + 1];
+        c[m] = dpp_xadd<0x128>(keep, send);
+    }
+    c[2] = dpp_add<0x128>(bb[4]);  // row_ror:8 (= lane ^ 8)
+#pragma unroll
+    for (int m = 0; m < 3; m++) {
+        c[m] = dpp_add<0xB1>(c[m]);   // quad_perm [1,0,3,2]
+        c[m] = dpp_add<0x4E>(c[m]);   // quad_perm [2,3,0,1]
+        c[m] = dpp_add<0x141>(c[m]);  // row_half_mirror
+    }
+    float *row = dst + (hi5 ? PART : 0);
+    const int low = ((lane >> 2) & 2) | ((lane >> 4) & 1);  // 2 b3 + b4
+    if (!BOTH && hi5) return;
+    if ((lane & 7) == 0) {
+        row[low] = c[0];
+        row[4 + low] = c[1];
+    }
+    if ((lane & 15) == 0) row[8 + (low & 1)] = c[2];
+}
+
 template <bool HAS_INV, int MIN_WAVES, int WPB>
 __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_bwd_v3_kernel(RenderBwdParams p) {
     __shared__ float4 s_a[WPB][BWD_BATCH];
@@ -214,18 +283,8 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_bwd_v3_kernel(Rend
             }
             float *dst = s_part[w][j];
             if (__ballot(any)) {
-                float m[10];
-                m[0] = Q0;
-                m[1] = Q0 * dx;
-                m[2] = Q1;
-                m[3] = m[1] * dx;
-                m[4] = Q1 * dx;
-                m[5] = Q2;
-                m[6] = w0;
-                m[7] = w1;
-                m[8] = w2;
-                m[9] = w3;
-                wave_reduce10_store(m, dst, lane);
+                const float m[8] = {Q0, Q1, Q2, w0, w1, w2, w3, dx};
+                wave_reduce_one_store(m, dst, lane);
             } else if (lane < 10) {
                 dst[lane] = 0.f;
             }
@@ -344,8 +403,8 @@ __global__ __launch_bounds__(64, MIN_WAVES) void render_bwd_v4_kernel(RenderBwdP
         wave_lds_sync();
         float4 na = s_a[0], nb = s_b[0];
         float2 nc = s_c[0];
-        // one instance's pass over the lane's pixels: updates T / D, returns the 10 per-lane sums in m
-        auto pass = [&](const int j, float m[10]) -> bool {
+        // one instance's pass over the lane's pixels: updates T / D, returns the lane's raw sums and dx in m (wave_reduce_one_store)
+        auto pass = [&](const int j, float m[8]) -> bool {
             const uint32_t idx = (uint32_t)(bend - 1 - j);
             float4 a, b;  // a: x, y, A, B; b: C, o, r, g
             float2 c;     // b, 1/depth
@@ -426,32 +485,30 @@ __global__ __launch_bounds__(64, MIN_WAVES) void render_bwd_v4_kernel(RenderBwdP
                 }
             }
             m[0] = Q0;
-            m[1] = Q0 * dx;
-            m[2] = Q1;
-            m[3] = m[1] * dx;
-            m[4] = Q1 * dx;
-            m[5] = Q2;
-            m[6] = w0;
-            m[7] = w1;
-            m[8] = w2;
-            m[9] = w3;
+            m[1] = Q1;
+            m[2] = Q2;
+            m[3] = w0;
+            m[4] = w1;
+            m[5] = w2;
+            m[6] = w3;
+            m[7] = dx;
             return any;
         };
         for (int j = 0; j < cnt; j += PAIR ? 2 : 1) {
-            float m0[10];
+            float m0[8];
             const bool any0 = pass(j, m0);
             float *dst = s_part[j];
             if (PAIR && j + 1 < cnt) {
-                float m1[10];
+                float m1[8];
                 const bool any1 = pass(j + 1, m1);
                 if (__ballot(any0 || any1)) {
-                    wave_reduce20_store(m0, m1, dst, lane);
+                    wave_reduce_pair_store(m0, m1, dst, lane);
                 } else if (lane < 10) {
                     dst[lane] = 0.f;
                     dst[PART + lane] = 0.f;
                 }
             } else if (__ballot(any0)) {
-                wave_reduce10_store(m0, dst, lane);
+                wave_reduce_pair_store<false>(m0, kZero8, dst, lane);
             } else if (lane < 10) {
                 dst[lane] = 0.f;
             }
@@ -554,7 +611,7 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
         uint64_t sk[NP];
 #pragma unroll
         for (int k = 0; k < NP; k++) sk[k] = __ballot((mm >> (kbase + k)) & 1u);
-        auto pass = [&](const int j, float m[10]) -> bool {
+        auto pass = [&](const int j, float m[8]) -> bool {
             const uint32_t idx = (uint32_t)(bend - 1 - j);
             const float4 a = s_a[j], b = s_b[j];  // a: x, y, A, B; b: C, o, r, g
             const float2 c = s_c[j];              // b, 1/depth
@@ -588,32 +645,30 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
                 Q2 = fmaf(qdy, dy, Q2);
             }
             m[0] = Q0;
-            m[1] = Q0 * dx;
-            m[2] = Q1;
-            m[3] = m[1] * dx;
-            m[4] = Q1 * dx;
-            m[5] = Q2;
-            m[6] = w0;
-            m[7] = w1;
-            m[8] = w2;
-            m[9] = w3;
+            m[1] = Q1;
+            m[2] = Q2;
+            m[3] = w0;
+            m[4] = w1;
+            m[5] = w2;
+            m[6] = w3;
+            m[7] = dx;
             return any;
         };
         for (int j = 0; j < cnt; j += 2) {
-            float m0[10];
+            float m0[8];
             const bool any0 = pass(j, m0);
             float *dst = s_part[w][j];
             if (j + 1 < cnt) {
-                float m1[10];
+                float m1[8];
                 const bool any1 = pass(j + 1, m1);
                 if (__ballot(any0 || any1)) {
-                    wave_reduce20_store(m0, m1, dst, lane);
+                    wave_reduce_pair_store(m0, m1, dst, lane);
                 } else if (lane < 10) {
                     dst[lane] = 0.f;
                     dst[PART + lane] = 0.f;
                 }
             } else if (__ballot(any0)) {
-                wave_reduce10_store(m0, dst, lane);
+                wave_reduce_pair_store<false>(m0, kZero8, dst, lane);
             } else if (lane < 10) {
                 dst[lane] = 0.f;
             }
@@ -735,9 +790,9 @@ __global__ __launch_bounds__(64, 5) void render_bwd_v5_kernel(RenderBwdParams p)
             }
         }
         wave_lds_sync();
-        // one instance's pass over the lane's pixels: updates T / D, returns the 10 per-lane sums in m and the
+        // one instance's pass over the lane's pixels: updates T / D, returns the lane's raw sums and dx in m (wave_reduce_one_store) and the
         // ballot of the lanes that contributed
-        auto pass = [&](const int j, float m[10]) -> bool {
+        auto pass = [&](const int j, float m[8]) -> uint64_t {
             const uint32_t idx = (uint32_t)(bend - 1 - j);
             const FwdRec &r = s_rec[j];
             const float4 a = r.a, b = r.b;  // a: x, y, A, B; b: C, o, r, g
@@ -745,7 +800,7 @@ __global__ __launch_bounds__(64, 5) void render_bwd_v5_kernel(RenderBwdParams p)
             const float dx = a.x - pfx, dy0 = a.y - pfy0;
             const float P0 = (a.z * dx) * dx, L = a.w * dx;
             float Q0 = 0.f, Q1 = 0.f, Q2 = 0.f, w0 = 0.f, w1 = 0.f, w2 = 0.f, w3 = 0.f;
-            bool any = false;
+            uint64_t any = 0;
 #pragma unroll
             for (int k = 0; k < PIX_PER_LANE; k++) {
                 if (!((sk[k] >> j) & 1u)) continue;  // wave-uniform
@@ -753,10 +808,14 @@ __global__ __launch_bounds__(64, 5) void render_bwd_v5_kernel(RenderBwdParams p)
                 const float power2 = power2_at(b.x, dy, P0, L);
                 const float G = __builtin_amdgcn_exp2f(power2);
                 const float alpha = fminf(0.99f, b.y * G);
+                // the contributing lanes as a scalar mask straight from the compares: !(power2 > 0),
+                // !(alpha < 1/255) and, where some lane of the strip may have finished, idx < n_contrib
                 const bool need = (nd[k] >> j) & 1u;  // wave-uniform
-                const bool ok = !(power2 > 0.0f) & !(alpha < 1.0f / 255.0f) & (!need | (idx < lastc[k]));
-                if (!ok) continue;
-                any = true;
+                uint64_t ok = __builtin_amdgcn_fcmpf(power2, 0.0f, FCMP_ULE) &
+                              __builtin_amdgcn_fcmpf(alpha, 1.0f / 255.0f, FCMP_UGE);
+                if (need) ok &= __builtin_amdgcn_uicmp(idx, lastc[k], ICMP_ULT);
+                any |= ok;
+                if (!__builtin_amdgcn_inverse_ballot_w64(ok)) continue;  // exec = ok
                 T[k] = T[k] * fast_rcp(1.f - alpha);
                 const float wgt = alpha * T[k];
                 float cd = fmaf(c.x, dp2[k], fmaf(b.w, dp1[k], b.z * dp0[k]));
@@ -774,32 +833,30 @@ __global__ __launch_bounds__(64, 5) void render_bwd_v5_kernel(RenderBwdParams p)
                 Q2 = fmaf(qdy, dy, Q2);
             }
             m[0] = Q0;
-            m[1] = Q0 * dx;
-            m[2] = Q1;
-            m[3] = m[1] * dx;
-            m[4] = Q1 * dx;
-            m[5] = Q2;
-            m[6] = w0;
-            m[7] = w1;
-            m[8] = w2;
-            m[9] = w3;
+            m[1] = Q1;
+            m[2] = Q2;
+            m[3] = w0;
+            m[4] = w1;
+            m[5] = w2;
+            m[6] = w3;
+            m[7] = dx;
             return any;
         };
         for (int j = 0; j < cnt; j += 2) {
-            float m0[10];
-            const bool any0 = pass(j, m0);
+            float m0[8];
+            const uint64_t any0 = pass(j, m0);
             float *dst = s_part[j];
             if (j + 1 < cnt) {
-                float m1[10];
-                const bool any1 = pass(j + 1, m1);
-                if (__ballot(any0 || any1)) {
-                    wave_reduce20_store(m0, m1, dst, lane);
+                float m1[8];
+                const uint64_t any1 = pass(j + 1, m1);
+                if (any0 | any1) {
+                    wave_reduce_pair_store(m0, m1, dst, lane);
                 } else if (lane < 10) {
                     dst[lane] = 0.f;
                     dst[PART + lane] = 0.f;
                 }
-            } else if (__ballot(any0)) {
-                wave_reduce10_store(m0, dst, lane);
+            } else if (any0) {
+                wave_reduce_pair_store<false>(m0, kZero8, dst, lane);
             } else if (lane < 10) {
                 dst[lane] = 0.f;
             }
@@ -907,9 +964,9 @@ __global__ __launch_bounds__(64, 5) void render_bwd_v6_kernel(RenderBwdParams p)
 #pragma unroll
         for (int k = 0; k < PIX_PER_LANE; k++) sk[k] = (uint32_t)__ballot((my_m >> k) & 1u);
         wave_lds_sync();
-        // one instance's pass over the lane's pixels: updates T / D, returns the 10 per-lane sums in m and the
+        // one instance's pass over the lane's pixels: updates T / D, returns the lane's raw sums and dx in m (wave_reduce_one_store) and the
         // ballot of the lanes that contributed
-        auto pass = [&](const int j, float m[10]) -> uint64_t {
+        auto pass = [&](const int j, float m[8]) -> uint64_t {
             const uint32_t idx = (uint32_t)(bend - 1 - j);
             const FwdRec &r = s_rec[j];
             const float4 a = r.a, b = r.b;  // a: x, y, A, B; b: C, o, r, g
@@ -949,32 +1006,30 @@ __global__ __launch_bounds__(64, 5) void render_bwd_v6_kernel(RenderBwdParams p)
                 Q2 = fmaf(qdy, dy, Q2);
             }
             m[0] = Q0;
-            m[1] = Q0 * dx;
-            m[2] = Q1;
-            m[3] = m[1] * dx;
-            m[4] = Q1 * dx;
-            m[5] = Q2;
-            m[6] = w0;
-            m[7] = w1;
-            m[8] = w2;
-            m[9] = w3;
+            m[1] = Q1;
+            m[2] = Q2;
+            m[3] = w0;
+            m[4] = w1;
+            m[5] = w2;
+            m[6] = w3;
+            m[7] = dx;
             return any;
         };
         for (int j = 0; j < cnt; j += 2) {
-            float m0[10];
+            float m0[8];
             const uint64_t any0 = pass(j, m0);
             float *dst = s_part[j];
             if (j + 1 < cnt) {
-                float m1[10];
+                float m1[8];
                 const uint64_t any1 = pass(j + 1, m1);
                 if (any0 | any1) {
-                    wave_reduce20_store(m0, m1, dst, lane);
+                    wave_reduce_pair_store(m0, m1, dst, lane);
                 } else if (lane < 10) {
                     dst[lane] = 0.f;
                     dst[PART + lane] = 0.f;
                 }
             } else if (any0) {
-                wave_reduce10_store(m0, dst, lane);
+                wave_reduce_pair_store<false>(m0, kZero8, dst, lane);
             } else if (lane < 10) {
                 dst[lane] = 0.f;
             }
