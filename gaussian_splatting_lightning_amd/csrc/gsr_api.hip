@@ -587,7 +587,7 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     char *scratch = alloc(alloc_ctx, GSR_BUF_BWD_SCRATCH, bwd_scratch_bytes(R, nbig));
     if (!scratch) return fail(GSR_ERR_ALLOC, "backward scratch allocation failed");
     float *rows = reinterpret_cast<float *>(scratch);
-    // Gaussian-major gradient rows: render_bwd scatters its 48-B rows to the instances' expansion indices so
+    // Gaussian-major gradient rows: render_bwd scatters its 40-B rows to the instances' expansion indices so
     // the per-Gaussian gather in preprocess_bwd reads each Gaussian's rows contiguously.
     const int rows_by_u = tuning("rows_by_u", 1);
     float *bigsum = bwd_bigsum_ptr(scratch, R);

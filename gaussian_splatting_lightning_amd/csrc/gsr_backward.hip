@@ -4,7 +4,7 @@
 //
 // The upstream CUDA backward scatters every (pixel, Gaussian) contribution with ~10 global float
 // atomics (SURVEY.md §2.1 BACKWARD::render).  Here one wave owns one tile: each lane walks 4 pixels
-// in reverse, the wave sums the per-instance contributions with DPP reductions, and writes ONE 48-byte
+// in reverse, the wave sums the per-instance contributions with DPP reductions, and writes ONE 40-byte
 // gradient row per (tile, Gaussian) instance, contiguously in sorted order.  The per-Gaussian kernel
 // then gathers its rows through the inverse permutation.  No float atomics, so gradients are
 // bitwise reproducible run to run.

@@ -72,25 +72,21 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
                 uint32_t sidx[4];
 #pragma unroll
                 for (int j = 0; j < 4; j++) sidx[j] = (k0 + j < cnt) ? p.inv[start + k0 + j] : INV_NONE;
-                float4 ra[4], rb[4], rc[4];
+                float rw[4][10];
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     if (sidx[j] != INV_NONE) {
                         const size_t ri = p.rows_by_u ? (size_t)(start + k0 + j) : (size_t)sidx[j];
-                        const float4 *src = reinterpret_cast<const float4 *>(p.rows + ri * GRAD_ROW);
-                        ra[j] = src[0];
-                        rb[j] = src[1];
-                        rc[j] = src[2];
+                        load_row(p.rows, ri, rw[j]);
                     } else {
-                        ra[j] = rb[j] = rc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                        for (int k = 0; k < 10; k++) rw[j][k] = 0.f;
                     }
                 }
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    gs[0] += ra[j].x; gs[1] += ra[j].y; gs[2] += ra[j].z; gs[3] += ra[j].w;
-                    gs[4] += rb[j].x; gs[5] += rb[j].y; gs[6] += rb[j].z; gs[7] += rb[j].w;
-                    gs[8] += rc[j].x; gs[9] += rc[j].y;
-                }
+                for (int j = 0; j < 4; j++)
+#pragma unroll
+                    for (int k = 0; k < 10; k++) gs[k] += rw[j][k];
             }
         }
     }
@@ -323,8 +319,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         s_meta[lane] = make_uint2(pst, len ? p.inst_start[i] : 0u);
         wave_lds_sync();
         for (uint32_t c0 = 0; c0 < total; c0 += CH) {
-            float4 ra[PER], rb[PER];
-            float2 rc[PER];
+            float rw[PER][10];
             uint32_t sidx[PER];
             uint32_t uu[PER];
 #pragma unroll
@@ -344,22 +339,16 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
             }
 #pragma unroll
             for (uint32_t r = 0; r < PER; r++) {  // ... then only the rows the composite wrote
-                ra[r] = rb[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-                rc[r] = make_float2(0.f, 0.f);
-                if (sidx[r] != INV_NONE) {
-                    const float4 *src = reinterpret_cast<const float4 *>(p.rows + (size_t)uu[r] * GRAD_ROW);
-                    ra[r] = src[0];
-                    rb[r] = src[1];
-                    rc[r] = *reinterpret_cast<const float2 *>(src + 2);
-                }
+#pragma unroll
+                for (int k = 0; k < 10; k++) rw[r][k] = 0.f;
+                if (sidx[r] != INV_NONE) load_row(p.rows, uu[r], rw[r]);
             }
 #pragma unroll
             for (uint32_t r = 0; r < PER; r++) {
                 const uint32_t q = r * 64 + lane;  // pair within the chunk
                 float *d = sw + q * 10;
-                d[0] = ra[r].x; d[1] = ra[r].y; d[2] = ra[r].z; d[3] = ra[r].w;
-                d[4] = rb[r].x; d[5] = rb[r].y; d[6] = rb[r].z; d[7] = rb[r].w;
-                d[8] = rc[r].x; d[9] = rc[r].y;
+#pragma unroll
+                for (int k = 0; k < 10; k++) d[k] = rw[r][k];
             }
             wave_lds_sync();
             const uint32_t lo = max(pst, c0), hi = min(pst + len, c0 + CH);

@@ -36,7 +36,7 @@ def test_buffer_sizes_and_layout():
     g1, g2 = lib.gsr_geom_buffer_bytes(1000), lib.gsr_geom_buffer_bytes(2000)
     assert 0 < g1 < g2
     assert lib.gsr_binning_buffer_bytes(10_000, 640, 480) > 10_000 * 16
-    assert lib.gsr_bwd_scratch_bytes(1000, 10) >= (1000 + 10) * 48
+    assert lib.gsr_bwd_scratch_bytes(1000, 10) >= (1000 + 10) * 40
     lay = _native.state_layout(1000, 5000, 100, 80)
     assert all(v % 256 == 0 for v in lay.values())
     # distinct arrays inside one buffer never start at the same offset
