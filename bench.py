@@ -39,6 +39,7 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
 FP32_VALU_PEAK_TF = 157.3  # MI355X_MICROARCH.md chip table (spec)
 VALU_ISSUE_NS = 1.29   # per wave-instruction per SIMD, every SIMD issuing fp32 FMA (tools/probes/valu_rate_probe.hip)
 TRANS_EXTRA_NS = 2.2   # v_exp / v_rcp cost ~3.5 ns on the same pipe
+EVENT_EVERY = 4  # timed steps per step that carries the dominant kernel's event pair
 PY_REFERENCE_CFG3_S = 730.0  # reference Python rasterizer, cfg 3 fwd+bwd, 8-core Xeon
 
 CONFIGS = {
@@ -138,20 +139,22 @@ def main():
         torch.cuda.synchronize()
         _native.set_profiling(False)
         stage_avg = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in _native.stage_times().items()}
-    # Every event is a marker packet in the stream, so the timed steps carry events around the dominant
-    # composite kernel only (its live launch time for the roofline), not around every stage.
+    # Every event is a marker packet in the stream, and the kernel after one waits ~6 us for it (rocprofv3 trace:
+    # an event pair around render_bwd adds ~12 us to a step), so the timed steps carry events around the dominant
+    # composite kernel only (its live launch time for the roofline), and only on every EVENT_EVERY-th step.
     dom = max(("render_fwd", "render_bwd"), key=lambda k: stage_avg.get(k, 0.0))
 
     # ---- timed region ----
     _native.reset_stage_times()
     if use_events:
         _native.set_tuning("prof_mask", _native.stage_mask(dom))
-        _native.set_profiling(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if use_events:
+            _native.set_profiling(i % EVENT_EVERY == 0)
         st = step()
     torch.cuda.synchronize()
     if world > 1:
@@ -177,7 +180,7 @@ def main():
         # F6 composite fwd = 8 B/T + 44 B/I + 24 B/P; B1 composite bwd adds 40 B/I of grads
         "render_fwd": 8 * T + 44 * I + 24 * npix,
         "render_bwd": 8 * T + 44 * I + 24 * npix + 40 * I,
-        "preprocess": n * (40 + 12 * M) + n * 48,
+        "preprocess": n * (40 + 12 * M) + n * (48 + 36),  # + the SH colour's direction Jacobian (9 floats)
         "preprocess_bwd": n * (40 + 12 * M) + 88 * n + n * (56 + 12 * M),
     }
     flops = {"render_fwd": 25.0 * sum_contrib, "render_bwd": 70.0 * sum_contrib}
@@ -259,7 +262,8 @@ def main():
         "config": {"workload": cfg["desc"], "gaussians": n, "width": W, "height": H, "sh_degree": deg,
                    "views_per_step": world, "parallelism": f"dp{world} (one view per GPU, RCCL gradient exchange: {mode})",
                    "instances_per_view": I, "sum_n_contrib": sum_contrib,
-                   "stage_events": ("timed steps: dominant kernel only; stages_ms: separate untimed pass"
+                   "stage_events": (f"timed steps: dominant kernel only, every {EVENT_EVERY}th step; stages_ms: "
+                                    "separate untimed pass"
                                     if use_events else "none")},
         **({"multi_gpu_note": "the RCCL exchange cannot be rehearsed on a 1-GPU box (RCCL rejects two ranks on one "
                               "device); gloo world-size-2 tests cover its logic (DESIGN.md §6)"} if world > 1 else {}),

@@ -13,6 +13,7 @@
 #include <mutex>
 
 #include <immintrin.h>
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -219,10 +220,12 @@ uint32_t next_readback_seq(int dev) {
 
 // Spin until the preprocess's last workgroup has published {total lo, hi, big count, seq} at hw[CNT_WORDS] (one
 // 16-B store, read here with one 16-B load: aligned 16-B SSE loads are single-copy atomic on AVX-capable x86).
-// Every 4096 polls the stream is queried, so a failed launch or a kernel fault returns an error instead of
-// spinning forever.
+// Once the wait has lasted a millisecond the stream is queried every millisecond, so a failed launch or a kernel
+// fault returns an error instead of spinning forever.  Not sooner: a hipStreamQuery puts a marker on the stream,
+// and the next kernel's dispatch waited ~6 us behind it (a gap before the bucket scatter on every forward).
 int wait_readback(const uint32_t *hw, uint32_t seq, hipStream_t s, uint64_t *total, uint32_t *nbig) {
     const __m128i *src = reinterpret_cast<const __m128i *>(hw + CNT_WORDS);
+    auto next_query = std::chrono::steady_clock::now() + std::chrono::milliseconds(1);
     for (uint64_t it = 1;; it++) {
         const __m128i v = _mm_load_si128((const __m128i *)(volatile const void *)src);
         alignas(16) uint32_t w[4];
@@ -232,11 +235,12 @@ int wait_readback(const uint32_t *hw, uint32_t seq, hipStream_t s, uint64_t *tot
             *nbig = w[2];
             return GSR_OK;
         }
-        if ((it & 4095) == 0) {
+        if ((it & 255) == 0 && std::chrono::steady_clock::now() >= next_query) {
             const hipError_t e = hipStreamQuery(s);
             if (e != hipSuccess && e != hipErrorNotReady) return fail(GSR_ERR_HIP, hipGetErrorString(e));
             if (e == hipSuccess && __atomic_load_n(hw + CNT_WORDS + 3, __ATOMIC_ACQUIRE) != seq)
                 return fail(GSR_ERR_HIP, "preprocess finished without publishing its counters");
+            next_query = std::chrono::steady_clock::now() + std::chrono::milliseconds(1);
         }
         _mm_pause();
     }

@@ -709,8 +709,11 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
 //     `idx < n_contrib` compare is skipped (a scalar bit test selects the variant);
 //   * the staged records are one 48-byte FwdRec array.
 //   The pixel update is v4's, so gradients are bitwise those of v4.
+#ifndef GSR_BWD_MINW
+#define GSR_BWD_MINW 5
+#endif
 template <bool HAS_INV, bool LASTC>
-__global__ __launch_bounds__(64, 5) void render_bwd_v5_kernel(RenderBwdParams p) {
+__global__ __launch_bounds__(64, GSR_BWD_MINW) void render_bwd_v5_kernel(RenderBwdParams p) {
     __shared__ FwdRec s_rec[BWD_BATCH];
     __shared__ __attribute__((aligned(16))) float s_part[BWD_BATCH][PART];  // [instance][10 sums]
     const int lane = threadIdx.x;

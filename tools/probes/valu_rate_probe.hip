@@ -13,6 +13,7 @@ template <int OP>
 __global__ __launch_bounds__(256) void probe(float *out, unsigned long long *cyc, float seed, unsigned useed) {
     float a[8];
     unsigned sc[8];
+    unsigned long long m64 = ((unsigned long long)useed << 32) | useed, m64b = ~0ull ^ useed;
     f2 p[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) {
@@ -47,6 +48,14 @@ __global__ __launch_bounds__(256) void probe(float *out, unsigned long long *cyc
                 if (i & 1) asm volatile("s_add_u32 %0, %0, 3" : "+s"(sc[i]) : : "scc");
                 else asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c));
             }
+            if (OP == 11) {  // 3 v_fma : 1 s_add (the composite backward's VALU : SALU mix)
+                if ((i & 3) == 3) asm volatile("s_add_u32 %0, %0, 3" : "+s"(sc[i]) : : "scc");
+                else asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c));
+            }
+            if (OP == 12) {  // 1 v_fma : 1 s_and_b64 (64-bit mask logic, as the exec-mask control uses)
+                if (i & 1) asm volatile("s_and_b64 %0, %0, %1" : "+s"(m64) : "s"(m64b) : "scc");
+                else asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c));
+            }
             if (OP == 8) {  // alternating v_fma / v_pk_fma
                 if (i & 1) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(p[i]) : "v"(b2), "v"(c2));
                 else asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c));
@@ -58,6 +67,7 @@ __global__ __launch_bounds__(256) void probe(float *out, unsigned long long *cyc
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < 8; i++) s += a[i] + p[i].x + p[i].y + (float)sc[i];
+    s += (float)(unsigned)m64;
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
     if (threadIdx.x % 64 == 0) {
         cyc[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = t1 - t0;
@@ -117,5 +127,7 @@ int main() {
     run<8>("fma / pk_fma alt", out, cyc);
     run<9>("s_add_u32", out, cyc);
     run<10>("fma / s_add alt", out, cyc);
+    run<11>("3 fma : 1 s_add", out, cyc);
+    run<12>("fma / s_and_b64 alt", out, cyc);
     return 0;
 }
