@@ -83,7 +83,9 @@ def main():
     torch.cuda.synchronize()
     _native.set_tuning("stamp", 0)
     T = ((cfg["W"] + 15) // 16) * ((cfg["H"] + 15) // 16)
-    nfwd = T + T * 5 // 100  # launch slots incl. split halves (fwd_split_pct default 5)
+    # launch slots: whole tiles (render_fwd_v6 <4, 6>) unless the image is small enough for 4 row-strip parts
+    # (launch_render_fwd's fwd_part_slots rule)
+    nfwd = T * 4 if T * 4 <= 16384 else T
     out = {"fwd": summarise(_native.wave_stamps(0, nfwd), nfwd), "bwd": summarise(_native.wave_stamps(1, T), T)}
     print(json.dumps(out, indent=1))
 
