@@ -7,15 +7,16 @@
 
 One step on every rank = one forward + backward of the HIP rasterizer (C ABI, include/gsrast.h) for that
 rank's view of the shared 1M-Gaussian scene (view k = the treehill view rotated 2*pi*k/8 about world y),
-with the upstream gradients dL/dimage, dL/dinvdepth fixed, followed by the per-view densification
-statistics and -- for N > 1 -- one RCCL all-reduce (sum) of the per-Gaussian gradients + statistics and a
-max-reduce of the radii (BASELINE.json config 4: one view per GPU).  Per-GPU work is fixed, so scaling is
-weak.  value = N * Gaussians * W * H / step time (Gaussians*pixels/s, whole job).
+with the upstream gradients dL/dimage, dL/dinvdepth fixed, the per-view densification statistics accumulated
+by the backward kernel, and -- for N > 1 -- the per-step exchange of multiview.py: one RCCL all-reduce (sum)
+of the per-Gaussian parameter gradients plus one all-gather of the compact SH factors (BASELINE.json config
+4: one view per GPU).  The statistics are reduced over ranks only when the model densifies.  Per-GPU work is
+fixed, so scaling is weak.  value = N * Gaussians * W * H / step time (Gaussians*pixels/s, whole job).
 
 Extra fields on the one JSON line:
   roofline      dominant kernel (a composite pass, fp32-VALU-bound): algorithmic flops / its average duration
-                from a hipEvent pair recorded around that kernel's stage on the launch stream during the timed
-                steps (the only events in the timed region; SURVEY.md §8(d) flops), with the same launch's
+                from a hipEvent pair recorded around that kernel's stage on the launch stream on every 4th timed
+                step (the only events in the timed region; SURVEY.md §8(d) flops), with the same launch's
                 algorithmic-bytes HBM figure and PMC traffic beside it;
   cpu_baseline  the oracle (oracle/gsr_oracle.c, C + OpenMP) on the same workload on the host cores;
   stages_ms     average device time of every pipeline stage per step, from a separate untimed pass of K steps
@@ -118,8 +119,10 @@ def main():
     def step():
         color, radii, invd, st = forward_raw(sc.means3D, sc.shs, None, sc.opacities, sc.scales, sc.rotations, None,
                                              settings)
-        backward_raw(st, settings, dcolor, dinv, out=red.backward_out(), compact_sh=red.compact)
-        red.record_view(red.means2D, radii, stats_written=True)
+        # densification statistics and max radii accumulate in the backward kernel; they are reduced over ranks
+        # only when the model densifies (ViewGradReducer.sync_densify_stats), not every step
+        backward_raw(st, settings, dcolor, dinv, out=red.backward_out(), compact_sh=red.compact,
+                     accumulate_stats=True)
         red.reduce(sc.means3D, c.campos)
         return st
 

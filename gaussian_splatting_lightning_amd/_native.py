@@ -41,6 +41,7 @@ class BackwardArgs(ctypes.Structure):
         ("dL_drotations", _fp),
         ("dL_dcolors_sh", _fp),
         ("densify_stats", _fp),
+        ("densify_accumulate", ctypes.c_int), ("max_radii2D", _fp),
     ]
 
 

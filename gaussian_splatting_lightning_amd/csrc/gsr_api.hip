@@ -639,6 +639,8 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     pp.dL_dmeans3D = a->dL_dmeans3D; pp.dL_dcov3D = a->dL_dcov3D; pp.dL_dsh = a->dL_dsh;
     pp.dL_dcolors_sh = a->dL_dcolors_sh;
     pp.densify_stats = a->densify_stats;
+    pp.densify_accumulate = a->densify_accumulate;
+    pp.max_radii2D = a->max_radii2D;
     pp.dL_dscales = a->dL_dscales; pp.dL_drot = a->dL_drotations;
     if (pp.shs == nullptr && a->dL_dsh && a->M > 0)
         GSR_HIP(hipMemsetAsync(a->dL_dsh, 0, sizeof(float) * (size_t)P * a->M * 3, stream));

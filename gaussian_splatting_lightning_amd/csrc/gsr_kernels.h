@@ -166,6 +166,8 @@ struct PreprocessBwdParams {
     float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales, *dL_drot;
     float *dL_dcolors_sh;  // clamp-masked colour gradient (may be null)
     float *densify_stats;  // (P,2) |dL/dmeans2D[:2]|, radii > 0 (may be null)
+    int densify_accumulate;  // densify_stats += instead of =
+    int *max_radii2D;        // (P) max(max_radii2D, radii) (may be null)
 };
 void launch_preprocess_bwd(hipStream_t s, const PreprocessBwdParams &p);
 

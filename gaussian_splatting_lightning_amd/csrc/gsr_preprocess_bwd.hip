@@ -95,9 +95,16 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
         p.dL_dmeans2D[3 * i + 1] = gs[1];
         p.dL_dmeans2D[3 * i + 2] = 0.f;
     }
-    if (p.densify_stats)  // torch.linalg.vector_norm(grad[:, :2]) and the visibility count of this view
-        *reinterpret_cast<float2 *>(p.densify_stats + 2 * i) =
-            make_float2(sqrtf(gs[0] * gs[0] + gs[1] * gs[1]), vis ? 1.f : 0.f);
+    if (p.densify_stats) {  // torch.linalg.vector_norm(grad[:, :2]) and the visibility count of this view
+        float2 st = make_float2(sqrtf(gs[0] * gs[0] + gs[1] * gs[1]), vis ? 1.f : 0.f);
+        float2 *dst = reinterpret_cast<float2 *>(p.densify_stats + 2 * i);
+        if (p.densify_accumulate) {
+            const float2 old = *dst;
+            st = make_float2(old.x + st.x, old.y + st.y);
+        }
+        *dst = st;
+    }
+    if (p.max_radii2D) p.max_radii2D[i] = max(p.max_radii2D[i], p.radii[i]);
     if (p.dL_dcolors) {
         p.dL_dcolors[3 * i] = gs[6];
         p.dL_dcolors[3 * i + 1] = gs[7];

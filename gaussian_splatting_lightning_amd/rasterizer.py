@@ -154,13 +154,15 @@ def forward_raw(means3D, sh, colors_precomp, opacities, scales, rotations, cov3D
 
 
 def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_depth=None, out=None,
-                 compact_sh=False):
+                 compact_sh=False, accumulate_stats=False):
     """One call of gsr_backward.  Returns a dict of gradients (means3D, means2D, shs, colors_precomp,
     opacities, scales, rotations, cov3D_precomp); entries are None where the input was absent.
     `out` may supply preallocated contiguous float32 destinations (e.g. views into one flat buffer that is
     then all-reduced): keys means2D (P,3), colors (P,3), opacities (P,1), means3D (P,3), cov3D (P,6),
     shs (P,M,3), scales (P,3), rotations (P,4), colors_sh (P,3), densify_stats (P,2) (|dL/dmeans2D[:2]| and
-    radii > 0 of this view, gaussian_model.py:175-181).
+    radii > 0 of this view, gaussian_model.py:175-181), max_radii2D (P,) int32.
+    accumulate_stats=True adds this view's densify_stats to out["densify_stats"] (the reference's
+    add_densification_stats); out["max_radii2D"] is always max-accumulated with this view's radii.
     compact_sh=True skips dL/dshs and returns the clamp-masked colour gradient "colors_sh" instead -- the
     per-view factor that `sh_backward_views` expands after an all-gather (multiview.py)."""
     lib = _native.load()
@@ -195,6 +197,9 @@ def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_
     dsh = None if compact_sh else dst("shs", P, max(M, 0), 3)
     dcsh = dst("colors_sh", P, 3) if (compact_sh or "colors_sh" in out) else None
     dstats = dst("densify_stats", P, 2) if "densify_stats" in out else None
+    mrad = out.get("max_radii2D")
+    if mrad is not None and (tuple(mrad.shape) != (P,) or mrad.dtype != torch.int32 or not mrad.is_contiguous()):
+        raise RuntimeError(f"out['max_radii2D'] must be a contiguous int32 tensor of shape ({P},)")
     dscales = dst("scales", P, 3)
     drot = dst("rotations", P, 4)
     bufs = _Buffers(device)
@@ -210,7 +215,7 @@ def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_
         dL_dmeans2D=dmeans2D.data_ptr(), dL_dcolors=_ptr(dcolors), dL_dopacity=dopac.data_ptr(),
         dL_dmeans3D=dmeans3D.data_ptr(), dL_dcov3D=_ptr(dcov), dL_dsh=_ptr(dsh),
         dL_dscales=dscales.data_ptr(), dL_drotations=drot.data_ptr(), dL_dcolors_sh=_ptr(dcsh),
-        densify_stats=_ptr(dstats))
+        densify_stats=_ptr(dstats), densify_accumulate=int(bool(accumulate_stats)), max_radii2D=_ptr(mrad))
     with torch.cuda.device(device):
         rc = lib.gsr_backward(ctypes.byref(a), bufs.callback, None, _stream_handle(device))
     _native.check(rc, "rasterize_gaussians_backward")

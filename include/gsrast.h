@@ -117,6 +117,11 @@ typedef struct gsr_backward_args {
     /* (P,2) densification statistics of this view (gaussian_model.py:175-181): [i][0] = |dL/dmeans2D[i][:2]|,
      * [i][1] = 1 if radii[i] > 0 else 0; NULL to skip. */
     float *densify_stats;
+    /* densify_accumulate != 0: densify_stats += this view's statistics instead of =, i.e. the reference's
+     * add_densification_stats (xyz_gradient_accum += norm, denom += 1 for visible Gaussians) across views and
+     * steps; max_radii2D (P) int32, if non-NULL, becomes max(max_radii2D, radii) (gaussian_model.py:175-176). */
+    int densify_accumulate;
+    int *max_radii2D;
 } gsr_backward_args;
 
 /* Replaces `_C.rasterize_gaussians_backward` (RasterizeGaussiansBackwardCUDA -> Rasterizer::backward).

@@ -55,8 +55,9 @@ def worker(rank, world, port, mode, result_dir):
         red.record_view(red.means2D, torch.from_numpy(g["radii"]))
         red.reduce(torch.from_numpy(g["means3D_in"]), torch.from_numpy(g["campos"]))
         res = {k: v.numpy() for k, v in red.grads.items()}
-        res["stats"] = red.stats.numpy()
-        res["radii_max"] = red.radii_max.numpy()
+        stats, radii_max = red.sync_densify_stats()
+        res["stats"] = stats.numpy()
+        res["radii_max"] = radii_max.numpy()
         np.savez(os.path.join(result_dir, f"rank{rank}.npz"), **res)
     finally:
         dist.destroy_process_group()

@@ -362,6 +362,12 @@ def test_densify_stats_from_backward(gpu_device):
     ref = torch.linalg.vector_norm(g["means2D"][:, :2], dim=1)
     assert torch.allclose(stats[:, 0], ref, rtol=1e-6, atol=0)
     assert torch.equal(stats[:, 1], (radii > 0).float())
+    # accumulate mode (the reference's add_densification_stats over steps) and the max-radii accumulator
+    acc = stats.clone()
+    mrad = torch.full((5000,), 3, dtype=torch.int32, device=gpu_device)
+    backward_raw(st, rs, dc, di, out={"densify_stats": acc, "max_radii2D": mrad}, accumulate_stats=True)
+    assert torch.allclose(acc, 2 * stats, rtol=1e-6, atol=0)
+    assert torch.equal(mrad, torch.maximum(radii.to(torch.int32), torch.full_like(mrad, 3)))
 
 
 @pytest.mark.gpu
