@@ -114,19 +114,22 @@ class ViewGradReducer:
         """The per-step exchange: SUM of the parameter gradients over ranks (and the SH expansion)."""
         if self.compact:
             self.gather_in[3 * self.n:].copy_(campos.reshape(3))
-        if self.world > 1:
-            work = [dist.all_reduce(self.flat, group=self.group, async_op=True)]
-            if self.compact:
-                work.append(_all_gather(self.gather_all, self.gather_in, self.group))
-            for w in work:
-                if w is not None:
-                    w.wait()
-        elif self.compact:
-            self.gather_all[0].copy_(self.gather_in)
+        # the all-gather is issued first: the collectives run in issue order on the communicator's stream, so the
+        # SH expansion (which needs only the gathered factors) overlaps the all-reduce
+        gather = None
+        if self.world > 1 and self.compact:
+            gather = _all_gather(self.gather_all, self.gather_in, self.group)
+        reduce = dist.all_reduce(self.flat, group=self.group, async_op=True) if self.world > 1 else None
         if self.compact:
+            if gather is not None:
+                gather.wait()
+            elif self.world == 1:
+                self.gather_all[0].copy_(self.gather_in)
             colors_all = self.gather_all[:, :3 * self.n].view(self.world, self.n, 3)
             campos_all = self.gather_all[:, 3 * self.n:]
             self._sh_views(means3D, campos_all, colors_all, self.D, self.M, out=self.shs)
+        if reduce is not None:
+            reduce.wait()
 
     def sync_densify_stats(self):
         """SUM the accumulated statistics and MAX the radii over ranks, in place; returns (stats, radii_max):
