@@ -973,7 +973,11 @@ void launch_render_fwd(hipStream_t s, const RenderFwdParams &p0) {
         RenderFwdParams q = p;
         q.stamps = tuning("stamp", 0) ? stamp_buffer(0) : nullptr;
         const dim3 grid(div_up(p.num_tiles, 4)), block(256);
-        if (tuning("fwd_part_waves", 8) >= 6) render_fwd_v6_kernel<4, 6><<<grid, block, 0, s>>>(q);
+        // 8 waves per SIMD (64 VGPRs, one 8-byte spill outside the pair loop): cfg3 0.180 -> 0.172 ms, cfg5 0.517 ->
+        // 0.478 ms against 6 waves (65 VGPRs, i.e. 7 resident)
+        const int mw = tuning("fwd_whole_waves", 8);
+        if (mw >= 8) render_fwd_v6_kernel<4, 8><<<grid, block, 0, s>>>(q);
+        else if (mw >= 6) render_fwd_v6_kernel<4, 6><<<grid, block, 0, s>>>(q);
         else render_fwd_v6_kernel<4, 4><<<grid, block, 0, s>>>(q);
         return;
     }
