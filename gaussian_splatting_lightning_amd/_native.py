@@ -174,6 +174,10 @@ def load(path: str | None = None):
     lib.gsr_last_error.restype = ctypes.c_char_p
     lib.gsr_build_info.restype = ctypes.c_char_p
     _lib = lib
+    # A/B experiments from the command line: GSR_TUNE="knob=value,knob=value" (gsr_set_tuning before first use)
+    for kv in filter(None, os.environ.get("GSR_TUNE", "").split(",")):
+        k, v = kv.split("=")
+        lib.gsr_set_tuning(k.strip().encode(), int(v))
     return lib
 
 
