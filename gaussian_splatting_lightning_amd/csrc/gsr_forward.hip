@@ -236,7 +236,7 @@ void launch_preprocess(hipStream_t s, const PreprocessParams &p) {
 // rank window and then walk EXP_PER consecutive instances, emitting the tile id (sort key) and the
 // Gaussian id of each.
 // ------------------------------------------------------------------------------------------------
-constexpr int EXP_PER = 8;
+constexpr int EXP_PER = 4;  // 1024 instances per block, 36 KB of LDS: 4 blocks/CU (cfg 5: 0.396 -> 0.380 ms; 2: 0.400)
 constexpr int EXP_TILE = 256 * EXP_PER;
 
 // Wave-cooperative search: last index r in [0, n] with off[r] <= u (off non-decreasing, off[0] <= u).
