@@ -41,6 +41,7 @@ FP32_VALU_PEAK_TF = 157.3  # MI355X_MICROARCH.md chip table (spec)
 VALU_ISSUE_NS = 1.29   # per wave-instruction per SIMD, every SIMD issuing fp32 FMA (tools/probes/valu_rate_probe.hip)
 TRANS_EXTRA_NS = 2.2   # v_exp / v_rcp cost ~3.5 ns on the same pipe
 EVENT_EVERY = 4  # timed steps per step that carries the dominant kernel's event pair
+SETTLE_S = 0.3   # minimum untimed warmup (seconds of steps) before timing
 PY_REFERENCE_CFG3_S = 730.0  # reference Python rasterizer, cfg 3 fwd+bwd, 8-core Xeon
 
 CONFIGS = {
@@ -127,9 +128,22 @@ def main():
         return st
 
     # ---- warmup ----
+    # W steps, and then more untimed steps until SETTLE_S of GPU work have run: from idle the GPU's clocks
+    # take tens of ms to ramp, so 5 steps (~4 ms) left the first timed steps slow (0.899 vs 0.858 ms/step
+    # measured with 5 vs 25 warmup steps)
+    t_w = time.perf_counter()
     for _ in range(args.warmup):
         st = step()
     torch.cuda.synchronize()
+    while True:  # ranks agree on every extension (the steps run collectives)
+        more = torch.tensor([1.0 if time.perf_counter() - t_w < SETTLE_S else 0.0], device=dev)
+        if world > 1:
+            dist.all_reduce(more, op=dist.ReduceOp.MAX)
+        if more.item() == 0.0:
+            break
+        for _ in range(10):
+            st = step()
+        torch.cuda.synchronize()
 
     # ---- per-stage breakdown (untimed): an event pair around every stage ----
     use_events = not args.no_stage_events
@@ -260,7 +274,7 @@ def main():
     value = world * n * W * H / (ms_per_step * 1e-3)
     line = {
         "metric": METRIC, "value": value, "unit": "Gaussians·pixels/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+        "warmup": args.warmup, "warmup_settle_s": SETTLE_S, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": cfg["desc"], "gaussians": n, "width": W, "height": H, "sh_degree": deg,
                    "views_per_step": world, "parallelism": f"dp{world} (one view per GPU, RCCL gradient exchange: {mode})",
