@@ -25,6 +25,7 @@ Extra fields on the one JSON line:
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import math
 import os
@@ -165,6 +166,11 @@ def main():
     _native.reset_stage_times()
     if use_events:
         _native.set_tuning("prof_mask", _native.stage_mask(dom))
+    # Python's cyclic garbage collector is held off while timing: a collection pass stalled the host for
+    # ~0.6 ms in the middle of a step (rocprofv3 trace: one gap before a backward's first kernel), which the
+    # GPU then waits out
+    gc.collect()
+    gc.disable()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -177,6 +183,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     _native.set_profiling(False)
     _native.set_tuning("prof_mask", -1)
     timed_stages = _native.stage_times()
