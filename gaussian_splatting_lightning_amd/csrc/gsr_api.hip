@@ -331,9 +331,10 @@ void gsr_state_layout_query(int P, int64_t R, int W, int H, gsr_state_layout *ou
     carve_binning(base, R, T, b);
     ImageState im;
     carve_image(base, W, H, im);
-    out->geom_rec_a = off(g.rec_a);
-    out->geom_rec_b = off(g.rec_b);
-    out->geom_rec_c = off(g.rec_c);
+    out->geom_rec_a = off(&g.rec->a);
+    out->geom_rec_b = off(&g.rec->b);
+    out->geom_rec_c = off(&g.rec->c);
+    out->geom_rec_stride = sizeof(GRec);
     out->geom_tiles = off(g.tiles);
     out->geom_order = off(g.order);
     out->geom_inst_off = off(g.inst_off);
@@ -545,7 +546,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     rp.tile_order = lpt ? im.order_fwd : nullptr;
     rp.ranges = im.ranges; rp.sorted_u = b.sorted_u; rp.inst_gid = b.inst_gid;
     rp.point_list = b.point_list; rp.inv = b.inv; rp.tile_loaded = im.tile_loaded;
-    rp.rec_a = g.rec_a; rp.rec_b = g.rec_b; rp.rec_c = g.rec_c;
+    rp.rec = g.rec;
     rp.bg = a->background;
     rp.out_color = a->out_color; rp.out_invdepth = a->out_invdepth; rp.final_T = im.final_T;
     rp.n_contrib = im.n_contrib; rp.tile_last = im.tile_last;
@@ -606,7 +607,7 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
         if (own_order) launch_tile_order(stream, im.ranges, im.tile_last, 1, (int)T, im.order_bwd);
         rp.tile_order = lpt ? (own_order ? im.order_bwd : im.order_fwd) : nullptr;
         rp.tile_last = im.tile_last; rp.tile_loaded = im.tile_loaded;
-        rp.rec_a = g.rec_a; rp.rec_b = g.rec_b; rp.rec_c = g.rec_c;
+        rp.rec = g.rec;
         rp.bg = a->background; rp.final_T = im.final_T; rp.dL_dpix = a->dL_dpix; rp.dL_dinvdepth = a->dL_dinvdepth;
         rp.rows = rows;
         rp.sorted_u = b.sorted_u;

@@ -227,11 +227,11 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_bwd_v3_kernel(Rend
             const uint32_t s_me = range.x + (uint32_t)(bend - 1 - lane);
             my_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
             const uint32_t gid = p.point_list[s_me];
-            my_a = p.rec_a[gid];
-            my_b = p.rec_b[gid];
+            my_a = p.rec[gid].a;
+            my_b = p.rec[gid].b;
             s_a[w][lane] = stage_rec_a(my_a);
             s_b[w][lane] = stage_rec_b(my_b);
-            s_c[w][lane] = p.rec_c[gid];
+            s_c[w][lane] = p.rec[gid].c;
         }
         wave_lds_sync();
         for (int j = 0; j < cnt; j++) {
@@ -389,11 +389,11 @@ __global__ __launch_bounds__(64, MIN_WAVES) void render_bwd_v4_kernel(RenderBwdP
             const uint32_t s_me = range.x + (uint32_t)(bend - 1 - lane);
             my_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
             const uint32_t gid = p.point_list[s_me];
-            my_a = p.rec_a[gid];
-            my_b = p.rec_b[gid];
+            my_a = p.rec[gid].a;
+            my_b = p.rec[gid].b;
             s_a[lane] = stage_rec_a(my_a);
             s_b[lane] = stage_rec_b(my_b);
-            s_c[lane] = p.rec_c[gid];
+            s_c[lane] = p.rec[gid].c;
             if (STRIP) my_m = cell_mask(p.strip_exact, my_a, my_b, row0, (float)(tx * BLOCK_X));
         }
         // strip k of instance j is live iff bit j of sk[k] (wave-uniform, scalar registers)
@@ -598,11 +598,11 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
             const uint32_t s_me = range.x + (uint32_t)(bend - 1 - lane);
             my_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
             const uint32_t gid = p.point_list[s_me];
-            my_a = p.rec_a[gid];
-            my_b = p.rec_b[gid];
+            my_a = p.rec[gid].a;
+            my_b = p.rec[gid].b;
             s_a[lane] = stage_rec_a(my_a);
             s_b[lane] = stage_rec_b(my_b);
-            s_c[lane] = p.rec_c[gid];
+            s_c[lane] = p.rec[gid].c;
             s_m[lane] = cell_mask(p.strip_exact, my_a, my_b, row0, (float)(tx * BLOCK_X));
         }
         __syncthreads();
@@ -770,11 +770,11 @@ __global__ __launch_bounds__(64, GSR_BWD_MINW) void render_bwd_v5_kernel(RenderB
             const uint32_t s_me = r0 + (uint32_t)(bend - 1 - lane);
             my_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
             const uint32_t gid = p.point_list[s_me];
-            my_a = p.rec_a[gid];
-            my_b = p.rec_b[gid];
+            my_a = p.rec[gid].a;
+            my_b = p.rec[gid].b;
             s_rec[lane].a = stage_rec_a(my_a);
             s_rec[lane].b = stage_rec_b(my_b);
-            s_rec[lane].c = p.rec_c[gid];
+            s_rec[lane].c = p.rec[gid].c;
             my_m = cell_mask(p.strip_exact, my_a, my_b, row0, col0);
         }
         // sk[k] bit j: strip k of instance j (idx = bend - 1 - j) may hold a contributing pixel;
@@ -954,11 +954,11 @@ __global__ __launch_bounds__(64, 5) void render_bwd_v6_kernel(RenderBwdParams p)
             const uint32_t s_me = r0 + (uint32_t)(bend - 1 - lane);
             my_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
             const uint32_t gid = p.point_list[s_me];
-            my_a = p.rec_a[gid];
-            my_b = p.rec_b[gid];
+            my_a = p.rec[gid].a;
+            my_b = p.rec[gid].b;
             s_rec[lane].a = stage_rec_a(my_a);
             s_rec[lane].b = stage_rec_b(my_b);
-            s_rec[lane].c = p.rec_c[gid];
+            s_rec[lane].c = p.rec[gid].c;
             my_m = cell_mask(p.strip_exact, my_a, my_b, row0, col0);
         }
         // sk[k] bit j: strip k of instance j (idx = bend - 1 - j) may hold a contributing pixel (the batch's 32

@@ -2,9 +2,9 @@
 //
 // Layout of the three caller-owned scratch buffers (SURVEY.md §8(b) "Ownership"; the reference keeps
 // GeometryState/BinningState/ImageState in uint8 torch tensors, notes/rasterizer_note.h:27-40).  All
-// per-Gaussian render attributes are packed into 40 B so one tile batch gathers them with three
-// 16/16/8-byte loads per instance:
-//   rec_a = (x_pix, y_pix, conic.x, conic.y)   rec_b = (conic.z, opacity, r, g)   rec_c = (b, 1/depth)
+// per-Gaussian render attributes are packed into one 48-B record (GRec) so a tile batch gathers an instance with
+// three 16/16/8-byte loads from the same cache line:
+//   a = (x_pix, y_pix, conic.x, conic.y)   b = (conic.z, opacity, r, g)   c = (b, 1/depth)
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -90,11 +90,19 @@ constexpr uint32_t SEG_CAP = 511;         // longest tile the per-wave register 
                                           // SEG_CAP + 1 is a multiple of the LPT bucket width (seg_block)
 constexpr uint32_t SEG_BLOCK_CAP = 2048;  // longest tile one workgroup sorts (4 waves x 512 keys); longer: chunks
 
+// One Gaussian's render record: interleaved rather than three arrays, so the composite passes' random gathers
+// touch one or two cache lines per instance instead of three.
+struct GRec {
+    float4 a;  // x_pix, y_pix, conic.x, conic.y
+    float4 b;  // conic.z, opacity, r, g
+    float2 c;  // b, 1/depth
+    float2 pad;
+};
+static_assert(sizeof(GRec) == 48, "render record");
+
 struct GeomState {
     uint32_t *counters;    // CNT_WORDS
-    float4 *rec_a;         // P
-    float4 *rec_b;         // P
-    float2 *rec_c;         // P
+    GRec *rec;             // P
     uint32_t *depth_key;   // P: float bits of view depth, 0xffffffff if culled
     uint32_t *tiles;       // P: tiles touched
     uint8_t *clamped;      // P: bit c set if SH colour channel c was clamped at 0
@@ -120,9 +128,7 @@ inline size_t carve_geom(char *base, int P, GeomState &g) {
     g.counters = c.take<uint32_t>(CNT_WORDS);
     g.scan_status = c.take<uint64_t>(div_up(n + 1, SCAN_TILE) + 1);  // cleared together with the counters
     g.tile_status = c.take<uint64_t>(BK_MAX_TILES / 64 + 1);         // cleared together with the counters
-    g.rec_a = c.take<float4>(n);
-    g.rec_b = c.take<float4>(n);
-    g.rec_c = c.take<float2>(n);
+    g.rec = c.take<GRec>(n);
     g.tiles = c.take<uint32_t>(n);
     g.clamped = c.take<uint8_t>(n);
     g.sh_jac = c.take<float>((size_t)9 * n);

@@ -107,9 +107,9 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
         rgb = make_float3(fmaxf(rgb.x, 0.f), fmaxf(rgb.y, 0.f), fmaxf(rgb.z, 0.f));
     }
     const float opacity = opacity_in * hscale;
-    g.rec_a[i] = make_float4(pimg.x, pimg.y, conic_x, conic_y);
-    g.rec_b[i] = make_float4(conic_z, opacity, rgb.x, rgb.y);
-    g.rec_c[i] = make_float2(rgb.z, 1.f / pv.z);
+    g.rec[i].a = make_float4(pimg.x, pimg.y, conic_x, conic_y);
+    g.rec[i].b = make_float4(conic_z, opacity, rgb.x, rgb.y);
+    g.rec[i].c = make_float2(rgb.z, 1.f / pv.z);
     g.clamped[i] = clamp_bits;
     p.radii[i] = (int)radius;
     ci.need = p.cull && area <= (uint32_t)CULL_MAX_AREA;
@@ -435,9 +435,9 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_fwd_v3_kernel(Rend
             const uint32_t gid = p.inst_gid[u];
             p.point_list[s] = gid;
             p.inv[u] = s;
-            s_a[w][lane] = stage_rec_a(p.rec_a[gid]);
-            s_b[w][lane] = stage_rec_b(p.rec_b[gid]);
-            s_c[w][lane] = p.rec_c[gid];
+            s_a[w][lane] = stage_rec_a(p.rec[gid].a);
+            s_b[w][lane] = stage_rec_b(p.rec[gid].b);
+            s_c[w][lane] = p.rec[gid].c;
         }
         loaded_end = min(range.y, base + 64u);
         wave_lds_sync();
@@ -555,9 +555,9 @@ __device__ __forceinline__ void composite_fwd(const RenderFwdParams &p, const in
         if (s0 < range.y) {
             u1 = p.sorted_u[s0];
             g1 = p.inst_gid[u1];
-            ra = p.rec_a[g1];
-            rb = p.rec_b[g1];
-            rc = p.rec_c[g1];
+            ra = p.rec[g1].a;
+            rb = p.rec[g1].b;
+            rc = p.rec[g1].c;
         }
         if (s0 + 64 < range.y) {
             u2 = p.sorted_u[s0 + 64];
@@ -581,9 +581,9 @@ __device__ __forceinline__ void composite_fwd(const RenderFwdParams &p, const in
                 if (STRIP) s_m[lane] = cell_mask(p.strip_exact, ra, rb, row0, (float)(tx * BLOCK_X));
             }
             if (s + 64 < range.y) {
-                ra = p.rec_a[g2];
-                rb = p.rec_b[g2];
-                rc = p.rec_c[g2];
+                ra = p.rec[g2].a;
+                rb = p.rec[g2].b;
+                rc = p.rec[g2].c;
             }
             uint32_t ng2 = 0, nu3 = 0;
             if (s + 128 < range.y) ng2 = p.inst_gid[u3];
@@ -598,10 +598,10 @@ __device__ __forceinline__ void composite_fwd(const RenderFwdParams &p, const in
             const uint32_t gid = p.inst_gid[u];
             p.point_list[s] = gid;
             p.inv[u] = s;
-            const float4 ga = p.rec_a[gid], gb = p.rec_b[gid];
+            const float4 ga = p.rec[gid].a, gb = p.rec[gid].b;
             s_a[lane] = stage_rec_a(ga);
             s_b[lane] = stage_rec_b(gb);
-            s_c[lane] = p.rec_c[gid];
+            s_c[lane] = p.rec[gid].c;
             if (STRIP) s_m[lane] = cell_mask(p.strip_exact, ga, gb, row0, (float)(tx * BLOCK_X));
         }
         loaded_end = min(range.y, base + 64u);
@@ -756,10 +756,10 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v5_kernel(RenderFwd
             const uint32_t gid = p.inst_gid[u];
             p.point_list[s] = gid;
             p.inv[u] = s;
-            const float4 ga = p.rec_a[gid], gb = p.rec_b[gid];
+            const float4 ga = p.rec[gid].a, gb = p.rec[gid].b;
             sr[lane].a = stage_rec_a(ga);
             sr[lane].b = stage_rec_b(gb);
-            sr[lane].c = p.rec_c[gid];
+            sr[lane].c = p.rec[gid].c;
             m = cell_mask(p.strip_exact, ga, gb, row0, col0) >> kbase;
         }
         uint64_t sk[NPIX];
@@ -875,10 +875,10 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
             const uint32_t gid = p.inst_gid[u];
             p.point_list[s] = gid;
             p.inv[u] = s;
-            const float4 ga = p.rec_a[gid], gb = p.rec_b[gid];
+            const float4 ga = p.rec[gid].a, gb = p.rec[gid].b;
             sr[lane].a = stage_rec_a(ga);
             sr[lane].b = stage_rec_b(gb);
-            sr[lane].c = p.rec_c[gid];
+            sr[lane].c = p.rec[gid].c;
             m = cell_mask(p.strip_exact, ga, gb, row0, col0) >> kbase;
         }
         uint64_t sk[NPIX];

@@ -111,8 +111,7 @@ struct RenderFwdParams {
     const uint32_t *tile_order;  // launch slot -> tile (heaviest first), or null for identity
     const uint32_t *sorted_u, *inst_gid;
     uint32_t *point_list, *inv, *tile_loaded;
-    const float4 *rec_a, *rec_b;
-    const float2 *rec_c;
+    const GRec *rec;
     const float *bg;
     float *out_color, *out_invdepth, *final_T;
     uint32_t *n_contrib, *tile_last;
@@ -131,8 +130,7 @@ struct RenderBwdParams {
     const uint32_t *tile_order;  // launch slot -> tile (heaviest first), or null for identity
     const uint32_t *point_list, *n_contrib, *tile_last, *tile_loaded;
     const uint32_t *sorted_u;  // sorted position -> expansion index u (rows_by_u)
-    const float4 *rec_a, *rec_b;
-    const float2 *rec_c;
+    const GRec *rec;
     const float *bg, *final_T, *dL_dpix, *dL_dinvdepth;
     float *rows;    // R x GRAD_ROW
     int rows_by_u;  // 1: row of an instance at its expansion index u (Gaussian-major), 0: at its sorted position

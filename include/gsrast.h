@@ -240,7 +240,8 @@ size_t gsr_bwd_scratch_bytes(int64_t R, int64_t num_big);
  * the parity tests to compare the integer binning state (sorted instance list, tile ranges,
  * per-pixel contributor counts) bit for bit against the oracle. */
 typedef struct gsr_state_layout {
-    size_t geom_rec_a, geom_rec_b, geom_rec_c; /* float4, float4, float2 per Gaussian */
+    size_t geom_rec_a, geom_rec_b, geom_rec_c; /* float4, float4, float2 of Gaussian 0's record; Gaussian i's at
+                                                  + i * geom_rec_stride */
     size_t geom_tiles, geom_order, geom_inst_off, geom_inst_start, geom_clamped; /* u32, u32, u32, u32, u8 */
     size_t geom_depth_key;    /* u32 float bits of each Gaussian's view depth (0xffffffff: not rendered) */
     size_t geom_expand_rec;   /* uint4 {kept-tile mask lo, hi, rmin.x | rmin.y << 16, rect width} (mask 0 = all) */
@@ -248,6 +249,7 @@ typedef struct gsr_state_layout {
     size_t bin_sorted_u, bin_inst_gid;                                /* u32 per instance */
     size_t img_final_T, img_n_contrib, img_ranges, img_tile_last;     /* f32/u32 per pixel, uint2/u32 per tile */
     size_t img_tile_loaded;                                           /* u32 per tile */
+    size_t geom_rec_stride;                                           /* bytes per render record (48) */
 } gsr_state_layout;
 void gsr_state_layout_query(int P, int64_t R, int W, int H, gsr_state_layout *out);
 

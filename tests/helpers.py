@@ -111,9 +111,11 @@ def hip_state_arrays(out: dict) -> dict:
         final_T=view(st.image_buffer, lay["img_final_T"], W * H, torch.float32).reshape(H, W),
         tiles=view(st.geom_buffer, lay["geom_tiles"], P, i32).astype(np.uint32),
         num_rendered=R)
-    rec_a = view(st.geom_buffer, lay["geom_rec_a"], 4 * P, torch.float32).reshape(P, 4)
+    # render records: one 48-B (12-float) record per Gaussian, a = floats 0..3, b = 4..7, c = 8..9
+    stride = lay["geom_rec_stride"] // 4
+    rec = view(st.geom_buffer, lay["geom_rec_a"], stride * P, torch.float32).reshape(P, stride)
+    rec_a, rec_b = rec[:, 0:4], rec[:, 4:8]
     depth_bits = view(st.geom_buffer, lay["geom_depth_key"], P, i32)
-    rec_b = view(st.geom_buffer, lay["geom_rec_b"], 4 * P, torch.float32).reshape(P, 4)
     res["xy"] = np.ascontiguousarray(rec_a[:, :2])
     res["conic_opacity"] = np.ascontiguousarray(np.concatenate([rec_a[:, 2:4], rec_b[:, 0:2]], 1))
     res["depths"] = depth_bits.view(np.float32)

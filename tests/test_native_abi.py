@@ -38,7 +38,11 @@ def test_buffer_sizes_and_layout():
     assert lib.gsr_binning_buffer_bytes(10_000, 640, 480) > 10_000 * 16
     assert lib.gsr_bwd_scratch_bytes(1000, 10) >= (1000 + 10) * 40
     lay = _native.state_layout(1000, 5000, 100, 80)
-    assert all(v % 256 == 0 for v in lay.values())
+    stride = lay.pop("geom_rec_stride")
+    assert stride == 48
+    # the render record's three fields are interleaved (16, 16, 8 B at +0, +16, +32 of each 48-B record)
+    assert (lay["geom_rec_b"] - lay["geom_rec_a"], lay["geom_rec_c"] - lay["geom_rec_a"]) == (16, 32)
+    assert all(v % 256 == 0 for k, v in lay.items() if k not in ("geom_rec_b", "geom_rec_c"))
     # distinct arrays inside one buffer never start at the same offset
     geom = [v for k, v in lay.items() if k.startswith("geom_")]
     assert len(set(geom)) == len(geom)
