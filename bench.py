@@ -42,7 +42,7 @@ FP32_VALU_PEAK_TF = 157.3  # MI355X_MICROARCH.md chip table (spec)
 VALU_ISSUE_NS = 1.29   # per wave-instruction per SIMD, every SIMD issuing fp32 FMA (tools/probes/valu_rate_probe.hip)
 TRANS_EXTRA_NS = 2.2   # v_exp / v_rcp cost ~3.5 ns on the same pipe
 EVENT_EVERY = 4  # timed steps per step that carries the dominant kernel's event pair
-SETTLE_S = 0.3   # minimum untimed warmup (seconds of steps) before timing
+SETTLE_S = 0.2   # untimed steps (seconds) right before the timed ones, clocks at steady state
 PY_REFERENCE_CFG3_S = 730.0  # reference Python rasterizer, cfg 3 fwd+bwd, 8-core Xeon
 
 CONFIGS = {
@@ -129,22 +129,9 @@ def main():
         return st
 
     # ---- warmup ----
-    # W steps, and then more untimed steps until SETTLE_S of GPU work have run: from idle the GPU's clocks
-    # take tens of ms to ramp, so 5 steps (~4 ms) left the first timed steps slow (0.899 vs 0.858 ms/step
-    # measured with 5 vs 25 warmup steps)
-    t_w = time.perf_counter()
     for _ in range(args.warmup):
         st = step()
     torch.cuda.synchronize()
-    while True:  # ranks agree on every extension (the steps run collectives)
-        more = torch.tensor([1.0 if time.perf_counter() - t_w < SETTLE_S else 0.0], device=dev)
-        if world > 1:
-            dist.all_reduce(more, op=dist.ReduceOp.MAX)
-        if more.item() == 0.0:
-            break
-        for _ in range(10):
-            st = step()
-        torch.cuda.synchronize()
 
     # ---- per-stage breakdown (untimed): an event pair around every stage ----
     use_events = not args.no_stage_events
@@ -164,13 +151,27 @@ def main():
 
     # ---- timed region ----
     _native.reset_stage_times()
-    if use_events:
-        _native.set_tuning("prof_mask", _native.stage_mask(dom))
     # Python's cyclic garbage collector is held off while timing: a collection pass stalled the host for
     # ~0.6 ms in the middle of a step (rocprofv3 trace: one gap before a backward's first kernel), which the
     # GPU then waits out
     gc.collect()
     gc.disable()
+    # Settle: untimed steps for SETTLE_S right before the timed ones, after all host bookkeeping.  Idle, the
+    # GPU's clocks drop within milliseconds and take tens of ms of work to ramp back: a 43 ms pause before the
+    # timed steps (trace) made them run 918 -> 867 us per step, and 5 warmup steps alone measured 0.899 against
+    # 0.858 ms/step after 25.  Ranks agree on every extension (the steps run collectives).
+    t_w = time.perf_counter()
+    while True:
+        more = torch.tensor([1.0 if time.perf_counter() - t_w < SETTLE_S else 0.0], device=dev)
+        if world > 1:
+            dist.all_reduce(more, op=dist.ReduceOp.MAX)
+        if more.item() == 0.0:
+            break
+        for _ in range(10):
+            st = step()
+        torch.cuda.synchronize()
+    if use_events:
+        _native.set_tuning("prof_mask", _native.stage_mask(dom))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
