@@ -481,11 +481,19 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     // Otherwise the radix path: depth sort, depth-ordered expansion, stable tile sort.
     const bool bucket = bk_possible && (bk == 2 || (uint64_t)R <= (uint64_t)BK_MAX_MEAN * T);
     if (!bucket) {
-        GSR_STAGE(ST_DEPTH_SORT, dbg, launch_radix_sort(stream, g.sort, (uint32_t)P, 32, false, g.depth_key));
+        // the depth sort's last pass also writes the tile counts in depth order ("sort_gather" 0: the scan gathers
+        // them through the order instead)
+        bool sorted_tiles = false;
+        const bool sg = tuning("sort_gather", 1) != 0;
+        GSR_STAGE(ST_DEPTH_SORT, dbg,
+                  sorted_tiles = launch_radix_sort(stream, g.sort, (uint32_t)P, 32, false, g.depth_key,
+                                                   sg ? g.tiles : nullptr, sg ? g.tiles_sorted : nullptr));
         if (tuning("scan_lookback", 1))
             GSR_STAGE(ST_SCAN, dbg,
-                      launch_exclusive_scan_lookback(stream, g.tiles, g.order, (uint32_t)P, g.inst_off, g.scan_status,
-                                                     g.counters + CNT_SCAN_TICKET, g.counters + CNT_OVERFLOW));
+                      launch_exclusive_scan_lookback(stream, sorted_tiles ? g.tiles_sorted : g.tiles,
+                                                     sorted_tiles ? nullptr : g.order, (uint32_t)P, g.inst_off,
+                                                     g.scan_status, g.counters + CNT_SCAN_TICKET,
+                                                     g.counters + CNT_OVERFLOW));
         else
             GSR_STAGE(ST_SCAN, dbg,
                       launch_exclusive_scan(stream, g.tiles, g.order, (uint32_t)P, g.inst_off, g.scan_tmp,

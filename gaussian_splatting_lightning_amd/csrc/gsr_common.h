@@ -110,6 +110,7 @@ struct GeomState {
     uint4 *exp_rec;        // P: expansion record {kept-tile mask lo, hi, rmin.x | rmin.y << 16, rect width}; mask 0 =
                            //    all tiles of the rect (area > 64 or culling off).  One 16-B gather per Gaussian.
     uint32_t *inst_off;    // P+1: radix path: exclusive scan of tiles in depth order, [P] = total
+    uint32_t *tiles_sorted;  // P: radix path: tiles in depth order (written by the depth sort's last pass)
     uint32_t *inst_start;  // P+1: first instance (expansion order) of each Gaussian (bucket path: the
                            //      exclusive scan of tiles in Gaussian order, [P] = total)
     uint32_t *block_sums;  // div_up(P, 256): kept-tile totals of the preprocess blocks (bucket path)
@@ -134,6 +135,7 @@ inline size_t carve_geom(char *base, int P, GeomState &g) {
     g.sh_jac = c.take<float>((size_t)9 * n);
     g.exp_rec = c.take<uint4>(n);
     g.inst_off = c.take<uint32_t>((size_t)n + 1);
+    g.tiles_sorted = c.take<uint32_t>(n);
     g.inst_start = c.take<uint32_t>((size_t)n + 1);
     g.depth_key = c.take<uint32_t>(n);
     g.block_sums = c.take<uint32_t>(div_up(n, 256) + 1);

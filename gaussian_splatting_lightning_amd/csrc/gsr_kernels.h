@@ -28,8 +28,9 @@ void launch_exclusive_scan_lookback(hipStream_t s, const uint32_t *in, const uin
 // LSD radix sort of sc.k[0] (nbits significant bits); values are the iota permutation unless `keyed`, in which
 // case sc.v[0] holds the input values.  The result lands in buffer index (passes & 1).
 // keys0 (optional): read the first pass's keys from there instead of sc.k[0] (left unmodified).
-void launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bool keyed = false,
-                       const uint32_t *keys0 = nullptr);
+// gsrc / gdst (optional): also writes gdst[i] = gsrc[sorted value i] (onesweep path); returns whether it did.
+bool launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bool keyed = false,
+                       const uint32_t *keys0 = nullptr, const uint32_t *gsrc = nullptr, uint32_t *gdst = nullptr);
 
 // ---- forward (gsr_forward.hip) ----
 struct PreprocessParams {
