@@ -480,14 +480,20 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     // takes 0.20 ms against the radix path's 0.30; at 5M / 4K stress (1240 per tile) 4.4 ms against 1.4.
     // Otherwise the radix path: depth sort, depth-ordered expansion, stable tile sort.
     const bool bucket = bk_possible && (bk == 2 || (uint64_t)R <= (uint64_t)BK_MAX_MEAN * T);
+    bool sorted_exp = false;
     if (!bucket) {
-        // the depth sort's last pass also writes the tile counts in depth order ("sort_gather" 0: the scan gathers
-        // them through the order instead)
-        bool sorted_tiles = false;
-        const bool sg = tuning("sort_gather", 1) != 0;
+        // the depth sort's last pass also writes the tile counts and expansion records in depth order ("sort_gather"
+        // bit 0 / bit 1; unset: the scan / the expansion gathers them through the order instead)
+        const int sg = tuning("sort_gather", 1);
+        SortGather ga;
+        if (sg & 1) { ga.src = g.tiles; ga.dst = g.tiles_sorted; }
+        if (sg & 2) { ga.src4 = g.exp_rec; ga.dst4 = g.exp_sorted; }
+        bool sorted_recs = false;
         GSR_STAGE(ST_DEPTH_SORT, dbg,
-                  sorted_tiles = launch_radix_sort(stream, g.sort, (uint32_t)P, 32, false, g.depth_key,
-                                                   sg ? g.tiles : nullptr, sg ? g.tiles_sorted : nullptr));
+                  sorted_recs = launch_radix_sort(stream, g.sort, (uint32_t)P, 32, false, g.depth_key,
+                                                  sg ? &ga : nullptr));
+        const bool sorted_tiles = sorted_recs && (sg & 1);
+        sorted_exp = sorted_recs && (sg & 2);
         if (tuning("scan_lookback", 1))
             GSR_STAGE(ST_SCAN, dbg,
                       launch_exclusive_scan_lookback(stream, sorted_tiles ? g.tiles_sorted : g.tiles,
@@ -531,6 +537,8 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             ExpandParams ep;
             ep.P = (uint32_t)P; ep.R = R; ep.gx = gx; ep.gy = gy;
             ep.order = g.order; ep.inst_off = g.inst_off; ep.tiles = g.tiles; ep.exp_rec = g.exp_rec;
+            ep.exp_sorted = sorted_exp ? g.exp_sorted : nullptr;
+            ep.exp_owner = tuning("exp_owner", 1) ? b.exp_owner : nullptr;
             ep.keys_out = b.sort.k[0]; ep.inst_gid = b.inst_gid; ep.inst_start = g.inst_start;
             GSR_STAGE(ST_EXPAND, dbg, launch_expand(stream, ep));
             GSR_STAGE(ST_TILE_SORT, dbg, launch_radix_sort(stream, b.sort, R, tile_key_bits(T)));

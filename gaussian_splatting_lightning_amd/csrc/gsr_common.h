@@ -111,6 +111,7 @@ struct GeomState {
                            //    all tiles of the rect (area > 64 or culling off).  One 16-B gather per Gaussian.
     uint32_t *inst_off;    // P+1: radix path: exclusive scan of tiles in depth order, [P] = total
     uint32_t *tiles_sorted;  // P: radix path: tiles in depth order (written by the depth sort's last pass)
+    uint4 *exp_sorted;       // P: radix path: exp_rec in depth order (likewise)
     uint32_t *inst_start;  // P+1: first instance (expansion order) of each Gaussian (bucket path: the
                            //      exclusive scan of tiles in Gaussian order, [P] = total)
     uint32_t *block_sums;  // div_up(P, 256): kept-tile totals of the preprocess blocks (bucket path)
@@ -136,6 +137,7 @@ inline size_t carve_geom(char *base, int P, GeomState &g) {
     g.exp_rec = c.take<uint4>(n);
     g.inst_off = c.take<uint32_t>((size_t)n + 1);
     g.tiles_sorted = c.take<uint32_t>(n);
+    g.exp_sorted = c.take<uint4>(n);
     g.inst_start = c.take<uint32_t>((size_t)n + 1);
     g.depth_key = c.take<uint32_t>(n);
     g.block_sums = c.take<uint32_t>(div_up(n, 256) + 1);
@@ -155,6 +157,7 @@ inline int tile_key_bits(uint32_t num_tiles) {
 inline int radix_passes(int bits) { return (bits + 7) / 8; }
 
 struct BinningState {
+    uint32_t *exp_owner;   // div_up(R, 256) + 2: radix path: depth rank owning each expansion block's first instance
     uint32_t *inst_gid;    // R: Gaussian of each instance (expansion order)
     uint32_t *point_list;  // R: Gaussian ids sorted by (tile, depth, id); written by the forward composite
                            //    for the instances it loads (every instance any pixel can reach)
@@ -178,6 +181,7 @@ inline size_t carve_binning(char *base, int64_t R, uint32_t num_tiles, BinningSt
     Carver cr = c;  // radix view
     int passes = radix_passes(tile_key_bits(num_tiles));
     carve_sort(cr, b.sort, n, passes >= 2);
+    b.exp_owner = cr.take<uint32_t>(div_up(n, 256u) + 2);
     // keys and values end in slot (passes & 1); the last pass writes its values straight into sorted_u
     b.keys_sorted = b.sort.k[passes & 1];
     b.sort.v[passes & 1] = b.sorted_u;

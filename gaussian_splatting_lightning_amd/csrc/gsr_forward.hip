@@ -262,14 +262,22 @@ __device__ __forceinline__ uint32_t wave_last_le(const uint32_t *__restrict__ of
 
 __global__ __launch_bounds__(256) void expand_kernel(ExpandParams p) {
     __shared__ uint32_t s_off[EXP_TILE + 2];
-    __shared__ int4 s_rect[EXP_TILE + 1];       // (gid, rmin.x, rmin.y, width)
-    __shared__ uint64_t s_mask[EXP_TILE + 1];   // kept-tile mask (0: all tiles of the rect)
+    __shared__ uint4 s_e[EXP_TILE + 1];     // expansion record: kept-tile mask lo, hi (0: all tiles), rmin, width
+    __shared__ uint32_t s_gid[EXP_TILE + 1];
     static_assert(sizeof(uint4) == 16, "expansion record");
     __shared__ uint32_t s_lo, s_n;
-    __shared__ uint2 s_out[EXP_TILE];           // (tile key, gid) staged for coalesced stores
     const uint32_t u0 = blockIdx.x * EXP_TILE;
     const uint32_t u1 = min(p.R, u0 + (uint32_t)EXP_TILE);
-    if (threadIdx.x < 64) {
+    if (p.exp_owner) {  // owners of the block starts from expand_owner_kernel: one load instead of two searches
+        if (threadIdx.x == 0) {
+            const uint32_t lo = p.exp_owner[blockIdx.x];
+            // the next block's first owner, or (last block) every remaining rank; ranks between two block starts
+            // own >= 1 instance each, so at most EXP_TILE + 1 of them
+            const uint32_t hi = blockIdx.x + 1 < gridDim.x ? p.exp_owner[blockIdx.x + 1] : p.P - 1;
+            s_lo = lo;
+            s_n = min(hi - lo + 1, (uint32_t)EXP_TILE + 1);
+        }
+    } else if (threadIdx.x < 64) {
         // owner(u) = last r with inst_off[r] <= u.  Every Gaussian that renders owns >= 1 instance and the
         // others are sorted to the end, so the owners of [u0, u1) are consecutive ranks.
         const int lane = threadIdx.x;
@@ -281,36 +289,46 @@ __global__ __launch_bounds__(256) void expand_kernel(ExpandParams p) {
         }
     }
     __syncthreads();
-    const uint32_t r_lo = s_lo, nr = s_n;  // nr <= EXP_TILE
+    const uint32_t r_lo = s_lo, nr = s_n;  // nr <= EXP_TILE + 1
     for (uint32_t k = threadIdx.x; k < nr + 1; k += 256) s_off[k] = p.inst_off[r_lo + k];
     for (uint32_t k = threadIdx.x; k < nr; k += 256) {
         const uint32_t gid = p.order[r_lo + k];
-        const uint4 e = p.exp_rec[gid];  // rect and kept-tile mask from the preprocess: one 16-B gather
-        s_rect[k] = make_int4((int)gid, (int)(e.z & 0xffffu), (int)(e.z >> 16), (int)e.w);
-        s_mask[k] = (uint64_t)e.x | ((uint64_t)e.y << 32);
+        // rect and kept-tile mask from the preprocess: in depth order already, or one 16-B gather
+        s_e[k] = p.exp_sorted ? p.exp_sorted[r_lo + k] : p.exp_rec[gid];
+        s_gid[k] = gid;
     }
     __syncthreads();
+    // each thread expands EXP_PER consecutive instances and stores them as one 16-B vector per output array
     const uint32_t ub = u0 + threadIdx.x * EXP_PER;
-    if (ub < u1) {
-        // owner of ub within the window
-        uint32_t lo = 0, hi = nr - 1;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1) >> 1;
-            if (s_off[mid] <= ub) lo = mid; else hi = mid - 1;
-        }
-        uint32_t r = lo;
-        uint32_t next = s_off[r + 1];
-        int4 rect = s_rect[r];
-        uint64_t m = s_mask[r];
-        uint32_t k = ub - s_off[r];
-        for (uint32_t j = 0; j < k && m; j++) m &= m - 1;  // skip the kept tiles of earlier threads
-        const uint32_t ue = min(u1, ub + (uint32_t)EXP_PER);
-        for (uint32_t u = ub; u < ue; u++) {
+    if (ub >= u1) return;
+    // owner of ub within the window
+    uint32_t lo = 0, hi = nr - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (s_off[mid] <= ub) lo = mid; else hi = mid - 1;
+    }
+    uint32_t r = lo;
+    uint32_t next = s_off[r + 1];
+    uint4 e = s_e[r];
+    uint32_t gid = s_gid[r];
+    uint64_t m = (uint64_t)e.x | ((uint64_t)e.y << 32);
+    uint32_t k = ub - s_off[r];
+    for (uint32_t j = 0; j < k && m; j++) m &= m - 1;  // skip the kept tiles of earlier threads
+    float rw = __builtin_amdgcn_rcpf((float)e.w);
+    uint32_t key[EXP_PER], gv[EXP_PER];
+#pragma unroll
+    for (int q = 0; q < EXP_PER; q++) {
+        const uint32_t u = ub + q;
+        key[q] = 0;
+        gv[q] = 0;
+        if (u < u1) {
             while (u >= next) {
                 r++;
                 next = s_off[r + 1];
-                rect = s_rect[r];
-                m = s_mask[r];
+                e = s_e[r];
+                gid = s_gid[r];
+                m = (uint64_t)e.x | ((uint64_t)e.y << 32);
+                rw = __builtin_amdgcn_rcpf((float)e.w);
                 k = 0;
             }
             uint32_t bit = k;
@@ -318,23 +336,44 @@ __global__ __launch_bounds__(256) void expand_kernel(ExpandParams p) {
                 bit = (uint32_t)__builtin_ctzll(m);
                 m &= m - 1;
             }
-            const uint32_t w = (uint32_t)rect.w;
-            const uint32_t ty = (uint32_t)rect.z + bit / w, tx = (uint32_t)rect.y + bit % w;
-            s_out[u - u0] = make_uint2(ty * (uint32_t)p.gx + tx, (uint32_t)rect.x);
-            if (k == 0) p.inst_start[rect.x] = u;
+            // bit / w through the reciprocal (bit < 2^24: off by at most one, corrected)
+            const uint32_t w = e.w;
+            uint32_t dy = (uint32_t)((float)bit * rw);
+            int32_t dx = (int32_t)(bit - dy * w);
+            if (dx < 0) { dy--; dx += (int32_t)w; }
+            if (dx >= (int32_t)w) { dy++; dx -= (int32_t)w; }
+            const uint32_t ty = (e.z >> 16) + dy, tx = (e.z & 0xffffu) + (uint32_t)dx;
+            key[q] = ty * (uint32_t)p.gx + tx;
+            gv[q] = gid;
+            if (k == 0) p.inst_start[gid] = u;
             k++;
         }
     }
-    __syncthreads();
-    for (uint32_t u = u0 + threadIdx.x; u < u1; u += 256) {
-        const uint2 o = s_out[u - u0];
-        p.keys_out[u] = o.x;
-        p.inst_gid[u] = o.y;
+    if (ub + EXP_PER <= u1) {
+        static_assert(EXP_PER == 4, "one uint4 store per thread");
+        *reinterpret_cast<uint4 *>(p.keys_out + ub) = make_uint4(key[0], key[1], key[2], key[3]);
+        *reinterpret_cast<uint4 *>(p.inst_gid + ub) = make_uint4(gv[0], gv[1], gv[2], gv[3]);
+    } else {
+        for (uint32_t u = ub; u < u1; u++) {
+            p.keys_out[u] = key[u - ub];
+            p.inst_gid[u] = gv[u - ub];
+        }
     }
+}
+
+// exp_owner[b] = the depth rank owning instance b * EXP_TILE (its inst_off range contains it): each rank writes
+// the block starts inside its own range, so every entry b < div_up(R, EXP_TILE) is written exactly once.
+__global__ __launch_bounds__(256) void expand_owner_kernel(const uint32_t *__restrict__ inst_off, uint32_t P,
+                                                           uint32_t *__restrict__ exp_owner) {
+    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= P) return;
+    const uint32_t a = inst_off[r], e = inst_off[r + 1];
+    for (uint32_t b = (uint32_t)(((uint64_t)a + EXP_TILE - 1) / EXP_TILE); b * (uint64_t)EXP_TILE < e; b++) exp_owner[b] = r;
 }
 
 void launch_expand(hipStream_t s, const ExpandParams &p) {
     if (p.R == 0) return;
+    if (p.exp_owner) expand_owner_kernel<<<div_up(p.P, 256u), 256, 0, s>>>(p.inst_off, p.P, p.exp_owner);
     expand_kernel<<<div_up(p.R, EXP_TILE), 256, 0, s>>>(p);
 }
 

@@ -28,9 +28,16 @@ void launch_exclusive_scan_lookback(hipStream_t s, const uint32_t *in, const uin
 // LSD radix sort of sc.k[0] (nbits significant bits); values are the iota permutation unless `keyed`, in which
 // case sc.v[0] holds the input values.  The result lands in buffer index (passes & 1).
 // keys0 (optional): read the first pass's keys from there instead of sc.k[0] (left unmodified).
-// gsrc / gdst (optional): also writes gdst[i] = gsrc[sorted value i] (onesweep path); returns whether it did.
+// gather (optional): the last pass also writes dst[i] = src[sorted value i] for each non-null pair (onesweep
+// path only); returns whether it did.
+struct SortGather {
+    const uint32_t *src = nullptr;
+    uint32_t *dst = nullptr;
+    const uint4 *src4 = nullptr;
+    uint4 *dst4 = nullptr;
+};
 bool launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bool keyed = false,
-                       const uint32_t *keys0 = nullptr, const uint32_t *gsrc = nullptr, uint32_t *gdst = nullptr);
+                       const uint32_t *keys0 = nullptr, const SortGather *gather = nullptr);
 
 // ---- forward (gsr_forward.hip) ----
 struct PreprocessParams {
@@ -55,6 +62,8 @@ struct ExpandParams {
     int gx, gy;
     const uint32_t *order, *inst_off, *tiles;
     const uint4 *exp_rec;
+    const uint4 *exp_sorted;  // optional: exp_rec already in depth order (read by rank, no gather)
+    uint32_t *exp_owner;      // optional: owner ranks of the block starts (div_up(R, EXP_TILE) + 1 words)
     uint32_t *keys_out, *inst_gid, *inst_start;
 };
 void launch_expand(hipStream_t s, const ExpandParams &p);

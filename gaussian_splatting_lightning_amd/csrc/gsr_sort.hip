@@ -425,9 +425,9 @@ __global__ __launch_bounds__(256) void rs_hist_scan_kernel(uint32_t *__restrict_
     }
 }
 
-// gsrc / gdst (final pass only, else null): gdst[sorted position] = gsrc[value], i.e. an array permuted into the
-// sorted order while the values are written (the depth sort hands the instance scan its tile counts in depth
-// order this way, instead of the scan gathering them through the order with a dependent random load each).
+// ga (final pass only, else empty): dst[sorted position] = src[value], i.e. arrays permuted into the sorted
+// order while the values are written (the depth sort hands the instance scan and the expansion their per-Gaussian
+// inputs in depth order this way, instead of each gathering them through the order with a dependent random load).
 template <bool IOTA_IN, int ITEMS, int LBW>
 __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__restrict__ keys_in,
                                                           const uint32_t *__restrict__ vals_in, uint32_t n,
@@ -435,8 +435,7 @@ __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__rest
                                                           uint32_t *__restrict__ status,
                                                           uint32_t *__restrict__ keys_out,
                                                           uint32_t *__restrict__ vals_out, uint4 *stamps,
-                                                          const uint32_t *__restrict__ gsrc,
-                                                          uint32_t *__restrict__ gdst) {
+                                                          SortGather ga) {
     __shared__ uint32_t s_cnt[4][RS_BINS];  // per-wave running digit counts, then per-wave bases
     __shared__ uint32_t s_dstart[RS_BINS];  // block-local start of each digit's run
     __shared__ uint32_t s_gbase[RS_BINS];   // global start of this block's run of each digit
@@ -563,8 +562,9 @@ __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__rest
     }
     __syncthreads();
     const uint32_t cnt_blk = min(TILE, n - blk);
-    if (gsrc) {  // the gathers of a thread's elements are issued together, then stored
+    if (ga.dst || ga.dst4) {  // the gathers of a thread's elements are issued together, then stored
         uint32_t g[ITEMS], gp[ITEMS];
+        uint4 g4[ITEMS];
 #pragma unroll
         for (int it = 0; it < ITEMS; it++) {
             const uint32_t i = tid + it * 256;
@@ -575,12 +575,16 @@ __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__rest
                 gp[it] = s_gbase[d] + (i - s_dstart[d]);
                 keys_out[gp[it]] = k;
                 vals_out[gp[it]] = v;
-                g[it] = gsrc[v];
+                if (ga.dst) g[it] = ga.src[v];
+                if (ga.dst4) g4[it] = ga.src4[v];
             }
         }
 #pragma unroll
         for (int it = 0; it < ITEMS; it++)
-            if (gp[it] != 0xffffffffu) gdst[gp[it]] = g[it];
+            if (gp[it] != 0xffffffffu) {
+                if (ga.dst) ga.dst[gp[it]] = g[it];
+                if (ga.dst4) ga.dst4[gp[it]] = g4[it];
+            }
     } else {
         for (uint32_t i = tid; i < cnt_blk; i += 256) {
             const uint32_t k = s_keys[i], v = s_vals[i];
@@ -595,7 +599,7 @@ __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__rest
 
 template <int ITEMS, int LBW>
 static void launch_radix_sort_onesweep(hipStream_t s, SortScratch &sc, uint32_t n, int passes, bool keyed,
-                                       const uint32_t *keys0, const uint32_t *gsrc, uint32_t *gdst) {
+                                       const uint32_t *keys0, const SortGather *gather) {
     const uint32_t nb = div_up(n, (uint32_t)ITEMS * 256u);
     (void)hipMemsetAsync(sc.ctrl, 0, sizeof(uint32_t) * (RS_CTRL_WORDS + (size_t)passes * nb * RS_BINS), s);
     const uint32_t hb = min(div_up(n, 256u * 8u), 2048u);
@@ -607,21 +611,20 @@ static void launch_radix_sort_onesweep(hipStream_t s, SortScratch &sc, uint32_t 
         const int in = p & 1, out = (p + 1) & 1;
         uint32_t *st = sc.status + (size_t)p * nb * RS_BINS;
         const uint32_t *kin = p == 0 ? keys0 : sc.k[in];
-        const bool last = p == passes - 1;
+        SortGather ga;
+        if (p == passes - 1 && gather) ga = *gather;
         if (p == 0 && !keyed)
             rs_onesweep_kernel<true, ITEMS, LBW><<<nb, 256, 0, s>>>(kin, nullptr, n, p, sc.ctrl, st, sc.k[out],
-                                                               sc.v[out], stamps, last ? gsrc : nullptr,
-                                                               last ? gdst : nullptr);
+                                                               sc.v[out], stamps, ga);
         else
             rs_onesweep_kernel<false, ITEMS, LBW><<<nb, 256, 0, s>>>(kin, sc.v[in], n, p, sc.ctrl, st, sc.k[out],
-                                                                sc.v[out], stamps, last ? gsrc : nullptr,
-                                                                last ? gdst : nullptr);
+                                                                sc.v[out], stamps, ga);
     }
 }
 
 bool launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bool keyed, const uint32_t *keys0,
-                       const uint32_t *gsrc, uint32_t *gdst) {
-    if (n == 0) return gsrc != nullptr;
+                       const SortGather *gather) {
+    if (n == 0) return gather != nullptr;
     if (!keys0) keys0 = sc.k[0];
     const uint32_t nb = div_up(n, RS_TILE);
     const int passes = radix_passes(nbits);
@@ -629,9 +632,9 @@ bool launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bo
     const int os = tuning("onesweep", 1);
     if (n <= RS_ONESWEEP_MAX_N && passes <= RS_MAX_PASSES && (os & (nbits == 32 ? 1 : 2))) {
         // 8-/32-key tiles measured slower
-        if (tuning("lbw", 16) >= 16) launch_radix_sort_onesweep<RS_ITEMS, 16>(s, sc, n, passes, keyed, keys0, gsrc, gdst);
-        else launch_radix_sort_onesweep<RS_ITEMS, 1>(s, sc, n, passes, keyed, keys0, gsrc, gdst);
-        return gsrc != nullptr;
+        if (tuning("lbw", 16) >= 16) launch_radix_sort_onesweep<RS_ITEMS, 16>(s, sc, n, passes, keyed, keys0, gather);
+        else launch_radix_sort_onesweep<RS_ITEMS, 1>(s, sc, n, passes, keyed, keys0, gather);
+        return gather != nullptr;
     }
     for (int p = 0; p < passes; p++) {
         const int shift = 8 * p, in = p & 1, out = (p + 1) & 1;
