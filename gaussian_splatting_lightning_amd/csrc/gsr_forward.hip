@@ -380,26 +380,40 @@ void launch_expand(hipStream_t s, const ExpandParams &p) {
 // ------------------------------------------------------------------------------------------------
 // ranges: [start, end) of every tile's run in the sorted instance list
 // ------------------------------------------------------------------------------------------------
+// Tile boundaries of the sorted keys: 8 consecutive keys per thread (two 16-B loads) and the key before them.
+constexpr uint32_t IR_PER = 8;
 __global__ __launch_bounds__(256) void identify_ranges_kernel(const uint32_t *__restrict__ keys, uint32_t R,
                                                               uint2 *__restrict__ ranges) {
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= R) return;
-    const uint32_t cur = keys[i];
-    if (i == 0) {
-        ranges[cur].x = 0;
+    const uint32_t base = (blockIdx.x * 256 + threadIdx.x) * IR_PER;
+    if (base >= R) return;
+    uint32_t k[IR_PER];
+    if (base + IR_PER <= R) {
+        const uint4 *k4 = reinterpret_cast<const uint4 *>(keys + base);
+        const uint4 a = k4[0], b = k4[1];
+        k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w; k[4] = b.x; k[5] = b.y; k[6] = b.z; k[7] = b.w;
     } else {
-        const uint32_t prev = keys[i - 1];
-        if (cur != prev) {
-            ranges[prev].y = i;
-            ranges[cur].x = i;
+#pragma unroll
+        for (uint32_t q = 0; q < IR_PER; q++) k[q] = base + q < R ? keys[base + q] : 0u;
+    }
+    uint32_t prev = base ? keys[base - 1] : 0u;
+    if (base == 0) ranges[k[0]].x = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < IR_PER; q++) {
+        const uint32_t i = base + q;
+        if (i < R) {
+            if (i > 0 && k[q] != prev) {
+                ranges[prev].y = i;
+                ranges[k[q]].x = i;
+            }
+            if (i == R - 1) ranges[k[q]].y = R;
+            prev = k[q];
         }
     }
-    if (i == R - 1) ranges[cur].y = R;
 }
 
 void launch_identify_ranges(hipStream_t s, const uint32_t *keys_sorted, uint32_t R, uint2 *ranges) {
     if (R == 0) return;
-    identify_ranges_kernel<<<div_up(R, 256), 256, 0, s>>>(keys_sorted, R, ranges);
+    identify_ranges_kernel<<<div_up(R, 256 * IR_PER), 256, 0, s>>>(keys_sorted, R, ranges);
 }
 
 // LPT (longest first) launch order for the composite kernels: tile costs vary ~2x around the image centre,

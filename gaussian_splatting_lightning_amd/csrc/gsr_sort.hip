@@ -632,7 +632,10 @@ bool launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bo
     const int os = tuning("onesweep", 1);
     if (n <= RS_ONESWEEP_MAX_N && passes <= RS_MAX_PASSES && (os & (nbits == 32 ? 1 : 2))) {
         // 8-/32-key tiles measured slower
-        if (tuning("lbw", 16) >= 16) launch_radix_sort_onesweep<RS_ITEMS, 16>(s, sc, n, passes, keyed, keys0, gather);
+        const int lbw = tuning("lbw", 16);
+        if (lbw >= 64) launch_radix_sort_onesweep<RS_ITEMS, 64>(s, sc, n, passes, keyed, keys0, gather);
+        else if (lbw >= 32) launch_radix_sort_onesweep<RS_ITEMS, 32>(s, sc, n, passes, keyed, keys0, gather);
+        else if (lbw >= 16) launch_radix_sort_onesweep<RS_ITEMS, 16>(s, sc, n, passes, keyed, keys0, gather);
         else launch_radix_sort_onesweep<RS_ITEMS, 1>(s, sc, n, passes, keyed, keys0, gather);
         return gather != nullptr;
     }

@@ -14,6 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg3")
+    ap.add_argument("--knob", action="append", default=[], help="name=value tuning knob set before the runs")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -27,13 +28,18 @@ def main():
     cam = make_camera(cfg["W"], cfg["H"]).to(dev)
     rs = GaussianRasterizationSettings(cfg["H"], cfg["W"], cam.tanfovx, cam.tanfovy, torch.zeros(3, device=dev), 1.0,
                                        cam.viewmatrix, cam.projmatrix, cfg["deg"], cam.campos, False, False, False)
+    for kv in args.knob:
+        k, v = kv.split("=")
+        _native.set_tuning(k, int(v))
     for _ in range(2):
         forward_raw(sc.means3D, sc.shs, None, sc.opacities, sc.scales, sc.rotations, None, rs)
     _native.set_tuning("stamp", 1)
-    forward_raw(sc.means3D, sc.shs, None, sc.opacities, sc.scales, sc.rotations, None, rs)
+    st_ = forward_raw(sc.means3D, sc.shs, None, sc.opacities, sc.scales, sc.rotations, None, rs)[3]
     torch.cuda.synchronize()
     _native.set_tuning("stamp", 0)
     n = cfg["n"]
+    if cfg["W"] * cfg["H"] > 16384 * 256:  # radix path: the tile sort ran last
+        n = st_.num_rendered
     nb = (n + 4095) // 4096
     hb = min((n + 2047) // 2048, 2048)
     out = {}
@@ -51,6 +57,7 @@ def main():
         else:
             out[name] = {"blocks": cnt, "start_us": q(rel[:, 0]), "loop_us": q(rel[:, 1] - rel[:, 0]),
                          "global_atomics_us": q(rel[:, 2] - rel[:, 1]), "end_us": q(rel[:, 2])}
+    out["n"] = n
     print(json.dumps(out, indent=1))
 
 
