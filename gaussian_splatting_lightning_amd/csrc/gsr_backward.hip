@@ -1147,9 +1147,34 @@ __global__ __launch_bounds__(256) void big_reduce_kernel(BigReduceParams p) {
     const uint32_t gidx = p.big_list[bi];
     const uint32_t start = p.inst_start[gidx], cnt = p.tiles[gidx];
     float acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (uint32_t k = threadIdx.x; k < cnt; k += 256) {
-        const uint32_t sidx = p.inv[start + k];
-        if (sidx != INV_NONE) add_row(p.rows, p.rows_by_u ? start + k : sidx, acc);
+    if (p.rows_by_u) {
+        // rows by expansion index: BR_UNROLL inv words per thread are loaded together, then the rows of the
+        // loaded instances (most instances of a big Gaussian sit in saturated tiles and have none), summed in the
+        // same k order as one at a time
+        constexpr int BR_UNROLL = 4;
+        for (uint32_t k0 = threadIdx.x; k0 < cnt; k0 += 256 * BR_UNROLL) {
+            float r[BR_UNROLL][10];
+            bool use[BR_UNROLL];
+#pragma unroll
+            for (int q = 0; q < BR_UNROLL; q++) {
+                const uint32_t k = k0 + 256 * q;
+                use[q] = k < cnt && p.inv[start + k] != INV_NONE;
+            }
+#pragma unroll
+            for (int q = 0; q < BR_UNROLL; q++)
+                if (use[q]) load_row(p.rows, start + k0 + 256 * q, r[q]);
+#pragma unroll
+            for (int q = 0; q < BR_UNROLL; q++)
+                if (use[q]) {
+#pragma unroll
+                    for (int v = 0; v < 10; v++) acc[v] += r[q][v];
+                }
+        }
+    } else {
+        for (uint32_t k = threadIdx.x; k < cnt; k += 256) {
+            const uint32_t sidx = p.inv[start + k];
+            if (sidx != INV_NONE) add_row(p.rows, sidx, acc);
+        }
     }
 #pragma unroll
     for (int v = 0; v < 10; v++) {
