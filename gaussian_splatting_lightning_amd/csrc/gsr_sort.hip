@@ -222,17 +222,18 @@ void launch_exclusive_scan_lookback(hipStream_t s, const uint32_t *in, const uin
 // ------------------------------------------------------------------------------------------------
 // radix sort pass: histogram
 // ------------------------------------------------------------------------------------------------
+template <int TILE>
 __global__ __launch_bounds__(256) void rs_hist_kernel(const uint32_t *__restrict__ keys, uint32_t n, int shift,
                                                       uint32_t *__restrict__ counts, uint32_t nb) {
     __shared__ uint32_t h[4][RS_BINS];
     const int tid = threadIdx.x, w = tid >> 6;
     for (int i = tid; i < 4 * RS_BINS; i += 256) (&h[0][0])[i] = 0;
     __syncthreads();
-    const uint32_t base = blockIdx.x * RS_TILE;
-    if (base + RS_TILE <= n) {
+    const uint32_t base = blockIdx.x * TILE;
+    if (base + TILE <= n) {
         const uint4 *k4 = reinterpret_cast<const uint4 *>(keys + base);
 #pragma unroll
-        for (int i = 0; i < RS_TILE / 4 / 256; i++) {
+        for (int i = 0; i < TILE / 4 / 256; i++) {
             const uint4 q = k4[i * 256 + tid];
             atomicAdd(&h[w][(q.x >> shift) & 255u], 1u);
             atomicAdd(&h[w][(q.y >> shift) & 255u], 1u);
@@ -240,7 +241,7 @@ __global__ __launch_bounds__(256) void rs_hist_kernel(const uint32_t *__restrict
             atomicAdd(&h[w][(q.w >> shift) & 255u], 1u);
         }
     } else {
-        for (int i = tid; i < RS_TILE; i += 256) {
+        for (int i = tid; i < TILE; i += 256) {
             const uint32_t j = base + i;
             if (j < n) atomicAdd(&h[w][(keys[j] >> shift) & 255u], 1u);
         }
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(256) void rs_hist_kernel(const uint32_t *__restrict
 // ------------------------------------------------------------------------------------------------
 // radix sort pass: stable scatter
 // ------------------------------------------------------------------------------------------------
-template <bool IOTA_IN>
+template <bool IOTA_IN, int ITEMS>
 __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restrict__ keys_in,
                                                          const uint32_t *__restrict__ vals_in, uint32_t n,
                                                          int shift, const uint32_t *__restrict__ counts_scanned,
@@ -262,27 +263,27 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restr
     __shared__ uint32_t s_dstart[RS_BINS];  // block-local start of each digit's run
     __shared__ uint32_t s_gbase[RS_BINS];   // global start of this block's run of each digit
     __shared__ uint32_t s_wsum[4];
-    __shared__ uint32_t s_keys[RS_TILE];
-    __shared__ uint32_t s_vals[RS_TILE];
+    __shared__ uint32_t s_keys[ITEMS * 256];
+    __shared__ uint32_t s_vals[ITEMS * 256];
 
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const uint32_t blk = blockIdx.x * RS_TILE;
+    const uint32_t blk = blockIdx.x * (ITEMS * 256);
     for (int i = tid; i < 4 * RS_BINS; i += 256) (&s_cnt[0][0])[i] = 0;
     __syncthreads();
 
-    // Each wave ranks a contiguous segment of 1024 keys, 64 at a time, in input order (stable).
-    uint32_t key[RS_ITEMS], val[RS_ITEMS], rank[RS_ITEMS];
+    // Each wave ranks a contiguous segment of 64 * ITEMS keys, 64 at a time, in input order (stable).
+    uint32_t key[ITEMS], val[ITEMS], rank[ITEMS];
     const uint64_t lt = lanemask_lt(lane);
 #pragma unroll
-    for (int it = 0; it < RS_ITEMS; it++) {  // loads first (see rs_onesweep_kernel)
-        const uint32_t j = blk + w * (RS_TILE / 4) + it * 64 + lane;
+    for (int it = 0; it < ITEMS; it++) {  // loads first (see rs_onesweep_kernel)
+        const uint32_t j = blk + w * ((ITEMS * 256) / 4) + it * 64 + lane;
         const bool valid = j < n;
         key[it] = valid ? keys_in[j] : 0u;
         val[it] = IOTA_IN ? j : (valid ? vals_in[j] : 0u);
     }
 #pragma unroll
-    for (int it = 0; it < RS_ITEMS; it++) {
-        const uint32_t j = blk + w * (RS_TILE / 4) + it * 64 + lane;
+    for (int it = 0; it < ITEMS; it++) {
+        const uint32_t j = blk + w * ((ITEMS * 256) / 4) + it * 64 + lane;
         const bool valid = j < n;
         const uint32_t k = key[it];
         const uint32_t d = (k >> shift) & 255u;
@@ -321,8 +322,8 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restr
     }
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < RS_ITEMS; it++) {
-        const uint32_t j = blk + w * (RS_TILE / 4) + it * 64 + lane;
+    for (int it = 0; it < ITEMS; it++) {
+        const uint32_t j = blk + w * ((ITEMS * 256) / 4) + it * 64 + lane;
         if (j < n) {
             const uint32_t d = (key[it] >> shift) & 255u;
             const uint32_t pos = s_dstart[d] + s_cnt[w][d] + rank[it];
@@ -331,7 +332,7 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restr
         }
     }
     __syncthreads();
-    const uint32_t cnt_blk = min((uint32_t)RS_TILE, n - blk);
+    const uint32_t cnt_blk = min((uint32_t)(ITEMS * 256), n - blk);
     for (uint32_t i = tid; i < cnt_blk; i += 256) {
         const uint32_t k = s_keys[i], v = s_vals[i];
         const uint32_t d = (k >> shift) & 255u;
@@ -622,11 +623,29 @@ static void launch_radix_sort_onesweep(hipStream_t s, SortScratch &sc, uint32_t 
     }
 }
 
+// multi-kernel path: per pass a block histogram, a scan of the (digit x block) counts, a stable scatter
+template <int ITEMS>
+static void launch_radix_sort_multi(hipStream_t s, SortScratch &sc, uint32_t n, int passes, bool keyed,
+                                    const uint32_t *keys0) {
+    const uint32_t nb = div_up(n, (uint32_t)ITEMS * 256u);  // <= the RS_TILE block count carve_sort sized
+    for (int p = 0; p < passes; p++) {
+        const int shift = 8 * p, in = p & 1, out = (p + 1) & 1;
+        const uint32_t *kin = p == 0 ? keys0 : sc.k[in];
+        rs_hist_kernel<ITEMS * 256><<<nb, 256, 0, s>>>(kin, n, shift, sc.counts, nb);
+        launch_exclusive_scan(s, sc.counts, nullptr, RS_BINS * nb, sc.counts, sc.scan_tmp, nullptr);
+        if (p == 0 && !keyed)
+            rs_scatter_kernel<true, ITEMS><<<nb, 256, 0, s>>>(kin, nullptr, n, shift, sc.counts, nb, sc.k[out],
+                                                              sc.v[out]);
+        else
+            rs_scatter_kernel<false, ITEMS><<<nb, 256, 0, s>>>(kin, sc.v[in], n, shift, sc.counts, nb, sc.k[out],
+                                                               sc.v[out]);
+    }
+}
+
 bool launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bool keyed, const uint32_t *keys0,
                        const SortGather *gather) {
     if (n == 0) return gather != nullptr;
     if (!keys0) keys0 = sc.k[0];
-    const uint32_t nb = div_up(n, RS_TILE);
     const int passes = radix_passes(nbits);
     // onesweep knob: bit 0 = depth-size sorts (nbits == 32), bit 1 = tile sorts
     const int os = tuning("onesweep", 1);
@@ -639,17 +658,9 @@ bool launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bo
         else launch_radix_sort_onesweep<RS_ITEMS, 1>(s, sc, n, passes, keyed, keys0, gather);
         return gather != nullptr;
     }
-    for (int p = 0; p < passes; p++) {
-        const int shift = 8 * p, in = p & 1, out = (p + 1) & 1;
-        const uint32_t *kin = p == 0 ? keys0 : sc.k[in];
-        rs_hist_kernel<<<nb, 256, 0, s>>>(kin, n, shift, sc.counts, nb);
-        launch_exclusive_scan(s, sc.counts, nullptr, RS_BINS * nb, sc.counts, sc.scan_tmp, nullptr);
-        if (p == 0 && !keyed)
-            rs_scatter_kernel<true><<<nb, 256, 0, s>>>(kin, nullptr, n, shift, sc.counts, nb, sc.k[out], sc.v[out]);
-        else
-            rs_scatter_kernel<false><<<nb, 256, 0, s>>>(kin, sc.v[in], n, shift, sc.counts, nb, sc.k[out],
-                                                        sc.v[out]);
-    }
+    // "rs_items": keys per thread of the multi-kernel path (16 or 32; fewer blocks, longer digit runs per block)
+    if (tuning("rs_items", 32) >= 32) launch_radix_sort_multi<32>(s, sc, n, passes, keyed, keys0);
+    else launch_radix_sort_multi<RS_ITEMS>(s, sc, n, passes, keyed, keys0);
     return false;  // no permuted gather on this path
 }
 
