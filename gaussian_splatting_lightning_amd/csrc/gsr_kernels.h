@@ -28,8 +28,8 @@ void launch_exclusive_scan_lookback(hipStream_t s, const uint32_t *in, const uin
 // LSD radix sort of sc.k[0] (nbits significant bits); values are the iota permutation unless `keyed`, in which
 // case sc.v[0] holds the input values.  The result lands in buffer index (passes & 1).
 // keys0 (optional): read the first pass's keys from there instead of sc.k[0] (left unmodified).
-// gather (optional): the last pass also writes dst[i] = src[sorted value i] for each non-null pair (onesweep
-// path only); returns whether it did.
+// gather (optional): the last pass also writes dst[i] = src[sorted value i] for each non-null pair; returns
+// whether it did (always, with a gather).
 struct SortGather {
     const uint32_t *src = nullptr;
     uint32_t *dst = nullptr;

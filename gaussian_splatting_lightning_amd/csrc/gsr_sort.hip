@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restr
                                                          const uint32_t *__restrict__ vals_in, uint32_t n,
                                                          int shift, const uint32_t *__restrict__ counts_scanned,
                                                          uint32_t nb, uint32_t *__restrict__ keys_out,
-                                                         uint32_t *__restrict__ vals_out) {
+                                                         uint32_t *__restrict__ vals_out, SortGather ga) {
     __shared__ uint32_t s_cnt[4][RS_BINS];  // per-wave running digit counts, then per-wave bases
     __shared__ uint32_t s_dstart[RS_BINS];  // block-local start of each digit's run
     __shared__ uint32_t s_gbase[RS_BINS];   // global start of this block's run of each digit
@@ -333,6 +333,33 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restr
     }
     __syncthreads();
     const uint32_t cnt_blk = min((uint32_t)(ITEMS * 256), n - blk);
+    if (ga.dst || ga.dst4) {  // final pass with a permuted gather (see rs_onesweep_kernel)
+        for (uint32_t i0 = 0; i0 < cnt_blk; i0 += 256 * 8) {
+            uint32_t g[8], gp[8];
+            uint4 g4[8];
+#pragma unroll
+            for (int it = 0; it < 8; it++) {
+                const uint32_t i = i0 + tid + it * 256;
+                gp[it] = 0xffffffffu;
+                if (i < cnt_blk) {
+                    const uint32_t k = s_keys[i], v = s_vals[i];
+                    const uint32_t d = (k >> shift) & 255u;
+                    gp[it] = s_gbase[d] + (i - s_dstart[d]);
+                    keys_out[gp[it]] = k;
+                    vals_out[gp[it]] = v;
+                    if (ga.dst) g[it] = ga.src[v];
+                    if (ga.dst4) g4[it] = ga.src4[v];
+                }
+            }
+#pragma unroll
+            for (int it = 0; it < 8; it++)
+                if (gp[it] != 0xffffffffu) {
+                    if (ga.dst) ga.dst[gp[it]] = g[it];
+                    if (ga.dst4) ga.dst4[gp[it]] = g4[it];
+                }
+        }
+        return;
+    }
     for (uint32_t i = tid; i < cnt_blk; i += 256) {
         const uint32_t k = s_keys[i], v = s_vals[i];
         const uint32_t d = (k >> shift) & 255u;
@@ -626,19 +653,21 @@ static void launch_radix_sort_onesweep(hipStream_t s, SortScratch &sc, uint32_t 
 // multi-kernel path: per pass a block histogram, a scan of the (digit x block) counts, a stable scatter
 template <int ITEMS>
 static void launch_radix_sort_multi(hipStream_t s, SortScratch &sc, uint32_t n, int passes, bool keyed,
-                                    const uint32_t *keys0) {
+                                    const uint32_t *keys0, const SortGather *gather) {
     const uint32_t nb = div_up(n, (uint32_t)ITEMS * 256u);  // <= the RS_TILE block count carve_sort sized
     for (int p = 0; p < passes; p++) {
         const int shift = 8 * p, in = p & 1, out = (p + 1) & 1;
         const uint32_t *kin = p == 0 ? keys0 : sc.k[in];
         rs_hist_kernel<ITEMS * 256><<<nb, 256, 0, s>>>(kin, n, shift, sc.counts, nb);
         launch_exclusive_scan(s, sc.counts, nullptr, RS_BINS * nb, sc.counts, sc.scan_tmp, nullptr);
+        SortGather ga;
+        if (p == passes - 1 && gather) ga = *gather;
         if (p == 0 && !keyed)
             rs_scatter_kernel<true, ITEMS><<<nb, 256, 0, s>>>(kin, nullptr, n, shift, sc.counts, nb, sc.k[out],
-                                                              sc.v[out]);
+                                                              sc.v[out], ga);
         else
             rs_scatter_kernel<false, ITEMS><<<nb, 256, 0, s>>>(kin, sc.v[in], n, shift, sc.counts, nb, sc.k[out],
-                                                               sc.v[out]);
+                                                               sc.v[out], ga);
     }
 }
 
@@ -649,7 +678,10 @@ bool launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bo
     const int passes = radix_passes(nbits);
     // onesweep knob: bit 0 = depth-size sorts (nbits == 32), bit 1 = tile sorts
     const int os = tuning("onesweep", 1);
-    if (n <= RS_ONESWEEP_MAX_N && passes <= RS_MAX_PASSES && (os & (nbits == 32 ? 1 : 2))) {
+    // measured (depth sorts, with the permuted gather): onesweep 0.121 / 0.378 ms at 1 M / 5 M keys against
+    // 0.183 / 0.329 for the multi-kernel path (32 keys per thread); linear fits cross near 3.2 M keys
+    const uint32_t os_max = (uint32_t)tuning("onesweep_max_n", 3 << 20);
+    if (n <= RS_ONESWEEP_MAX_N && n <= os_max && passes <= RS_MAX_PASSES && (os & (nbits == 32 ? 1 : 2))) {
         // 8-/32-key tiles measured slower
         const int lbw = tuning("lbw", 16);
         if (lbw >= 64) launch_radix_sort_onesweep<RS_ITEMS, 64>(s, sc, n, passes, keyed, keys0, gather);
@@ -659,9 +691,9 @@ bool launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bo
         return gather != nullptr;
     }
     // "rs_items": keys per thread of the multi-kernel path (16 or 32; fewer blocks, longer digit runs per block)
-    if (tuning("rs_items", 32) >= 32) launch_radix_sort_multi<32>(s, sc, n, passes, keyed, keys0);
-    else launch_radix_sort_multi<RS_ITEMS>(s, sc, n, passes, keyed, keys0);
-    return false;  // no permuted gather on this path
+    if (tuning("rs_items", 32) >= 32) launch_radix_sort_multi<32>(s, sc, n, passes, keyed, keys0, gather);
+    else launch_radix_sort_multi<RS_ITEMS>(s, sc, n, passes, keyed, keys0, gather);
+    return gather != nullptr;
 }
 
 }  // namespace gsr

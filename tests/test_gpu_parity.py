@@ -462,10 +462,11 @@ def test_dense_tiles_fall_back_to_radix_after_speculative_count(gpu_device):
         assert np.array_equal(hip["grads"][k], forced["grads"][k]), k
 
 
-@pytest.mark.parametrize("W,H", [(1280, 720), (96, 64)])
-def test_binning_paths_are_bitwise_identical(gpu_device, W, H):
+@pytest.mark.parametrize("W,H,onesweep", [(1280, 720, 1), (96, 64, 1), (1280, 720, 0), (1280, 720, 3)])
+def test_binning_paths_are_bitwise_identical(gpu_device, W, H, onesweep):
     """The bucket binning (per-tile sorts) and the radix binning (depth sort + stable tile sort) produce the
-    same instance order, so every output and gradient is bit for bit the same."""
+    same instance order, so every output and gradient is bit for bit the same -- with either radix-sort
+    implementation (onesweep 0: the multi-kernel passes for every sort, 3: onesweep for every sort)."""
     from gaussian_splatting_lightning_amd import _native
     inp = scene_inputs(200_000 if W > 100 else 60_000, W, H, sh_degree=3, seed=6, stress_fraction=0.01)
     dc, di = upstream(W, H, 6)
@@ -473,9 +474,11 @@ def test_binning_paths_are_bitwise_identical(gpu_device, W, H):
         _native.set_tuning("bucket", 2)
         ref = run_hip(inp, gpu_device, dc, di)
         _native.set_tuning("bucket", 0)
+        _native.set_tuning("onesweep", onesweep)
         alt = run_hip(inp, gpu_device, dc, di)
     finally:
         _native.set_tuning("bucket", 1)
+        _native.set_tuning("onesweep", 1)
     a, b = hip_state_arrays(ref), hip_state_arrays(alt)
     for k in ("point_list", "ranges", "tiles", "n_contrib", "tile_last", "tile_loaded"):
         assert np.array_equal(a[k], b[k]), k
