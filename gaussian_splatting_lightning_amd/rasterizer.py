@@ -58,21 +58,38 @@ def _prep(t: Optional[torch.Tensor], device, name: str) -> Optional[torch.Tensor
 
 
 class _Buffers:
-    """Caller-owned scratch buffers grown through the C callback (reference: resizeFunctional)."""
+    """Caller-owned scratch buffers grown through the C callback (reference: resizeFunctional).
+
+    The callback is a closure over the buffer dict, not a bound method: a bound method would make a reference
+    cycle (object -> callback -> method -> object), so the buffers (GBs at 5M Gaussians / 4K) would outlive the
+    call until the cyclic garbage collector ran -- never, while it is disabled (bench.py's timed region),
+    which ran the device out of memory.  An exception inside the callback (e.g. torch.OutOfMemoryError) is
+    kept and re-raised after the library call; the callback then returns NULL, which the library reports as
+    GSR_ERR_ALLOC (a ctypes callback that raises would hand the library an undefined pointer)."""
 
     def __init__(self, device):
         self.device = device
-        self.bufs = {}
-        self._cb = _native.ALLOC_FN(self._alloc)
+        self.bufs = bufs = {}
+        self.errors = errors = []
 
-    def _alloc(self, _ctx, which, nbytes):
-        t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=self.device)
-        self.bufs[int(which)] = t
-        return t.data_ptr()
+        def alloc(_ctx, which, nbytes):
+            try:
+                t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+            except BaseException as e:  # noqa: BLE001 -- re-raised by raise_pending()
+                errors.append(e)
+                return None
+            bufs[int(which)] = t
+            return t.data_ptr()
+
+        self._cb = _native.ALLOC_FN(alloc)
 
     @property
     def callback(self):
         return self._cb
+
+    def raise_pending(self):
+        if self.errors:
+            raise self.errors[0]
 
     def get(self, which) -> torch.Tensor:
         t = self.bufs.get(which)
@@ -146,6 +163,7 @@ def forward_raw(means3D, sh, colors_precomp, opacities, scales, rotations, cov3D
     with torch.cuda.device(device):  # the library also switches to its stream's device (gsr_api.hip)
         rc = lib.gsr_forward(ctypes.byref(a), bufs.callback, None, _stream_handle(device),
                              ctypes.byref(num_rendered))
+    bufs.raise_pending()
     _native.check(rc, "rasterize_gaussians")
     state = ForwardState(means3D_c, sh_c, col_c, op_c, sc_c, rot_c, cov_c, radii, bg, view, proj, campos,
                          bufs.get(_native.GSR_BUF_GEOM), bufs.get(_native.GSR_BUF_BINNING),
@@ -218,6 +236,7 @@ def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_
         densify_stats=_ptr(dstats), densify_accumulate=int(bool(accumulate_stats)), max_radii2D=_ptr(mrad))
     with torch.cuda.device(device):
         rc = lib.gsr_backward(ctypes.byref(a), bufs.callback, None, _stream_handle(device))
+    bufs.raise_pending()
     _native.check(rc, "rasterize_gaussians_backward")
     return dict(
         means3D=dmeans3D, means2D=dmeans2D,
