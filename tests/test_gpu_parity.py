@@ -531,3 +531,37 @@ def test_render_on_non_current_device():
         assert np.array_equal(a[k], b[k]) and np.array_equal(a[k], c[k]), k
     for k in GRADS:
         assert np.array_equal(a["grads"][k], b["grads"][k]), k
+
+
+@pytest.mark.parametrize("fail_buf", ["GSR_BUF_GEOM", "GSR_BUF_BINNING", "GSR_BUF_BWD_SCRATCH"])
+def test_failed_scratch_allocation_is_a_clean_error(gpu_device, fail_buf, monkeypatch):
+    """An out-of-memory inside the caller's allocator (here injected for one buffer) surfaces as that exception
+    from forward_raw / backward_raw, with nothing launched on a NULL buffer: the next call renders normally."""
+    from gaussian_splatting_lightning_amd import _native, rasterizer
+    which = getattr(_native, fail_buf)
+    inp = scene_inputs(2000, 96, 64, sh_degree=1, seed=41)
+    dc, di = upstream(96, 64, 41)
+    ref = run_hip(inp, gpu_device, dc, di)
+
+    class Failing(rasterizer._Buffers):
+        def __init__(self, device):
+            super().__init__(device)
+            inner = self._cb
+
+            def alloc(ctx, w, nbytes):
+                if w == which:
+                    self.errors.append(torch.OutOfMemoryError("injected"))
+                    return None
+                return inner(ctx, w, nbytes)
+
+            self._keep = inner
+            self._cb = _native.ALLOC_FN(alloc)
+
+    monkeypatch.setattr(rasterizer, "_Buffers", Failing)
+    with pytest.raises(torch.OutOfMemoryError):
+        run_hip(inp, gpu_device, dc, di)
+    monkeypatch.undo()
+    again = run_hip(inp, gpu_device, dc, di)
+    assert np.array_equal(ref["color"], again["color"])
+    for k in GRADS:
+        assert np.array_equal(ref["grads"][k], again["grads"][k]), k
