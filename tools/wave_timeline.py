@@ -58,6 +58,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg3")
     ap.add_argument("--knob", action="append", default=[])
+    ap.add_argument("--dump", default="", help="also save the raw stamps, launch orders, ranges and tile_last (.npz)")
     args = ap.parse_args()
     import torch
     from bench import CONFIGS
@@ -86,8 +87,22 @@ def main():
     # launch slots: whole tiles (render_fwd_v6 <4, 6>) unless the image is small enough for 4 row-strip parts
     # (launch_render_fwd's fwd_part_slots rule)
     nfwd = T * 4 if T * 4 <= 16384 else T
-    out = {"fwd": summarise(_native.wave_stamps(0, nfwd), nfwd), "bwd": summarise(_native.wave_stamps(1, T), T)}
+    sf, sb = _native.wave_stamps(0, nfwd), _native.wave_stamps(1, T)
+    out = {"fwd": summarise(sf, nfwd), "bwd": summarise(sb, T)}
     print(json.dumps(out, indent=1))
+    if args.dump:
+        import numpy as np
+        lay = _native.state_layout(cfg["n"], st.num_rendered, cfg["W"], cfg["H"])
+        img = st.image_buffer.view(torch.uint8)
+        al = lambda o: (o + 255) // 256 * 256  # noqa: E731  (Carver alignment)
+
+        def u32(off, n):
+            return img[off: off + 4 * n].view(torch.int32).cpu().numpy().view(np.uint32)
+        o_fwd = al(lay["img_tile_loaded"] + 4 * (T + 1))
+        o_bwd = al(o_fwd + 4 * (T + 1))
+        np.savez(args.dump, fwd=np.asarray(sf)[:nfwd], bwd=np.asarray(sb)[:T], order_fwd=u32(o_fwd, T),
+                 order_bwd=u32(o_bwd, T), ranges=u32(lay["img_ranges"], 2 * T).reshape(T, 2),
+                 tile_last=u32(lay["img_tile_last"], T))
 
 
 if __name__ == "__main__":
