@@ -277,6 +277,40 @@ def test_cfg5_full_size_properties(gpu_device):
     compare_backward(hip, run, dc, di, 1e-3)
 
 
+def test_cfg4_eight_views_full_size(gpu_device):
+    """BASELINE config 4 at full size on one device: 1M Gaussians, the 8 orbit views at 1920x1080, each view's
+    forward + compact backward, and the multi-view sums the one-view-per-GPU exchange forms (the
+    summed gradients == the sum of the 8 single-view gradients).  The 11 non-SH gradient columns are summed per
+    view, dL/dshs is expanded once from the 8 views' colour factors and camera positions (gsr_sh_backward_views);
+    both match the oracle's per-view gradients summed in float64 within 1e-3 relative L2."""
+    from gaussian_splatting_lightning_amd.rasterizer import backward_raw, forward_raw, sh_backward_views
+    W, H, V = 1920, 1080, 8
+    keys = ("means3D", "opacities", "scales", "rotations")
+    hip_sum, ora_sum, factors, camposes = {}, {}, [], []
+    for v in range(V):
+        inp = scene_inputs(1_000_000, W, H, sh_degree=3, seed=0, view_index=v, num_views=V)
+        dc, di = upstream(W, H, v)
+        rs = settings_for(inp, gpu_device)
+        t = {k: torch.as_tensor(inp[k], device=gpu_device) for k in keys + ("shs",)}
+        _, _, _, st = forward_raw(t["means3D"], t["shs"], None, t["opacities"], t["scales"], t["rotations"], None, rs)
+        g = backward_raw(st, rs, torch.as_tensor(dc, device=gpu_device), torch.as_tensor(di, device=gpu_device),
+                         compact_sh=True)
+        for k in keys:
+            x = g[k].double().cpu().numpy()
+            hip_sum[k] = x if v == 0 else hip_sum[k] + x
+        factors.append(g["colors_sh"])
+        camposes.append(rs.campos)
+        go = run_oracle(inp)[3].backward(dc, di)
+        for k in keys + ("shs",):
+            x = np.asarray(go[k], np.float64)
+            ora_sum[k] = x if v == 0 else ora_sum[k] + x
+    torch.cuda.synchronize()
+    hip_sum["shs"] = sh_backward_views(t["means3D"], torch.stack(camposes), torch.stack(factors), 3, 16).cpu().numpy()
+    for k in keys + ("shs",):
+        a, b = hip_sum[k].reshape(ora_sum[k].shape), ora_sum[k]
+        assert rel_l2(a, b) <= 1e-3, (k, rel_l2(a, b))
+
+
 def test_exact_culling_is_bitwise_invisible(gpu_device):
     """Culled instances are exactly those that would hit alpha < 1/255 at every pixel of their tile:
     turning the culling off must reproduce every output and gradient bit for bit."""
