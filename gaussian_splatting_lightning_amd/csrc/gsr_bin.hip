@@ -36,21 +36,6 @@ namespace gsr {
 // Big Gaussians (every rect cell kept) are spread over the blocks round-robin; a whole block strides over
 // each rect.  The next group's per-Gaussian records are loaded while the current group is walked.
 
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ int dpp_max_step(int v) {
-    return max(v, __builtin_amdgcn_update_dpp(-1, v, CTRL, ROW_MASK, 0xf, false));
-}
-// inclusive max-scan over the wave for values >= -1
-__device__ __forceinline__ int wave_inclusive_max(int v) {
-    v = dpp_max_step<0x111, 0xf>(v);  // row_shr:1
-    v = dpp_max_step<0x112, 0xf>(v);  // row_shr:2
-    v = dpp_max_step<0x114, 0xf>(v);  // row_shr:4
-    v = dpp_max_step<0x118, 0xf>(v);  // row_shr:8
-    v = dpp_max_step<0x142, 0xa>(v);  // row_bcast:15
-    v = dpp_max_step<0x143, 0xc>(v);  // row_bcast:31
-    return v;
-}
-
 // (row, column) of cell c of a rect of width w: floor((c + 1/2) / w) in fp32 is exact here ((c + 1/2) / w is
 // at least 1/(2w) from an integer and far below 2^20)
 __device__ __forceinline__ uint32_t rect_tile(uint32_t c, uint32_t rx, uint32_t ry, uint32_t w, float inv_w,

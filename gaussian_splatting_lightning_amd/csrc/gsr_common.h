@@ -667,6 +667,21 @@ __device__ __forceinline__ void stamp_store(uint4 *stamps, int slot, uint32_t t0
     stamps[slot] = make_uint4(t0, t1, hw, xcc);
 }
 
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ int dpp_max_step(int v) {
+    return max(v, __builtin_amdgcn_update_dpp(-1, v, CTRL, ROW_MASK, 0xf, false));
+}
+// inclusive max-scan over the wave for values >= -1
+__device__ __forceinline__ int wave_inclusive_max(int v) {
+    v = dpp_max_step<0x111, 0xf>(v);  // row_shr:1
+    v = dpp_max_step<0x112, 0xf>(v);  // row_shr:2
+    v = dpp_max_step<0x114, 0xf>(v);  // row_shr:4
+    v = dpp_max_step<0x118, 0xf>(v);  // row_shr:8
+    v = dpp_max_step<0x142, 0xa>(v);  // row_bcast:15
+    v = dpp_max_step<0x143, 0xc>(v);  // row_bcast:31
+    return v;
+}
+
 // Orders LDS writes before later LDS reads of other lanes of the SAME wave (no s_barrier).
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
