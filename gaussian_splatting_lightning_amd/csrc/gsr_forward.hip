@@ -952,12 +952,19 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
         for (int k = 0; k < NPIX; k++) sk[k] = livek[k] ? __ballot((m >> k) & 1u) : 0ull;  // finished strips: none
         loaded_end = min(r1, base + 64u);
         wave_lds_sync();
-        uint32_t cnt = min(64u, r1 - base);
-        uint64_t bit = 1;  // 1 << j
-        for (uint32_t j = 0; j < cnt; j++, bit <<= 1) {
+        // walk only the batch's instances that reach a live strip (in order): instances whose strips are all
+        // unreachable or finished cost nothing
+        uint64_t un = 0;
+#pragma unroll
+        for (int k = 0; k < NPIX; k++) un |= sk[k];
+        const uint32_t cbase = contributor;
+        while (un) {
+            const uint32_t j = (uint32_t)__builtin_ctzll(un);
+            un &= un - 1;
+            const uint64_t bit = 1ull << j;
             const float4 a = sr[j].a, b = sr[j].b;
             const float2 c = sr[j].c;
-            contributor++;
+            contributor = cbase + j + 1;
             const float dx = a.x - pfx, dy0 = a.y - pfy0;
             const float P0 = (a.z * dx) * dx, L = a.w * dx;
 #pragma unroll
@@ -984,14 +991,15 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
                     livek[k] &= ~stop;
                     if (livek[k] == 0) {  // the whole strip finished: skip it for the rest of the batch
                         sk[k] = 0;
-                        uint64_t anylive = 0;
+                        uint64_t live = 0;
 #pragma unroll
-                        for (int q = 0; q < NPIX; q++) anylive |= livek[q];
-                        if (anylive == 0) cnt = j + 1;  // every pixel of the wave finished: end the walk
+                        for (int q = 0; q < NPIX; q++) live |= sk[q];
+                        un &= live;  // every pixel of the wave finished: un = 0 ends the walk
                     }
                 }
             }
         }
+        contributor = cbase + min(64u, r1 - base);
         wave_lds_sync();
         uint64_t anylive = 0;
 #pragma unroll
