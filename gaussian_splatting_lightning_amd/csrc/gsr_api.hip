@@ -615,7 +615,7 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
 
     if (R > 0) {
         RenderBwdParams rp;
-        rp.W = W; rp.H = H; rp.gx = gx; rp.gy = gy; rp.num_tiles = (int)T;
+        rp.W = W; rp.H = H; rp.gx = gx; rp.gy = gy; rp.num_tiles = (int)T; rp.num_rendered = R;
         rp.ranges = im.ranges; rp.point_list = b.point_list; rp.n_contrib = im.n_contrib;
         const int lpt = tuning("lpt", 1);
         // "bwd_order" 0: reuse the forward's order (range lengths) and skip the tile_last ordering launch

@@ -130,7 +130,7 @@ __device__ __forceinline__ void wave_reduce_one_store(const float r[8], float *_
 // instance's gradient bits do not depend on whether it was paired.
 template <bool BOTH = true>
 __device__ __forceinline__ void wave_reduce_pair_store(const float r0[8], const float r1[8], float *__restrict__ dst,
-                                                       int lane) {
+                                                       int lane, float *__restrict__ dst1 = nullptr) {
     const bool hi5 = (lane & 32) != 0;
     const float dx = hi5 ? r1[7] : r0[7];
     const float s0 = sum_swap32(r0[0], r1[0]), s1 = sum_swap32(r0[1], r1[1]), s2 = sum_swap32(r0[2], r1[2]);
@@ -160,7 +160,7 @@ __device__ __forceinline__ void wave_reduce_pair_store(const float r0[8], const 
         c[m] = dpp_add<0x4E>(c[m]);   // quad_perm [2,3,0,1]
         c[m] = dpp_add<0x141>(c[m]);  // row_half_mirror
     }
-    float *row = dst + (hi5 ? PART : 0);
+    float *row = hi5 ? (dst1 ? dst1 : dst + PART) : dst;  // instance 1's row: dst1, or the next PART-float row
     const int low = ((lane >> 2) & 2) | ((lane >> 4) & 1);  // 2 b3 + b4
     if (!BOTH && hi5) return;
     if ((lane & 7) == 0) {
@@ -712,7 +712,7 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
 #ifndef GSR_BWD_MINW
 #define GSR_BWD_MINW 5
 #endif
-template <bool HAS_INV, bool LASTC>
+template <bool HAS_INV, bool LASTC, bool UNION = false>
 __global__ __launch_bounds__(64, GSR_BWD_MINW) void render_bwd_v5_kernel(RenderBwdParams p) {
     __shared__ FwdRec s_rec[BWD_BATCH];
     __shared__ __attribute__((aligned(16))) float s_part[BWD_BATCH][PART];  // [instance][10 sums]
@@ -845,6 +845,44 @@ __global__ __launch_bounds__(64, GSR_BWD_MINW) void render_bwd_v5_kernel(RenderB
             m[7] = dx;
             return any;
         };
+        if constexpr (UNION) {
+        // pair up only the instances that reach a live strip (lowest first); an instance's gradient bits do not
+        // depend on its partner (wave_reduce_pair_store), and the others get zero sums from their own lane
+        uint64_t un = 0;
+#pragma unroll
+        for (int k = 0; k < PIX_PER_LANE; k++) un |= sk[k];
+        un &= cnt >= 64 ? ~0ull : (1ull << cnt) - 1ull;
+        if (lane < cnt && !((un >> lane) & 1ull)) {
+            float4 *z = reinterpret_cast<float4 *>(s_part[lane]);
+            z[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+            z[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+            *reinterpret_cast<float2 *>(s_part[lane] + 8) = make_float2(0.f, 0.f);
+        }
+        while (un) {
+            const int j0 = (int)__builtin_ctzll(un);
+            un &= un - 1;
+            float m0[8];
+            const uint64_t any0 = pass(j0, m0);
+            float *dst = s_part[j0];
+            if (un) {
+                const int j1 = (int)__builtin_ctzll(un);
+                un &= un - 1;
+                float m1[8];
+                const uint64_t any1 = pass(j1, m1);
+                float *dst1 = s_part[j1];
+                if (any0 | any1) {
+                    wave_reduce_pair_store(m0, m1, dst, lane, dst1);
+                } else if (lane < 10) {
+                    dst[lane] = 0.f;
+                    dst1[lane] = 0.f;
+                }
+            } else if (any0) {
+                wave_reduce_pair_store<false>(m0, kZero8, dst, lane);
+            } else if (lane < 10) {
+                dst[lane] = 0.f;
+            }
+        }
+        } else {
         for (int j = 0; j < cnt; j += 2) {
             float m0[8];
             const uint64_t any0 = pass(j, m0);
@@ -863,6 +901,7 @@ __global__ __launch_bounds__(64, GSR_BWD_MINW) void render_bwd_v5_kernel(RenderB
             } else if (lane < 10) {
                 dst[lane] = 0.f;
             }
+        }
         }
         wave_lds_sync();
         if (lane < cnt) {
@@ -1096,11 +1135,18 @@ void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
         }
         if (bv == 5) {  // "bwd_lastc" 1: strip liveness and compare skipping by n_contrib bounds (measured 2.5 % slower: SALU)
             const bool lc = tuning("bwd_lastc", 0) != 0;
+            // "bwd_union" -1 (auto): pair only the instances that reach a strip when tiles are long (mean above
+            // 1024 instances: cfg 5 render_bwd 0.93 -> 0.90 ms; at cfg 3's 517 the plain walk is faster, 0.305 vs
+            // 0.329 ms); 0 / 1 force it
+            const int un = tuning("bwd_union", -1);
+            const bool u = un < 0 ? p.num_rendered > (uint64_t)1024 * (uint64_t)p.num_tiles : un != 0;
             if (p.dL_dinvdepth) {
-                if (lc) render_bwd_v5_kernel<true, true><<<grid, block, 0, s>>>(q);
+                if (u) render_bwd_v5_kernel<true, false, true><<<grid, block, 0, s>>>(q);
+                else if (lc) render_bwd_v5_kernel<true, true><<<grid, block, 0, s>>>(q);
                 else render_bwd_v5_kernel<true, false><<<grid, block, 0, s>>>(q);
             } else {
-                if (lc) render_bwd_v5_kernel<false, true><<<grid, block, 0, s>>>(q);
+                if (u) render_bwd_v5_kernel<false, false, true><<<grid, block, 0, s>>>(q);
+                else if (lc) render_bwd_v5_kernel<false, true><<<grid, block, 0, s>>>(q);
                 else render_bwd_v5_kernel<false, false><<<grid, block, 0, s>>>(q);
             }
             return;

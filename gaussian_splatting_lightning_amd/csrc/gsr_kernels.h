@@ -147,6 +147,7 @@ struct RenderBwdParams {
     int prio_div;   // as RenderFwdParams::prio_div (set by launch)
     uint4 *stamps;  // diagnostics (set by launch), or null
     int strip_exact;  // as RenderFwdParams::strip_exact (set by launch)
+    uint64_t num_rendered = 0;  // instances (the launch's walk-variant choice)
 };
 void launch_render_bwd(hipStream_t s, const RenderBwdParams &p);
 

@@ -425,7 +425,8 @@ def test_densify_stats_from_backward(gpu_device):
                                    {"bwd_v": 4}, {"bwd_v": 6}, {"bwd_lastc": 1},
                                    {"bwd_v": 4, "bwd_strip": 0},
                                    {"bwd_v": 4, "bwd_pred": 0}, {"bwd_v": 4, "bwd_pred": 1}, {"bwd_v": 3},
-                                   {"bwd_v": 4, "bwd_pair": 0}, {"bwd_parts": 2}, {"bwd_parts": 4}])
+                                   {"bwd_v": 4, "bwd_pair": 0}, {"bwd_parts": 2}, {"bwd_parts": 4},
+                                   {"bwd_union": 1}, {"fwd_parts": 1, "bwd_union": 1}])
 def test_composite_variants_are_bitwise_identical(gpu_device, knobs):
     """Strip skipping (row-band or exact column-band masks) only skips rows where every pixel fails
     alpha >= 1/255, the wave-uniform v5 / v6 forwards perform composite_fwd's pixel update (v6 retiring finished
@@ -434,7 +435,9 @@ def test_composite_variants_are_bitwise_identical(gpu_device, knobs):
     (the default at this size) or whole (with a 5 % share of split heavy tiles) gives the same pixels and
     contributor counts, the v5 backward's n_contrib strip bounds only skip strips and compares that cannot
     contribute, and the v6 backward's select-predicated update leaves every accumulator bitwise unchanged on the
-    lanes it masks: outputs and gradients must match bit for bit (with a non-zero background).  The v3
+    lanes it masks, and the union walk (bwd_union: pairs formed only from instances that reach a strip) gives each
+    instance the same reduction tree whatever its partner: outputs and gradients must match bit for bit (with a
+    non-zero background).  The v3
     backward keeps the per-channel accumulators, and the parts backward adds its waves' per-instance sums:
     gradients agree to rounding only."""
     from gaussian_splatting_lightning_amd import _native
@@ -450,7 +453,7 @@ def test_composite_variants_are_bitwise_identical(gpu_device, knobs):
         for k in knobs:
             _native.set_tuning(k, {"fwd_strip": 0, "fwd_parts": 0, "bwd_strip": 1, "bwd_pred": 2, "bwd_v": 5,
                                    "bwd_pair": 1, "bwd_parts": 0, "fwd_v": 6, "fwd_strip_parts": 1,
-                                   "strip_exact": 1, "bwd_lastc": 0}[k])
+                                   "strip_exact": 1, "bwd_lastc": 0, "bwd_union": -1}[k])
         _native.set_tuning("bwd_parts", 0)
     for k in ("color", "invdepth", "radii"):
         assert np.array_equal(ref[k], alt[k]), k
