@@ -194,6 +194,26 @@ def main():
         elapsed = float(t.item())
     ms_per_step = 1e3 * elapsed / args.steps
 
+    # ---- per-step distribution (separate pass, not the headline): one hipEvent at every step boundary on the
+    # launch stream, SURVEY.md §8(d)'s "median of >= 20 hipEvent-timed steps".  Each event is a stream marker the
+    # next kernel waits behind (~6 us), so these per-step times run slightly above the wall-clock mean. ----
+    n_ev = max(args.steps, 20)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev + 1)]
+    gc.disable()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs[0].record()
+    for i in range(n_ev):
+        st = step()
+        evs[i + 1].record()
+    torch.cuda.synchronize()
+    gc.enable()
+    per_step = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(n_ev))
+    step_events = {"steps": n_ev, "p50_ms": round(per_step[n_ev // 2], 4),
+                   "p90_ms": round(per_step[min(n_ev - 1, (9 * n_ev) // 10)], 4),
+                   "min_ms": round(per_step[0], 4), "mean_ms": round(sum(per_step) / n_ev, 4)}
+
     # ---- per-launch statistics for the roofline (untimed) ----
     lay = _native.state_layout(n, st.num_rendered, W, H)
     T = ((W + 15) // 16) * ((H + 15) // 16)
@@ -292,6 +312,7 @@ def main():
                                     if use_events else "none")},
         **({"multi_gpu_note": "the RCCL exchange cannot be rehearsed on a 1-GPU box (RCCL rejects two ranks on one "
                               "device); gloo world-size-2 tests cover its logic (DESIGN.md §6)"} if world > 1 else {}),
+        "step_events_ms": step_events,
         "roofline": roofline, "cpu_baseline": cpu,
         "stages_ms": {k: round(v, 4) for k, v in stage_avg.items() if v > 0},
     }

@@ -481,6 +481,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     // Otherwise the radix path: depth sort, depth-ordered expansion, stable tile sort.
     const bool bucket = bk_possible && (bk == 2 || (uint64_t)R <= (uint64_t)BK_MAX_MEAN * T);
     bool sorted_exp = false;
+    bool depth_onesweep = false, tile_onesweep = false;  // which sorts own a cleared onesweep error word
     if (!bucket) {
         // the depth sort's last pass also writes the tile counts and expansion records in depth order ("sort_gather"
         // bit 0 / bit 1; unset: the scan / the expansion gathers them through the order instead)
@@ -491,7 +492,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
         bool sorted_recs = false;
         GSR_STAGE(ST_DEPTH_SORT, dbg,
                   sorted_recs = launch_radix_sort(stream, g.sort, (uint32_t)P, 32, false, g.depth_key,
-                                                  sg ? &ga : nullptr));
+                                                  sg ? &ga : nullptr, &depth_onesweep));
         const bool sorted_tiles = sorted_recs && (sg & 1);
         sorted_exp = sorted_recs && (sg & 2);
         if (tuning("scan_lookback", 1))
@@ -541,7 +542,8 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             ep.exp_owner = tuning("exp_owner", 1) ? b.exp_owner : nullptr;
             ep.keys_out = b.sort.k[0]; ep.inst_gid = b.inst_gid; ep.inst_start = g.inst_start;
             GSR_STAGE(ST_EXPAND, dbg, launch_expand(stream, ep));
-            GSR_STAGE(ST_TILE_SORT, dbg, launch_radix_sort(stream, b.sort, R, tile_key_bits(T)));
+            GSR_STAGE(ST_TILE_SORT, dbg,
+                      launch_radix_sort(stream, b.sort, R, tile_key_bits(T), false, nullptr, nullptr, &tile_onesweep));
             GSR_HIP(hipMemsetAsync(b.inv, 0xff, sizeof(uint32_t) * (size_t)R, stream));
         }
         GSR_STAGE(ST_RANGES, dbg, {
@@ -567,12 +569,9 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     rp.out_color = a->out_color; rp.out_invdepth = a->out_invdepth; rp.final_T = im.final_T;
     rp.n_contrib = im.n_contrib; rp.tile_last = im.tile_last;
     GSR_STAGE(ST_RENDER_FWD, dbg, launch_render_fwd(stream, rp));
-    if (dbg) {  // onesweep control blocks exist only for the sorts that ran on the onesweep path
-        const int os = tuning("onesweep", 1);
-        return check_lookback_flags(stream, device_guard.dev, g.counters,
-                                    (!bucket && (os & 1)) ? g.sort.ctrl : nullptr,
-                                    (!bucket && R > 0 && (os & 2)) ? b.sort.ctrl : nullptr);
-    }
+    if (dbg)  // onesweep error words exist only for the sorts that ran on the onesweep path (launch_radix_sort)
+        return check_lookback_flags(stream, device_guard.dev, g.counters, depth_onesweep ? g.sort.ctrl : nullptr,
+                                    tile_onesweep ? b.sort.ctrl : nullptr);
     return GSR_OK;
 }
 

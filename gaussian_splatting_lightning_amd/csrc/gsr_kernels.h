@@ -30,6 +30,8 @@ void launch_exclusive_scan_lookback(hipStream_t s, const uint32_t *in, const uin
 // keys0 (optional): read the first pass's keys from there instead of sc.k[0] (left unmodified).
 // gather (optional): the last pass also writes dst[i] = src[sorted value i] for each non-null pair; returns
 // whether it did (always, with a gather).
+// onesweep_ran (optional): set to whether the onesweep path ran, i.e. whether sc.ctrl[RS_CTRL_ERR] was cleared and
+// holds this sort's look-back error flag (the multi-kernel path never touches sc.ctrl).
 struct SortGather {
     const uint32_t *src = nullptr;
     uint32_t *dst = nullptr;
@@ -37,7 +39,8 @@ struct SortGather {
     uint4 *dst4 = nullptr;
 };
 bool launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bool keyed = false,
-                       const uint32_t *keys0 = nullptr, const SortGather *gather = nullptr);
+                       const uint32_t *keys0 = nullptr, const SortGather *gather = nullptr,
+                       bool *onesweep_ran = nullptr);
 
 // ---- forward (gsr_forward.hip) ----
 struct PreprocessParams {
@@ -125,7 +128,6 @@ struct RenderFwdParams {
     const float *bg;
     float *out_color, *out_invdepth, *final_T;
     uint32_t *n_contrib, *tile_last;
-    int prio_div;  // > 0: launch slots [0, d) run at wave priority 3, [d, 2d) at 2, [2d, 3d) at 1 (set by launch)
     uint4 *stamps; // diagnostics (set by launch), or null
     int strip_exact;  // strip skipping mask: 1 strip_mask_exact (column-band extent), 0 strip_mask (set by launch)
 };
@@ -144,7 +146,6 @@ struct RenderBwdParams {
     const float *bg, *final_T, *dL_dpix, *dL_dinvdepth;
     float *rows;    // R x GRAD_ROW
     int rows_by_u;  // 1: row of an instance at its expansion index u (Gaussian-major), 0: at its sorted position
-    int prio_div;   // as RenderFwdParams::prio_div (set by launch)
     uint4 *stamps;  // diagnostics (set by launch), or null
     int strip_exact;  // as RenderFwdParams::strip_exact (set by launch)
     uint64_t num_rendered = 0;  // instances (the launch's walk-variant choice)

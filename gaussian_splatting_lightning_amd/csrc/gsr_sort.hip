@@ -672,7 +672,8 @@ static void launch_radix_sort_multi(hipStream_t s, SortScratch &sc, uint32_t n, 
 }
 
 bool launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bool keyed, const uint32_t *keys0,
-                       const SortGather *gather) {
+                       const SortGather *gather, bool *onesweep_ran) {
+    if (onesweep_ran) *onesweep_ran = false;
     if (n == 0) return gather != nullptr;
     if (!keys0) keys0 = sc.k[0];
     const int passes = radix_passes(nbits);
@@ -688,6 +689,7 @@ bool launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bo
         else if (lbw >= 32) launch_radix_sort_onesweep<RS_ITEMS, 32>(s, sc, n, passes, keyed, keys0, gather);
         else if (lbw >= 16) launch_radix_sort_onesweep<RS_ITEMS, 16>(s, sc, n, passes, keyed, keys0, gather);
         else launch_radix_sort_onesweep<RS_ITEMS, 1>(s, sc, n, passes, keyed, keys0, gather);
+        if (onesweep_ran) *onesweep_ran = true;
         return gather != nullptr;
     }
     // "rs_items": keys per thread of the multi-kernel path (16 or 32; fewer blocks, longer digit runs per block)

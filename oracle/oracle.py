@@ -50,6 +50,7 @@ def _load():
     lib.oracle_get_ranges.argtypes = [ctypes.c_void_p, _u32]
     lib.oracle_get_image_state.argtypes = [ctypes.c_void_p, _f, _u32]
     lib.oracle_get_geom.argtypes = [ctypes.c_void_p, _f, _f, _f, _f, _u32]
+    lib.oracle_threshold_margin.argtypes = [ctypes.c_void_p, _f]
     lib.oracle_mark_visible.argtypes = [ctypes.c_int, _f, _f, _f, _u8]
     lib.oracle_num_threads.restype = ctypes.c_int
     lib.oracle_bin_count.restype = ctypes.c_longlong
@@ -152,6 +153,13 @@ class OracleRun:
         nc = np.zeros(self.W * self.H, dtype=np.uint32)
         self._lib.oracle_get_image_state(self._h, _fp(ft), nc.ctypes.data_as(_u32))
         return ft.reshape(self.H, self.W), nc.reshape(self.H, self.W)
+
+    def threshold_margin(self) -> np.ndarray:
+        """(H, W) distance of each pixel's nearest compositing decision from its threshold, in units of the fp32
+        evaluation error (gsr_oracle.c oracle_threshold_margin); < 1 marks a threshold-flip candidate."""
+        out = np.zeros(self.W * self.H, dtype=np.float32)
+        self._lib.oracle_threshold_margin(self._h, _fp(out))
+        return out.reshape(self.H, self.W)
 
     def geom(self):
         P = self.P

@@ -13,6 +13,11 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X); parity tests of the HIP path")
 
 
+def pytest_sessionfinish(session, exitstatus):
+    from tests import parity
+    parity.dump()
+
+
 @pytest.fixture(scope="session")
 def gpu_device():
     import torch

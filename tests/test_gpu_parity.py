@@ -1,17 +1,23 @@
 """Parity of the HIP path (through the C ABI) against the CPU oracle and the reference's golden vectors.
 
-Bars (DESIGN.md "Parity"):
+Bars (DESIGN.md "Parity"), against the oracle's OWN forward on the same inputs:
   * integer state is bit-exact: radii, num_rendered, tiles touched, the sorted instance list
-    (tile, depth, index order) and the per-tile ranges;
-  * n_contrib (last contributor per pixel) matches on >= 99.9 % of pixels -- the rest are alpha == 1/255
-    or T == 1e-4 threshold flips from 1-ulp differences between the device expf and glibc's;
-  * colour / inverse depth: |err| <= 1e-5 on >= 99.9 % of pixels and <= 2e-2 everywhere (a flip);
-  * gradients: relative L2 <= 1e-4 (unsaturated scenes) or <= 1e-3 (saturating scenes);
+    (tile, depth, index order), the per-tile ranges -- and the per-Gaussian render records (pixel centre, conic,
+    opacity, depth bits), since the device evaluates that geometry chain uncontracted like the oracle;
+  * n_contrib (last contributor per pixel) is exact on every pixel except the oracle's threshold-flip candidates
+    (a decision alpha = 1/255, T = 1e-4 or power = 0 within the fp32 evaluation error, oracle.threshold_margin);
+  * colour / inverse depth: |err| <= 1e-5 outside the candidates and <= 2e-2 everywhere (a flip);
+  * gradients: relative L2 <= 1e-4 over the Gaussians no candidate pixel touches, and the per-case bar over all;
   * the backward is deterministic: two runs give bitwise identical gradients.
+Achieved errors are recorded per case (tests/parity.py; GSR_PARITY_JSON=path writes them).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
+
+from tests import parity
 
 from tests.helpers import (close_fraction, golden_inputs, hip_state_arrays, load_golden, rel_l2, run_hip,
                            run_oracle, scene_inputs, settings_for, upstream)
@@ -21,22 +27,41 @@ pytestmark = pytest.mark.gpu
 GRADS = ("means3D", "means2D", "opacities", "scales", "rotations", "shs")
 
 
+# Bars are about 2x the achieved errors recorded in profiles/parity_r3.json (every case of this file, round 3):
+FLIP_MARGIN = 1.0    # oracle threshold margin below which a pixel is a threshold-flip candidate (oracle.threshold_margin)
+COLOR_TOL = 3e-6     # |colour|, |inverse depth| (relative to max(1, |v|)) on every other pixel; achieved <= 1.31e-6
+                     # (SURVEY Appendix A13 asks ~1e-5)
+FLIP_TOL = 2e-2      # anywhere (one alpha = 1/255 or T = 1e-4 flip moves a pixel by < alpha T); achieved <= 3.4e-3
+GRAD_CLEAN_TOL = 5e-6  # gradient rel-L2 over the Gaussians no flip candidate touches; achieved <= 1.95e-6
+                       # (A13 asks ~1e-4)
+GRAD_TOL_ADHOC = 1e-3  # the few cases checked without flip separation (precomputed inputs, the autograd API)
+
+
+def _case():
+    return os.environ.get("PYTEST_CURRENT_TEST", "unknown").rsplit("::", 1)[-1].split(" ")[0]
+
+
 def compare_forward(inp, hip, oracle_out):
-    from oracle import oracle as O
+    """HIP forward against the oracle's own forward on the same inputs.  Integer state and the per-Gaussian render
+    records are bit-exact; pixels are exact in contributor count and within COLOR_TOL in value everywhere except the
+    oracle's threshold-flip candidates, which stay within FLIP_TOL.  Achieved errors go to the parity record."""
     color, radii, invd, run = oracle_out
     W, H = inp["image_width"], inp["image_height"]
-    # radius = ceil(3 sqrt(lambda_max)) is integer-valued but derived from floating point: FMA contraction
-    # on the device may move it by one at an exact integer boundary.
-    d = hip["radii"].astype(np.int64) - radii
-    assert np.mean(d == 0) >= 0.9999 and np.abs(d).max(initial=0) <= 1
     hs = hip_state_arrays(hip)
-    # The integer binning (scan, expansion, both radix sorts, ranges) is bit-exact on the HIP path's own
-    # preprocess outputs: (tile, depth bits, Gaussian index) order, identical ranges.
-    pl, rg, tt = O.bin_instances(hs["xy"], hip["radii"], hs["depths"], hs["conic_opacity"], W, H, cull=True)
-    assert hs["num_rendered"] == len(pl)
+    g = run.geom()
+    # integer outputs: bit-exact against the oracle's own preprocess (radii, kept tiles) and binning
+    assert np.array_equal(hip["radii"], radii)
+    assert hs["num_rendered"] == run.num_rendered
+    assert np.array_equal(hs["tiles"], g["tiles_touched"])
+    pl, rg = run.point_list(), run.ranges()
     assert np.array_equal(hs["point_list"], pl)
     assert np.array_equal(hs["ranges"], rg)
-    assert np.array_equal(hs["tiles"], tt)
+    # the render records the compositor reads: the same bits for every rendered Gaussian
+    on = radii > 0
+    for k in ("xy", "conic_opacity"):
+        assert np.array_equal(hs[k][on].view(np.uint32), g[k][on].view(np.uint32)), k
+    kept = g["tiles_touched"] > 0
+    assert np.array_equal(hs["depths"][kept].view(np.uint32), g["depths"][kept].view(np.uint32))
     # The forward gathers every instance any pixel can reach; for exactly those it writes the sorted id
     # list and the inverse permutation (sorted position of each expansion index); others keep INV_NONE.
     loaded = np.zeros(len(pl), bool)
@@ -47,23 +72,62 @@ def compare_forward(inp, hip, oracle_out):
     s_idx = np.nonzero(loaded)[0]
     assert np.array_equal(hs["inv"][hs["sorted_u"][s_idx]], s_idx.astype(np.uint32))
     assert np.sum(hs["inv"] != 0xFFFFFFFF) == loaded.sum()
-    assert abs(hs["num_rendered"] - run.num_rendered) <= 1e-4 * run.num_rendered + 2
-    ft, nc = run.image_state()
-    # threshold flips: at most 0.1 % of the pixels (and at least 3 allowed, for tiny images)
-    flips = max(3, int(1e-3 * W * H))
-    assert np.sum(hs["n_contrib"] != nc) <= flips
-    assert np.sum(np.any(np.abs(hip["color"] - color) > 1e-5, axis=0)) <= flips
-    assert np.abs(hip["color"] - color).max() <= 2e-2
-    assert np.sum(np.abs(hip["invdepth"] - invd) > 1e-5 + 1e-5 * np.abs(invd)) <= flips
+    # pixels
+    _, nc = run.image_state()
+    flip = run.threshold_margin() < FLIP_MARGIN
+    ok = ~flip
+    nc_bad = hs["n_contrib"] != nc
+    cerr = np.abs(hip["color"] - color)
+    ierr = np.abs(hip["invdepth"] - invd)[0]
+    ierr_rel = ierr / np.maximum(np.abs(invd[0]), 1.0)
+    rec = dict(W=W, H=H, P=int(len(radii)), num_rendered=int(run.num_rendered), flip_candidates=int(flip.sum()),
+               n_contrib_mismatch=int(nc_bad.sum()), n_contrib_mismatch_outside_candidates=int((nc_bad & ok).sum()),
+               color_maxabs_clean=float(cerr[:, ok].max(initial=0)), color_maxabs_all=float(cerr.max(initial=0)),
+               color_rel_l2=rel_l2(hip["color"], color),
+               invdepth_maxrel_clean=float(ierr_rel[ok].max(initial=0)),
+               invdepth_maxrel_all=float(ierr_rel.max(initial=0)), invdepth_rel_l2=rel_l2(hip["invdepth"], invd))
+    parity.record(_case(), "forward", rec)
+    assert rec["n_contrib_mismatch_outside_candidates"] == 0, rec
+    assert rec["color_maxabs_clean"] <= COLOR_TOL, rec
+    assert rec["invdepth_maxrel_clean"] <= COLOR_TOL, rec
+    assert rec["color_maxabs_all"] <= FLIP_TOL, rec
+    # Gaussians whose gradient a flip candidate can move: those the pixel's walk reaches on either side
+    gx = (W + 15) // 16
+    touched = np.zeros(len(radii), bool)
+    ys, xs = np.nonzero(flip)
+    if len(ys):
+        t = (ys // 16) * gx + xs // 16
+        n = np.maximum(hs["n_contrib"][ys, xs], nc[ys, xs]).astype(np.int64)
+        for tt in np.unique(t):
+            m = int(n[t == tt].max())
+            touched[pl[rg[tt, 0]: rg[tt, 0] + m]] = True
+    run.flip_touched = touched
     return run
 
 
 def compare_backward(hip, run, dc, di, tol):
+    """Gradients against the oracle's backward: relative L2 <= tol over all Gaussians, and <= GRAD_CLEAN_TOL over
+    the Gaussians no threshold-flip candidate pixel touches (their gradients see the same decisions)."""
     g = run.backward(dc, di)
+    touched = getattr(run, "flip_touched", None)
+    rec = {"touched_gaussians": int(touched.sum()) if touched is not None else None}
     for k in GRADS:
         if hip["grads"].get(k) is None:
             continue
-        assert rel_l2(hip["grads"][k], g[k]) <= tol, (k, rel_l2(hip["grads"][k], g[k]))
+        a, b = hip["grads"][k], g[k]
+        e = {"rel_l2": rel_l2(a, b)}
+        if touched is not None:
+            clean = ~touched
+            e["rel_l2_clean"] = rel_l2(a[clean], b[clean])
+            e["maxabs_clean_over_maxref"] = float(np.abs(a[clean] - b[clean]).max(initial=0) /
+                                                  max(np.abs(b).max(initial=0), 1e-30))
+        rec[k] = e
+    parity.record(_case(), "backward", rec)
+    for k in GRADS:
+        if k in rec:
+            assert rec[k]["rel_l2"] <= tol, (k, rec[k])
+            if "rel_l2_clean" in rec[k]:
+                assert rec[k]["rel_l2_clean"] <= GRAD_CLEAN_TOL, (k, rec[k])
     return g
 
 
@@ -108,18 +172,19 @@ def test_golden_cfg1_direct(gpu_device):
     hip = run_hip(inp, gpu_device)
     hs = hip_state_arrays(hip)
     _, _, _, run = run_oracle(inp)
-    assert abs(hs["num_rendered"] - run.num_rendered) <= 2
+    assert hs["num_rendered"] == run.num_rendered
     keep = hs["final_T"] >= 0.011
     err = np.abs(hip["color"] - z["ref_color"])[:, keep].max(0)
     assert np.mean(err <= 1e-5) >= 0.999 and err.max() <= 5e-3
 
 
 CASES = {
-    # name: (n, W, H, sh_degree, opacity_scale, bg, seed, grad_tol)
-    "unsat_sh3_200x136": (3000, 200, 136, 3, 0.05, (0.3, 0.6, 0.9), 11, 1e-4),
-    "cfg1_10k_256_sh0": (10_000, 256, 256, 0, 1.0, (0.0, 0.0, 0.0), 0, 1e-3),
-    "sat_sh2_white_333x211": (20_000, 333, 211, 2, 1.0, (1.0, 1.0, 1.0), 7, 1e-3),
-    "cfg2_100k_800_sh3": (100_000, 800, 800, 3, 1.0, (0.0, 0.0, 0.0), 0, 1e-3),
+    # name: (n, W, H, sh_degree, opacity_scale, bg, seed, grad_tol over ALL Gaussians, threshold flips included:
+    # about 2x the achieved maximum over the gradient fields, profiles/parity_r3.json)
+    "unsat_sh3_200x136": (3000, 200, 136, 3, 0.05, (0.3, 0.6, 0.9), 11, 2e-6),   # achieved 7.3e-7
+    "cfg1_10k_256_sh0": (10_000, 256, 256, 0, 1.0, (0.0, 0.0, 0.0), 0, 6e-4),    # 3.1e-4: flips touch 13 % of Gaussians
+    "sat_sh2_white_333x211": (20_000, 333, 211, 2, 1.0, (1.0, 1.0, 1.0), 7, 2e-6),  # 9.2e-7
+    "cfg2_100k_800_sh3": (100_000, 800, 800, 3, 1.0, (0.0, 0.0, 0.0), 0, 4e-6),  # 1.9e-6
 }
 
 
@@ -139,7 +204,7 @@ def test_no_invdepth_gradient_path(gpu_device):
     hip = run_hip(inp, gpu_device, dc, None)
     out = run_oracle(inp)
     run = compare_forward(inp, hip, out)
-    compare_backward(hip, run, dc, None, 1e-3)
+    compare_backward(hip, run, dc, None, 2e-6)  # achieved 8.2e-7
 
 
 def test_big_gaussians_and_partial_tiles(gpu_device):
@@ -150,7 +215,7 @@ def test_big_gaussians_and_partial_tiles(gpu_device):
     hip = run_hip(inp, gpu_device, dc, di)
     run = compare_forward(inp, hip, run_oracle(inp))
     assert int((run.geom()["tiles_touched"] > 64).sum()) > 10
-    compare_backward(hip, run, dc, di, 1e-3)
+    compare_backward(hip, run, dc, di, 4e-4)  # achieved 1.6e-4 (threshold flips; 1.2e-6 over the untouched Gaussians)
 
 
 def test_precomputed_colors_and_cov3d(gpu_device):
@@ -172,9 +237,10 @@ def test_precomputed_colors_and_cov3d(gpu_device):
     out = run_oracle(inp, colors_precomp=colors, cov3D_precomp=cov)
     run = compare_forward(inp, hip, out)
     g = run.backward(dc, di)
-    assert rel_l2(hip["grads"]["colors"], g["colors"]) <= 1e-4
-    assert rel_l2(hip["grads"]["cov3D"], g["cov3D"]) <= 1e-3
-    assert rel_l2(hip["grads"]["means3D"], g["means3D"]) <= 1e-3
+    rec = {k: rel_l2(hip["grads"][k], g[k]) for k in ("colors", "cov3D", "means3D", "means2D", "opacities")}
+    parity.record(_case(), "backward", rec)
+    for k, e in rec.items():
+        assert e <= GRAD_TOL_ADHOC, (k, e)
 
 
 def test_antialiasing(gpu_device):
@@ -182,7 +248,7 @@ def test_antialiasing(gpu_device):
     dc, di = upstream(144, 144, 13)
     hip = run_hip(inp, gpu_device, dc, di, antialiasing=True)
     run = compare_forward(inp, hip, run_oracle(inp, antialiasing=True))
-    compare_backward(hip, run, dc, di, 1e-3)
+    compare_backward(hip, run, dc, di, 4e-6)  # achieved 1.9e-6
 
 
 @pytest.mark.parametrize("W,H", [(1, 1), (7, 5), (16, 16), (17, 33)])
@@ -191,7 +257,7 @@ def test_tiny_images(gpu_device, W, H):
     dc, di = upstream(W, H, 3)
     hip = run_hip(inp, gpu_device, dc, di)
     run = compare_forward(inp, hip, run_oracle(inp))
-    compare_backward(hip, run, dc, di, 1e-3)
+    compare_backward(hip, run, dc, di, 2e-6)  # achieved 6.9e-7
 
 
 def test_all_culled_and_empty(gpu_device):
@@ -239,16 +305,19 @@ def test_autograd_api_and_means2d(gpu_device):
     loss.backward()
     _, _, _, run = run_oracle(inp)
     g = run.backward(dc, di)
-    assert rel_l2(screen.grad.cpu().numpy(), g["means2D"]) <= 1e-3
-    assert rel_l2(means.grad.cpu().numpy(), g["means3D"]) <= 1e-3
-    assert rel_l2(shs.grad.cpu().numpy(), g["shs"]) <= 1e-3
+    rec = {"means2D": rel_l2(screen.grad.cpu().numpy(), g["means2D"]),
+           "means3D": rel_l2(means.grad.cpu().numpy(), g["means3D"]), "shs": rel_l2(shs.grad.cpu().numpy(), g["shs"])}
+    parity.record(_case(), "backward", rec)
+    for k, e in rec.items():
+        assert e <= GRAD_TOL_ADHOC, (k, e)
     vis = radii > 0
     assert torch.all(screen.grad[~vis] == 0)
 
 
 def test_cfg3_full_size_properties(gpu_device):
     """BASELINE config 3 (1M Gaussians, 1920x1080, SH3) at full size: exact instance count and sorted
-    list against the oracle, image within tolerance, gradients within 1e-3 relative L2."""
+    list against the oracle, image within the forward bars, gradients within 2e-4 relative L2 (5e-6 over the
+    Gaussians no threshold flip touches)."""
     inp = scene_inputs(1_000_000, 1920, 1080, sh_degree=3, seed=0)
     dc, di = upstream(1920, 1080, 0)
     hip = run_hip(inp, gpu_device, dc, di)
@@ -260,20 +329,23 @@ def test_cfg3_full_size_properties(gpu_device):
     g = run.geom()
     full, _, _ = O.bin_instances(g["xy"], out[1], g["depths"], g["conic_opacity"], 1920, 1080, cull=False)
     assert abs(len(full) - 6_560_987) <= 2
-    compare_backward(hip, run, dc, di, 1e-3)
+    compare_backward(hip, run, dc, di, 2e-4)  # achieved 8.9e-5 (threshold flips; 9.7e-7 over the untouched Gaussians)
 
 
 def test_cfg5_full_size_properties(gpu_device):
     """BASELINE config 5 (5M Gaussians, 3840x2160, SH3, 1 % bloated "densification-era" Gaussians) at full size:
     48M instances, so the forward takes the radix binning path (depth sort, depth-ordered expansion, stable tile
     sort).  The sorted instance list and tile ranges are bit-exact against the oracle's binning of the same
-    preprocess outputs, the image matches within the forward bars and the gradients within 1e-3 relative L2."""
+    preprocess outputs, the image matches within the forward bars and the gradients within 1e-3 relative L2 (5e-6
+    over the Gaussians no threshold flip touches)."""
     W, H = 3840, 2160
     inp = scene_inputs(5_000_000, W, H, sh_degree=3, seed=0, stress_fraction=0.01)
     dc, di = upstream(W, H, 0)
     hip = run_hip(inp, gpu_device, dc, di)
     assert hip["state"].num_rendered > 1024 * ((W + 15) // 16) * ((H + 15) // 16)  # above the bucket path's mean
     run = compare_forward(inp, hip, run_oracle(inp))
+    # 3914 flip-candidate pixels touch 124k Gaussians (2.5 %) whose long saturated walks carry the flips into the
+    # gradients: 4.9e-4 over all Gaussians (scales), 9.0e-7 over the untouched ones (GRAD_CLEAN_TOL)
     compare_backward(hip, run, dc, di, 1e-3)
 
 
@@ -306,9 +378,10 @@ def test_cfg4_eight_views_full_size(gpu_device):
             ora_sum[k] = x if v == 0 else ora_sum[k] + x
     torch.cuda.synchronize()
     hip_sum["shs"] = sh_backward_views(t["means3D"], torch.stack(camposes), torch.stack(factors), 3, 16).cpu().numpy()
-    for k in keys + ("shs",):
-        a, b = hip_sum[k].reshape(ora_sum[k].shape), ora_sum[k]
-        assert rel_l2(a, b) <= 1e-3, (k, rel_l2(a, b))
+    rec = {k: rel_l2(hip_sum[k].reshape(ora_sum[k].shape), ora_sum[k]) for k in keys + ("shs",)}
+    parity.record(_case(), "backward_view_sums", rec)
+    for k, e in rec.items():
+        assert e <= 1e-3, (k, e)
 
 
 def test_exact_culling_is_bitwise_invisible(gpu_device):
@@ -418,31 +491,22 @@ def test_densify_stats_from_backward(gpu_device):
     assert torch.equal(mrad, torch.maximum(radii.to(torch.int32), torch.full_like(mrad, 3)))
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("knobs", [{"fwd_strip": 1, "fwd_parts": 1}, {"fwd_parts": 2}, {"fwd_v": 4}, {"fwd_v": 5},
-                                   {"fwd_v": 5, "fwd_parts": 4}, {"fwd_parts": 4}, {"fwd_parts": 1},
-                                   {"fwd_v": 4, "fwd_parts": 2, "fwd_strip_parts": 0}, {"strip_exact": 0},
-                                   {"bwd_v": 4}, {"bwd_v": 6}, {"bwd_lastc": 1},
-                                   {"bwd_v": 4, "bwd_strip": 0},
-                                   {"bwd_v": 4, "bwd_pred": 0}, {"bwd_v": 4, "bwd_pred": 1}, {"bwd_v": 3},
-                                   {"bwd_v": 4, "bwd_pair": 0}, {"bwd_parts": 2}, {"bwd_parts": 4},
+@pytest.mark.parametrize("knobs", [{"fwd_parts": 1}, {"fwd_parts": 2}, {"fwd_parts": 4}, {"fwd_whole_waves": 6},
+                                   {"strip_exact": 0}, {"bwd_lastc": 1}, {"bwd_parts": 2}, {"bwd_parts": 4},
                                    {"bwd_union": 1}, {"fwd_parts": 1, "bwd_union": 1}])
 def test_composite_variants_are_bitwise_identical(gpu_device, knobs):
-    """Strip skipping (row-band or exact column-band masks) only skips rows where every pixel fails
-    alpha >= 1/255, the wave-uniform v5 / v6 forwards perform composite_fwd's pixel update (v6 retiring finished
-    pixels by a NaN row offset instead of a negated T), and the predicated backward
-    body performs the same operations as the branchy one, and a tile composited in 4 or 2 row-strip parts
-    (the default at this size) or whole (with a 5 % share of split heavy tiles) gives the same pixels and
-    contributor counts, the v5 backward's n_contrib strip bounds only skip strips and compares that cannot
-    contribute, and the v6 backward's select-predicated update leaves every accumulator bitwise unchanged on the
-    lanes it masks, and the union walk (bwd_union: pairs formed only from instances that reach a strip) gives each
-    instance the same reduction tree whatever its partner: outputs and gradients must match bit for bit (with a
-    non-zero background).  The v3
-    backward keeps the per-channel accumulators, and the parts backward adds its waves' per-instance sums:
-    gradients agree to rounding only."""
+    """Every composite launch shape gives the same bits: a tile composited whole (4 pixels per lane) or in 2 / 4
+    row-strip parts gives the same pixels and contributor counts; strip skipping (row-band or exact column-band
+    masks) only skips strips where every pixel fails alpha >= 1/255; the backward's n_contrib strip bounds only
+    skip strips and compares that cannot contribute; the union walk (pairs formed only from instances that reach a
+    strip) gives each instance the same reduction tree whatever its partner.  Outputs and gradients must match bit
+    for bit (with a non-zero background).  The parts backward adds its waves' per-instance sums: gradients agree to
+    rounding only."""
     from gaussian_splatting_lightning_amd import _native
     inp = scene_inputs(200_000, 1280, 720, sh_degree=3, seed=4, bg=(0.3, 0.6, 0.9))
     dc, di = upstream(1280, 720, 4)
+    defaults = {"fwd_parts": 0, "fwd_whole_waves": 8, "strip_exact": 1, "bwd_lastc": 0, "bwd_parts": 0,
+                "bwd_union": -1}
     try:
         _native.set_tuning("bwd_parts", 1)  # the reference side: one wave per tile (the default here is 2)
         ref = run_hip(inp, gpu_device, dc, di)
@@ -451,14 +515,12 @@ def test_composite_variants_are_bitwise_identical(gpu_device, knobs):
         alt = run_hip(inp, gpu_device, dc, di)
     finally:
         for k in knobs:
-            _native.set_tuning(k, {"fwd_strip": 0, "fwd_parts": 0, "bwd_strip": 1, "bwd_pred": 2, "bwd_v": 5,
-                                   "bwd_pair": 1, "bwd_parts": 0, "fwd_v": 6, "fwd_strip_parts": 1,
-                                   "strip_exact": 1, "bwd_lastc": 0, "bwd_union": -1}[k])
+            _native.set_tuning(k, defaults[k])
         _native.set_tuning("bwd_parts", 0)
     for k in ("color", "invdepth", "radii"):
         assert np.array_equal(ref[k], alt[k]), k
     for k in GRADS:
-        if knobs.get("bwd_v") == 3 or "bwd_parts" in knobs:
+        if "bwd_parts" in knobs:
             assert rel_l2(alt["grads"][k], ref["grads"][k]) <= 1e-5, k
         else:
             assert np.array_equal(ref["grads"][k], alt["grads"][k]), k
@@ -486,7 +548,7 @@ def test_long_tiles_and_depth_ties(gpu_device, n, W, H):
         assert n_tile.max() > 2048 and np.any((n_tile > 511) & (n_tile <= 2048))
     else:
         assert n_tile.max() > 8192
-    compare_backward(hip, run, dc, di, 1e-3)
+    compare_backward(hip, run, dc, di, 2e-6)  # achieved 7.8e-7
 
 
 def test_dense_tiles_fall_back_to_radix_after_speculative_count(gpu_device):
@@ -501,7 +563,7 @@ def test_dense_tiles_fall_back_to_radix_after_speculative_count(gpu_device):
     T = ((W + 15) // 16) * ((H + 15) // 16)
     assert hip["state"].num_rendered > 1024 * T  # the radix path was chosen
     run = compare_forward(inp, hip, run_oracle(inp))
-    compare_backward(hip, run, dc, di, 1e-3)
+    compare_backward(hip, run, dc, di, 2e-6)  # achieved 8.8e-7
     try:
         _native.set_tuning("bucket", 2)
         forced = run_hip(inp, gpu_device, dc, di)
@@ -545,7 +607,7 @@ def test_beyond_lpt_and_bucket_tile_limits(gpu_device):
     dc, di = upstream(4160, 2336, 31)
     hip = run_hip(inp, gpu_device, dc, di)
     run = compare_forward(inp, hip, run_oracle(inp))
-    compare_backward(hip, run, dc, di, 1e-3)
+    compare_backward(hip, run, dc, di, 2e-4)  # achieved 1.0e-4 (threshold flips; 6.4e-7 over the untouched Gaussians)
 
 
 @pytest.mark.parametrize("bucket", [0, 1])
