@@ -34,7 +34,7 @@ COLOR_TOL = 3e-6     # |colour|, |inverse depth| (relative to max(1, |v|)) on ev
 FLIP_TOL = 2e-2      # anywhere (one alpha = 1/255 or T = 1e-4 flip moves a pixel by < alpha T); achieved <= 3.4e-3
 GRAD_CLEAN_TOL = 5e-6  # gradient rel-L2 over the Gaussians no flip candidate touches; achieved <= 1.95e-6
                        # (A13 asks ~1e-4)
-GRAD_TOL_ADHOC = 1e-3  # the few cases checked without flip separation (precomputed inputs, the autograd API)
+GRAD_TOL_ADHOC = 2e-6  # cases checked without flip separation (precomputed inputs, the autograd API); achieved 6.2e-7
 
 
 def _case():
@@ -354,7 +354,7 @@ def test_cfg4_eight_views_full_size(gpu_device):
     forward + compact backward, and the multi-view sums the one-view-per-GPU exchange forms (the
     summed gradients == the sum of the 8 single-view gradients).  The 11 non-SH gradient columns are summed per
     view, dL/dshs is expanded once from the 8 views' colour factors and camera positions (gsr_sh_backward_views);
-    both match the oracle's per-view gradients summed in float64 within 1e-3 relative L2."""
+    both match the oracle's per-view gradients summed in float64 within 1e-4 relative L2."""
     from gaussian_splatting_lightning_amd.rasterizer import backward_raw, forward_raw, sh_backward_views
     W, H, V = 1920, 1080, 8
     keys = ("means3D", "opacities", "scales", "rotations")
@@ -380,8 +380,8 @@ def test_cfg4_eight_views_full_size(gpu_device):
     hip_sum["shs"] = sh_backward_views(t["means3D"], torch.stack(camposes), torch.stack(factors), 3, 16).cpu().numpy()
     rec = {k: rel_l2(hip_sum[k].reshape(ora_sum[k].shape), ora_sum[k]) for k in keys + ("shs",)}
     parity.record(_case(), "backward_view_sums", rec)
-    for k, e in rec.items():
-        assert e <= 1e-3, (k, e)
+    for k, e in rec.items():  # achieved 4.4e-5 (rotations): eight views' threshold flips
+        assert e <= 1e-4, (k, e)
 
 
 def test_exact_culling_is_bitwise_invisible(gpu_device):
