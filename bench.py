@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"))
     ap.add_argument("--exchange", default="compact", choices=("compact", "dense"),
                     help="N>1 gradient exchange (gaussian_splatting_lightning_amd/multiview.py)")
+    ap.add_argument("--exchange-chunks", type=int, default=4,
+                    help="N>1: Gaussian chunks whose exchange overlaps the rest of the backward (1: after it)")
     return ap.parse_args()
 
 
@@ -80,7 +82,8 @@ def main():
     import torch.distributed as dist
 
     from gaussian_splatting_lightning_amd import _native
-    from gaussian_splatting_lightning_amd.rasterizer import GaussianRasterizationSettings, backward_raw, forward_raw
+    from gaussian_splatting_lightning_amd.rasterizer import (GaussianRasterizationSettings, backward_chunked,
+                                                             backward_raw, forward_raw)
     from gaussian_splatting_lightning_amd.multiview import ViewGradReducer
     from gaussian_splatting_lightning_amd.synthetic import make_camera, make_scene, make_upstream
 
@@ -116,16 +119,23 @@ def main():
     # Per-Gaussian gradient destinations + the cross-rank exchange (multiview.py): one view per rank; dense
     # all-reduce at N=1 (nothing to exchange), compact SH exchange at N>1 unless --exchange dense.
     mode = args.exchange if world > 1 else "dense"
-    red = ViewGradReducer(n, M, deg, dev, mode=mode)
+    # N>1: the backward's per-Gaussian stage runs in --exchange-chunks Gaussian ranges and each range's collectives
+    # are issued as soon as it is enqueued (overlap with the rest of the backward); N=1: one chunk, nothing to send
+    red = ViewGradReducer(n, M, deg, dev, mode=mode, chunks=args.exchange_chunks if world > 1 else 1)
 
     def step():
         color, radii, invd, st = forward_raw(sc.means3D, sc.shs, None, sc.opacities, sc.scales, sc.rotations, None,
                                              settings)
         # densification statistics and max radii accumulate in the backward kernel; they are reduced over ranks
         # only when the model densifies (ViewGradReducer.sync_densify_stats), not every step
-        backward_raw(st, settings, dcolor, dinv, out=red.backward_out(), compact_sh=red.compact,
-                     accumulate_stats=True)
-        red.reduce(sc.means3D, c.campos)
+        if red.chunks == 1:
+            backward_raw(st, settings, dcolor, dinv, **red.backward_kwargs())
+            red.reduce(sc.means3D, c.campos)
+        else:
+            red.begin_step(c.campos)
+            backward_chunked(st, settings, dcolor, dinv, red.chunk_outputs(), on_chunk=red.start_chunk,
+                             compact_sh=red.compact, accumulate_stats=True)
+            red.finish(sc.means3D)
         return st
 
     # ---- warmup ----
@@ -305,7 +315,8 @@ def main():
         "warmup": args.warmup, "warmup_settle_s": SETTLE_S, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": cfg["desc"], "gaussians": n, "width": W, "height": H, "sh_degree": deg,
-                   "views_per_step": world, "parallelism": f"dp{world} (one view per GPU, RCCL gradient exchange: {mode})",
+                   "views_per_step": world, "parallelism": f"dp{world} (one view per GPU, RCCL gradient exchange: {mode}, "
+                                                  f"{red.chunks} overlapped chunk(s))",
                    "instances_per_view": I, "sum_n_contrib": sum_contrib,
                    "stage_events": (f"timed steps: dominant kernel only, every {EVENT_EVERY}th step; stages_ms: "
                                     "separate untimed pass"

@@ -42,7 +42,11 @@ class BackwardArgs(ctypes.Structure):
         ("dL_dcolors_sh", _fp),
         ("densify_stats", _fp),
         ("densify_accumulate", ctypes.c_int), ("max_radii2D", _fp),
+        ("stages", ctypes.c_int), ("g_begin", ctypes.c_int64), ("g_end", ctypes.c_int64), ("bwd_scratch", _fp),
     ]
+
+
+GSR_BWD_ALL, GSR_BWD_COMPOSITE, GSR_BWD_GAUSSIANS = 0, 1, 2
 
 
 class AdamGroup(ctypes.Structure):

@@ -585,9 +585,15 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     if (!a->dL_dpix || !a->radii) return fail(GSR_ERR_ARG, "dL_dpix and radii are required");
     if (!a->geom_buffer || !a->image_buffer || (a->R > 0 && !a->binning_buffer))
         return fail(GSR_ERR_ARG, "forward buffers are required");
-    if (a->shs && a->M > 0 && !a->dL_dsh && !a->dL_dcolors_sh)
+    if (a->stages != GSR_BWD_COMPOSITE && a->shs && a->M > 0 && !a->dL_dsh && !a->dL_dcolors_sh)
         return fail(GSR_ERR_ARG, "dL_dsh (or dL_dcolors_sh) is required when shs are given");
     if (a->R < 0 || a->R > 0xffffffffLL) return fail(GSR_ERR_ARG, "bad num_rendered");
+    if (a->stages < GSR_BWD_ALL || a->stages > GSR_BWD_GAUSSIANS) return fail(GSR_ERR_ARG, "bad backward stages");
+    int64_t g0 = a->g_begin, g1 = a->g_end;
+    if (g0 == 0 && g1 == 0) g1 = a->P;
+    if (g0 < 0 || g1 < g0 || g1 > a->P) return fail(GSR_ERR_ARG, "bad Gaussian range [g_begin, g_end)");
+    if (a->stages == GSR_BWD_GAUSSIANS && a->R > 0 && !a->bwd_scratch)
+        return fail(GSR_ERR_ARG, "GSR_BWD_GAUSSIANS needs the bwd_scratch of the GSR_BWD_COMPOSITE call");
     hipStream_t stream = (hipStream_t)stream_ptr;
     StreamDeviceGuard device_guard(stream);
     const bool dbg = a->debug != 0;
@@ -604,15 +610,16 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     carve_image(a->image_buffer, W, H, im);
     if (a->num_big < 0 || a->num_big > a->P) return fail(GSR_ERR_ARG, "bad num_big");
     const uint32_t nbig = (uint32_t)a->num_big;
-    char *scratch = alloc(alloc_ctx, GSR_BUF_BWD_SCRATCH, bwd_scratch_bytes(R, nbig));
-    if (!scratch) return fail(GSR_ERR_ALLOC, "backward scratch allocation failed");
+    char *scratch = a->stages == GSR_BWD_GAUSSIANS ? a->bwd_scratch
+                                                   : alloc(alloc_ctx, GSR_BUF_BWD_SCRATCH, bwd_scratch_bytes(R, nbig));
+    if (!scratch && a->stages != GSR_BWD_GAUSSIANS) return fail(GSR_ERR_ALLOC, "backward scratch allocation failed");
     float *rows = reinterpret_cast<float *>(scratch);
     // Gaussian-major gradient rows: render_bwd scatters its 40-B rows to the instances' expansion indices so
     // the per-Gaussian gather in preprocess_bwd reads each Gaussian's rows contiguously.
     const int rows_by_u = tuning("rows_by_u", 1);
     float *bigsum = bwd_bigsum_ptr(scratch, R);
 
-    if (R > 0) {
+    if (R > 0 && a->stages != GSR_BWD_GAUSSIANS) {
         RenderBwdParams rp;
         rp.W = W; rp.H = H; rp.gx = gx; rp.gy = gy; rp.num_tiles = (int)T; rp.num_rendered = R;
         rp.ranges = im.ranges; rp.point_list = b.point_list; rp.n_contrib = im.n_contrib;
@@ -633,8 +640,16 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
         bp.inv = b.inv; bp.rows = rows; bp.bigsum = bigsum; bp.rows_by_u = rows_by_u;
         GSR_STAGE(ST_BIG_REDUCE, dbg, launch_big_reduce(stream, bp, nbig));
     }
+    if (a->stages == GSR_BWD_COMPOSITE) return GSR_OK;
+    // Chunk-relative outputs (a split backward) address Gaussian g0's row: shift them so the kernel indexes every
+    // output by the absolute Gaussian index (integer arithmetic: the shifted address is never dereferenced)
+    auto rel = [g0](auto *ptr, int64_t width) -> decltype(ptr) {
+        if (!ptr || g0 == 0) return ptr;
+        return reinterpret_cast<decltype(ptr)>(reinterpret_cast<uintptr_t>(ptr) - (uintptr_t)(g0 * width) * sizeof(*ptr));
+    };
     PreprocessBwdParams pp;
     pp.P = P; pp.D = a->D; pp.M = a->M; pp.W = W; pp.H = H;
+    pp.g0 = (int)g0; pp.g1 = (int)g1;
     pp.tan_fovx = a->tan_fovx; pp.tan_fovy = a->tan_fovy;
     pp.focal_x = W / (2.0f * a->tan_fovx);
     pp.focal_y = H / (2.0f * a->tan_fovy);
@@ -651,17 +666,19 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     pp.rows = rows;
     pp.sh_vec16 = pp.shs && a->M == 16 && (((uintptr_t)pp.shs | (uintptr_t)a->dL_dsh) & 15) == 0 &&
                   tuning("sh_vec16", 1);
-    pp.dL_dmeans2D = a->dL_dmeans2D; pp.dL_dcolors = a->dL_dcolors; pp.dL_dopacity = a->dL_dopacity;
-    pp.dL_dmeans3D = a->dL_dmeans3D; pp.dL_dcov3D = a->dL_dcov3D; pp.dL_dsh = a->dL_dsh;
-    pp.dL_dcolors_sh = a->dL_dcolors_sh;
-    pp.densify_stats = a->densify_stats;
+    pp.dL_dmeans2D = rel(a->dL_dmeans2D, 3); pp.dL_dcolors = rel(a->dL_dcolors, 3);
+    pp.dL_dopacity = rel(a->dL_dopacity, 1); pp.dL_dmeans3D = rel(a->dL_dmeans3D, 3);
+    pp.dL_dcov3D = rel(a->dL_dcov3D, 6); pp.dL_dsh = rel(a->dL_dsh, (int64_t)a->M * 3);
+    pp.dL_dcolors_sh = rel(a->dL_dcolors_sh, 3);
+    pp.densify_stats = rel(a->densify_stats, 2);
     pp.densify_accumulate = a->densify_accumulate;
-    pp.max_radii2D = a->max_radii2D;
-    pp.dL_dscales = a->dL_dscales; pp.dL_drot = a->dL_drotations;
+    pp.max_radii2D = rel(a->max_radii2D, 1);
+    pp.dL_dscales = rel(a->dL_dscales, 3); pp.dL_drot = rel(a->dL_drotations, 4);
+    const size_t ng = (size_t)(g1 - g0);
     if (pp.shs == nullptr && a->dL_dsh && a->M > 0)
-        GSR_HIP(hipMemsetAsync(a->dL_dsh, 0, sizeof(float) * (size_t)P * a->M * 3, stream));
+        GSR_HIP(hipMemsetAsync(a->dL_dsh, 0, sizeof(float) * ng * a->M * 3, stream));
     if (pp.shs == nullptr && a->dL_dcolors_sh)
-        GSR_HIP(hipMemsetAsync(a->dL_dcolors_sh, 0, sizeof(float) * (size_t)P * 3, stream));
+        GSR_HIP(hipMemsetAsync(a->dL_dcolors_sh, 0, sizeof(float) * ng * 3, stream));
     GSR_STAGE(ST_PREPROCESS_BWD, dbg, launch_preprocess_bwd(stream, pp));
     return GSR_OK;
 }

@@ -162,6 +162,8 @@ void launch_big_reduce(hipStream_t s, const BigReduceParams &p, uint32_t nbig);
 
 struct PreprocessBwdParams {
     int P, D, M, W, H;
+    int g0, g1;  // Gaussians [g0, g1) (the whole [0, P) unless the backward is split into chunks); every output pointer
+                 // is indexed by the absolute Gaussian index (the API pre-offsets chunk-relative ones)
     float tan_fovx, tan_fovy, focal_x, focal_y, scale_modifier;
     int antialiasing, has_invdepth;
     int sh_vec16;  // M == 16 and shs / dL_dsh 16-byte aligned: vectorised SH path

@@ -293,17 +293,17 @@ constexpr int SH_STRIDE = 52;
 constexpr int PBWD_STAGE = 32 * SH_STRIDE;  // floats of LDS per wave
 template <bool LDS_SH>
 __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams p) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int i = p.g0 + blockIdx.x * 256 + threadIdx.x;
     if (!LDS_SH) {
         const float none[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         float3 d3, v3;
-        if (i < p.P) preprocess_bwd_one<false>(p, i, false, none, d3, v3);
+        if (i < p.g1) preprocess_bwd_one<false>(p, i, false, none, d3, v3);
         return;
     }
     __shared__ __attribute__((aligned(16))) float s_sh[4][PBWD_STAGE];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const size_t gbase = ((size_t)blockIdx.x * 256 + (size_t)w * 64) * 48;  // first float of the wave's block
-    const size_t gend = (size_t)p.P * 48;
+    const size_t gbase = ((size_t)p.g0 + (size_t)blockIdx.x * 256 + (size_t)w * 64) * 48;  // the wave's first float
+    const size_t gend = (size_t)p.g1 * 48;
     float *sw = s_sh[w];
     // Gradient rows of the wave's 64 Gaussians (rows_by_u: each Gaussian's rows are contiguous), gathered
     // jointly: the (Gaussian, row) pairs of all lanes are enumerated in order, every lane loads the inv words of
@@ -313,7 +313,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
     // take their block-reduced sum in preprocess_bwd_one.
     float gs[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (p.rows_by_u) {
-        const bool vis = i < p.P && p.radii[i] > 0;
+        const bool vis = i < p.g1 && p.radii[i] > 0;
         const uint32_t cnt = vis ? p.tiles[i] : 0u;
         const uint32_t len = cnt <= BIG_GAUSSIAN_TILES ? cnt : 0u;
         const uint32_t incl = wave_inclusive_scan(len, lane);
@@ -368,7 +368,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         }
     }
     float3 dRGB = make_float3(0.f, 0.f, 0.f), dir = make_float3(1.f, 0.f, 0.f);
-    if (i < p.P) preprocess_bwd_one<true>(p, i, p.rows_by_u != 0, gs, dRGB, dir);
+    if (i < p.g1) preprocess_bwd_one<true>(p, i, p.rows_by_u != 0, gs, dRGB, dir);
     if (!p.dL_dsh) return;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
@@ -387,11 +387,12 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
 }
 
 void launch_preprocess_bwd(hipStream_t s, const PreprocessBwdParams &p) {
-    if (p.P <= 0) return;
+    if (p.g1 <= p.g0) return;
+    const uint32_t grid = div_up((uint32_t)(p.g1 - p.g0), 256);
     if (p.sh_vec16 && tuning("pbwd_lds_sh", 1))
-        preprocess_bwd_kernel<true><<<div_up(p.P, 256), 256, 0, s>>>(p);
+        preprocess_bwd_kernel<true><<<grid, 256, 0, s>>>(p);
     else
-        preprocess_bwd_kernel<false><<<div_up(p.P, 256), 256, 0, s>>>(p);
+        preprocess_bwd_kernel<false><<<grid, 256, 0, s>>>(p);
 }
 
 }  // namespace gsr

@@ -248,6 +248,68 @@ def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_
         cov3D_precomp=dcov if st.cov3D_precomp is not None else None, cov3D=dcov)
 
 
+def backward_chunked(state: ForwardState, raster_settings, grad_out_color, grad_out_depth, chunks, on_chunk=None,
+                     compact_sh=False, accumulate_stats=False):
+    """The backward split so that a gradient exchange overlaps it (multiview.py): ONE gsr_backward call for the
+    compositing backward (GSR_BWD_COMPOSITE: instance gradient rows into a scratch buffer kept here), then one call
+    per Gaussian chunk for the per-Gaussian stage (GSR_BWD_GAUSSIANS), each followed by on_chunk(k) -- which may
+    issue collectives on the chunk's finished gradients while the next chunks compute.
+
+    chunks: list of (g_begin, g_end, out) with out a dict of destinations for those Gaussians only (same keys and
+    row widths as backward_raw's `out`, (g_end - g_begin) rows each, contiguous float32; max_radii2D int32).
+    Results are bitwise those of one backward_raw call: every Gaussian is computed by the same code."""
+    lib = _native.load()
+    rs = raster_settings
+    st = state
+    device = st.means3D.device
+    P, M = st.means3D.shape[0], st.M
+    H, W = int(rs.image_height), int(rs.image_width)
+    grad_out_color = grad_out_color.to(torch.float32).contiguous()
+    if grad_out_depth is not None:
+        grad_out_depth = grad_out_depth.to(torch.float32).contiguous()
+    bufs = _Buffers(device)
+    base = dict(
+        P=P, D=int(rs.sh_degree), M=M, W=W, H=H, R=st.num_rendered, num_big=st.num_big, background=_ptr(st.bg),
+        means3D=_ptr(st.means3D), colors_precomp=_ptr(st.colors_precomp), opacities=_ptr(st.opacities),
+        scales=_ptr(st.scales), scale_modifier=float(rs.scale_modifier), rotations=_ptr(st.rotations),
+        cov3D_precomp=_ptr(st.cov3D_precomp), viewmatrix=_ptr(st.viewmatrix), projmatrix=_ptr(st.projmatrix),
+        campos=_ptr(st.campos), tan_fovx=float(rs.tanfovx), tan_fovy=float(rs.tanfovy),
+        dL_dpix=grad_out_color.data_ptr(), dL_dinvdepth=_ptr(grad_out_depth), shs=_ptr(st.shs),
+        radii=_ptr(st.radii), geom_buffer=_ptr(st.geom_buffer), binning_buffer=_ptr(st.binning_buffer),
+        image_buffer=_ptr(st.image_buffer), antialiasing=int(bool(rs.antialiasing)), debug=int(bool(rs.debug)),
+        densify_accumulate=int(bool(accumulate_stats)))
+    with torch.cuda.device(device):
+        a = _native.BackwardArgs(stages=_native.GSR_BWD_COMPOSITE, **base)
+        rc = lib.gsr_backward(ctypes.byref(a), bufs.callback, None, _stream_handle(device))
+        bufs.raise_pending()
+        _native.check(rc, "rasterize_gaussians_backward (composite)")
+        scratch = bufs.get(_native.GSR_BUF_BWD_SCRATCH)
+        widths = dict(means2D=3, colors=3, opacities=1, means3D=3, cov3D=6, shs=3 * max(M, 0), scales=3, rotations=4,
+                      colors_sh=3, densify_stats=2)
+        for k, (g0, g1, out) in enumerate(chunks):
+            n = int(g1) - int(g0)
+            for name, t in out.items():
+                want = (torch.int32, (n,)) if name == "max_radii2D" else (torch.float32, None)
+                if t.dtype != want[0] or not t.is_contiguous() or t.shape[0] != n or (
+                        name in widths and t.numel() != n * widths[name]):
+                    raise RuntimeError(f"chunk {k}: out[{name!r}] must be a contiguous {want[0]} tensor of {n} rows")
+            if compact_sh and "colors_sh" not in out and st.shs is not None:
+                raise RuntimeError("compact_sh needs out['colors_sh'] in every chunk")
+            a = _native.BackwardArgs(
+                stages=_native.GSR_BWD_GAUSSIANS, g_begin=int(g0), g_end=int(g1), bwd_scratch=_ptr(scratch),
+                dL_dmeans2D=_ptr(out.get("means2D")), dL_dcolors=_ptr(out.get("colors")),
+                dL_dopacity=_ptr(out.get("opacities")), dL_dmeans3D=_ptr(out.get("means3D")),
+                dL_dcov3D=_ptr(out.get("cov3D")), dL_dsh=None if compact_sh else _ptr(out.get("shs")),
+                dL_dscales=_ptr(out.get("scales")), dL_drotations=_ptr(out.get("rotations")),
+                dL_dcolors_sh=_ptr(out.get("colors_sh")), densify_stats=_ptr(out.get("densify_stats")),
+                max_radii2D=_ptr(out.get("max_radii2D")), **base)
+            rc = lib.gsr_backward(ctypes.byref(a), bufs.callback, None, _stream_handle(device))
+            _native.check(rc, f"rasterize_gaussians_backward (chunk {k})")
+            if on_chunk is not None:
+                on_chunk(k)
+    return scratch
+
+
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,

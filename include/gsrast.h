@@ -122,7 +122,21 @@ typedef struct gsr_backward_args {
      * steps; max_radii2D (P) int32, if non-NULL, becomes max(max_radii2D, radii) (gaussian_model.py:175-176). */
     int densify_accumulate;
     int *max_radii2D;
+    /* Split backward, so a gradient exchange can overlap the per-Gaussian stage (multiview.py; no counterpart in
+     * the reference, whose batch is one view):
+     *   stages = GSR_BWD_ALL (0): everything in one call;
+     *   GSR_BWD_COMPOSITE: the compositing backward and the big-Gaussian reduction only -- the per-instance gradient
+     *     rows land in the GSR_BUF_BWD_SCRATCH buffer, which the caller keeps for the next calls; no output written;
+     *   GSR_BWD_GAUSSIANS: the per-Gaussian stage only, over Gaussians [g_begin, g_end), reading the rows from
+     *     bwd_scratch (the GSR_BWD_COMPOSITE call's buffer).  Every output pointer then addresses Gaussian
+     *     g_begin's row (a slice of a full array, or a chunk-sized buffer).
+     * g_begin = g_end = 0 means the whole range [0, P) (any stage). */
+    int stages;
+    int64_t g_begin, g_end;
+    char *bwd_scratch;
 } gsr_backward_args;
+
+enum { GSR_BWD_ALL = 0, GSR_BWD_COMPOSITE = 1, GSR_BWD_GAUSSIANS = 2 };
 
 /* Replaces `_C.rasterize_gaussians_backward` (RasterizeGaussiansBackwardCUDA -> Rasterizer::backward).
  * Deterministic: per-tile gradient rows are reduced in fixed order (no float atomics). */

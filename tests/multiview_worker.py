@@ -37,23 +37,35 @@ def oracle_sh_views(means3D, campos, dcolors_sh, sh_degree, M, out):
     return out
 
 
-def worker(rank, world, port, mode, result_dir):
+def worker(rank, world, port, mode, result_dir, chunks=1):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from gaussian_splatting_lightning_amd.multiview import ViewGradReducer
         g = oracle_view(rank, world)
-        red = ViewGradReducer(N, 16, DEG, "cpu", mode=mode, sh_views_fn=oracle_sh_views)
-        out = red.backward_out()
-        for k in ("means3D", "scales", "rotations", "opacities", "means2D"):
-            out[k].copy_(torch.from_numpy(g[k]).reshape(out[k].shape))
-        if red.compact:
-            out["colors_sh"].copy_(torch.from_numpy(g["colors_sh"]))
-        else:
-            out["shs"].copy_(torch.from_numpy(g["shs"]))
+        red = ViewGradReducer(N, 16, DEG, "cpu", mode=mode, sh_views_fn=oracle_sh_views, chunks=chunks)
+        means3D = torch.from_numpy(g["means3D_in"])
+
+        def fill(out, g0, g1):  # what the backward writes for Gaussians [g0, g1)
+            for k in ("means3D", "scales", "rotations", "opacities"):
+                out[k].copy_(torch.from_numpy(g[k][g0:g1]).reshape(out[k].shape))
+            if red.compact:
+                out["colors_sh"].copy_(torch.from_numpy(g["colors_sh"][g0:g1]))
+            else:
+                out["shs"].copy_(torch.from_numpy(g["shs"][g0:g1]).reshape(out["shs"].shape))
+
+        red.means2D.copy_(torch.from_numpy(g["means2D"]))
+        if red.chunks == 1:
+            fill(red.backward_out(), 0, N)
+            red.reduce(means3D, torch.from_numpy(g["campos"]))
+        else:  # the overlapped form: each chunk's exchange starts as soon as its gradients exist
+            red.begin_step(torch.from_numpy(g["campos"]))
+            for c, (g0, g1, out) in enumerate(red.chunk_outputs()):
+                fill(out, g0, g1)
+                red.start_chunk(c)
+            red.finish(means3D)
         red.record_view(red.means2D, torch.from_numpy(g["radii"]))
-        red.reduce(torch.from_numpy(g["means3D_in"]), torch.from_numpy(g["campos"]))
         res = {k: v.numpy() for k, v in red.grads.items()}
         stats, radii_max = red.sync_densify_stats()
         res["stats"] = stats.numpy()

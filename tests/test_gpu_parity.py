@@ -678,3 +678,44 @@ def test_failed_scratch_allocation_is_a_clean_error(gpu_device, fail_buf, monkey
     assert np.array_equal(ref["color"], again["color"])
     for k in GRADS:
         assert np.array_equal(ref["grads"][k], again["grads"][k]), k
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_chunked_backward_is_bitwise_the_single_call(gpu_device, compact):
+    """backward_chunked (one compositing call, then the per-Gaussian stage over Gaussian ranges with chunk-relative
+    destinations -- the overlapped multi-GPU exchange's backward, multiview.py) writes bit for bit what one
+    backward_raw call writes, for ranges on and off the 256-Gaussian block grid, with the statistics accumulated."""
+    from gaussian_splatting_lightning_amd.rasterizer import backward_chunked, backward_raw, forward_raw
+    n, W, H = 30_000, 320, 240
+    inp = scene_inputs(n, W, H, sh_degree=3, seed=12, stress_fraction=0.01)
+    rs = settings_for(inp, gpu_device)
+    t = {k: torch.as_tensor(inp[k], device=gpu_device) for k in ("means3D", "opacities", "scales", "rotations", "shs")}
+    dc, di = (torch.as_tensor(a, device=gpu_device) for a in upstream(W, H, seed=12))
+    _, radii, _, st = forward_raw(t["means3D"], t["shs"], None, t["opacities"], t["scales"], t["rotations"], None, rs)
+    assert st.num_big > 0  # the big-Gaussian reduction feeds the chunks too
+    stats = torch.ones(n, 2, device=gpu_device)
+    mrad = torch.full((n,), 2, dtype=torch.int32, device=gpu_device)
+    ref = backward_raw(st, rs, dc, di, out={"densify_stats": stats, "max_radii2D": mrad}, compact_sh=compact,
+                       accumulate_stats=True)
+    widths = dict(means3D=3, scales=3, rotations=4, opacities=1, means2D=3)
+    if compact:
+        widths["colors_sh"] = 3
+    else:
+        widths["shs"] = 48
+    bounds = [0, 256, 1000, 7777, 20_480, n]
+    chunks, seen = [], []
+    stats2 = torch.ones(n, 2, device=gpu_device)
+    mrad2 = torch.full((n,), 2, dtype=torch.int32, device=gpu_device)
+    for g0, g1 in zip(bounds[:-1], bounds[1:]):
+        out = {k: torch.full((g1 - g0, w), float("nan"), device=gpu_device) for k, w in widths.items()}
+        out["densify_stats"] = stats2[g0:g1]
+        out["max_radii2D"] = mrad2[g0:g1]
+        chunks.append((g0, g1, out))
+    backward_chunked(st, rs, dc, di, chunks, on_chunk=seen.append, compact_sh=compact, accumulate_stats=True)
+    torch.cuda.synchronize()
+    assert seen == list(range(len(chunks)))
+    for k in widths:
+        got = torch.cat([o[k] for _, _, o in chunks], 0)
+        want = ref[k].reshape(n, -1)
+        assert torch.equal(got, want), k
+    assert torch.equal(stats2, stats) and torch.equal(mrad2, mrad)
