@@ -100,7 +100,7 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
         return;
     }
     if (SCATTER) {
-        const uint32_t *hrow = p.hist + (size_t)b * T;
+        const uint32_t *hrow = p.hist_pre + (size_t)b * T;
         for (uint32_t t = tid; t < T; t += 64 * BKW) s_tab[t] = p.tile_start[t] + hrow[t];
     } else {
         for (uint32_t t = tid; t < T; t += 64 * BKW) s_tab[t] = 0u;
@@ -200,8 +200,9 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// steps 2 and 3: column prefixes of the count matrix, tile totals, and the tile starts / ranges from a
-// decoupled look-back over the workgroups in tile order.  A workgroup owns 64 tile columns (one per lane); its
+// steps 2 and 3: column prefixes of the count matrix (into hist_pre), tile totals, and the tile starts / ranges
+// from a decoupled look-back over the workgroups in tile order (a column workgroup that has not published is
+// recomputed from the counts, wave_lookback).  A workgroup owns 64 tile columns (one per lane); its
 // four waves own four contiguous quarters of the block rows.  Workgroup ids come from an atomic ticket, so a
 // workgroup only waits on workgroups that started before it.  The long tiles are appended to two lists for
 // the workgroup sorts: list 0 holds tiles of (SEG_CAP, SEG_BLOCK_CAP] instances, list 1 longer ones.
@@ -210,7 +211,8 @@ __global__ __launch_bounds__(256) void bk_columns_kernel(BucketParams p) {
     __shared__ uint32_t s_sum[4][64];
     __shared__ uint32_t s_bid;
     __shared__ unsigned long long s_excl;
-    uint32_t *__restrict__ hist = p.hist;
+    const uint32_t *__restrict__ hist = p.hist;
+    uint32_t *__restrict__ hist_pre = p.hist_pre;
     const uint32_t nb = p.nb, T = p.T;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     if (tid == 0) s_bid = atomicAdd(p.ticket, 1u);
@@ -235,8 +237,16 @@ __global__ __launch_bounds__(256) void bk_columns_kernel(BucketParams p) {
     const uint32_t tot = s_sum[0][lane] + s_sum[1][lane] + s_sum[2][lane] + s_sum[3][lane];  // tile total
     if (w == 0) {
         const uint32_t inc = wave_inclusive_scan(tot, lane);
+        // fallback aggregate of column workgroup q: its 64 tiles' totals, summed from the (read-only) counts
+        auto agg_of = [&](uint32_t q) -> uint64_t {
+            const uint32_t tq = q * 64 + lane;
+            uint64_t v = 0;
+            if (tq < T)
+                for (uint32_t r = 0; r < nb; r++) v += hist[(size_t)r * T + tq];
+            return wave_sum_u64(v);
+        };
         const uint64_t excl = wave_lookback(p.tile_status, bid, (uint64_t)__builtin_amdgcn_readlane((int)inc, 63),
-                                            lane, p.err);
+                                            lane, p.err, p.lb_patience, p.lb_force != 0, agg_of);
         if (t < T) {
             const uint32_t st = (uint32_t)(excl + inc - tot);
             p.tile_start[t] = st;
@@ -269,13 +279,13 @@ __global__ __launch_bounds__(256) void bk_columns_kernel(BucketParams p) {
             for (int i = 0; i < 8; i++) v[i] = hist[(size_t)(r + i) * T + t];
 #pragma unroll
             for (int i = 0; i < 8; i++) {
-                hist[(size_t)(r + i) * T + t] = run;
+                hist_pre[(size_t)(r + i) * T + t] = run;
                 run += v[i];
             }
         }
         for (; r < r1; r++) {
             const uint32_t v = hist[(size_t)r * T + t];
-            hist[(size_t)r * T + t] = run;
+            hist_pre[(size_t)r * T + t] = run;
             run += v;
         }
     }

@@ -203,6 +203,8 @@ struct ImageState {
     // bucket path count-pass scratch (gsr_bin.hip), here rather than in the binning buffer so that the pass
     // can run before the instance total (the binning buffer's size) reaches the host
     uint32_t *bk_hist;       // BK_MAX_BLOCKS x T count matrix (empty above BK_MAX_TILES)
+    uint32_t *bk_hist_pre;   // its column prefixes (a separate array: the counts stay readable for the look-back's
+                             // fallback while later column workgroups run)
     uint32_t *bk_tile_cnt;   // T
     uint32_t *bk_tile_start; // T + 1
     uint32_t *bk_long_list;  // 2 x (T + 1): tiles of (SEG_CAP, SEG_BLOCK_CAP] instances, longer tiles
@@ -222,6 +224,7 @@ inline size_t carve_image(char *base, int W, int H, ImageState &im) {
     im.order_bwd = c.take<uint32_t>((size_t)gx * gy + 1);
     const size_t nt = (size_t)gx * gy;
     im.bk_hist = c.take<uint32_t>((nt <= BK_MAX_TILES ? (size_t)BK_MAX_BLOCKS * nt : 0) + 1);
+    im.bk_hist_pre = c.take<uint32_t>((nt <= BK_MAX_TILES ? (size_t)BK_MAX_BLOCKS * nt : 0) + 1);
     im.bk_tile_cnt = c.take<uint32_t>(nt + 1);
     im.bk_tile_start = c.take<uint32_t>(nt + 1);
     im.bk_long_list = c.take<uint32_t>(2 * (nt + 1));
@@ -615,13 +618,20 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v, int lane) {
 
 __device__ __forceinline__ uint64_t lanemask_lt(int lane) { return (lane == 0) ? 0ull : (~0ull >> (64 - lane)); }
 
-// Decoupled look-back by one whole wave: publishes the block's aggregate, then sums predecessors' words 64 at a
-// time (nearest first) up to the first inclusive prefix, and publishes its own inclusive prefix.  Returns the
-// block's exclusive prefix (every lane).  Status words: 2-bit flag | 62-bit value, zero = not yet published.
-// Block ids must follow start order (atomic ticket).  A chain that never completes sets bit 1 of *err.
+// Decoupled look-back by one whole wave, with decoupled fallback: publishes the block's aggregate, then sums
+// predecessors' words 64 at a time (nearest first) up to the first inclusive prefix, and publishes its own
+// inclusive prefix.  Returns the block's exclusive prefix (every lane).  Status words: 2-bit flag | 62-bit value,
+// zero = not yet published.  Block ids follow start order (atomic ticket).
+// A predecessor that has not published within `patience` polls -- a block that is not running, e.g. preempted --
+// is not waited for: its aggregate is recomputed from the kernel's input by agg_of(q) (a wave-cooperative call
+// returning the same value that block would publish; the inputs are never written by the kernel), so the chain
+// always completes with the same result (the "decoupled fallback" of Smith, Levien & Owens).  With `force` every
+// status word is ignored and every predecessor recomputed (the test of the fallback).  Bit 2 of *err records that
+// a fallback ran (diagnostic only: the output is exact either way).
 constexpr uint64_t SLB_AGG = 1ull << 62, SLB_INC = 2ull << 62, SLB_MASK = (1ull << 62) - 1;
+template <class AggOf>
 __device__ __forceinline__ uint64_t wave_lookback(uint64_t *status, uint32_t bid, uint64_t agg, int lane,
-                                                  uint32_t *err) {
+                                                  uint32_t *err, uint32_t patience, bool force, AggOf agg_of) {
     if (lane == 0)
         __hip_atomic_store(status + bid, (bid == 0 ? SLB_INC : SLB_AGG) | agg, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -630,19 +640,25 @@ __device__ __forceinline__ uint64_t wave_lookback(uint64_t *status, uint32_t bid
     uint32_t spins = 0;
     while (look >= 0) {
         const int64_t q = look - lane;
-        const uint64_t sv =
-            q >= 0 ? __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : SLB_INC;
-        const uint64_t flag = sv & ~SLB_MASK;
-        const uint64_t inc_mask = __ballot(flag == SLB_INC);
+        uint64_t sv = q < 0 ? SLB_INC
+                            : force ? 0ull : __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t inc_mask = __ballot((sv & ~SLB_MASK) == SLB_INC);
         const int first = inc_mask ? __builtin_ctzll(inc_mask) : 64;
         const uint64_t upto = first < 63 ? ((2ull << first) - 1) : ~0ull;
-        if (__ballot(flag == 0) & upto) {  // a predecessor in the window has not published yet
-            if (++spins > (1u << 24)) {
-                if (lane == 0) atomicOr(err, 2u);
-                break;
+        uint64_t unpub = __ballot((sv & ~SLB_MASK) == 0) & upto;
+        if (unpub) {  // a predecessor in the window has not published yet
+            if (!force && ++spins <= patience) {
+                __builtin_amdgcn_s_sleep(1);
+                continue;
             }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
+            if (lane == 0) atomicOr(err, 4u);
+            while (unpub) {  // recompute those aggregates, nearest first (wave-uniform loop)
+                const int j = __builtin_ctzll(unpub);
+                unpub &= unpub - 1;
+                const uint64_t v = agg_of((uint32_t)(look - j));
+                if (lane == j) sv = SLB_AGG | v;
+            }
+            spins = 0;
         }
         uint64_t part = (lane <= first) ? (sv & SLB_MASK) : 0ull;
 #pragma unroll
@@ -654,6 +670,13 @@ __device__ __forceinline__ uint64_t wave_lookback(uint64_t *status, uint32_t bid
     if (lane == 0 && bid > 0)
         __hip_atomic_store(status + bid, SLB_INC | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return excl;
+}
+
+// wave-uniform 64-bit sum of one value per lane
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
 }
 
 // Wave timeline stamp (diagnostics): 100 MHz real-time clock at start / end, HW_ID and XCC_ID registers.

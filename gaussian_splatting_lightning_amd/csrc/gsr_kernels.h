@@ -82,7 +82,8 @@ struct BucketParams {
     const uint32_t *block_sums;  // preprocess block totals (256 Gaussians each)
     uint32_t *inst_start;  // P + 1: written by the count pass (Gaussian-order exclusive scan of tiles)
     const uint4 *exp_rec;
-    uint32_t *hist;        // nb x T counts, then column prefixes
+    uint32_t *hist;        // nb x T counts (the count pass writes them; read-only for the column pass)
+    uint32_t *hist_pre;    // nb x T column prefixes (column pass), seeding the scatter's bucket slots
     uint32_t *tile_cnt;    // T
     uint32_t *tile_start;  // T + 1
     uint2 *ranges;         // T
@@ -90,7 +91,9 @@ struct BucketParams {
     uint32_t *long_cnt;    // 2 counts (zeroed)
     uint32_t *ticket;      // zeroed: column-pass workgroup ticket
     uint64_t *tile_status; // zeroed: div_up(T, 64) look-back words of the column pass
-    uint32_t *err;         // look-back failure flag
+    uint32_t *err;         // look-back flags (bit 2: a decoupled fallback ran; diagnostic)
+    uint32_t lb_patience;  // look-back polls before recomputing an unpublished predecessor
+    int lb_force;          // recompute every predecessor (tests the fallback)
     uint32_t *tile_last, *tile_loaded;  // T each: cleared by the column pass for the forward composite
     unsigned long long *keys;  // R: depth << 32 | u, bucketed by tile
     uint32_t *inst_gid;    // R

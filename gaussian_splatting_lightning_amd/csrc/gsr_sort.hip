@@ -136,7 +136,8 @@ __global__ __launch_bounds__(256) void scan_lookback_kernel(const uint32_t *__re
                                                             const uint32_t *__restrict__ idx, uint32_t n,
                                                             uint32_t *__restrict__ out, uint64_t *__restrict__ status,
                                                             uint32_t *__restrict__ ticket,
-                                                            uint32_t *__restrict__ overflow) {
+                                                            uint32_t *__restrict__ flags, uint32_t patience,
+                                                            int force) {
     constexpr int PER = SCAN_TILE / 256;
     __shared__ uint32_t s_bid, s_w[4];
     __shared__ unsigned long long s_excl;
@@ -158,43 +159,20 @@ __global__ __launch_bounds__(256) void scan_lookback_kernel(const uint32_t *__re
     __syncthreads();
     if (w == 0) {
         const uint64_t agg = (uint64_t)s_w[0] + s_w[1] + s_w[2] + s_w[3];
-        if (lane == 0)
-            __hip_atomic_store(status + bid, (bid == 0 ? SLB_INC : SLB_AGG) | agg, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        uint64_t excl = 0;
-        int64_t look = (int64_t)bid - 1;
-        uint32_t spins = 0;
-        while (look >= 0) {
-            const int64_t q = look - lane;
-            const uint64_t sv = q >= 0 ? __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                       : SLB_INC;
-            const uint64_t flag = sv & ~SLB_MASK;
-            const uint64_t inc_mask = __ballot(flag == SLB_INC);
-            const int first = inc_mask ? __builtin_ctzll(inc_mask) : 64;
-            const uint64_t upto = first < 63 ? ((2ull << first) - 1) : ~0ull;
-            if (__ballot(flag == 0) & upto) {  // a predecessor in the window has not published yet
-                if (++spins > (1u << 24)) {
-                    if (lane == 0) atomicOr(overflow, 2u);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-                continue;
-            }
-            uint64_t part = (lane <= first) ? (sv & SLB_MASK) : 0ull;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
-            excl += part;
-            if (first < 64) break;
-            look -= 64;
-        }
+        // fallback aggregate of block q: the sum of its SCAN_TILE inputs (the input is never written here)
+        auto agg_of = [&](uint32_t q) -> uint64_t {
+            uint64_t a = 0;
+            for (uint32_t j = q * SCAN_TILE + lane; j < min(n, (q + 1) * SCAN_TILE); j += 64)
+                a += scan_load<GATHER>(in, idx, j);
+            return wave_sum_u64(a);
+        };
+        const uint64_t excl = wave_lookback(status, bid, agg, lane, flags, patience, force != 0, agg_of);
         if (lane == 0) {
-            if (bid > 0)
-                __hip_atomic_store(status + bid, SLB_INC | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_excl = excl;
             if (base <= n && n < bid * SCAN_TILE + SCAN_TILE) {  // the block holding element n writes the total
                 const uint64_t tot = excl + agg;
                 out[n] = (uint32_t)tot;
-                if (tot > 0xffffffffull) atomicOr(overflow, 1u);
+                if (tot > 0xffffffffull) atomicOr(flags, 1u);
             }
         }
     }
@@ -210,13 +188,15 @@ __global__ __launch_bounds__(256) void scan_lookback_kernel(const uint32_t *__re
 }
 
 void launch_exclusive_scan_lookback(hipStream_t s, const uint32_t *in, const uint32_t *idx, uint32_t n, uint32_t *out,
-                                    uint64_t *status, uint32_t *ticket, uint32_t *overflow_flag) {
+                                    uint64_t *status, uint32_t *ticket, uint32_t *flags) {
     // status (div_up(n + 1, SCAN_TILE) words) and *ticket must be zero (cleared with the forward's counters)
     const uint32_t nb = div_up(n + 1, (uint32_t)SCAN_TILE);
+    const uint32_t pat = (uint32_t)tuning("lb_patience", 1 << 16);
+    const int force = tuning("lb_force", 0);
     if (idx)
-        scan_lookback_kernel<true><<<nb, 256, 0, s>>>(in, idx, n, out, status, ticket, overflow_flag);
+        scan_lookback_kernel<true><<<nb, 256, 0, s>>>(in, idx, n, out, status, ticket, flags, pat, force);
     else
-        scan_lookback_kernel<false><<<nb, 256, 0, s>>>(in, nullptr, n, out, status, ticket, overflow_flag);
+        scan_lookback_kernel<false><<<nb, 256, 0, s>>>(in, nullptr, n, out, status, ticket, flags, pat, force);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -376,7 +356,6 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restr
 // ids come from an atomic ticket).  3 + passes launches instead of 5 per pass.
 // ------------------------------------------------------------------------------------------------
 constexpr uint32_t LB_AGG = 1u << 30, LB_INC = 2u << 30, LB_MASK = (1u << 30) - 1;
-constexpr uint32_t LB_SPIN_LIMIT = 1u << 24;  // safety net: a broken chain raises an error, never hangs
 
 __device__ __forceinline__ uint32_t lb_load(const uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -463,7 +442,7 @@ __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__rest
                                                           uint32_t *__restrict__ status,
                                                           uint32_t *__restrict__ keys_out,
                                                           uint32_t *__restrict__ vals_out, uint4 *stamps,
-                                                          SortGather ga) {
+                                                          SortGather ga, uint32_t patience, int force) {
     __shared__ uint32_t s_cnt[4][RS_BINS];  // per-wave running digit counts, then per-wave bases
     __shared__ uint32_t s_dstart[RS_BINS];  // block-local start of each digit's run
     __shared__ uint32_t s_gbase[RS_BINS];   // global start of this block's run of each digit
@@ -542,17 +521,27 @@ __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__rest
                 uint32_t v[LBW];
 #pragma unroll
                 for (int i = 0; i < LBW; i++)
-                    v[i] = (look - i >= 0) ? lb_load(status + (size_t)(look - i) * RS_BINS + d) : LB_INC;
+                    v[i] = (look - i >= 0) ? (force ? 0u : lb_load(status + (size_t)(look - i) * RS_BINS + d)) : LB_INC;
+                // decoupled fallback (wave_lookback): after `patience` polls (at once with force) an unpublished
+                // predecessor's digit count is recounted from its keys, which this pass never writes
+                const bool fb = force || spins >= patience;
                 bool found = false, stalled = false;
                 int used = 0;
 #pragma unroll
                 for (int i = 0; i < LBW; i++) {
                     if (!found && !stalled) {
-                        const uint32_t f = v[i] & ~LB_MASK;
+                        uint32_t f = v[i] & ~LB_MASK, val = v[i] & LB_MASK;
+                        if (f == 0 && fb) {
+                            const uint32_t q = (uint32_t)(look - i), e = min(n, (q + 1) * TILE);
+                            val = 0;
+                            for (uint32_t j = q * TILE; j < e; j++) val += ((keys_in[j] >> shift) & 255u) == (uint32_t)d;
+                            f = LB_AGG;
+                            atomicOr(&ctrl[RS_CTRL_ERR], 4u);
+                        }
                         if (f == 0) {
                             stalled = true;
                         } else {
-                            excl += v[i] & LB_MASK;
+                            excl += val;
                             used = i + 1;
                             found = f == LB_INC;
                         }
@@ -561,10 +550,7 @@ __global__ __launch_bounds__(256) void rs_onesweep_kernel(const uint32_t *__rest
                 if (found) break;
                 look -= used;
                 if (stalled) {
-                    if (++spins > LB_SPIN_LIMIT) {
-                        atomicOr(&ctrl[RS_CTRL_ERR], 1u);
-                        break;
-                    }
+                    ++spins;
                     __builtin_amdgcn_s_sleep(1);
                 }
             }
@@ -632,6 +618,8 @@ static void launch_radix_sort_onesweep(hipStream_t s, SortScratch &sc, uint32_t 
     (void)hipMemsetAsync(sc.ctrl, 0, sizeof(uint32_t) * (RS_CTRL_WORDS + (size_t)passes * nb * RS_BINS), s);
     const uint32_t hb = min(div_up(n, 256u * 8u), 2048u);
     uint4 *stamps = tuning("stamp", 0) ? stamp_buffer(2) : nullptr;
+    const uint32_t pat = (uint32_t)tuning("lb_patience", 1 << 16);
+    const int force = tuning("lb_force", 0);
     rs_multi_hist_kernel<<<max(hb, 1u), 256, 0, s>>>(keys0, n, passes, sc.ctrl,
                                                     stamps ? stamp_buffer(3) : nullptr);
     rs_hist_scan_kernel<<<1, 256, 0, s>>>(sc.ctrl, passes);
@@ -643,10 +631,10 @@ static void launch_radix_sort_onesweep(hipStream_t s, SortScratch &sc, uint32_t 
         if (p == passes - 1 && gather) ga = *gather;
         if (p == 0 && !keyed)
             rs_onesweep_kernel<true, ITEMS, LBW><<<nb, 256, 0, s>>>(kin, nullptr, n, p, sc.ctrl, st, sc.k[out],
-                                                               sc.v[out], stamps, ga);
+                                                               sc.v[out], stamps, ga, pat, force);
         else
             rs_onesweep_kernel<false, ITEMS, LBW><<<nb, 256, 0, s>>>(kin, sc.v[in], n, p, sc.ctrl, st, sc.k[out],
-                                                                sc.v[out], stamps, ga);
+                                                                sc.v[out], stamps, ga, pat, force);
     }
 }
 

@@ -629,6 +629,33 @@ def test_debug_mode_is_bitwise_identical(gpu_device, bucket):
         assert np.array_equal(a["grads"][k], b["grads"][k]), k
 
 
+@pytest.mark.parametrize("bucket,onesweep", [(1, 1), (0, 3), (0, 0)])
+def test_lookback_fallback_is_bitwise_invisible(gpu_device, bucket, onesweep):
+    """Every decoupled look-back (bucket tile scan, instance scan, onesweep digit look-back) forced onto its
+    fallback -- every predecessor's aggregate recomputed from the kernel input instead of read from its status word
+    ("lb_force"), the path a look-back takes when a predecessor block is not running -- gives the same bits."""
+    from gaussian_splatting_lightning_amd import _native
+    inp = scene_inputs(20_000, 320, 240, sh_degree=2, seed=43, stress_fraction=0.01)
+    dc, di = upstream(320, 240, 43)
+    try:
+        _native.set_tuning("bucket", bucket)
+        _native.set_tuning("onesweep", onesweep)
+        a = run_hip(inp, gpu_device, dc, di)
+        _native.set_tuning("lb_force", 1)
+        b = run_hip(inp, gpu_device, dc, di)
+    finally:
+        _native.set_tuning("lb_force", 0)
+        _native.set_tuning("bucket", 1)
+        _native.set_tuning("onesweep", 1)
+    sa, sb = hip_state_arrays(a), hip_state_arrays(b)
+    for k in ("point_list", "ranges", "tiles", "n_contrib"):
+        assert np.array_equal(sa[k], sb[k]), k
+    for k in ("color", "invdepth", "radii"):
+        assert np.array_equal(a[k], b[k]), k
+    for k in GRADS:
+        assert np.array_equal(a["grads"][k], b["grads"][k]), k
+
+
 @pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2, reason="needs two HIP devices")
 def test_render_on_non_current_device():
     """Inputs on cuda:1 while cuda:0 is current (and the reverse afterwards): the library runs on its stream's
