@@ -82,5 +82,41 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+EXT_SRC = os.path.join(PKG, "csrc_torch", "gsr_torch_ext.cpp")
+EXT_DIR = os.path.join(REPO, "diff_gaussian_rasterization")
+EXT_LIB = os.path.join(EXT_DIR, "_C.so")
+
+
+def build_torch_ext(force: bool = False, verbose: bool = False) -> str:
+    """The thin torch extension `diff_gaussian_rasterization._C` (csrc_torch/gsr_torch_ext.cpp): upstream's pybind
+    entry points over libgsrast.so, compiled by hipcc against the installed PyTorch-ROCm, in-tree next to the package
+    (the rpath finds libgsrast.so in gaussian_splatting_lightning_amd/)."""
+    import sysconfig
+
+    import torch
+    import torch.utils.cpp_extension as ce
+    if not force and os.path.exists(EXT_LIB):
+        t = os.path.getmtime(EXT_LIB)
+        if all(os.path.getmtime(d) <= t for d in (EXT_SRC, LIB, os.path.join(INCLUDE, "gsrast.h"))):
+            return EXT_LIB
+    incs = ce.include_paths(device_type="cuda") + [sysconfig.get_paths()["include"], INCLUDE]
+    libdirs = ce.library_paths(device_type="cuda")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    tmp = EXT_LIB + ".tmp"
+    cmd = [_hipcc(), "-shared", "-fPIC", "-O2", "-std=c++17", "-DTORCH_EXTENSION_NAME=_C",
+           "-DTORCH_API_INCLUDE_EXTENSION_H", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-w",
+           *[f"-I{i}" for i in incs], EXT_SRC, "-o", tmp, *[f"-L{d}" for d in libdirs], f"-L{PKG}",
+           "-lgsrast", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
+           "-Wl,-rpath,$ORIGIN/../gaussian_splatting_lightning_amd", *[f"-Wl,-rpath,{d}" for d in libdirs]]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"torch extension build failed:\n{r.stdout}\n{r.stderr}")
+    if verbose and r.stderr.strip():
+        print(r.stderr, file=sys.stderr)
+    os.replace(tmp, EXT_LIB)
+    return EXT_LIB
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print(build_torch_ext(force="--force" in sys.argv, verbose=True))

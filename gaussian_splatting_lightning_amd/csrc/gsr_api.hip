@@ -605,8 +605,12 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     carve_binning(a->binning_buffer, R, T, b);
     ImageState im;
     carve_image(a->image_buffer, W, H, im);
-    if (a->num_big < 0 || a->num_big > a->P) return fail(GSR_ERR_ARG, "bad num_big");
-    const uint32_t nbig = (uint32_t)a->num_big;
+    if (a->num_big > a->P) return fail(GSR_ERR_ARG, "bad num_big");
+    // num_big < 0: not known on the host (the upstream backward signature has no such argument, gsr_torch_ext):
+    // size the big-Gaussian sums for the most there can be (each has > BIG_GAUSSIAN_TILES instances) and let the
+    // reduction read the count the preprocess left in the geometry buffer
+    const bool nbig_on_device = a->num_big < 0;
+    const uint32_t nbig = nbig_on_device ? R / (BIG_GAUSSIAN_TILES + 1) + 1 : (uint32_t)a->num_big;
     char *scratch = a->stages == GSR_BWD_GAUSSIANS ? a->bwd_scratch
                                                    : alloc(alloc_ctx, GSR_BUF_BWD_SCRATCH, bwd_scratch_bytes(R, nbig));
     if (!scratch && a->stages != GSR_BWD_GAUSSIANS) return fail(GSR_ERR_ALLOC, "backward scratch allocation failed");
@@ -635,6 +639,7 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
         BigReduceParams bp;
         bp.big_list = g.big_list; bp.inst_start = g.inst_start; bp.tiles = g.tiles;
         bp.inv = b.inv; bp.rows = rows; bp.bigsum = bigsum; bp.rows_by_u = rows_by_u;
+        bp.nbig_dev = nbig_on_device ? g.counters + CNT_BIG : nullptr;
         GSR_STAGE(ST_BIG_REDUCE, dbg, launch_big_reduce(stream, bp, nbig));
     }
     if (a->stages == GSR_BWD_COMPOSITE) return GSR_OK;

@@ -536,6 +536,7 @@ __global__ __launch_bounds__(256) void big_reduce_kernel(BigReduceParams p) {
     __shared__ float s_part[4][10];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t bi = blockIdx.x;
+    if (p.nbig_dev && bi >= *p.nbig_dev) return;  // workgroup-uniform: the launch was sized by an upper bound
     const uint32_t gidx = p.big_list[bi];
     const uint32_t start = p.inst_start[gidx], cnt = p.tiles[gidx];
     float acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};

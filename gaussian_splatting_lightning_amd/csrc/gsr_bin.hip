@@ -93,6 +93,7 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
     __shared__ uint4 s_rec[BKW][64];      // expansion records: kept mask lo, hi, rect x | y << 16, rect width
     __shared__ uint4 s_aux[BKW][64];      // first cell pair, first expansion index, depth key, 1/width bits
     __shared__ int s_own[BKW][64];        // lane whose cell run starts at this pair of the step, else -1
+    static_assert(BKW * 64 >= LPT_HIST_WORDS, "the LPT workgroup's histogram lives in s_own");
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const uint32_t b = blockIdx.x, T = p.T, gx = (uint32_t)p.gx;
     if (SCATTER && b == p.nb) {  // the extra workgroup: the forward LPT order (the column pass wrote the ranges)

@@ -714,18 +714,81 @@ __device__ __forceinline__ void wave_lds_sync() {
 // LPT (longest-processing-time-first) tile order by one workgroup of any multiple of 64 threads: histogram of the
 // tile weights (range length, or tile_last when use_last) in 2^shift-instance buckets, heaviest first, exclusive
 // scan by one wave, scatter.  Order inside a bucket is arbitrary -- it only changes which tile runs when, never
-// a result.  hist: 256 words of LDS.  Run by tile_order_kernel and by the bucket scatter's extra workgroup.
+// a result.  hist: 256 + 16 words of LDS (LPT_HIST_WORDS).  Run by tile_order_kernel and by the bucket scatter's extra workgroup.
+// * shift adapts to the heaviest tile: max(shift0, bits(max weight) - 8), at most 9, so long-tile images (4K
+//   stress: ~1500 instances per tile) spread over the buckets instead of piling into bucket 0 (the first slots
+//   stay exactly the tiles above SEG_CAP while 512 is a multiple of the bucket width, which seg_sort relies on);
+// * a thread's weights are loaded once, all together (up to KMAX per thread), not one dependent load per
+//   histogram / scatter iteration (one workgroup over 32400 tiles took 25-30 us);
+// * lanes of a wave with the same bucket share one LDS atomic (ballot-matched peers), so heavily shared buckets do
+//   not serialise.
+constexpr int LPT_KMAX = 32;
+constexpr int LPT_HIST_WORDS = 256 + 16;  // tile weights a thread keeps in registers (T <= 32 x the workgroup size)
+// One histogram (order == null) or scatter pass over the tiles; item k of thread tid is tile tid + k nt.
+__device__ __forceinline__ void lpt_item(int t, uint32_t wgt, bool valid, uint32_t shift, uint32_t *hist,
+                                         uint32_t *order, int lane, uint64_t lt) {
+    const uint32_t b = valid ? 255u - min(255u, wgt >> shift) : 0u;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int bit = 0; bit < 8; bit++) {
+        const bool set = (b >> bit) & 1u;
+        const uint64_t m = __ballot(set);
+        peers &= set ? m : ~m;
+    }
+    const uint64_t lower = peers & lt;
+    uint32_t base = 0;
+    if (valid && lower == 0) base = atomicAdd(&hist[b], (uint32_t)__popcll(peers));
+    if (order) {
+        const int leader = valid ? __builtin_ctzll(peers) : lane;
+        base = (uint32_t)__shfl((int)base, leader);
+        if (valid) order[base + (uint32_t)__popcll(lower)] = (uint32_t)t;
+    }
+}
+template <class LoadW>
+__device__ __forceinline__ void lpt_walk(int T, bool cached, const uint32_t (&wt)[LPT_KMAX], LoadW load_w,
+                                         uint32_t shift, uint32_t *hist, uint32_t *order) {
+    const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63;
+    const uint64_t lt = lanemask_lt(lane);
+    if (cached) {
+#pragma unroll
+        for (int k = 0; k < LPT_KMAX; k++) {
+            if (k * nt >= T) break;  // uniform
+            const int t = tid + k * nt;
+            lpt_item(t, wt[k], t < T, shift, hist, order, lane, lt);
+        }
+    } else {
+        for (int k0 = 0; k0 < T; k0 += nt) {  // uniform trip count
+            const int t = tid + k0;
+            lpt_item(t, t < T ? load_w(t) : 0u, t < T, shift, hist, order, lane, lt);
+        }
+    }
+}
 __device__ __forceinline__ void lpt_order_block(const uint2 *__restrict__ ranges, const uint32_t *__restrict__ tile_last,
-                                                int use_last, int T, int shift, uint32_t *__restrict__ order,
+                                                int use_last, int T, int shift0, uint32_t *__restrict__ order,
                                                 uint32_t *hist) {
-    const int tid = threadIdx.x, nt = blockDim.x;
-    auto bucket = [&](int t) -> uint32_t {
-        const uint32_t w = use_last ? tile_last[t] : ranges[t].y - ranges[t].x;
-        return 255u - min(255u, w >> shift);  // heaviest first
-    };
+    const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, w = tid >> 6;
+    auto load_w = [&](int t) -> uint32_t { return use_last ? tile_last[t] : ranges[t].y - ranges[t].x; };
+    const bool cached = T <= nt * LPT_KMAX;
+    uint32_t wt[LPT_KMAX];
+    uint32_t mx = 0;
+#pragma unroll
+    for (int k = 0; k < LPT_KMAX; k++) {  // every load issued before any use
+        const int t = tid + k * nt;
+        wt[k] = (cached && t < T) ? load_w(t) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < LPT_KMAX; k++) mx = max(mx, wt[k]);
+    if (!cached)
+        for (int t = tid; t < T; t += nt) mx = max(mx, load_w(t));
     for (int k = tid; k < 256; k += nt) hist[k] = 0;
+    mx = wave_max_u32(mx);
+    if (lane == 0) hist[256 + w] = mx;
     __syncthreads();
-    for (int t = tid; t < T; t += nt) atomicAdd(&hist[bucket(t)], 1u);
+    uint32_t m = 0;
+    for (int i = 0; i < (nt >> 6); i++) m = max(m, hist[256 + i]);
+    const int bits = m ? 32 - __builtin_clz(m) : 0;
+    const uint32_t shift = (uint32_t)max(shift0, min(9, bits - 8));
+    lpt_walk(T, cached, wt, load_w, shift, hist, nullptr);
     __syncthreads();
     if (tid < 64) {  // exclusive scan of the 256 buckets by one wave, 4 per lane
         const uint32_t a = hist[4 * tid], b = hist[4 * tid + 1], c = hist[4 * tid + 2], d = hist[4 * tid + 3];
@@ -737,7 +800,7 @@ __device__ __forceinline__ void lpt_order_block(const uint2 *__restrict__ ranges
         hist[4 * tid + 3] = excl + a + b + c;
     }
     __syncthreads();
-    for (int t = tid; t < T; t += nt) order[atomicAdd(&hist[bucket(t)], 1u)] = (uint32_t)t;
+    lpt_walk(T, cached, wt, load_w, shift, hist, order);
 }
 
 #endif  // __HIPCC__

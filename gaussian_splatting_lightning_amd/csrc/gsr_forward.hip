@@ -433,13 +433,13 @@ void launch_identify_ranges(hipStream_t s, const uint32_t *keys_sorted, uint32_t
 
 // LPT (longest first) launch order for the composite kernels: tile costs vary ~2x around the image centre,
 // and the GPU runs only ~8 tile waves per SIMD, so launching heavy tiles first keeps the tail short.  One
-// workgroup: bucket histogram of the tile weights (8 instances per bucket), descending exclusive scan,
-// scatter.  Order inside a bucket is arbitrary -- it only changes which tile runs when, never a result.
+// workgroup: bucket histogram of the tile weights (2^shift instances per bucket, shift adapted to the heaviest
+// tile), descending exclusive scan, scatter (lpt_order_block).  Order inside a bucket is arbitrary -- it only changes which tile runs when, never a result.
 // (A 1024-bucket variant with ballot-ranked, tile-ordered buckets measured 4 % slower in render_fwd.)
 __global__ __launch_bounds__(1024) void tile_order_kernel(const uint2 *__restrict__ ranges,
                                                              const uint32_t *__restrict__ tile_last, int use_last,
                                                              int T, int shift, uint32_t *__restrict__ order) {
-    __shared__ uint32_t hist[256];
+    __shared__ uint32_t hist[LPT_HIST_WORDS];
     lpt_order_block(ranges, tile_last, use_last, T, shift, order, hist);
 }
 

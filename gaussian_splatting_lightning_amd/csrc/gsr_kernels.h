@@ -160,6 +160,7 @@ struct BigReduceParams {
     int rows_by_u;
     const float *rows;
     float *bigsum;  // nbig x GRAD_ROW
+    const uint32_t *nbig_dev;  // or null: the launch's nbig is exact; else an upper bound and this the count
 };
 void launch_big_reduce(hipStream_t s, const BigReduceParams &p, uint32_t nbig);
 

@@ -84,7 +84,8 @@ int gsr_forward(gsr_forward_args *args, gsr_alloc_fn alloc, void *alloc_ctx, voi
 typedef struct gsr_backward_args {
     int P, D, M, W, H;
     int64_t R;                    /* num_rendered returned by gsr_forward */
-    int64_t num_big;              /* num_big_out returned by gsr_forward */
+    int64_t num_big;              /* num_big_out returned by gsr_forward, or < 0: read from geom_buffer on the device
+                                     (the upstream backward signature does not carry it; gsr_torch_ext.cpp) */
     const float *background;
     const float *means3D;
     const float *colors_precomp;  /* or NULL */
