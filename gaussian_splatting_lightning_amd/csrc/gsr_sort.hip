@@ -6,7 +6,7 @@
 //   * a 32-bit depth sort over the P Gaussians (4 passes over P, not over the ~6.5x larger instance list),
 //   * a stable tile-id sort (ceil(log2 T) bits, 2 passes at 1080p) over the instances, which are
 //     expanded in depth order, so the result equals the reference's stable (tile, depth, index) order.
-// Each pass is histogram -> scan of the [digit][block] counts -> stable scatter.  The scatter ranks
+// Each pass is histogram -> scan of the [block][digit] counts in (digit, block) order -> stable scatter.  The scatter ranks
 // keys inside a wave with eight 64-lane ballots (wave64 multisplit), keeps per-wave digit counters in
 // LDS, stages the block's output in LDS, and writes each digit's run contiguously.
 #include "gsr_kernels.h"
@@ -227,7 +227,79 @@ __global__ __launch_bounds__(256) void rs_hist_kernel(const uint32_t *__restrict
         }
     }
     __syncthreads();
-    counts[(size_t)tid * nb + blockIdx.x] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+    counts[(size_t)blockIdx.x * RS_BINS + tid] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+}
+
+// ------------------------------------------------------------------------------------------------
+// radix sort pass: global digit offsets of every (block, digit)
+// ------------------------------------------------------------------------------------------------
+// The count matrix is block-major -- [block][digit], one coalesced 1 KB row per histogram block, read back as one
+// row by that block's scatter -- where a digit-major matrix scattered 4-B writes and reads over nb x 256 cache
+// lines per pass (at 48M keys ~200 MB of partial-line traffic for 6 MB of counts).  The scan runs in (digit,
+// block) order over it in three short launches: column sums of RS_COL_CHUNK-row chunks, one workgroup scanning the
+// chunk sums per digit and the digit totals, then every chunk's rows.
+__global__ __launch_bounds__(256) void rs_colsum_kernel(const uint32_t *__restrict__ counts, uint32_t nb,
+                                                        uint32_t *__restrict__ colsum) {
+    const uint32_t c = blockIdx.x, d = threadIdx.x;
+    const uint32_t b0 = c * RS_COL_CHUNK, b1 = min(nb, b0 + RS_COL_CHUNK);
+    uint32_t s = 0;
+    uint32_t b = b0;
+    for (; b + 8 <= b1; b += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) v[i] = counts[(size_t)(b + i) * RS_BINS + d];
+#pragma unroll
+        for (int i = 0; i < 8; i++) s += v[i];
+    }
+    for (; b < b1; b++) s += counts[(size_t)b * RS_BINS + d];
+    colsum[(size_t)c * RS_BINS + d] = s;
+}
+
+__global__ __launch_bounds__(256) void rs_colscan_kernel(uint32_t *__restrict__ colsum, uint32_t nchunks) {
+    __shared__ uint32_t s_w[4];
+    const int d = threadIdx.x, lane = d & 63, w = d >> 6;
+    uint32_t run = 0;
+    for (uint32_t c = 0; c < nchunks; c++) {  // per digit: exclusive over the chunks
+        const uint32_t v = colsum[(size_t)c * RS_BINS + d];
+        colsum[(size_t)c * RS_BINS + d] = run;
+        run += v;
+    }
+    const uint32_t inc = wave_inclusive_scan(run, lane);  // digit totals -> exclusive digit offsets
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    uint32_t off = inc - run;
+    for (int i = 0; i < w; i++) off += s_w[i];
+    for (uint32_t c = 0; c < nchunks; c++) colsum[(size_t)c * RS_BINS + d] += off;
+}
+
+__global__ __launch_bounds__(256) void rs_colbase_kernel(uint32_t *__restrict__ counts, uint32_t nb,
+                                                         const uint32_t *__restrict__ colsum) {
+    const uint32_t c = blockIdx.x, d = threadIdx.x;
+    const uint32_t b0 = c * RS_COL_CHUNK, b1 = min(nb, b0 + RS_COL_CHUNK);
+    uint32_t run = colsum[(size_t)c * RS_BINS + d];
+    uint32_t b = b0;
+    for (; b + 8 <= b1; b += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) v[i] = counts[(size_t)(b + i) * RS_BINS + d];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            counts[(size_t)(b + i) * RS_BINS + d] = run;
+            run += v[i];
+        }
+    }
+    for (; b < b1; b++) {
+        const uint32_t v = counts[(size_t)b * RS_BINS + d];
+        counts[(size_t)b * RS_BINS + d] = run;
+        run += v;
+    }
+}
+
+static void launch_count_scan(hipStream_t s, uint32_t *counts, uint32_t nb, uint32_t *colsum) {
+    const uint32_t nch = div_up(nb, RS_COL_CHUNK);
+    rs_colsum_kernel<<<nch, RS_BINS, 0, s>>>(counts, nb, colsum);
+    rs_colscan_kernel<<<1, RS_BINS, 0, s>>>(colsum, nch);
+    rs_colbase_kernel<<<nch, RS_BINS, 0, s>>>(counts, nb, colsum);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -298,7 +370,7 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restr
         uint32_t woff = 0;
         for (int i = 0; i < w; i++) woff += s_wsum[i];
         s_dstart[d] = woff + inc - tot;
-        s_gbase[d] = counts_scanned[(size_t)d * nb + blockIdx.x];
+        s_gbase[d] = counts_scanned[(size_t)blockIdx.x * RS_BINS + d];
     }
     __syncthreads();
 #pragma unroll
@@ -647,7 +719,7 @@ static void launch_radix_sort_multi(hipStream_t s, SortScratch &sc, uint32_t n, 
         const int shift = 8 * p, in = p & 1, out = (p + 1) & 1;
         const uint32_t *kin = p == 0 ? keys0 : sc.k[in];
         rs_hist_kernel<ITEMS * 256><<<nb, 256, 0, s>>>(kin, n, shift, sc.counts, nb);
-        launch_exclusive_scan(s, sc.counts, nullptr, RS_BINS * nb, sc.counts, sc.scan_tmp, nullptr);
+        launch_count_scan(s, sc.counts, nb, sc.scan_tmp);
         SortGather ga;
         if (p == passes - 1 && gather) ga = *gather;
         if (p == 0 && !keyed)

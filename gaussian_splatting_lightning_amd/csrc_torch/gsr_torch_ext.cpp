@@ -7,8 +7,9 @@
 // (it goes through the Python API, gaussian_splatting_lightning_amd/rasterizer.py); this module is for code that
 // imports `diff_gaussian_rasterization._C` directly, and tests/test_torch_ext.py checks it against the Python path.
 #include <torch/extension.h>
-#include <c10/hip/HIPGuard.h>
-#include <c10/hip/HIPStream.h>
+// PyTorch-ROCm tags HIP devices as "cuda"; its own guard and stream accessors for them are the MasqueradingAsCUDA ones
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
 #include <algorithm>
 #include <tuple>
@@ -45,7 +46,9 @@ torch::Tensor f32c(const torch::Tensor &t, const char *name) {
     return t.contiguous();
 }
 
-void *stream_of(const torch::Tensor &t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+void *stream_of(const torch::Tensor &t) {
+    return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
+}
 
 }  // namespace
 
@@ -59,7 +62,7 @@ rasterize_gaussians(const torch::Tensor &background, const torch::Tensor &means3
                     const int image_width, const torch::Tensor &sh, const int degree, const torch::Tensor &campos,
                     const bool prefiltered, const bool antialiasing, const bool debug) {
     TORCH_CHECK(means3D.ndimension() == 2 && means3D.size(1) == 3, "means3D must have dimensions (num_points, 3)");
-    const c10::hip::OptionalHIPGuard guard(means3D.device());
+    const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(means3D.device());
     const int P = (int)means3D.size(0), H = image_height, W = image_width;
     auto m = f32c(means3D, "means3D"), bg = f32c(background, "background"), col = f32c(colors, "colors"),
          op = f32c(opacity, "opacity"), sc = f32c(scales, "scales"), rot = f32c(rotations, "rotations"),
@@ -101,7 +104,7 @@ rasterize_gaussians_backward(const torch::Tensor &background, const torch::Tenso
                              const torch::Tensor &sh, const int degree, const torch::Tensor &campos,
                              const torch::Tensor &geomBuffer, const int R, const torch::Tensor &binningBuffer,
                              const torch::Tensor &imageBuffer, const bool antialiasing, const bool debug) {
-    const c10::hip::OptionalHIPGuard guard(means3D.device());
+    const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(means3D.device());
     const int P = (int)means3D.size(0), H = (int)dL_dout_color.size(1), W = (int)dL_dout_color.size(2);
     auto m = f32c(means3D, "means3D"), bg = f32c(background, "background"), col = f32c(colors, "colors"),
          op = f32c(opacities, "opacities"), sc = f32c(scales, "scales"), rot = f32c(rotations, "rotations"),
@@ -140,7 +143,7 @@ rasterize_gaussians_backward(const torch::Tensor &background, const torch::Tenso
 // markVisible -> bool (P)
 torch::Tensor mark_visible(const torch::Tensor &means3D, const torch::Tensor &viewmatrix,
                            const torch::Tensor &projmatrix) {
-    const c10::hip::OptionalHIPGuard guard(means3D.device());
+    const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(means3D.device());
     auto m = f32c(means3D, "means3D"), vm = f32c(viewmatrix, "viewmatrix"), pm = f32c(projmatrix, "projmatrix");
     const int P = (int)means3D.size(0);
     auto present = torch::zeros({P}, torch::TensorOptions().dtype(torch::kBool).device(means3D.device()));
