@@ -400,7 +400,6 @@ constexpr uint32_t IR_PER = 8;
 __global__ __launch_bounds__(256) void identify_ranges_kernel(const uint32_t *__restrict__ keys, uint32_t R,
                                                               uint2 *__restrict__ ranges) {
     const uint32_t base = (blockIdx.x * 256 + threadIdx.x) * IR_PER;
-    if (base >= R) return;
     uint32_t k[IR_PER];
     if (base + IR_PER <= R) {
         const uint4 *k4 = reinterpret_cast<const uint4 *>(keys + base);
@@ -410,7 +409,11 @@ __global__ __launch_bounds__(256) void identify_ranges_kernel(const uint32_t *__
 #pragma unroll
         for (uint32_t q = 0; q < IR_PER; q++) k[q] = base + q < R ? keys[base + q] : 0u;
     }
-    uint32_t prev = base ? keys[base - 1] : 0u;
+    // the key before this thread's run: the previous lane's last key (one load per wave, not per thread); every
+    // lane takes part in the shuffle, lanes past the end only lend their (unused) keys
+    const int lane = threadIdx.x & 63;
+    uint32_t prev = (uint32_t)__shfl_up((int)k[IR_PER - 1], 1);
+    if (lane == 0) prev = (base > 0 && base <= R) ? keys[base - 1] : 0u;
     if (base == 0) ranges[k[0]].x = 0;
 #pragma unroll
     for (uint32_t q = 0; q < IR_PER; q++) {

@@ -412,6 +412,32 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restr
         }
         return;
     }
+    if (cnt_blk == (uint32_t)(ITEMS * 256)) {
+        // full block: LDS reads and offsets of 8 elements first, then their 16 stores (one LDS round trip per 8
+        // elements instead of per element)
+#pragma unroll
+        for (int i0 = 0; i0 < ITEMS; i0 += 8) {
+            uint32_t k[8], v[8], g[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const uint32_t i = (uint32_t)(i0 + q) * 256 + tid;
+                k[q] = s_keys[i];
+                v[q] = s_vals[i];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const uint32_t i = (uint32_t)(i0 + q) * 256 + tid;
+                const uint32_t d = (k[q] >> shift) & 255u;
+                g[q] = s_gbase[d] + (i - s_dstart[d]);
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                keys_out[g[q]] = k[q];
+                vals_out[g[q]] = v[q];
+            }
+        }
+        return;
+    }
     for (uint32_t i = tid; i < cnt_blk; i += 256) {
         const uint32_t k = s_keys[i], v = s_vals[i];
         const uint32_t d = (k >> shift) & 255u;
