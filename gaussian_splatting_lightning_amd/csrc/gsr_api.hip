@@ -565,6 +565,14 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     rp.bg = a->background;
     rp.out_color = a->out_color; rp.out_invdepth = a->out_invdepth; rp.final_T = im.final_T;
     rp.n_contrib = im.n_contrib; rp.tile_last = im.tile_last;
+    // checkpoints for the segmented backward ("bwd_seg" 1, spacing "seg_k" instances: 32 or a multiple of 64) while the image
+    // has few tiles; the forward records in ck_flag whether it wrote them, so the backward never reads stale ones
+    rp.ck_flag = im.ck_flag;
+    if (T <= SEG_MAX_TILES && tuning("bwd_seg", 1)) {
+        rp.ckpt = b.ckpt; rp.ctot = im.ctot;
+        const int k = tuning("seg_k", 64);  // cfg 2: 32 / 64 / 128 -> render_bwd 0.106 / 0.107 / 0.129 ms, render_fwd 0.070 / 0.065 / 0.062
+        rp.ck_k = k <= 32 ? 32u : (uint32_t)(k / 64) * 64u;
+    }
     GSR_STAGE(ST_RENDER_FWD, dbg, launch_render_fwd(stream, rp));
     if (dbg)  // onesweep error words exist only for the sorts that ran on the onesweep path (launch_radix_sort)
         return check_lookback_flags(stream, device_guard.dev, g.counters, depth_onesweep ? g.sort.ctrl : nullptr,
@@ -635,6 +643,10 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
         rp.rows = rows;
         rp.sorted_u = b.sorted_u;
         rp.rows_by_u = rows_by_u;
+        if (T <= SEG_MAX_TILES && tuning("bwd_seg", 1)) {  // segmented walk (from the forward's checkpoints, if any)
+            rp.ckpt = b.ckpt; rp.ctot = im.ctot; rp.ck_flag = im.ck_flag;
+            rp.seg_list = b.seg_list; rp.seg_count = im.seg_count;
+        }
         GSR_STAGE(ST_RENDER_BWD, dbg, launch_render_bwd(stream, rp));
         BigReduceParams bp;
         bp.big_list = g.big_list; bp.inst_start = g.inst_start; bp.tiles = g.tiles;

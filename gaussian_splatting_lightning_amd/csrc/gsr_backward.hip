@@ -271,14 +271,32 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
 #ifndef GSR_BWD_MINW
 #define GSR_BWD_MINW 5
 #endif
-template <bool HAS_INV, bool LASTC, bool UNION = false>
-__global__ __launch_bounds__(64, GSR_BWD_MINW) void render_bwd_v5_kernel(RenderBwdParams p) {
+#ifndef GSR_BWD_SEG_MINW
+#define GSR_BWD_SEG_MINW 6  // the segment walk's extra scalars took it to 83 VGPRs (5 waves / SIMD); 6 caps it at 80
+#endif
+// SEG (small images): the launch slot is a (tile, segment) work item of seg_list; with the forward's checkpoints
+// (*ck_flag = K) segment s walks instances [s K, min((s + 1) K, tile_last)) back to front, starting each pixel from the
+// checkpoint at the segment's end: T = T_e and D = (colour still to come . dL/dpix + T_final bg . dL/dpix) / T_e, the
+// scalar accumulator's value there (D_k T_(k+1) = sum_(j > k) w_j c_j . dL/dpix + T_final bg . dL/dpix).  Without
+// checkpoints every tile is one segment.  Rows agree with the one-walk backward to rounding.
+template <bool HAS_INV, bool LASTC, bool UNION = false, bool SEG = false>
+__global__ __launch_bounds__(64, SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MINW) void render_bwd_v5_kernel(RenderBwdParams p) {
     __shared__ FwdRec s_rec[BWD_BATCH];
     __shared__ __attribute__((aligned(16))) float s_part[BWD_BATCH][PART];  // [instance][10 sums]
     const int lane = threadIdx.x;
     const int slot = blockIdx.x;
     const uint32_t t_start = p.stamps ? stamp_now() : 0u;
-    const int tile = __builtin_amdgcn_readfirstlane(p.tile_order ? (int)p.tile_order[slot] : slot);
+    uint32_t seg = 0, ck_k = 0;
+    int tile;
+    if constexpr (SEG) {
+        if ((uint32_t)slot >= __builtin_amdgcn_readfirstlane(*p.seg_count)) return;
+        const uint2 item = p.seg_list[slot];
+        tile = __builtin_amdgcn_readfirstlane((int)item.x);
+        seg = __builtin_amdgcn_readfirstlane(item.y);
+        ck_k = __builtin_amdgcn_readfirstlane(*p.ck_flag);
+    } else {
+        tile = __builtin_amdgcn_readfirstlane(p.tile_order ? (int)p.tile_order[slot] : slot);
+    }
     const int tx = tile % p.gx, ty = tile / p.gx;
     const int px = tx * BLOCK_X + (lane & 15);
     const int py0 = ty * BLOCK_Y + (lane >> 4);
@@ -288,11 +306,20 @@ __global__ __launch_bounds__(64, GSR_BWD_MINW) void render_bwd_v5_kernel(RenderB
     const uint32_t r0 = __builtin_amdgcn_readfirstlane(range.x);
     const uint32_t tl = __builtin_amdgcn_readfirstlane(p.tile_last[tile]);
     const uint32_t loaded = __builtin_amdgcn_readfirstlane(p.tile_loaded[tile]);
-    for (uint32_t s = r0 + tl + lane; s < r0 + loaded; s += 64) {
-        const float z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        store_row(p.rows, p.rows_by_u ? p.sorted_u[s] : s, z);
+    // this wave's instances [lo, hi) (tile-relative); the last segment also zeroes the rows of [tile_last, loaded)
+    uint32_t lo = 0, hi = tl;
+    bool last_seg = true;
+    if (SEG && ck_k) {
+        lo = seg * ck_k;
+        hi = min(lo + ck_k, tl);
+        last_seg = lo + ck_k >= tl;
     }
-    if (tl == 0) {
+    if (last_seg)
+        for (uint32_t s = r0 + tl + lane; s < r0 + loaded; s += 64) {
+            const float z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+            store_row(p.rows, p.rows_by_u ? p.sorted_u[s] : s, z);
+        }
+    if (hi == 0) {
         stamp_store(p.stamps, slot, t_start, lane);
         return;
     }
@@ -319,10 +346,26 @@ __global__ __launch_bounds__(64, GSR_BWD_MINW) void render_bwd_v5_kernel(RenderB
             smin[k] = __builtin_amdgcn_readfirstlane(wave_min_u32(lastc[k]));
         }
     }
+    if (SEG && !last_seg) {  // start from the checkpoint before instance hi
+        const float *ck = p.ckpt + (size_t)(r0 / ck_k + (uint32_t)tile + seg) * CK_FLOATS;
+        const float *ct = p.ctot + (size_t)tile * 1024;
+#pragma unroll
+        for (int k = 0; k < PIX_PER_LANE; k++) {
+            const int i = lane + 64 * k;
+            if (hi < lastc[k]) {
+                const float Te = ck[i];
+                const float c0 = ct[i] - ck[256 + i], c1 = ct[256 + i] - ck[512 + i], c2 = ct[512 + i] - ck[768 + i];
+                float num = fmaf(c2, dp2[k], fmaf(c1, dp1[k], c0 * dp0[k]));
+                if (HAS_INV) num = fmaf(ct[768 + i] - ck[1024 + i], dinv[k], num);
+                D[k] = fmaf(T[k], D[k], num) / Te;
+                T[k] = Te;
+            }
+        }
+    }
     const float hW = 0.5f * p.W, hH = 0.5f * p.H;
 
-    for (int bend = (int)tl; bend > 0; bend -= BWD_BATCH) {
-        const int cnt = min(BWD_BATCH, bend);
+    for (int bend = (int)hi; bend > (int)lo; bend -= BWD_BATCH) {
+        const int cnt = min(BWD_BATCH, bend - (int)lo);
         float4 my_a = make_float4(0, 0, 0, 0), my_b = my_a;
         uint32_t my_row = 0, my_m = 0;
         if (lane < cnt) {
@@ -487,11 +530,56 @@ __global__ __launch_bounds__(64, GSR_BWD_MINW) void render_bwd_v5_kernel(RenderB
     stamp_store(p.stamps, slot, t_start, lane);
 }
 
+// (tile, segment) work list of the segmented backward, one workgroup: tiles in the backward's LPT order (heaviest
+// first), each split into ceil(tile_last / K) segments (K = *ck_flag, the forward's checkpoint spacing; 0: one
+// segment per tile); *seg_count = the number of items.  T <= SEG_MAX_TILES (4 tiles per thread).
+__global__ __launch_bounds__(1024) void seg_list_kernel(const uint32_t *__restrict__ order,
+                                                        const uint32_t *__restrict__ tile_last, int T,
+                                                        const uint32_t *__restrict__ ck_flag, uint2 *__restrict__ list,
+                                                        uint32_t *__restrict__ count) {
+    __shared__ uint32_t s_wsum[16];
+    constexpr int PER = (int)SEG_MAX_TILES / 1024;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t K = *ck_flag;
+    uint32_t t[PER], n[PER], sum = 0;
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int i = tid * PER + q;
+        t[q] = i < T ? (order ? order[i] : (uint32_t)i) : 0u;
+        const uint32_t tl = i < T ? tile_last[t[q]] : 0u;
+        n[q] = i < T ? (K ? max(1u, (tl + K - 1) / K) : 1u) : 0u;
+        sum += n[q];
+    }
+    const uint32_t inc = wave_inclusive_scan(sum, lane);
+    if (lane == 63) s_wsum[w] = inc;
+    __syncthreads();
+    uint32_t base = inc - sum, total = 0;
+    for (int i = 0; i < 16; i++) {
+        const uint32_t v = s_wsum[i];
+        if (i < w) base += v;
+        total += v;
+    }
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        for (uint32_t s = 0; s < n[q]; s++) list[base + s] = make_uint2(t[q], s);
+        base += n[q];
+    }
+    if (tid == 0) *count = total;
+}
+
 void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
     if (p.num_tiles <= 0) return;
     RenderBwdParams q = p;
     q.strip_exact = tuning("strip_exact", 1);
     q.stamps = tuning("stamp", 0) ? stamp_buffer(1) : nullptr;
+    if (p.seg_list && p.ck_flag && p.ckpt && p.ctot && p.seg_count && p.num_tiles <= (int)SEG_MAX_TILES) {
+        // segmented walk (800x800, 2500 tiles: one wave per 128-instance segment against 4 part-waves per tile)
+        seg_list_kernel<<<1, 1024, 0, s>>>(p.tile_order, p.tile_last, p.num_tiles, p.ck_flag, q.seg_list, q.seg_count);
+        const dim3 grid((uint32_t)seg_slots((int64_t)p.num_rendered, (uint32_t)p.num_tiles)), block(64);
+        if (p.dL_dinvdepth) render_bwd_v5_kernel<true, false, false, true><<<grid, block, 0, s>>>(q);
+        else render_bwd_v5_kernel<false, false, false, true><<<grid, block, 0, s>>>(q);
+        return;
+    }
     // "bwd_parts" 1, 2 or 4; 0 (default): 4 or 2 while that many part-waves fit within bwd_part_slots
     // (1024 SIMDs x 12: 800x800 (2500 tiles) takes 4 parts, 0.143 ms against 0.149 in 2 and 0.181 whole; 1080p
     // (8160 tiles) whole tiles)

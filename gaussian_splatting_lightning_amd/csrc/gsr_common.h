@@ -169,8 +169,19 @@ struct BinningState {
     SortScratch sort;      // radix path: tile sort (R keys); its final value buffer is sorted_u
     unsigned long long *bk_keys;  // bucket path: R keys (depth << 32 | u) bucketed by tile
     unsigned long long *bk_keys2; // bucket path: R, chunk-sorted keys of tiles longer than SEG_BLOCK_CAP
+    // segmented backward (small images, num_tiles <= SEG_MAX_TILES; else null): the forward's per-pixel checkpoints
+    // at every K-th instance of a tile (CK_FLOATS each: T, then the colour / inverse-depth sums so far), tile t's
+    // checkpoint j (before instance (j + 1) K) at index ranges[t].x / K + t + j; and the backward's work list
+    float *ckpt;           // (R / CK_MIN_K + T + 1) x CK_FLOATS
+    uint2 *seg_list;       // R / CK_MIN_K + T + 1 entries (tile, segment)
 };
 constexpr uint32_t INV_NONE = 0xffffffffu;
+// Segmented backward: tiles are split into K-instance segments walked by independent waves, each starting from the
+// forward's checkpoint at its end (T and the colour still to come), while the image has few tiles.
+constexpr uint32_t SEG_MAX_TILES = 4096;
+constexpr uint32_t CK_MIN_K = 32;
+constexpr uint32_t CK_FLOATS = 5 * 256;
+inline uint64_t seg_slots(int64_t R, uint32_t num_tiles) { return (uint64_t)(R > 0 ? R : 0) / CK_MIN_K + num_tiles + 1; }
 
 inline size_t carve_binning(char *base, int64_t R, uint32_t num_tiles, BinningState &b) {
     Carver c(base);
@@ -190,6 +201,13 @@ inline size_t carve_binning(char *base, int64_t R, uint32_t num_tiles, BinningSt
     b.bk_keys = cb.take<unsigned long long>(n ? n : 1);
     b.bk_keys2 = cb.take<unsigned long long>(n ? n : 1);
     c.off = cr.off > cb.off ? cr.off : cb.off;
+    b.ckpt = nullptr;
+    b.seg_list = nullptr;
+    if (num_tiles <= SEG_MAX_TILES) {
+        const uint64_t ns = seg_slots(R, num_tiles);
+        b.ckpt = c.take<float>((size_t)ns * CK_FLOATS);
+        b.seg_list = c.take<uint2>((size_t)ns);
+    }
     return c.off + 256;
 }
 
@@ -210,6 +228,12 @@ struct ImageState {
     uint32_t *bk_tile_start; // T + 1
     uint32_t *bk_long_list;  // 2 x (T + 1): tiles of (SEG_CAP, SEG_BLOCK_CAP] instances, longer tiles
     uint32_t *bk_tie_list;   // T + 1: tiles whose 32-bit proxy-key sort did not converge
+    // segmented backward (num_tiles <= SEG_MAX_TILES): each pixel's final colour / inverse-depth sums, tile-major
+    // (tile t, plane c, pixel i at t * 1024 + c * 256 + i); the checkpoint spacing K the forward used (0: none);
+    // the backward's segment count
+    float *ctot;
+    uint32_t *ck_flag;
+    uint32_t *seg_count;
 };
 
 inline size_t carve_image(char *base, int W, int H, ImageState &im) {
@@ -230,6 +254,9 @@ inline size_t carve_image(char *base, int W, int H, ImageState &im) {
     im.bk_tile_start = c.take<uint32_t>(nt + 1);
     im.bk_long_list = c.take<uint32_t>(2 * (nt + 1));
     im.bk_tie_list = c.take<uint32_t>(nt + 1);
+    im.ctot = c.take<float>(nt <= SEG_MAX_TILES ? nt * 1024 : 1);
+    im.ck_flag = c.take<uint32_t>(1);
+    im.seg_count = c.take<uint32_t>(1);
     return c.off + 256;
 }
 

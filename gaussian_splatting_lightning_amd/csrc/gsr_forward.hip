@@ -471,13 +471,19 @@ void launch_tile_order(hipStream_t s, const uint2 *ranges, const uint32_t *tile_
 // branch that retires the pixel and clears its lane from the strip's live mask (scalar), so a strip whose pixels
 // have all finished is skipped like a dead cell, and the wave stops when no strip is live without any
 // per-instance vector compare.
-template <int NPIX, int MIN_WAVES>
+// CKPT (segmented backward, small images): at every ck_k-th instance of the tile the wave stores each pixel's T and
+// colour / inverse-depth sums so far (checkpoint j before instance (j + 1) ck_k, at ckpt index ranges.x / ck_k + tile
+// + j), and at the end the pixel's final sums (ctot); the backward walks each ck_k-instance segment from the
+// checkpoint at its end.  A pixel still compositing at instance e is still walked when its wave reaches e, so every
+// checkpoint the backward reads (e < the pixel's n_contrib) is written.
+template <int NPIX, int MIN_WAVES, bool CKPT = false>
 __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwdParams p) {
     constexpr int PARTS = 4 / NPIX;
     __shared__ FwdRec s_rec[4][64];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int slot = blockIdx.x * 4 + w;
+    if (p.ck_flag && slot == 0 && lane == 0) *p.ck_flag = CKPT ? p.ck_k : 0u;
     if (slot >= p.num_tiles * PARTS) return;
     const int half = slot % PARTS;
     const int tile = __builtin_amdgcn_readfirstlane(p.tile_order ? (int)p.tile_order[slot / PARTS] : slot / PARTS);
@@ -506,7 +512,21 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
     uint32_t contributor = 0;
     uint32_t loaded_end = r0;
     FwdRec *sr = s_rec[w];
+    // checkpoint before tile-relative instance e (a multiple of ck_k)
+    auto store_ck = [&](uint32_t e) {
+        float *ck = p.ckpt + (size_t)(r0 / p.ck_k + (uint32_t)tile + e / p.ck_k - 1) * CK_FLOATS;
+#pragma unroll
+        for (int k = 0; k < NPIX; k++) {
+            const int i = lane + 64 * (kbase + k);  // pixel within the tile
+            ck[i] = T[k];
+            ck[256 + i] = C0[k];
+            ck[512 + i] = C1[k];
+            ck[768 + i] = C2[k];
+            ck[1024 + i] = ID[k];
+        }
+    };
     for (uint32_t base = r0; base < r1; base += 64) {
+        if (CKPT && base > r0 && (base - r0) % p.ck_k == 0) store_ck(base - r0);
         const uint32_t s = base + lane;
         uint32_t m = 0;
         if (s < r1) {
@@ -531,6 +551,7 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
 #pragma unroll
         for (int k = 0; k < NPIX; k++) un |= sk[k];
         const uint32_t cbase = contributor;
+        auto walk = [&](uint64_t &un) {
         while (un) {
             const uint32_t j = (uint32_t)__builtin_ctzll(un);
             un &= un - 1;
@@ -572,6 +593,19 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
                 }
             }
         }
+        };
+        if (CKPT && p.ck_k == 32 && base + 32 < r1) {  // 32-instance checkpoints: one in the middle of the batch
+            uint64_t lo = un & 0xffffffffull;
+            walk(lo);
+            store_ck(base + 32 - r0);
+            uint64_t live = 0;
+#pragma unroll
+            for (int k = 0; k < NPIX; k++) live |= sk[k];
+            uint64_t hi = un & live & ~0xffffffffull;
+            walk(hi);
+        } else {
+            walk(un);
+        }
         contributor = cbase + min(64u, r1 - base);
         wave_lds_sync();
         uint64_t anylive = 0;
@@ -595,6 +629,13 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
             p.out_color[2 * HW + pid] = C2[k] + Tk * bg2;
             if (p.out_invdepth) p.out_invdepth[pid] = ID[k];
             mx = max(mx, last[k]);
+        }
+        if (CKPT) {
+            float *ct = p.ctot + (size_t)tile * 1024 + lane + 64 * (kbase + k);
+            ct[0] = C0[k];
+            ct[256] = C1[k];
+            ct[512] = C2[k];
+            ct[768] = ID[k];
         }
     }
     mx = wave_max_u32(mx);
@@ -628,7 +669,9 @@ void launch_render_fwd(hipStream_t s, const RenderFwdParams &p0) {
         return;
     }
     const int mw = tuning("fwd_part_waves", 8);
-    if (parts == 2 && mw >= 8) render_fwd_v6_kernel<2, 8><<<grid, block, 0, s>>>(p);
+    if (parts == 4 && p.ckpt && p.ctot && p.ck_k >= CK_MIN_K && p.ck_k % 32 == 0 && (p.ck_k == 32 || p.ck_k % 64 == 0))
+        render_fwd_v6_kernel<1, 8, true><<<grid, block, 0, s>>>(p);
+    else if (parts == 2 && mw >= 8) render_fwd_v6_kernel<2, 8><<<grid, block, 0, s>>>(p);
     else if (parts == 2) render_fwd_v6_kernel<2, 4><<<grid, block, 0, s>>>(p);
     else if (mw >= 8) render_fwd_v6_kernel<1, 8><<<grid, block, 0, s>>>(p);
     else render_fwd_v6_kernel<1, 4><<<grid, block, 0, s>>>(p);

@@ -133,6 +133,11 @@ struct RenderFwdParams {
     uint32_t *n_contrib, *tile_last;
     uint4 *stamps; // diagnostics (set by launch), or null
     int strip_exact;  // strip skipping mask: 1 strip_mask_exact (column-band extent), 0 strip_mask (set by launch)
+    // segmented-backward checkpoints (BinningState::ckpt, ImageState::ctot / ck_flag), or null: written every ck_k
+    // instances when the launch runs tiles in 4 parts; *ck_flag = ck_k if it did, else 0
+    float *ckpt = nullptr, *ctot = nullptr;
+    uint32_t *ck_flag = nullptr;
+    uint32_t ck_k = 0;
 };
 void launch_render_fwd(hipStream_t s, const RenderFwdParams &p);
 
@@ -152,6 +157,12 @@ struct RenderBwdParams {
     uint4 *stamps;  // diagnostics (set by launch), or null
     int strip_exact;  // as RenderFwdParams::strip_exact (set by launch)
     uint64_t num_rendered = 0;  // instances (the launch's walk-variant choice)
+    // segmented walk (small images): the forward's checkpoints, or null for one wave (or workgroup) per tile
+    const float *ckpt = nullptr, *ctot = nullptr;
+    const uint32_t *ck_flag = nullptr;
+    uint2 *seg_list = nullptr;
+    uint32_t *seg_count = nullptr;
+    uint32_t ck_k = 0;
 };
 void launch_render_bwd(hipStream_t s, const RenderBwdParams &p);
 

@@ -87,8 +87,14 @@ def main():
     # launch slots: whole tiles (render_fwd_v6 <4, 6>) unless the image is small enough for 4 row-strip parts
     # (launch_render_fwd's fwd_part_slots rule)
     nfwd = T * 4 if T * 4 <= 16384 else T
-    sf, sb = _native.wave_stamps(0, nfwd), _native.wave_stamps(1, T)
-    out = {"fwd": summarise(sf, nfwd), "bwd": summarise(sb, T)}
+    sf = _native.wave_stamps(0, nfwd)
+    # backward slots: one per tile, or one per (tile, segment) work item of the segmented walk (small images); the
+    # stamp buffer starts zeroed and slots past the work list never stamp, so the stamped prefix is the launch
+    import numpy as np
+    sb = _native.wave_stamps(1, 1 << 16)
+    nz = np.nonzero(sb[:, 1])[0]
+    nbwd = int(nz.max()) + 1 if len(nz) else T
+    out = {"fwd": summarise(sf, nfwd), "bwd": summarise(sb, nbwd)}
     print(json.dumps(out, indent=1))
     if args.dump:
         import numpy as np
@@ -100,7 +106,7 @@ def main():
             return img[off: off + 4 * n].view(torch.int32).cpu().numpy().view(np.uint32)
         o_fwd = al(lay["img_tile_loaded"] + 4 * (T + 1))
         o_bwd = al(o_fwd + 4 * (T + 1))
-        np.savez(args.dump, fwd=np.asarray(sf)[:nfwd], bwd=np.asarray(sb)[:T], order_fwd=u32(o_fwd, T),
+        np.savez(args.dump, fwd=np.asarray(sf)[:nfwd], bwd=np.asarray(sb)[:nbwd], order_fwd=u32(o_fwd, T),
                  order_bwd=u32(o_bwd, T), ranges=u32(lay["img_ranges"], 2 * T).reshape(T, 2),
                  tile_last=u32(lay["img_tile_last"], T))
 
