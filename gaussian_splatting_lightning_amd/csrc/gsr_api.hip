@@ -528,7 +528,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             GSR_STAGE(ST_SEG_SORT, dbg, launch_seg_sort(stream, sp));
         } else {
             GSR_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * T, stream));
-            if (lpt) launch_tile_order(stream, im.ranges, nullptr, 0, (int)T, im.order_fwd);
+            if (lpt) launch_tile_order(stream, im.ranges, nullptr, 0, (int)T, im.order_fwd, im.lpt_hist);
         }
     } else {
         if (R > 0) {
@@ -547,7 +547,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             GSR_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * T, stream));
             launch_identify_ranges(stream, b.keys_sorted, R, im.ranges);
         });
-        if (lpt) launch_tile_order(stream, im.ranges, nullptr, 0, (int)T, im.order_fwd);
+        if (lpt) launch_tile_order(stream, im.ranges, nullptr, 0, (int)T, im.order_fwd, im.lpt_hist);
     }
     // split heavy tiles combine tile_last / tile_loaded with atomicMax: start from zero (adjacent arrays; the
     // bucket path's column pass clears them)
@@ -635,7 +635,7 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
         const int lpt = tuning("lpt", 1);
         // "bwd_order" 0: reuse the forward's order (range lengths) and skip the tile_last ordering launch
         const bool own_order = lpt && tuning("bwd_order", 1);
-        if (own_order) launch_tile_order(stream, im.ranges, im.tile_last, 1, (int)T, im.order_bwd);
+        if (own_order) launch_tile_order(stream, im.ranges, im.tile_last, 1, (int)T, im.order_bwd, im.lpt_hist);
         rp.tile_order = lpt ? (own_order ? im.order_bwd : im.order_fwd) : nullptr;
         rp.tile_last = im.tile_last; rp.tile_loaded = im.tile_loaded;
         rp.rec = g.rec;

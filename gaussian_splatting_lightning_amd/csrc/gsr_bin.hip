@@ -36,13 +36,6 @@ namespace gsr {
 // Big Gaussians (every rect cell kept) are spread over the blocks round-robin; a whole block strides over
 // each rect.  The next group's per-Gaussian records are loaded while the current group is walked.
 
-// (row, column) of cell c of a rect of width w: floor((c + 1/2) / w) in fp32 is exact here ((c + 1/2) / w is
-// at least 1/(2w) from an integer and far below 2^20)
-__device__ __forceinline__ uint32_t rect_tile(uint32_t c, uint32_t rx, uint32_t ry, uint32_t w, float inv_w,
-                                              uint32_t gx) {
-    const uint32_t cy = (uint32_t)(((float)c + 0.5f) * inv_w);
-    return (ry + cy) * gx + rx + (c - cy * w);
-}
 
 // Gaussian-order exclusive scan of the kept-tile counts over [g_lo, g_hi) (the instances' Gaussian-major
 // expansion offsets u): the preprocess block totals before g_lo (a multiple of 256) give the base, then a

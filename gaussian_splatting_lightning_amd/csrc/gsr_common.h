@@ -234,6 +234,7 @@ struct ImageState {
     float *ctot;
     uint32_t *ck_flag;
     uint32_t *seg_count;
+    uint32_t *lpt_hist;      // (T / 4096 + 1) x 256: per-workgroup bucket histograms of the multi-workgroup LPT order
 };
 
 inline size_t carve_image(char *base, int W, int H, ImageState &im) {
@@ -257,6 +258,7 @@ inline size_t carve_image(char *base, int W, int H, ImageState &im) {
     im.ctot = c.take<float>(nt <= SEG_MAX_TILES ? nt * 1024 : 1);
     im.ck_flag = c.take<uint32_t>(1);
     im.seg_count = c.take<uint32_t>(1);
+    im.lpt_hist = c.take<uint32_t>((nt / 4096 + 1) * 256);
     return c.off + 256;
 }
 
@@ -732,6 +734,16 @@ __device__ __forceinline__ int wave_inclusive_max(int v) {
     return v;
 }
 
+// Tile of cell c of a rect at (rx, ry) of width w: the row floor((c + 1/2) / w) in fp32 is exact here ((c + 1/2) / w is
+// at least 1/(2w) from an integer and far below 2^20).  Used by the bucket walks and the radix path's expansion.
+// (row, column) of cell c of a rect of width w: floor((c + 1/2) / w) in fp32 is exact here ((c + 1/2) / w is
+// at least 1/(2w) from an integer and far below 2^20)
+__device__ __forceinline__ uint32_t rect_tile(uint32_t c, uint32_t rx, uint32_t ry, uint32_t w, float inv_w,
+                                              uint32_t gx) {
+    const uint32_t cy = (uint32_t)(((float)c + 0.5f) * inv_w);
+    return (ry + cy) * gx + rx + (c - cy * w);
+}
+
 // Orders LDS writes before later LDS reads of other lanes of the SAME wave (no s_barrier).
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -753,9 +765,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 constexpr int LPT_KMAX = 32;
 constexpr int LPT_HIST_WORDS = 256 + 16;  // tile weights a thread keeps in registers (T <= 32 x the workgroup size)
 // One histogram (order == null) or scatter pass over the tiles; item k of thread tid is tile tid + k nt.
-__device__ __forceinline__ void lpt_item(int t, uint32_t wgt, bool valid, uint32_t shift, uint32_t *hist,
-                                         uint32_t *order, int lane, uint64_t lt) {
-    const uint32_t b = valid ? 255u - min(255u, wgt >> shift) : 0u;
+// bucket b of tile t (ballot-matched peers share one LDS atomic): histogram (order == null) or scatter to order
+__device__ __forceinline__ void lpt_item_b(int t, uint32_t b, bool valid, uint32_t *hist, uint32_t *order, int lane,
+                                           uint64_t lt) {
     uint64_t peers = __ballot(valid);
 #pragma unroll
     for (int bit = 0; bit < 8; bit++) {
@@ -771,6 +783,18 @@ __device__ __forceinline__ void lpt_item(int t, uint32_t wgt, bool valid, uint32
         base = (uint32_t)__shfl((int)base, leader);
         if (valid) order[base + (uint32_t)__popcll(lower)] = (uint32_t)t;
     }
+}
+__device__ __forceinline__ void lpt_item(int t, uint32_t wgt, bool valid, uint32_t shift, uint32_t *hist,
+                                         uint32_t *order, int lane, uint64_t lt) {
+    lpt_item_b(t, valid ? 255u - min(255u, wgt >> shift) : 0u, valid, hist, order, lane, lt);
+}
+// Scale-free LPT bucket for the multi-workgroup order (no max pass): heaviest first by the weight's exponent and
+// its next 3 bits (buckets 1/8 of a binade wide); weight 0 last.
+__device__ __forceinline__ uint32_t lpt_log_bucket(uint32_t w) {
+    if (w == 0) return 255u;
+    const uint32_t e = 31u - (uint32_t)__builtin_clz(w);
+    const uint32_t m = e >= 3 ? (w >> (e - 3)) & 7u : (w << (3 - e)) & 7u;
+    return 255u - (e * 8u + m);
 }
 template <class LoadW>
 __device__ __forceinline__ void lpt_walk(int T, bool cached, const uint32_t (&wt)[LPT_KMAX], LoadW load_w,

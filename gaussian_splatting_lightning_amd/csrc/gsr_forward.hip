@@ -446,9 +446,84 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint2 *__restric
     lpt_order_block(ranges, tile_last, use_last, T, shift, order, hist);
 }
 
+// Many tiles (4K: 32400): the order by LPT_WG_TILES-tile workgroups in two launches, a per-workgroup histogram of
+// scale-free buckets (lpt_log_bucket) and a scatter from the bucket bases every workgroup forms from all histograms
+// (one 1024-thread workgroup over 32400 tiles took 40-47 us).
+constexpr int LPT_WG_TILES = 4096;
+__device__ __forceinline__ uint32_t lpt_weight(const uint2 *ranges, const uint32_t *tile_last, int use_last, int t) {
+    return use_last ? tile_last[t] : ranges[t].y - ranges[t].x;
+}
+__global__ __launch_bounds__(1024) void lpt_hist_kernel(const uint2 *__restrict__ ranges,
+                                                        const uint32_t *__restrict__ tile_last, int use_last, int T,
+                                                        uint32_t *__restrict__ ghist) {
+    __shared__ uint32_t hist[256];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const uint64_t lt = lanemask_lt(lane);
+    if (tid < 256) hist[tid] = 0;
+    __syncthreads();
+    constexpr int PER = LPT_WG_TILES / 1024;
+    uint32_t b[PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int t = blockIdx.x * LPT_WG_TILES + q * 1024 + tid;
+        b[q] = t < T ? lpt_log_bucket(lpt_weight(ranges, tile_last, use_last, t)) : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int t = blockIdx.x * LPT_WG_TILES + q * 1024 + tid;
+        lpt_item_b(t, b[q], t < T, hist, nullptr, lane, lt);
+    }
+    __syncthreads();
+    if (tid < 256) ghist[blockIdx.x * 256 + tid] = hist[tid];
+}
+__global__ __launch_bounds__(1024) void lpt_scatter_kernel(const uint2 *__restrict__ ranges,
+                                                           const uint32_t *__restrict__ tile_last, int use_last, int T,
+                                                           const uint32_t *__restrict__ ghist,
+                                                           uint32_t *__restrict__ order) {
+    __shared__ uint32_t hist[256];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const uint64_t lt = lanemask_lt(lane);
+    constexpr int PER = LPT_WG_TILES / 1024;
+    uint32_t b[PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int t = blockIdx.x * LPT_WG_TILES + q * 1024 + tid;
+        b[q] = t < T ? lpt_log_bucket(lpt_weight(ranges, tile_last, use_last, t)) : 0u;
+    }
+    if (tid < 64) {  // bucket bases: all workgroups' earlier buckets, plus this bucket in earlier workgroups
+        uint32_t tot[4] = {0, 0, 0, 0}, pre[4] = {0, 0, 0, 0};
+        for (int g = 0; g < (int)gridDim.x; g++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t v = ghist[g * 256 + 4 * tid + q];
+                tot[q] += v;
+                if (g < (int)blockIdx.x) pre[q] += v;
+            }
+        const uint32_t sum = tot[0] + tot[1] + tot[2] + tot[3];
+        uint32_t run = wave_inclusive_scan(sum, tid) - sum;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            hist[4 * tid + q] = run + pre[q];
+            run += tot[q];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int t = blockIdx.x * LPT_WG_TILES + q * 1024 + tid;
+        lpt_item_b(t, b[q], t < T, hist, order, lane, lt);
+    }
+}
+
 void launch_tile_order(hipStream_t s, const uint2 *ranges, const uint32_t *tile_last, int use_last, int T,
-                       uint32_t *order) {
+                       uint32_t *order, uint32_t *scratch) {
     if (T <= 0) return;
+    if (scratch && T > tuning("lpt_multi_tiles", 16384)) {
+        const uint32_t g = div_up((uint32_t)T, (uint32_t)LPT_WG_TILES);
+        lpt_hist_kernel<<<g, 1024, 0, s>>>(ranges, tile_last, use_last, T, scratch);
+        lpt_scatter_kernel<<<g, 1024, 0, s>>>(ranges, tile_last, use_last, T, scratch, order);
+        return;
+    }
     tile_order_kernel<<<1, 1024, 0, s>>>(ranges, tile_last, use_last, T, tuning("lpt_shift", 3), order);
 }
 

@@ -119,7 +119,7 @@ void launch_seg_sort(hipStream_t s, const SegSortParams &p);
 
 // Tiles ordered by descending work (range length, or tile_last when use_last) for an LPT launch order.
 void launch_tile_order(hipStream_t s, const uint2 *ranges, const uint32_t *tile_last, int use_last, int T,
-                       uint32_t *order);
+                       uint32_t *order, uint32_t *scratch = nullptr);  // scratch: ImageState::lpt_hist
 
 struct RenderFwdParams {
     int W, H, gx, gy, num_tiles;
