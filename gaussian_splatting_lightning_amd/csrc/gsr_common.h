@@ -383,6 +383,31 @@ __host__ __device__ inline bool cull_keep(const CullGauss &g, int tx, int ty, in
     return !(qmin > g.thr);
 }
 
+// Tight rect: the tiles of [x0, x1) x [y0, y1) (the reference rect on entry) that meet the bounding box of the ellipse
+// q <= thr, outside which no pixel centre can pass the compositing test (cull_setup's error-adjusted threshold);
+// tile tx is kept while 16 tx <= x + ex and 16 (tx + 1) > x - ex.  Mode 2 empties the rect, mode 1 keeps it.  Big
+// Gaussians (tight rect > CULL_MAX_AREA tiles) keep their whole tight rect; smaller ones are culled tile by tile
+// inside it.  At 4K with 1 % bloated Gaussians the 3-sigma rects of the big ones held 24 M of 48 M instances.
+__host__ __device__ inline void cull_rect(const CullGauss &g, int &x0, int &y0, int &x1, int &y1) {
+    if (g.mode == 2) {
+        x1 = x0;
+        y1 = y0;
+        return;
+    }
+    if (g.mode == 1) return;
+    const double det = g.a * g.c - g.b * g.b;  // > 0 (lambda_min > 0)
+    const double ex = sqrt(g.thr * g.c / det) * (1.0 + 1e-9) + 1e-6;
+    const double ey = sqrt(g.thr * g.a / det) * (1.0 + 1e-9) + 1e-6;
+    const int tx0 = (int)floor((g.x - ex) / BLOCK_X), tx1 = (int)floor((g.x + ex) / BLOCK_X) + 1;
+    const int ty0 = (int)floor((g.y - ey) / BLOCK_Y), ty1 = (int)floor((g.y + ey) / BLOCK_Y) + 1;
+    x0 = x0 > tx0 ? x0 : tx0;
+    x1 = x1 < tx1 ? x1 : tx1;
+    y0 = y0 > ty0 ? y0 : ty0;
+    y1 = y1 < ty1 ? y1 : ty1;
+    if (x1 < x0) x1 = x0;
+    if (y1 < y0) y1 = y0;
+}
+
 // SH basis constants (utils/sh.py:7-28 of the reference)
 #define GSR_SH_C0 0.28209479177387814f
 #define GSR_SH_C1 0.4886025119029199f

@@ -114,13 +114,21 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
     g.rec[i].c = make_float2(rgb.z, 1.f / pv.z);
     g.clamped[i] = clamp_bits;
     p.radii[i] = (int)radius;
-    ci.need = p.cull && area <= (uint32_t)CULL_MAX_AREA;
-    if (ci.need) ci.cg = cull_setup(pimg.x, pimg.y, conic_x, conic_y, conic_z, opacity);
+    // culling (p.cull): the reference rect shrinks to the tight rect (cull_rect), whose tiles are then tested one by
+    // one when there are at most CULL_MAX_AREA of them
+    uint32_t tarea = area;
+    ci.need = false;
+    if (p.cull) {
+        ci.cg = cull_setup(pimg.x, pimg.y, conic_x, conic_y, conic_z, opacity);
+        cull_rect(ci.cg, rmin.x, rmin.y, rmax.x, rmax.y);
+        tarea = (uint32_t)((rmax.x - rmin.x) * (rmax.y - rmin.y));
+        ci.need = tarea > 0 && tarea <= (uint32_t)CULL_MAX_AREA;
+    }
     ci.rx = rmin.x;
     ci.ry = rmin.y;
     ci.rw = rmax.x - rmin.x;
     ci.depth = __float_as_uint(pv.z);
-    return area;
+    return tarea;
 }
 
 // Exact tile culling is balanced across the wave: the (Gaussian, tile) pairs of all 64 lanes' rects are
