@@ -454,7 +454,7 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint2 *__restric
     lpt_order_block(ranges, tile_last, use_last, T, shift, order, hist);
 }
 
-// Many tiles (4K: 32400): the order by LPT_WG_TILES-tile workgroups in two launches, a per-workgroup histogram of
+// More than 4096 tiles (1080p: 8160, 4K: 32400): the order by LPT_WG_TILES-tile workgroups in two launches, a per-workgroup histogram of
 // scale-free buckets (lpt_log_bucket) and a scatter from the bucket bases every workgroup forms from all histograms
 // (one 1024-thread workgroup over 32400 tiles took 40-47 us).
 constexpr int LPT_WG_TILES = 4096;
@@ -526,7 +526,7 @@ __global__ __launch_bounds__(1024) void lpt_scatter_kernel(const uint2 *__restri
 void launch_tile_order(hipStream_t s, const uint2 *ranges, const uint32_t *tile_last, int use_last, int T,
                        uint32_t *order, uint32_t *scratch) {
     if (T <= 0) return;
-    if (scratch && T > tuning("lpt_multi_tiles", 16384)) {
+    if (scratch && T > tuning("lpt_multi_tiles", 4096)) {  // cfg 3 (8160 tiles): step -12 us against one workgroup (14 us)
         const uint32_t g = div_up((uint32_t)T, (uint32_t)LPT_WG_TILES);
         lpt_hist_kernel<<<g, 1024, 0, s>>>(ranges, tile_last, use_last, T, scratch);
         lpt_scatter_kernel<<<g, 1024, 0, s>>>(ranges, tile_last, use_last, T, scratch, order);
