@@ -54,38 +54,9 @@ __device__ __forceinline__ void cov3d_backward(float3 scale, float mod, float4 r
 // One Gaussian.  In the LDS-staged path (LDS) dL/dsh is not written here: the Gaussian's clamp-masked colour
 // gradient and view direction go to dRGB_out / dir_out (dRGB zero when not visible) for the kernel's staged
 // coalesced store; otherwise dL/dsh is written directly.
-// Per-Gaussian inputs of the geometry / SH part, loaded by the kernel before the row gather so their latency
-// overlaps it (the LDS-staged kernel runs at 4 waves per SIMD, which leaves the registers for them).
-struct PbwdIn {
-    float3 mean, scale;
-    float4 rot;
-    float3 jx, jy, jz;
-    uint32_t clamped;
-};
-__device__ __forceinline__ void pbwd_load(const PreprocessBwdParams &p, int i, PbwdIn &in) {
-    in.mean = load_f3(p.means3D, i);
-    if (!p.cov3D_precomp) {
-        in.scale = load_f3(p.scales, i);
-        in.rot = make_float4(p.rotations[4 * i], p.rotations[4 * i + 1], p.rotations[4 * i + 2], p.rotations[4 * i + 3]);
-    }
-    in.jx = in.jy = in.jz = make_float3(0.f, 0.f, 0.f);
-    in.clamped = 0;
-    if (p.shs && p.M > 0) {
-        in.clamped = p.clamped[i];
-        if (p.D > 0) {
-            const size_t n = (size_t)p.P;
-            const float *J = p.sh_jac + i;
-            in.jx = make_float3(J[0], J[n], J[2 * n]);
-            in.jy = make_float3(J[3 * n], J[4 * n], J[5 * n]);
-            in.jz = make_float3(J[6 * n], J[7 * n], J[8 * n]);
-        }
-    }
-}
-
 template <bool LDS>
 __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p, const int i, bool have_gs,
-                                                   const float (&gs_in)[10], float3 &dRGB_out, float3 &dir_out,
-                                                   const PbwdIn *pre = nullptr) {
+                                                   const float (&gs_in)[10], float3 &dRGB_out, float3 &dir_out) {
     const bool vis = p.radii[i] > 0;
     float gs[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (vis && have_gs && p.tiles[i] <= BIG_GAUSSIAN_TILES) {
@@ -156,7 +127,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
         return;
     }
     const Mat4 view = load_mat4(p.view);
-    const float3 mean = pre ? pre->mean : load_f3(p.means3D, i);
+    const float3 mean = load_f3(p.means3D, i);
     float c6[6];
     float3 scale = make_float3(0, 0, 0);
     float4 rot = make_float4(1, 0, 0, 0);
@@ -164,13 +135,8 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
 #pragma unroll
         for (int k = 0; k < 6; k++) c6[k] = p.cov3D_precomp[6 * i + k];
     } else {
-        if (pre) {
-            scale = pre->scale;
-            rot = pre->rot;
-        } else {
-            scale = load_f3(p.scales, i);
-            rot = make_float4(p.rotations[4 * i], p.rotations[4 * i + 1], p.rotations[4 * i + 2], p.rotations[4 * i + 3]);
-        }
+        scale = load_f3(p.scales, i);
+        rot = make_float4(p.rotations[4 * i], p.rotations[4 * i + 1], p.rotations[4 * i + 2], p.rotations[4 * i + 3]);
         cov3d_from_scale_rot(scale, p.scale_modifier, rot, c6);
     }
     // ---- computeCov2D backward ----
@@ -262,7 +228,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
     // direction Jacobian the forward stored (sh_jac), so the 48 coefficients are not read here.  (The backward's
     // shs are the forward's, as in the autograd function and the upstream API.)
     if (p.shs && p.M > 0) {
-        const uint32_t cl = pre ? pre->clamped : p.clamped[i];
+        const uint8_t cl = p.clamped[i];
         const float3 dRGB = make_float3((cl & 1) ? 0.f : gs[6], (cl & 2) ? 0.f : gs[7], (cl & 4) ? 0.f : gs[8]);
         const float3 campos = make_float3(p.campos[0], p.campos[1], p.campos[2]);
         if (p.dL_dcolors_sh) {
@@ -271,11 +237,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
             p.dL_dcolors_sh[3 * i + 2] = dRGB.z;
         }
         float3 jx = make_float3(0, 0, 0), jy = jx, jz = jx;
-        if (pre) {
-            jx = pre->jx;
-            jy = pre->jy;
-            jz = pre->jz;
-        } else if (p.D > 0) {
+        if (p.D > 0) {
             const size_t n = (size_t)p.P;
             const float *J = p.sh_jac + i;
             jx = make_float3(J[0], J[n], J[2 * n]);
@@ -327,9 +289,6 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
 // writes to its own Gaussian (52 = 4 x 13, 13 odd: 16 lanes of a b128 lane group hit 16 distinct 4-bank windows)
 // are free of bank conflicts.  The coefficients themselves are not read (sh_jac).  A half-wave staging area
 // (6.5 KB, shared with the row-gather chunks) keeps the block at 26 KB of LDS: six blocks, the VGPR limit, per CU.
-#ifndef GSR_PBWD_PREFETCH
-#define GSR_PBWD_PREFETCH 0
-#endif
 constexpr int SH_STRIDE = 52;
 constexpr int PBWD_STAGE = 32 * SH_STRIDE;  // floats of LDS per wave
 template <bool LDS_SH>
@@ -353,10 +312,6 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
     // loops of dependent loads cost ~40 % of the kernel otherwise.  Gaussians above BIG_GAUSSIAN_TILES rows
     // take their block-reduced sum in preprocess_bwd_one.
     float gs[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-#if GSR_PBWD_PREFETCH
-    PbwdIn pre;
-    if (i < p.g1) pbwd_load(p, i, pre);
-#endif
     if (p.rows_by_u) {
         const bool vis = i < p.g1 && p.radii[i] > 0;
         const uint32_t cnt = vis ? p.tiles[i] : 0u;
@@ -413,11 +368,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         }
     }
     float3 dRGB = make_float3(0.f, 0.f, 0.f), dir = make_float3(1.f, 0.f, 0.f);
-#if GSR_PBWD_PREFETCH
-    if (i < p.g1) preprocess_bwd_one<true>(p, i, p.rows_by_u != 0, gs, dRGB, dir, &pre);
-#else
     if (i < p.g1) preprocess_bwd_one<true>(p, i, p.rows_by_u != 0, gs, dRGB, dir);
-#endif
     if (!p.dL_dsh) return;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
