@@ -32,7 +32,8 @@ FLIP_MARGIN = 1.0    # oracle threshold margin below which a pixel is a threshol
 COLOR_TOL = 3e-6     # |colour|, |inverse depth| (relative to max(1, |v|)) on every other pixel; achieved <= 1.31e-6
                      # (SURVEY Appendix A13 asks ~1e-5)
 FLIP_TOL = 2e-2      # anywhere (one alpha = 1/255 or T = 1e-4 flip moves a pixel by < alpha T); achieved <= 3.4e-3
-GRAD_CLEAN_TOL = 5e-6  # gradient rel-L2 over the Gaussians no flip candidate touches; achieved <= 1.95e-6
+GRAD_CLEAN_TOL = 5e-6  # gradient rel-L2 over the Gaussians no flip candidate touches; achieved <= 2.99e-6 (the
+                       # long-tile stress cases, walked in 64-instance segments; <= 1.95e-6 elsewhere)
                        # (A13 asks ~1e-4)
 GRAD_TOL_ADHOC = 2e-6  # cases checked without flip separation (precomputed inputs, the autograd API); achieved 6.2e-7
 
