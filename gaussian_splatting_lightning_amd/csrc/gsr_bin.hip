@@ -201,8 +201,11 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
 // workgroup only waits on workgroups that started before it.  The long tiles are appended to two lists for
 // the workgroup sorts: list 0 holds tiles of (SEG_CAP, SEG_BLOCK_CAP] instances, list 1 longer ones.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void bk_columns_kernel(BucketParams p) {
-    __shared__ uint32_t s_sum[4][64];
+// CW waves per workgroup split the block rows into CW contiguous slices (16: 2048 waves at 1080p instead of 512, a
+// quarter of the dependent load chain per wave).
+template <int CW>
+__global__ __launch_bounds__(64 * CW) void bk_columns_kernel(BucketParams p) {
+    __shared__ uint32_t s_sum[CW][64];
     __shared__ uint32_t s_bid;
     __shared__ unsigned long long s_excl;
     const uint32_t *__restrict__ hist = p.hist;
@@ -213,7 +216,7 @@ __global__ __launch_bounds__(256) void bk_columns_kernel(BucketParams p) {
     __syncthreads();
     const uint32_t bid = s_bid;
     const uint32_t t = bid * 64 + lane;
-    const uint32_t q = (nb + 3) / 4, r0 = min(nb, w * q), r1 = min(nb, r0 + q);
+    const uint32_t q = (nb + CW - 1) / CW, r0 = min(nb, w * q), r1 = min(nb, r0 + q);
     uint32_t sum = 0;
     if (t < T) {
         uint32_t r = r0;
@@ -228,7 +231,9 @@ __global__ __launch_bounds__(256) void bk_columns_kernel(BucketParams p) {
     }
     s_sum[w][lane] = sum;
     __syncthreads();
-    const uint32_t tot = s_sum[0][lane] + s_sum[1][lane] + s_sum[2][lane] + s_sum[3][lane];  // tile total
+    uint32_t tot = 0;  // tile total
+#pragma unroll
+    for (int i = 0; i < CW; i++) tot += s_sum[i][lane];
     if (w == 0) {
         const uint32_t inc = wave_inclusive_scan(tot, lane);
         // fallback aggregate of column workgroup q: its 64 tiles' totals, summed from the (read-only) counts
@@ -738,7 +743,8 @@ static void launch_walk(hipStream_t s, const BucketParams &p, uint32_t grid) {
 
 void launch_bucket_count(hipStream_t s, const BucketParams &p) {
     launch_walk<false>(s, p, p.nb);
-    bk_columns_kernel<<<div_up(p.T, 64), 256, 0, s>>>(p);
+    if (tuning("bk_colw", 16) >= 16) bk_columns_kernel<16><<<div_up(p.T, 64), 1024, 0, s>>>(p);
+    else bk_columns_kernel<4><<<div_up(p.T, 64), 256, 0, s>>>(p);
 }
 
 // plus one workgroup for the forward LPT order when p.order is set
