@@ -432,7 +432,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
         bp.tiles = g.tiles; bp.inst_start = g.inst_start; bp.block_sums = g.block_sums; bp.depth_key = g.depth_key;
         bp.big_list = g.big_list; bp.exp_rec = g.exp_rec;
         bp.hist = im.bk_hist; bp.hist_pre = im.bk_hist_pre; bp.tile_cnt = im.bk_tile_cnt; bp.tile_start = im.bk_tile_start; bp.ranges = im.ranges;
-        bp.tile_last = im.tile_last; bp.tile_loaded = im.tile_loaded;
+        bp.tile_last = im.tile_last; bp.tile_loaded = im.tile_loaded; bp.lpt_bcnt = im.lpt_bcnt;
         bp.ticket = g.counters + CNT_COL_TICKET; bp.tile_status = g.tile_status; bp.err = g.counters + CNT_OVERFLOW;
         bp.long_list = im.bk_long_list; bp.long_cnt = g.counters + CNT_LONG;
         bp.lb_patience = (uint32_t)tuning("lb_patience", 1 << 16); bp.lb_force = tuning("lb_force", 0);
@@ -553,7 +553,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     // bucket path's column pass clears them)
     if (!bucket || R == 0)
         GSR_HIP(hipMemsetAsync(im.tile_last, 0,
-                               (size_t)(reinterpret_cast<char *>(im.tile_loaded + T) -
+                               (size_t)(reinterpret_cast<char *>(im.lpt_bcnt + 256) -
                                         reinterpret_cast<char *>(im.tile_last)),
                                stream));
     RenderFwdParams rp;
@@ -568,6 +568,11 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     // checkpoints for the segmented backward ("bwd_seg" 1, spacing "seg_k" instances: 32 or a multiple of 64) while the image
     // has few tiles; the forward records in ck_flag whether it wrote them, so the backward never reads stale ones
     rp.ck_flag = im.ck_flag;
+    // the backward's LPT order from bucket lists the whole-tile waves append (no ordering launch in the backward)
+    rp.lpt_valid = im.lpt_valid;
+    if (lpt_append_range(T) && lpt && tuning("bwd_order", 1) && tuning("lpt_append", 1)) {
+        rp.lpt_bcnt = im.lpt_bcnt; rp.lpt_blist = im.lpt_blist;
+    }
     if (T <= SEG_MAX_TILES && tuning("bwd_seg", 1)) {
         rp.ckpt = b.ckpt; rp.ctot = im.ctot;
         const int k = tuning("seg_k", 64);  // cfg 2: 32 / 64 / 128 -> render_bwd 0.106 / 0.107 / 0.129 ms, render_fwd 0.070 / 0.065 / 0.062
@@ -635,8 +640,15 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
         const int lpt = tuning("lpt", 1);
         // "bwd_order" 0: reuse the forward's order (range lengths) and skip the tile_last ordering launch
         const bool own_order = lpt && tuning("bwd_order", 1);
-        if (own_order) launch_tile_order(stream, im.ranges, im.tile_last, 1, (int)T, im.order_bwd, im.lpt_hist);
-        rp.tile_order = lpt ? (own_order ? im.order_bwd : im.order_fwd) : nullptr;
+        // in lpt_append_range the forward's whole-tile waves filled the bucket lists (render_bwd falls back to the
+        // identity order if that forward did not, *lpt_valid = 0: the order never changes a result)
+        const bool lists = own_order && lpt_append_range(T) && tuning("lpt_append", 1);
+        if (own_order && !lists)
+            launch_tile_order(stream, im.ranges, im.tile_last, 1, (int)T, im.order_bwd, im.lpt_hist);
+        rp.tile_order = lpt ? (own_order ? (lists ? nullptr : im.order_bwd) : im.order_fwd) : nullptr;
+        if (lists) {
+            rp.lpt_bcnt = im.lpt_bcnt; rp.lpt_blist = im.lpt_blist; rp.lpt_valid = im.lpt_valid;
+        }
         rp.tile_last = im.tile_last; rp.tile_loaded = im.tile_loaded;
         rp.rec = g.rec;
         rp.bg = a->background; rp.final_T = im.final_T; rp.dL_dpix = a->dL_dpix; rp.dL_dinvdepth = a->dL_dinvdepth;

@@ -294,6 +294,8 @@ __global__ __launch_bounds__(64, SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MINW) void ren
         tile = __builtin_amdgcn_readfirstlane((int)item.x);
         seg = __builtin_amdgcn_readfirstlane(item.y);
         ck_k = __builtin_amdgcn_readfirstlane(*p.ck_flag);
+    } else if (p.lpt_blist && __builtin_amdgcn_readfirstlane(*p.lpt_valid)) {
+        tile = lpt_list_tile(p.lpt_bcnt, p.lpt_blist, (uint32_t)p.num_tiles, (uint32_t)slot, lane);
     } else {
         tile = __builtin_amdgcn_readfirstlane(p.tile_order ? (int)p.tile_order[slot] : slot);
     }

@@ -213,6 +213,7 @@ __global__ __launch_bounds__(64 * CW) void bk_columns_kernel(BucketParams p) {
     const uint32_t nb = p.nb, T = p.T;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     if (tid == 0) s_bid = atomicAdd(p.ticket, 1u);
+    if (blockIdx.x == 0 && tid < 256 && p.lpt_bcnt) p.lpt_bcnt[tid] = 0u;
     __syncthreads();
     const uint32_t bid = s_bid;
     const uint32_t t = bid * 64 + lane;

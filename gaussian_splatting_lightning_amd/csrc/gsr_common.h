@@ -217,6 +217,8 @@ struct ImageState {
     uint2 *ranges;        // T
     uint32_t *tile_last;  // T: max n_contrib over the tile's pixels
     uint32_t *tile_loaded; // T: instances of the tile the forward composite gathered (>= tile_last)
+    uint32_t *lpt_bcnt;    // 256: tiles per backward LPT bucket, appended by the forward's whole-tile waves (cleared
+                           //      with tile_last / tile_loaded)
     uint32_t *order_fwd;   // tiles in descending forward work (instances in range), LPT launch order
     uint32_t *order_bwd;   // tiles in descending backward work (tile_last)
     // bucket path count-pass scratch (gsr_bin.hip), here rather than in the binning buffer so that the pass
@@ -235,7 +237,14 @@ struct ImageState {
     uint32_t *ck_flag;
     uint32_t *seg_count;
     uint32_t *lpt_hist;      // (T / 4096 + 1) x 256: per-workgroup bucket histograms of the multi-workgroup LPT order
+    uint32_t *lpt_blist;     // 256 x T in lpt_append_range (else 1): bucket b's tiles at [b T, b T + lpt_bcnt[b])
+    uint32_t *lpt_valid;     // 1 when this forward appended every tile to the bucket lists, else 0
 };
+// Between these tile counts the forward's whole-tile waves append each finished tile to its backward LPT bucket, so
+// the backward needs no ordering launch (1080p, 8160 tiles: step -13 us).  At 4K (32400 tiles of similar weight in a
+// few buckets) the appends' atomics on the same counters cost render_fwd 27 us, more than the launch they save.
+constexpr uint32_t LPT_APPEND_TILES = 4096, LPT_APPEND_MAX_TILES = 16384;
+inline bool lpt_append_range(uint32_t T) { return T > LPT_APPEND_TILES && T <= LPT_APPEND_MAX_TILES; }
 
 inline size_t carve_image(char *base, int W, int H, ImageState &im) {
     Carver c(base);
@@ -246,6 +255,7 @@ inline size_t carve_image(char *base, int W, int H, ImageState &im) {
     im.ranges = c.take<uint2>((size_t)gx * gy + 1);
     im.tile_last = c.take<uint32_t>((size_t)gx * gy + 1);
     im.tile_loaded = c.take<uint32_t>((size_t)gx * gy + 1);
+    im.lpt_bcnt = c.take<uint32_t>(256);
     im.order_fwd = c.take<uint32_t>((size_t)gx * gy + 1);
     im.order_bwd = c.take<uint32_t>((size_t)gx * gy + 1);
     const size_t nt = (size_t)gx * gy;
@@ -259,6 +269,8 @@ inline size_t carve_image(char *base, int W, int H, ImageState &im) {
     im.ck_flag = c.take<uint32_t>(1);
     im.seg_count = c.take<uint32_t>(1);
     im.lpt_hist = c.take<uint32_t>((nt / 4096 + 1) * 256);
+    im.lpt_blist = c.take<uint32_t>(lpt_append_range((uint32_t)nt) ? 256 * nt : 1);
+    im.lpt_valid = c.take<uint32_t>(1);
     return c.off + 256;
 }
 
@@ -787,6 +799,31 @@ __device__ __forceinline__ void wave_lds_sync() {
 //   histogram / scatter iteration (one workgroup over 32400 tiles took 25-30 us);
 // * lanes of a wave with the same bucket share one LDS atomic (ballot-matched peers), so heavily shared buckets do
 //   not serialise.
+// Backward launch slot -> tile from the forward's bucket lists (heaviest bucket first): the wave forms the exclusive
+// prefix of the 256 bucket counts (4 per lane) and picks the bucket holding the slot.  Uniform result.
+__device__ __forceinline__ int lpt_list_tile(const uint32_t *__restrict__ bcnt, const uint32_t *__restrict__ blist,
+                                             uint32_t T, uint32_t slot, int lane) {
+    const uint4 c = reinterpret_cast<const uint4 *>(bcnt)[lane];
+    const uint32_t sum = c.x + c.y + c.z + c.w;
+    const uint32_t pre = wave_inclusive_scan(sum, lane) - sum;
+    const uint32_t p1 = pre + c.x, p2 = p1 + c.y, p3 = p2 + c.z, p4 = p3 + c.w;
+    const bool mine = slot >= pre && slot < p4;
+    const uint64_t m = __ballot(mine);
+    int tile = (int)slot;  // unreachable fallback (the counts cover every tile)
+    if (m) {
+        const int src = __builtin_ctzll(m);
+        uint32_t b = 0, off = 0;
+        if (mine) {
+            b = 4u * (uint32_t)lane + (slot >= p1) + (slot >= p2) + (slot >= p3);
+            off = slot - (slot >= p3 ? p3 : slot >= p2 ? p2 : slot >= p1 ? p1 : pre);
+        }
+        b = (uint32_t)__shfl((int)b, src);
+        off = (uint32_t)__shfl((int)off, src);
+        tile = (int)blist[(size_t)b * T + off];
+    }
+    return __builtin_amdgcn_readfirstlane(tile);
+}
+
 constexpr int LPT_KMAX = 32;
 constexpr int LPT_HIST_WORDS = 256 + 16;  // tile weights a thread keeps in registers (T <= 32 x the workgroup size)
 // One histogram (order == null) or scatter pass over the tiles; item k of thread tid is tile tid + k nt.

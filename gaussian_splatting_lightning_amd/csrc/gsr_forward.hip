@@ -567,6 +567,7 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
     const int lane = threadIdx.x & 63;
     const int slot = blockIdx.x * 4 + w;
     if (p.ck_flag && slot == 0 && lane == 0) *p.ck_flag = CKPT ? p.ck_k : 0u;
+    if (p.lpt_valid && slot == 0 && lane == 0) *p.lpt_valid = (PARTS == 1 && p.lpt_blist) ? 1u : 0u;
     if (slot >= p.num_tiles * PARTS) return;
     const int half = slot % PARTS;
     const int tile = __builtin_amdgcn_readfirstlane(p.tile_order ? (int)p.tile_order[slot / PARTS] : slot / PARTS);
@@ -725,6 +726,11 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
     if (lane == 0) {
         atomicMax(&p.tile_last[tile], mx);
         atomicMax(&p.tile_loaded[tile], loaded_end - r0);
+        if (PARTS == 1 && p.lpt_blist) {  // whole tile: mx is final; append it to its backward LPT bucket
+            const uint32_t b = lpt_log_bucket(mx);
+            const uint32_t pos = atomicAdd(&p.lpt_bcnt[b], 1u);
+            p.lpt_blist[(size_t)b * (uint32_t)p.num_tiles + pos] = (uint32_t)tile;
+        }
     }
     stamp_store(p.stamps, slot, t_start, lane);
 }

@@ -95,6 +95,7 @@ struct BucketParams {
     uint32_t lb_patience;  // look-back polls before recomputing an unpublished predecessor
     int lb_force;          // recompute every predecessor (tests the fallback)
     uint32_t *tile_last, *tile_loaded;  // T each: cleared by the column pass for the forward composite
+    uint32_t *lpt_bcnt;    // 256: cleared by the column pass (the forward's backward-LPT bucket counts)
     unsigned long long *keys;  // R: depth << 32 | u, bucketed by tile
     uint32_t *inst_gid;    // R
     uint32_t *inv;         // R: reset to INV_NONE by the scatter (the forward composite fills it)
@@ -138,6 +139,9 @@ struct RenderFwdParams {
     float *ckpt = nullptr, *ctot = nullptr;
     uint32_t *ck_flag = nullptr;
     uint32_t ck_k = 0;
+    // backward LPT bucket lists (ImageState::lpt_*), or null: whole-tile waves append their tile; *lpt_valid = 1 if
+    // every tile was appended (whole tiles and lists given), else 0
+    uint32_t *lpt_bcnt = nullptr, *lpt_blist = nullptr, *lpt_valid = nullptr;
 };
 void launch_render_fwd(hipStream_t s, const RenderFwdParams &p);
 
@@ -163,6 +167,8 @@ struct RenderBwdParams {
     uint2 *seg_list = nullptr;
     uint32_t *seg_count = nullptr;
     uint32_t ck_k = 0;
+    // launch order from the forward's LPT bucket lists when *lpt_valid (else tile_order / identity)
+    const uint32_t *lpt_bcnt = nullptr, *lpt_blist = nullptr, *lpt_valid = nullptr;
 };
 void launch_render_bwd(hipStream_t s, const RenderBwdParams &p);
 
