@@ -289,6 +289,9 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
 // writes to its own Gaussian (52 = 4 x 13, 13 odd: 16 lanes of a b128 lane group hit 16 distinct 4-bank windows)
 // are free of bank conflicts.  The coefficients themselves are not read (sh_jac).  A half-wave staging area
 // (6.5 KB, shared with the row-gather chunks) keeps the block at 26 KB of LDS: six blocks, the VGPR limit, per CU.
+#ifndef GSR_PBWD_INV_AHEAD
+#define GSR_PBWD_INV_AHEAD 1  // next chunk's inv words during this chunk's row loads: cfg3 0.104 -> 0.100 ms, cfg5 0.521 -> 0.507
+#endif
 constexpr int SH_STRIDE = 52;
 constexpr int PBWD_STAGE = 32 * SH_STRIDE;  // floats of LDS per wave
 template <bool LDS_SH>
@@ -325,12 +328,10 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         static_assert(CH * 10 + 128 <= PBWD_STAGE, "row chunk + meta fit the staging area");
         s_meta[lane] = make_uint2(pst, len ? p.inst_start[i] : 0u);
         wave_lds_sync();
-        for (uint32_t c0 = 0; c0 < total; c0 += CH) {
-            float rw[PER][10];
-            uint32_t sidx[PER];
-            uint32_t uu[PER];
+        // the inv words of chunk c0 (expansion index uu, written-row marker sidx)
+        auto inv_chunk = [&](uint32_t c0, uint32_t (&uu)[PER], uint32_t (&sidx)[PER]) {
 #pragma unroll
-            for (uint32_t r = 0; r < PER; r++) {  // all inv words of the chunk first ...
+            for (uint32_t r = 0; r < PER; r++) {
                 const uint32_t j = c0 + r * 64 + lane;
                 sidx[r] = INV_NONE;
                 uu[r] = 0;
@@ -344,12 +345,33 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
                     sidx[r] = p.inv[uu[r]];
                 }
             }
+        };
+#if GSR_PBWD_INV_AHEAD
+        uint32_t uu_n[PER], sidx_n[PER];
+        if (total) inv_chunk(0, uu_n, sidx_n);
+#endif
+        for (uint32_t c0 = 0; c0 < total; c0 += CH) {
+            float rw[PER][10];
+            uint32_t sidx[PER];
+            uint32_t uu[PER];
+#if GSR_PBWD_INV_AHEAD
+#pragma unroll
+            for (uint32_t r = 0; r < PER; r++) {  // this chunk's inv words, loaded during the previous chunk
+                uu[r] = uu_n[r];
+                sidx[r] = sidx_n[r];
+            }
+#else
+            inv_chunk(c0, uu, sidx);  // all inv words of the chunk first ...
+#endif
 #pragma unroll
             for (uint32_t r = 0; r < PER; r++) {  // ... then only the rows the composite wrote
 #pragma unroll
                 for (int k = 0; k < 10; k++) rw[r][k] = 0.f;
                 if (sidx[r] != INV_NONE) load_row(p.rows, uu[r], rw[r]);
             }
+#if GSR_PBWD_INV_AHEAD
+            if (c0 + CH < total) inv_chunk(c0 + CH, uu_n, sidx_n);  // the next chunk's inv words meanwhile
+#endif
 #pragma unroll
             for (uint32_t r = 0; r < PER; r++) {
                 const uint32_t q = r * 64 + lane;  // pair within the chunk
