@@ -138,7 +138,7 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
 // With p.block_sums (bucket binning) every block also stores its kept-tile total, from which the bucket count
 // pass forms the Gaussian-order instance offsets.
 #ifndef GSR_PRE_MINW
-#define GSR_PRE_MINW 5
+#define GSR_PRE_MINW 4  // 112 VGPRs, no spills: cfg3 0.106 -> 0.103 ms against 5 waves (96 VGPRs, 2 spilled); 6: 0.112
 #endif
 __global__ __launch_bounds__(256, GSR_PRE_MINW) void preprocess_kernel(PreprocessParams p) {
     __shared__ CullGauss s_cg[4][64];
