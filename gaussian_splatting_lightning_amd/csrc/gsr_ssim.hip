@@ -190,7 +190,7 @@ __global__ __launch_bounds__(256) void ssim_bwd_kernel(int H, int W, int tiles_x
 }
 
 // ------------------------------------------------------------------------------------------------
-// Streaming kernels: one wave owns a 64-column strip of SX_CH output rows of one plane and walks its input rows
+// Streaming forward: one wave owns a 64-column strip of SX_CH output rows of one plane and walks its input rows
 // (SX_CH + 10 of them) top to bottom once.  Each row is loaded with coalesced 64-lane loads (plus the 10 halo
 // columns), staged in a 74-float LDS row, filtered horizontally per lane (11 taps, the same FMA order as the tiled
 // kernels), and pushed into a 12-slot ring of horizontal results held in registers; once 11 rows are in, the lane
@@ -296,110 +296,10 @@ __global__ __launch_bounds__(64) void ssim_fwd_stream_kernel(int H, int W, const
     if (lane == 0) partial[((size_t)plane * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] = acc;
 }
 
-__global__ __launch_bounds__(64) void ssim_bwd_stream_kernel(int H, int W, const float *__restrict__ img1,
-                                                             const float *__restrict__ img2, int valid,
-                                                             SsimWindow win, const float *__restrict__ dL_dmean,
-                                                             float inv_n, const float *__restrict__ d_mu1,
-                                                             const float *__restrict__ d_s11,
-                                                             const float *__restrict__ d_s12,
-                                                             float *__restrict__ dL_dimg1) {
-    __shared__ float s_in[3][SX_IW];
-    const int lane = threadIdx.x;
-    const int c0 = blockIdx.x * 64, r0 = blockIdx.y * SX_CH, plane = blockIdx.z;
-    const size_t base = (size_t)plane * H * W;
-    const int nrows = SX_CH + 2 * SS_R;
-    const float g = dL_dmean[0] * inv_n;  // dL/dmap at every counted pixel
-    const int gx0 = c0 - SS_R + lane, gx1 = c0 + 64 - SS_R + lane;
-    auto ld = [&](int gy, int gxx, float (&v)[3]) {
-        const bool in = gy >= 0 && gy < H && gxx >= 0 && gxx < W && ssim_counted(gxx, gy, W, H, valid);
-        const size_t pid = base + (size_t)gy * W + gxx;
-        v[0] = in ? g * d_mu1[pid] : 0.f;
-        v[1] = in ? g * d_s11[pid] : 0.f;
-        v[2] = in ? g * d_s12[pid] : 0.f;
-    };
-    // pf[.][0..5]: the input row's three maps (column, halo column); pf[.][6..7]: img1 / img2 of the output row that
-    // iteration finishes (input row i - 5), loaded with the same lead
-    const int gx = c0 + lane;
-    auto ld_out = [&](int i, float &v1, float &v2) {
-        const int gy = r0 + i - 2 * SS_R;
-        const bool in = i >= 2 * SS_R && gy < H && gx < W;
-        const size_t pid = base + (size_t)gy * W + gx;
-        v1 = in ? img1[pid] : 0.f;
-        v2 = in ? img2[pid] : 0.f;
-    };
-    float pf[SX_PF][8];
-#pragma unroll
-    for (int q = 0; q < SX_PF; q++) {
-        const int gy = r0 - SS_R + q;
-        float a[3], b[3] = {0.f, 0.f, 0.f};
-        ld(gy, gx0, a);
-        if (lane < 2 * SS_R) ld(gy, gx1, b);
-#pragma unroll
-        for (int j = 0; j < 3; j++) {
-            pf[q][j] = a[j];
-            pf[q][3 + j] = b[j];
-        }
-        ld_out(q, pf[q][6], pf[q][7]);
-    }
-    float ring[3][SX_RING];
-    for (int i0 = 0; i0 < nrows; i0 += SX_RING) {
-#pragma unroll
-        for (int u = 0; u < SX_RING; u++) {
-            const int i = i0 + u;
-            if (i >= nrows) break;  // uniform
-            const int slot = u % SX_PF;
-#pragma unroll
-            for (int j = 0; j < 3; j++) {
-                s_in[j][lane] = pf[slot][j];
-                if (lane < 2 * SS_R) s_in[j][64 + lane] = pf[slot][3 + j];
-            }
-            const float x1 = pf[slot][6], x2 = pf[slot][7];
-            if (i + SX_PF < nrows) {
-                const int gy = r0 - SS_R + i + SX_PF;
-                float a[3], b[3] = {0.f, 0.f, 0.f};
-                ld(gy, gx0, a);
-                if (lane < 2 * SS_R) ld(gy, gx1, b);
-#pragma unroll
-                for (int j = 0; j < 3; j++) {
-                    pf[slot][j] = a[j];
-                    pf[slot][3 + j] = b[j];
-                }
-                ld_out(i + SX_PF, pf[slot][6], pf[slot][7]);
-            }
-            wave_lds_sync();
-            float h[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-            for (int k = 0; k < SS_K; k++) {
-                const float wk = win.w[k];
-                h[0] = fmaf(wk, s_in[0][lane + k], h[0]);
-                h[1] = fmaf(wk, s_in[1][lane + k], h[1]);
-                h[2] = fmaf(wk, s_in[2][lane + k], h[2]);
-            }
-            wave_lds_sync();
-#pragma unroll
-            for (int q = 0; q < 3; q++) ring[q][u] = h[q];
-            if (i < 2 * SS_R) continue;
-            const int gy = r0 + i - 2 * SS_R;
-            float a = 0.f, b = 0.f, d = 0.f;
-#pragma unroll
-            for (int k = 0; k < SS_K; k++) {
-                const float wk = win.w[k];
-                const int rk = (u + SX_RING - 2 * SS_R + k) % SX_RING;
-                a = fmaf(wk, ring[0][rk], a);
-                b = fmaf(wk, ring[1][rk], b);
-                d = fmaf(wk, ring[2][rk], d);
-            }
-            if (gx >= W || gy >= H) continue;
-            dL_dimg1[base + (size_t)gy * W + gx] = a + 2.f * x1 * b + x2 * d;
-        }
-    }
-}
-
-// "ssim_stream" bit 0: streaming forward (1080p x 3: 59 us against 86 for the tiled kernel), bit 1: streaming
-// backward (92 us against 72: its per-row LDS round trips at 5 waves per SIMD cost more than the tiled kernel's
-// halo re-reads), so the default streams the forward only
-static bool ssim_stream_fwd() { return (tuning("ssim_stream", 1) & 1) != 0; }
-static bool ssim_stream_bwd() { return (tuning("ssim_stream", 1) & 2) != 0; }
+// "ssim_stream" 1 (default): the streaming forward (1080p x 3: 59-68 us against 86 for the tiled kernel).  A streaming
+// backward of the same shape measured 92 us against the tiled backward's 72 (its per-row LDS round trips at 5 waves
+// per SIMD cost more than the tiled kernel's halo re-reads) and was removed.
+static bool ssim_stream_fwd() { return tuning("ssim_stream", 1) != 0; }
 
 static SsimWindow ssim_window() {
     SsimWindow w;
@@ -435,12 +335,6 @@ void launch_ssim_forward(hipStream_t s, int planes, int H, int W, const float *i
 void launch_ssim_backward(hipStream_t s, int planes, int H, int W, const float *img1, const float *img2, int valid,
                           const float *dL_dmean, float inv_n, const float *d_mu1, const float *d_s11,
                           const float *d_s12, float *dL_dimg1) {
-    if (ssim_stream_bwd()) {
-        const dim3 grid(div_up(W, 64), div_up(H, SX_CH), planes), block(64);
-        ssim_bwd_stream_kernel<<<grid, block, 0, s>>>(H, W, img1, img2, valid, ssim_window(), dL_dmean, inv_n, d_mu1,
-                                                      d_s11, d_s12, dL_dimg1);
-        return;
-    }
     const int tiles_x = div_up(W, SB_TW), tiles = tiles_x * div_up(H, SS_TH);
     const dim3 grid(tiles, planes), block(256);
     ssim_bwd_kernel<<<grid, block, 0, s>>>(H, W, tiles_x, img1, img2, valid, ssim_window(), dL_dmean, inv_n, d_mu1,
