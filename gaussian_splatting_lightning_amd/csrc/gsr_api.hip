@@ -194,12 +194,31 @@ struct StreamDeviceGuard {
 constexpr int kMaxDevices = 64;
 
 // The readback event and pinned words are per thread AND per device: an event recorded on a stream of
-// another device is an invalid handle.
+// another device is an invalid handle.  One holder per thread owns them and releases them when the thread exits.
+struct ReadbackSlots {
+    hipEvent_t ev[64] = {};
+    uint32_t *words[64] = {};
+    ~ReadbackSlots() {
+        for (int d = 0; d < 64; d++) {
+            if (!ev[d] && !words[d]) continue;
+            int prev = -1;
+            if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(d) != hipSuccess) continue;
+            if (ev[d]) (void)hipEventDestroy(ev[d]);
+            if (words[d]) (void)hipHostFree(words[d]);
+            if (prev >= 0) (void)hipSetDevice(prev);
+        }
+    }
+};
+ReadbackSlots &readback_slots() {
+    thread_local ReadbackSlots s;
+    return s;
+}
+
 hipEvent_t readback_event(int dev) {
-    thread_local hipEvent_t e[kMaxDevices] = {};
     if (dev < 0 || dev >= kMaxDevices) return nullptr;
-    if (!e[dev] && hipEventCreateWithFlags(&e[dev], hipEventDisableTiming) != hipSuccess) e[dev] = nullptr;
-    return e[dev];
+    hipEvent_t &e = readback_slots().ev[dev];
+    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+    return e;
 }
 
 // Instance total of the last forward on this thread and device (the binning buffer's pre-wait size hint).
@@ -227,10 +246,17 @@ int wait_readback(const uint32_t *hw, uint32_t seq, hipStream_t s, uint64_t *tot
     const __m128i *src = reinterpret_cast<const __m128i *>(hw + CNT_WORDS);
     auto next_query = std::chrono::steady_clock::now() + std::chrono::milliseconds(1);
     for (uint64_t it = 1;; it++) {
-        const __m128i v = _mm_load_si128((const __m128i *)(volatile const void *)src);
+        // the compiler barrier forces a fresh load every iteration (the GPU writes this memory behind the
+        // compiler's back); a matching sequence word is accepted only when a second 16-B load returns the same
+        // bytes, so even a torn read of the 16-B store could not hand back a stale total
+        asm volatile("" ::: "memory");
+        const __m128i v = _mm_load_si128(src);
         alignas(16) uint32_t w[4];
         _mm_store_si128(reinterpret_cast<__m128i *>(w), v);
         if (w[3] == seq) {
+            asm volatile("" ::: "memory");
+            const __m128i v2 = _mm_load_si128(src);
+            if (_mm_movemask_epi8(_mm_cmpeq_epi8(v, v2)) != 0xffff) continue;
             *total = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
             *nbig = w[2];
             return GSR_OK;
@@ -247,15 +273,26 @@ int wait_readback(const uint32_t *hw, uint32_t seq, hipStream_t s, uint64_t *tot
 }
 
 uint32_t *pinned_words(int dev) {
-    thread_local uint32_t *p[kMaxDevices] = {};
     if (dev < 0 || dev >= kMaxDevices) return nullptr;
-    if (!p[dev]) {
+    uint32_t *&p = readback_slots().words[dev];
+    if (!p) {
         // coherent (fine-grained) pinned memory: the preprocess writes the counters here directly
-        if (hipHostMalloc((void **)&p[dev], 4096, hipHostMallocCoherent) != hipSuccess) p[dev] = nullptr;
-        else memset(p[dev], 0, 4096);
+        if (hipHostMalloc((void **)&p, 4096, hipHostMallocCoherent) != hipSuccess) p = nullptr;
+        else memset(p, 0, 4096);
     }
-    return p[dev];
+    return p;
 }
+
+// Armed while a preprocess that publishes into this thread's pinned words may still be in flight: an early error
+// return then waits for the stream, so the late store of an abandoned sequence number can never land after the
+// next forward's (possibly on another stream) and hide it.
+struct InflightReadback {
+    hipStream_t s = nullptr;
+    bool armed = false;
+    ~InflightReadback() {
+        if (armed) (void)hipStreamSynchronize(s);
+    }
+};
 
 // The decoupled look-backs (instance scan, bucket tile scan, onesweep sorts) never wait on a predecessor that is not
 // running: after lb_patience polls they recompute its aggregate from their input (wave_lookback's decoupled
@@ -415,7 +452,10 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     const uint32_t seq = next_readback_seq(device_guard.dev);
     pp.host_words = rb_spin ? hw : nullptr;
     pp.seq = seq;
+    InflightReadback inflight;
     GSR_STAGE(ST_PREPROCESS, dbg, launch_preprocess(stream, pp));
+    inflight.s = stream;
+    inflight.armed = rb_spin;
     if (!rb_spin) {
         GSR_HIP(hipMemcpyAsync(hw, g.counters, CNT_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
         GSR_HIP(hipEventRecord(rb_ev, stream));
@@ -459,6 +499,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             const int rc = wait_readback(hw, seq, stream, &total64, &nbig);
             if (rc) return rc;
         });
+        inflight.armed = false;
     } else {
         GSR_STAGE(ST_READBACK, dbg, GSR_HIP(hipEventSynchronize(rb_ev)));
         for (int k = 0; k < CNT_NPART; k++) {
