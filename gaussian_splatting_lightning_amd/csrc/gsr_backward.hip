@@ -87,6 +87,9 @@ __device__ __forceinline__ void wave_reduce_pair_store(const float r0[8], const 
         c[m] = dpp_add<0xB1>(c[m]);   // quad_perm [1,0,3,2]
         c[m] = dpp_add<0x4E>(c[m]);   // quad_perm [2,3,0,1]
         c[m] = dpp_add<0x141>(c[m]);  // row_half_mirror
+        // materialise the sums in every lane: otherwise the last add sinks into the masked store blocks and the
+        // row_half_mirror step costs a v_mov_b32_dpp plus a v_add instead of one v_add_f32_dpp
+        asm volatile("" : "+v"(c[m]));
     }
     float *row = hi5 ? (dst1 ? dst1 : dst + PART) : dst;  // instance 1's row: dst1, or the next PART-float row
     const int low = ((lane >> 2) & 2) | ((lane >> 4) & 1);  // 2 b3 + b4
