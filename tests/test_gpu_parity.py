@@ -776,7 +776,12 @@ def test_failed_scratch_allocation_is_a_clean_error(gpu_device, fail_buf, monkey
     with pytest.raises(torch.OutOfMemoryError):
         run_hip(inp, gpu_device, dc, di)
     monkeypatch.undo()
-    again = run_hip(inp, gpu_device, dc, di)
+    # the next forward runs on another stream: a preprocess abandoned by the failed call must not publish its
+    # readback word over this call's (gsr_forward waits for it before returning the error)
+    side = torch.cuda.Stream(device=gpu_device)
+    with torch.cuda.stream(side):
+        again = run_hip(inp, gpu_device, dc, di)
+    side.synchronize()
     assert np.array_equal(ref["color"], again["color"])
     for k in GRADS:
         assert np.array_equal(ref["grads"][k], again["grads"][k]), k
