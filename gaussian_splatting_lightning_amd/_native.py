@@ -94,7 +94,7 @@ EXPORTED_SYMBOLS = (
     "gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_sh_backward_views", "gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes",
     "gsr_image_buffer_bytes", "gsr_bwd_scratch_bytes", "gsr_set_profiling", "gsr_num_stages", "gsr_stage_name",
     "gsr_stage_times", "gsr_reset_stage_times", "gsr_last_error", "gsr_build_info", "gsr_state_layout_query",
-    "gsr_set_tuning", "gsr_ssim_num_partials", "gsr_ssim_forward", "gsr_ssim_backward", "gsr_adam_step",
+    "gsr_set_tuning", "gsr_ssim_num_partials", "gsr_ssim_forward", "gsr_ssim_backward", "gsr_adam_step", "gsr_sparse_adam_step",
     "gsr_densify_workspace_bytes", "gsr_densify_classify", "gsr_densify_apply", "gsr_ply_unpack", "gsr_ply_pack",
     "gsr_knn_workspace_bytes", "gsr_knn_mean_dist2", "gsr_debug_wave_stamps",
 )
@@ -126,6 +126,9 @@ def load(path: str | None = None):
     lib.gsr_adam_step.argtypes = [ctypes.POINTER(AdamGroup), ctypes.c_int, ctypes.c_double, ctypes.c_double,
                                   ctypes.c_double, ctypes.c_void_p]
     lib.gsr_adam_step.restype = ctypes.c_int
+    lib.gsr_sparse_adam_step.argtypes = [ctypes.POINTER(AdamGroup), ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
+                                         ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_void_p]
+    lib.gsr_sparse_adam_step.restype = ctypes.c_int
     lib.gsr_densify_workspace_bytes.argtypes = [ctypes.c_int64]
     lib.gsr_densify_workspace_bytes.restype = ctypes.c_size_t
     lib.gsr_densify_classify.argtypes = [ctypes.POINTER(DensifyArgs), ctypes.c_void_p, ctypes.c_void_p,

@@ -57,6 +57,70 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamLaunch L) {
     }
 }
 
+// SparseGaussianAdam.step(visibility, N) of the upstream rasterizer package (the optimizer the reference's
+// third_party GaussianModel takes with optimizer_type "sparse_adam", gaussian_model.py:26,194-196): only the
+// elements of Gaussians with visibility set are updated, with the upstream kernel's arithmetic -- fixed betas, no
+// bias correction, the step state never advanced:
+//     m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g^2;  p += -lr m / (sqrt(v) + eps)
+// Same slice layout as adam_kernel; a thread's 4 elements may straddle Gaussians (M = 1, 3, 4, 45 ...), so each
+// element takes its own visibility byte, and a thread whose 4 elements are all invisible loads nothing else.
+__device__ __forceinline__ void sparse_adam_one(float &p, float g, float &m, float &v, float b1, float b1c, float b2,
+                                                float b2c, float lr, float eps) {
+    m = b1 * m + b1c * g;
+    v = b2 * v + b2c * g * g;
+    p += -lr * m / (sqrtf(v) + eps);
+}
+
+__global__ __launch_bounds__(256) void sparse_adam_kernel(AdamLaunch L) {
+    int gi = 0;
+#pragma unroll 1
+    while (gi + 1 < L.num_groups && (int64_t)blockIdx.x >= L.slice_start[gi + 1]) gi++;
+    const AdamGroupDev &G = L.g[gi];
+    const int64_t e0 = ((int64_t)blockIdx.x - L.slice_start[gi]) * ADAM_SLICE + (int64_t)threadIdx.x * ADAM_PER;
+    if (e0 >= G.n) return;
+    const int64_t e1 = min(G.n, e0 + ADAM_PER);
+    bool vis[ADAM_PER];
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < ADAM_PER; k++) {
+        vis[k] = e0 + k < e1 && L.visible[(e0 + k) / G.M] != 0;
+        any |= vis[k];
+    }
+    if (!any) return;
+    const float b1 = L.beta1, b1c = L.one_minus_beta1, b2 = L.beta2, b2c = L.one_minus_beta2, eps = L.eps, lr = G.lr;
+    if (G.vec4 && e1 - e0 == ADAM_PER) {
+        float4 p = *reinterpret_cast<const float4 *>(G.param + e0);
+        const float4 g = *reinterpret_cast<const float4 *>(G.grad + e0);
+        float4 m = *reinterpret_cast<const float4 *>(G.exp_avg + e0);
+        float4 v = *reinterpret_cast<const float4 *>(G.exp_avg_sq + e0);
+        float pa[4] = {p.x, p.y, p.z, p.w}, ga[4] = {g.x, g.y, g.z, g.w}, ma[4] = {m.x, m.y, m.z, m.w},
+              va[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            float pk = pa[k], mk = ma[k], vk = va[k];
+            sparse_adam_one(pk, ga[k], mk, vk, b1, b1c, b2, b2c, lr, eps);
+            if (vis[k]) { pa[k] = pk; ma[k] = mk; va[k] = vk; }
+        }
+        *reinterpret_cast<float4 *>(G.param + e0) = make_float4(pa[0], pa[1], pa[2], pa[3]);
+        *reinterpret_cast<float4 *>(G.exp_avg + e0) = make_float4(ma[0], ma[1], ma[2], ma[3]);
+        *reinterpret_cast<float4 *>(G.exp_avg_sq + e0) = make_float4(va[0], va[1], va[2], va[3]);
+    } else {
+        for (int64_t e = e0; e < e1; e++) {
+            if (!vis[e - e0]) continue;
+            float p = G.param[e], m = G.exp_avg[e], v = G.exp_avg_sq[e];
+            sparse_adam_one(p, G.grad[e], m, v, b1, b1c, b2, b2c, lr, eps);
+            G.param[e] = p;
+            G.exp_avg[e] = m;
+            G.exp_avg_sq[e] = v;
+        }
+    }
+}
+
+void launch_sparse_adam(hipStream_t s, const AdamLaunch &L, int64_t total_slices) {
+    if (total_slices <= 0) return;
+    sparse_adam_kernel<<<(unsigned)total_slices, 256, 0, s>>>(L);
+}
+
 int64_t adam_slices(int64_t n) { return (n + ADAM_SLICE - 1) / ADAM_SLICE; }
 
 void launch_adam(hipStream_t s, const AdamLaunch &L, int64_t total_slices) {

@@ -799,6 +799,45 @@ int gsr_adam_step(const gsr_adam_group *groups, int num_groups, double beta1, do
     return GSR_OK;
 }
 
+int gsr_sparse_adam_step(const gsr_adam_group *groups, int num_groups, const uint8_t *visible, int64_t N,
+                         double beta1, double beta2, double eps, void *stream_ptr) {
+    if (num_groups < 0 || num_groups > ADAM_MAX_GROUPS) return fail(GSR_ERR_ARG, "sparse adam: 0..16 parameter groups");
+    if (num_groups && !groups) return fail(GSR_ERR_ARG, "sparse adam: null groups");
+    if (N <= 0) return fail(GSR_ERR_ARG, "sparse adam: N must be positive");
+    if (!visible) return fail(GSR_ERR_ARG, "sparse adam: null visibility");
+    AdamLaunch L{};
+    int64_t slices = 0;
+    int ng = 0;
+    for (int i = 0; i < num_groups; i++) {
+        const gsr_adam_group &g = groups[i];
+        if (g.n < 0) return fail(GSR_ERR_ARG, "sparse adam: n must be >= 0");
+        if (g.n == 0) continue;
+        if (g.n % N != 0) return fail(GSR_ERR_ARG, "sparse adam: a group's element count is not a multiple of N");
+        if (!g.param || !g.grad || !g.exp_avg || !g.exp_avg_sq) return fail(GSR_ERR_ARG, "sparse adam: null array");
+        AdamGroupDev &d = L.g[ng];
+        d.param = g.param; d.grad = g.grad; d.exp_avg = g.exp_avg; d.exp_avg_sq = g.exp_avg_sq; d.n = g.n;
+        d.M = g.n / N;
+        d.lr = (float)g.lr;
+        d.vec4 = ((((uintptr_t)g.param) | ((uintptr_t)g.grad) | ((uintptr_t)g.exp_avg) |
+                   ((uintptr_t)g.exp_avg_sq)) & 15) == 0;
+        L.slice_start[ng] = slices;
+        slices += adam_slices(g.n);
+        ng++;
+    }
+    if (slices > 0x7fffffffLL) return fail(GSR_ERR_ARG, "sparse adam: too many elements");
+    L.num_groups = ng;
+    L.beta1 = (float)beta1;
+    L.one_minus_beta1 = 1.0f - (float)beta1;  // the upstream kernel forms 1 - b1 in float
+    L.beta2 = (float)beta2;
+    L.one_minus_beta2 = 1.0f - (float)beta2;
+    L.eps = (float)eps;
+    L.visible = visible;
+    StreamDeviceGuard device_guard((hipStream_t)stream_ptr);
+    launch_sparse_adam((hipStream_t)stream_ptr, L, slices);
+    GSR_HIP(hipGetLastError());
+    return GSR_OK;
+}
+
 // densify workspace: [dst_map 2N i32 | split_rank N i32 | block_counts 3*blocks i32 | row_class N u8]
 static size_t densify_ws(int64_t N, size_t *o_rank, size_t *o_blk, size_t *o_cls) {
     const size_t nb = (size_t)densify_blocks(N);

@@ -217,15 +217,20 @@ struct AdamGroupDev {
     int64_t n;
     float step_size, bc2_sqrt;
     int vec4;
+    int64_t M;   // sparse step: elements per Gaussian (element e belongs to Gaussian e / M)
+    float lr;    // sparse step: the group's learning rate (no bias correction)
 };
 struct AdamLaunch {
     AdamGroupDev g[ADAM_MAX_GROUPS];
     int64_t slice_start[ADAM_MAX_GROUPS];
     int num_groups;
     float one_minus_beta1, beta2, one_minus_beta2, eps;
+    float beta1;                 // sparse step
+    const uint8_t *visible;      // sparse step: N bytes, nonzero = the Gaussian was rendered this step
 };
 int64_t adam_slices(int64_t n);
 void launch_adam(hipStream_t s, const AdamLaunch &L, int64_t total_slices);
+void launch_sparse_adam(hipStream_t s, const AdamLaunch &L, int64_t total_slices);
 
 // ---- densify_and_prune (gsr_densify.hip) ----
 struct DensifyParams {

@@ -183,6 +183,14 @@ typedef struct gsr_adam_group {
 } gsr_adam_group;
 int gsr_adam_step(const gsr_adam_group *groups, int num_groups, double beta1, double beta2, double eps, void *stream);
 
+/* SparseGaussianAdam.step(visibility, N) of the upstream rasterizer package (diff_gaussian_rasterization, taken by
+ * the reference's third_party GaussianModel with optimizer_type "sparse_adam": gaussian_model.py:26,194-196).  Each
+ * group's n elements are N Gaussians of n / N elements; only the Gaussians with visible[g] != 0 are updated, as
+ * m = b1 m + (1 - b1) g, v = b2 v + (1 - b2) g^2, p += -lr m / (sqrt(v) + eps) -- no bias correction, `step` is
+ * ignored.  visible: N bytes on the device (a torch bool tensor). */
+int gsr_sparse_adam_step(const gsr_adam_group *groups, int num_groups, const uint8_t *visible, int64_t N,
+                         double beta1, double beta2, double eps, void *stream);
+
 /* densify_and_prune of gs_lightning/modules/gaussian_model.py:184-287 with the optimizer-state re-indexing of
  * gs_lightning_module.py:213-235, in two calls:
  *   gsr_densify_classify  classifies every row (prune / keep / clone / split) and builds the row maps;

@@ -164,7 +164,84 @@ def test_no_cpu_fallback():
         densify_and_prune(Model(pp, ss, "cpu"), 0.0002, 0.01, 0.05, 0.4)
 
 
+def sparse_adam_restatement(p, g, m, v, vis, M, lr, eps, b1=0.9, b2=0.999):
+    """The upstream SparseGaussianAdam kernel (diff_gaussian_rasterization adamUpdate, the optimizer of the reference's
+    third_party gaussian_model.py:194-196) as fp32 torch ops: only the visible Gaussians' elements change, no bias
+    correction.  Parity unpinned: the package is an empty submodule here, so this restates its published kernel."""
+    keep = vis.repeat_interleave(M).view(p.shape)
+    f = torch.float32
+    m2 = torch.tensor(b1, dtype=f) * m + torch.tensor(1.0 - b1, dtype=f) * g
+    v2 = torch.tensor(b2, dtype=f) * v + torch.tensor(1.0 - b2, dtype=f) * g * g
+    p2 = p + (-lr) * m2 / (torch.sqrt(v2) + eps)
+    return torch.where(keep, p2, p), torch.where(keep, m2, m), torch.where(keep, v2, v)
+
+
+def test_sparse_adam_is_the_upstream_package_class_and_has_no_cpu_fallback():
+    """`from diff_gaussian_rasterization import SparseGaussianAdam` (third_party gaussian_model.py:26) resolves to the
+    HIP optimizer: upstream constructor (params, lr, eps), a torch.optim.Adam, and a loud error off the GPU."""
+    from diff_gaussian_rasterization import SparseGaussianAdam
+    p = nn.Parameter(torch.zeros(6, 3))
+    opt = SparseGaussianAdam([{"params": [p], "lr": 0.01, "name": "xyz"}], lr=0.0, eps=1e-15)
+    assert isinstance(opt, torch.optim.Adam) and opt.param_groups[0]["name"] == "xyz"
+    opt.step(torch.ones(6, dtype=torch.bool), 6)  # no gradient yet: nothing to do, as upstream
+    p.grad = torch.ones(6, 3)
+    with pytest.raises(RuntimeError, match="GPU"):
+        opt.step(torch.ones(6, dtype=torch.bool), 6)
+    with pytest.raises(ValueError):
+        opt.step(torch.ones(6, dtype=torch.bool), 0)
+    # the restatement leaves invisible Gaussians untouched and matches dense Adam-without-bias-correction elsewhere
+    g = torch.randn(6, 3)
+    vis = torch.tensor([1, 0, 1, 0, 0, 1], dtype=torch.bool)
+    z = torch.zeros(6, 3)
+    p2, m2, v2 = sparse_adam_restatement(z, g, z, z, vis, 3, 0.01, 1e-15)
+    assert torch.equal(p2[~vis], z[~vis]) and torch.equal(m2[~vis], z[~vis])
+    torch.testing.assert_close(p2[vis], -0.01 * (0.1 * g[vis]) / (torch.sqrt(0.001 * g[vis] ** 2) + 1e-15))
+
+
 # ---------------------------------------------------------------------------------------------------- GPU
+
+
+@pytest.mark.gpu
+def test_sparse_adam_matches_restatement():
+    """SparseGaussianAdam.step(visibility, N) over the six reference groups (M = 3, 3, 45, 1, 3, 4 elements per
+    Gaussian, so float4 accesses straddle Gaussians) for 5 steps with a fresh random visibility each step, one
+    group without a gradient in one step: 1e-5 relative / 1e-7 absolute against the fp32 restatement, and the
+    Gaussians never visible bitwise unchanged."""
+    from diff_gaussian_rasterization import SparseGaussianAdam
+    N = 20_001
+    p, s = make_scene(N, seed=5)
+    a = Model(p, s, "cuda")
+    opt = _optimizer(a, SparseGaussianAdam)
+    ref = {k: [getattr(a, f"_{k}").detach().clone(), None, None] for k in NAMES}
+    for k in NAMES:
+        ref[k][1] = torch.zeros_like(ref[k][0])
+        ref[k][2] = torch.zeros_like(ref[k][0])
+    lrs = {g["name"]: g["lr"] for g in opt.param_groups}
+    gen = torch.Generator(device="cuda").manual_seed(1)
+    never = torch.ones(N, dtype=torch.bool, device="cuda")
+    for step in range(5):
+        vis = torch.rand(N, device="cuda", generator=gen) < 0.6
+        never &= ~vis
+        for k in NAMES:
+            prm = getattr(a, f"_{k}")
+            if step == 2 and k == "rotation":
+                prm.grad = None
+                continue
+            g = torch.randn(prm.shape, device="cuda", generator=gen) * 10 ** (-(step % 3))
+            prm.grad = g.clone()
+            M = prm.numel() // N
+            ref[k] = list(sparse_adam_restatement(ref[k][0], g, ref[k][1], ref[k][2], vis, M, lrs[k], 1e-15))
+        opt.step(vis, N)
+    torch.cuda.synchronize()
+    for k in NAMES:
+        prm = getattr(a, f"_{k}")
+        st = opt.state[prm]
+        torch.testing.assert_close(prm.detach(), ref[k][0], rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(st["exp_avg"], ref[k][1], rtol=1e-5, atol=1e-9)
+        torch.testing.assert_close(st["exp_avg_sq"], ref[k][2], rtol=1e-5, atol=1e-12)
+        assert float(st["step"]) == 0.0  # upstream never advances it
+        rows = never.repeat_interleave(prm.numel() // N).view(prm.shape)
+        assert torch.equal(prm.detach()[rows], torch.tensor(p[k], device="cuda")[rows]), k
 
 
 def _optimizer(model, cls, lrs=None):

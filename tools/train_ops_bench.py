@@ -2,7 +2,7 @@
 """Per-step optimizer and densification cost at the cfg3 scale (1M Gaussians, SH degree 3).
 
 * Adam: GaussianAdam.step() (one fused launch over the six groups) vs torch.optim.Adam (foreach, the
-  reference's optimizer) on the same parameters.  Algorithmic bytes per element: read param, grad, exp_avg,
+  reference's optimizer) on the same parameters; SparseGaussianAdam.step(visibility, N) at 100 % / 60 % visible.  Algorithmic bytes per element: read param, grad, exp_avg,
   exp_avg_sq (16 B) + write param, exp_avg, exp_avg_sq (12 B) = 28 B; 59 floats per Gaussian.
 * densify_and_prune (+ optimizer-state re-indexing): gaussian_splatting_lightning_amd.densify vs the
   reference's torch op sequence (gaussian_model.py:184-287 + gs_lightning_module.py:213-235) on the GPU.
@@ -163,6 +163,25 @@ def main():
                    "speedup": round(res["torch_foreach"] / res["fused"], 2), "algorithmic_bytes": algo,
                    "achieved_GBps": round(algo / (res["fused"] * 1e-3) / 1e9, 1), "hbm_peak_GBps": 8000.0,
                    "frac": round(algo / (res["fused"] * 1e-3) / 1e9 / 8000.0, 4)}
+
+    # ---- SparseGaussianAdam.step(visibility, N) (upstream package optimizer, third_party optimizer_type
+    # "sparse_adam"): bytes scale with the visible fraction (28 B per visible element + 1 B per Gaussian) ----
+    from gaussian_splatting_lightning_amd.optim import SparseGaussianAdam
+    sp = {}
+    for frac in (1.0, 0.6):
+        m = make_model(N, torch, nn)
+        opt = optimizer(m, lambda groups, lr, eps: SparseGaussianAdam(groups, lr=lr, eps=eps))
+        for k in NAMES:
+            p = getattr(m, f"_{k}")
+            p.grad = torch.randn_like(p)
+        vis = torch.rand(N, device="cuda") < frac
+        nvis = int(vis.sum().item())
+        ms = timed(lambda: opt.step(vis, N), 50, torch)
+        algo_s = 28 * 59 * nvis + N
+        sp[f"visible_{frac}"] = {"ms": round(ms, 4), "algorithmic_bytes": algo_s,
+                                 "achieved_GBps": round(algo_s / (ms * 1e-3) / 1e9, 1),
+                                 "frac": round(algo_s / (ms * 1e-3) / 1e9 / 8000.0, 4)}
+    out["sparse_adam"] = sp
 
     # ---- densify_and_prune + optimizer re-indexing (fresh model per run: the op changes N) ----
     thr = (0.0002, 0.01, 0.05, 0.4, 20.0)
