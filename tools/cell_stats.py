@@ -52,6 +52,55 @@ def strip_mask_exact(x, y, A, B, C, o, row0, col0):
     return m
 
 
+def quad_mask_exact(x, y, A, B, C, o, row0, col0):
+    """strip_mask_exact's bound per 8-column half of the tile, tested against the two 8-row bands: (n,) -> (n, 4)
+    bool, bit 2 qy + qx for the quadrant (qx, qy)."""
+    out = []
+    for qy in range(2):
+        for qx in range(2):
+            m = strip_mask_exact_band(x, y, A, B, C, o, row0, col0 + 8 * qx, 7)
+            lo, hi = m
+            out.append((hi >= 8 * qy) & (lo <= 8 * qy + 7))
+    m = np.stack(out, 1)
+    f = np.float32
+    with np.errstate(all="ignore"):
+        o255 = f(255) * np.asarray(o, f)
+        A, B, C = (np.asarray(v, f) for v in (A, B, C))
+        det = A * C - B * B
+        hd = f(0.5) * (A - C)
+        lmin = f(0.5) * (A + C) - np.sqrt(hd * hd + B * B)
+        eps = f(1e-5) * (np.abs(A) + np.abs(B) + np.abs(C)) / lmin
+        V = np.sqrt(((f(2) * np.log(np.maximum(o255 * f(1.00001), f(1))) + f(1e-3)) / (f(1) - eps)) * A / det)
+        keep_all = ~((det > 0) & (lmin > 0) & (eps < 1e-2) & (V < 1e6)) | np.isnan(o255)
+    m[keep_all] = True
+    m[o255 < 0.999] = False
+    return m
+
+
+def strip_mask_exact_band(x, y, A, B, C, o, row0, col0, width):
+    """The (lo, hi) row interval (tile-relative) of strip_mask_exact over the columns [col0, col0 + width]."""
+    f = np.float32
+    x, y, A, B, C, o = (np.asarray(v, f) for v in (x, y, A, B, C, o))
+    with np.errstate(all="ignore"):
+        o255 = f(255) * o
+        det = A * C - B * B
+        hd = f(0.5) * (A - C)
+        lmin = f(0.5) * (A + C) - np.sqrt(hd * hd + B * B)
+        eps = f(1e-5) * (np.abs(A) + np.abs(B) + np.abs(C)) / lmin
+        tau = (f(2) * np.log(np.maximum(o255 * f(1.00001), f(1))) + f(1e-3)) / (f(1) - eps)
+        V = np.sqrt(tau * A / det)
+        uL = f(col0) - x
+        uR = uL + f(width)
+        ut = -B * V / A
+        ic, ctau = f(1) / C, C * tau
+        u = np.minimum(np.maximum(ut, uL), uR)
+        vmax = np.where((ut >= uL) & (ut <= uR), V, (-B * u + np.sqrt(np.maximum(ctau - det * u * u, 0))) * ic)
+        u = np.minimum(np.maximum(-ut, uL), uR)
+        vmin = np.where((-ut >= uL) & (-ut <= uR), -V, (-B * u - np.sqrt(np.maximum(ctau - det * u * u, 0))) * ic)
+        mg = f(1e-2) * V + f(1e-3) * (np.abs(uL) + np.abs(uR)) + f(0.0625)
+        return y + vmin - mg - f(row0), y + vmax + mg - f(row0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg2")
@@ -81,7 +130,7 @@ def main():
     ly, lx = ly.reshape(-1), lx.reshape(-1)
     strip_of = ly // 4
     quad_of = (ly // 8) * 2 + (lx // 8)
-    tot = dict(strip_fn=0, strip_fn_miss=0, pairs=0, strip_band=0, quad_box=0, quad_exact=0, strip_exact=0, quad_active=0, strip_active=0,
+    tot = dict(quad_fn=0, quad_fn_miss=0, strip_fn=0, strip_fn_miss=0, pairs=0, strip_band=0, quad_box=0, quad_exact=0, strip_exact=0, quad_active=0, strip_active=0,
                active_pairs=0, fwd_pairs_tile=0, strip_fn_lastc=0, need_cmp=0, inst_dead=0)
     for t in tiles:
         tx, ty = t % gx, t // gx
@@ -121,6 +170,11 @@ def main():
             tot["quad_active"] += int(act[:, quad_of == q].any(1).sum())
         sm = strip_mask_exact(m[:, 0], m[:, 1], c[:, 0], c[:, 1], c[:, 2], c[:, 3], r0y, r0x)
         tot["strip_fn"] += int(sm.sum())
+        qm = quad_mask_exact(m[:, 0], m[:, 1], c[:, 0], c[:, 1], c[:, 2], c[:, 3], r0y, r0x)
+        tot["quad_fn"] += int(qm.sum())
+        for q in range(4):
+            qy, qx = q // 2, q % 2
+            tot["quad_fn_miss"] += int((ok[:, quad_of == qy * 2 + qx] .any(1) & ~qm[:, q]).sum())
         tot["inst_dead"] += int((~act.any(1)).sum())
         idx = np.arange(last)
         for k in range(4):
@@ -137,10 +191,11 @@ def main():
     cells = tot["pairs"] // 64
     print(f"{args.config}: tiles {len(tiles)}, walked (tile, instance) pairs {tot['pairs'] // 256}, "
           f"active pixel pairs {tot['active_pairs']} ({tot['active_pairs'] / tot['pairs']:.3f} of walked)")
-    print(f"  strip_mask_exact: misses {tot['strip_fn_miss']} (must be 0)")
+    print(f"  strip_mask_exact: misses {tot['strip_fn_miss']} (must be 0); quad_mask_exact misses {tot['quad_fn_miss']}")
     print(f"  walked instances contributing to no pixel: {tot['inst_dead'] / (tot['pairs'] // 256):.3f}; "
           f"strip evaluations needing the n_contrib compare: {tot['need_cmp'] / max(tot['strip_fn_lastc'], 1):.3f}")
-    for k in ("strip_band", "strip_fn", "strip_fn_lastc", "strip_exact", "strip_active", "quad_box", "quad_exact", "quad_active"):
+    for k in ("strip_band", "strip_fn", "strip_fn_lastc", "strip_exact", "strip_active", "quad_box", "quad_fn", "quad_exact",
+              "quad_active"):
         print(f"  {k:12s} live cells {tot[k]:>12d}  {tot[k] / cells:.3f} of all, "
               f"active-pixel density {tot['active_pairs'] / max(tot[k] * 64, 1):.3f}")
 
