@@ -1,6 +1,7 @@
 // gsr_torch_ext.cpp -- the thin torch extension of the drop-in: the `_C` module of the diff_gaussian_rasterization
 // package, with the pybind entry points the upstream package exports (graphdeco-inria/diff-gaussian-rasterization
-// @dr_aa, ext.cpp / rasterize_points.h: rasterize_gaussians, rasterize_gaussians_backward, mark_visible; SURVEY.md
+// @dr_aa, ext.cpp / rasterize_points.h: rasterize_gaussians, rasterize_gaussians_backward, mark_visible, and adam.h's
+// adamUpdate behind SparseGaussianAdam; SURVEY.md
 // §8(b) "C-ABI / extension"), implemented over the C ABI of libgsrast.so (include/gsrast.h).  Tensors in, tensors
 // out, on torch's current HIP stream; the scratch buffers are uint8 tensors grown through the ABI's allocation
 // callback (the upstream resizeFunctional, notes/rasterizer_note.h:27-40).  The reference never calls _C itself
@@ -154,8 +155,30 @@ torch::Tensor mark_visible(const torch::Tensor &means3D, const torch::Tensor &vi
     return present;
 }
 
+// adamUpdate (the upstream package's SparseGaussianAdam step, adam.h): param, exp_avg, exp_avg_sq updated in place
+// for the Gaussians with visible set; N Gaussians of M elements each
+void adamUpdate(torch::Tensor &param, torch::Tensor &param_grad, torch::Tensor &exp_avg, torch::Tensor &exp_avg_sq,
+                torch::Tensor &visible, const float lr, const float b1, const float b2, const float eps, const uint32_t N,
+                const uint32_t M) {
+    const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(param.device());
+    for (const torch::Tensor *t : {&param, &param_grad, &exp_avg, &exp_avg_sq}) {
+        TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kFloat32 && t->is_contiguous(),
+                    "adamUpdate: param, grad and moments must be contiguous float32 HIP tensors");
+        TORCH_CHECK(t->numel() == (int64_t)N * M, "adamUpdate: tensors must hold N x M elements");
+    }
+    TORCH_CHECK(visible.is_cuda() && visible.numel() == (int64_t)N && visible.element_size() == 1 && visible.is_contiguous(),
+                "adamUpdate: visible must be a contiguous (N,) bool HIP tensor");
+    if ((int64_t)N * M == 0) return;
+    gsr_adam_group g{param.data_ptr<float>(), param_grad.data_ptr<float>(), exp_avg.data_ptr<float>(),
+                     exp_avg_sq.data_ptr<float>(), (int64_t)N * M, (double)lr, 0};
+    check(gsr_sparse_adam_step(&g, 1, reinterpret_cast<const uint8_t *>(visible.data_ptr()), (int64_t)N, (double)b1,
+                               (double)b2, (double)eps, stream_of(param)),
+          "adamUpdate");
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("rasterize_gaussians", &rasterize_gaussians);
     m.def("rasterize_gaussians_backward", &rasterize_gaussians_backward);
     m.def("mark_visible", &mark_visible);
+    m.def("adamUpdate", &adamUpdate);
 }

@@ -16,7 +16,7 @@ def test_extension_exports_upstream_entry_points():
     if not os.path.exists(EXT):
         pytest.skip("diff_gaussian_rasterization/_C.so not built (gaussian_splatting_lightning_amd.build)")
     from diff_gaussian_rasterization import _C
-    for name in ("rasterize_gaussians", "rasterize_gaussians_backward", "mark_visible"):
+    for name in ("rasterize_gaussians", "rasterize_gaussians_backward", "mark_visible", "adamUpdate"):
         assert callable(getattr(_C, name)), name
 
 
@@ -56,3 +56,26 @@ def test_extension_matches_python_path_bitwise(gpu_device, stress):
     from gaussian_splatting_lightning_amd.rasterizer import mark_visible
     assert torch.equal(vis, mark_visible(t["means3D"], rs.viewmatrix, rs.projmatrix))
     assert np.any(vis.cpu().numpy())
+
+
+@pytest.mark.gpu
+def test_extension_adam_update_is_the_sparse_adam_step(gpu_device):
+    """_C.adamUpdate (upstream adam.h, called by SparseGaussianAdam.step) writes bit for bit what the Python
+    SparseGaussianAdam writes for the same group: both launch gsr_sparse_adam_step."""
+    from diff_gaussian_rasterization import SparseGaussianAdam, _C
+    N, M = 5003, 3
+    gen = torch.Generator(device=gpu_device).manual_seed(3)
+    p0 = torch.randn(N, M, device=gpu_device, generator=gen)
+    g = torch.randn(N, M, device=gpu_device, generator=gen)
+    vis = torch.rand(N, device=gpu_device, generator=gen) < 0.5
+    a = torch.nn.Parameter(p0.clone())
+    a.grad = g.clone()
+    opt = SparseGaussianAdam([a], lr=0.01, eps=1e-15)
+    opt.step(vis, N)
+    opt.step(vis, N)
+    b, m, v = p0.clone(), torch.zeros_like(p0), torch.zeros_like(p0)
+    for _ in range(2):
+        _C.adamUpdate(b, g, m, v, vis, 0.01, 0.9, 0.999, 1e-15, N, M)
+    torch.cuda.synchronize()
+    assert torch.equal(a.detach(), b)
+    assert torch.equal(opt.state[a]["exp_avg"], m) and torch.equal(opt.state[a]["exp_avg_sq"], v)
