@@ -452,10 +452,10 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     const uint32_t seq = next_readback_seq(device_guard.dev);
     pp.host_words = rb_spin ? hw : nullptr;
     pp.seq = seq;
-    InflightReadback inflight;
-    GSR_STAGE(ST_PREPROCESS, dbg, launch_preprocess(stream, pp));
+    InflightReadback inflight;  // armed before the launch: an error reported after it still waits for the kernel
     inflight.s = stream;
     inflight.armed = rb_spin;
+    GSR_STAGE(ST_PREPROCESS, dbg, launch_preprocess(stream, pp));
     if (!rb_spin) {
         GSR_HIP(hipMemcpyAsync(hw, g.counters, CNT_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
         GSR_HIP(hipEventRecord(rb_ev, stream));
