@@ -323,6 +323,8 @@ def main():
                                     if use_events else "none")},
         **({"multi_gpu_note": "the RCCL exchange cannot be rehearsed on a 1-GPU box (RCCL rejects two ranks on one "
                               "device); gloo world-size-2 tests cover its logic (DESIGN.md §6)"} if world > 1 else {}),
+        # also the evaluated (pixel, Gaussian) pairs per second, sum(n_contrib) of every view / step
+        "contrib_pairs_per_s": world * sum_contrib / (ms_per_step * 1e-3),
         "step_events_ms": step_events,
         "roofline": roofline, "cpu_baseline": cpu,
         "stages_ms": {k: round(v, 4) for k, v in stage_avg.items() if v > 0},
