@@ -467,13 +467,13 @@ __global__ __launch_bounds__(64, SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MINW) void ren
         }
         while (un) {
             const int j0 = (int)__builtin_ctzll(un);
-            un &= un - 1;
+            un &= ~(1ull << j0);  // s_andn2 with the strip tests' bit (un & (un - 1) costs three SALU)
             float m0[8];
             const uint64_t any0 = pass(j0, m0);
             float *dst = s_part[j0];
             if (un) {
                 const int j1 = (int)__builtin_ctzll(un);
-                un &= un - 1;
+                un &= ~(1ull << j1);
                 float m1[8];
                 const uint64_t any1 = pass(j1, m1);
                 float *dst1 = s_part[j1];

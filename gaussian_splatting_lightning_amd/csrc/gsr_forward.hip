@@ -638,8 +638,8 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
         auto walk = [&](uint64_t &un) {
         while (un) {
             const uint32_t j = (uint32_t)__builtin_ctzll(un);
-            un &= un - 1;
             const uint64_t bit = 1ull << j;
+            un &= ~bit;  // one s_andn2_b64 with the bit the strip tests need anyway (un & (un - 1) costs three SALU)
             const float4 a = sr[j].a, b = sr[j].b;
             const float2 c = sr[j].c;
             contributor = cbase + j + 1;
