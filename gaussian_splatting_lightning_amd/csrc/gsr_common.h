@@ -49,7 +49,7 @@ constexpr int RS_TILE = RS_THREADS * RS_ITEMS;  // 4096 keys per block
 constexpr int RS_BINS = 256;
 constexpr int SCAN_TILE = 4096;
 constexpr int SCAN_MAX_BLOCKS = 1024 * 16;  // single-block scan of block sums
-constexpr uint32_t RS_COL_CHUNK = 128;      // radix count-matrix rows (histogram blocks) per column-scan workgroup
+constexpr uint32_t RS_COL_CHUNK = 32;  // smallest radix count-matrix row chunk per column-scan workgroup (sizes scan_tmp)
 
 inline uint32_t div_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 

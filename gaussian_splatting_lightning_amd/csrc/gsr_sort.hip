@@ -256,12 +256,12 @@ __global__ __launch_bounds__(256) void rs_hist_kernel(const uint32_t *__restrict
 // The count matrix is block-major -- [block][digit], one coalesced 1 KB row per histogram block, read back as one
 // row by that block's scatter -- where a digit-major matrix scattered 4-B writes and reads over nb x 256 cache
 // lines per pass (at 48M keys ~200 MB of partial-line traffic for 6 MB of counts).  The scan runs in (digit,
-// block) order over it in three short launches: column sums of RS_COL_CHUNK-row chunks, one workgroup scanning the
+// block) order over it in three short launches: column sums of row chunks (launch_count_scan), one workgroup scanning the
 // chunk sums per digit and the digit totals, then every chunk's rows.
 __global__ __launch_bounds__(256) void rs_colsum_kernel(const uint32_t *__restrict__ counts, uint32_t nb,
-                                                        uint32_t *__restrict__ colsum) {
+                                                        uint32_t chunk, uint32_t *__restrict__ colsum) {
     const uint32_t c = blockIdx.x, d = threadIdx.x;
-    const uint32_t b0 = c * RS_COL_CHUNK, b1 = min(nb, b0 + RS_COL_CHUNK);
+    const uint32_t b0 = c * chunk, b1 = min(nb, b0 + chunk);
     uint32_t s = 0;
     uint32_t b = b0;
     for (; b + 8 <= b1; b += 8) {
@@ -275,28 +275,37 @@ __global__ __launch_bounds__(256) void rs_colsum_kernel(const uint32_t *__restri
     colsum[(size_t)c * RS_BINS + d] = s;
 }
 
+// One workgroup, thread d = digit: the exclusive prefix of column d over the chunks (the chunk sums of 16 chunks are
+// loaded together, so the chain costs one memory round trip per 16 chunks, not one per chunk), then the exclusive
+// digit offsets into row nchunks (added by rs_colbase_kernel instead of a second pass over the chunks here).
 __global__ __launch_bounds__(256) void rs_colscan_kernel(uint32_t *__restrict__ colsum, uint32_t nchunks) {
     __shared__ uint32_t s_w[4];
     const int d = threadIdx.x, lane = d & 63, w = d >> 6;
+    constexpr uint32_t G = 16;
     uint32_t run = 0;
-    for (uint32_t c = 0; c < nchunks; c++) {  // per digit: exclusive over the chunks
-        const uint32_t v = colsum[(size_t)c * RS_BINS + d];
-        colsum[(size_t)c * RS_BINS + d] = run;
-        run += v;
+    for (uint32_t c0 = 0; c0 < nchunks; c0 += G) {
+        uint32_t v[G];
+#pragma unroll
+        for (uint32_t i = 0; i < G; i++) v[i] = c0 + i < nchunks ? colsum[(size_t)(c0 + i) * RS_BINS + d] : 0u;
+#pragma unroll
+        for (uint32_t i = 0; i < G; i++) {
+            if (c0 + i < nchunks) colsum[(size_t)(c0 + i) * RS_BINS + d] = run;
+            run += v[i];
+        }
     }
     const uint32_t inc = wave_inclusive_scan(run, lane);  // digit totals -> exclusive digit offsets
     if (lane == 63) s_w[w] = inc;
     __syncthreads();
     uint32_t off = inc - run;
     for (int i = 0; i < w; i++) off += s_w[i];
-    for (uint32_t c = 0; c < nchunks; c++) colsum[(size_t)c * RS_BINS + d] += off;
+    colsum[(size_t)nchunks * RS_BINS + d] = off;
 }
 
-__global__ __launch_bounds__(256) void rs_colbase_kernel(uint32_t *__restrict__ counts, uint32_t nb,
+__global__ __launch_bounds__(256) void rs_colbase_kernel(uint32_t *__restrict__ counts, uint32_t nb, uint32_t chunk,
                                                          const uint32_t *__restrict__ colsum) {
     const uint32_t c = blockIdx.x, d = threadIdx.x;
-    const uint32_t b0 = c * RS_COL_CHUNK, b1 = min(nb, b0 + RS_COL_CHUNK);
-    uint32_t run = colsum[(size_t)c * RS_BINS + d];
+    const uint32_t b0 = c * chunk, b1 = min(nb, b0 + chunk);
+    uint32_t run = colsum[(size_t)c * RS_BINS + d] + colsum[(size_t)gridDim.x * RS_BINS + d];
     uint32_t b = b0;
     for (; b + 8 <= b1; b += 8) {
         uint32_t v[8];
@@ -315,11 +324,15 @@ __global__ __launch_bounds__(256) void rs_colbase_kernel(uint32_t *__restrict__ 
     }
 }
 
+// Chunk rows per column workgroup: the column chains (chunk / 8 round trips in colsum and colbase) against the
+// chunk-sum chain (nch / 16 in colscan).  cfg 5 (round 3): the 1221-row depth-sort matrices 0.280 -> 0.259 ms with 32
+// rows (0.271 with 128), the 4822-row tile-sort matrices 0.531 -> 0.513 ms with 128 (0.520 with 32).
 static void launch_count_scan(hipStream_t s, uint32_t *counts, uint32_t nb, uint32_t *colsum) {
-    const uint32_t nch = div_up(nb, RS_COL_CHUNK);
-    rs_colsum_kernel<<<nch, RS_BINS, 0, s>>>(counts, nb, colsum);
+    const uint32_t chunk = nb <= 2048u ? RS_COL_CHUNK : 4u * RS_COL_CHUNK;  // colsum is sized for RS_COL_CHUNK
+    const uint32_t nch = div_up(nb, chunk);
+    rs_colsum_kernel<<<nch, RS_BINS, 0, s>>>(counts, nb, chunk, colsum);
     rs_colscan_kernel<<<1, RS_BINS, 0, s>>>(colsum, nch);
-    rs_colbase_kernel<<<nch, RS_BINS, 0, s>>>(counts, nb, colsum);
+    rs_colbase_kernel<<<nch, RS_BINS, 0, s>>>(counts, nb, chunk, colsum);
 }
 
 // ------------------------------------------------------------------------------------------------
