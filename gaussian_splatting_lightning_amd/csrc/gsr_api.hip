@@ -579,10 +579,17 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             ep.exp_sorted = sorted_exp ? g.exp_sorted : nullptr;
             ep.exp_owner = tuning("exp_owner", 1) ? b.exp_owner : nullptr;
             ep.keys_out = b.sort.k[0]; ep.inst_gid = b.inst_gid; ep.inst_start = g.inst_start;
+#ifndef GSR_EXP_INV
+#define GSR_EXP_INV 1
+#endif
+            // inv = INV_NONE for every instance: written by the expansion beside its keys (16-B stores at the same
+            // indices), or by a separate fill ("exp_inv" 0)
+            const bool exp_inv = tuning("exp_inv", GSR_EXP_INV) != 0;
+            ep.inv_none = exp_inv ? b.inv : nullptr;
             GSR_STAGE(ST_EXPAND, dbg, launch_expand(stream, ep));
             GSR_STAGE(ST_TILE_SORT, dbg,
                       launch_radix_sort(stream, b.sort, R, tile_key_bits(T), false, nullptr, nullptr, &tile_onesweep));
-            GSR_HIP(hipMemsetAsync(b.inv, 0xff, sizeof(uint32_t) * (size_t)R, stream));
+            if (!exp_inv) GSR_HIP(hipMemsetAsync(b.inv, 0xff, sizeof(uint32_t) * (size_t)R, stream));
         }
         GSR_STAGE(ST_RANGES, dbg, {
             GSR_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * T, stream));

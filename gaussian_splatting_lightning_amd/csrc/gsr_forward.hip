@@ -376,10 +376,12 @@ __global__ __launch_bounds__(256) void expand_kernel(ExpandParams p) {
         static_assert(EXP_PER == 4, "one uint4 store per thread");
         *reinterpret_cast<uint4 *>(p.keys_out + ub) = make_uint4(key[0], key[1], key[2], key[3]);
         *reinterpret_cast<uint4 *>(p.inst_gid + ub) = make_uint4(gv[0], gv[1], gv[2], gv[3]);
+        if (p.inv_none) *reinterpret_cast<uint4 *>(p.inv_none + ub) = make_uint4(INV_NONE, INV_NONE, INV_NONE, INV_NONE);
     } else {
         for (uint32_t u = ub; u < u1; u++) {
             p.keys_out[u] = key[u - ub];
             p.inst_gid[u] = gv[u - ub];
+            if (p.inv_none) p.inv_none[u] = INV_NONE;
         }
     }
 }

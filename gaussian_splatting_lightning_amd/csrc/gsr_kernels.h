@@ -68,6 +68,7 @@ struct ExpandParams {
     const uint4 *exp_sorted;  // optional: exp_rec already in depth order (read by rank, no gather)
     uint32_t *exp_owner;      // optional: owner ranks of the block starts (div_up(R, EXP_TILE) + 1 words)
     uint32_t *keys_out, *inst_gid, *inst_start;
+    uint32_t *inv_none;       // optional: inv, set to INV_NONE for every instance here (no separate fill)
 };
 void launch_expand(hipStream_t s, const ExpandParams &p);
 
