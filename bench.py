@@ -72,6 +72,9 @@ def parse():
                     help="N>1 gradient exchange (gaussian_splatting_lightning_amd/multiview.py)")
     ap.add_argument("--exchange-chunks", type=int, default=4,
                     help="N>1: Gaussian chunks whose exchange overlaps the rest of the backward (1: after it)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="take the N>1 path (process group, RCCL exchange) even with one rank, e.g. under "
+                         "torchrun --nproc-per-node 1")
     return ap.parse_args()
 
 
@@ -94,7 +97,11 @@ def main():
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     dev = torch.device("cuda", local_rank % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
-    if world > 1:
+    distributed = world > 1 or args.force_dist
+    if distributed:
+        if "MASTER_ADDR" not in os.environ:  # --force-dist without a launcher: a one-rank group on this host
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("MASTER_PORT", "29531"),
+                              RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:  # rehearsal of the N>1 path on fewer GPUs than ranks (RCCL needs one GPU per rank)
@@ -118,10 +125,11 @@ def main():
 
     # Per-Gaussian gradient destinations + the cross-rank exchange (multiview.py): one view per rank; dense
     # all-reduce at N=1 (nothing to exchange), compact SH exchange at N>1 unless --exchange dense.
-    mode = args.exchange if world > 1 else "dense"
+    mode = args.exchange if distributed else "dense"
     # N>1: the backward's per-Gaussian stage runs in --exchange-chunks Gaussian ranges and each range's collectives
     # are issued as soon as it is enqueued (overlap with the rest of the backward); N=1: one chunk, nothing to send
-    red = ViewGradReducer(n, M, deg, dev, mode=mode, chunks=args.exchange_chunks if world > 1 else 1)
+    red = ViewGradReducer(n, M, deg, dev, mode=mode, chunks=args.exchange_chunks if distributed else 1)
+    assert red.distributed == distributed
 
     def step():
         color, radii, invd, st = forward_raw(sc.means3D, sc.shs, None, sc.opacities, sc.scales, sc.rotations, None,
@@ -173,7 +181,7 @@ def main():
     t_w = time.perf_counter()
     while True:
         more = torch.tensor([1.0 if time.perf_counter() - t_w < SETTLE_S else 0.0], device=dev)
-        if world > 1:
+        if distributed:
             dist.all_reduce(more, op=dist.ReduceOp.MAX)
         if more.item() == 0.0:
             break
@@ -182,7 +190,7 @@ def main():
         torch.cuda.synchronize()
     if use_events:
         _native.set_tuning("prof_mask", _native.stage_mask(dom))
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -191,14 +199,14 @@ def main():
             _native.set_profiling(i % EVENT_EVERY == 0)
         st = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     gc.enable()
     _native.set_profiling(False)
     _native.set_tuning("prof_mask", -1)
     timed_stages = _native.stage_times()
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -210,7 +218,7 @@ def main():
     n_ev = max(args.steps, 20)
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev + 1)]
     gc.disable()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     evs[0].record()
@@ -321,8 +329,9 @@ def main():
                    "stage_events": (f"timed steps: dominant kernel only, every {EVENT_EVERY}th step; stages_ms: "
                                     "separate untimed pass"
                                     if use_events else "none")},
-        **({"multi_gpu_note": "the RCCL exchange cannot be rehearsed on a 1-GPU box (RCCL rejects two ranks on one "
-                              "device); gloo world-size-2 tests cover its logic (DESIGN.md §6)"} if world > 1 else {}),
+        **({"distributed": {"backend": dist.get_backend(), "world_size": world,
+                            "note": "process group initialised: every step ran the exchange's collectives"}}
+           if distributed else {}),
         # also the contributing (pixel, Gaussian) pairs per second (this rank's sum(n_contrib) x N)
         "contrib_pairs_per_s": world * sum_contrib / (ms_per_step * 1e-3),
         "step_events_ms": step_events,
@@ -331,7 +340,7 @@ def main():
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

@@ -79,7 +79,8 @@ class ViewGradReducer:
 
     def __init__(self, n: int, M: int, sh_degree: int, device, mode: str = "compact", group=None,
                  world_size: Optional[int] = None,
-                 sh_views_fn: Optional[Callable[..., torch.Tensor]] = None, chunks: int = 1):
+                 sh_views_fn: Optional[Callable[..., torch.Tensor]] = None, chunks: int = 1,
+                 distributed: Optional[bool] = None):
         if mode not in ("dense", "compact"):
             raise ValueError(f"mode must be 'dense' or 'compact', got {mode!r}")
         self.n, self.M, self.D = int(n), int(M), int(sh_degree)
@@ -87,8 +88,13 @@ class ViewGradReducer:
         self.mode = mode
         self.compact = mode == "compact"
         self.group = group
+        # Collectives run whenever a process group exists, even of one rank (the RCCL code path then executes on a
+        # single GPU exactly as it does on eight); distributed=False keeps a reducer local inside a process group.
+        if distributed is None:
+            distributed = bool(dist.is_available() and dist.is_initialized())
+        self.distributed = bool(distributed)
         self.world = int(world_size if world_size is not None else
-                         (dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1))
+                         (dist.get_world_size(group) if self.distributed else 1))
         self._sh_views = sh_views_fn or sh_backward_views
         self.widths = dict(means3D=3, scales=3, rotations=4, opacities=1, shs=3 * self.M)
         self.fields = FIELDS_COMPACT if self.compact else FIELDS_DENSE
@@ -140,6 +146,7 @@ class ViewGradReducer:
         """Whole-range destinations for backward_raw(out=..., accumulate_stats=True) (chunks == 1 only)."""
         if self.chunks != 1:
             raise RuntimeError("backward_out() is the unchunked form; use chunk_outputs() with backward_chunked")
+        self._check_not_synced()
         v = self.chunk_views[0]
         out = dict(means3D=v["means3D"], scales=v["scales"], rotations=v["rotations"], opacities=v["opacities"],
                    means2D=self.means2D, densify_stats=self.stats_accum, max_radii2D=self.radii_max)
@@ -157,6 +164,7 @@ class ViewGradReducer:
 
     def chunk_outputs(self) -> List[Tuple[int, int, Dict[str, torch.Tensor]]]:
         """(g_begin, g_end, destinations) per chunk, for rasterizer.backward_chunked."""
+        self._check_not_synced()
         res = []
         for c, (g0, g1) in enumerate(self.bounds):
             v = self.chunk_views[c]
@@ -173,6 +181,7 @@ class ViewGradReducer:
     def record_view(self, dmeans2D: torch.Tensor, radii: torch.Tensor) -> None:
         """Accumulate one view's densification statistics (gaussian_model.py:175-181) when the backward did not
         (backward_raw without backward_out()'s densify_stats / max_radii2D)."""
+        self._check_not_synced()
         self.stats_accum[:, 0] += torch.linalg.vector_norm(dmeans2D[:, :2], dim=1)
         self.stats_accum[:, 1] += (radii > 0).to(torch.float32)
         torch.maximum(self.radii_max, radii.to(torch.int32), out=self.radii_max)
@@ -184,8 +193,9 @@ class ViewGradReducer:
         self._materialised = None
         if not self.compact:
             return
+        self._check_not_synced()
         self.campos_in.copy_(campos.reshape(3))
-        if self.world > 1:
+        if self.distributed:
             self._campos_work = _all_gather(self.campos_all, self.campos_in, self.group)
         else:
             self.campos_all[0].copy_(self.campos_in)
@@ -195,7 +205,7 @@ class ViewGradReducer:
         """Chunk c's gradients have been enqueued on the current stream: issue its collectives (async).  The
         all-gather goes first, so the SH expansion that needs it can start while the all-reduce still runs."""
         gather = reduce = None
-        if self.world > 1:
+        if self.distributed:
             if self.compact:
                 gather = _all_gather(self.gather_all[c], self.gather_in[c], self.group)
             reduce = dist.all_reduce(self.chunk_flat[c], group=self.group, async_op=True)
@@ -212,7 +222,7 @@ class ViewGradReducer:
             if gather is not None:
                 gather.wait()
             g0, g1 = self.bounds[c]
-            factors = self.gather_all[c] if self.world > 1 else self.gather_in[c].unsqueeze(0)
+            factors = self.gather_all[c] if self.distributed else self.gather_in[c].unsqueeze(0)
             self._sh_views(means3D[g0:g1], self.campos_all, factors, self.D, self.M, out=self.shs[g0:g1])
         for _, _, reduce in self._pending:
             if reduce is not None:
@@ -229,14 +239,20 @@ class ViewGradReducer:
     def sync_densify_stats(self):
         """SUM the accumulated statistics and MAX the radii over ranks, in place; returns (stats, radii_max):
         stats (n, 2) = [sum of ||dL/dmeans2D[:, :2]||, number of visible views] since the last reset.  Reduces once
-        per reset_densify_stats(); accumulate further views only after that reset."""
-        if self.world > 1 and not self._stats_synced:  # idempotent until reset: a second call must not re-add
+        per reset_densify_stats(); accumulating further views before that reset raises (a second reduction would
+        count the other ranks' views twice)."""
+        if self.distributed and not self._stats_synced:  # idempotent until reset: a second call must not re-add
             work = [dist.all_reduce(self.stats_accum, group=self.group, async_op=True),
                     dist.all_reduce(self.radii_max, op=dist.ReduceOp.MAX, group=self.group, async_op=True)]
             for w in work:
                 w.wait()
         self._stats_synced = True
         return self.stats_accum, self.radii_max
+
+    def _check_not_synced(self) -> None:
+        if self._stats_synced and self.distributed:
+            raise RuntimeError("densification statistics were reduced over ranks (sync_densify_stats); call "
+                               "reset_densify_stats() before accumulating more views")
 
     def reset_densify_stats(self) -> None:
         """After densifying (the reference zeroes xyz_gradient_accum, denom and max_radii2D there)."""

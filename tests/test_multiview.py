@@ -73,3 +73,41 @@ def test_chunked_exchange_is_bitwise_the_unchunked_one(tmp_path, mode):
     for r in range(2):
         for k in ("means3D", "scales", "rotations", "opacities", "stats", "radii_max", "shs"):
             assert np.array_equal(one[r][k], four[r][k]), (r, k)
+
+
+def test_one_rank_group_takes_the_collective_path_and_guards_resync():
+    """A process group of ONE rank still runs the exchange's collectives (the code path an N-GPU node runs), with the
+    local path's results; statistics accumulated after sync_densify_stats and before reset_densify_stats raise (a
+    second reduction would add the other ranks' views twice)."""
+    import torch
+    import torch.distributed as dist
+    from gaussian_splatting_lightning_amd.multiview import ViewGradReducer
+    if dist.is_initialized():
+        pytest.skip("a process group already exists in this process")
+    n = 1000
+    g = torch.Generator().manual_seed(0)
+    dm = torch.randn(n, 3, generator=g)
+    radii = torch.randint(0, 5, (n,), generator=g, dtype=torch.int32)
+    local = ViewGradReducer(n, 16, 3, "cpu", mode="dense", chunks=3)
+    assert not local.distributed
+    dist.init_process_group("gloo", store=dist.HashStore(), rank=0, world_size=1)
+    try:
+        red = ViewGradReducer(n, 16, 3, "cpu", mode="dense", chunks=3)
+        assert red.distributed and red.world == 1
+        for r in (local, red):
+            r.record_view(dm, radii)
+            r.flat.copy_(torch.arange(r.flat.numel(), dtype=torch.float32))
+            r.begin_step(torch.zeros(3))
+            for c in range(r.chunks):
+                r.start_chunk(c)
+            r.finish(None)
+        assert torch.equal(local.flat, red.flat)
+        s_red, m_red = red.sync_densify_stats()
+        s_loc, m_loc = local.sync_densify_stats()
+        assert torch.equal(s_red, s_loc) and torch.equal(m_red, m_loc)
+        with pytest.raises(RuntimeError):
+            red.record_view(dm, radii)
+        red.reset_densify_stats()
+        red.record_view(dm, radii)
+    finally:
+        dist.destroy_process_group()

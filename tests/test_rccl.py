@@ -1,0 +1,77 @@
+"""The RCCL exchange of multiview.py, executed on the GPU with a one-rank process group.
+
+The gradient exchange of the one-view-per-GPU split (the reference consumes the reduced gradients
+in gs_lightning/lightning/gs_lightning_module.py:167-169 and the per-view statistics of
+gs_lightning/modules/gaussian_model.py:175-181) issues its collectives whenever a process group exists.  With one
+rank every collective is an identity, so the reduced gradients, statistics and radii must be bitwise those of the
+local (no-group) path -- and the RCCL calls themselves (`init_process_group("nccl", device_id=)`,
+`all_gather_into_tensor`, the async all-reduce handles and their waits) run on real hardware.
+"""
+import pytest
+import torch
+import torch.distributed as dist
+
+from tests.helpers import scene_inputs, settings_for, upstream
+
+pytestmark = pytest.mark.gpu
+
+
+def _step(red, st, rs, dc, di, means3D, chunked):
+    from gaussian_splatting_lightning_amd.rasterizer import backward_chunked, backward_raw
+    if chunked:
+        red.begin_step(rs.campos)
+        backward_chunked(st, rs, dc, di, red.chunk_outputs(), on_chunk=red.start_chunk, compact_sh=red.compact,
+                         accumulate_stats=True)
+        red.finish(means3D)
+    else:
+        backward_raw(st, rs, dc, di, **red.backward_kwargs())
+        red.reduce(means3D, rs.campos)
+
+
+def _run(dev, distributed, mode, chunks, views=2):
+    from gaussian_splatting_lightning_amd.multiview import ViewGradReducer
+    from gaussian_splatting_lightning_amd.rasterizer import forward_raw
+    n, W, H = 30_000, 320, 240
+    red = ViewGradReducer(n, 16, 3, dev, mode=mode, chunks=chunks, distributed=distributed)
+    assert red.distributed == distributed
+    for v in range(views):  # two steps: the statistics accumulate over views before the sync
+        inp = scene_inputs(n, W, H, sh_degree=3, seed=12, stress_fraction=0.01, view_index=v, num_views=4)
+        rs = settings_for(inp, dev)
+        t = {k: torch.as_tensor(inp[k], device=dev) for k in ("means3D", "opacities", "scales", "rotations", "shs")}
+        dc, di = (torch.as_tensor(a, device=dev) for a in upstream(W, H, seed=12 + v))
+        _, radii, _, st = forward_raw(t["means3D"], t["shs"], None, t["opacities"], t["scales"], t["rotations"],
+                                      None, rs)
+        _step(red, st, rs, dc, di, t["means3D"], chunks > 1)
+    torch.cuda.synchronize()
+    grads = {k: g.clone() for k, g in red.grads.items()}
+    stats, rmax = red.sync_densify_stats()
+    torch.cuda.synchronize()
+    return grads, stats.clone(), rmax.clone(), red
+
+
+@pytest.mark.parametrize("mode,chunks", [("compact", 4), ("dense", 4), ("compact", 1)])
+def test_rccl_exchange_one_rank_is_bitwise_local(gpu_device, mode, chunks):
+    ref = _run(gpu_device, False, mode, chunks)
+    assert not dist.is_initialized()
+    torch.cuda.set_device(gpu_device)
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=gpu_device)
+    try:
+        got = _run(gpu_device, True, mode, chunks)
+        red = got[3]
+        # the RCCL branch really ran: the chunk gathers landed in the (world, L, 3) buffers
+        if mode == "compact":
+            for c in range(red.chunks):
+                assert torch.equal(red.gather_all[c][0], red.gather_in[c])
+        # a second reduction before reset would count other ranks' views twice: accumulating after a sync raises
+        with pytest.raises(RuntimeError):
+            red.begin_step(torch.zeros(3, device=gpu_device))
+        red.reset_densify_stats()
+        red.begin_step(torch.zeros(3, device=gpu_device))
+        red.finish(None)  # waits for the camera-position gather before the group goes
+    finally:
+        dist.destroy_process_group()
+    for k in ref[0]:
+        assert torch.equal(ref[0][k], got[0][k]), k
+    assert torch.equal(ref[1], got[1])
+    assert torch.equal(ref[2], got[2])
+    assert float(got[1][:, 1].max()) == 2.0  # two views accumulated before the sync
