@@ -476,6 +476,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
         bp.ticket = g.counters + CNT_COL_TICKET; bp.tile_status = g.tile_status; bp.err = g.counters + CNT_OVERFLOW;
         bp.long_list = im.bk_long_list; bp.long_cnt = g.counters + CNT_LONG;
         bp.lb_patience = (uint32_t)tuning("lb_patience", 1 << 16); bp.lb_force = tuning("lb_force", 0);
+        bp.xcd_major = tuning("bk_xcd", 1);
         GSR_STAGE(ST_BK_COUNT, dbg, launch_bucket_count(stream, bp));
     }
     // The binning buffer's size depends on the instance total.  Requesting it through the caller's allocator

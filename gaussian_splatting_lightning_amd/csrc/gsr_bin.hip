@@ -203,6 +203,29 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
 // ------------------------------------------------------------------------------------------------
 // CW waves per workgroup split the block rows into CW contiguous slices (16: 2048 waves at 1080p instead of 512, a
 // quarter of the dependent load chain per wave).
+//
+// Bucket layout (p.xcd_major): a tile's bucket holds the runs of the walk blocks in the order the column prefix visits
+// them, and the per-tile sort makes that order irrelevant to the result.  Visiting the blocks XCD-major -- all blocks
+// b = x (mod 8) first, then x + 1, ... -- puts the runs that blocks sharing an XCD write (observed round-robin
+// placement, MI355X_MICROARCH.md "Workgroup dispatch") next to each other, so a 128-B line of keys is filled by one
+// XCD's L2 instead of partly by several (each writing back its own dirty part): runs are ~2 instances per (block,
+// tile) at 1080p.  Position r of the visiting order -> block.
+__device__ __forceinline__ uint32_t bk_row_block(uint32_t r, uint32_t nb, int xcd_major) {
+    if (!xcd_major) return r;
+    const uint32_t q = nb >> 3, rem = nb & 7u;  // XCD groups x < rem hold q + 1 blocks, the others q
+    const uint32_t big = rem * (q + 1);
+    uint32_t x, k;
+    if (r < big) {
+        x = r / (q + 1);
+        k = r - x * (q + 1);
+    } else {
+        const uint32_t r2 = r - big;
+        x = rem + r2 / q;
+        k = r2 - (x - rem) * q;
+    }
+    return k * 8 + x;
+}
+
 template <int CW>
 __global__ __launch_bounds__(64 * CW) void bk_columns_kernel(BucketParams p) {
     __shared__ uint32_t s_sum[CW][64];
@@ -219,16 +242,17 @@ __global__ __launch_bounds__(64 * CW) void bk_columns_kernel(BucketParams p) {
     const uint32_t t = bid * 64 + lane;
     const uint32_t q = (nb + CW - 1) / CW, r0 = min(nb, w * q), r1 = min(nb, r0 + q);
     uint32_t sum = 0;
+    const int xm = p.xcd_major;
     if (t < T) {
         uint32_t r = r0;
         for (; r + 8 <= r1; r += 8) {
             uint32_t v[8];
 #pragma unroll
-            for (int i = 0; i < 8; i++) v[i] = hist[(size_t)(r + i) * T + t];
+            for (int i = 0; i < 8; i++) v[i] = hist[(size_t)bk_row_block(r + i, nb, xm) * T + t];
 #pragma unroll
             for (int i = 0; i < 8; i++) sum += v[i];
         }
-        for (; r < r1; r++) sum += hist[(size_t)r * T + t];
+        for (; r < r1; r++) sum += hist[(size_t)bk_row_block(r, nb, xm) * T + t];
     }
     s_sum[w][lane] = sum;
     __syncthreads();
@@ -275,17 +299,22 @@ __global__ __launch_bounds__(64 * CW) void bk_columns_kernel(BucketParams p) {
         uint32_t r = r0;
         for (; r + 8 <= r1; r += 8) {
             uint32_t v[8];
-#pragma unroll
-            for (int i = 0; i < 8; i++) v[i] = hist[(size_t)(r + i) * T + t];
+            size_t row[8];
 #pragma unroll
             for (int i = 0; i < 8; i++) {
-                hist_pre[(size_t)(r + i) * T + t] = run;
+                row[i] = (size_t)bk_row_block(r + i, nb, xm) * T + t;
+                v[i] = hist[row[i]];
+            }
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                hist_pre[row[i]] = run;
                 run += v[i];
             }
         }
         for (; r < r1; r++) {
-            const uint32_t v = hist[(size_t)r * T + t];
-            hist_pre[(size_t)r * T + t] = run;
+            const size_t row = (size_t)bk_row_block(r, nb, xm) * T + t;
+            const uint32_t v = hist[row];
+            hist_pre[row] = run;
             run += v;
         }
     }

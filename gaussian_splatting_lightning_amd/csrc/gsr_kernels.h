@@ -102,6 +102,7 @@ struct BucketParams {
     uint32_t *inv;         // R: reset to INV_NONE by the scatter (the forward composite fills it)
     uint32_t *order;       // scatter: an extra workgroup writes the forward LPT order here (or null: none)
     int lpt_shift;
+    int xcd_major;         // bucket runs in XCD-major block order (bk_row_block)
 };
 void launch_bucket_count(hipStream_t s, const BucketParams &p);    // walk + column prefixes + tile ranges
 void launch_bucket_scatter(hipStream_t s, const BucketParams &p);
