@@ -239,13 +239,23 @@ def main():
     nc = st.image_buffer[lay["img_n_contrib"]: lay["img_n_contrib"] + 4 * npix].view(torch.int32)
     sum_contrib = int(nc.sum(dtype=torch.int64).item())
     I = st.num_rendered
+    # The composite passes touch only the instances they walk: the forward loads a tile's instances up to the batch in
+    # which its last pixel terminates (sum of tile_loaded), the backward walks each tile from its last contributor
+    # (sum of tile_last) and zeroes the rows of the loaded-but-not-contributing rest.  At cfg 3, 57 % of the
+    # instances lie beyond tile_loaded and are never read, so SURVEY.md §8(d)'s per-instance figures are charged
+    # for these counts; the figure over all I instances stays beside it as "nominal_bytes_per_launch".
+    tl_sum = int(st.image_buffer[lay["img_tile_last"]: lay["img_tile_last"] + 4 * T].view(torch.int32)
+                 .sum(dtype=torch.int64).item())
+    ld_sum = int(st.image_buffer[lay["img_tile_loaded"]: lay["img_tile_loaded"] + 4 * T].view(torch.int32)
+                 .sum(dtype=torch.int64).item())
     algo_bytes = {
         # F6 composite fwd = 8 B/T + 44 B/I + 24 B/P; B1 composite bwd adds 40 B/I of grads
-        "render_fwd": 8 * T + 44 * I + 24 * npix,
-        "render_bwd": 8 * T + 44 * I + 24 * npix + 40 * I,
+        "render_fwd": 8 * T + 44 * ld_sum + 24 * npix,
+        "render_bwd": 8 * T + (44 + 40) * tl_sum + 40 * (ld_sum - tl_sum) + 24 * npix,
         "preprocess": n * (40 + 12 * M) + n * (48 + 36),  # + the SH colour's direction Jacobian (9 floats)
         "preprocess_bwd": n * (40 + 12 * M) + 88 * n + n * (56 + 12 * M),
     }
+    nominal_bytes = {"render_fwd": 8 * T + 44 * I + 24 * npix, "render_bwd": 8 * T + 44 * I + 24 * npix + 40 * I}
     flops = {"render_fwd": 25.0 * sum_contrib, "render_bwd": 70.0 * sum_contrib}
     tot, calls = timed_stages.get(dom, (0.0, 0))
     dom_ms = tot / calls if calls else 0.0  # measured over the timed steps
@@ -285,7 +295,12 @@ def main():
                     "unit": "TFLOP/s", "frac": round(tflops / FP32_VALU_PEAK_TF, 4), "traffic": traffic,
                     "algorithmic_flops_per_launch": flops[dom], "avg_launch_ms": round(dom_ms, 4),
                     "hbm": {"achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": algo_bytes[dom]},
+                            "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": algo_bytes[dom],
+                            "instances_walked": tl_sum, "instances_loaded": ld_sum, "instances_total": I,
+                            "nominal_bytes_per_launch": nominal_bytes.get(dom),
+                            "note": "algorithmic bytes charge SURVEY §8(d)'s 44 B (+40 B gradient row) per instance the "
+                                    "pass loads (sum tile_loaded) / walks (sum tile_last), not per binned instance; "
+                                    "nominal_bytes_per_launch is the all-instance figure"},
                     "valu_issue": issue,
                     "note": "fp32 VALU bound (no MFMA work on this path); flops = 25 (fwd) / 70 (bwd) per pair x "
                             "sum(n_contrib) (SURVEY §8(d)); traffic = PMC HBM bytes per launch "

@@ -315,6 +315,36 @@ def test_autograd_api_and_means2d(gpu_device):
     assert torch.all(screen.grad[~vis] == 0)
 
 
+def test_inference_call_with_means2d_none(gpu_device):
+    """The render script's call (scripts/render_trained_image.py:115-124): means2D=None, grad-requiring parameters,
+    no torch.no_grad().  The outputs are those of the training call, carry a graph, and a backward through them gives
+    the training call's parameter gradients (the absent means2D simply gets none)."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    from tests.helpers import settings_for
+    inp = scene_inputs(6000, 160, 120, sh_degree=3, seed=19)
+    dc, di = (torch.as_tensor(a, device=gpu_device) for a in upstream(160, 120, 19))
+    r = GaussianRasterizer(raster_settings=settings_for(inp, gpu_device))
+
+    def params():
+        return [torch.as_tensor(inp[k], device=gpu_device).clone().requires_grad_(True)
+                for k in ("means3D", "opacities", "scales", "rotations", "shs")]
+
+    m, o, sc, rot, shs = params()
+    img, radii, invd = r(means3D=m, means2D=None, shs=shs, colors_precomp=None, opacities=o, scales=sc,
+                         rotations=rot, cov3D_precomp=None)
+    assert img.requires_grad and invd.requires_grad
+    m2, o2, sc2, rot2, shs2 = params()
+    screen = torch.zeros_like(m2, requires_grad=True)
+    img2, radii2, invd2 = r(means3D=m2, means2D=screen, shs=shs2, colors_precomp=None, opacities=o2, scales=sc2,
+                            rotations=rot2, cov3D_precomp=None)
+    assert torch.equal(img, img2) and torch.equal(radii, radii2) and torch.equal(invd, invd2)
+    img.clamp(0, 1)  # the script's post-processing on a graph-carrying output
+    ((img * dc).sum() + (invd * di).sum()).backward()
+    ((img2 * dc).sum() + (invd2 * di).sum()).backward()
+    for a, b in ((m, m2), (o, o2), (sc, sc2), (rot, rot2), (shs, shs2)):
+        assert torch.equal(a.grad, b.grad)
+
+
 def test_cfg3_full_size_properties(gpu_device):
     """BASELINE config 3 (1M Gaussians, 1920x1080, SH3) at full size: exact instance count and sorted
     list against the oracle, image within the forward bars, gradients within 2e-4 relative L2 (5e-6 over the
