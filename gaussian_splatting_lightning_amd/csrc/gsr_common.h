@@ -65,6 +65,7 @@ struct SortScratch {
     uint32_t *k[2];
     uint32_t *v[2];
     uint32_t *counts;    // RS_BINS * nblocks (multi-kernel path)
+    uint32_t *counts_pre;  // RS_BINS * nblocks column prefixes, then RS_BINS digit offsets (one-launch count scan)
     uint32_t *scan_tmp;  // column sums of the count matrix (RS_COL_CHUNK-row chunks x RS_BINS)
     uint32_t *ctrl;      // RS_CTRL_WORDS, then the look-back status words (onesweep path)
     uint32_t *status;
@@ -77,6 +78,7 @@ inline void carve_sort(Carver &c, SortScratch &s, uint32_t n, bool need_v0) {
     s.v[1] = c.take<uint32_t>(n ? n : 1);
     uint32_t nb = div_up(n ? n : 1, RS_TILE);
     s.counts = c.take<uint32_t>((size_t)RS_BINS * nb + 1);
+    s.counts_pre = c.take<uint32_t>((size_t)RS_BINS * (nb + 1));
     s.scan_tmp = c.take<uint32_t>(((size_t)div_up(nb, RS_COL_CHUNK) + 1) * RS_BINS);
     const uint32_t nb_os = div_up(n ? n : 1, RS_TILE / 2);  // onesweep tiles may be half a RS_TILE
     s.ctrl = c.take<uint32_t>(RS_CTRL_WORDS + (size_t)RS_MAX_PASSES * nb_os * RS_BINS);

@@ -219,14 +219,32 @@ void launch_exclusive_scan_lookback(hipStream_t s, const uint32_t *in, const uin
         scan_lookback_kernel<false><<<nb, 256, 0, s>>>(in, nullptr, n, out, status, ticket, flags, pat, force);
 }
 
+// look-back status words of the radix passes: 2-bit flag | 30-bit count
+constexpr uint32_t LB_AGG = 1u << 30, LB_INC = 2u << 30, LB_MASK = (1u << 30) - 1;
+
+__device__ __forceinline__ uint32_t lb_load(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ------------------------------------------------------------------------------------------------
 // radix sort pass: histogram
 // ------------------------------------------------------------------------------------------------
+// With cs_status, the histogram also clears what the pass's one-launch count scan starts from: its look-back words
+// (one RS_BINS row per chunk, cs_rows rows) and its ticket.
 template <int TILE>
 __global__ __launch_bounds__(256) void rs_hist_kernel(const uint32_t *__restrict__ keys, uint32_t n, int shift,
-                                                      uint32_t *__restrict__ counts, uint32_t nb) {
+                                                      uint32_t *__restrict__ counts, uint32_t nb,
+                                                      uint32_t *__restrict__ cs_status, uint32_t cs_rows,
+                                                      uint32_t *__restrict__ cs_ticket) {
     __shared__ uint32_t h[4][RS_BINS];
     const int tid = threadIdx.x, w = tid >> 6;
+    if (cs_status) {
+        for (uint32_t r = blockIdx.x; r < cs_rows; r += gridDim.x) cs_status[(size_t)r * RS_BINS + tid] = 0u;
+        if (blockIdx.x == 0 && tid == 0) *cs_ticket = 0u;
+    }
     for (int i = tid; i < 4 * RS_BINS; i += 256) (&h[0][0])[i] = 0;
     __syncthreads();
     const uint32_t base = blockIdx.x * TILE;
@@ -324,6 +342,92 @@ __global__ __launch_bounds__(256) void rs_colbase_kernel(uint32_t *__restrict__ 
     }
 }
 
+// One launch instead of rs_colsum / rs_colscan / rs_colbase (cfg 5 ran those three 6 times per step, ~16 us per pass).
+// Workgroup = C consecutive block rows, thread = digit: the thread loads its column's C counts (C coalesced 1-KB
+// rows), publishes their sum, and obtains the column prefix of the chunks before it by a decoupled look-back over
+// their status words (flag | 30-bit count, as onesweep's; chunk ids from a ticket, so a workgroup only waits on
+// workgroups that started before it; an unpublished predecessor is recounted from the counts, which this kernel never
+// writes, after `patience` polls).  It writes the rows' exclusive prefixes to counts_pre and the last chunk writes
+// the exclusive digit offsets behind them (row nb), which the scatter adds.  Counts < 2^30 (launch_radix_sort).
+constexpr int CS_LBW = 16;  // predecessors' words loaded per look-back round trip
+template <int C>
+__global__ __launch_bounds__(256) void rs_countscan_kernel(const uint32_t *__restrict__ counts, uint32_t nb,
+                                                           uint32_t *__restrict__ counts_pre,
+                                                           uint32_t *__restrict__ status,
+                                                           uint32_t *__restrict__ ticket, uint32_t *__restrict__ err,
+                                                           uint32_t patience, int force) {
+    __shared__ uint32_t s_bid, s_w[4];
+    const int d = threadIdx.x, lane = d & 63, w = d >> 6;
+    if (d == 0) s_bid = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t c = s_bid, nch = gridDim.x;
+    const uint32_t b0 = c * C;
+    uint32_t v[C];
+    uint32_t agg = 0;
+#pragma unroll
+    for (int r = 0; r < C; r++) {
+        v[r] = b0 + r < nb ? counts[(size_t)(b0 + r) * RS_BINS + d] : 0u;
+        agg += v[r];
+    }
+    uint32_t *st = status + (size_t)c * RS_BINS + d;
+    lb_store(st, (c == 0 ? LB_INC : LB_AGG) | agg);
+    uint32_t excl = 0;
+    if (c > 0) {
+        int look = (int)c - 1;
+        uint32_t spins = 0;
+        while (true) {
+            uint32_t sv[CS_LBW];
+#pragma unroll
+            for (int i = 0; i < CS_LBW; i++)
+                sv[i] = (look - i >= 0) ? (force ? 0u : lb_load(status + (size_t)(look - i) * RS_BINS + d)) : LB_INC;
+            const bool fb = force || spins >= patience;
+            bool found = false, stalled = false;
+            int used = 0;
+#pragma unroll
+            for (int i = 0; i < CS_LBW; i++) {
+                if (!found && !stalled) {
+                    uint32_t f = sv[i] & ~LB_MASK, val = sv[i] & LB_MASK;
+                    if (f == 0 && fb) {  // recount chunk look - i of this column
+                        const uint32_t q0 = (uint32_t)(look - i) * C, q1 = min(nb, q0 + C);
+                        val = 0;
+                        for (uint32_t b = q0; b < q1; b++) val += counts[(size_t)b * RS_BINS + d];
+                        f = LB_AGG;
+                        atomicOr(err, 4u);
+                    }
+                    if (f == 0) {
+                        stalled = true;
+                    } else {
+                        excl += val;
+                        used = i + 1;
+                        found = f == LB_INC;
+                    }
+                }
+            }
+            if (found) break;
+            look -= used;
+            if (stalled) {
+                ++spins;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        lb_store(st, LB_INC | (excl + agg));
+    }
+    uint32_t run = excl;
+#pragma unroll
+    for (int r = 0; r < C; r++) {
+        if (b0 + r < nb) counts_pre[(size_t)(b0 + r) * RS_BINS + d] = run;
+        run += v[r];
+    }
+    if (c == nch - 1) {  // run = digit total: exclusive digit offsets into row nb
+        const uint32_t inc = wave_inclusive_scan(run, lane);
+        if (lane == 63) s_w[w] = inc;
+        __syncthreads();
+        uint32_t off = inc - run;
+        for (int i = 0; i < w; i++) off += s_w[i];
+        counts_pre[(size_t)nb * RS_BINS + d] = off;
+    }
+}
+
 // Chunk rows per column workgroup: the column chains (chunk / 8 round trips in colsum and colbase) against the
 // chunk-sum chain (nch / 16 in colscan).  cfg 5 (round 3): the 1221-row depth-sort matrices 0.280 -> 0.259 ms with 32
 // rows (0.271 with 128), the 4822-row tile-sort matrices 0.531 -> 0.513 ms with 128 (0.520 with 32).
@@ -338,10 +442,12 @@ static void launch_count_scan(hipStream_t s, uint32_t *counts, uint32_t nb, uint
 // ------------------------------------------------------------------------------------------------
 // radix sort pass: stable scatter
 // ------------------------------------------------------------------------------------------------
+// digit_off (or null): exclusive digit offsets added to counts_scanned's column prefixes (rs_countscan_kernel)
 template <bool IOTA_IN, int ITEMS>
 __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restrict__ keys_in,
                                                          const uint32_t *__restrict__ vals_in, uint32_t n,
                                                          int shift, const uint32_t *__restrict__ counts_scanned,
+                                                         const uint32_t *__restrict__ digit_off,
                                                          uint32_t nb, uint32_t *__restrict__ keys_out,
                                                          uint32_t *__restrict__ vals_out, SortGather ga) {
     __shared__ uint32_t s_cnt[4][RS_BINS];  // per-wave running digit counts, then per-wave bases
@@ -403,7 +509,7 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restr
         uint32_t woff = 0;
         for (int i = 0; i < w; i++) woff += s_wsum[i];
         s_dstart[d] = woff + inc - tot;
-        s_gbase[d] = counts_scanned[(size_t)blockIdx.x * RS_BINS + d];
+        s_gbase[d] = counts_scanned[(size_t)blockIdx.x * RS_BINS + d] + (digit_off ? digit_off[d] : 0u);
     }
     __syncthreads();
 #pragma unroll
@@ -486,14 +592,6 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restr
 // counts, then its inclusive prefix; a block only waits on blocks that started before it, since block
 // ids come from an atomic ticket).  3 + passes launches instead of 5 per pass.
 // ------------------------------------------------------------------------------------------------
-constexpr uint32_t LB_AGG = 1u << 30, LB_INC = 2u << 30, LB_MASK = (1u << 30) - 1;
-
-__device__ __forceinline__ uint32_t lb_load(const uint32_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void lb_store(uint32_t *p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 constexpr int MH_BATCH = 8;
 // Digit histograms of every pass in one read of the keys.  Keys that share a digit inside a wave are
@@ -774,19 +872,36 @@ template <int ITEMS>
 static void launch_radix_sort_multi(hipStream_t s, SortScratch &sc, uint32_t n, int passes, bool keyed,
                                     const uint32_t *keys0, const SortGather *gather) {
     const uint32_t nb = div_up(n, (uint32_t)ITEMS * 256u);  // <= the RS_TILE block count carve_sort sized
+    // "rs_cscan" 1 (default): the one-launch count scan (look-back counts < 2^30); 0: the three-launch column scan
+    const bool one = tuning("rs_cscan", 1) != 0 && n <= RS_ONESWEEP_MAX_N;
+    constexpr uint32_t CS_C = 32;
+    const uint32_t nch = div_up(nb, CS_C);  // <= RS_MAX_PASSES * nb_os rows of sc.status per pass
+    const uint32_t pat = (uint32_t)tuning("lb_patience", 1 << 16);
+    const int force = tuning("lb_force", 0);
     for (int p = 0; p < passes; p++) {
         const int shift = 8 * p, in = p & 1, out = (p + 1) & 1;
         const uint32_t *kin = p == 0 ? keys0 : sc.k[in];
-        rs_hist_kernel<ITEMS * 256><<<nb, 256, 0, s>>>(kin, n, shift, sc.counts, nb);
-        launch_count_scan(s, sc.counts, nb, sc.scan_tmp);
+        uint32_t *cs_status = one ? sc.status + (size_t)p * nch * RS_BINS : nullptr;
+        rs_hist_kernel<ITEMS * 256><<<nb, 256, 0, s>>>(kin, n, shift, sc.counts, nb, cs_status, nch,
+                                                      sc.ctrl + RS_CTRL_COUNTER + p);
+        const uint32_t *scanned = sc.counts, *doff = nullptr;
+        if (one) {
+            rs_countscan_kernel<CS_C><<<nch, RS_BINS, 0, s>>>(sc.counts, nb, sc.counts_pre, cs_status,
+                                                             sc.ctrl + RS_CTRL_COUNTER + p, sc.ctrl + RS_CTRL_ERR,
+                                                             pat, force);
+            scanned = sc.counts_pre;
+            doff = sc.counts_pre + (size_t)nb * RS_BINS;
+        } else {
+            launch_count_scan(s, sc.counts, nb, sc.scan_tmp);
+        }
         SortGather ga;
         if (p == passes - 1 && gather) ga = *gather;
         if (p == 0 && !keyed)
-            rs_scatter_kernel<true, ITEMS><<<nb, 256, 0, s>>>(kin, nullptr, n, shift, sc.counts, nb, sc.k[out],
+            rs_scatter_kernel<true, ITEMS><<<nb, 256, 0, s>>>(kin, nullptr, n, shift, scanned, doff, nb, sc.k[out],
                                                               sc.v[out], ga);
         else
-            rs_scatter_kernel<false, ITEMS><<<nb, 256, 0, s>>>(kin, sc.v[in], n, shift, sc.counts, nb, sc.k[out],
-                                                               sc.v[out], ga);
+            rs_scatter_kernel<false, ITEMS><<<nb, 256, 0, s>>>(kin, sc.v[in], n, shift, scanned, doff, nb,
+                                                               sc.k[out], sc.v[out], ga);
     }
 }
 

@@ -675,23 +675,30 @@ def test_dense_tiles_fall_back_to_radix_after_speculative_count(gpu_device):
         assert np.array_equal(hip["grads"][k], forced["grads"][k]), k
 
 
-@pytest.mark.parametrize("W,H,onesweep", [(1280, 720, 1), (96, 64, 1), (1280, 720, 0), (1280, 720, 3)])
-def test_binning_paths_are_bitwise_identical(gpu_device, W, H, onesweep):
+@pytest.mark.parametrize("W,H,onesweep,cscan,xcd", [(1280, 720, 1, 1, 1), (96, 64, 1, 1, 1), (1280, 720, 0, 1, 1),
+                                                    (1280, 720, 3, 1, 1), (1280, 720, 0, 0, 0)])
+def test_binning_paths_are_bitwise_identical(gpu_device, W, H, onesweep, cscan, xcd):
     """The bucket binning (per-tile sorts) and the radix binning (depth sort + stable tile sort) produce the
     same instance order, so every output and gradient is bit for bit the same -- with either radix-sort
-    implementation (onesweep 0: the multi-kernel passes for every sort, 3: onesweep for every sort)."""
+    implementation (onesweep 0: the multi-kernel passes for every sort, 3: onesweep for every sort), either count
+    scan of the multi-kernel passes (cscan 1: one launch with look-back, 0: three launches) and either bucket run
+    order (xcd 1: XCD-major, 0: block order)."""
     from gaussian_splatting_lightning_amd import _native
     inp = scene_inputs(200_000 if W > 100 else 60_000, W, H, sh_degree=3, seed=6, stress_fraction=0.01)
     dc, di = upstream(W, H, 6)
     try:
         _native.set_tuning("bucket", 2)
+        _native.set_tuning("bk_xcd", xcd)
         ref = run_hip(inp, gpu_device, dc, di)
         _native.set_tuning("bucket", 0)
         _native.set_tuning("onesweep", onesweep)
+        _native.set_tuning("rs_cscan", cscan)
         alt = run_hip(inp, gpu_device, dc, di)
     finally:
         _native.set_tuning("bucket", 1)
         _native.set_tuning("onesweep", 1)
+        _native.set_tuning("rs_cscan", 1)
+        _native.set_tuning("bk_xcd", 1)
     a, b = hip_state_arrays(ref), hip_state_arrays(alt)
     for k in ("point_list", "ranges", "tiles", "n_contrib", "tile_last", "tile_loaded"):
         assert np.array_equal(a[k], b[k]), k
