@@ -573,13 +573,19 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             if (lpt) launch_tile_order(stream, im.ranges, nullptr, 0, (int)T, im.order_fwd, im.lpt_hist);
         }
     } else {
+        bool keys16 = false;
         if (R > 0) {
             ExpandParams ep;
             ep.P = (uint32_t)P; ep.R = R; ep.gx = gx; ep.gy = gy;
             ep.order = g.order; ep.inst_off = g.inst_off; ep.tiles = g.tiles; ep.exp_rec = g.exp_rec;
             ep.exp_sorted = sorted_exp ? g.exp_sorted : nullptr;
             ep.exp_owner = tuning("exp_owner", 1) ? b.exp_owner : nullptr;
-            ep.keys_out = b.sort.k[0]; ep.inst_gid = b.inst_gid; ep.inst_start = g.inst_start;
+            // 16-bit tile keys up to 65536 tiles ("tile_key16" 0: 32-bit): the tile sort, the expansion's key stores and
+            // the range search move 2 bytes per key instead of 4
+            const bool k16 = T <= 65536u && tuning("tile_key16", 1) != 0;
+            ep.keys_out = k16 ? nullptr : b.sort.k[0];
+            ep.keys16_out = k16 ? reinterpret_cast<uint16_t *>(b.sort.k[0]) : nullptr;
+            ep.inst_gid = b.inst_gid; ep.inst_start = g.inst_start;
 #ifndef GSR_EXP_INV
 #define GSR_EXP_INV 1
 #endif
@@ -588,13 +594,19 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             const bool exp_inv = tuning("exp_inv", GSR_EXP_INV) != 0;
             ep.inv_none = exp_inv ? b.inv : nullptr;
             GSR_STAGE(ST_EXPAND, dbg, launch_expand(stream, ep));
-            GSR_STAGE(ST_TILE_SORT, dbg,
-                      launch_radix_sort(stream, b.sort, R, tile_key_bits(T), false, nullptr, nullptr, &tile_onesweep));
+            if (k16)
+                GSR_STAGE(ST_TILE_SORT, dbg, launch_radix_sort16(stream, b.sort, R, tile_key_bits(T)));
+            else
+                GSR_STAGE(ST_TILE_SORT, dbg,
+                          launch_radix_sort(stream, b.sort, R, tile_key_bits(T), false, nullptr, nullptr,
+                                            &tile_onesweep));
+            keys16 = k16;
             if (!exp_inv) GSR_HIP(hipMemsetAsync(b.inv, 0xff, sizeof(uint32_t) * (size_t)R, stream));
         }
         GSR_STAGE(ST_RANGES, dbg, {
             GSR_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * T, stream));
-            launch_identify_ranges(stream, b.keys_sorted, R, im.ranges);
+            if (keys16) launch_identify_ranges16(stream, reinterpret_cast<const uint16_t *>(b.keys_sorted), R, im.ranges);
+            else launch_identify_ranges(stream, b.keys_sorted, R, im.ranges);
         });
         if (lpt) launch_tile_order(stream, im.ranges, nullptr, 0, (int)T, im.order_fwd, im.lpt_hist);
     }

@@ -24,7 +24,10 @@ struct CullIn {
 
 // Projection, conic, radius, SH colour and render records of one Gaussian.  Returns the area of its tile
 // rect (0: not rendered); the tile culling, tile count and sort key are finished by preprocess_kernel.
-__device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &p, const int i, CullIn &ci) {
+// sh_row: the Gaussian's SH coefficients staged in LDS by the wave (SH_LDS), else null (read from p.shs).
+template <bool SH_LDS = false>
+__device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &p, const int i, CullIn &ci,
+                                                        const float *sh_row = nullptr) {
     // uncontracted like the helpers it calls (gsr_common.h): radii, rects and render records bit-equal the oracle's
 #pragma clang fp contract(off)
     const GeomState &g = p.g;
@@ -95,7 +98,7 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
         dir = make_float3(dir.x / len, dir.y / len, dir.z / len);
         if (p.D > 0) {  // the colour and its direction Jacobian for the backward (9 planes, coalesced)
             float3 jx, jy, jz;
-            rgb = sh_eval_jac_dispatch(p.D, p.shs + (size_t)i * p.M * 3, dir, jx, jy, jz);
+            rgb = sh_eval_jac_dispatch(p.D, SH_LDS ? sh_row : p.shs + (size_t)i * p.M * 3, dir, jx, jy, jz);
             const size_t n = (size_t)p.P;
             float *J = g.sh_jac + i;
             J[0] = jx.x; J[n] = jx.y; J[2 * n] = jx.z;
@@ -140,52 +143,87 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
 #ifndef GSR_PRE_MINW
 #define GSR_PRE_MINW 4  // 112 VGPRs, no spills: cfg3 0.106 -> 0.103 ms against 5 waves (96 VGPRs, 2 spilled); 6: 0.112
 #endif
+// SH_LDS (M = 16, 16-B aligned coefficients): the wave loads its 64 Gaussians' coefficient rows (12 KB, contiguous)
+// with coalesced 16-B loads -- 12 per lane, each covering 1 KB of consecutive bytes -- into LDS at a 52-float row
+// stride (bank-conflict-free row reads, as preprocess_bwd's staging), and each lane evaluates its colour from LDS,
+// instead of 12 loads per lane that each touch 64 cache lines.  The culling's LDS arrays share the staging area.
+constexpr int PRE_SH_STRIDE = 52;
+struct PreCullLds {
+    CullGauss cg[64];
+    int4 rect[64];  // rx, ry, rw, start of the lane's pairs
+    unsigned long long mask[64];
+    int own[64];    // lane whose rect's pair run starts at this pair of the step, else -1
+};
+template <bool SH_LDS>
 __global__ __launch_bounds__(256, GSR_PRE_MINW) void preprocess_kernel(PreprocessParams p) {
-    __shared__ CullGauss s_cg[4][64];
-    __shared__ int4 s_rect[4][64];        // rx, ry, rw, start of the lane's pairs
-    __shared__ unsigned long long s_mask[4][64];
+    constexpr size_t WAVE_LDS = SH_LDS ? (sizeof(PreCullLds) > 64 * PRE_SH_STRIDE * 4 ? sizeof(PreCullLds)
+                                                                                        : 64 * PRE_SH_STRIDE * 4)
+                                       : sizeof(PreCullLds);
+    __shared__ __attribute__((aligned(16))) unsigned char s_lds[4][WAVE_LDS];
     __shared__ uint32_t s_w[4];
-    __shared__ int s_own[4][64];  // lane whose rect's pair run starts at this pair of the step, else -1
     const uint32_t bid = blockIdx.x;
     const int i = (int)bid * 256 + threadIdx.x;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    PreCullLds &L = *reinterpret_cast<PreCullLds *>(s_lds[w]);
     CullIn ci;
     ci.need = false;
-    const uint32_t area = i < p.P ? preprocess_gaussian(p, i, ci) : 0u;
+    uint32_t area;
+    if constexpr (SH_LDS) {
+        float *ssh = reinterpret_cast<float *>(s_lds[w]);
+        const int i0 = (int)bid * 256 + w * 64;
+        const int nf4 = max(0, min(64, p.P - i0)) * 12;  // float4s of the wave's rows
+        const float4 *src = reinterpret_cast<const float4 *>(p.shs + (size_t)i0 * 48);
+        float4 v[12];
+#pragma unroll
+        for (int q = 0; q < 12; q++) {
+            const int f = q * 64 + lane;
+            v[q] = f < nf4 ? src[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int q = 0; q < 12; q++) {
+            const int f = q * 64 + lane, row = f / 12, c4 = f - row * 12;
+            *reinterpret_cast<float4 *>(ssh + row * PRE_SH_STRIDE + 4 * c4) = v[q];
+        }
+        wave_lds_sync();
+        area = i < p.P ? preprocess_gaussian<true>(p, i, ci, ssh + lane * PRE_SH_STRIDE) : 0u;
+        wave_lds_sync();  // the staging area becomes the culling arrays
+    } else {
+        area = i < p.P ? preprocess_gaussian<false>(p, i, ci) : 0u;
+    }
     const uint32_t need_area = ci.need ? area : 0u;
     const uint32_t incl = wave_inclusive_scan(need_area, lane);
     const uint32_t total = __shfl((int)incl, 63);
-    if (ci.need) s_cg[w][lane] = ci.cg;
-    s_rect[w][lane] = make_int4(ci.rx, ci.ry, ci.rw, (int)(incl - need_area));
-    s_mask[w][lane] = 0ull;
+    if (ci.need) L.cg[lane] = ci.cg;
+    L.rect[lane] = make_int4(ci.rx, ci.ry, ci.rw, (int)(incl - need_area));
+    L.mask[lane] = 0ull;
     // pair owners by marks and a max-scan (as the bucket walk): the lane whose pair run starts inside the step
     // marks its start, and every pair takes the largest marking lane at or before it (or the previous step's last
     // owner) -- one LDS round trip per step instead of a 6-deep dependent binary search over the starts (cfg 3
     // preprocess 0.1092 -> 0.1080 ms)
-    s_own[w][lane] = -1;
+    L.own[lane] = -1;
     const uint32_t my_start = incl - need_area;
     int carry = -1;
     wave_lds_sync();
     for (uint32_t B = 0; B < total; B += 64) {
         const uint32_t j = B + (uint32_t)lane;
         const bool marks = need_area > 0 && my_start >= B && my_start < B + 64;
-        if (marks) s_own[w][my_start - B] = lane;
+        if (marks) L.own[my_start - B] = lane;
         wave_lds_sync();
-        const int o = max(wave_inclusive_max(s_own[w][lane]), carry);
+        const int o = max(wave_inclusive_max(L.own[lane]), carry);
         carry = __builtin_amdgcn_readlane(o, 63);
         wave_lds_sync();
-        if (marks) s_own[w][my_start - B] = -1;
+        if (marks) L.own[my_start - B] = -1;
         if (j >= total) continue;
-        const int4 r = s_rect[w][o];
+        const int4 r = L.rect[o];
         const uint32_t t = j - (uint32_t)r.w;
         const int tx = r.x + (int)(t % (uint32_t)r.z), ty = r.y + (int)(t / (uint32_t)r.z);
-        if (cull_keep(s_cg[w][o], tx, ty, p.W, p.H)) atomicOr(&s_mask[w][o], 1ull << t);
+        if (cull_keep(L.cg[o], tx, ty, p.W, p.H)) atomicOr(&L.mask[o], 1ull << t);
     }
     wave_lds_sync();
     uint32_t kept = area;
     if (i < p.P && area > 0) {
         const GeomState &g = p.g;
-        const uint64_t mask = ci.need ? s_mask[w][lane] : 0ull;
+        const uint64_t mask = ci.need ? L.mask[lane] : 0ull;
         if (ci.need) kept = (uint32_t)__popcll(mask);
         g.exp_rec[i] = make_uint4((uint32_t)mask, (uint32_t)(mask >> 32), (uint32_t)ci.rx | ((uint32_t)ci.ry << 16),
                                   (uint32_t)ci.rw);
@@ -249,7 +287,10 @@ __global__ __launch_bounds__(256, GSR_PRE_MINW) void preprocess_kernel(Preproces
 
 void launch_preprocess(hipStream_t s, const PreprocessParams &p) {
     if (p.P <= 0) return;
-    preprocess_kernel<<<div_up(p.P, 256), 256, 0, s>>>(p);
+    const bool sh_lds = p.shs && !p.colors_precomp && p.M == 16 && p.D > 0 && ((uintptr_t)p.shs & 15) == 0 &&
+                        tuning("pre_sh_lds", 0) != 0;
+    if (sh_lds) preprocess_kernel<true><<<div_up(p.P, 256), 256, 0, s>>>(p);
+    else preprocess_kernel<false><<<div_up(p.P, 256), 256, 0, s>>>(p);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -374,12 +415,16 @@ __global__ __launch_bounds__(256) void expand_kernel(ExpandParams p) {
     }
     if (ub + EXP_PER <= u1) {
         static_assert(EXP_PER == 4, "one uint4 store per thread");
-        *reinterpret_cast<uint4 *>(p.keys_out + ub) = make_uint4(key[0], key[1], key[2], key[3]);
+        if (p.keys16_out)
+            *reinterpret_cast<uint2 *>(p.keys16_out + ub) = make_uint2(key[0] | (key[1] << 16), key[2] | (key[3] << 16));
+        else
+            *reinterpret_cast<uint4 *>(p.keys_out + ub) = make_uint4(key[0], key[1], key[2], key[3]);
         *reinterpret_cast<uint4 *>(p.inst_gid + ub) = make_uint4(gv[0], gv[1], gv[2], gv[3]);
         if (p.inv_none) *reinterpret_cast<uint4 *>(p.inv_none + ub) = make_uint4(INV_NONE, INV_NONE, INV_NONE, INV_NONE);
     } else {
         for (uint32_t u = ub; u < u1; u++) {
-            p.keys_out[u] = key[u - ub];
+            if (p.keys16_out) p.keys16_out[u] = (uint16_t)key[u - ub];
+            else p.keys_out[u] = key[u - ub];
             p.inst_gid[u] = gv[u - ub];
             if (p.inv_none) p.inv_none[u] = INV_NONE;
         }
@@ -407,14 +452,21 @@ void launch_expand(hipStream_t s, const ExpandParams &p) {
 // ------------------------------------------------------------------------------------------------
 // Tile boundaries of the sorted keys: 8 consecutive keys per thread (two 16-B loads) and the key before them.
 constexpr uint32_t IR_PER = 8;
-__global__ __launch_bounds__(256) void identify_ranges_kernel(const uint32_t *__restrict__ keys, uint32_t R,
+template <typename KT>
+__global__ __launch_bounds__(256) void identify_ranges_kernel(const KT *__restrict__ keys, uint32_t R,
                                                               uint2 *__restrict__ ranges) {
     const uint32_t base = (blockIdx.x * 256 + threadIdx.x) * IR_PER;
     uint32_t k[IR_PER];
     if (base + IR_PER <= R) {
-        const uint4 *k4 = reinterpret_cast<const uint4 *>(keys + base);
-        const uint4 a = k4[0], b = k4[1];
-        k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w; k[4] = b.x; k[5] = b.y; k[6] = b.z; k[7] = b.w;
+        if constexpr (sizeof(KT) == 2) {  // 8 keys in one 16-B load
+            const uint4 a = *reinterpret_cast<const uint4 *>(keys + base);
+            k[0] = a.x & 0xffffu; k[1] = a.x >> 16; k[2] = a.y & 0xffffu; k[3] = a.y >> 16;
+            k[4] = a.z & 0xffffu; k[5] = a.z >> 16; k[6] = a.w & 0xffffu; k[7] = a.w >> 16;
+        } else {
+            const uint4 *k4 = reinterpret_cast<const uint4 *>(keys + base);
+            const uint4 a = k4[0], b = k4[1];
+            k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w; k[4] = b.x; k[5] = b.y; k[6] = b.z; k[7] = b.w;
+        }
     } else {
 #pragma unroll
         for (uint32_t q = 0; q < IR_PER; q++) k[q] = base + q < R ? keys[base + q] : 0u;
@@ -441,7 +493,11 @@ __global__ __launch_bounds__(256) void identify_ranges_kernel(const uint32_t *__
 
 void launch_identify_ranges(hipStream_t s, const uint32_t *keys_sorted, uint32_t R, uint2 *ranges) {
     if (R == 0) return;
-    identify_ranges_kernel<<<div_up(R, 256 * IR_PER), 256, 0, s>>>(keys_sorted, R, ranges);
+    identify_ranges_kernel<uint32_t><<<div_up(R, 256 * IR_PER), 256, 0, s>>>(keys_sorted, R, ranges);
+}
+void launch_identify_ranges16(hipStream_t s, const uint16_t *keys_sorted, uint32_t R, uint2 *ranges) {
+    if (R == 0) return;
+    identify_ranges_kernel<uint16_t><<<div_up(R, 256 * IR_PER), 256, 0, s>>>(keys_sorted, R, ranges);
 }
 
 // LPT (longest first) launch order for the composite kernels: tile costs vary ~2x around the image centre,

@@ -41,6 +41,9 @@ struct SortGather {
 bool launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bool keyed = false,
                        const uint32_t *keys0 = nullptr, const SortGather *gather = nullptr,
                        bool *onesweep_ran = nullptr);
+// The same sort on 16-bit keys (nbits <= 16; multi-kernel passes): sc.k[] hold uint16_t keys, values as above.  The
+// radix binning's tile sort takes it up to 65536 tiles (a third less HBM traffic than 32-bit keys).
+void launch_radix_sort16(hipStream_t s, SortScratch &sc, uint32_t n, int nbits);
 
 // ---- forward (gsr_forward.hip) ----
 struct PreprocessParams {
@@ -68,11 +71,13 @@ struct ExpandParams {
     const uint4 *exp_sorted;  // optional: exp_rec already in depth order (read by rank, no gather)
     uint32_t *exp_owner;      // optional: owner ranks of the block starts (div_up(R, EXP_TILE) + 1 words)
     uint32_t *keys_out, *inst_gid, *inst_start;
+    uint16_t *keys16_out;     // optional: 16-bit tile keys (launch_radix_sort16) instead of keys_out
     uint32_t *inv_none;       // optional: inv, set to INV_NONE for every instance here (no separate fill)
 };
 void launch_expand(hipStream_t s, const ExpandParams &p);
 
 void launch_identify_ranges(hipStream_t s, const uint32_t *keys_sorted, uint32_t R, uint2 *ranges);
+void launch_identify_ranges16(hipStream_t s, const uint16_t *keys_sorted, uint32_t R, uint2 *ranges);
 
 // ---- bucket binning (gsr_bin.hip) ----
 struct BucketParams {

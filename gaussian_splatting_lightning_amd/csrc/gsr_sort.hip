@@ -234,8 +234,8 @@ __device__ __forceinline__ void lb_store(uint32_t *p, uint32_t v) {
 // ------------------------------------------------------------------------------------------------
 // With cs_status, the histogram also clears what the pass's one-launch count scan starts from: its look-back words
 // (one RS_BINS row per chunk, cs_rows rows) and its ticket.
-template <int TILE>
-__global__ __launch_bounds__(256) void rs_hist_kernel(const uint32_t *__restrict__ keys, uint32_t n, int shift,
+template <int TILE, typename KT = uint32_t>
+__global__ __launch_bounds__(256) void rs_hist_kernel(const KT *__restrict__ keys, uint32_t n, int shift,
                                                       uint32_t *__restrict__ counts, uint32_t nb,
                                                       uint32_t *__restrict__ cs_status, uint32_t cs_rows,
                                                       uint32_t *__restrict__ cs_ticket) {
@@ -250,18 +250,28 @@ __global__ __launch_bounds__(256) void rs_hist_kernel(const uint32_t *__restrict
     const uint32_t base = blockIdx.x * TILE;
     if (base + TILE <= n) {
         const uint4 *k4 = reinterpret_cast<const uint4 *>(keys + base);
+        constexpr int PER16 = 16 / (int)sizeof(KT);  // keys per 16-B load
 #pragma unroll
-        for (int i = 0; i < TILE / 4 / 256; i++) {
+        for (int i = 0; i < TILE / PER16 / 256; i++) {
             const uint4 q = k4[i * 256 + tid];
-            atomicAdd(&h[w][(q.x >> shift) & 255u], 1u);
-            atomicAdd(&h[w][(q.y >> shift) & 255u], 1u);
-            atomicAdd(&h[w][(q.z >> shift) & 255u], 1u);
-            atomicAdd(&h[w][(q.w >> shift) & 255u], 1u);
+            if constexpr (sizeof(KT) == 2) {
+                const uint32_t wds[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    atomicAdd(&h[w][((wds[k] & 0xffffu) >> shift) & 255u], 1u);
+                    atomicAdd(&h[w][((wds[k] >> 16) >> shift) & 255u], 1u);
+                }
+            } else {
+                atomicAdd(&h[w][(q.x >> shift) & 255u], 1u);
+                atomicAdd(&h[w][(q.y >> shift) & 255u], 1u);
+                atomicAdd(&h[w][(q.z >> shift) & 255u], 1u);
+                atomicAdd(&h[w][(q.w >> shift) & 255u], 1u);
+            }
         }
     } else {
         for (int i = tid; i < TILE; i += 256) {
             const uint32_t j = base + i;
-            if (j < n) atomicAdd(&h[w][(keys[j] >> shift) & 255u], 1u);
+            if (j < n) atomicAdd(&h[w][((uint32_t)keys[j] >> shift) & 255u], 1u);
         }
     }
     __syncthreads();
@@ -443,18 +453,18 @@ static void launch_count_scan(hipStream_t s, uint32_t *counts, uint32_t nb, uint
 // radix sort pass: stable scatter
 // ------------------------------------------------------------------------------------------------
 // digit_off (or null): exclusive digit offsets added to counts_scanned's column prefixes (rs_countscan_kernel)
-template <bool IOTA_IN, int ITEMS>
-__global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restrict__ keys_in,
+template <bool IOTA_IN, int ITEMS, typename KT = uint32_t>
+__global__ __launch_bounds__(256) void rs_scatter_kernel(const KT *__restrict__ keys_in,
                                                          const uint32_t *__restrict__ vals_in, uint32_t n,
                                                          int shift, const uint32_t *__restrict__ counts_scanned,
                                                          const uint32_t *__restrict__ digit_off,
-                                                         uint32_t nb, uint32_t *__restrict__ keys_out,
+                                                         uint32_t nb, KT *__restrict__ keys_out,
                                                          uint32_t *__restrict__ vals_out, SortGather ga) {
     __shared__ uint32_t s_cnt[4][RS_BINS];  // per-wave running digit counts, then per-wave bases
     __shared__ uint32_t s_dstart[RS_BINS];  // block-local start of each digit's run
     __shared__ uint32_t s_gbase[RS_BINS];   // global start of this block's run of each digit
     __shared__ uint32_t s_wsum[4];
-    __shared__ uint32_t s_keys[ITEMS * 256];
+    __shared__ KT s_keys[ITEMS * 256];
     __shared__ uint32_t s_vals[ITEMS * 256];
 
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -518,7 +528,7 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restr
         if (j < n) {
             const uint32_t d = (key[it] >> shift) & 255u;
             const uint32_t pos = s_dstart[d] + s_cnt[w][d] + rank[it];
-            s_keys[pos] = key[it];
+            s_keys[pos] = (KT)key[it];
             s_vals[pos] = val[it];
         }
     }
@@ -536,7 +546,7 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restr
                     const uint32_t k = s_keys[i], v = s_vals[i];
                     const uint32_t d = (k >> shift) & 255u;
                     gp[it] = s_gbase[d] + (i - s_dstart[d]);
-                    keys_out[gp[it]] = k;
+                    keys_out[gp[it]] = (KT)k;
                     vals_out[gp[it]] = v;
                     if (ga.dst) g[it] = ga.src[v];
                     if (ga.dst4) g4[it] = ga.src4[v];
@@ -571,7 +581,7 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restr
             }
 #pragma unroll
             for (int q = 0; q < 8; q++) {
-                keys_out[g[q]] = k[q];
+                keys_out[g[q]] = (KT)k[q];
                 vals_out[g[q]] = v[q];
             }
         }
@@ -581,7 +591,7 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const uint32_t *__restr
         const uint32_t k = s_keys[i], v = s_vals[i];
         const uint32_t d = (k >> shift) & 255u;
         const uint32_t gpos = s_gbase[d] + (i - s_dstart[d]);
-        keys_out[gpos] = k;
+        keys_out[gpos] = (KT)k;
         vals_out[gpos] = v;
     }
 }
@@ -868,9 +878,10 @@ static void launch_radix_sort_onesweep(hipStream_t s, SortScratch &sc, uint32_t 
 }
 
 // multi-kernel path: per pass a block histogram, a scan of the (digit x block) counts, a stable scatter
-template <int ITEMS>
+template <int ITEMS, typename KT = uint32_t>
 static void launch_radix_sort_multi(hipStream_t s, SortScratch &sc, uint32_t n, int passes, bool keyed,
-                                    const uint32_t *keys0, const SortGather *gather) {
+                                    const KT *keys0, const SortGather *gather) {
+    KT *k[2] = {reinterpret_cast<KT *>(sc.k[0]), reinterpret_cast<KT *>(sc.k[1])};
     const uint32_t nb = div_up(n, (uint32_t)ITEMS * 256u);  // <= the RS_TILE block count carve_sort sized
     // "rs_cscan" 1 (default): the one-launch count scan (look-back counts < 2^30); 0: the three-launch column scan
     const bool one = tuning("rs_cscan", 1) != 0 && n <= RS_ONESWEEP_MAX_N;
@@ -880,10 +891,10 @@ static void launch_radix_sort_multi(hipStream_t s, SortScratch &sc, uint32_t n, 
     const int force = tuning("lb_force", 0);
     for (int p = 0; p < passes; p++) {
         const int shift = 8 * p, in = p & 1, out = (p + 1) & 1;
-        const uint32_t *kin = p == 0 ? keys0 : sc.k[in];
+        const KT *kin = p == 0 ? keys0 : k[in];
         uint32_t *cs_status = one ? sc.status + (size_t)p * nch * RS_BINS : nullptr;
-        rs_hist_kernel<ITEMS * 256><<<nb, 256, 0, s>>>(kin, n, shift, sc.counts, nb, cs_status, nch,
-                                                      sc.ctrl + RS_CTRL_COUNTER + p);
+        rs_hist_kernel<ITEMS * 256, KT><<<nb, 256, 0, s>>>(kin, n, shift, sc.counts, nb, cs_status, nch,
+                                                          sc.ctrl + RS_CTRL_COUNTER + p);
         const uint32_t *scanned = sc.counts, *doff = nullptr;
         if (one) {
             rs_countscan_kernel<CS_C><<<nch, RS_BINS, 0, s>>>(sc.counts, nb, sc.counts_pre, cs_status,
@@ -897,11 +908,11 @@ static void launch_radix_sort_multi(hipStream_t s, SortScratch &sc, uint32_t n, 
         SortGather ga;
         if (p == passes - 1 && gather) ga = *gather;
         if (p == 0 && !keyed)
-            rs_scatter_kernel<true, ITEMS><<<nb, 256, 0, s>>>(kin, nullptr, n, shift, scanned, doff, nb, sc.k[out],
-                                                              sc.v[out], ga);
+            rs_scatter_kernel<true, ITEMS, KT><<<nb, 256, 0, s>>>(kin, nullptr, n, shift, scanned, doff, nb, k[out],
+                                                                  sc.v[out], ga);
         else
-            rs_scatter_kernel<false, ITEMS><<<nb, 256, 0, s>>>(kin, sc.v[in], n, shift, scanned, doff, nb,
-                                                               sc.k[out], sc.v[out], ga);
+            rs_scatter_kernel<false, ITEMS, KT><<<nb, 256, 0, s>>>(kin, sc.v[in], n, shift, scanned, doff, nb,
+                                                                   k[out], sc.v[out], ga);
     }
 }
 
@@ -934,6 +945,16 @@ bool launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bo
     if (items >= 32) launch_radix_sort_multi<32>(s, sc, n, passes, keyed, keys0, gather);
     else launch_radix_sort_multi<RS_ITEMS>(s, sc, n, passes, keyed, keys0, gather);
     return gather != nullptr;
+}
+
+void launch_radix_sort16(hipStream_t s, SortScratch &sc, uint32_t n, int nbits) {
+    if (n == 0) return;
+    const int passes = radix_passes(nbits);
+    const uint16_t *k0 = reinterpret_cast<const uint16_t *>(sc.k[0]);
+    int items = tuning("rs_items", 0);
+    if (items == 0) items = n <= (8u << 20) ? 16 : 32;
+    if (items >= 32) launch_radix_sort_multi<32, uint16_t>(s, sc, n, passes, false, k0, nullptr);
+    else launch_radix_sort_multi<RS_ITEMS, uint16_t>(s, sc, n, passes, false, k0, nullptr);
 }
 
 }  // namespace gsr

@@ -675,14 +675,15 @@ def test_dense_tiles_fall_back_to_radix_after_speculative_count(gpu_device):
         assert np.array_equal(hip["grads"][k], forced["grads"][k]), k
 
 
-@pytest.mark.parametrize("W,H,onesweep,cscan,xcd", [(1280, 720, 1, 1, 1), (96, 64, 1, 1, 1), (1280, 720, 0, 1, 1),
-                                                    (1280, 720, 3, 1, 1), (1280, 720, 0, 0, 0)])
-def test_binning_paths_are_bitwise_identical(gpu_device, W, H, onesweep, cscan, xcd):
+@pytest.mark.parametrize("W,H,onesweep,cscan,xcd,k16", [(1280, 720, 1, 1, 1, 1), (96, 64, 1, 1, 1, 1),
+                                                        (1280, 720, 0, 1, 1, 1), (1280, 720, 3, 1, 1, 0),
+                                                        (1280, 720, 0, 0, 0, 0)])
+def test_binning_paths_are_bitwise_identical(gpu_device, W, H, onesweep, cscan, xcd, k16):
     """The bucket binning (per-tile sorts) and the radix binning (depth sort + stable tile sort) produce the
     same instance order, so every output and gradient is bit for bit the same -- with either radix-sort
     implementation (onesweep 0: the multi-kernel passes for every sort, 3: onesweep for every sort), either count
-    scan of the multi-kernel passes (cscan 1: one launch with look-back, 0: three launches) and either bucket run
-    order (xcd 1: XCD-major, 0: block order)."""
+    scan of the multi-kernel passes (cscan 1: one launch with look-back, 0: three launches), either bucket run
+    order (xcd 1: XCD-major, 0: block order) and 16- or 32-bit tile keys in the radix tile sort (k16)."""
     from gaussian_splatting_lightning_amd import _native
     inp = scene_inputs(200_000 if W > 100 else 60_000, W, H, sh_degree=3, seed=6, stress_fraction=0.01)
     dc, di = upstream(W, H, 6)
@@ -693,8 +694,10 @@ def test_binning_paths_are_bitwise_identical(gpu_device, W, H, onesweep, cscan, 
         _native.set_tuning("bucket", 0)
         _native.set_tuning("onesweep", onesweep)
         _native.set_tuning("rs_cscan", cscan)
+        _native.set_tuning("tile_key16", k16)
         alt = run_hip(inp, gpu_device, dc, di)
     finally:
+        _native.set_tuning("tile_key16", 1)
         _native.set_tuning("bucket", 1)
         _native.set_tuning("onesweep", 1)
         _native.set_tuning("rs_cscan", 1)
