@@ -189,11 +189,11 @@ class ViewGradReducer:
     # ---- exchange ----
     def begin_step(self, campos: torch.Tensor) -> None:
         """Start of a step's exchange: the camera positions of every rank's view (compact mode)."""
+        self._check_not_synced()
         self._pending = []
         self._materialised = None
         if not self.compact:
             return
-        self._check_not_synced()
         self.campos_in.copy_(campos.reshape(3))
         if self.distributed:
             self._campos_work = _all_gather(self.campos_all, self.campos_in, self.group)
