@@ -1,0 +1,86 @@
+#!/usr/bin/env python
+"""Where the multi-GPU step's extra time goes, on ONE GPU with a one-rank RCCL group (bench.py --force-dist measured
+1.14 ms/step against 0.81 for the plain step at cfg 3).
+
+    python tools/dist_overhead.py [--config cfg3] [--steps 20]
+
+Variants (each: wall ms per step over --steps steps bracketed by synchronize, and the host's issue time per step):
+  plain            backward_raw into a dense reducer, no process group (bench.py at N = 1)
+  local_cK_mode    the reducer's chunked / compact arithmetic with distributed=False (no collectives)
+  dist_cK_mode     the same with the one-rank RCCL group (every collective issued and waited)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="cfg3")
+    ap.add_argument("--steps", type=int, default=20)
+    args = ap.parse_args()
+    import torch
+    import torch.distributed as dist
+    from bench import CONFIGS
+    from gaussian_splatting_lightning_amd.multiview import ViewGradReducer
+    from gaussian_splatting_lightning_amd.rasterizer import (GaussianRasterizationSettings, backward_chunked,
+                                                             backward_raw, forward_raw)
+    from gaussian_splatting_lightning_amd.synthetic import make_camera, make_scene, make_upstream
+    cfg = CONFIGS[args.config]
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    sc = make_scene(cfg["n"], cfg["deg"], seed=0, stress_fraction=cfg["stress"]).to(dev)
+    cam = make_camera(cfg["W"], cfg["H"]).to(dev)
+    dc, di = (t.to(dev) for t in make_upstream(cfg["W"], cfg["H"], 0))
+    rs = GaussianRasterizationSettings(cfg["H"], cfg["W"], cam.tanfovx, cam.tanfovy, torch.zeros(3, device=dev), 1.0,
+                                       cam.viewmatrix, cam.projmatrix, cfg["deg"], cam.campos, False, False, False)
+    n, M = cfg["n"], sc.shs.shape[1]
+
+    def make_step(red):
+        def step():
+            _, _, _, st = forward_raw(sc.means3D, sc.shs, None, sc.opacities, sc.scales, sc.rotations, None, rs)
+            if red.chunks == 1:
+                backward_raw(st, rs, dc, di, **red.backward_kwargs())
+                red.reduce(sc.means3D, cam.campos)
+            else:
+                red.begin_step(cam.campos)
+                backward_chunked(st, rs, dc, di, red.chunk_outputs(), on_chunk=red.start_chunk,
+                                 compact_sh=red.compact, accumulate_stats=True)
+                red.finish(sc.means3D)
+        return step
+
+    def timeit(step):
+        for _ in range(5):
+            step()
+        torch.cuda.synchronize()
+        host = 0.0
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            h0 = time.perf_counter()
+            step()
+            host += time.perf_counter() - h0
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        return {"wall_ms": round(1e3 * wall / args.steps, 4), "host_ms": round(1e3 * host / args.steps, 4)}
+
+    res = {"plain": timeit(make_step(ViewGradReducer(n, M, cfg["deg"], dev, mode="dense", chunks=1,
+                                                     distributed=False)))}
+    variants = [("dense", 1), ("compact", 1), ("dense", 4), ("compact", 4), ("compact", 2)]
+    for mode, k in variants:
+        res[f"local_c{k}_{mode}"] = timeit(make_step(ViewGradReducer(n, M, cfg["deg"], dev, mode=mode, chunks=k,
+                                                                     distributed=False)))
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
+    try:
+        for mode, k in variants:
+            res[f"dist_c{k}_{mode}"] = timeit(make_step(ViewGradReducer(n, M, cfg["deg"], dev, mode=mode, chunks=k)))
+    finally:
+        dist.destroy_process_group()
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -11,6 +11,7 @@ timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 
 timeout -k 10 300 python tools/stage_ab.py --config cfg3 --knob bk_xcd=0,1 --rounds 6 --steps 5 > $O/ab_xcd.txt 2>&1
 timeout -k 10 300 python tools/stage_ab.py --config cfg5 --knob rs_cscan=0,1 --knob tile_key16=0,1 --rounds 3 --steps 3 > $O/ab_cscan_cfg5.txt 2>&1
 timeout -k 10 300 python tools/stage_ab.py --config cfg3 --knob pre_sh_lds=0,1 --rounds 6 --steps 5 > $O/ab_shlds_cfg3.txt 2>&1
+timeout -k 10 300 python tools/stage_ab.py --config cfg3 --knob rb_spin=0,1 --knob cull=0,1 --rounds 4 --steps 5 > $O/ab_rbspin_cfg3.txt 2>&1
 for v in 0 1; do
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmcw$v -o run --output-format csv -- python tools/run_steps.py --config cfg3 --steps 3 --knob bk_xcd=$v > $O/pmcw$v.log 2>&1
 done
