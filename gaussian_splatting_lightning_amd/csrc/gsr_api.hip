@@ -381,6 +381,7 @@ void gsr_state_layout_query(int P, int64_t R, int W, int H, gsr_state_layout *ou
     out->bin_sorted_u = off(b.sorted_u);
     out->bin_inst_gid = off(b.inst_gid);
     out->img_tile_loaded = off(im.tile_loaded);
+    out->img_tile_sorted = off(im.tile_sorted);
     out->img_final_T = off(im.final_T);
     out->img_n_contrib = off(im.n_contrib);
     out->img_ranges = off(im.ranges);
@@ -520,6 +521,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     // Otherwise the radix path: depth sort, depth-ordered expansion, stable tile sort.
     const bool bucket = bk_possible && (bk == 2 || (uint64_t)R <= (uint64_t)BK_MAX_MEAN * T);
     bool sorted_exp = false;
+    bool prefix = false;  // prefix binning: buckets sorted only up to tile_sorted (render_fwd extends them)
     bool depth_onesweep = false, tile_onesweep = false;  // which sorts own a cleared onesweep error word
     if (!bucket) {
         // the depth sort's last pass also writes the tile counts and expansion records in depth order ("sort_gather"
@@ -567,6 +569,16 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
                                 ? im.order_fwd : nullptr; sp.keys = b.bk_keys; sp.keys2 = b.bk_keys2;
             sp.sorted_u = b.sorted_u; sp.long_list = im.bk_long_list; sp.long_cnt = g.counters + CNT_LONG;
             sp.tie_list = im.bk_tie_list; sp.tie_cnt = g.counters + CNT_TIES;
+            // prefix binning ("bk_prefix" instances, a multiple of 64 <= 512; 0: sort every bucket whole) where the
+            // composite runs whole tiles: tiles longer than that get only their front-most instances sorted, and a
+            // walk that outlives them selects its further batches itself (render_fwd)
+            const int pk = tuning("bk_prefix", 512);
+            if (pk > 0 && render_fwd_parts((int)T) == 1) {
+                sp.prefix_k = (uint32_t)std::min(512, std::max(64, pk / 64 * 64));
+                sp.tile_sorted = im.tile_sorted;
+                sp.tile_thresh = im.tile_thresh;
+                prefix = true;
+            }
             GSR_STAGE(ST_SEG_SORT, dbg, launch_seg_sort(stream, sp));
         } else {
             GSR_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * T, stream));
@@ -626,6 +638,11 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     rp.bg = a->background;
     rp.out_color = a->out_color; rp.out_invdepth = a->out_invdepth; rp.final_T = im.final_T;
     rp.n_contrib = im.n_contrib; rp.tile_last = im.tile_last;
+    rp.prefix_flag = im.tile_sorted + T;
+    if (prefix) {
+        rp.bk_keys = b.bk_keys; rp.tile_sorted = im.tile_sorted; rp.tile_thresh = im.tile_thresh;
+        rp.sorted_u_w = b.sorted_u;
+    }
     // checkpoints for the segmented backward ("bwd_seg" 1, spacing "seg_k" instances: 32 or a multiple of 64) while the image
     // has few tiles; the forward records in ck_flag whether it wrote them, so the backward never reads stale ones
     rp.ck_flag = im.ck_flag;

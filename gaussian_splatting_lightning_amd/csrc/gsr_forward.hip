@@ -24,10 +24,7 @@ struct CullIn {
 
 // Projection, conic, radius, SH colour and render records of one Gaussian.  Returns the area of its tile
 // rect (0: not rendered); the tile culling, tile count and sort key are finished by preprocess_kernel.
-// sh_row: the Gaussian's SH coefficients staged in LDS by the wave (SH_LDS), else null (read from p.shs).
-template <bool SH_LDS = false>
-__device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &p, const int i, CullIn &ci,
-                                                        const float *sh_row = nullptr) {
+__device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &p, const int i, CullIn &ci) {
     // uncontracted like the helpers it calls (gsr_common.h): radii, rects and render records bit-equal the oracle's
 #pragma clang fp contract(off)
     const GeomState &g = p.g;
@@ -98,7 +95,7 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
         dir = make_float3(dir.x / len, dir.y / len, dir.z / len);
         if (p.D > 0) {  // the colour and its direction Jacobian for the backward (9 planes, coalesced)
             float3 jx, jy, jz;
-            rgb = sh_eval_jac_dispatch(p.D, SH_LDS ? sh_row : p.shs + (size_t)i * p.M * 3, dir, jx, jy, jz);
+            rgb = sh_eval_jac_dispatch(p.D, p.shs + (size_t)i * p.M * 3, dir, jx, jy, jz);
             const size_t n = (size_t)p.P;
             float *J = g.sh_jac + i;
             J[0] = jx.x; J[n] = jx.y; J[2 * n] = jx.z;
@@ -143,53 +140,22 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
 #ifndef GSR_PRE_MINW
 #define GSR_PRE_MINW 4  // 112 VGPRs, no spills: cfg3 0.106 -> 0.103 ms against 5 waves (96 VGPRs, 2 spilled); 6: 0.112
 #endif
-// SH_LDS (M = 16, 16-B aligned coefficients): the wave loads its 64 Gaussians' coefficient rows (12 KB, contiguous)
-// with coalesced 16-B loads -- 12 per lane, each covering 1 KB of consecutive bytes -- into LDS at a 52-float row
-// stride (bank-conflict-free row reads, as preprocess_bwd's staging), and each lane evaluates its colour from LDS,
-// instead of 12 loads per lane that each touch 64 cache lines.  The culling's LDS arrays share the staging area.
-constexpr int PRE_SH_STRIDE = 52;
 struct PreCullLds {
     CullGauss cg[64];
     int4 rect[64];  // rx, ry, rw, start of the lane's pairs
     unsigned long long mask[64];
     int own[64];    // lane whose rect's pair run starts at this pair of the step, else -1
 };
-template <bool SH_LDS>
 __global__ __launch_bounds__(256, GSR_PRE_MINW) void preprocess_kernel(PreprocessParams p) {
-    constexpr size_t WAVE_LDS = SH_LDS ? (sizeof(PreCullLds) > 64 * PRE_SH_STRIDE * 4 ? sizeof(PreCullLds)
-                                                                                        : 64 * PRE_SH_STRIDE * 4)
-                                       : sizeof(PreCullLds);
-    __shared__ __attribute__((aligned(16))) unsigned char s_lds[4][WAVE_LDS];
+    __shared__ PreCullLds s_lds[4];
     __shared__ uint32_t s_w[4];
     const uint32_t bid = blockIdx.x;
     const int i = (int)bid * 256 + threadIdx.x;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    PreCullLds &L = *reinterpret_cast<PreCullLds *>(s_lds[w]);
+    PreCullLds &L = s_lds[w];
     CullIn ci;
     ci.need = false;
-    uint32_t area;
-    if constexpr (SH_LDS) {
-        float *ssh = reinterpret_cast<float *>(s_lds[w]);
-        const int i0 = (int)bid * 256 + w * 64;
-        const int nf4 = max(0, min(64, p.P - i0)) * 12;  // float4s of the wave's rows
-        const float4 *src = reinterpret_cast<const float4 *>(p.shs + (size_t)i0 * 48);
-        float4 v[12];
-#pragma unroll
-        for (int q = 0; q < 12; q++) {
-            const int f = q * 64 + lane;
-            v[q] = f < nf4 ? src[f] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#pragma unroll
-        for (int q = 0; q < 12; q++) {
-            const int f = q * 64 + lane, row = f / 12, c4 = f - row * 12;
-            *reinterpret_cast<float4 *>(ssh + row * PRE_SH_STRIDE + 4 * c4) = v[q];
-        }
-        wave_lds_sync();
-        area = i < p.P ? preprocess_gaussian<true>(p, i, ci, ssh + lane * PRE_SH_STRIDE) : 0u;
-        wave_lds_sync();  // the staging area becomes the culling arrays
-    } else {
-        area = i < p.P ? preprocess_gaussian<false>(p, i, ci) : 0u;
-    }
+    const uint32_t area = i < p.P ? preprocess_gaussian(p, i, ci) : 0u;
     const uint32_t need_area = ci.need ? area : 0u;
     const uint32_t incl = wave_inclusive_scan(need_area, lane);
     const uint32_t total = __shfl((int)incl, 63);
@@ -287,10 +253,7 @@ __global__ __launch_bounds__(256, GSR_PRE_MINW) void preprocess_kernel(Preproces
 
 void launch_preprocess(hipStream_t s, const PreprocessParams &p) {
     if (p.P <= 0) return;
-    const bool sh_lds = p.shs && !p.colors_precomp && p.M == 16 && p.D > 0 && ((uintptr_t)p.shs & 15) == 0 &&
-                        tuning("pre_sh_lds", 0) != 0;
-    if (sh_lds) preprocess_kernel<true><<<div_up(p.P, 256), 256, 0, s>>>(p);
-    else preprocess_kernel<false><<<div_up(p.P, 256), 256, 0, s>>>(p);
+    preprocess_kernel<<<div_up(p.P, 256), 256, 0, s>>>(p);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -617,7 +580,43 @@ void launch_tile_order(hipStream_t s, const uint2 *ranges, const uint32_t *tile_
 // + j), and at the end the pixel's final sums (ctot); the backward walks each ck_k-instance segment from the
 // checkpoint at its end.  A pixel still compositing at instance e is still walked when its wave reaches e, so every
 // checkpoint the backward reads (e < the pixel's n_contrib) is written.
-template <int NPIX, int MIN_WAVES, bool CKPT = false>
+// Prefix binning (seg_sort sorted only a tile's front-most instances): the next batch of a walk that outlives the
+// sorted prefix -- the cnt smallest bucketed keys of the tile above `last` (all keys when `none`), sorted, written to
+// out[0, cnt) -- selected by the wave in one pass over the tile's n keys: each 64-key chunk is sorted descending across
+// the lanes (bitonic, one key per lane) and merged into the running ascending best-64 (elementwise min, then a
+// bitonic clean).  Returns the largest selected key.  ~160 VALU per 64 keys of the tile: a slow path for the rare
+// tile that composites past its prefix (none at cfg 3).
+__device__ __forceinline__ unsigned long long u64_sel(bool take_min, unsigned long long a, unsigned long long b) {
+    return take_min == (a < b) ? a : b;
+}
+__device__ __forceinline__ unsigned long long prefix_extend(const unsigned long long *__restrict__ keys, uint32_t n,
+                                                            bool none, unsigned long long last,
+                                                            uint32_t *__restrict__ out, uint32_t cnt, int lane,
+                                                            uint32_t &mine) {
+    unsigned long long best = ~0ull;
+    for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+        unsigned long long x = c0 + lane < n ? keys[c0 + lane] : ~0ull;
+        if (!none && x <= last) x = ~0ull;
+        if (__ballot(x != ~0ull) == 0) continue;
+        for (int k = 2; k <= 64; k <<= 1) {      // descending bitonic sort of the chunk
+            const bool desc = k == 64 || (lane & k) == 0;
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                const unsigned long long y = __shfl_xor(x, j);
+                x = u64_sel(((lane & j) == 0) != desc, x, y);
+            }
+        }
+        best = best < x ? best : x;              // the 64 smallest of both, as a bitonic sequence
+        for (int j = 32; j > 0; j >>= 1) {       // clean it ascending
+            const unsigned long long y = __shfl_xor(best, j);
+            best = u64_sel((lane & j) == 0, best, y);
+        }
+    }
+    mine = (uint32_t)best;  // this lane's instance of the batch (its expansion index)
+    if ((uint32_t)lane < cnt) out[lane] = mine;
+    return __shfl(best, (int)cnt - 1);
+}
+
+template <int NPIX, int MIN_WAVES, bool CKPT = false, bool PREFIX = false>
 __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwdParams p) {
     constexpr int PARTS = 4 / NPIX;
     __shared__ FwdRec s_rec[4][64];
@@ -626,6 +625,7 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
     const int slot = blockIdx.x * 4 + w;
     if (p.ck_flag && slot == 0 && lane == 0) *p.ck_flag = CKPT ? p.ck_k : 0u;
     if (p.lpt_valid && slot == 0 && lane == 0) *p.lpt_valid = (PARTS == 1 && p.lpt_blist) ? 1u : 0u;
+    if (p.prefix_flag && slot == 0 && lane == 0) *p.prefix_flag = PREFIX ? 1u : 0u;
     if (slot >= p.num_tiles * PARTS) return;
     const int half = slot % PARTS;
     const int tile = __builtin_amdgcn_readfirstlane(p.tile_order ? (int)p.tile_order[slot / PARTS] : slot / PARTS);
@@ -654,6 +654,10 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
     uint32_t contributor = 0;
     uint32_t loaded_end = r0;
     FwdRec *sr = s_rec[w];
+    // prefix binning: instances [r0, r0 + ks) are sorted; a walk past them selects further batches itself
+    uint32_t ks = PREFIX ? __builtin_amdgcn_readfirstlane(p.tile_sorted[tile]) : 0u;
+    const uint32_t ks0 = ks;
+    unsigned long long last_key = PREFIX && ks ? p.tile_thresh[tile] : 0ull;
     // checkpoint before tile-relative instance e (a multiple of ck_k)
     auto store_ck = [&](uint32_t e) {
         float *ck = p.ckpt + (size_t)(r0 / p.ck_k + (uint32_t)tile + e / p.ck_k - 1) * CK_FLOATS;
@@ -669,10 +673,17 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
     };
     for (uint32_t base = r0; base < r1; base += 64) {
         if (CKPT && base > r0 && (base - r0) % p.ck_k == 0) store_ck(base - r0);
+        uint32_t u_sel = 0;
+        const bool ext = PREFIX && base >= r0 + ks;  // batch boundary: ks is a multiple of 64 or the whole tile
+        if (ext) {
+            const uint32_t cnt = min(64u, r1 - base);
+            last_key = prefix_extend(p.bk_keys + r0, r1 - r0, ks == 0, last_key, p.sorted_u_w + base, cnt, lane, u_sel);
+            ks += cnt;
+        }
         const uint32_t s = base + lane;
         uint32_t m = 0;
         if (s < r1) {
-            const uint32_t u = p.sorted_u[s];
+            const uint32_t u = ext ? u_sel : p.sorted_u[s];
             const uint32_t gid = p.inst_gid[u];
             p.point_list[s] = gid;
             p.inv[u] = s;
@@ -781,6 +792,7 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
         }
     }
     mx = wave_max_u32(mx);
+    if (PREFIX && ks != ks0 && lane == 0) p.tile_sorted[tile] = ks;
     if (lane == 0) {
         atomicMax(&p.tile_last[tile], mx);
         atomicMax(&p.tile_loaded[tile], loaded_end - r0);
@@ -793,23 +805,31 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
     stamp_store(p.stamps, slot, t_start, lane);
 }
 
+// "fwd_parts" 1, 2 or 4; 0 (default): 4 when that many part-waves still fit the GPU's ~8 resident waves per SIMD,
+// twice over (small images, where one heavy tile's latency sets the kernel time), else whole tiles (measured at
+// 1080p, 8160 tiles: whole tiles 0.175 ms against 0.196 in 2 parts; at 800x800, 2500 tiles: 4 parts 0.073, 2 parts
+// 0.092, whole 0.126)
+int render_fwd_parts(int num_tiles) {
+    int parts = tuning("fwd_parts", 0);
+    if (parts == 0) parts = num_tiles * 4 <= tuning("fwd_part_slots", 16384) ? 4 : 1;
+    return (parts == 2 || parts == 4) ? parts : 1;
+}
+
 void launch_render_fwd(hipStream_t s, const RenderFwdParams &p0) {
     if (p0.num_tiles <= 0) return;
     RenderFwdParams p = p0;
     p.strip_exact = tuning("strip_exact", 1);
     p.stamps = tuning("stamp", 0) ? stamp_buffer(0) : nullptr;
-    // "fwd_parts" 1, 2 or 4; 0 (default): 4 when that many part-waves still fit the GPU's ~8 resident waves per
-    // SIMD, twice over (small images, where one heavy tile's latency sets the kernel time), else whole tiles
-    // (measured at 1080p, 8160 tiles: whole tiles 0.175 ms against 0.196 in 2 parts; at 800x800, 2500 tiles:
-    // 4 parts 0.073, 2 parts 0.092, whole 0.126)
-    int parts = tuning("fwd_parts", 0);
-    if (parts == 0) parts = p.num_tiles * 4 <= tuning("fwd_part_slots", 16384) ? 4 : 1;
-    if (parts != 2 && parts != 4) parts = 1;
+    const int parts = render_fwd_parts(p.num_tiles);
     const dim3 grid(div_up((uint64_t)p.num_tiles * parts, 4)), block(256);
     if (parts == 1) {
         // 8 waves per SIMD (64 VGPRs, one 8-byte spill outside the pair loop): cfg3 0.180 -> 0.172 ms, cfg5 0.517 ->
         // 0.478 ms against 6 waves (65 VGPRs, i.e. 7 resident)
         const int mw = tuning("fwd_whole_waves", 8);
+        if (p.tile_sorted && p.bk_keys) {
+            render_fwd_v6_kernel<4, 8, false, true><<<grid, block, 0, s>>>(p);
+            return;
+        }
         if (mw >= 8) render_fwd_v6_kernel<4, 8><<<grid, block, 0, s>>>(p);
         else if (mw >= 6) render_fwd_v6_kernel<4, 6><<<grid, block, 0, s>>>(p);
         else render_fwd_v6_kernel<4, 4><<<grid, block, 0, s>>>(p);

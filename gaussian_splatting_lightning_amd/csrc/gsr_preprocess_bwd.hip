@@ -411,7 +411,9 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
 void launch_preprocess_bwd(hipStream_t s, const PreprocessBwdParams &p) {
     if (p.g1 <= p.g0) return;
     const uint32_t grid = div_up((uint32_t)(p.g1 - p.g0), 256);
-    if (p.sh_vec16 && tuning("pbwd_lds_sh", 1))
+    // the joint row gather and the LDS-staged dL/dsh stores; without dL/dsh (the compact multi-view exchange) only
+    // the gather, which the per-lane path pays ~40 % of the kernel for
+    if ((p.dL_dsh ? p.sh_vec16 : true) && tuning("pbwd_lds_sh", 1))
         preprocess_bwd_kernel<true><<<grid, 256, 0, s>>>(p);
     else
         preprocess_bwd_kernel<false><<<grid, 256, 0, s>>>(p);

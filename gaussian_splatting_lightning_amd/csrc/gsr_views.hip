@@ -10,20 +10,26 @@
 
 namespace gsr {
 
-template <int DEG>
+// M = 16 with a 16-B aligned output (STAGED): each half-wave's 32 rows are staged in LDS at a 52-float stride (as
+// preprocess_bwd's dL/dsh) and the wave stores them as coalesced float4s, not 12 stores per lane 192 B apart.
+constexpr int VIEWS_STRIDE = 52;
+template <int DEG, bool STAGED>
 __global__ __launch_bounds__(256) void sh_backward_views_kernel(int P, int M, int V, const float *__restrict__ means3D,
                                                                 const float *__restrict__ campos,
                                                                 const float *__restrict__ dc,
                                                                 float *__restrict__ dsh) {
     constexpr int NB = (DEG + 1) * (DEG + 1);
+    __shared__ __attribute__((aligned(16))) float s_row[STAGED ? 4 : 1][STAGED ? 32 * VIEWS_STRIDE : 1];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P) return;
-    const float mx = means3D[3 * i], my = means3D[3 * i + 1], mz = means3D[3 * i + 2];
+    if (!STAGED && i >= P) return;
+    const bool live = i < P;
+    const int ii = live ? i : P - 1;
+    const float mx = means3D[3 * ii], my = means3D[3 * ii + 1], mz = means3D[3 * ii + 2];
     float acc[3 * NB];
 #pragma unroll
     for (int k = 0; k < 3 * NB; k++) acc[k] = 0.f;
     for (int v = 0; v < V; v++) {
-        const float *d = dc + ((size_t)v * P + i) * 3;
+        const float *d = dc + ((size_t)v * P + ii) * 3;
         const float r = d[0], g = d[1], b = d[2];
         if (r == 0.f && g == 0.f && b == 0.f) continue;  // not rendered (or fully clamped) in view v
         const float dx = mx - campos[3 * v], dy = my - campos[3 * v + 1], dz = mz - campos[3 * v + 2];
@@ -36,6 +42,35 @@ __global__ __launch_bounds__(256) void sh_backward_views_kernel(int P, int M, in
             acc[3 * k + 1] += basis[k] * g;
             acc[3 * k + 2] += basis[k] * b;
         }
+    }
+    if constexpr (STAGED) {
+        const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        float *sw = s_row[w];
+        const size_t gbase = ((size_t)blockIdx.x * 256 + (size_t)w * 64) * 48, gend = (size_t)P * 48;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            wave_lds_sync();
+            if ((lane >> 5) == h) {
+                float *r = sw + (lane & 31) * VIEWS_STRIDE;
+#pragma unroll
+                for (int k = 0; k < 12; k++)
+                    *reinterpret_cast<float4 *>(r + 4 * k) =
+                        make_float4(4 * k < 3 * NB ? acc[4 * k < 3 * NB ? 4 * k : 0] : 0.f,
+                                    4 * k + 1 < 3 * NB ? acc[4 * k + 1 < 3 * NB ? 4 * k + 1 : 0] : 0.f,
+                                    4 * k + 2 < 3 * NB ? acc[4 * k + 2 < 3 * NB ? 4 * k + 2 : 0] : 0.f,
+                                    4 * k + 3 < 3 * NB ? acc[4 * k + 3 < 3 * NB ? 4 * k + 3 : 0] : 0.f);
+            }
+            wave_lds_sync();
+#pragma unroll
+            for (int c = 0; c < 6; c++) {  // 32 rows x 48 floats = 384 float4, 6 per lane
+                const uint32_t f = c * 256 + lane * 4;
+                const size_t go = gbase + (size_t)h * 1536 + f;
+                if (go < gend)
+                    *reinterpret_cast<float4 *>(dsh + go) =
+                        *reinterpret_cast<const float4 *>(sw + (f / 48) * VIEWS_STRIDE + f % 48);
+            }
+        }
+        return;
     }
     float *o = dsh + (size_t)i * M * 3;
     if (M == 16 && (((uintptr_t)dsh) & 15) == 0) {
@@ -56,12 +91,15 @@ void launch_sh_backward_views(hipStream_t s, int P, int D, int M, int V, const f
                               const float *dcolors_sh, float *dsh) {
     if (P <= 0) return;
     const dim3 grid(div_up(P, 256)), block(256);
+    const bool staged = M == 16 && (((uintptr_t)dsh) & 15) == 0 && tuning("views_staged", 1);
+#define GSR_VIEWS(D_, S_) sh_backward_views_kernel<D_, S_><<<grid, block, 0, s>>>(P, M, V, means3D, campos, dcolors_sh, dsh)
     switch (D) {
-        case 0: sh_backward_views_kernel<0><<<grid, block, 0, s>>>(P, M, V, means3D, campos, dcolors_sh, dsh); break;
-        case 1: sh_backward_views_kernel<1><<<grid, block, 0, s>>>(P, M, V, means3D, campos, dcolors_sh, dsh); break;
-        case 2: sh_backward_views_kernel<2><<<grid, block, 0, s>>>(P, M, V, means3D, campos, dcolors_sh, dsh); break;
-        default: sh_backward_views_kernel<3><<<grid, block, 0, s>>>(P, M, V, means3D, campos, dcolors_sh, dsh); break;
+        case 0: if (staged) GSR_VIEWS(0, true); else GSR_VIEWS(0, false); break;
+        case 1: if (staged) GSR_VIEWS(1, true); else GSR_VIEWS(1, false); break;
+        case 2: if (staged) GSR_VIEWS(2, true); else GSR_VIEWS(2, false); break;
+        default: if (staged) GSR_VIEWS(3, true); else GSR_VIEWS(3, false); break;
     }
+#undef GSR_VIEWS
 }
 
 }  // namespace gsr

@@ -273,6 +273,8 @@ typedef struct gsr_state_layout {
     size_t img_final_T, img_n_contrib, img_ranges, img_tile_last;     /* f32/u32 per pixel, uint2/u32 per tile */
     size_t img_tile_loaded;                                           /* u32 per tile */
     size_t geom_rec_stride;                                           /* bytes per render record (48) */
+    size_t img_tile_sorted;   /* u32 per tile: length of the tile's bucket sorted by the forward (prefix binning: a
+                                 prefix when the tile's walk ended before it; else the whole bucket) */
 } gsr_state_layout;
 void gsr_state_layout_query(int P, int64_t R, int W, int H, gsr_state_layout *out);
 

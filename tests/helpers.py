@@ -111,6 +111,11 @@ def hip_state_arrays(out: dict) -> dict:
         final_T=view(st.image_buffer, lay["img_final_T"], W * H, torch.float32).reshape(H, W),
         tiles=view(st.geom_buffer, lay["geom_tiles"], P, i32).astype(np.uint32),
         num_rendered=R)
+    # prefix binning: entry T is 1 when the forward ran in prefix mode, then entry t < T is the length
+    # of tile t's bucket in sorted order (>= its loaded instances); the rest of the bucket holds the same instances
+    ts = view(st.image_buffer, lay["img_tile_sorted"], T + 1, i32).astype(np.uint32)
+    res["prefix_mode"] = bool(ts[T] == 1)
+    res["tile_sorted"] = ts[:T]
     # render records: one 48-B (12-float) record per Gaussian, a = floats 0..3, b = 4..7, c = 8..9
     stride = lay["geom_rec_stride"] // 4
     rec = view(st.geom_buffer, lay["geom_rec_a"], stride * P, torch.float32).reshape(P, stride)

@@ -55,8 +55,8 @@ def compare_forward(inp, hip, oracle_out):
     assert hs["num_rendered"] == run.num_rendered
     assert np.array_equal(hs["tiles"], g["tiles_touched"])
     pl, rg = run.point_list(), run.ranges()
-    assert np.array_equal(hs["point_list"], pl)
     assert np.array_equal(hs["ranges"], rg)
+    check_point_list(hs, pl, rg)
     # the render records the compositor reads: the same bits for every rendered Gaussian
     on = radii > 0
     for k in ("xy", "conic_opacity"):
@@ -104,6 +104,25 @@ def compare_forward(inp, hip, oracle_out):
             touched[pl[rg[tt, 0]: rg[tt, 0] + m]] = True
     run.flip_touched = touched
     return run
+
+
+def check_point_list(hs, pl, rg):
+    """The sorted instance list against the reference order: bit-exact everywhere, or -- in prefix binning mode -- on
+    every tile's sorted prefix (which covers every instance the forward loaded), with the rest of each tile's bucket
+    holding exactly the reference's instances."""
+    hp = hs["point_list"]
+    if not hs["prefix_mode"]:
+        assert np.array_equal(hp, pl)
+        return
+    n = (rg[:, 1] - rg[:, 0]).astype(np.int64)
+    ts = hs["tile_sorted"].astype(np.int64)
+    live = n > 0
+    assert np.all(ts[live] <= n[live]) and np.all(ts[live] >= hs["tile_loaded"][live])
+    tile_of = np.repeat(np.arange(len(n)), n)
+    rel = np.arange(len(pl)) - rg[tile_of, 0].astype(np.int64)
+    srt = rel < ts[tile_of]
+    assert np.array_equal(hp[srt], pl[srt])
+    assert np.array_equal(hp[np.lexsort((hp, tile_of))], pl[np.lexsort((pl, tile_of))])
 
 
 def compare_backward(hip, run, dc, di, tol):
@@ -709,6 +728,44 @@ def test_binning_paths_are_bitwise_identical(gpu_device, W, H, onesweep, cscan, 
         assert np.array_equal(ref[k], alt[k]), k
     for k in GRADS:
         assert np.array_equal(ref["grads"][k], alt["grads"][k]), k
+
+
+@pytest.mark.parametrize("n,k,dup", [(600_000, 512, False), (600_000, 64, False), (300_000, 512, True)])
+def test_prefix_binning_is_bitwise_the_full_sort(gpu_device, n, k, dup):
+    """Prefix binning (whole-tile composite, > 4096 tiles): buckets longer than k get only their k front-most instances
+    sorted and the forward selects further batches itself when a tile's walk outlives them.  Every output, gradient and
+    loaded instance is bitwise that of sorting every bucket whole -- with the default k (no walk outlives it here),
+    with k = 64 (most walks extend their prefix, batch after batch), and on duplicated Gaussians whose exact depth ties
+    the proxy-key sort cannot order (those tiles get no sorted prefix at all)."""
+    from gaussian_splatting_lightning_amd import _native
+    W, H = 1920, 1080
+    inp = scene_inputs(n, W, H, sh_degree=3, seed=8)
+    if dup:
+        for key in ("means3D", "scales", "rotations", "opacities", "shs"):
+            inp[key][1000:1400] = inp[key][1000]
+            inp[key][7000:7300] = inp[key][7001]
+    dc, di = upstream(W, H, 8)
+    try:
+        _native.set_tuning("bk_prefix", 0)
+        ref = run_hip(inp, gpu_device, dc, di)
+        _native.set_tuning("bk_prefix", k)
+        alt = run_hip(inp, gpu_device, dc, di)
+    finally:
+        _native.set_tuning("bk_prefix", 512)
+    a, b = hip_state_arrays(ref), hip_state_arrays(alt)
+    assert not a["prefix_mode"] and b["prefix_mode"]
+    for key in ("ranges", "tiles", "n_contrib", "tile_last", "tile_loaded"):
+        assert np.array_equal(a[key], b[key]), key
+    for key in ("color", "invdepth", "radii"):
+        assert np.array_equal(ref[key], alt[key]), key
+    for key in GRADS:
+        assert np.array_equal(ref["grads"][key], alt["grads"][key]), key
+    rg = a["ranges"]
+    check_point_list(b, a["point_list"], rg)
+    nt = (rg[:, 1] - rg[:, 0]).astype(np.int64)
+    assert np.any(b["tile_sorted"] < nt)  # some bucket really was sorted only in part
+    if k == 64:
+        assert np.any((b["tile_sorted"] > 64) & (nt > b["tile_sorted"]))  # walks extended their prefix
 
 
 def test_beyond_lpt_and_bucket_tile_limits(gpu_device):
