@@ -754,7 +754,7 @@ __device__ bool seg_prefix_sort(const unsigned long long *__restrict__ keys, uin
     for (int q = 0; q < w; q++) pos += misc[16 + q];
     for (uint32_t i = tid; i < n; i += 256) {
         const unsigned long long key = k0[i];
-        if (((key - base) >> sh) <= P) cbuf[pos++] = key;
+        if (((key - base) >> sh) <= P && pos < 512u) cbuf[pos++] = key;  // exactly K <= 512 are selected
     }
     __syncthreads();
     if (w == 0) {
