@@ -85,7 +85,7 @@ class StateLayout(ctypes.Structure):
     _fields_ = [(n, ctypes.c_size_t) for n in (
         "geom_rec_a", "geom_rec_b", "geom_rec_c", "geom_tiles", "geom_order", "geom_inst_off", "geom_inst_start",
         "geom_clamped", "geom_depth_key", "geom_expand_rec", "bin_point_list", "bin_inv", "bin_keys_sorted", "bin_sorted_u", "bin_inst_gid",
-        "img_final_T", "img_n_contrib", "img_ranges", "img_tile_last", "img_tile_loaded", "geom_rec_stride", "img_tile_sorted")]
+        "img_final_T", "img_n_contrib", "img_ranges", "img_tile_last", "img_tile_loaded", "geom_rec_stride", "img_tile_sorted", "bin_bk_keys", "img_tile_lastkey")]
 
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t)

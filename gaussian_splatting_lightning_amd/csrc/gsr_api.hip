@@ -376,12 +376,14 @@ void gsr_state_layout_query(int P, int64_t R, int W, int H, gsr_state_layout *ou
     out->geom_expand_rec = off(g.exp_rec);
     out->geom_depth_key = off(g.depth_key);
     out->bin_point_list = off(b.point_list);
-    out->bin_inv = off(b.inv);
+    out->bin_inv = 0;  // no inverse permutation any more (ImageState::tile_lastkey, instance_loaded)
     out->bin_keys_sorted = off(b.keys_sorted);
     out->bin_sorted_u = off(b.sorted_u);
     out->bin_inst_gid = off(b.inst_gid);
     out->img_tile_loaded = off(im.tile_loaded);
     out->img_tile_sorted = off(im.tile_sorted);
+    out->bin_bk_keys = off(b.bk_keys);
+    out->img_tile_lastkey = off(im.tile_lastkey);
     out->img_final_T = off(im.final_T);
     out->img_n_contrib = off(im.n_contrib);
     out->img_ranges = off(im.ranges);
@@ -558,7 +560,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
         return fail(GSR_ERR_OVERFLOW, "too many tile instances for the single-level scan");
     if (bucket) {
         if (R > 0) {
-            bp.keys = b.bk_keys; bp.inst_gid = b.inst_gid; bp.inv = b.inv;
+            bp.keys = b.bk_keys; bp.inst_gid = b.inst_gid;
             bp.order = lpt ? im.order_fwd : nullptr;
             bp.lpt_shift = tuning("lpt_shift", 3);
             GSR_STAGE(ST_BK_SCATTER, dbg, launch_bucket_scatter(stream, bp));  // and the forward LPT order
@@ -598,13 +600,6 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             ep.keys_out = k16 ? nullptr : b.sort.k[0];
             ep.keys16_out = k16 ? reinterpret_cast<uint16_t *>(b.sort.k[0]) : nullptr;
             ep.inst_gid = b.inst_gid; ep.inst_start = g.inst_start;
-#ifndef GSR_EXP_INV
-#define GSR_EXP_INV 1
-#endif
-            // inv = INV_NONE for every instance: written by the expansion beside its keys (16-B stores at the same
-            // indices), or by a separate fill ("exp_inv" 0)
-            const bool exp_inv = tuning("exp_inv", GSR_EXP_INV) != 0;
-            ep.inv_none = exp_inv ? b.inv : nullptr;
             GSR_STAGE(ST_EXPAND, dbg, launch_expand(stream, ep));
             if (k16)
                 GSR_STAGE(ST_TILE_SORT, dbg, launch_radix_sort16(stream, b.sort, R, tile_key_bits(T)));
@@ -613,7 +608,6 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
                           launch_radix_sort(stream, b.sort, R, tile_key_bits(T), false, nullptr, nullptr,
                                             &tile_onesweep));
             keys16 = k16;
-            if (!exp_inv) GSR_HIP(hipMemsetAsync(b.inv, 0xff, sizeof(uint32_t) * (size_t)R, stream));
         }
         GSR_STAGE(ST_RANGES, dbg, {
             GSR_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * T, stream));
@@ -633,7 +627,8 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     rp.W = W; rp.H = H; rp.gx = gx; rp.gy = gy; rp.num_tiles = (int)T;
     rp.tile_order = lpt ? im.order_fwd : nullptr;
     rp.ranges = im.ranges; rp.sorted_u = b.sorted_u; rp.inst_gid = b.inst_gid;
-    rp.point_list = b.point_list; rp.inv = b.inv; rp.tile_loaded = im.tile_loaded;
+    rp.point_list = b.point_list; rp.tile_loaded = im.tile_loaded;
+    rp.depth_key = g.depth_key; rp.tile_lastkey = im.tile_lastkey;
     rp.rec = g.rec;
     rp.bg = a->background;
     rp.out_color = a->out_color; rp.out_invdepth = a->out_invdepth; rp.final_T = im.final_T;
@@ -708,7 +703,6 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     float *rows = reinterpret_cast<float *>(scratch);
     // Gaussian-major gradient rows: render_bwd scatters its 40-B rows to the instances' expansion indices so
     // the per-Gaussian gather in preprocess_bwd reads each Gaussian's rows contiguously.
-    const int rows_by_u = tuning("rows_by_u", 1);
     float *bigsum = bwd_bigsum_ptr(scratch, R);
 
     if (R > 0 && a->stages != GSR_BWD_GAUSSIANS) {
@@ -732,7 +726,6 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
         rp.bg = a->background; rp.final_T = im.final_T; rp.dL_dpix = a->dL_dpix; rp.dL_dinvdepth = a->dL_dinvdepth;
         rp.rows = rows;
         rp.sorted_u = b.sorted_u;
-        rp.rows_by_u = rows_by_u;
         if (T <= SEG_MAX_TILES && tuning("bwd_seg", 1)) {  // segmented walk (from the forward's checkpoints, if any)
             rp.ckpt = b.ckpt; rp.ctot = im.ctot; rp.ck_flag = im.ck_flag;
             rp.seg_list = b.seg_list; rp.seg_count = im.seg_count;
@@ -740,7 +733,8 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
         GSR_STAGE(ST_RENDER_BWD, dbg, launch_render_bwd(stream, rp));
         BigReduceParams bp;
         bp.big_list = g.big_list; bp.inst_start = g.inst_start; bp.tiles = g.tiles;
-        bp.inv = b.inv; bp.rows = rows; bp.bigsum = bigsum; bp.rows_by_u = rows_by_u;
+        bp.exp_rec = g.exp_rec; bp.depth_key = g.depth_key; bp.tile_lastkey = im.tile_lastkey; bp.gx = (uint32_t)gx;
+        bp.rows = rows; bp.bigsum = bigsum;
         bp.nbig_dev = nbig_on_device ? g.counters + CNT_BIG : nullptr;
         GSR_STAGE(ST_BIG_REDUCE, dbg, launch_big_reduce(stream, bp, nbig));
     }
@@ -763,9 +757,9 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     pp.means3D = a->means3D; pp.opacities = a->opacities; pp.scales = a->scales; pp.rotations = a->rotations;
     pp.cov3D_precomp = a->cov3D_precomp; pp.shs = (a->colors_precomp ? nullptr : a->shs);
     pp.view = a->viewmatrix; pp.proj = a->projmatrix; pp.campos = a->campos;
-    pp.radii = a->radii; pp.tiles = g.tiles; pp.inst_start = g.inst_start; pp.inv = b.inv; pp.clamped = g.clamped;
+    pp.radii = a->radii; pp.tiles = g.tiles; pp.inst_start = g.inst_start; pp.clamped = g.clamped;
+    pp.exp_rec = g.exp_rec; pp.depth_key = g.depth_key; pp.tile_lastkey = im.tile_lastkey; pp.gx = (uint32_t)gx;
     pp.sh_jac = g.sh_jac;  // the forward's d rgb / d dir: the SH term of dL/dmeans3D reads no coefficient
-    pp.rows_by_u = rows_by_u;
     pp.big_slot = g.big_slot; pp.bigsum = bigsum;
     pp.rows = rows;
     pp.sh_vec16 = pp.shs && a->M == 16 && (((uintptr_t)pp.shs | (uintptr_t)a->dL_dsh) & 15) == 0 &&

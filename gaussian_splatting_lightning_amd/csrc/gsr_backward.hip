@@ -128,7 +128,7 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
     const uint32_t loaded = p.tile_loaded[tile];
     for (uint32_t s = range.x + tl + threadIdx.x; s < range.x + loaded; s += 64 * PARTS) {
         const float z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        store_row(p.rows, p.rows_by_u ? p.sorted_u[s] : s, z);
+        store_row(p.rows, p.sorted_u[s], z);
     }
     if (tl == 0) return;  // workgroup-uniform
 
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
         uint32_t my_row = 0;
         if (w == 0 && lane < cnt) {
             const uint32_t s_me = range.x + (uint32_t)(bend - 1 - lane);
-            my_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
+            my_row = p.sorted_u[s_me];
             const uint32_t gid = p.point_list[s_me];
             my_a = p.rec[gid].a;
             my_b = p.rec[gid].b;
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(64, SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MINW) void ren
     if (last_seg)
         for (uint32_t s = r0 + tl + lane; s < r0 + loaded; s += 64) {
             const float z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-            store_row(p.rows, p.rows_by_u ? p.sorted_u[s] : s, z);
+            store_row(p.rows, p.sorted_u[s], z);
         }
     if (hi == 0) {
         stamp_store(p.stamps, slot, t_start, lane);
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(64, SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MINW) void ren
         uint32_t my_row = 0, my_m = 0;
         if (lane < cnt) {
             const uint32_t s_me = r0 + (uint32_t)(bend - 1 - lane);
-            my_row = p.rows_by_u ? p.sorted_u[s_me] : s_me;
+            my_row = p.sorted_u[s_me];
             const uint32_t gid = p.point_list[s_me];
             my_a = p.rec[gid].a;
             my_b = p.rec[gid].b;
@@ -633,34 +633,30 @@ __global__ __launch_bounds__(256) void big_reduce_kernel(BigReduceParams p) {
     const uint32_t gidx = p.big_list[bi];
     const uint32_t start = p.inst_start[gidx], cnt = p.tiles[gidx];
     float acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    if (p.rows_by_u) {
-        // rows by expansion index: BR_UNROLL inv words per thread are loaded together, then the rows of the
-        // loaded instances (most instances of a big Gaussian sit in saturated tiles and have none), summed in the
-        // same k order as one at a time
-        constexpr int BR_UNROLL = 4;
-        for (uint32_t k0 = threadIdx.x; k0 < cnt; k0 += 256 * BR_UNROLL) {
-            float r[BR_UNROLL][10];
-            bool use[BR_UNROLL];
+    // rows by expansion index (every cell of a big Gaussian's rect is an instance): BR_UNROLL loaded-instance tests
+    // per thread (the tile of row k and its last loaded key, instance_loaded) go first, then the rows of the loaded
+    // instances (most instances of a big Gaussian sit in saturated tiles and have none), summed in the same k order as
+    // one at a time
+    const uint4 e = p.exp_rec[gidx];
+    const uint32_t dk = p.depth_key[gidx];
+    constexpr int BR_UNROLL = 4;
+    for (uint32_t k0 = threadIdx.x; k0 < cnt; k0 += 256 * BR_UNROLL) {
+        float r[BR_UNROLL][10];
+        bool use[BR_UNROLL];
 #pragma unroll
-            for (int q = 0; q < BR_UNROLL; q++) {
-                const uint32_t k = k0 + 256 * q;
-                use[q] = k < cnt && p.inv[start + k] != INV_NONE;
+        for (int q = 0; q < BR_UNROLL; q++) {
+            const uint32_t k = k0 + 256 * q;
+            use[q] = k < cnt && instance_loaded(dk, start + k, p.tile_lastkey[instance_tile(e, k, p.gx)]);
+        }
+#pragma unroll
+        for (int q = 0; q < BR_UNROLL; q++)
+            if (use[q]) load_row(p.rows, start + k0 + 256 * q, r[q]);
+#pragma unroll
+        for (int q = 0; q < BR_UNROLL; q++)
+            if (use[q]) {
+#pragma unroll
+                for (int v = 0; v < 10; v++) acc[v] += r[q][v];
             }
-#pragma unroll
-            for (int q = 0; q < BR_UNROLL; q++)
-                if (use[q]) load_row(p.rows, start + k0 + 256 * q, r[q]);
-#pragma unroll
-            for (int q = 0; q < BR_UNROLL; q++)
-                if (use[q]) {
-#pragma unroll
-                    for (int v = 0; v < 10; v++) acc[v] += r[q][v];
-                }
-        }
-    } else {
-        for (uint32_t k = threadIdx.x; k < cnt; k += 256) {
-            const uint32_t sidx = p.inv[start + k];
-            if (sidx != INV_NONE) add_row(p.rows, sidx, acc);
-        }
     }
 #pragma unroll
     for (int v = 0; v < 10; v++) {

@@ -159,7 +159,6 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
                         const uint32_t slot = atomicAdd(&s_tab[tile], 1u);
                         p.keys[slot] = ((unsigned long long)x.z << 32) | ui;
                         p.inst_gid[ui] = g0 + (uint32_t)o;
-                        p.inv[ui] = INV_NONE;
                     }
                 }
             }
@@ -182,7 +181,6 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
                 const uint32_t slot = atomicAdd(&s_tab[tile], 1u);
                 p.keys[slot] = dk | (u0 + c);
                 p.inst_gid[u0 + c] = gb;
-                p.inv[u0 + c] = INV_NONE;
             }
         }
     }
@@ -278,6 +276,7 @@ __global__ __launch_bounds__(64 * CW) void bk_columns_kernel(BucketParams p) {
             p.tile_cnt[t] = tot;
             p.tile_last[t] = 0u;
             p.tile_loaded[t] = 0u;
+            p.tile_lastkey[t] = 0ull;
             if (t == T - 1) p.tile_start[T] = st + tot;
         }
         const bool l0 = t < T && tot > SEG_CAP && tot <= SEG_BLOCK_CAP, l1 = t < T && tot > SEG_BLOCK_CAP;

@@ -164,7 +164,6 @@ struct BinningState {
     uint32_t *inst_gid;    // R: Gaussian of each instance (expansion order)
     uint32_t *point_list;  // R: Gaussian ids sorted by (tile, depth, id); written by the forward composite
                            //    for the instances it loads (every instance any pixel can reach)
-    uint32_t *inv;         // R: expansion index -> sorted position, for loaded instances; else INV_NONE
     uint32_t *sorted_u;    // R: expansion index of each sorted instance
     // scratch of the two binning paths (overlapping: only one runs per forward)
     uint32_t *keys_sorted; // radix path: R tile ids of the sorted instances
@@ -190,7 +189,6 @@ inline size_t carve_binning(char *base, int64_t R, uint32_t num_tiles, BinningSt
     uint32_t n = (uint32_t)R;
     b.inst_gid = c.take<uint32_t>(n ? n : 1);
     b.point_list = c.take<uint32_t>(n ? n : 1);
-    b.inv = c.take<uint32_t>(n ? n : 1);
     b.sorted_u = c.take<uint32_t>(n ? n : 1);
     Carver cr = c;  // radix view
     int passes = radix_passes(tile_key_bits(num_tiles));
@@ -219,6 +217,8 @@ struct ImageState {
     uint2 *ranges;        // T
     uint32_t *tile_last;  // T: max n_contrib over the tile's pixels
     uint32_t *tile_loaded; // T: instances of the tile the forward composite gathered (>= tile_last)
+    unsigned long long *tile_lastkey;  // T: key (depth bits << 32 | u) of the last instance the composite gathered, 0 if
+                                       //    none (zeroed with tile_last / tile_loaded: instance_loaded)
     uint32_t *lpt_bcnt;    // 256: tiles per backward LPT bucket, appended by the forward's whole-tile waves (cleared
                            //      with tile_last / tile_loaded)
     uint32_t *order_fwd;   // tiles in descending forward work (instances in range), LPT launch order
@@ -261,6 +261,7 @@ inline size_t carve_image(char *base, int W, int H, ImageState &im) {
     im.ranges = c.take<uint2>((size_t)gx * gy + 1);
     im.tile_last = c.take<uint32_t>((size_t)gx * gy + 1);
     im.tile_loaded = c.take<uint32_t>((size_t)gx * gy + 1);
+    im.tile_lastkey = c.take<unsigned long long>((size_t)gx * gy + 1);  // inside the range the radix path zeroes
     im.lpt_bcnt = c.take<uint32_t>(256);
     im.order_fwd = c.take<uint32_t>((size_t)gx * gy + 1);
     im.order_bwd = c.take<uint32_t>((size_t)gx * gy + 1);
@@ -787,6 +788,35 @@ __device__ __forceinline__ uint32_t rect_tile(uint32_t c, uint32_t rx, uint32_t 
                                               uint32_t gx) {
     const uint32_t cy = (uint32_t)(((float)c + 0.5f) * inv_w);
     return (ry + cy) * gx + rx + (c - cy * w);
+}
+
+// Tile of a Gaussian's j-th instance (Gaussian-major expansion index inst_start + j): its expansion record's j-th kept
+// rect cell (the j-th set bit of the kept-tile mask; mask 0 = every cell, the j-th).
+__device__ __forceinline__ uint32_t instance_tile(uint4 e, uint32_t j, uint32_t gx) {
+    uint64_t m = (uint64_t)e.x | ((uint64_t)e.y << 32);
+    uint32_t c = j;
+    if (m) {  // j-th set bit: binary search on popcounts
+        c = 0;
+        uint32_t r = j;
+#pragma unroll
+        for (int wd = 32; wd >= 1; wd >>= 1) {
+            const uint32_t cnt = (uint32_t)__popcll(m & ((1ull << wd) - 1ull));
+            if (r >= cnt) {
+                r -= cnt;
+                m >>= wd;
+                c += (uint32_t)wd;
+            }
+        }
+    }
+    return rect_tile(c, e.z & 0xffffu, e.z >> 16, e.w, 1.0f / (float)e.w, gx);
+}
+// Whether the forward composite loaded instance u (of a Gaussian with depth bits dk) in its tile: the composite loads a
+// prefix of the tile's (depth, u)-sorted bucket, and records the key of the last instance it loaded per tile
+// (ImageState::tile_lastkey, 0 when none), so the instance was loaded iff its key is not above that one.  This
+// replaces an inverse-permutation word per instance, which the composite had to scatter (a random 4-B store per
+// loaded instance) and the binning had to fill.
+__device__ __forceinline__ bool instance_loaded(uint32_t dk, uint32_t u, unsigned long long lastkey) {
+    return (((unsigned long long)dk << 32) | u) <= lastkey;
 }
 
 // Orders LDS writes before later LDS reads of other lanes of the SAME wave (no s_barrier).

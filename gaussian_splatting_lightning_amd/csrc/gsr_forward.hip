@@ -383,13 +383,11 @@ __global__ __launch_bounds__(256) void expand_kernel(ExpandParams p) {
         else
             *reinterpret_cast<uint4 *>(p.keys_out + ub) = make_uint4(key[0], key[1], key[2], key[3]);
         *reinterpret_cast<uint4 *>(p.inst_gid + ub) = make_uint4(gv[0], gv[1], gv[2], gv[3]);
-        if (p.inv_none) *reinterpret_cast<uint4 *>(p.inv_none + ub) = make_uint4(INV_NONE, INV_NONE, INV_NONE, INV_NONE);
     } else {
         for (uint32_t u = ub; u < u1; u++) {
             if (p.keys16_out) p.keys16_out[u] = (uint16_t)key[u - ub];
             else p.keys_out[u] = key[u - ub];
             p.inst_gid[u] = gv[u - ub];
-            if (p.inv_none) p.inv_none[u] = INV_NONE;
         }
     }
 }
@@ -563,8 +561,9 @@ void launch_tile_order(hipStream_t s, const uint2 *ranges, const uint32_t *tile_
 // Front-to-back: alpha = min(0.99, o*exp(power)); skip alpha < 1/255; stop a pixel before the Gaussian that
 // would take T below 1e-4.  No block barriers: the four waves of a block work on four independent tiles.
 // The batch gather also materialises, for exactly the instances it loads, the sorted Gaussian id list
-// (point_list) and the inverse permutation (inv) that the backward needs, so the tile sort itself writes
-// only coalesced runs; instances no pixel reaches are never gathered and keep inv = INV_NONE.
+// (point_list) the backward walks, and per tile the key of the last instance it loaded (tile_lastkey), from which the
+// backward's per-Gaussian gather tells the instances that have a gradient row (instance_loaded): no per-instance
+// inverse permutation is scattered, nor filled by the binning.
 // Every piece of per-instance control is wave-uniform: the tile, its range and the contributor counter live
 // in SGPRs, each batch's strip masks (cell_mask) are ballots (bit j = instance j can reach the strip), and the
 // records of a batch sit in one LDS array of 48-byte entries read with immediate offsets.
@@ -653,6 +652,7 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
     const uint32_t r0 = __builtin_amdgcn_readfirstlane(rg.x), r1 = __builtin_amdgcn_readfirstlane(rg.y);
     uint32_t contributor = 0;
     uint32_t loaded_end = r0;
+    uint32_t u_last = 0, g_last = 0;  // the last loaded instance (its key, instance_loaded, is recorded per tile)
     FwdRec *sr = s_rec[w];
     // prefix binning: instances [r0, r0 + ks) are sorted; a walk past them selects further batches itself
     uint32_t ks = PREFIX ? __builtin_amdgcn_readfirstlane(p.tile_sorted[tile]) : 0u;
@@ -681,12 +681,11 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
             ks += cnt;
         }
         const uint32_t s = base + lane;
-        uint32_t m = 0;
+        uint32_t m = 0, u = 0, gid = 0;
         if (s < r1) {
-            const uint32_t u = ext ? u_sel : p.sorted_u[s];
-            const uint32_t gid = p.inst_gid[u];
+            u = ext ? u_sel : p.sorted_u[s];
+            gid = p.inst_gid[u];
             p.point_list[s] = gid;
-            p.inv[u] = s;
             const float4 ga = p.rec[gid].a, gb = p.rec[gid].b;
             sr[lane].a = stage_rec_a(ga);
             sr[lane].b = stage_rec_b(gb);
@@ -697,6 +696,8 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
 #pragma unroll
         for (int k = 0; k < NPIX; k++) sk[k] = livek[k] ? __ballot((m >> k) & 1u) : 0ull;  // finished strips: none
         loaded_end = min(r1, base + 64u);
+        u_last = __builtin_amdgcn_readlane((int)u, (int)(loaded_end - 1 - base));
+        g_last = __builtin_amdgcn_readlane((int)gid, (int)(loaded_end - 1 - base));
         wave_lds_sync();
         // walk only the batch's instances that reach a live strip (in order): instances whose strips are all
         // unreachable or finished cost nothing
@@ -796,6 +797,8 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
     if (lane == 0) {
         atomicMax(&p.tile_last[tile], mx);
         atomicMax(&p.tile_loaded[tile], loaded_end - r0);
+        if (loaded_end > r0)  // parts of a tile: the largest key is the one at the furthest loaded position
+            atomicMax(&p.tile_lastkey[tile], ((unsigned long long)p.depth_key[g_last] << 32) | u_last);
         if (PARTS == 1 && p.lpt_blist) {  // whole tile: mx is final; append it to its backward LPT bucket
             const uint32_t b = lpt_log_bucket(mx);
             const uint32_t pos = atomicAdd(&p.lpt_bcnt[b], 1u);

@@ -72,7 +72,6 @@ struct ExpandParams {
     uint32_t *exp_owner;      // optional: owner ranks of the block starts (div_up(R, EXP_TILE) + 1 words)
     uint32_t *keys_out, *inst_gid, *inst_start;
     uint16_t *keys16_out;     // optional: 16-bit tile keys (launch_radix_sort16) instead of keys_out
-    uint32_t *inv_none;       // optional: inv, set to INV_NONE for every instance here (no separate fill)
 };
 void launch_expand(hipStream_t s, const ExpandParams &p);
 
@@ -101,10 +100,10 @@ struct BucketParams {
     uint32_t lb_patience;  // look-back polls before recomputing an unpublished predecessor
     int lb_force;          // recompute every predecessor (tests the fallback)
     uint32_t *tile_last, *tile_loaded;  // T each: cleared by the column pass for the forward composite
+    unsigned long long *tile_lastkey;   // T: likewise
     uint32_t *lpt_bcnt;    // 256: cleared by the column pass (the forward's backward-LPT bucket counts)
     unsigned long long *keys;  // R: depth << 32 | u, bucketed by tile
     uint32_t *inst_gid;    // R
-    uint32_t *inv;         // R: reset to INV_NONE by the scatter (the forward composite fills it)
     uint32_t *order;       // scatter: an extra workgroup writes the forward LPT order here (or null: none)
     int lpt_shift;
     int xcd_major;         // bucket runs in XCD-major block order (bk_row_block)
@@ -141,7 +140,9 @@ struct RenderFwdParams {
     const uint2 *ranges;
     const uint32_t *tile_order;  // launch slot -> tile (heaviest first), or null for identity
     const uint32_t *sorted_u, *inst_gid;
-    uint32_t *point_list, *inv, *tile_loaded;
+    uint32_t *point_list, *tile_loaded;
+    const uint32_t *depth_key;            // per Gaussian: the key of the last loaded instance needs its depth bits
+    unsigned long long *tile_lastkey;     // T: key of the last instance each tile's walk loaded (atomicMax, zeroed)
     const GRec *rec;
     const float *bg;
     float *out_color, *out_invdepth, *final_T;
@@ -175,11 +176,10 @@ struct RenderBwdParams {
     const uint2 *ranges;
     const uint32_t *tile_order;  // launch slot -> tile (heaviest first), or null for identity
     const uint32_t *point_list, *n_contrib, *tile_last, *tile_loaded;
-    const uint32_t *sorted_u;  // sorted position -> expansion index u (rows_by_u)
+    const uint32_t *sorted_u;  // sorted position -> expansion index u: an instance's gradient row is row u
     const GRec *rec;
     const float *bg, *final_T, *dL_dpix, *dL_dinvdepth;
     float *rows;    // R x GRAD_ROW
-    int rows_by_u;  // 1: row of an instance at its expansion index u (Gaussian-major), 0: at its sorted position
     uint4 *stamps;  // diagnostics (set by launch), or null
     int strip_exact;  // as RenderFwdParams::strip_exact (set by launch)
     uint64_t num_rendered = 0;  // instances (the launch's walk-variant choice)
@@ -195,8 +195,11 @@ struct RenderBwdParams {
 void launch_render_bwd(hipStream_t s, const RenderBwdParams &p);
 
 struct BigReduceParams {
-    const uint32_t *big_list, *inst_start, *tiles, *inv;
-    int rows_by_u;
+    const uint32_t *big_list, *inst_start, *tiles;
+    const uint4 *exp_rec;           // per Gaussian: the tile of each row (instance_tile)
+    const uint32_t *depth_key;      // per Gaussian: the instances' keys (instance_loaded)
+    const unsigned long long *tile_lastkey;
+    uint32_t gx;
     const float *rows;
     float *bigsum;  // nbig x GRAD_ROW
     const uint32_t *nbig_dev;  // or null: the launch's nbig is exact; else an upper bound and this the count
@@ -213,8 +216,11 @@ struct PreprocessBwdParams {
     const float *means3D, *opacities, *scales, *rotations, *cov3D_precomp, *shs;
     const float *view, *proj, *campos;
     const int *radii;
-    const uint32_t *tiles, *inst_start, *inv, *big_slot;
-    int rows_by_u;
+    const uint32_t *tiles, *inst_start, *big_slot;
+    const uint4 *exp_rec;           // per Gaussian: the tile of each row (instance_tile)
+    const uint32_t *depth_key;      // per Gaussian: the instances' keys (instance_loaded)
+    const unsigned long long *tile_lastkey;
+    uint32_t gx;
     const uint8_t *clamped;
     const float *sh_jac;  // 9 x P direction Jacobian of the colour, from the forward (SH degree > 0)
     const float *rows, *bigsum;

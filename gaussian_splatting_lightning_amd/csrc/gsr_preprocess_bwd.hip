@@ -67,17 +67,20 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
         if (cnt > BIG_GAUSSIAN_TILES) {
             add_row(p.bigsum, p.big_slot[i], gs);
         } else {
-            // issue the index loads, then all row loads of a group, before summing (memory-level parallelism)
+            // the loaded-instance tests first, then all row loads of a group, before summing (memory-level parallelism)
+            const uint4 e = p.exp_rec[i];
+            const uint32_t dk = p.depth_key[i];
             for (uint32_t k0 = 0; k0 < cnt; k0 += 4) {
-                uint32_t sidx[4];
+                bool use[4];
 #pragma unroll
-                for (int j = 0; j < 4; j++) sidx[j] = (k0 + j < cnt) ? p.inv[start + k0 + j] : INV_NONE;
+                for (int j = 0; j < 4; j++)
+                    use[j] = k0 + j < cnt &&
+                             instance_loaded(dk, start + k0 + j, p.tile_lastkey[instance_tile(e, k0 + j, p.gx)]);
                 float rw[4][10];
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    if (sidx[j] != INV_NONE) {
-                        const size_t ri = p.rows_by_u ? (size_t)(start + k0 + j) : (size_t)sidx[j];
-                        load_row(p.rows, ri, rw[j]);
+                    if (use[j]) {
+                        load_row(p.rows, (size_t)(start + k0 + j), rw[j]);
                     } else {
 #pragma unroll
                         for (int k = 0; k < 10; k++) rw[j][k] = 0.f;
@@ -290,7 +293,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
 // are free of bank conflicts.  The coefficients themselves are not read (sh_jac).  A half-wave staging area
 // (6.5 KB, shared with the row-gather chunks) keeps the block at 26 KB of LDS: six blocks, the VGPR limit, per CU.
 #ifndef GSR_PBWD_INV_AHEAD
-#define GSR_PBWD_INV_AHEAD 1  // next chunk's inv words during this chunk's row loads: cfg3 0.104 -> 0.100 ms, cfg5 0.521 -> 0.507
+#define GSR_PBWD_INV_AHEAD 1  // next chunk's loaded tests during this chunk's row loads: cfg3 0.104 -> 0.100 ms, cfg5 0.521 -> 0.507
 #endif
 constexpr int SH_STRIDE = 52;
 constexpr int PBWD_STAGE = 32 * SH_STRIDE;  // floats of LDS per wave
@@ -308,14 +311,14 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
     const size_t gbase = ((size_t)p.g0 + (size_t)blockIdx.x * 256 + (size_t)w * 64) * 48;  // the wave's first float
     const size_t gend = (size_t)p.g1 * 48;
     float *sw = s_sh[w];
-    // Gradient rows of the wave's 64 Gaussians (rows_by_u: each Gaussian's rows are contiguous), gathered
-    // jointly: the (Gaussian, row) pairs of all lanes are enumerated in order, every lane loads the inv words of
+    // Gradient rows of the wave's 64 Gaussians (each Gaussian's rows are contiguous), gathered
+    // jointly: the (Gaussian, row) pairs of all lanes are enumerated in order, every lane tests (instance_loaded)
     // pairs l, l + 64, ... of a chunk, then the rows the composite wrote (others read as zero) into the LDS that later
     // stages dL/dsh, then each lane sums its own Gaussian's rows in row order.  Divergent per-lane
     // loops of dependent loads cost ~40 % of the kernel otherwise.  Gaussians above BIG_GAUSSIAN_TILES rows
     // take their block-reduced sum in preprocess_bwd_one.
     float gs[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    if (p.rows_by_u) {
+    {
         const bool vis = i < p.g1 && p.radii[i] > 0;
         const uint32_t cnt = vis ? p.tiles[i] : 0u;
         const uint32_t len = cnt <= BIG_GAUSSIAN_TILES ? cnt : 0u;
@@ -328,7 +331,10 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         static_assert(CH * 10 + 128 <= PBWD_STAGE, "row chunk + meta fit the staging area");
         s_meta[lane] = make_uint2(pst, len ? p.inst_start[i] : 0u);
         wave_lds_sync();
-        // the inv words of chunk c0 (expansion index uu, written-row marker sidx)
+        // the loaded-instance tests of chunk c0 (expansion index uu, written-row marker sidx): the pair's tile from
+        // its Gaussian's expansion record (the wave's 64 records and depth keys are contiguous: cache hits), then
+        // that tile's last loaded key (instance_loaded)
+        const int gw0 = p.g0 + (int)blockIdx.x * 256 + w * 64;  // the wave's first Gaussian
         auto inv_chunk = [&](uint32_t c0, uint32_t (&uu)[PER], uint32_t (&sidx)[PER]) {
 #pragma unroll
             for (uint32_t r = 0; r < PER; r++) {
@@ -341,8 +347,11 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
                     for (int step = 32; step; step >>= 1)
                         if (s_meta[o + step].x <= j) o += step;
                     const uint2 m = s_meta[o];
-                    uu[r] = m.y + (j - m.x);
-                    sidx[r] = p.inv[uu[r]];
+                    const uint32_t jj = j - m.x;
+                    uu[r] = m.y + jj;
+                    const int go = gw0 + o;
+                    if (instance_loaded(p.depth_key[go], uu[r], p.tile_lastkey[instance_tile(p.exp_rec[go], jj, p.gx)]))
+                        sidx[r] = 0u;
                 }
             }
         };
@@ -356,7 +365,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
             uint32_t uu[PER];
 #if GSR_PBWD_INV_AHEAD
 #pragma unroll
-            for (uint32_t r = 0; r < PER; r++) {  // this chunk's inv words, loaded during the previous chunk
+            for (uint32_t r = 0; r < PER; r++) {  // this chunk's loaded tests, made during the previous chunk
                 uu[r] = uu_n[r];
                 sidx[r] = sidx_n[r];
             }
@@ -390,7 +399,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         }
     }
     float3 dRGB = make_float3(0.f, 0.f, 0.f), dir = make_float3(1.f, 0.f, 0.f);
-    if (i < p.g1) preprocess_bwd_one<true>(p, i, p.rows_by_u != 0, gs, dRGB, dir);
+    if (i < p.g1) preprocess_bwd_one<true>(p, i, true, gs, dRGB, dir);
     if (!p.dL_dsh) return;
 #pragma unroll
     for (int h = 0; h < 2; h++) {

@@ -268,13 +268,16 @@ typedef struct gsr_state_layout {
     size_t geom_tiles, geom_order, geom_inst_off, geom_inst_start, geom_clamped; /* u32, u32, u32, u32, u8 */
     size_t geom_depth_key;    /* u32 float bits of each Gaussian's view depth (0xffffffff: not rendered) */
     size_t geom_expand_rec;   /* uint4 {kept-tile mask lo, hi, rmin.x | rmin.y << 16, rect width} (mask 0 = all) */
-    size_t bin_point_list, bin_inv, bin_keys_sorted;                  /* u32 per instance */
+    size_t bin_point_list, bin_inv, bin_keys_sorted;                  /* u32 per instance (bin_inv: unused, 0) */
     size_t bin_sorted_u, bin_inst_gid;                                /* u32 per instance */
     size_t img_final_T, img_n_contrib, img_ranges, img_tile_last;     /* f32/u32 per pixel, uint2/u32 per tile */
     size_t img_tile_loaded;                                           /* u32 per tile */
     size_t geom_rec_stride;                                           /* bytes per render record (48) */
     size_t img_tile_sorted;   /* u32 per tile: length of the tile's bucket sorted by the forward (prefix binning: a
-                                 prefix when the tile's walk ended before it; else the whole bucket) */
+                                 prefix when the tile's walk ended before it; else the whole bucket); entry [T] is 1
+                                 when the forward ran in prefix mode */
+    size_t bin_bk_keys;       /* u64 per instance: the bucket binning's keys (depth bits << 32 | u) grouped by tile */
+    size_t img_tile_lastkey;  /* u64 per tile: key of the last instance the forward composite loaded (0: none) */
 } gsr_state_layout;
 void gsr_state_layout_query(int P, int64_t R, int W, int H, gsr_state_layout *out);
 

@@ -102,7 +102,6 @@ def hip_state_arrays(out: dict) -> dict:
     res = dict(
         point_list=inst_gid[sorted_u] if R else np.zeros(0, np.uint32),
         point_list_written=view(st.binning_buffer, lay["bin_point_list"], R, i32).astype(np.uint32),
-        inv=view(st.binning_buffer, lay["bin_inv"], R, i32).astype(np.uint32),
         sorted_u=sorted_u.astype(np.uint32),
         tile_loaded=view(st.image_buffer, lay["img_tile_loaded"], T, i32).astype(np.uint32),
         tile_last=view(st.image_buffer, lay["img_tile_last"], T, i32).astype(np.uint32),
@@ -116,6 +115,12 @@ def hip_state_arrays(out: dict) -> dict:
     ts = view(st.image_buffer, lay["img_tile_sorted"], T + 1, i32).astype(np.uint32)
     res["prefix_mode"] = bool(ts[T] == 1)
     res["tile_sorted"] = ts[:T]
+    if res["prefix_mode"]:  # the bucket keys: the rest of each bucket, beyond its sorted prefix
+        bk = view(st.binning_buffer, lay["bin_bk_keys"], R, torch.int64).view(np.uint64)
+        res["bucket_point_list"] = inst_gid[(bk & np.uint64(0xFFFFFFFF)).astype(np.int64)] if R else np.zeros(0, np.uint32)
+    lk = view(st.image_buffer, lay["img_tile_lastkey"], T, torch.int64).view(np.uint64)
+    res["tile_lastkey"] = lk
+    res["depth_bits"] = view(st.geom_buffer, lay["geom_depth_key"], P, i32).astype(np.uint32)
     # render records: one 48-B (12-float) record per Gaussian, a = floats 0..3, b = 4..7, c = 8..9
     stride = lay["geom_rec_stride"] // 4
     rec = view(st.geom_buffer, lay["geom_rec_a"], stride * P, torch.float32).reshape(P, stride)

@@ -63,16 +63,21 @@ def compare_forward(inp, hip, oracle_out):
         assert np.array_equal(hs[k][on].view(np.uint32), g[k][on].view(np.uint32)), k
     kept = g["tiles_touched"] > 0
     assert np.array_equal(hs["depths"][kept].view(np.uint32), g["depths"][kept].view(np.uint32))
-    # The forward gathers every instance any pixel can reach; for exactly those it writes the sorted id
-    # list and the inverse permutation (sorted position of each expansion index); others keep INV_NONE.
+    # The forward gathers every instance any pixel can reach; for exactly those it writes the sorted id list, and per
+    # tile the key (depth bits << 32 | expansion index) of the last one, from which the backward tells loaded
+    # instances (instance_loaded in gsr_common.h)
     loaded = np.zeros(len(pl), bool)
     for t in np.nonzero(hs["tile_loaded"])[0]:
         loaded[rg[t, 0]: rg[t, 0] + hs["tile_loaded"][t]] = True
     assert np.all(hs["tile_loaded"] >= hs["tile_last"])
     assert np.array_equal(hs["point_list_written"][loaded], pl[loaded])
-    s_idx = np.nonzero(loaded)[0]
-    assert np.array_equal(hs["inv"][hs["sorted_u"][s_idx]], s_idx.astype(np.uint32))
-    assert np.sum(hs["inv"] != 0xFFFFFFFF) == loaded.sum()
+    ld = hs["tile_loaded"].astype(np.int64)
+    has = ld > 0
+    s_last = rg[has, 0].astype(np.int64) + ld[has] - 1
+    u_last = hs["sorted_u"][s_last].astype(np.uint64)
+    want = (hs["depth_bits"][pl[s_last]].astype(np.uint64) << np.uint64(32)) | u_last
+    assert np.array_equal(hs["tile_lastkey"][has], want)
+    assert np.all(hs["tile_lastkey"][~has] == 0)
     # pixels
     _, nc = run.image_state()
     flip = run.threshold_margin() < FLIP_MARGIN
@@ -122,7 +127,8 @@ def check_point_list(hs, pl, rg):
     rel = np.arange(len(pl)) - rg[tile_of, 0].astype(np.int64)
     srt = rel < ts[tile_of]
     assert np.array_equal(hp[srt], pl[srt])
-    assert np.array_equal(hp[np.lexsort((hp, tile_of))], pl[np.lexsort((pl, tile_of))])
+    bp = hs["bucket_point_list"]  # each bucket holds exactly the reference's instances of its tile
+    assert np.array_equal(bp[np.lexsort((bp, tile_of))], pl[np.lexsort((pl, tile_of))])
 
 
 def compare_backward(hip, run, dc, di, tol):
