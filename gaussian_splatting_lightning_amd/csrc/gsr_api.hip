@@ -300,15 +300,22 @@ struct InflightReadback {
 // the counters' overflow word, bit 2 of a onesweep error word) only record that a fallback ran.  What remains to
 // check is the instance scan's overflow bit (bit 0), which the debug forward reads back (the readback total already
 // bounds the count, so this is a second line).  Onesweep error words exist only for the sorts that ran onesweep.
-int check_lookback_flags(hipStream_t s, int dev, const uint32_t *counters, const uint32_t *depth_ctrl,
-                         const uint32_t *tile_ctrl) {
-    (void)depth_ctrl;
-    (void)tile_ctrl;
+// Debug mode: the instance scan's overflow flag, and whether a decoupled look-back had to recompute a stalled
+// predecessor (bit 2 of the counters' flag word and of the radix sorts' error words: exact either way, but a sign of
+// a scheduling problem; reported to stderr).  sort_err: the radix sorts' error words that this forward cleared (the
+// depth and the tile sort), or null.
+int check_lookback_flags(hipStream_t s, int dev, const uint32_t *counters, const uint32_t *depth_err,
+                         const uint32_t *tile_err) {
     uint32_t *hw = pinned_words(dev);
     if (!hw) return fail(GSR_ERR_HIP, "pinned host buffer allocation failed");
+    hw[1] = hw[2] = 0u;
     GSR_HIP(hipMemcpyAsync(hw, counters + CNT_OVERFLOW, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if (depth_err) GSR_HIP(hipMemcpyAsync(hw + 1, depth_err, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if (tile_err) GSR_HIP(hipMemcpyAsync(hw + 2, tile_err, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     GSR_HIP(hipStreamSynchronize(s));
     if (hw[0] & 1u) return fail(GSR_ERR_OVERFLOW, "instance scan overflow");
+    if ((hw[0] | hw[1] | hw[2]) & 4u)
+        fprintf(stderr, "gsrast debug: a decoupled look-back recomputed a stalled predecessor\n");
     return GSR_OK;
 }
 
@@ -524,7 +531,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     const bool bucket = bk_possible && (bk == 2 || (uint64_t)R <= (uint64_t)BK_MAX_MEAN * T);
     bool sorted_exp = false;
     bool prefix = false;  // prefix binning: buckets sorted only up to tile_sorted (render_fwd extends them)
-    bool depth_onesweep = false, tile_onesweep = false;  // which sorts own a cleared onesweep error word
+    bool depth_onesweep = false, tile_onesweep = false;  // which sorts ran on the onesweep path (diagnostics)
     if (!bucket) {
         // the depth sort's last pass also writes the tile counts and expansion records in depth order ("sort_gather"
         // bit 0 / bit 1; unset: the scan / the expansion gathers them through the order instead)
@@ -652,9 +659,11 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
         rp.ck_k = k <= 32 ? 32u : (uint32_t)(k / 64) * 64u;
     }
     GSR_STAGE(ST_RENDER_FWD, dbg, launch_render_fwd(stream, rp));
-    if (dbg)  // onesweep error words exist only for the sorts that ran on the onesweep path (launch_radix_sort)
-        return check_lookback_flags(stream, device_guard.dev, g.counters, depth_onesweep ? g.sort.ctrl : nullptr,
-                                    tile_onesweep ? b.sort.ctrl : nullptr);
+    (void)depth_onesweep;
+    (void)tile_onesweep;
+    if (dbg)  // every radix sort clears its error word (onesweep: with its control block; multi-kernel: pass 0)
+        return check_lookback_flags(stream, device_guard.dev, g.counters, bucket ? nullptr : g.sort.ctrl + RS_CTRL_ERR,
+                                    bucket || R == 0 ? nullptr : b.sort.ctrl + RS_CTRL_ERR);
     return GSR_OK;
 }
 

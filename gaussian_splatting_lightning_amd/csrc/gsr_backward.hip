@@ -628,8 +628,10 @@ void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
 __global__ __launch_bounds__(256) void big_reduce_kernel(BigReduceParams p) {
     __shared__ float s_part[4][10];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t bi = blockIdx.x;
-    if (p.nbig_dev && bi >= *p.nbig_dev) return;  // workgroup-uniform: the launch was sized by an upper bound
+    // persistent over the big Gaussians when their count is only known on the device (the launch is then sized by
+    // min(upper bound, 2048) workgroups instead of one per possible big Gaussian)
+    const uint32_t nb = p.nbig_dev ? *p.nbig_dev : gridDim.x;
+    for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {  // workgroup-uniform
     const uint32_t gidx = p.big_list[bi];
     const uint32_t start = p.inst_start[gidx], cnt = p.tiles[gidx];
     float acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -670,11 +672,13 @@ __global__ __launch_bounds__(256) void big_reduce_kernel(BigReduceParams p) {
         for (int v = 0; v < 10; v++) tot[v] = ((s_part[0][v] + s_part[1][v]) + s_part[2][v]) + s_part[3][v];
         store_row(p.bigsum, bi, tot);
     }
+    __syncthreads();  // s_part is rewritten by the next big Gaussian
+    }
 }
 
 void launch_big_reduce(hipStream_t s, const BigReduceParams &p, uint32_t nbig) {
     if (nbig == 0) return;
-    big_reduce_kernel<<<nbig, 256, 0, s>>>(p);
+    big_reduce_kernel<<<p.nbig_dev ? std::min(nbig, 2048u) : nbig, 256, 0, s>>>(p);
 }
 
 }  // namespace gsr

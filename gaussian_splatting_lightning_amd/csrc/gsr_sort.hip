@@ -238,13 +238,14 @@ template <int TILE, typename KT = uint32_t>
 __global__ __launch_bounds__(256) void rs_hist_kernel(const KT *__restrict__ keys, uint32_t n, int shift,
                                                       uint32_t *__restrict__ counts, uint32_t nb,
                                                       uint32_t *__restrict__ cs_status, uint32_t cs_rows,
-                                                      uint32_t *__restrict__ cs_ticket) {
+                                                      uint32_t *__restrict__ cs_ticket, uint32_t *__restrict__ cs_err) {
     __shared__ uint32_t h[4][RS_BINS];
     const int tid = threadIdx.x, w = tid >> 6;
     if (cs_status) {
         for (uint32_t r = blockIdx.x; r < cs_rows; r += gridDim.x) cs_status[(size_t)r * RS_BINS + tid] = 0u;
         if (blockIdx.x == 0 && tid == 0) *cs_ticket = 0u;
     }
+    if (cs_err && blockIdx.x == 0 && tid == 0) *cs_err = 0u;  // pass 0: the sort's look-back diagnostic word
     for (int i = tid; i < 4 * RS_BINS; i += 256) (&h[0][0])[i] = 0;
     __syncthreads();
     const uint32_t base = blockIdx.x * TILE;
@@ -894,7 +895,8 @@ static void launch_radix_sort_multi(hipStream_t s, SortScratch &sc, uint32_t n, 
         const KT *kin = p == 0 ? keys0 : k[in];
         uint32_t *cs_status = one ? sc.status + (size_t)p * nch * RS_BINS : nullptr;
         rs_hist_kernel<ITEMS * 256, KT><<<nb, 256, 0, s>>>(kin, n, shift, sc.counts, nb, cs_status, nch,
-                                                          sc.ctrl + RS_CTRL_COUNTER + p);
+                                                          sc.ctrl + RS_CTRL_COUNTER + p,
+                                                          p == 0 ? sc.ctrl + RS_CTRL_ERR : nullptr);
         const uint32_t *scanned = sc.counts, *doff = nullptr;
         if (one) {
             rs_countscan_kernel<CS_C><<<nch, RS_BINS, 0, s>>>(sc.counts, nb, sc.counts_pre, cs_status,
