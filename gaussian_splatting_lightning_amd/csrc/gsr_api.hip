@@ -603,13 +603,14 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             ep.exp_owner = tuning("exp_owner", 1) ? b.exp_owner : nullptr;
             // 16-bit tile keys up to 65536 tiles ("tile_key16" 0: 32-bit): the tile sort, the expansion's key stores and
             // the range search move 2 bytes per key instead of 4
-            const bool k16 = T <= 65536u && tuning("tile_key16", 1) != 0;
+            const TileSortPlan plan = tile_sort_plan(T);
+            const bool k16 = plan.k16;
             ep.keys_out = k16 ? nullptr : b.sort.k[0];
             ep.keys16_out = k16 ? reinterpret_cast<uint16_t *>(b.sort.k[0]) : nullptr;
             ep.inst_gid = b.inst_gid; ep.inst_start = g.inst_start;
             GSR_STAGE(ST_EXPAND, dbg, launch_expand(stream, ep));
             if (k16)
-                GSR_STAGE(ST_TILE_SORT, dbg, launch_radix_sort16(stream, b.sort, R, tile_key_bits(T)));
+                GSR_STAGE(ST_TILE_SORT, dbg, launch_radix_sort16(stream, b.sort, R, plan.digit_bits, plan.passes));
             else
                 GSR_STAGE(ST_TILE_SORT, dbg,
                           launch_radix_sort(stream, b.sort, R, tile_key_bits(T), false, nullptr, nullptr,

@@ -12,6 +12,8 @@
 
 namespace gsr {
 
+int tuning(const char *name, int default_value);  // gsr_api.hip: runtime knobs (gsr_set_tuning)
+
 constexpr int BLOCK_X = 16;
 constexpr int BLOCK_Y = 16;
 constexpr int TILE_PIX = BLOCK_X * BLOCK_Y;
@@ -159,6 +161,24 @@ inline int tile_key_bits(uint32_t num_tiles) {
 }
 inline int radix_passes(int bits) { return (bits + 7) / 8; }
 
+// The radix binning's tile sort (gsr_api.hip): 16-bit keys up to 65536 tiles ("tile_key16"), sorted in digits of
+// "tile_db" bits (5: three passes over 15-bit tile ids at 4K instead of two of 8 bits -- a pass's stable scatter writes
+// each block's run of each digit, and with 32 digits instead of 256 the runs are 8x longer, so far fewer partial cache
+// lines; else 8 bits).  The carving of the binning buffer (which ping-pong slot ends as sorted_u) follows the same plan.
+struct TileSortPlan {
+    bool k16;
+    int digit_bits, passes;
+};
+inline TileSortPlan tile_sort_plan(uint32_t num_tiles) {
+    TileSortPlan t;
+    const int bits = tile_key_bits(num_tiles);
+    t.k16 = num_tiles <= 65536u && tuning("tile_key16", 1) != 0;
+    t.digit_bits = t.k16 ? tuning("tile_db", 5) : 8;
+    if (t.digit_bits < 4 || t.digit_bits > 8) t.digit_bits = 8;
+    t.passes = (bits + t.digit_bits - 1) / t.digit_bits;
+    return t;
+}
+
 struct BinningState {
     uint32_t *exp_owner;   // div_up(R, 256) + 2: radix path: depth rank owning each expansion block's first instance
     uint32_t *inst_gid;    // R: Gaussian of each instance (expansion order)
@@ -191,7 +211,7 @@ inline size_t carve_binning(char *base, int64_t R, uint32_t num_tiles, BinningSt
     b.point_list = c.take<uint32_t>(n ? n : 1);
     b.sorted_u = c.take<uint32_t>(n ? n : 1);
     Carver cr = c;  // radix view
-    int passes = radix_passes(tile_key_bits(num_tiles));
+    const int passes = tile_sort_plan(num_tiles).passes;
     carve_sort(cr, b.sort, n, passes >= 2);
     b.exp_owner = cr.take<uint32_t>(div_up(n, 256u) + 2);
     // keys and values end in slot (passes & 1); the last pass writes its values straight into sorted_u

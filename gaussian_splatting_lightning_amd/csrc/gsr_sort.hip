@@ -235,7 +235,7 @@ __device__ __forceinline__ void lb_store(uint32_t *p, uint32_t v) {
 // With cs_status, the histogram also clears what the pass's one-launch count scan starts from: its look-back words
 // (one RS_BINS row per chunk, cs_rows rows) and its ticket.
 template <int TILE, typename KT = uint32_t>
-__global__ __launch_bounds__(256) void rs_hist_kernel(const KT *__restrict__ keys, uint32_t n, int shift,
+__global__ __launch_bounds__(256) void rs_hist_kernel(const KT *__restrict__ keys, uint32_t n, int shift, uint32_t dmask,
                                                       uint32_t *__restrict__ counts, uint32_t nb,
                                                       uint32_t *__restrict__ cs_status, uint32_t cs_rows,
                                                       uint32_t *__restrict__ cs_ticket, uint32_t *__restrict__ cs_err) {
@@ -259,20 +259,20 @@ __global__ __launch_bounds__(256) void rs_hist_kernel(const KT *__restrict__ key
                 const uint32_t wds[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    atomicAdd(&h[w][((wds[k] & 0xffffu) >> shift) & 255u], 1u);
-                    atomicAdd(&h[w][((wds[k] >> 16) >> shift) & 255u], 1u);
+                    atomicAdd(&h[w][((wds[k] & 0xffffu) >> shift) & dmask], 1u);
+                    atomicAdd(&h[w][((wds[k] >> 16) >> shift) & dmask], 1u);
                 }
             } else {
-                atomicAdd(&h[w][(q.x >> shift) & 255u], 1u);
-                atomicAdd(&h[w][(q.y >> shift) & 255u], 1u);
-                atomicAdd(&h[w][(q.z >> shift) & 255u], 1u);
-                atomicAdd(&h[w][(q.w >> shift) & 255u], 1u);
+                atomicAdd(&h[w][(q.x >> shift) & dmask], 1u);
+                atomicAdd(&h[w][(q.y >> shift) & dmask], 1u);
+                atomicAdd(&h[w][(q.z >> shift) & dmask], 1u);
+                atomicAdd(&h[w][(q.w >> shift) & dmask], 1u);
             }
         }
     } else {
         for (int i = tid; i < TILE; i += 256) {
             const uint32_t j = base + i;
-            if (j < n) atomicAdd(&h[w][((uint32_t)keys[j] >> shift) & 255u], 1u);
+            if (j < n) atomicAdd(&h[w][((uint32_t)keys[j] >> shift) & dmask], 1u);
         }
     }
     __syncthreads();
@@ -460,7 +460,8 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const KT *__restrict__ 
                                                          int shift, const uint32_t *__restrict__ counts_scanned,
                                                          const uint32_t *__restrict__ digit_off,
                                                          uint32_t nb, KT *__restrict__ keys_out,
-                                                         uint32_t *__restrict__ vals_out, SortGather ga) {
+                                                         uint32_t *__restrict__ vals_out, SortGather ga,
+                                                         uint32_t dmask = 255u) {
     __shared__ uint32_t s_cnt[4][RS_BINS];  // per-wave running digit counts, then per-wave bases
     __shared__ uint32_t s_dstart[RS_BINS];  // block-local start of each digit's run
     __shared__ uint32_t s_gbase[RS_BINS];   // global start of this block's run of each digit
@@ -488,10 +489,11 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const KT *__restrict__ 
         const uint32_t j = blk + w * ((ITEMS * 256) / 4) + it * 64 + lane;
         const bool valid = j < n;
         const uint32_t k = key[it];
-        const uint32_t d = (k >> shift) & 255u;
+        const uint32_t d = (k >> shift) & dmask;
         uint64_t peers = __ballot(valid);
 #pragma unroll
         for (int bit = 0; bit < 8; bit++) {
+            if (!((dmask >> bit) & 1u)) break;  // digits of fewer than 8 bits (uniform)
             const bool set = (d >> bit) & 1u;
             const uint64_t m = __ballot(set);
             peers &= set ? m : ~m;
@@ -527,7 +529,7 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const KT *__restrict__ 
     for (int it = 0; it < ITEMS; it++) {
         const uint32_t j = blk + w * ((ITEMS * 256) / 4) + it * 64 + lane;
         if (j < n) {
-            const uint32_t d = (key[it] >> shift) & 255u;
+            const uint32_t d = (key[it] >> shift) & dmask;
             const uint32_t pos = s_dstart[d] + s_cnt[w][d] + rank[it];
             s_keys[pos] = (KT)key[it];
             s_vals[pos] = val[it];
@@ -545,7 +547,7 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const KT *__restrict__ 
                 gp[it] = 0xffffffffu;
                 if (i < cnt_blk) {
                     const uint32_t k = s_keys[i], v = s_vals[i];
-                    const uint32_t d = (k >> shift) & 255u;
+                    const uint32_t d = (k >> shift) & dmask;
                     gp[it] = s_gbase[d] + (i - s_dstart[d]);
                     keys_out[gp[it]] = (KT)k;
                     vals_out[gp[it]] = v;
@@ -577,7 +579,7 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const KT *__restrict__ 
 #pragma unroll
             for (int q = 0; q < 8; q++) {
                 const uint32_t i = (uint32_t)(i0 + q) * 256 + tid;
-                const uint32_t d = (k[q] >> shift) & 255u;
+                const uint32_t d = (k[q] >> shift) & dmask;
                 g[q] = s_gbase[d] + (i - s_dstart[d]);
             }
 #pragma unroll
@@ -590,7 +592,7 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const KT *__restrict__ 
     }
     for (uint32_t i = tid; i < cnt_blk; i += 256) {
         const uint32_t k = s_keys[i], v = s_vals[i];
-        const uint32_t d = (k >> shift) & 255u;
+        const uint32_t d = (k >> shift) & dmask;
         const uint32_t gpos = s_gbase[d] + (i - s_dstart[d]);
         keys_out[gpos] = (KT)k;
         vals_out[gpos] = v;
@@ -881,7 +883,8 @@ static void launch_radix_sort_onesweep(hipStream_t s, SortScratch &sc, uint32_t 
 // multi-kernel path: per pass a block histogram, a scan of the (digit x block) counts, a stable scatter
 template <int ITEMS, typename KT = uint32_t>
 static void launch_radix_sort_multi(hipStream_t s, SortScratch &sc, uint32_t n, int passes, bool keyed,
-                                    const KT *keys0, const SortGather *gather) {
+                                    const KT *keys0, const SortGather *gather, int dbits = 8) {
+    const uint32_t dmask = (1u << dbits) - 1u;
     KT *k[2] = {reinterpret_cast<KT *>(sc.k[0]), reinterpret_cast<KT *>(sc.k[1])};
     const uint32_t nb = div_up(n, (uint32_t)ITEMS * 256u);  // <= the RS_TILE block count carve_sort sized
     // "rs_cscan" 1 (default): the one-launch count scan (look-back counts < 2^30); 0: the three-launch column scan
@@ -891,10 +894,10 @@ static void launch_radix_sort_multi(hipStream_t s, SortScratch &sc, uint32_t n, 
     const uint32_t pat = (uint32_t)tuning("lb_patience", 1 << 16);
     const int force = tuning("lb_force", 0);
     for (int p = 0; p < passes; p++) {
-        const int shift = 8 * p, in = p & 1, out = (p + 1) & 1;
+        const int shift = dbits * p, in = p & 1, out = (p + 1) & 1;
         const KT *kin = p == 0 ? keys0 : k[in];
         uint32_t *cs_status = one ? sc.status + (size_t)p * nch * RS_BINS : nullptr;
-        rs_hist_kernel<ITEMS * 256, KT><<<nb, 256, 0, s>>>(kin, n, shift, sc.counts, nb, cs_status, nch,
+        rs_hist_kernel<ITEMS * 256, KT><<<nb, 256, 0, s>>>(kin, n, shift, dmask, sc.counts, nb, cs_status, nch,
                                                           sc.ctrl + RS_CTRL_COUNTER + p,
                                                           p == 0 ? sc.ctrl + RS_CTRL_ERR : nullptr);
         const uint32_t *scanned = sc.counts, *doff = nullptr;
@@ -911,10 +914,10 @@ static void launch_radix_sort_multi(hipStream_t s, SortScratch &sc, uint32_t n, 
         if (p == passes - 1 && gather) ga = *gather;
         if (p == 0 && !keyed)
             rs_scatter_kernel<true, ITEMS, KT><<<nb, 256, 0, s>>>(kin, nullptr, n, shift, scanned, doff, nb, k[out],
-                                                                  sc.v[out], ga);
+                                                                  sc.v[out], ga, dmask);
         else
             rs_scatter_kernel<false, ITEMS, KT><<<nb, 256, 0, s>>>(kin, sc.v[in], n, shift, scanned, doff, nb,
-                                                                   k[out], sc.v[out], ga);
+                                                                   k[out], sc.v[out], ga, dmask);
     }
 }
 
@@ -949,14 +952,13 @@ bool launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bo
     return gather != nullptr;
 }
 
-void launch_radix_sort16(hipStream_t s, SortScratch &sc, uint32_t n, int nbits) {
+void launch_radix_sort16(hipStream_t s, SortScratch &sc, uint32_t n, int dbits, int passes) {
     if (n == 0) return;
-    const int passes = radix_passes(nbits);
     const uint16_t *k0 = reinterpret_cast<const uint16_t *>(sc.k[0]);
     int items = tuning("rs_items", 0);
     if (items == 0) items = n <= (8u << 20) ? 16 : 32;
-    if (items >= 32) launch_radix_sort_multi<32, uint16_t>(s, sc, n, passes, false, k0, nullptr);
-    else launch_radix_sort_multi<RS_ITEMS, uint16_t>(s, sc, n, passes, false, k0, nullptr);
+    if (items >= 32) launch_radix_sort_multi<32, uint16_t>(s, sc, n, passes, false, k0, nullptr, dbits);
+    else launch_radix_sort_multi<RS_ITEMS, uint16_t>(s, sc, n, passes, false, k0, nullptr, dbits);
 }
 
 }  // namespace gsr

@@ -736,6 +736,28 @@ def test_binning_paths_are_bitwise_identical(gpu_device, W, H, onesweep, cscan, 
         assert np.array_equal(ref["grads"][k], alt["grads"][k]), k
 
 
+@pytest.mark.parametrize("db", [4, 8])
+def test_tile_sort_digit_width_is_invisible(gpu_device, db):
+    """The radix binning's 16-bit tile sort in digits of 4 or 8 bits (4 or 2 passes at 1280x720's 12-bit tile ids)
+    gives bitwise the instance order of the default 5-bit digits (3 passes)."""
+    from gaussian_splatting_lightning_amd import _native
+    inp = scene_inputs(200_000, 1280, 720, sh_degree=3, seed=6, stress_fraction=0.01)
+    dc, di = upstream(1280, 720, 6)
+    try:
+        _native.set_tuning("bucket", 0)
+        ref = run_hip(inp, gpu_device, dc, di)
+        _native.set_tuning("tile_db", db)
+        alt = run_hip(inp, gpu_device, dc, di)
+    finally:
+        _native.set_tuning("bucket", 1)
+        _native.set_tuning("tile_db", 5)
+    a, b = hip_state_arrays(ref), hip_state_arrays(alt)
+    for k in ("point_list", "ranges", "n_contrib"):
+        assert np.array_equal(a[k], b[k]), k
+    for k in ("color", "invdepth", "radii"):
+        assert np.array_equal(ref[k], alt[k]), k
+
+
 @pytest.mark.parametrize("n,k,dup", [(600_000, 512, False), (600_000, 64, False), (300_000, 512, True)])
 def test_prefix_binning_is_bitwise_the_full_sort(gpu_device, n, k, dup):
     """Prefix binning (whole-tile composite, > 4096 tiles): buckets longer than k get only their k front-most instances
