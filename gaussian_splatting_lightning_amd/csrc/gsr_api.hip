@@ -482,11 +482,15 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
         bp.tiles = g.tiles; bp.inst_start = g.inst_start; bp.block_sums = g.block_sums; bp.depth_key = g.depth_key;
         bp.big_list = g.big_list; bp.exp_rec = g.exp_rec;
         bp.hist = im.bk_hist; bp.hist_pre = im.bk_hist_pre; bp.tile_cnt = im.bk_tile_cnt; bp.tile_start = im.bk_tile_start; bp.ranges = im.ranges;
-        bp.tile_last = im.tile_last; bp.tile_loaded = im.tile_loaded; bp.lpt_bcnt = im.lpt_bcnt;
+        bp.tile_last = im.tile_last; bp.tile_loaded = im.tile_loaded; bp.tile_lastkey = im.tile_lastkey;
+        bp.lpt_bcnt = im.lpt_bcnt;
         bp.ticket = g.counters + CNT_COL_TICKET; bp.tile_status = g.tile_status; bp.err = g.counters + CNT_OVERFLOW;
         bp.long_list = im.bk_long_list; bp.long_cnt = g.counters + CNT_LONG;
         bp.lb_patience = (uint32_t)tuning("lb_patience", 1 << 16); bp.lb_force = tuning("lb_force", 0);
         bp.xcd_major = tuning("bk_xcd", 1);
+        // every buffer the column pass clears must be wired (a null one would fault the GPU, not fail here)
+        if (!bp.tile_last || !bp.tile_loaded || !bp.tile_lastkey || !bp.ranges || !bp.tile_start || !bp.hist_pre)
+            return fail(GSR_ERR_ARG, "internal: bucket binning buffer not set");
         GSR_STAGE(ST_BK_COUNT, dbg, launch_bucket_count(stream, bp));
     }
     // The binning buffer's size depends on the instance total.  Requesting it through the caller's allocator
@@ -659,6 +663,8 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
         const int k = tuning("seg_k", 64);  // cfg 2: 32 / 64 / 128 -> render_bwd 0.106 / 0.107 / 0.129 ms, render_fwd 0.070 / 0.065 / 0.062
         rp.ck_k = k <= 32 ? 32u : (uint32_t)(k / 64) * 64u;
     }
+    if (R > 0 && (!rp.depth_key || !rp.tile_lastkey || !rp.point_list || !rp.inst_gid || !rp.sorted_u))
+        return fail(GSR_ERR_ARG, "internal: composite buffer not set");
     GSR_STAGE(ST_RENDER_FWD, dbg, launch_render_fwd(stream, rp));
     (void)depth_onesweep;
     (void)tile_onesweep;
