@@ -80,12 +80,13 @@ enum Stage {
     ST_BK_COUNT,
     ST_BK_SCATTER,
     ST_SEG_SORT,
+    ST_PRE_COLOR,
     ST_COUNT
 };
 const char *kStageNames[ST_COUNT] = {"preprocess", "depth_sort", "instance_scan", "readback",
                                      "expand",     "tile_sort",  "tile_ranges",   "render_fwd",
                                      "render_bwd", "big_reduce", "preprocess_bwd", "sh_views",
-                                     "bucket_count", "bucket_scatter", "seg_sort"};
+                                     "bucket_count", "bucket_scatter", "seg_sort", "preprocess_color"};
 
 struct Profiler {
     std::mutex mu;
@@ -465,6 +466,10 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     InflightReadback inflight;  // armed before the launch: an error reported after it still waits for the kernel
     inflight.s = stream;
     inflight.armed = rb_spin;
+    // SH colours in a second kernel (preprocess_color_kernel, "pre_split" 1): the projection kernel drops the 192-B
+    // coefficient stream and ~40 registers, and the colour stream runs behind the bucket count pass, while the
+    // host waits for the instance total
+    pp.split = (a->shs && !a->colors_precomp && tuning("pre_split", 1)) ? 1 : 0;
     GSR_STAGE(ST_PREPROCESS, dbg, launch_preprocess(stream, pp));
     if (!rb_spin) {
         GSR_HIP(hipMemcpyAsync(hw, g.counters, CNT_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
@@ -493,6 +498,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             return fail(GSR_ERR_ARG, "internal: bucket binning buffer not set");
         GSR_STAGE(ST_BK_COUNT, dbg, launch_bucket_count(stream, bp));
     }
+    GSR_STAGE(ST_PRE_COLOR, dbg, launch_preprocess_color(stream, pp));
     // The binning buffer's size depends on the instance total.  Requesting it through the caller's allocator
     // (a Python callback from rasterizer.py) after the readback put ~40 us of host work between the preprocess and
     // the next launch, longer than the queued count passes cover; so with a total from an earlier call on this

@@ -24,6 +24,9 @@ struct CullIn {
 
 // Projection, conic, radius, SH colour and render records of one Gaussian.  Returns the area of its tile
 // rect (0: not rendered); the tile culling, tile count and sort key are finished by preprocess_kernel.
+// SPLIT: the colour (SH evaluation, its Jacobian, the clamp bits and the colour words of the record) is left to
+// preprocess_color_kernel, launched behind the bucket count pass.
+template <bool SPLIT>
 __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &p, const int i, CullIn &ci) {
     // uncontracted like the helpers it calls (gsr_common.h): radii, rects and render records bit-equal the oracle's
 #pragma clang fp contract(off)
@@ -84,9 +87,11 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
     const uint32_t area = (uint32_t)((rmax.x - rmin.x) * (rmax.y - rmin.y));
     if (area == 0) return 0u;
 
-    float3 rgb;
+    const float opacity = opacity_in * hscale;
+    float3 rgb = make_float3(0.f, 0.f, 0.f);
     uint8_t clamp_bits = 0;
-    if (p.colors_precomp) {
+    if (SPLIT) {
+    } else if (p.colors_precomp) {
         rgb = load_f3(p.colors_precomp, i);
     } else {
         const float3 campos = make_float3(p.campos[0], p.campos[1], p.campos[2]);
@@ -108,11 +113,15 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
         clamp_bits = (rgb.x < 0.f ? 1 : 0) | (rgb.y < 0.f ? 2 : 0) | (rgb.z < 0.f ? 4 : 0);
         rgb = make_float3(fmaxf(rgb.x, 0.f), fmaxf(rgb.y, 0.f), fmaxf(rgb.z, 0.f));
     }
-    const float opacity = opacity_in * hscale;
     g.rec[i].a = make_float4(pimg.x, pimg.y, conic_x, conic_y);
-    g.rec[i].b = make_float4(conic_z, opacity, rgb.x, rgb.y);
-    g.rec[i].c = make_float2(rgb.z, 1.f / pv.z);
-    g.clamped[i] = clamp_bits;
+    if (SPLIT) {
+        *reinterpret_cast<float2 *>(&g.rec[i].b) = make_float2(conic_z, opacity);
+        g.rec[i].c.y = 1.f / pv.z;
+    } else {
+        g.rec[i].b = make_float4(conic_z, opacity, rgb.x, rgb.y);
+        g.rec[i].c = make_float2(rgb.z, 1.f / pv.z);
+        g.clamped[i] = clamp_bits;
+    }
     p.radii[i] = (int)radius;
     // culling (p.cull): the reference rect shrinks to the tight rect (cull_rect), whose tiles are then tested one by
     // one when there are at most CULL_MAX_AREA of them
@@ -146,7 +155,11 @@ struct PreCullLds {
     unsigned long long mask[64];
     int own[64];    // lane whose rect's pair run starts at this pair of the step, else -1
 };
-__global__ __launch_bounds__(256, GSR_PRE_MINW) void preprocess_kernel(PreprocessParams p) {
+#ifndef GSR_PRE_SPLIT_MINW
+#define GSR_PRE_SPLIT_MINW 7  // split (no colour): 70 VGPRs, 7 waves per SIMD (asking for 8 does not get under 64)
+#endif
+template <bool SPLIT>
+__global__ __launch_bounds__(256, SPLIT ? GSR_PRE_SPLIT_MINW : GSR_PRE_MINW) void preprocess_kernel(PreprocessParams p) {
     __shared__ PreCullLds s_lds[4];
     __shared__ uint32_t s_w[4];
     const uint32_t bid = blockIdx.x;
@@ -155,7 +168,7 @@ __global__ __launch_bounds__(256, GSR_PRE_MINW) void preprocess_kernel(Preproces
     PreCullLds &L = s_lds[w];
     CullIn ci;
     ci.need = false;
-    const uint32_t area = i < p.P ? preprocess_gaussian(p, i, ci) : 0u;
+    const uint32_t area = i < p.P ? preprocess_gaussian<SPLIT>(p, i, ci) : 0u;
     const uint32_t need_area = ci.need ? area : 0u;
     const uint32_t incl = wave_inclusive_scan(need_area, lane);
     const uint32_t total = __shfl((int)incl, 63);
@@ -253,7 +266,56 @@ __global__ __launch_bounds__(256, GSR_PRE_MINW) void preprocess_kernel(Preproces
 
 void launch_preprocess(hipStream_t s, const PreprocessParams &p) {
     if (p.P <= 0) return;
-    preprocess_kernel<<<div_up(p.P, 256), 256, 0, s>>>(p);
+    if (p.split) preprocess_kernel<true><<<div_up(p.P, 256), 256, 0, s>>>(p);
+    else preprocess_kernel<false><<<div_up(p.P, 256), 256, 0, s>>>(p);
+}
+
+// The colour half of a split preprocess: one thread per Gaussian the projection kept (radii != 0, exactly the ones
+// preprocess_gaussian colours), the same expressions as there, so the record, clamp bits and Jacobian are bitwise
+// those of the fused kernel.  A pure stream (192 B of coefficients in, 49 B out) at a fraction of the fused
+// kernel's registers, so it runs at full occupancy; the forward queues it behind the bucket count pass, where
+// the GPU would otherwise wait for the host's readback of the instance total.
+template <int DEG>
+__global__ __launch_bounds__(256) void preprocess_color_kernel(PreprocessParams p) {
+#pragma clang fp contract(off)
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= p.P || p.radii[i] == 0) return;
+    const GeomState &g = p.g;
+    const float3 mean = load_f3(p.means3D, i);
+    const float3 campos = make_float3(p.campos[0], p.campos[1], p.campos[2]);
+    float3 dir = mean - campos;
+    const float len = sqrtf(dot3(dir, dir));
+    dir = make_float3(dir.x / len, dir.y / len, dir.z / len);
+    const float *sh = p.shs + (size_t)i * p.M * 3;
+    float3 rgb;
+    if (DEG > 0) {
+        float3 jx, jy, jz;
+        rgb = sh_eval_jac<DEG>(sh, dir, jx, jy, jz);
+        const size_t n = (size_t)p.P;
+        float *J = g.sh_jac + i;
+        J[0] = jx.x; J[n] = jx.y; J[2 * n] = jx.z;
+        J[3 * n] = jy.x; J[4 * n] = jy.y; J[5 * n] = jy.z;
+        J[6 * n] = jz.x; J[7 * n] = jz.y; J[8 * n] = jz.z;
+    } else {
+        rgb = sh_eval<0>(sh, dir);
+    }
+    rgb = rgb + make_float3(0.5f, 0.5f, 0.5f);
+    const uint8_t clamp_bits = (rgb.x < 0.f ? 1 : 0) | (rgb.y < 0.f ? 2 : 0) | (rgb.z < 0.f ? 4 : 0);
+    rgb = make_float3(fmaxf(rgb.x, 0.f), fmaxf(rgb.y, 0.f), fmaxf(rgb.z, 0.f));
+    *reinterpret_cast<float2 *>(&g.rec[i].b.z) = make_float2(rgb.x, rgb.y);
+    g.rec[i].c.x = rgb.z;
+    g.clamped[i] = clamp_bits;
+}
+
+void launch_preprocess_color(hipStream_t s, const PreprocessParams &p) {
+    if (p.P <= 0 || !p.split) return;
+    const dim3 grid(div_up(p.P, 256)), block(256);
+    switch (p.D) {
+        case 0: preprocess_color_kernel<0><<<grid, block, 0, s>>>(p); break;
+        case 1: preprocess_color_kernel<1><<<grid, block, 0, s>>>(p); break;
+        case 2: preprocess_color_kernel<2><<<grid, block, 0, s>>>(p); break;
+        default: preprocess_color_kernel<3><<<grid, block, 0, s>>>(p); break;
+    }
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -60,8 +60,10 @@ struct PreprocessParams {
     // to host_words[CNT_WORDS .. +4) in one 16-B store (the forward's readback without a copy or an event)
     uint32_t *host_words;
     uint32_t seq;
+    int split = 0;  // colour left to launch_preprocess_color (SH colours only)
 };
 void launch_preprocess(hipStream_t s, const PreprocessParams &p);
+void launch_preprocess_color(hipStream_t s, const PreprocessParams &p);  // the colour half of a split preprocess
 
 struct ExpandParams {
     uint32_t P, R;

@@ -129,6 +129,11 @@ def hip_state_arrays(out: dict) -> dict:
     res["xy"] = np.ascontiguousarray(rec_a[:, :2])
     res["conic_opacity"] = np.ascontiguousarray(np.concatenate([rec_a[:, 2:4], rec_b[:, 0:2]], 1))
     res["depths"] = depth_bits.view(np.float32)
+    # the full record words (a, b, c: position, conic, opacity, colour, inverse depth) and the colour clamp bits of
+    # every rendered Gaussian (the others' words are never written)
+    on = out["radii"] > 0
+    res["rec"] = np.ascontiguousarray(rec[:, :10]).view(np.uint32)[on]
+    res["clamped"] = view(st.geom_buffer, lay["geom_clamped"], P, torch.uint8)[on]
     return res
 
 

@@ -796,6 +796,31 @@ def test_prefix_binning_is_bitwise_the_full_sort(gpu_device, n, k, dup):
         assert np.any((b["tile_sorted"] > 64) & (nt > b["tile_sorted"]))  # walks extended their prefix
 
 
+@pytest.mark.parametrize("deg,bucket", [(3, 1), (2, 1), (1, 0), (0, 1)])
+def test_split_colour_preprocess_is_bitwise_the_fused_one(gpu_device, deg, bucket):
+    """The SH colour evaluated by its own kernel behind the bucket count pass ("pre_split" 1, default) gives bitwise
+    the records, outputs and gradients of the fused preprocess (colour inside the projection kernel)."""
+    from gaussian_splatting_lightning_amd import _native
+    inp = scene_inputs(60_000, 640, 480, sh_degree=deg, seed=12 + deg)
+    dc, di = upstream(640, 480, 12 + deg)
+    try:
+        _native.set_tuning("bucket", bucket)
+        _native.set_tuning("pre_split", 0)
+        ref = run_hip(inp, gpu_device, dc, di)
+        _native.set_tuning("pre_split", 1)
+        alt = run_hip(inp, gpu_device, dc, di)
+    finally:
+        _native.set_tuning("bucket", 1)
+        _native.set_tuning("pre_split", 1)
+    a, b = hip_state_arrays(ref), hip_state_arrays(alt)
+    for key in ("rec", "clamped", "ranges", "point_list", "n_contrib"):
+        assert np.array_equal(a[key], b[key]), key
+    for key in ("color", "invdepth", "radii"):
+        assert np.array_equal(ref[key], alt[key]), key
+    for key in GRADS:
+        assert np.array_equal(ref["grads"][key], alt["grads"][key]), key
+
+
 def test_beyond_lpt_and_bucket_tile_limits(gpu_device):
     """More than 32768 tiles (8K-class image): the radix binning path."""
     inp = scene_inputs(3000, 4160, 2336, sh_degree=1, seed=31)

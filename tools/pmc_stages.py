@@ -18,7 +18,8 @@ import os
 import sys
 
 FIXED = [  # (substring of the kernel name, stage) for kernels that always belong to one stage
-    ("preprocess_kernel", "preprocess"), ("preprocess_bwd_kernel", "preprocess_bwd"),
+    ("preprocess_kernel", "preprocess"), ("preprocess_color_kernel", "preprocess_color"),
+    ("preprocess_bwd_kernel", "preprocess_bwd"),
     ("render_fwd", "render_fwd"), ("render_bwd", "render_bwd"), ("big_reduce", "big_reduce"),
     ("bk_walk_kernel<false", "bucket_count_walk"), ("bk_walk_kernel<true", "bucket_scatter"),
     ("bk_columns", "bucket_columns"), ("seg_sort_kernel", "seg_sort"), ("seg_huge_kernel", "seg_huge"),
