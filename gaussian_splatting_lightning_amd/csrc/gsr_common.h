@@ -812,22 +812,23 @@ __device__ __forceinline__ uint32_t rect_tile(uint32_t c, uint32_t rx, uint32_t 
 
 // Tile of a Gaussian's j-th instance (Gaussian-major expansion index inst_start + j): its expansion record's j-th kept
 // rect cell (the j-th set bit of the kept-tile mask; mask 0 = every cell, the j-th).
-__device__ __forceinline__ uint32_t instance_tile(uint4 e, uint32_t j, uint32_t gx) {
-    uint64_t m = (uint64_t)e.x | ((uint64_t)e.y << 32);
-    uint32_t c = j;
-    if (m) {  // j-th set bit: binary search on popcounts
-        c = 0;
-        uint32_t r = j;
+// Position of the j-th (from 0) set bit of m, j < popcount(m): a branch-free binary search on popcounts.
+__device__ __forceinline__ uint32_t nth_set_bit(uint64_t m, uint32_t j) {
+    uint32_t c = 0, r = j;
 #pragma unroll
-        for (int wd = 32; wd >= 1; wd >>= 1) {
-            const uint32_t cnt = (uint32_t)__popcll(m & ((1ull << wd) - 1ull));
-            if (r >= cnt) {
-                r -= cnt;
-                m >>= wd;
-                c += (uint32_t)wd;
-            }
+    for (int wd = 32; wd >= 1; wd >>= 1) {
+        const uint32_t cnt = (uint32_t)__popcll(m & ((1ull << wd) - 1ull));
+        if (r >= cnt) {
+            r -= cnt;
+            m >>= wd;
+            c += (uint32_t)wd;
         }
     }
+    return c;
+}
+__device__ __forceinline__ uint32_t instance_tile(uint4 e, uint32_t j, uint32_t gx) {
+    const uint64_t m = (uint64_t)e.x | ((uint64_t)e.y << 32);
+    const uint32_t c = m ? nth_set_bit(m, j) : j;  // a culled rect's j-th kept cell
     return rect_tile(c, e.z & 0xffffu, e.z >> 16, e.w, 1.0f / (float)e.w, gx);
 }
 // Whether the forward composite loaded instance u (of a Gaussian with depth bits dk) in its tile: the composite loads a

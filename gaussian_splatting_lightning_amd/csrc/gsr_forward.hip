@@ -402,7 +402,7 @@ __global__ __launch_bounds__(256) void expand_kernel(ExpandParams p) {
     uint32_t gid = s_gid[r];
     uint64_t m = (uint64_t)e.x | ((uint64_t)e.y << 32);
     uint32_t k = ub - s_off[r];
-    for (uint32_t j = 0; j < k && m; j++) m &= m - 1;  // skip the kept tiles of earlier threads
+    if (m && k) m &= ~0ull << nth_set_bit(m, k);  // skip the kept tiles of earlier threads (k < popcount(m))
     float rw = __builtin_amdgcn_rcpf((float)e.w);
     uint32_t key[EXP_PER], gv[EXP_PER];
 #pragma unroll
