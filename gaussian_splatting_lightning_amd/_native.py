@@ -94,7 +94,7 @@ EXPORTED_SYMBOLS = (
     "gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_sh_backward_views", "gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes",
     "gsr_image_buffer_bytes", "gsr_bwd_scratch_bytes", "gsr_set_profiling", "gsr_num_stages", "gsr_stage_name",
     "gsr_stage_times", "gsr_reset_stage_times", "gsr_last_error", "gsr_build_info", "gsr_state_layout_query",
-    "gsr_set_tuning", "gsr_ssim_num_partials", "gsr_ssim_forward", "gsr_ssim_backward", "gsr_adam_step", "gsr_sparse_adam_step",
+    "gsr_set_tuning", "gsr_get_tuning", "gsr_ssim_num_partials", "gsr_ssim_forward", "gsr_ssim_backward", "gsr_adam_step", "gsr_sparse_adam_step",
     "gsr_densify_workspace_bytes", "gsr_densify_classify", "gsr_densify_apply", "gsr_ply_unpack", "gsr_ply_pack",
     "gsr_knn_workspace_bytes", "gsr_knn_mean_dist2", "gsr_debug_wave_stamps",
 )
@@ -176,6 +176,8 @@ def load(path: str | None = None):
     lib.gsr_state_layout_query.restype = None
     lib.gsr_set_tuning.argtypes = [ctypes.c_char_p, ctypes.c_int]
     lib.gsr_set_tuning.restype = None
+    lib.gsr_get_tuning.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    lib.gsr_get_tuning.restype = ctypes.c_int
     lib.gsr_debug_wave_stamps.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
     lib.gsr_debug_wave_stamps.restype = ctypes.c_int
     lib.gsr_last_error.restype = ctypes.c_char_p
@@ -230,6 +232,11 @@ def state_layout(P: int, R: int, W: int, H: int) -> dict:
 def set_tuning(name: str, value: int) -> None:
     """Internal A/B knob (see gsr_set_tuning)."""
     load().gsr_set_tuning(name.encode(), int(value))
+
+
+def get_tuning(name: str, default: int = 0) -> int:
+    """A knob's value, or a forward diagnostic "stat_*" (see gsr_get_tuning)."""
+    return int(load().gsr_get_tuning(name.encode(), int(default)))
 
 
 def wave_stamps(which: int, n: int):

@@ -243,7 +243,8 @@ uint32_t next_readback_seq(int dev) {
 // Once the wait has lasted a millisecond the stream is queried every millisecond, so a failed launch or a kernel
 // fault returns an error instead of spinning forever.  Not sooner: a hipStreamQuery puts a marker on the stream,
 // and the next kernel's dispatch waited ~6 us behind it (a gap before the bucket scatter on every forward).
-int wait_readback(const uint32_t *hw, uint32_t seq, hipStream_t s, uint64_t *total, uint32_t *nbig) {
+int wait_readback(const uint32_t *hw, uint32_t seq, hipStream_t s, uint64_t *total, uint32_t *nbig, uint32_t *kmin,
+                  uint32_t *kmax) {
     const __m128i *src = reinterpret_cast<const __m128i *>(hw + CNT_WORDS);
     auto next_query = std::chrono::steady_clock::now() + std::chrono::milliseconds(1);
     for (uint64_t it = 1;; it++) {
@@ -260,7 +261,23 @@ int wait_readback(const uint32_t *hw, uint32_t seq, hipStream_t s, uint64_t *tot
             if (_mm_movemask_epi8(_mm_cmpeq_epi8(v, v2)) != 0xffff) continue;
             *total = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
             *nbig = w[2];
-            return GSR_OK;
+            // the depth range word, stored just before (the same thread's earlier store; checked anyway)
+            const __m128i *src2 = src + 1;
+            for (uint64_t it2 = 0;; it2++) {
+                asm volatile("" ::: "memory");
+                const __m128i r = _mm_load_si128(src2);
+                alignas(16) uint32_t q[4];
+                _mm_store_si128(reinterpret_cast<__m128i *>(q), r);
+                asm volatile("" ::: "memory");
+                const __m128i r2 = _mm_load_si128(src2);
+                if (q[2] == seq && _mm_movemask_epi8(_mm_cmpeq_epi8(r, r2)) == 0xffff) {
+                    *kmin = q[0];
+                    *kmax = q[1];
+                    return GSR_OK;
+                }
+                if (it2 > (1u << 24)) return fail(GSR_ERR_HIP, "preprocess published its total without its depth range");
+                _mm_pause();
+            }
         }
         if ((it & 255) == 0 && std::chrono::steady_clock::now() >= next_query) {
             const hipError_t e = hipStreamQuery(s);
@@ -514,20 +531,24 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
         if (!bin) return fail(GSR_ERR_ALLOC, "binning buffer allocation failed");
     }
     uint64_t total64 = 0;
-    uint32_t nbig = 0;
+    uint32_t nbig = 0, kmin = 0xffffffffu, kmax = 0;  // the kept depth keys' range (kmin > kmax: none kept)
     if (rb_spin) {
         GSR_STAGE(ST_READBACK, dbg, {
-            const int rc = wait_readback(hw, seq, stream, &total64, &nbig);
+            const int rc = wait_readback(hw, seq, stream, &total64, &nbig, &kmin, &kmax);
             if (rc) return rc;
         });
         inflight.armed = false;
     } else {
         GSR_STAGE(ST_READBACK, dbg, GSR_HIP(hipEventSynchronize(rb_ev)));
+        uint32_t cmax = 0;
         for (int k = 0; k < CNT_NPART; k++) {
             uint64_t part;
             memcpy(&part, hw + CNT_PARTIALS + 2 * k, sizeof(part));
             total64 += part;
+            cmax = std::max(cmax, hw[CNT_DMIN + k]);
+            kmax = std::max(kmax, hw[CNT_DMAX + k]);
         }
+        kmin = ~cmax;
         nbig = hw[CNT_BIG];
     }
     if (total64 > 0xffffffffull) return fail(GSR_ERR_OVERFLOW, "more than 2^32-1 tile instances");
@@ -542,6 +563,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     bool sorted_exp = false;
     bool prefix = false;  // prefix binning: buckets sorted only up to tile_sorted (render_fwd extends them)
     bool depth_onesweep = false, tile_onesweep = false;  // which sorts ran on the onesweep path (diagnostics)
+    if (bucket) gsr_set_tuning("stat_depth_passes", 0);
     if (!bucket) {
         // the depth sort's last pass also writes the tile counts and expansion records in depth order ("sort_gather"
         // bit 0 / bit 1; unset: the scan / the expansion gathers them through the order instead)
@@ -550,9 +572,26 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
         if (sg & 1) { ga.src = g.tiles; ga.dst = g.tiles_sorted; }
         if (sg & 2) { ga.src4 = g.exp_rec; ga.dst4 = g.exp_sorted; }
         bool sorted_recs = false;
-        GSR_STAGE(ST_DEPTH_SORT, dbg,
-                  sorted_recs = launch_radix_sort(stream, g.sort, (uint32_t)P, 32, false, g.depth_key,
-                                                  sg ? &ga : nullptr, &depth_onesweep));
+        // Relative depth keys ("depth_rel" 1) where the sort takes the multi-kernel path: the kept keys span
+        // kmax - kmin, so rs_rel_key maps them onto [0, span] and the culled ones onto span + 1, and the sort runs
+        // ceil(bits / 9) passes instead of 4 (cfg 5: 26 bits, 3 passes of 9 bits)
+        const uint32_t os_max = (uint32_t)tuning("onesweep_max_n", 3 << 20);
+        int rel_bits = 32;
+        if (tuning("depth_rel", 1) && kmin <= kmax && (uint32_t)P > os_max && kmax - kmin < 0xfffffffeu) {
+            const uint32_t cap = kmax - kmin + 1;
+            rel_bits = 32 - __builtin_clz(cap);
+        }
+        gsr_set_tuning("stat_depth_passes", rel_bits <= 27 ? (rel_bits + 8) / 9 : 4);
+        if (rel_bits <= 27) {
+            GSR_STAGE(ST_DEPTH_SORT, dbg,
+                      launch_depth_sort_rel(stream, g.sort, (uint32_t)P, g.depth_key, kmin, kmax - kmin + 1, rel_bits,
+                                            sg ? &ga : nullptr));
+            sorted_recs = sg != 0;
+        } else {
+            GSR_STAGE(ST_DEPTH_SORT, dbg,
+                      sorted_recs = launch_radix_sort(stream, g.sort, (uint32_t)P, 32, false, g.depth_key,
+                                                      sg ? &ga : nullptr, &depth_onesweep));
+        }
         const bool sorted_tiles = sorted_recs && (sg & 1);
         sorted_exp = sorted_recs && (sg & 2);
         if (tuning("scan_lookback", 1))
@@ -1102,6 +1141,8 @@ void gsr_set_tuning(const char *name, int value) {
         }
     g_tune.emplace_back(name, value);
 }
+
+int gsr_get_tuning(const char *name, int default_value) { return name ? tuning(name, default_value) : default_value; }
 
 int gsr_debug_wave_stamps(int which, uint32_t *host_dst, int max_slots) {
     uint4 *b = stamp_buffer(which);

@@ -25,9 +25,10 @@ constexpr int GRAD_ROW = 10;                   // floats per instance gradient r
 
 // counters block at the head of the geometry buffer (zeroed every forward)
 // counters: [CNT_BIG] big-Gaussian count, [CNT_OVERFLOW] scan overflow flag, then CNT_NPART 64-bit partial
-// sums of the instance total (spread over addresses so the per-block atomics do not serialise)
+// sums of the instance total (spread over addresses so the per-block atomics do not serialise), then CNT_NPART
+// partial maxima of the complemented kept depth keys (their minimum) and CNT_NPART of the kept depth keys
 enum Counter : int { CNT_BIG = 0, CNT_OVERFLOW = 2, CNT_SCAN_TICKET = 3, CNT_COL_TICKET = 4, CNT_LONG = 6, CNT_TIES = 8, CNT_PRE_DONE = 10, CNT_PARTIALS = 16, CNT_NPART = 64,
-                     CNT_WORDS = 16 + 2 * 64 };
+                     CNT_DMIN = 16 + 2 * 64, CNT_DMAX = CNT_DMIN + 64, CNT_WORDS = CNT_DMAX + 64 };
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }
 
@@ -49,6 +50,7 @@ constexpr int RS_THREADS = 256;
 constexpr int RS_ITEMS = 16;
 constexpr int RS_TILE = RS_THREADS * RS_ITEMS;  // 4096 keys per block
 constexpr int RS_BINS = 256;
+constexpr int RS_BINS_MAX = 512;  // the relative depth sort's 9-bit digits (count matrix rows)
 constexpr int SCAN_TILE = 4096;
 constexpr int SCAN_MAX_BLOCKS = 1024 * 16;  // single-block scan of block sums
 constexpr uint32_t RS_COL_CHUNK = 32;  // smallest radix count-matrix row chunk per column-scan workgroup (sizes scan_tmp)
@@ -79,8 +81,8 @@ inline void carve_sort(Carver &c, SortScratch &s, uint32_t n, bool need_v0) {
     s.v[0] = need_v0 ? c.take<uint32_t>(n ? n : 1) : nullptr;
     s.v[1] = c.take<uint32_t>(n ? n : 1);
     uint32_t nb = div_up(n ? n : 1, RS_TILE);
-    s.counts = c.take<uint32_t>((size_t)RS_BINS * nb + 1);
-    s.counts_pre = c.take<uint32_t>((size_t)RS_BINS * (nb + 1));
+    s.counts = c.take<uint32_t>((size_t)RS_BINS_MAX * nb + 1);
+    s.counts_pre = c.take<uint32_t>((size_t)RS_BINS_MAX * (nb + 1));
     s.scan_tmp = c.take<uint32_t>(((size_t)div_up(nb, RS_COL_CHUNK) + 1) * RS_BINS);
     const uint32_t nb_os = div_up(n ? n : 1, RS_TILE / 2);  // onesweep tiles may be half a RS_TILE
     s.ctrl = c.take<uint32_t>(RS_CTRL_WORDS + (size_t)RS_MAX_PASSES * nb_os * RS_BINS);

@@ -217,17 +217,30 @@ __global__ __launch_bounds__(256, SPLIT ? GSR_PRE_SPLIT_MINW : GSR_PRE_MINW) voi
         }
     }
     // instance total for the early host readback (gsr_forward): block sum, one 64-bit atomic per block into
-    // one of CNT_NPART partial counters
+    // one of CNT_NPART partial counters; likewise the range of the kept depth keys (the radix path's relative
+    // depth sort), as the largest complemented key and the largest key
+    const uint32_t my_dk = (i < p.P && area > 0 && kept > 0) ? ci.depth : 0xffffffffu;
+    const uint32_t wmin = wave_min_u32(my_dk), wmax = wave_max_u32(my_dk == 0xffffffffu ? 0u : my_dk);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) kept += (uint32_t)__shfl_xor((int)kept, o);
-    if (lane == 0) s_w[w] = kept;
+    __shared__ uint32_t s_dmin[4], s_dmax[4];
+    if (lane == 0) {
+        s_w[w] = kept;
+        s_dmin[w] = wmin;
+        s_dmax[w] = wmax;
+    }
     __syncthreads();
     __shared__ uint32_t s_last;
     if (threadIdx.x == 0) {
         const unsigned long long tot = (unsigned long long)s_w[0] + s_w[1] + s_w[2] + s_w[3];
         unsigned long long old = 0;
-        if (tot)
+        if (tot) {
+            const uint32_t bmin = min(min(s_dmin[0], s_dmin[1]), min(s_dmin[2], s_dmin[3]));
+            const uint32_t bmax = max(max(s_dmax[0], s_dmax[1]), max(s_dmax[2], s_dmax[3]));
+            atomicMax(p.g.counters + CNT_DMIN + (bid % CNT_NPART), ~bmin);
+            atomicMax(p.g.counters + CNT_DMAX + (bid % CNT_NPART), bmax);
             old = atomicAdd(reinterpret_cast<unsigned long long *>(p.g.counters + CNT_PARTIALS) + (bid % CNT_NPART), tot);
+        }
         if (p.block_sums) p.block_sums[bid] = (uint32_t)tot;  // <= 256 * 2^16 tiles
         if (p.host_words) {
             // The workgroup's counter atomics have all returned before its ticket is taken (the big-slot ones before
@@ -248,6 +261,10 @@ __global__ __launch_bounds__(256, SPLIT ? GSR_PRE_SPLIT_MINW : GSR_PRE_MINW) voi
     const unsigned long long part = __hip_atomic_load(
         reinterpret_cast<unsigned long long *>(p.g.counters + CNT_PARTIALS) + threadIdx.x, __ATOMIC_RELAXED,
         __HIP_MEMORY_SCOPE_AGENT);  // CNT_NPART == 64: one partial per lane
+    const uint32_t kmin = ~wave_max_u32(__hip_atomic_load(p.g.counters + CNT_DMIN + threadIdx.x, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT));
+    const uint32_t kmax = wave_max_u32(__hip_atomic_load(p.g.counters + CNT_DMAX + threadIdx.x, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT));
     const unsigned long long lo = (uint32_t)part, hi = part >> 32;
     unsigned long long slo = lo, shi = hi;
 #pragma unroll
@@ -259,6 +276,8 @@ __global__ __launch_bounds__(256, SPLIT ? GSR_PRE_SPLIT_MINW : GSR_PRE_MINW) voi
         const unsigned long long total = slo + (shi << 32);
         const uint32_t nbig = __hip_atomic_load(&p.g.counters[CNT_BIG], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 r = {kmin, kmax, p.seq, 0u};  // the depth range word first (the host reads it second)
+        __builtin_nontemporal_store(r, reinterpret_cast<u32x4 *>(p.host_words + CNT_WORDS + 4));
         const u32x4 v = {(uint32_t)total, (uint32_t)(total >> 32), nbig, p.seq};
         __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p.host_words + CNT_WORDS));
     }

@@ -41,6 +41,9 @@ struct SortGather {
 bool launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bool keyed = false,
                        const uint32_t *keys0 = nullptr, const SortGather *gather = nullptr,
                        bool *onesweep_ran = nullptr);
+// relative-key depth sort (multi-kernel path, up to 9-bit digits): see gsr_sort.hip
+void launch_depth_sort_rel(hipStream_t s, SortScratch &sc, uint32_t n, const uint32_t *keys0, uint32_t kbase,
+                           uint32_t kcap, int bits, const SortGather *gather);
 // The same sort on 16-bit keys in `passes` digits of digit_bits bits (multi-kernel passes): sc.k[] hold uint16_t keys,
 // values as above.  The radix binning's tile sort takes it up to 65536 tiles (tile_sort_plan).
 void launch_radix_sort16(hipStream_t s, SortScratch &sc, uint32_t n, int digit_bits, int passes);

@@ -234,19 +234,27 @@ __device__ __forceinline__ void lb_store(uint32_t *p, uint32_t v) {
 // ------------------------------------------------------------------------------------------------
 // With cs_status, the histogram also clears what the pass's one-launch count scan starts from: its look-back words
 // (one RS_BINS row per chunk, cs_rows rows) and its ticket.
-template <int TILE, typename KT = uint32_t>
+// Relative keys (kcap != 0, 32-bit keys, the depth sort's first pass): the key ranked is min(key - kbase, kcap), an
+// order-preserving map of the kept depth keys onto [0, kcap) with every culled key (all ones) at kcap.
+__device__ __forceinline__ uint32_t rs_rel_key(uint32_t k, uint32_t kbase, uint32_t kcap) {
+    return kcap ? min(k - kbase, kcap) : k;
+}
+
+template <int TILE, typename KT = uint32_t, int BINS = RS_BINS>
 __global__ __launch_bounds__(256) void rs_hist_kernel(const KT *__restrict__ keys, uint32_t n, int shift, uint32_t dmask,
                                                       uint32_t *__restrict__ counts, uint32_t nb,
                                                       uint32_t *__restrict__ cs_status, uint32_t cs_rows,
-                                                      uint32_t *__restrict__ cs_ticket, uint32_t *__restrict__ cs_err) {
-    __shared__ uint32_t h[4][RS_BINS];
+                                                      uint32_t *__restrict__ cs_ticket, uint32_t *__restrict__ cs_err,
+                                                      uint32_t kbase = 0, uint32_t kcap = 0) {
+    __shared__ uint32_t h[4][BINS];
     const int tid = threadIdx.x, w = tid >> 6;
     if (cs_status) {
-        for (uint32_t r = blockIdx.x; r < cs_rows; r += gridDim.x) cs_status[(size_t)r * RS_BINS + tid] = 0u;
+        for (uint32_t r = blockIdx.x; r < cs_rows; r += gridDim.x)
+            for (int d = tid; d < BINS; d += 256) cs_status[(size_t)r * BINS + d] = 0u;
         if (blockIdx.x == 0 && tid == 0) *cs_ticket = 0u;
     }
     if (cs_err && blockIdx.x == 0 && tid == 0) *cs_err = 0u;  // pass 0: the sort's look-back diagnostic word
-    for (int i = tid; i < 4 * RS_BINS; i += 256) (&h[0][0])[i] = 0;
+    for (int i = tid; i < 4 * BINS; i += 256) (&h[0][0])[i] = 0;
     __syncthreads();
     const uint32_t base = blockIdx.x * TILE;
     if (base + TILE <= n) {
@@ -263,20 +271,20 @@ __global__ __launch_bounds__(256) void rs_hist_kernel(const KT *__restrict__ key
                     atomicAdd(&h[w][((wds[k] >> 16) >> shift) & dmask], 1u);
                 }
             } else {
-                atomicAdd(&h[w][(q.x >> shift) & dmask], 1u);
-                atomicAdd(&h[w][(q.y >> shift) & dmask], 1u);
-                atomicAdd(&h[w][(q.z >> shift) & dmask], 1u);
-                atomicAdd(&h[w][(q.w >> shift) & dmask], 1u);
+                atomicAdd(&h[w][(rs_rel_key(q.x, kbase, kcap) >> shift) & dmask], 1u);
+                atomicAdd(&h[w][(rs_rel_key(q.y, kbase, kcap) >> shift) & dmask], 1u);
+                atomicAdd(&h[w][(rs_rel_key(q.z, kbase, kcap) >> shift) & dmask], 1u);
+                atomicAdd(&h[w][(rs_rel_key(q.w, kbase, kcap) >> shift) & dmask], 1u);
             }
         }
     } else {
         for (int i = tid; i < TILE; i += 256) {
             const uint32_t j = base + i;
-            if (j < n) atomicAdd(&h[w][((uint32_t)keys[j] >> shift) & dmask], 1u);
+            if (j < n) atomicAdd(&h[w][(rs_rel_key((uint32_t)keys[j], kbase, kcap) >> shift) & dmask], 1u);
         }
     }
     __syncthreads();
-    counts[(size_t)blockIdx.x * RS_BINS + tid] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+    for (int d = tid; d < BINS; d += 256) counts[(size_t)blockIdx.x * BINS + d] = h[0][d] + h[1][d] + h[2][d] + h[3][d];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -361,13 +369,14 @@ __global__ __launch_bounds__(256) void rs_colbase_kernel(uint32_t *__restrict__ 
 // writes, after `patience` polls).  It writes the rows' exclusive prefixes to counts_pre and the last chunk writes
 // the exclusive digit offsets behind them (row nb), which the scatter adds.  Counts < 2^30 (launch_radix_sort).
 constexpr int CS_LBW = 16;  // predecessors' words loaded per look-back round trip
-template <int C>
-__global__ __launch_bounds__(256) void rs_countscan_kernel(const uint32_t *__restrict__ counts, uint32_t nb,
-                                                           uint32_t *__restrict__ counts_pre,
-                                                           uint32_t *__restrict__ status,
-                                                           uint32_t *__restrict__ ticket, uint32_t *__restrict__ err,
-                                                           uint32_t patience, int force) {
-    __shared__ uint32_t s_bid, s_w[4];
+template <int C, int BINS = RS_BINS>
+__global__ __launch_bounds__(BINS) void rs_countscan_kernel(const uint32_t *__restrict__ counts, uint32_t nb,
+                                                            uint32_t *__restrict__ counts_pre,
+                                                            uint32_t *__restrict__ status,
+                                                            uint32_t *__restrict__ ticket, uint32_t *__restrict__ err,
+                                                            uint32_t patience, int force) {
+    constexpr int RS_BINS = BINS;  // one thread per digit; rows of BINS counts
+    __shared__ uint32_t s_bid, s_w[BINS / 64];
     const int d = threadIdx.x, lane = d & 63, w = d >> 6;
     if (d == 0) s_bid = atomicAdd(ticket, 1u);
     __syncthreads();
@@ -454,24 +463,26 @@ static void launch_count_scan(hipStream_t s, uint32_t *counts, uint32_t nb, uint
 // radix sort pass: stable scatter
 // ------------------------------------------------------------------------------------------------
 // digit_off (or null): exclusive digit offsets added to counts_scanned's column prefixes (rs_countscan_kernel)
-template <bool IOTA_IN, int ITEMS, typename KT = uint32_t>
+template <bool IOTA_IN, int ITEMS, typename KT = uint32_t, int BINS = RS_BINS>
 __global__ __launch_bounds__(256) void rs_scatter_kernel(const KT *__restrict__ keys_in,
                                                          const uint32_t *__restrict__ vals_in, uint32_t n,
                                                          int shift, const uint32_t *__restrict__ counts_scanned,
                                                          const uint32_t *__restrict__ digit_off,
                                                          uint32_t nb, KT *__restrict__ keys_out,
                                                          uint32_t *__restrict__ vals_out, SortGather ga,
-                                                         uint32_t dmask = 255u) {
-    __shared__ uint32_t s_cnt[4][RS_BINS];  // per-wave running digit counts, then per-wave bases
-    __shared__ uint32_t s_dstart[RS_BINS];  // block-local start of each digit's run
-    __shared__ uint32_t s_gbase[RS_BINS];   // global start of this block's run of each digit
+                                                         uint32_t dmask = 255u, uint32_t kbase = 0, uint32_t kcap = 0) {
+    constexpr int DPT = BINS / 256;         // digits per thread in the base computation (consecutive digits)
+    constexpr int DBITS = BINS == 512 ? 9 : 8;
+    __shared__ uint32_t s_cnt[4][BINS];     // per-wave running digit counts, then per-wave bases
+    __shared__ uint32_t s_dstart[BINS];     // block-local start of each digit's run
+    __shared__ uint32_t s_gbase[BINS];      // global start of this block's run of each digit
     __shared__ uint32_t s_wsum[4];
     __shared__ KT s_keys[ITEMS * 256];
     __shared__ uint32_t s_vals[ITEMS * 256];
 
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const uint32_t blk = blockIdx.x * (ITEMS * 256);
-    for (int i = tid; i < 4 * RS_BINS; i += 256) (&s_cnt[0][0])[i] = 0;
+    for (int i = tid; i < 4 * BINS; i += 256) (&s_cnt[0][0])[i] = 0;
     __syncthreads();
 
     // Each wave ranks a contiguous segment of 64 * ITEMS keys, 64 at a time, in input order (stable).
@@ -481,7 +492,7 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const KT *__restrict__ 
     for (int it = 0; it < ITEMS; it++) {  // loads first (see rs_onesweep_kernel)
         const uint32_t j = blk + w * ((ITEMS * 256) / 4) + it * 64 + lane;
         const bool valid = j < n;
-        key[it] = valid ? keys_in[j] : 0u;
+        key[it] = valid ? rs_rel_key((uint32_t)keys_in[j], kbase, kcap) : 0u;
         val[it] = IOTA_IN ? j : (valid ? vals_in[j] : 0u);
     }
 #pragma unroll
@@ -492,8 +503,8 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const KT *__restrict__ 
         const uint32_t d = (k >> shift) & dmask;
         uint64_t peers = __ballot(valid);
 #pragma unroll
-        for (int bit = 0; bit < 8; bit++) {
-            if (!((dmask >> bit) & 1u)) break;  // digits of fewer than 8 bits (uniform)
+        for (int bit = 0; bit < DBITS; bit++) {
+            if (!((dmask >> bit) & 1u)) break;  // digits of fewer bits (uniform)
             const bool set = (d >> bit) & 1u;
             const uint64_t m = __ballot(set);
             peers &= set ? m : ~m;
@@ -509,20 +520,32 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const KT *__restrict__ 
     }
     __syncthreads();
     {
-        const int d = tid;
-        const uint32_t c0 = s_cnt[0][d], c1 = s_cnt[1][d], c2 = s_cnt[2][d], c3 = s_cnt[3][d];
-        s_cnt[0][d] = 0;
-        s_cnt[1][d] = c0;
-        s_cnt[2][d] = c0 + c1;
-        s_cnt[3][d] = c0 + c1 + c2;
-        const uint32_t tot = c0 + c1 + c2 + c3;
-        const uint32_t inc = wave_inclusive_scan(tot, lane);
+        // thread tid owns digits [DPT tid, DPT tid + DPT)
+        uint32_t tot[DPT], sum = 0;
+#pragma unroll
+        for (int q = 0; q < DPT; q++) {
+            const int d = DPT * tid + q;
+            const uint32_t c0 = s_cnt[0][d], c1 = s_cnt[1][d], c2 = s_cnt[2][d], c3 = s_cnt[3][d];
+            s_cnt[0][d] = 0;
+            s_cnt[1][d] = c0;
+            s_cnt[2][d] = c0 + c1;
+            s_cnt[3][d] = c0 + c1 + c2;
+            tot[q] = c0 + c1 + c2 + c3;
+            sum += tot[q];
+        }
+        const uint32_t inc = wave_inclusive_scan(sum, lane);
         if (lane == 63) s_wsum[w] = inc;
         __syncthreads();
         uint32_t woff = 0;
         for (int i = 0; i < w; i++) woff += s_wsum[i];
-        s_dstart[d] = woff + inc - tot;
-        s_gbase[d] = counts_scanned[(size_t)blockIdx.x * RS_BINS + d] + (digit_off ? digit_off[d] : 0u);
+        uint32_t run = woff + inc - sum;
+#pragma unroll
+        for (int q = 0; q < DPT; q++) {
+            const int d = DPT * tid + q;
+            s_dstart[d] = run;
+            run += tot[q];
+            s_gbase[d] = counts_scanned[(size_t)blockIdx.x * BINS + d] + (digit_off ? digit_off[d] : 0u);
+        }
     }
     __syncthreads();
 #pragma unroll
@@ -881,43 +904,48 @@ static void launch_radix_sort_onesweep(hipStream_t s, SortScratch &sc, uint32_t 
 }
 
 // multi-kernel path: per pass a block histogram, a scan of the (digit x block) counts, a stable scatter
-template <int ITEMS, typename KT = uint32_t>
+// BINS = 512: digits of up to 9 bits (the relative depth sort); the count matrix rows are BINS wide, and the
+// one-launch count scan (rs_cscan) is the only scan that takes them.  kcap != 0: pass 0 ranks relative keys
+// (rs_rel_key).  flip: the passes write slot (p + 1 + 1) & 1, so an odd number of passes still ends in slot 0.
+template <int ITEMS, typename KT = uint32_t, int BINS = RS_BINS>
 static void launch_radix_sort_multi(hipStream_t s, SortScratch &sc, uint32_t n, int passes, bool keyed,
-                                    const KT *keys0, const SortGather *gather, int dbits = 8) {
+                                    const KT *keys0, const SortGather *gather, int dbits = 8, uint32_t kbase = 0,
+                                    uint32_t kcap = 0, int flip = 0) {
     const uint32_t dmask = (1u << dbits) - 1u;
     KT *k[2] = {reinterpret_cast<KT *>(sc.k[0]), reinterpret_cast<KT *>(sc.k[1])};
     const uint32_t nb = div_up(n, (uint32_t)ITEMS * 256u);  // <= the RS_TILE block count carve_sort sized
     // "rs_cscan" 1 (default): the one-launch count scan (look-back counts < 2^30); 0: the three-launch column scan
-    const bool one = tuning("rs_cscan", 1) != 0 && n <= RS_ONESWEEP_MAX_N;
+    const bool one = BINS != RS_BINS || (tuning("rs_cscan", 1) != 0 && n <= RS_ONESWEEP_MAX_N);
     constexpr uint32_t CS_C = 32;
     const uint32_t nch = div_up(nb, CS_C);  // <= RS_MAX_PASSES * nb_os rows of sc.status per pass
     const uint32_t pat = (uint32_t)tuning("lb_patience", 1 << 16);
     const int force = tuning("lb_force", 0);
     for (int p = 0; p < passes; p++) {
-        const int shift = dbits * p, in = p & 1, out = (p + 1) & 1;
+        const int shift = dbits * p, in = (p + flip) & 1, out = (p + 1 + flip) & 1;
         const KT *kin = p == 0 ? keys0 : k[in];
-        uint32_t *cs_status = one ? sc.status + (size_t)p * nch * RS_BINS : nullptr;
-        rs_hist_kernel<ITEMS * 256, KT><<<nb, 256, 0, s>>>(kin, n, shift, dmask, sc.counts, nb, cs_status, nch,
-                                                          sc.ctrl + RS_CTRL_COUNTER + p,
-                                                          p == 0 ? sc.ctrl + RS_CTRL_ERR : nullptr);
+        const uint32_t cap = p == 0 ? kcap : 0u;
+        uint32_t *cs_status = one ? sc.status + (size_t)p * nch * BINS : nullptr;
+        rs_hist_kernel<ITEMS * 256, KT, BINS><<<nb, 256, 0, s>>>(kin, n, shift, dmask, sc.counts, nb, cs_status, nch,
+                                                                sc.ctrl + RS_CTRL_COUNTER + p,
+                                                                p == 0 ? sc.ctrl + RS_CTRL_ERR : nullptr, kbase, cap);
         const uint32_t *scanned = sc.counts, *doff = nullptr;
         if (one) {
-            rs_countscan_kernel<CS_C><<<nch, RS_BINS, 0, s>>>(sc.counts, nb, sc.counts_pre, cs_status,
-                                                             sc.ctrl + RS_CTRL_COUNTER + p, sc.ctrl + RS_CTRL_ERR,
-                                                             pat, force);
+            rs_countscan_kernel<CS_C, BINS><<<nch, BINS, 0, s>>>(sc.counts, nb, sc.counts_pre, cs_status,
+                                                                sc.ctrl + RS_CTRL_COUNTER + p, sc.ctrl + RS_CTRL_ERR,
+                                                                pat, force);
             scanned = sc.counts_pre;
-            doff = sc.counts_pre + (size_t)nb * RS_BINS;
+            doff = sc.counts_pre + (size_t)nb * BINS;
         } else {
             launch_count_scan(s, sc.counts, nb, sc.scan_tmp);
         }
         SortGather ga;
         if (p == passes - 1 && gather) ga = *gather;
         if (p == 0 && !keyed)
-            rs_scatter_kernel<true, ITEMS, KT><<<nb, 256, 0, s>>>(kin, nullptr, n, shift, scanned, doff, nb, k[out],
-                                                                  sc.v[out], ga, dmask);
+            rs_scatter_kernel<true, ITEMS, KT, BINS><<<nb, 256, 0, s>>>(kin, nullptr, n, shift, scanned, doff, nb,
+                                                                        k[out], sc.v[out], ga, dmask, kbase, cap);
         else
-            rs_scatter_kernel<false, ITEMS, KT><<<nb, 256, 0, s>>>(kin, sc.v[in], n, shift, scanned, doff, nb,
-                                                                   k[out], sc.v[out], ga, dmask);
+            rs_scatter_kernel<false, ITEMS, KT, BINS><<<nb, 256, 0, s>>>(kin, sc.v[in], n, shift, scanned, doff, nb,
+                                                                         k[out], sc.v[out], ga, dmask, kbase, cap);
     }
 }
 
@@ -950,6 +978,27 @@ bool launch_radix_sort(hipStream_t s, SortScratch &sc, uint32_t n, int nbits, bo
     if (items >= 32) launch_radix_sort_multi<32>(s, sc, n, passes, keyed, keys0, gather);
     else launch_radix_sort_multi<RS_ITEMS>(s, sc, n, passes, keyed, keys0, gather);
     return gather != nullptr;
+}
+
+// The depth sort on relative keys (the multi-kernel path's sizes): the P depth keys mapped onto [0, kcap] by
+// rs_rel_key (kcap = the kept keys' span + 1, the culled keys' slot), bits = bits of kcap, in ceil(bits / 9) passes
+// of at most 9 bits -- 3 instead of 4 for spans up to 2^27 (depth ranges up to ~16x).  Same order as the 32-bit sort
+// (stable, order-preserving map), values end in slot 0 (g.order) for any number of passes.
+void launch_depth_sort_rel(hipStream_t s, SortScratch &sc, uint32_t n, const uint32_t *keys0, uint32_t kbase,
+                           uint32_t kcap, int bits, const SortGather *gather) {
+    if (n == 0) return;
+    const int passes = (bits + 8) / 9;
+    const int dbits = (bits + passes - 1) / passes;
+    const int flip = passes & 1;
+    int items = tuning("rs_items", 0);
+    if (items == 0) items = n <= (8u << 20) ? 16 : 32;
+    if (dbits > 8) {
+        if (items >= 32) launch_radix_sort_multi<32, uint32_t, 512>(s, sc, n, passes, false, keys0, gather, dbits, kbase, kcap, flip);
+        else launch_radix_sort_multi<RS_ITEMS, uint32_t, 512>(s, sc, n, passes, false, keys0, gather, dbits, kbase, kcap, flip);
+    } else {
+        if (items >= 32) launch_radix_sort_multi<32>(s, sc, n, passes, false, keys0, gather, dbits, kbase, kcap, flip);
+        else launch_radix_sort_multi<RS_ITEMS>(s, sc, n, passes, false, keys0, gather, dbits, kbase, kcap, flip);
+    }
 }
 
 void launch_radix_sort16(hipStream_t s, SortScratch &sc, uint32_t n, int dbits, int passes) {

@@ -292,6 +292,9 @@ void gsr_reset_stage_times(void);
 
 /* Internal tuning knobs for A/B measurements (e.g. "bwd_occ4"); unknown names are ignored by kernels. */
 void gsr_set_tuning(const char *name, int value);
+/* A knob's value (default_value if never set).  The forward also records diagnostics here under "stat_*" names
+ * (e.g. "stat_depth_passes": the radix passes of the last depth sort, 0 on the bucket path). */
+int gsr_get_tuning(const char *name, int default_value);
 
 /* Diagnostics: with the "stamp" knob set, the composite kernels record one (start, end, HW_ID, XCC_ID)
  * uint32 quadruple per launch slot (start/end on the 100 MHz real-time clock).  which = 0: render_fwd,

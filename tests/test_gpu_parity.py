@@ -821,6 +821,39 @@ def test_split_colour_preprocess_is_bitwise_the_fused_one(gpu_device, deg, bucke
         assert np.array_equal(ref["grads"][key], alt["grads"][key]), key
 
 
+@pytest.mark.parametrize("n,depth_scale", [(150_000, 1.0), (150_000, 40.0), (2_000, 1.0)])
+def test_relative_depth_sort_is_bitwise_the_32bit_one(gpu_device, n, depth_scale):
+    """The radix path's depth sort on relative keys (kept keys minus their minimum, culled ones after them; 9-bit
+    digits, 3 passes for this scene's ~26-bit span) gives bitwise the order, outputs and gradients of the 4-pass
+    32-bit sort.  depth_scale 40 stretches the scene along the view axis (a wider key span), n = 2000 a small one;
+    onesweep_max_n = 0 sends every depth sort to the multi-kernel path, where relative keys apply."""
+    from gaussian_splatting_lightning_amd import _native
+    inp = scene_inputs(n, 960, 540, sh_degree=1, seed=21)
+    if depth_scale != 1.0:
+        inp["means3D"] = inp["means3D"] * np.array([1.0, 1.0, depth_scale], np.float32)
+    dc, di = upstream(960, 540, 21)
+    try:
+        _native.set_tuning("bucket", 0)
+        _native.set_tuning("onesweep_max_n", 0)
+        _native.set_tuning("depth_rel", 0)
+        ref = run_hip(inp, gpu_device, dc, di)
+        assert _native.get_tuning("stat_depth_passes") == 4
+        _native.set_tuning("depth_rel", 1)
+        alt = run_hip(inp, gpu_device, dc, di)
+        assert 1 <= _native.get_tuning("stat_depth_passes") <= 3  # the relative sort ran
+    finally:
+        _native.set_tuning("bucket", 1)
+        _native.set_tuning("onesweep_max_n", 3 << 20)
+        _native.set_tuning("depth_rel", 1)
+    a, b = hip_state_arrays(ref), hip_state_arrays(alt)
+    for key in ("point_list", "ranges", "n_contrib", "tiles"):
+        assert np.array_equal(a[key], b[key]), key
+    for key in ("color", "invdepth", "radii"):
+        assert np.array_equal(ref[key], alt[key]), key
+    for key in GRADS:
+        assert np.array_equal(ref["grads"][key], alt["grads"][key]), key
+
+
 def test_beyond_lpt_and_bucket_tile_limits(gpu_device):
     """More than 32768 tiles (8K-class image): the radix binning path."""
     inp = scene_inputs(3000, 4160, 2336, sh_degree=1, seed=31)
