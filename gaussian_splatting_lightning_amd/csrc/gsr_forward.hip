@@ -109,7 +109,7 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
         } else {
             rgb = sh_dispatch(p.D, p.shs + (size_t)i * p.M * 3, dir);
         }
-        rgb = rgb + make_float3(0.5f, 0.5f, 0.5f);
+        rgb = sh_offset(rgb);
         clamp_bits = (rgb.x < 0.f ? 1 : 0) | (rgb.y < 0.f ? 2 : 0) | (rgb.z < 0.f ? 4 : 0);
         rgb = make_float3(fmaxf(rgb.x, 0.f), fmaxf(rgb.y, 0.f), fmaxf(rgb.z, 0.f));
     }
@@ -318,7 +318,7 @@ __global__ __launch_bounds__(256) void preprocess_color_kernel(PreprocessParams 
     } else {
         rgb = sh_eval<0>(sh, dir);
     }
-    rgb = rgb + make_float3(0.5f, 0.5f, 0.5f);
+    rgb = sh_offset(rgb);
     const uint8_t clamp_bits = (rgb.x < 0.f ? 1 : 0) | (rgb.y < 0.f ? 2 : 0) | (rgb.z < 0.f ? 4 : 0);
     rgb = make_float3(fmaxf(rgb.x, 0.f), fmaxf(rgb.y, 0.f), fmaxf(rgb.z, 0.f));
     *reinterpret_cast<float2 *>(&g.rec[i].b.z) = make_float2(rgb.x, rgb.y);

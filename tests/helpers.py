@@ -99,8 +99,13 @@ def hip_state_arrays(out: dict) -> dict:
     i32 = torch.int32
     sorted_u = view(st.binning_buffer, lay["bin_sorted_u"], R, i32).astype(np.int64)
     inst_gid = view(st.binning_buffer, lay["bin_inst_gid"], R, i32).astype(np.uint32)
+    # in prefix binning mode sorted_u is written only over each tile's sorted prefix; the positions beyond it hold
+    # whatever the buffer held before (check_point_list compares the prefixes only), so index defensively
+    ok = (sorted_u >= 0) & (sorted_u < R)
+    point_list = np.full(R, 0xFFFFFFFF, np.uint32)
+    point_list[ok] = inst_gid[sorted_u[ok]]
     res = dict(
-        point_list=inst_gid[sorted_u] if R else np.zeros(0, np.uint32),
+        point_list=point_list,
         point_list_written=view(st.binning_buffer, lay["bin_point_list"], R, i32).astype(np.uint32),
         sorted_u=sorted_u.astype(np.uint32),
         tile_loaded=view(st.image_buffer, lay["img_tile_loaded"], T, i32).astype(np.uint32),
