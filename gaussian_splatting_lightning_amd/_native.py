@@ -6,6 +6,7 @@ raises, so a GPU run can never silently pass on another implementation.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
@@ -176,8 +177,9 @@ def load(path: str | None = None):
     lib.gsr_state_layout_query.restype = None
     lib.gsr_set_tuning.argtypes = [ctypes.c_char_p, ctypes.c_int]
     lib.gsr_set_tuning.restype = None
-    lib.gsr_get_tuning.argtypes = [ctypes.c_char_p, ctypes.c_int]
-    lib.gsr_get_tuning.restype = ctypes.c_int
+    if hasattr(lib, "gsr_get_tuning"):  # absent from pre-round-4 builds loaded for A/Bs through GSR_LIB
+        lib.gsr_get_tuning.argtypes = [ctypes.c_char_p, ctypes.c_int]
+        lib.gsr_get_tuning.restype = ctypes.c_int
     lib.gsr_debug_wave_stamps.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
     lib.gsr_debug_wave_stamps.restype = ctypes.c_int
     lib.gsr_last_error.restype = ctypes.c_char_p
@@ -232,6 +234,32 @@ def state_layout(P: int, R: int, W: int, H: int) -> dict:
 def set_tuning(name: str, value: int) -> None:
     """Internal A/B knob (see gsr_set_tuning)."""
     load().gsr_set_tuning(name.encode(), int(value))
+
+
+TUNING_UNSET = -2 ** 31  # gsr_set_tuning(name, GSR_TUNING_UNSET): the knob's built-in default applies again
+
+
+def unset_tuning(name: str) -> None:
+    load().gsr_set_tuning(name.encode(), TUNING_UNSET)
+
+
+@contextlib.contextmanager
+def tuned(**knobs):
+    """Set knobs for the body, then restore each one (its earlier value, or its built-in default if it was unset)."""
+    before = {}
+    for k in knobs:
+        a, b = get_tuning(k, TUNING_UNSET), get_tuning(k, TUNING_UNSET + 1)
+        before[k] = None if (a == TUNING_UNSET and b == TUNING_UNSET + 1) else a
+    try:
+        for k, v in knobs.items():
+            set_tuning(k, v)
+        yield
+    finally:
+        for k, v in before.items():
+            if v is None:
+                unset_tuning(k)
+            else:
+                set_tuning(k, v)
 
 
 def get_tuning(name: str, default: int = 0) -> int:

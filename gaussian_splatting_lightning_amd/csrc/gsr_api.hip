@@ -401,7 +401,7 @@ void gsr_state_layout_query(int P, int64_t R, int W, int H, gsr_state_layout *ou
     out->geom_expand_rec = off(g.exp_rec);
     out->geom_depth_key = off(g.depth_key);
     out->bin_point_list = off(b.point_list);
-    out->bin_inv = 0;  // no inverse permutation any more (ImageState::tile_lastkey, instance_loaded)
+    out->bin_inv = off(b.inv);
     out->bin_keys_sorted = off(b.keys_sorted);
     out->bin_sorted_u = off(b.sorted_u);
     out->bin_inst_gid = off(b.inst_gid);
@@ -485,8 +485,13 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     inflight.armed = rb_spin;
     // SH colours in a second kernel (preprocess_color_kernel, "pre_split" 1): the projection kernel drops the 192-B
     // coefficient stream and ~40 registers, and the colour stream runs behind the bucket count pass, while the
-    // host waits for the instance total
-    pp.split = (a->shs && !a->colors_precomp && tuning("pre_split", 1)) ? 1 : 0;
+    // host waits for the instance total.  Measured slower (cfg 3: preprocess 0.101 ms fused against 0.073 + 0.071 split,
+    // the host's wait is too short to hide the colour kernel; cfg 5: 0.32 + 0.35 ms), so the fused kernel is the default.
+    pp.split = (a->shs && !a->colors_precomp && tuning("pre_split", 0)) ? 1 : 0;
+    // the kept depth keys' range, for the radix path's relative depth sort: only where that sort can run (multi-kernel
+    // depth sorts, P above the onesweep limit); else the range words stay empty and the sort takes its 32-bit keys
+    const uint32_t os_max = (uint32_t)tuning("onesweep_max_n", 3 << 20);
+    pp.depth_range = (tuning("depth_rel", 1) && (uint32_t)P > os_max) ? 1 : 0;
     GSR_STAGE(ST_PREPROCESS, dbg, launch_preprocess(stream, pp));
     if (!rb_spin) {
         GSR_HIP(hipMemcpyAsync(hw, g.counters, CNT_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
@@ -575,7 +580,6 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
         // Relative depth keys ("depth_rel" 1) where the sort takes the multi-kernel path: the kept keys span
         // kmax - kmin, so rs_rel_key maps them onto [0, span] and the culled ones onto span + 1, and the sort runs
         // ceil(bits / 9) passes instead of 4 (cfg 5: 26 bits, 3 passes of 9 bits)
-        const uint32_t os_max = (uint32_t)tuning("onesweep_max_n", 3 << 20);
         int rel_bits = 32;
         if (tuning("depth_rel", 1) && kmin <= kmax && (uint32_t)P > os_max && kmax - kmin < 0xfffffffeu) {
             const uint32_t cap = kmax - kmin + 1;
@@ -616,7 +620,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
         return fail(GSR_ERR_OVERFLOW, "too many tile instances for the single-level scan");
     if (bucket) {
         if (R > 0) {
-            bp.keys = b.bk_keys; bp.inst_gid = b.inst_gid;
+            bp.keys = b.bk_keys; bp.inst_gid = b.inst_gid; bp.inv = b.inv;
             bp.order = lpt ? im.order_fwd : nullptr;
             bp.lpt_shift = tuning("lpt_shift", 3);
             GSR_STAGE(ST_BK_SCATTER, dbg, launch_bucket_scatter(stream, bp));  // and the forward LPT order
@@ -630,7 +634,10 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             // prefix binning ("bk_prefix" instances, a multiple of 64 <= 512; 0: sort every bucket whole) where the
             // composite runs whole tiles: tiles longer than that get only their front-most instances sorted, and a
             // walk that outlives them selects its further batches itself (render_fwd)
-            const int pk = tuning("bk_prefix", 512);
+            // Measured at cfg 3 (profiles/r4d_ab_prefix_cfg3.txt): seg_sort 0.053 -> 0.060 ms and render_fwd 0.171 ->
+            // 0.176 ms with 512-instance prefixes (the radix select's passes over a long bucket cost more than the
+            // bitonic sort they spare), so whole sorts are the default.
+            const int pk = tuning("bk_prefix", 0);
             if (pk > 0 && render_fwd_parts((int)T) == 1) {
                 sp.prefix_k = (uint32_t)std::min(512, std::max(64, pk / 64 * 64));
                 sp.tile_sorted = im.tile_sorted;
@@ -656,7 +663,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             const bool k16 = plan.k16;
             ep.keys_out = k16 ? nullptr : b.sort.k[0];
             ep.keys16_out = k16 ? reinterpret_cast<uint16_t *>(b.sort.k[0]) : nullptr;
-            ep.inst_gid = b.inst_gid; ep.inst_start = g.inst_start;
+            ep.inst_gid = b.inst_gid; ep.inst_start = g.inst_start; ep.inv_none = b.inv;
             GSR_STAGE(ST_EXPAND, dbg, launch_expand(stream, ep));
             if (k16)
                 GSR_STAGE(ST_TILE_SORT, dbg, launch_radix_sort16(stream, b.sort, R, plan.digit_bits, plan.passes));
@@ -686,6 +693,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     rp.ranges = im.ranges; rp.sorted_u = b.sorted_u; rp.inst_gid = b.inst_gid;
     rp.point_list = b.point_list; rp.tile_loaded = im.tile_loaded;
     rp.depth_key = g.depth_key; rp.tile_lastkey = im.tile_lastkey;
+    rp.inv = b.inv;
     rp.rec = g.rec;
     rp.bg = a->background;
     rp.out_color = a->out_color; rp.out_invdepth = a->out_invdepth; rp.final_T = im.final_T;
@@ -794,7 +802,7 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
         GSR_STAGE(ST_RENDER_BWD, dbg, launch_render_bwd(stream, rp));
         BigReduceParams bp;
         bp.big_list = g.big_list; bp.inst_start = g.inst_start; bp.tiles = g.tiles;
-        bp.exp_rec = g.exp_rec; bp.depth_key = g.depth_key; bp.tile_lastkey = im.tile_lastkey; bp.gx = (uint32_t)gx;
+        bp.inv = b.inv;
         bp.rows = rows; bp.bigsum = bigsum;
         bp.nbig_dev = nbig_on_device ? g.counters + CNT_BIG : nullptr;
         GSR_STAGE(ST_BIG_REDUCE, dbg, launch_big_reduce(stream, bp, nbig));
@@ -819,7 +827,7 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     pp.cov3D_precomp = a->cov3D_precomp; pp.shs = (a->colors_precomp ? nullptr : a->shs);
     pp.view = a->viewmatrix; pp.proj = a->projmatrix; pp.campos = a->campos;
     pp.radii = a->radii; pp.tiles = g.tiles; pp.inst_start = g.inst_start; pp.clamped = g.clamped;
-    pp.exp_rec = g.exp_rec; pp.depth_key = g.depth_key; pp.tile_lastkey = im.tile_lastkey; pp.gx = (uint32_t)gx;
+    pp.inv = b.inv;
     pp.sh_jac = g.sh_jac;  // the forward's d rgb / d dir: the SH term of dL/dmeans3D reads no coefficient
     pp.big_slot = g.big_slot; pp.bigsum = bigsum;
     pp.rows = rows;
@@ -1134,12 +1142,13 @@ int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const
 void gsr_set_tuning(const char *name, int value) {
     if (!name) return;
     std::lock_guard<std::mutex> lk(g_tune_mu);
-    for (auto &kv : g_tune)
-        if (kv.first == name) {
-            kv.second = value;
+    for (size_t k = 0; k < g_tune.size(); k++)
+        if (g_tune[k].first == name) {
+            if (value == GSR_TUNING_UNSET) g_tune.erase(g_tune.begin() + (long)k);  // back to the built-in default
+            else g_tune[k].second = value;
             return;
         }
-    g_tune.emplace_back(name, value);
+    if (value != GSR_TUNING_UNSET) g_tune.emplace_back(name, value);
 }
 
 int gsr_get_tuning(const char *name, int default_value) { return name ? tuning(name, default_value) : default_value; }

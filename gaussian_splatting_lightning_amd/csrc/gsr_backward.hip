@@ -625,60 +625,62 @@ void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
 // Gaussians with many instances: one block sums all their rows (fixed stride order, deterministic)
 // into bigsum[slot], which the preprocess backward then reads instead of walking the rows.
 // ------------------------------------------------------------------------------------------------
+template <bool PERSIST>
 __global__ __launch_bounds__(256) void big_reduce_kernel(BigReduceParams p) {
     __shared__ float s_part[4][10];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    // persistent over the big Gaussians when their count is only known on the device (the launch is then sized by
-    // min(upper bound, 2048) workgroups instead of one per possible big Gaussian)
-    const uint32_t nb = p.nbig_dev ? *p.nbig_dev : gridDim.x;
+    // PERSIST: the big-Gaussian count is only known on the device, so the launch is sized by min(upper bound, 2048)
+    // workgroups that loop to it, instead of one per possible big Gaussian; else one workgroup per big Gaussian (no loop:
+    // the loop's live state took the kernel from 64 to 80 VGPRs, 8 to 6 waves, cfg 5 0.078 -> 0.12 ms)
+    const uint32_t nb = PERSIST ? *p.nbig_dev : gridDim.x;
     for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {  // workgroup-uniform
-    const uint32_t gidx = p.big_list[bi];
-    const uint32_t start = p.inst_start[gidx], cnt = p.tiles[gidx];
-    float acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    // rows by expansion index (every cell of a big Gaussian's rect is an instance): BR_UNROLL loaded-instance tests
-    // per thread (the tile of row k and its last loaded key, instance_loaded) go first, then the rows of the loaded
-    // instances (most instances of a big Gaussian sit in saturated tiles and have none), summed in the same k order as
-    // one at a time
-    const uint4 e = p.exp_rec[gidx];
-    const uint32_t dk = p.depth_key[gidx];
-    constexpr int BR_UNROLL = 4;
-    for (uint32_t k0 = threadIdx.x; k0 < cnt; k0 += 256 * BR_UNROLL) {
-        float r[BR_UNROLL][10];
-        bool use[BR_UNROLL];
+        const uint32_t gidx = p.big_list[bi];
+        const uint32_t start = p.inst_start[gidx], cnt = p.tiles[gidx];
+        float acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        // rows by expansion index (every cell of a big Gaussian's rect is an instance): BR_UNROLL inv words per thread
+        // (INV_NONE: the forward composite did not load the instance, no row) are loaded together, then the rows of
+        // the loaded instances (most instances of a big Gaussian sit in saturated tiles and have none), summed in the
+        // same k order as one at a time
+        constexpr int BR_UNROLL = 4;
+        for (uint32_t k0 = threadIdx.x; k0 < cnt; k0 += 256 * BR_UNROLL) {
+            float r[BR_UNROLL][10];
+            bool use[BR_UNROLL];
 #pragma unroll
-        for (int q = 0; q < BR_UNROLL; q++) {
-            const uint32_t k = k0 + 256 * q;
-            use[q] = k < cnt && instance_loaded(dk, start + k, p.tile_lastkey[instance_tile(e, k, p.gx)]);
+            for (int q = 0; q < BR_UNROLL; q++) {
+                const uint32_t k = k0 + 256 * q;
+                use[q] = k < cnt && p.inv[start + k] != INV_NONE;
+            }
+#pragma unroll
+            for (int q = 0; q < BR_UNROLL; q++)
+                if (use[q]) load_row(p.rows, start + k0 + 256 * q, r[q]);
+#pragma unroll
+            for (int q = 0; q < BR_UNROLL; q++)
+                if (use[q]) {
+#pragma unroll
+                    for (int v = 0; v < 10; v++) acc[v] += r[q][v];
+                }
         }
 #pragma unroll
-        for (int q = 0; q < BR_UNROLL; q++)
-            if (use[q]) load_row(p.rows, start + k0 + 256 * q, r[q]);
+        for (int v = 0; v < 10; v++) {
+            const float sum = wave_sum(acc[v]);
+            if (lane == 0) s_part[w][v] = sum;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float tot[10];
 #pragma unroll
-        for (int q = 0; q < BR_UNROLL; q++)
-            if (use[q]) {
-#pragma unroll
-                for (int v = 0; v < 10; v++) acc[v] += r[q][v];
-            }
-    }
-#pragma unroll
-    for (int v = 0; v < 10; v++) {
-        const float sum = wave_sum(acc[v]);
-        if (lane == 0) s_part[w][v] = sum;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        float tot[10];
-#pragma unroll
-        for (int v = 0; v < 10; v++) tot[v] = ((s_part[0][v] + s_part[1][v]) + s_part[2][v]) + s_part[3][v];
-        store_row(p.bigsum, bi, tot);
-    }
-    __syncthreads();  // s_part is rewritten by the next big Gaussian
+            for (int v = 0; v < 10; v++) tot[v] = ((s_part[0][v] + s_part[1][v]) + s_part[2][v]) + s_part[3][v];
+            store_row(p.bigsum, bi, tot);
+        }
+        if (!PERSIST) break;
+        __syncthreads();  // s_part is rewritten by the next big Gaussian
     }
 }
 
 void launch_big_reduce(hipStream_t s, const BigReduceParams &p, uint32_t nbig) {
     if (nbig == 0) return;
-    big_reduce_kernel<<<p.nbig_dev ? std::min(nbig, 2048u) : nbig, 256, 0, s>>>(p);
+    if (p.nbig_dev) big_reduce_kernel<true><<<std::min(nbig, 2048u), 256, 0, s>>>(p);
+    else big_reduce_kernel<false><<<nbig, 256, 0, s>>>(p);
 }
 
 }  // namespace gsr

@@ -159,6 +159,7 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
                         const uint32_t slot = atomicAdd(&s_tab[tile], 1u);
                         p.keys[slot] = ((unsigned long long)x.z << 32) | ui;
                         p.inst_gid[ui] = g0 + (uint32_t)o;
+                        p.inv[ui] = INV_NONE;
                     }
                 }
             }
@@ -181,6 +182,7 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
                 const uint32_t slot = atomicAdd(&s_tab[tile], 1u);
                 p.keys[slot] = dk | (u0 + c);
                 p.inst_gid[u0 + c] = gb;
+                p.inv[u0 + c] = INV_NONE;
             }
         }
     }

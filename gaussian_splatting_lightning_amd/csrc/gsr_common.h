@@ -164,9 +164,8 @@ inline int tile_key_bits(uint32_t num_tiles) {
 inline int radix_passes(int bits) { return (bits + 7) / 8; }
 
 // The radix binning's tile sort (gsr_api.hip): 16-bit keys up to 65536 tiles ("tile_key16"), sorted in digits of
-// "tile_db" bits (5: three passes over 15-bit tile ids at 4K instead of two of 8 bits -- a pass's stable scatter writes
-// each block's run of each digit, and with 32 digits instead of 256 the runs are 8x longer, so far fewer partial cache
-// lines; else 8 bits).  The carving of the binning buffer (which ping-pong slot ends as sorted_u) follows the same plan.
+// "tile_db" bits (default 8; 5 gives three passes over 15-bit tile ids at 4K instead of two, with 8x longer scatter
+// runs per digit, but measured 1.03 ms against 0.75 for the two 8-bit passes at cfg 5).  The carving of the binning buffer (which ping-pong slot ends as sorted_u) follows the same plan.
 struct TileSortPlan {
     bool k16;
     int digit_bits, passes;
@@ -175,7 +174,7 @@ inline TileSortPlan tile_sort_plan(uint32_t num_tiles) {
     TileSortPlan t;
     const int bits = tile_key_bits(num_tiles);
     t.k16 = num_tiles <= 65536u && tuning("tile_key16", 1) != 0;
-    t.digit_bits = t.k16 ? tuning("tile_db", 5) : 8;
+    t.digit_bits = t.k16 ? tuning("tile_db", 8) : 8;  // cfg 5: 8-bit digits 0.75 ms, 5-bit 1.03 (r4d)
     if (t.digit_bits < 4 || t.digit_bits > 8) t.digit_bits = 8;
     t.passes = (bits + t.digit_bits - 1) / t.digit_bits;
     return t;
@@ -187,6 +186,8 @@ struct BinningState {
     uint32_t *point_list;  // R: Gaussian ids sorted by (tile, depth, id); written by the forward composite
                            //    for the instances it loads (every instance any pixel can reach)
     uint32_t *sorted_u;    // R: expansion index of each sorted instance
+    uint32_t *inv;         // R: sorted position of instance u (its gradient-row marker), INV_NONE where the forward
+                           //    composite did not load it (filled by the binning, set by the composite)
     // scratch of the two binning paths (overlapping: only one runs per forward)
     uint32_t *keys_sorted; // radix path: R tile ids of the sorted instances
     SortScratch sort;      // radix path: tile sort (R keys); its final value buffer is sorted_u
@@ -212,6 +213,7 @@ inline size_t carve_binning(char *base, int64_t R, uint32_t num_tiles, BinningSt
     b.inst_gid = c.take<uint32_t>(n ? n : 1);
     b.point_list = c.take<uint32_t>(n ? n : 1);
     b.sorted_u = c.take<uint32_t>(n ? n : 1);
+    b.inv = c.take<uint32_t>(n ? n : 1);
     Carver cr = c;  // radix view
     const int passes = tile_sort_plan(num_tiles).passes;
     carve_sort(cr, b.sort, n, passes >= 2);
@@ -240,7 +242,7 @@ struct ImageState {
     uint32_t *tile_last;  // T: max n_contrib over the tile's pixels
     uint32_t *tile_loaded; // T: instances of the tile the forward composite gathered (>= tile_last)
     unsigned long long *tile_lastkey;  // T: key (depth bits << 32 | u) of the last instance the composite gathered, 0 if
-                                       //    none (zeroed with tile_last / tile_loaded: instance_loaded)
+                                       //    none (zeroed with tile_last / tile_loaded; a diagnostic the tests check)
     uint32_t *lpt_bcnt;    // 256: tiles per backward LPT bucket, appended by the forward's whole-tile waves (cleared
                            //      with tile_last / tile_loaded)
     uint32_t *order_fwd;   // tiles in descending forward work (instances in range), LPT launch order
@@ -812,8 +814,6 @@ __device__ __forceinline__ uint32_t rect_tile(uint32_t c, uint32_t rx, uint32_t 
     return (ry + cy) * gx + rx + (c - cy * w);
 }
 
-// Tile of a Gaussian's j-th instance (Gaussian-major expansion index inst_start + j): its expansion record's j-th kept
-// rect cell (the j-th set bit of the kept-tile mask; mask 0 = every cell, the j-th).
 // Position of the j-th (from 0) set bit of m, j < popcount(m): a branch-free binary search on popcounts.
 __device__ __forceinline__ uint32_t nth_set_bit(uint64_t m, uint32_t j) {
     uint32_t c = 0, r = j;
@@ -828,20 +828,6 @@ __device__ __forceinline__ uint32_t nth_set_bit(uint64_t m, uint32_t j) {
     }
     return c;
 }
-__device__ __forceinline__ uint32_t instance_tile(uint4 e, uint32_t j, uint32_t gx) {
-    const uint64_t m = (uint64_t)e.x | ((uint64_t)e.y << 32);
-    const uint32_t c = m ? nth_set_bit(m, j) : j;  // a culled rect's j-th kept cell
-    return rect_tile(c, e.z & 0xffffu, e.z >> 16, e.w, 1.0f / (float)e.w, gx);
-}
-// Whether the forward composite loaded instance u (of a Gaussian with depth bits dk) in its tile: the composite loads a
-// prefix of the tile's (depth, u)-sorted bucket, and records the key of the last instance it loaded per tile
-// (ImageState::tile_lastkey, 0 when none), so the instance was loaded iff its key is not above that one.  This
-// replaces an inverse-permutation word per instance, which the composite had to scatter (a random 4-B store per
-// loaded instance) and the binning had to fill.
-__device__ __forceinline__ bool instance_loaded(uint32_t dk, uint32_t u, unsigned long long lastkey) {
-    return (((unsigned long long)dk << 32) | u) <= lastkey;
-}
-
 // Orders LDS writes before later LDS reads of other lanes of the SAME wave (no s_barrier).
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -219,8 +219,13 @@ __global__ __launch_bounds__(256, SPLIT ? GSR_PRE_SPLIT_MINW : GSR_PRE_MINW) voi
     // instance total for the early host readback (gsr_forward): block sum, one 64-bit atomic per block into
     // one of CNT_NPART partial counters; likewise the range of the kept depth keys (the radix path's relative
     // depth sort), as the largest complemented key and the largest key
-    const uint32_t my_dk = (i < p.P && area > 0 && kept > 0) ? ci.depth : 0xffffffffu;
-    const uint32_t wmin = wave_min_u32(my_dk), wmax = wave_max_u32(my_dk == 0xffffffffu ? 0u : my_dk);
+    // (only where the radix path's relative depth sort can use it: p.depth_range)
+    uint32_t wmin = 0xffffffffu, wmax = 0u;
+    if (p.depth_range) {
+        const uint32_t my_dk = (i < p.P && area > 0 && kept > 0) ? ci.depth : 0xffffffffu;
+        wmin = wave_min_u32(my_dk);
+        wmax = wave_max_u32(my_dk == 0xffffffffu ? 0u : my_dk);
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) kept += (uint32_t)__shfl_xor((int)kept, o);
     __shared__ uint32_t s_dmin[4], s_dmax[4];
@@ -237,8 +242,10 @@ __global__ __launch_bounds__(256, SPLIT ? GSR_PRE_SPLIT_MINW : GSR_PRE_MINW) voi
         if (tot) {
             const uint32_t bmin = min(min(s_dmin[0], s_dmin[1]), min(s_dmin[2], s_dmin[3]));
             const uint32_t bmax = max(max(s_dmax[0], s_dmax[1]), max(s_dmax[2], s_dmax[3]));
-            atomicMax(p.g.counters + CNT_DMIN + (bid % CNT_NPART), ~bmin);
-            atomicMax(p.g.counters + CNT_DMAX + (bid % CNT_NPART), bmax);
+            if (p.depth_range) {
+                atomicMax(p.g.counters + CNT_DMIN + (bid % CNT_NPART), ~bmin);
+                atomicMax(p.g.counters + CNT_DMAX + (bid % CNT_NPART), bmax);
+            }
             old = atomicAdd(reinterpret_cast<unsigned long long *>(p.g.counters + CNT_PARTIALS) + (bid % CNT_NPART), tot);
         }
         if (p.block_sums) p.block_sums[bid] = (uint32_t)tot;  // <= 256 * 2^16 tiles
@@ -464,11 +471,13 @@ __global__ __launch_bounds__(256) void expand_kernel(ExpandParams p) {
         else
             *reinterpret_cast<uint4 *>(p.keys_out + ub) = make_uint4(key[0], key[1], key[2], key[3]);
         *reinterpret_cast<uint4 *>(p.inst_gid + ub) = make_uint4(gv[0], gv[1], gv[2], gv[3]);
+        if (p.inv_none) *reinterpret_cast<uint4 *>(p.inv_none + ub) = make_uint4(INV_NONE, INV_NONE, INV_NONE, INV_NONE);
     } else {
         for (uint32_t u = ub; u < u1; u++) {
             if (p.keys16_out) p.keys16_out[u] = (uint16_t)key[u - ub];
             else p.keys_out[u] = key[u - ub];
             p.inst_gid[u] = gv[u - ub];
+            if (p.inv_none) p.inv_none[u] = INV_NONE;
         }
     }
 }
@@ -642,9 +651,10 @@ void launch_tile_order(hipStream_t s, const uint2 *ranges, const uint32_t *tile_
 // Front-to-back: alpha = min(0.99, o*exp(power)); skip alpha < 1/255; stop a pixel before the Gaussian that
 // would take T below 1e-4.  No block barriers: the four waves of a block work on four independent tiles.
 // The batch gather also materialises, for exactly the instances it loads, the sorted Gaussian id list
-// (point_list) the backward walks, and per tile the key of the last instance it loaded (tile_lastkey), from which the
-// backward's per-Gaussian gather tells the instances that have a gradient row (instance_loaded): no per-instance
-// inverse permutation is scattered, nor filled by the binning.
+// (point_list) the backward walks and the inverse permutation inv[u] = s the backward's per-Gaussian gather reads
+// (the binning filled it with INV_NONE: no row), and per tile the key of the last instance it loaded (tile_lastkey).
+// (Round 4 replaced inv by testing each row against tile_lastkey in the backward: preprocess_bwd 0.094 -> 0.118 ms at
+// cfg 3 for the row-tile search, for ~3 us of forward stores saved; measured and reverted.)
 // Every piece of per-instance control is wave-uniform: the tile, its range and the contributor counter live
 // in SGPRs, each batch's strip masks (cell_mask) are ballots (bit j = instance j can reach the strip), and the
 // records of a batch sit in one LDS array of 48-byte entries read with immediate offsets.
@@ -733,7 +743,7 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
     const uint32_t r0 = __builtin_amdgcn_readfirstlane(rg.x), r1 = __builtin_amdgcn_readfirstlane(rg.y);
     uint32_t contributor = 0;
     uint32_t loaded_end = r0;
-    uint32_t u_last = 0, g_last = 0;  // the last loaded instance (its key, instance_loaded, is recorded per tile)
+    uint32_t u_last = 0, g_last = 0;  // the last loaded instance (its key is recorded per tile)
     FwdRec *sr = s_rec[w];
     // prefix binning: instances [r0, r0 + ks) are sorted; a walk past them selects further batches itself
     uint32_t ks = PREFIX ? __builtin_amdgcn_readfirstlane(p.tile_sorted[tile]) : 0u;
@@ -767,6 +777,7 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
             u = ext ? u_sel : p.sorted_u[s];
             gid = p.inst_gid[u];
             p.point_list[s] = gid;
+            p.inv[u] = s;
             const float4 ga = p.rec[gid].a, gb = p.rec[gid].b;
             sr[lane].a = stage_rec_a(ga);
             sr[lane].b = stage_rec_b(gb);

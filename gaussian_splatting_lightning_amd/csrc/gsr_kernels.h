@@ -64,6 +64,7 @@ struct PreprocessParams {
     uint32_t *host_words;
     uint32_t seq;
     int split = 0;  // colour left to launch_preprocess_color (SH colours only)
+    int depth_range = 0;  // publish the kept depth keys' range with the instance total (relative depth sort)
 };
 void launch_preprocess(hipStream_t s, const PreprocessParams &p);
 void launch_preprocess_color(hipStream_t s, const PreprocessParams &p);  // the colour half of a split preprocess
@@ -77,6 +78,7 @@ struct ExpandParams {
     uint32_t *exp_owner;      // optional: owner ranks of the block starts (div_up(R, EXP_TILE) + 1 words)
     uint32_t *keys_out, *inst_gid, *inst_start;
     uint16_t *keys16_out;     // optional: 16-bit tile keys (launch_radix_sort16) instead of keys_out
+    uint32_t *inv_none;       // optional: inv, set to INV_NONE for every instance here (no separate fill)
 };
 void launch_expand(hipStream_t s, const ExpandParams &p);
 
@@ -106,6 +108,7 @@ struct BucketParams {
     int lb_force;          // recompute every predecessor (tests the fallback)
     uint32_t *tile_last, *tile_loaded;  // T each: cleared by the column pass for the forward composite
     unsigned long long *tile_lastkey;   // T: likewise
+    uint32_t *inv;         // R: reset to INV_NONE beside inst_gid (the forward composite fills it)
     uint32_t *lpt_bcnt;    // 256: cleared by the column pass (the forward's backward-LPT bucket counts)
     unsigned long long *keys;  // R: depth << 32 | u, bucketed by tile
     uint32_t *inst_gid;    // R
@@ -148,6 +151,7 @@ struct RenderFwdParams {
     uint32_t *point_list, *tile_loaded;
     const uint32_t *depth_key;            // per Gaussian: the key of the last loaded instance needs its depth bits
     unsigned long long *tile_lastkey;     // T: key of the last instance each tile's walk loaded (atomicMax, zeroed)
+    uint32_t *inv;                        // R: inv[u] = sorted position of every instance the walk loads
     const GRec *rec;
     const float *bg;
     float *out_color, *out_invdepth, *final_T;
@@ -201,10 +205,7 @@ void launch_render_bwd(hipStream_t s, const RenderBwdParams &p);
 
 struct BigReduceParams {
     const uint32_t *big_list, *inst_start, *tiles;
-    const uint4 *exp_rec;           // per Gaussian: the tile of each row (instance_tile)
-    const uint32_t *depth_key;      // per Gaussian: the instances' keys (instance_loaded)
-    const unsigned long long *tile_lastkey;
-    uint32_t gx;
+    const uint32_t *inv;  // the forward's inverse permutation: INV_NONE where the composite loaded no instance (no row)
     const float *rows;
     float *bigsum;  // nbig x GRAD_ROW
     const uint32_t *nbig_dev;  // or null: the launch's nbig is exact; else an upper bound and this the count
@@ -222,10 +223,7 @@ struct PreprocessBwdParams {
     const float *view, *proj, *campos;
     const int *radii;
     const uint32_t *tiles, *inst_start, *big_slot;
-    const uint4 *exp_rec;           // per Gaussian: the tile of each row (instance_tile)
-    const uint32_t *depth_key;      // per Gaussian: the instances' keys (instance_loaded)
-    const unsigned long long *tile_lastkey;
-    uint32_t gx;
+    const uint32_t *inv;  // the forward's inverse permutation: INV_NONE where the composite loaded no instance (no row)
     const uint8_t *clamped;
     const float *sh_jac;  // 9 x P direction Jacobian of the colour, from the forward (SH degree > 0)
     const float *rows, *bigsum;

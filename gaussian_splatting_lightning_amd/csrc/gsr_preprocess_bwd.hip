@@ -67,15 +67,13 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
         if (cnt > BIG_GAUSSIAN_TILES) {
             add_row(p.bigsum, p.big_slot[i], gs);
         } else {
-            // the loaded-instance tests first, then all row loads of a group, before summing (memory-level parallelism)
-            const uint4 e = p.exp_rec[i];
-            const uint32_t dk = p.depth_key[i];
+            // the inv words first (INV_NONE: not loaded by the forward composite, no row), then all row loads of a
+            // group, before summing (memory-level parallelism)
             for (uint32_t k0 = 0; k0 < cnt; k0 += 4) {
                 bool use[4];
 #pragma unroll
                 for (int j = 0; j < 4; j++)
-                    use[j] = k0 + j < cnt &&
-                             instance_loaded(dk, start + k0 + j, p.tile_lastkey[instance_tile(e, k0 + j, p.gx)]);
+                    use[j] = k0 + j < cnt && p.inv[start + k0 + j] != INV_NONE;
                 float rw[4][10];
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
@@ -312,7 +310,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
     const size_t gend = (size_t)p.g1 * 48;
     float *sw = s_sh[w];
     // Gradient rows of the wave's 64 Gaussians (each Gaussian's rows are contiguous), gathered
-    // jointly: the (Gaussian, row) pairs of all lanes are enumerated in order, every lane tests (instance_loaded)
+    // jointly: the (Gaussian, row) pairs of all lanes are enumerated in order, every lane loads the inv words of
     // pairs l, l + 64, ... of a chunk, then the rows the composite wrote (others read as zero) into the LDS that later
     // stages dL/dsh, then each lane sums its own Gaussian's rows in row order.  Divergent per-lane
     // loops of dependent loads cost ~40 % of the kernel otherwise.  Gaussians above BIG_GAUSSIAN_TILES rows
@@ -331,10 +329,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         static_assert(CH * 10 + 128 <= PBWD_STAGE, "row chunk + meta fit the staging area");
         s_meta[lane] = make_uint2(pst, len ? p.inst_start[i] : 0u);
         wave_lds_sync();
-        // the loaded-instance tests of chunk c0 (expansion index uu, written-row marker sidx): the pair's tile from
-        // its Gaussian's expansion record (the wave's 64 records and depth keys are contiguous: cache hits), then
-        // that tile's last loaded key (instance_loaded)
-        const int gw0 = p.g0 + (int)blockIdx.x * 256 + w * 64;  // the wave's first Gaussian
+        // the inv words of chunk c0 (expansion index uu, written-row marker sidx)
         auto inv_chunk = [&](uint32_t c0, uint32_t (&uu)[PER], uint32_t (&sidx)[PER]) {
 #pragma unroll
             for (uint32_t r = 0; r < PER; r++) {
@@ -347,11 +342,8 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
                     for (int step = 32; step; step >>= 1)
                         if (s_meta[o + step].x <= j) o += step;
                     const uint2 m = s_meta[o];
-                    const uint32_t jj = j - m.x;
-                    uu[r] = m.y + jj;
-                    const int go = gw0 + o;
-                    if (instance_loaded(p.depth_key[go], uu[r], p.tile_lastkey[instance_tile(p.exp_rec[go], jj, p.gx)]))
-                        sidx[r] = 0u;
+                    uu[r] = m.y + (j - m.x);
+                    sidx[r] = p.inv[uu[r]];
                 }
             }
         };

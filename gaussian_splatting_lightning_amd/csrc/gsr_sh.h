@@ -12,11 +12,13 @@ __device__ __forceinline__ float3 operator*(float a, float3 b) { return make_flo
 __device__ __forceinline__ float3 operator+(float3 a, float3 b) { return make_float3(a.x + b.x, a.y + b.y, a.z + b.z); }
 __device__ __forceinline__ float3 operator-(float3 a, float3 b) { return make_float3(a.x - b.x, a.y - b.y, a.z - b.z); }
 __device__ __forceinline__ float dot3(float3 a, float3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-// The colour offset rgb + 0.5 (render_tools.py:129) as a rounded add that is never contracted into the SH sum's last
-// multiply: at degree 0 that sum IS a multiply (C0 * sh), and whether the backend fused it depended on the block
-// layout around the call (the fused preprocess's runtime degree switch vs the split kernel's template).
+// The colour offset rgb + 0.5 (render_tools.py:129) as an add that is never contracted into the SH sum's last
+// multiply: at degree 0 that sum IS a multiply (C0 * sh), and whether the backend fused the two into an fma depended on
+// the block layout around the call (the fused preprocess's runtime degree switch vs the split kernel's template).
+// The pragma strips the add's contract flag (HIP's __fadd_rn is a plain, contractable add).
 __device__ __forceinline__ float3 sh_offset(float3 c) {
-    return make_float3(__fadd_rn(c.x, 0.5f), __fadd_rn(c.y, 0.5f), __fadd_rn(c.z, 0.5f));
+#pragma clang fp contract(off)
+    return make_float3(c.x + 0.5f, c.y + 0.5f, c.z + 0.5f);
 }
 
 template <int DEG>

@@ -236,11 +236,14 @@ __device__ __forceinline__ void lb_store(uint32_t *p, uint32_t v) {
 // (one RS_BINS row per chunk, cs_rows rows) and its ticket.
 // Relative keys (kcap != 0, 32-bit keys, the depth sort's first pass): the key ranked is min(key - kbase, kcap), an
 // order-preserving map of the kept depth keys onto [0, kcap) with every culled key (all ones) at kcap.
+// REL (a template flag, so that no other sort carries the map: compiled in with a runtime kcap it slowed the 39.5 M-key
+// cfg 5 tile-sort scatter passes from 0.19 to 0.30-0.35 ms each).
+template <bool REL>
 __device__ __forceinline__ uint32_t rs_rel_key(uint32_t k, uint32_t kbase, uint32_t kcap) {
-    return kcap ? min(k - kbase, kcap) : k;
+    return REL ? min(k - kbase, kcap) : k;
 }
 
-template <int TILE, typename KT = uint32_t, int BINS = RS_BINS>
+template <int TILE, typename KT = uint32_t, int BINS = RS_BINS, bool REL = false>
 __global__ __launch_bounds__(256) void rs_hist_kernel(const KT *__restrict__ keys, uint32_t n, int shift, uint32_t dmask,
                                                       uint32_t *__restrict__ counts, uint32_t nb,
                                                       uint32_t *__restrict__ cs_status, uint32_t cs_rows,
@@ -271,16 +274,16 @@ __global__ __launch_bounds__(256) void rs_hist_kernel(const KT *__restrict__ key
                     atomicAdd(&h[w][((wds[k] >> 16) >> shift) & dmask], 1u);
                 }
             } else {
-                atomicAdd(&h[w][(rs_rel_key(q.x, kbase, kcap) >> shift) & dmask], 1u);
-                atomicAdd(&h[w][(rs_rel_key(q.y, kbase, kcap) >> shift) & dmask], 1u);
-                atomicAdd(&h[w][(rs_rel_key(q.z, kbase, kcap) >> shift) & dmask], 1u);
-                atomicAdd(&h[w][(rs_rel_key(q.w, kbase, kcap) >> shift) & dmask], 1u);
+                atomicAdd(&h[w][(rs_rel_key<REL>(q.x, kbase, kcap) >> shift) & dmask], 1u);
+                atomicAdd(&h[w][(rs_rel_key<REL>(q.y, kbase, kcap) >> shift) & dmask], 1u);
+                atomicAdd(&h[w][(rs_rel_key<REL>(q.z, kbase, kcap) >> shift) & dmask], 1u);
+                atomicAdd(&h[w][(rs_rel_key<REL>(q.w, kbase, kcap) >> shift) & dmask], 1u);
             }
         }
     } else {
         for (int i = tid; i < TILE; i += 256) {
             const uint32_t j = base + i;
-            if (j < n) atomicAdd(&h[w][(rs_rel_key((uint32_t)keys[j], kbase, kcap) >> shift) & dmask], 1u);
+            if (j < n) atomicAdd(&h[w][(rs_rel_key<REL>((uint32_t)keys[j], kbase, kcap) >> shift) & dmask], 1u);
         }
     }
     __syncthreads();
@@ -463,7 +466,7 @@ static void launch_count_scan(hipStream_t s, uint32_t *counts, uint32_t nb, uint
 // radix sort pass: stable scatter
 // ------------------------------------------------------------------------------------------------
 // digit_off (or null): exclusive digit offsets added to counts_scanned's column prefixes (rs_countscan_kernel)
-template <bool IOTA_IN, int ITEMS, typename KT = uint32_t, int BINS = RS_BINS>
+template <bool IOTA_IN, int ITEMS, typename KT = uint32_t, int BINS = RS_BINS, bool REL = false>
 __global__ __launch_bounds__(256) void rs_scatter_kernel(const KT *__restrict__ keys_in,
                                                          const uint32_t *__restrict__ vals_in, uint32_t n,
                                                          int shift, const uint32_t *__restrict__ counts_scanned,
@@ -492,7 +495,7 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const KT *__restrict__ 
     for (int it = 0; it < ITEMS; it++) {  // loads first (see rs_onesweep_kernel)
         const uint32_t j = blk + w * ((ITEMS * 256) / 4) + it * 64 + lane;
         const bool valid = j < n;
-        key[it] = valid ? rs_rel_key((uint32_t)keys_in[j], kbase, kcap) : 0u;
+        key[it] = valid ? rs_rel_key<REL>((uint32_t)keys_in[j], kbase, kcap) : 0u;
         val[it] = IOTA_IN ? j : (valid ? vals_in[j] : 0u);
     }
 #pragma unroll
@@ -925,9 +928,14 @@ static void launch_radix_sort_multi(hipStream_t s, SortScratch &sc, uint32_t n, 
         const KT *kin = p == 0 ? keys0 : k[in];
         const uint32_t cap = p == 0 ? kcap : 0u;
         uint32_t *cs_status = one ? sc.status + (size_t)p * nch * BINS : nullptr;
-        rs_hist_kernel<ITEMS * 256, KT, BINS><<<nb, 256, 0, s>>>(kin, n, shift, dmask, sc.counts, nb, cs_status, nch,
-                                                                sc.ctrl + RS_CTRL_COUNTER + p,
-                                                                p == 0 ? sc.ctrl + RS_CTRL_ERR : nullptr, kbase, cap);
+        if (cap)
+            rs_hist_kernel<ITEMS * 256, KT, BINS, true><<<nb, 256, 0, s>>>(kin, n, shift, dmask, sc.counts, nb, cs_status,
+                                                                          nch, sc.ctrl + RS_CTRL_COUNTER + p,
+                                                                          sc.ctrl + RS_CTRL_ERR, kbase, cap);
+        else
+            rs_hist_kernel<ITEMS * 256, KT, BINS><<<nb, 256, 0, s>>>(kin, n, shift, dmask, sc.counts, nb, cs_status, nch,
+                                                                    sc.ctrl + RS_CTRL_COUNTER + p,
+                                                                    p == 0 ? sc.ctrl + RS_CTRL_ERR : nullptr);
         const uint32_t *scanned = sc.counts, *doff = nullptr;
         if (one) {
             rs_countscan_kernel<CS_C, BINS><<<nch, BINS, 0, s>>>(sc.counts, nb, sc.counts_pre, cs_status,
@@ -940,12 +948,15 @@ static void launch_radix_sort_multi(hipStream_t s, SortScratch &sc, uint32_t n, 
         }
         SortGather ga;
         if (p == passes - 1 && gather) ga = *gather;
-        if (p == 0 && !keyed)
+        if (p == 0 && !keyed && cap)
+            rs_scatter_kernel<true, ITEMS, KT, BINS, true><<<nb, 256, 0, s>>>(kin, nullptr, n, shift, scanned, doff, nb,
+                                                                              k[out], sc.v[out], ga, dmask, kbase, cap);
+        else if (p == 0 && !keyed)
             rs_scatter_kernel<true, ITEMS, KT, BINS><<<nb, 256, 0, s>>>(kin, nullptr, n, shift, scanned, doff, nb,
-                                                                        k[out], sc.v[out], ga, dmask, kbase, cap);
+                                                                        k[out], sc.v[out], ga, dmask);
         else
             rs_scatter_kernel<false, ITEMS, KT, BINS><<<nb, 256, 0, s>>>(kin, sc.v[in], n, shift, scanned, doff, nb,
-                                                                         k[out], sc.v[out], ga, dmask, kbase, cap);
+                                                                         k[out], sc.v[out], ga, dmask);
     }
 }
 

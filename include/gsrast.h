@@ -292,6 +292,8 @@ void gsr_reset_stage_times(void);
 
 /* Internal tuning knobs for A/B measurements (e.g. "bwd_occ4"); unknown names are ignored by kernels. */
 void gsr_set_tuning(const char *name, int value);
+/* gsr_set_tuning(name, GSR_TUNING_UNSET) forgets the knob: its built-in default applies again. */
+#define GSR_TUNING_UNSET (-2147483647 - 1)
 /* A knob's value (default_value if never set).  The forward also records diagnostics here under "stat_*" names
  * (e.g. "stat_depth_passes": the radix passes of the last depth sort, 0 on the bucket path). */
 int gsr_get_tuning(const char *name, int default_value);

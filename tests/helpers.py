@@ -107,6 +107,7 @@ def hip_state_arrays(out: dict) -> dict:
     res = dict(
         point_list=point_list,
         point_list_written=view(st.binning_buffer, lay["bin_point_list"], R, i32).astype(np.uint32),
+        inv=view(st.binning_buffer, lay["bin_inv"], R, i32).astype(np.uint32),
         sorted_u=sorted_u.astype(np.uint32),
         tile_loaded=view(st.image_buffer, lay["img_tile_loaded"], T, i32).astype(np.uint32),
         tile_last=view(st.image_buffer, lay["img_tile_last"], T, i32).astype(np.uint32),

@@ -63,14 +63,16 @@ def compare_forward(inp, hip, oracle_out):
         assert np.array_equal(hs[k][on].view(np.uint32), g[k][on].view(np.uint32)), k
     kept = g["tiles_touched"] > 0
     assert np.array_equal(hs["depths"][kept].view(np.uint32), g["depths"][kept].view(np.uint32))
-    # The forward gathers every instance any pixel can reach; for exactly those it writes the sorted id list, and per
-    # tile the key (depth bits << 32 | expansion index) of the last one, from which the backward tells loaded
-    # instances (instance_loaded in gsr_common.h)
+    # The forward gathers every instance any pixel can reach; for exactly those it writes the sorted id list and the
+    # inverse permutation (the backward's row markers), and per tile the key (depth bits << 32 | expansion index) of
+    # the last one
     loaded = np.zeros(len(pl), bool)
     for t in np.nonzero(hs["tile_loaded"])[0]:
         loaded[rg[t, 0]: rg[t, 0] + hs["tile_loaded"][t]] = True
     assert np.all(hs["tile_loaded"] >= hs["tile_last"])
     assert np.array_equal(hs["point_list_written"][loaded], pl[loaded])
+    su = hs["sorted_u"][loaded].astype(np.int64)
+    assert np.array_equal(hs["inv"][su], np.nonzero(loaded)[0].astype(np.uint32))
     ld = hs["tile_loaded"].astype(np.int64)
     has = ld > 0
     s_last = rg[has, 0].astype(np.int64) + ld[has] - 1
@@ -456,8 +458,8 @@ def test_exact_culling_is_bitwise_invisible(gpu_device):
         _native.set_tuning("cull", 1)
         cull = run_hip(inp, gpu_device, dc, di)
     finally:
-        _native.set_tuning("cull", 1)
-        _native.set_tuning("bwd_seg", 1)
+        _native.unset_tuning("cull")
+        _native.unset_tuning("bwd_seg")
     assert cull["state"].num_rendered < 0.8 * full["state"].num_rendered
     for k in ("color", "invdepth", "radii"):
         assert np.array_equal(cull[k], full[k]), k
@@ -582,8 +584,8 @@ def test_composite_variants_are_bitwise_identical(gpu_device, knobs):
     finally:
         for k in knobs:
             _native.set_tuning(k, defaults[k])
-        _native.set_tuning("bwd_parts", 0)
-        _native.set_tuning("bwd_seg", 1)
+        _native.unset_tuning("bwd_parts")
+        _native.unset_tuning("bwd_seg")
     for k in ("color", "invdepth", "radii"):
         assert np.array_equal(ref[k], alt[k]), k
     for k in GRADS:
@@ -613,9 +615,9 @@ def test_segmented_backward(gpu_device, seg_k):
         _native.set_tuning("seg_k", seg_k)
         alt = run_hip(inp, gpu_device, dc, di)
     finally:
-        _native.set_tuning("bwd_seg", 1)
-        _native.set_tuning("bwd_parts", 0)
-        _native.set_tuning("seg_k", 64)
+        _native.unset_tuning("bwd_seg")
+        _native.unset_tuning("bwd_parts")
+        _native.unset_tuning("seg_k")
     for k in ("color", "invdepth", "radii"):
         assert np.array_equal(ref[k], alt[k]), k
     errs = _seg_rel_errors(alt, ref)
@@ -645,8 +647,8 @@ def test_segmented_backward_without_checkpoints(gpu_device):
         _native.set_tuning("bwd_seg", 1)  # backward only: the forward wrote no checkpoints
         alt = backward_raw(st, rs, dct, dit)
     finally:
-        _native.set_tuning("bwd_seg", 1)
-        _native.set_tuning("bwd_parts", 0)
+        _native.unset_tuning("bwd_seg")
+        _native.unset_tuning("bwd_parts")
     for k in GRADS:
         assert torch.equal(ref[k], alt[k]), k
 
@@ -666,7 +668,7 @@ def test_long_tiles_and_depth_ties(gpu_device, n, W, H):
         _native.set_tuning("bucket", 2)  # bucket binning even for these long tiles (the default picks radix)
         hip = run_hip(inp, gpu_device, dc, di)
     finally:
-        _native.set_tuning("bucket", 1)
+        _native.unset_tuning("bucket")
     run = compare_forward(inp, hip, run_oracle(inp))
     n_tile = np.diff(hip_state_arrays(hip)["ranges"], axis=1)[:, 0]
     if W > 32:
@@ -693,7 +695,7 @@ def test_dense_tiles_fall_back_to_radix_after_speculative_count(gpu_device):
         _native.set_tuning("bucket", 2)
         forced = run_hip(inp, gpu_device, dc, di)
     finally:
-        _native.set_tuning("bucket", 1)
+        _native.unset_tuning("bucket")
     for k in ("color", "invdepth", "radii"):
         assert np.array_equal(hip[k], forced[k]), k
     for k in GRADS:
@@ -722,11 +724,11 @@ def test_binning_paths_are_bitwise_identical(gpu_device, W, H, onesweep, cscan, 
         _native.set_tuning("tile_key16", k16)
         alt = run_hip(inp, gpu_device, dc, di)
     finally:
-        _native.set_tuning("tile_key16", 1)
-        _native.set_tuning("bucket", 1)
-        _native.set_tuning("onesweep", 1)
-        _native.set_tuning("rs_cscan", 1)
-        _native.set_tuning("bk_xcd", 1)
+        _native.unset_tuning("tile_key16")
+        _native.unset_tuning("bucket")
+        _native.unset_tuning("onesweep")
+        _native.unset_tuning("rs_cscan")
+        _native.unset_tuning("bk_xcd")
     a, b = hip_state_arrays(ref), hip_state_arrays(alt)
     for k in ("point_list", "ranges", "tiles", "n_contrib", "tile_last", "tile_loaded"):
         assert np.array_equal(a[k], b[k]), k
@@ -736,10 +738,10 @@ def test_binning_paths_are_bitwise_identical(gpu_device, W, H, onesweep, cscan, 
         assert np.array_equal(ref["grads"][k], alt["grads"][k]), k
 
 
-@pytest.mark.parametrize("db", [4, 8])
+@pytest.mark.parametrize("db", [4, 5])
 def test_tile_sort_digit_width_is_invisible(gpu_device, db):
-    """The radix binning's 16-bit tile sort in digits of 4 or 8 bits (4 or 2 passes at 1280x720's 12-bit tile ids)
-    gives bitwise the instance order of the default 5-bit digits (3 passes)."""
+    """The radix binning's 16-bit tile sort in digits of 4 or 5 bits (3 passes at 1280x720's 12-bit tile ids)
+    gives bitwise the instance order of the default 8-bit digits (2 passes)."""
     from gaussian_splatting_lightning_amd import _native
     inp = scene_inputs(200_000, 1280, 720, sh_degree=3, seed=6, stress_fraction=0.01)
     dc, di = upstream(1280, 720, 6)
@@ -749,8 +751,8 @@ def test_tile_sort_digit_width_is_invisible(gpu_device, db):
         _native.set_tuning("tile_db", db)
         alt = run_hip(inp, gpu_device, dc, di)
     finally:
-        _native.set_tuning("bucket", 1)
-        _native.set_tuning("tile_db", 5)
+        _native.unset_tuning("bucket")
+        _native.unset_tuning("tile_db")
     a, b = hip_state_arrays(ref), hip_state_arrays(alt)
     for k in ("point_list", "ranges", "n_contrib"):
         assert np.array_equal(a[k], b[k]), k
@@ -779,7 +781,7 @@ def test_prefix_binning_is_bitwise_the_full_sort(gpu_device, n, k, dup):
         _native.set_tuning("bk_prefix", k)
         alt = run_hip(inp, gpu_device, dc, di)
     finally:
-        _native.set_tuning("bk_prefix", 512)
+        _native.unset_tuning("bk_prefix")
     a, b = hip_state_arrays(ref), hip_state_arrays(alt)
     assert not a["prefix_mode"] and b["prefix_mode"]
     for key in ("ranges", "tiles", "n_contrib", "tile_last", "tile_loaded"):
@@ -798,7 +800,7 @@ def test_prefix_binning_is_bitwise_the_full_sort(gpu_device, n, k, dup):
 
 @pytest.mark.parametrize("deg,bucket", [(3, 1), (2, 1), (1, 0), (0, 1)])
 def test_split_colour_preprocess_is_bitwise_the_fused_one(gpu_device, deg, bucket):
-    """The SH colour evaluated by its own kernel behind the bucket count pass ("pre_split" 1, default) gives bitwise
+    """The SH colour evaluated by its own kernel behind the bucket count pass ("pre_split" 1) gives bitwise
     the records, outputs and gradients of the fused preprocess (colour inside the projection kernel)."""
     from gaussian_splatting_lightning_amd import _native
     inp = scene_inputs(60_000, 640, 480, sh_degree=deg, seed=12 + deg)
@@ -810,8 +812,8 @@ def test_split_colour_preprocess_is_bitwise_the_fused_one(gpu_device, deg, bucke
         _native.set_tuning("pre_split", 1)
         alt = run_hip(inp, gpu_device, dc, di)
     finally:
-        _native.set_tuning("bucket", 1)
-        _native.set_tuning("pre_split", 1)
+        _native.unset_tuning("bucket")
+        _native.unset_tuning("pre_split")
     a, b = hip_state_arrays(ref), hip_state_arrays(alt)
     for key in ("rec", "clamped", "ranges", "point_list", "n_contrib"):
         assert np.array_equal(a[key], b[key]), key
@@ -842,9 +844,9 @@ def test_relative_depth_sort_is_bitwise_the_32bit_one(gpu_device, n, depth_scale
         alt = run_hip(inp, gpu_device, dc, di)
         assert 1 <= _native.get_tuning("stat_depth_passes") <= 3  # the relative sort ran
     finally:
-        _native.set_tuning("bucket", 1)
-        _native.set_tuning("onesweep_max_n", 3 << 20)
-        _native.set_tuning("depth_rel", 1)
+        _native.unset_tuning("bucket")
+        _native.unset_tuning("onesweep_max_n")
+        _native.unset_tuning("depth_rel")
     a, b = hip_state_arrays(ref), hip_state_arrays(alt)
     for key in ("point_list", "ranges", "n_contrib", "tiles"):
         assert np.array_equal(a[key], b[key]), key
@@ -879,8 +881,8 @@ def test_debug_mode_is_bitwise_identical(gpu_device, bucket, os_max):
         a = run_hip(inp, gpu_device, dc, di)
         b = run_hip(inp, gpu_device, dc, di, debug=True)
     finally:
-        _native.set_tuning("bucket", 1)
-        _native.set_tuning("onesweep_max_n", 3 << 20)
+        _native.unset_tuning("bucket")
+        _native.unset_tuning("onesweep_max_n")
     for k in ("color", "invdepth", "radii"):
         assert np.array_equal(a[k], b[k]), k
     for k in GRADS:
@@ -902,9 +904,9 @@ def test_lookback_fallback_is_bitwise_invisible(gpu_device, bucket, onesweep):
         _native.set_tuning("lb_force", 1)
         b = run_hip(inp, gpu_device, dc, di)
     finally:
-        _native.set_tuning("lb_force", 0)
-        _native.set_tuning("bucket", 1)
-        _native.set_tuning("onesweep", 1)
+        _native.unset_tuning("lb_force")
+        _native.unset_tuning("bucket")
+        _native.unset_tuning("onesweep")
     sa, sb = hip_state_arrays(a), hip_state_arrays(b)
     for k in ("point_list", "ranges", "tiles", "n_contrib"):
         assert np.array_equal(sa[k], sb[k]), k
@@ -1009,3 +1011,23 @@ def test_chunked_backward_is_bitwise_the_single_call(gpu_device, compact):
         want = ref[k].reshape(n, -1)
         assert torch.equal(got, want), k
     assert torch.equal(stats2, stats) and torch.equal(mrad2, mrad)
+
+
+@pytest.mark.parametrize("W,H,bucket,n", [(1920, 1080, 1, 300_000), (1280, 720, 0, 150_000), (320, 240, 1, 20_000)])
+def test_inverse_permutation_marks_exactly_the_loaded_instances(gpu_device, W, H, bucket, n):
+    """The backward finds the instances with a gradient row (the ones the forward composite loaded) through the inverse
+    permutation: inv[sorted_u[s]] = s over every tile's loaded prefix, INV_NONE for every other instance -- on the
+    bucket path (whole tiles at 1080p, row-strip parts at 320x240) and the radix path."""
+    from gaussian_splatting_lightning_amd import _native
+    inp = scene_inputs(n, W, H, sh_degree=3, seed=21, stress_fraction=0.01)
+    with _native.tuned(bucket=bucket):
+        out = run_hip(inp, gpu_device)
+    hs = hip_state_arrays(out)
+    rg, ld = hs["ranges"].astype(np.int64), hs["tile_loaded"].astype(np.int64)
+    pos = np.concatenate([np.arange(a, a + l) for a, l in zip(rg[:, 0], ld) if l > 0])
+    assert len(pos) > 0
+    u = hs["sorted_u"][pos].astype(np.int64)
+    assert np.array_equal(hs["inv"][u], pos.astype(np.uint32))
+    rest = np.ones(hs["num_rendered"], bool)
+    rest[u] = False
+    assert rest.any() and np.all(hs["inv"][rest] == 0xFFFFFFFF)

@@ -77,6 +77,6 @@ def test_streaming_ssim_matches_tiled_kernels(gpu_device, shape, padding):
             (1 - m).backward()
             out[mode] = (float(m), xt.grad.cpu().numpy())
     finally:
-        _native.set_tuning("ssim_stream", 1)
+        _native.unset_tuning("ssim_stream")
     assert abs(out[0][0] - out[1][0]) <= 1e-6 * max(1.0, abs(out[0][0]))
     assert np.array_equal(out[0][1], out[1][1])
