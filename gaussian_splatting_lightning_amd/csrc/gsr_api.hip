@@ -508,7 +508,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
         bp.nb = div_up(P, bp.gper);
         bp.tiles = g.tiles; bp.inst_start = g.inst_start; bp.block_sums = g.block_sums; bp.depth_key = g.depth_key;
         bp.big_list = g.big_list; bp.exp_rec = g.exp_rec;
-        bp.hist = im.bk_hist; bp.hist_pre = im.bk_hist_pre; bp.tile_cnt = im.bk_tile_cnt; bp.tile_start = im.bk_tile_start; bp.ranges = im.ranges;
+        bp.hist = im.bk_hist; bp.hist_pre = im.bk_hist_pre; bp.tile_next = im.bk_tile_next; bp.reg_start = im.bk_reg_start; bp.tile_start = im.bk_tile_start; bp.ranges = im.ranges;
         bp.tile_last = im.tile_last; bp.tile_loaded = im.tile_loaded; bp.tile_lastkey = im.tile_lastkey;
         bp.lpt_bcnt = im.lpt_bcnt;
         bp.ticket = g.counters + CNT_COL_TICKET; bp.tile_status = g.tile_status; bp.err = g.counters + CNT_OVERFLOW;
@@ -620,7 +620,17 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
         return fail(GSR_ERR_OVERFLOW, "too many tile instances for the single-level scan");
     if (bucket) {
         if (R > 0) {
-            bp.keys = b.bk_keys; bp.inst_gid = b.inst_gid; bp.inv = b.inv;
+            bp.keys = b.bk_keys; bp.inst_gid = b.inst_gid; bp.inv = b.inv; bp.R = R;
+            // region scatter: keys into 16-tile regions first (long runs per block), then a partition pass into the tile
+            // buckets (gsr_bin.hip bk_partition_kernel) -- "bk_region" 1 (default) above 4096 tiles (short runs: cfg 3 has
+            // ~2 keys per block and tile), 2 always, 0 never (at 800x800, 2500 tiles, the direct scatter's 12 us is
+            // already below the partition pass alone)
+            const int bkr = tuning("bk_region", 1);
+            // (the tile-in-region rides in u's top bits: R <= 2^28; the automatic choice also wants >= 256 keys per region
+            // on average, so that a partition chunk rarely spans more regions than its LDS bins cover)
+            const uint32_t nreg = div_up(T, BK_REGION);
+            bp.keys_reg = ((bkr == 2 || (bkr == 1 && T > 4096 && R >= 256u * nreg)) && R <= (1u << BK_REG_SHIFT))
+                              ? b.bk_keys2 : nullptr;
             bp.order = lpt ? im.order_fwd : nullptr;
             bp.lpt_shift = tuning("lpt_shift", 3);
             GSR_STAGE(ST_BK_SCATTER, dbg, launch_bucket_scatter(stream, bp));  // and the forward LPT order

@@ -93,7 +93,19 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
         lpt_order_block(p.ranges, nullptr, 0, (int)T, p.lpt_shift, p.order, reinterpret_cast<uint32_t *>(&s_own[0][0]));
         return;
     }
-    if (SCATTER) {
+    const bool reg = SCATTER && p.keys_reg != nullptr;  // region scatter (uniform)
+    if (SCATTER && reg) {
+        // region r's next free slot for this block: the region's first tile start plus this block's column prefixes of
+        // its tiles (the instances of the blocks before it in every tile of the region precede it)
+        const uint32_t *hrow = p.hist_pre + (size_t)b * T;
+        const uint32_t nr = (T + BK_REGION - 1) / BK_REGION;
+        for (uint32_t r = tid; r < nr; r += 64 * BKW) {
+            const uint32_t t0 = r * BK_REGION, t1 = min(T, t0 + BK_REGION);
+            uint32_t acc = p.tile_start[t0];
+            for (uint32_t t = t0; t < t1; t++) acc += hrow[t];
+            s_tab[r] = acc;
+        }
+    } else if (SCATTER) {
         const uint32_t *hrow = p.hist_pre + (size_t)b * T;
         for (uint32_t t = tid; t < T; t += 64 * BKW) s_tab[t] = p.tile_start[t] + hrow[t];
     } else {
@@ -156,8 +168,13 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
                         atomicAdd(&s_tab[tile], 1u);
                     } else {
                         const uint32_t ui = x.y + (mo ? (uint32_t)__popcll(mo & ((1ull << c) - 1ull)) : c);
-                        const uint32_t slot = atomicAdd(&s_tab[tile], 1u);
-                        p.keys[slot] = ((unsigned long long)x.z << 32) | ui;
+                        const unsigned long long key = ((unsigned long long)x.z << 32) | ui;
+                        if (reg) {
+                            const uint32_t slot = atomicAdd(&s_tab[tile / BK_REGION], 1u);
+                            p.keys_reg[slot] = key | ((unsigned long long)(tile % BK_REGION) << BK_REG_SHIFT);
+                        } else {
+                            p.keys[atomicAdd(&s_tab[tile], 1u)] = key;
+                        }
                         p.inst_gid[ui] = g0 + (uint32_t)o;
                         p.inv[ui] = INV_NONE;
                     }
@@ -179,8 +196,12 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
             if (!SCATTER) {
                 atomicAdd(&s_tab[tile], 1u);
             } else {
-                const uint32_t slot = atomicAdd(&s_tab[tile], 1u);
-                p.keys[slot] = dk | (u0 + c);
+                if (reg) {
+                    const uint32_t slot = atomicAdd(&s_tab[tile / BK_REGION], 1u);
+                    p.keys_reg[slot] = (dk | (u0 + c)) | ((unsigned long long)(tile % BK_REGION) << BK_REG_SHIFT);
+                } else {
+                    p.keys[atomicAdd(&s_tab[tile], 1u)] = dk | (u0 + c);
+                }
                 p.inst_gid[u0 + c] = gb;
                 p.inv[u0 + c] = INV_NONE;
             }
@@ -275,11 +296,15 @@ __global__ __launch_bounds__(64 * CW) void bk_columns_kernel(BucketParams p) {
             const uint32_t st = (uint32_t)(excl + inc - tot);
             p.tile_start[t] = st;
             p.ranges[t] = tot ? make_uint2(st, st + tot) : make_uint2(0, 0);  // empty: (0, 0), as the reference
-            p.tile_cnt[t] = tot;
+            p.tile_next[t] = st;
+            if (t % BK_REGION == 0) p.reg_start[t / BK_REGION] = st;  // compact region starts (the region partition)
             p.tile_last[t] = 0u;
             p.tile_loaded[t] = 0u;
             p.tile_lastkey[t] = 0ull;
-            if (t == T - 1) p.tile_start[T] = st + tot;
+            if (t == T - 1) {
+                p.tile_start[T] = st + tot;
+                p.reg_start[(T + BK_REGION - 1) / BK_REGION] = st + tot;
+            }
         }
         const bool l0 = t < T && tot > SEG_CAP && tot <= SEG_BLOCK_CAP, l1 = t < T && tot > SEG_BLOCK_CAP;
         const uint64_t m0 = __ballot(l0), m1 = __ballot(l1);
@@ -317,6 +342,121 @@ __global__ __launch_bounds__(64 * CW) void bk_columns_kernel(BucketParams p) {
             const uint32_t v = hist[row];
             hist_pre[row] = run;
             run += v;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Region scatter, second step (p.keys_reg): the region-grouped keys move into their tile buckets.  The direct scatter
+// stores every key at a random slot of its tile's bucket, where a block's run is ~2 keys at 1080p (256 blocks, 8160
+// tiles): 4.2 M partial-line stores (2.45x write amplification at cfg 3); into regions (BK_REGION consecutive tile ids)
+// the runs are 16x longer.  Here every workgroup takes a fixed chunk of PART_CHUNK region-grouped keys (so a dense
+// region is spread over many workgroups): a counting sort of the chunk by (region, tile) bin in LDS, one global atomic
+// per non-empty bin for its slots in the tile's bucket (tile_next), then each bin's run stored contiguously.  A chunk
+// over more than PART_MAXR regions (sparse ones) sends its keys one by one.  Bucket order is arbitrary (the per-tile
+// sorts make it irrelevant).
+constexpr int PART_THREADS = 256;
+constexpr int PART_ITEMS = 8;
+constexpr uint32_t PART_CHUNK = PART_THREADS * PART_ITEMS;
+constexpr uint32_t PART_MAXR = 32;
+constexpr uint32_t PART_BINS = PART_MAXR * BK_REGION;
+// region of sorted position i: the last r < n with rs[r] <= i (rs non-decreasing, rs[0] <= i)
+__device__ __forceinline__ uint32_t bk_region_of(const uint32_t *rs, uint32_t lo, uint32_t n, uint32_t i) {
+    uint32_t hi = n - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (rs[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+__global__ __launch_bounds__(PART_THREADS) void bk_partition_kernel(BucketParams p) {
+    __shared__ unsigned long long s_keys[PART_CHUNK];
+    __shared__ uint16_t s_bin[PART_CHUNK];
+    __shared__ uint32_t s_cnt[PART_BINS], s_lstart[PART_BINS], s_gbase[PART_BINS];
+    __shared__ uint32_t s_rstart[PART_MAXR + 1];
+    __shared__ uint32_t s_nle[2];
+    constexpr unsigned long long TB_MASK = (unsigned long long)(BK_REGION - 1) << BK_REG_SHIFT;
+    const uint32_t T = p.T, nr = (T + BK_REGION - 1) / BK_REGION, R = p.tile_start[T];
+    const uint32_t c0 = blockIdx.x * PART_CHUNK;
+    if (c0 >= R) return;  // workgroup-uniform
+    const uint32_t n = min(PART_CHUNK, R - c0);
+    const int tid = threadIdx.x;
+    unsigned long long k[PART_ITEMS];  // the chunk's keys, loaded first (they do not depend on the region search)
+#pragma unroll
+    for (int q = 0; q < PART_ITEMS; q++) {
+        const uint32_t i = (uint32_t)(q * PART_THREADS + tid);
+        k[q] = i < n ? p.keys_reg[c0 + i] : 0ull;
+    }
+    if (tid == 0) {  // the chunk's first and last regions: searches over the compact region starts (L2-resident)
+        s_nle[0] = bk_region_of(p.reg_start, 0, nr, c0);
+        s_nle[1] = bk_region_of(p.reg_start, 0, nr, c0 + n - 1);
+    }
+    __syncthreads();
+    const uint32_t rlo = s_nle[0], nreg = s_nle[1] - rlo + 1;  // regions rlo .. rlo + nreg - 1 hold the chunk
+    if (nreg > PART_MAXR) {  // sparse regions: every key takes its slot alone
+        for (uint32_t i = c0 + tid; i < c0 + n; i += PART_THREADS) {
+            const unsigned long long k = p.keys_reg[i];
+            const uint32_t t = bk_region_of(p.reg_start, rlo, rlo + nreg, i) * BK_REGION +
+                               (uint32_t)((k & TB_MASK) >> BK_REG_SHIFT);
+            p.keys[atomicAdd(&p.tile_next[t], 1u)] = k & ~TB_MASK;
+        }
+        return;
+    }
+    for (uint32_t j = tid; j <= nreg; j += PART_THREADS) s_rstart[j] = p.reg_start[rlo + j];
+    for (uint32_t j = tid; j < nreg * BK_REGION; j += PART_THREADS) s_cnt[j] = 0u;
+    __syncthreads();
+    uint32_t bin[PART_ITEMS], rank[PART_ITEMS];
+#pragma unroll
+    for (int q = 0; q < PART_ITEMS; q++) {
+        const uint32_t i = (uint32_t)(q * PART_THREADS + tid);
+        rank[q] = 0xffffffffu;
+        bin[q] = 0;
+        if (i < n) {
+            uint32_t j = 0;  // region of the key within the chunk's regions
+#pragma unroll
+            for (uint32_t step = PART_MAXR / 2; step; step >>= 1)
+                if (j + step < nreg && s_rstart[j + step] <= c0 + i) j += step;
+            bin[q] = j * BK_REGION + (uint32_t)((k[q] & TB_MASK) >> BK_REG_SHIFT);
+            rank[q] = atomicAdd(&s_cnt[bin[q]], 1u);
+        }
+    }
+    __syncthreads();
+    const uint32_t nbins = nreg * BK_REGION;
+    if (tid < 64) {  // chunk-local bin starts (one wave, PART_BINS / 64 bins per lane), then each bin's global slots
+        constexpr int PER = PART_BINS / 64;
+        uint32_t c[PER], sum = 0;
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const uint32_t b = (uint32_t)(tid * PER + q);
+            c[q] = b < nbins ? s_cnt[b] : 0u;
+            sum += c[q];
+        }
+        uint32_t run = wave_inclusive_scan(sum, tid) - sum;
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const uint32_t b = (uint32_t)(tid * PER + q);
+            if (b < nbins) {
+                s_lstart[b] = run;
+                if (c[q]) s_gbase[b] = atomicAdd(&p.tile_next[(rlo + b / BK_REGION) * BK_REGION + b % BK_REGION], c[q]);
+            }
+            run += c[q];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PART_ITEMS; q++)
+        if (rank[q] != 0xffffffffu) {
+            const uint32_t pos = s_lstart[bin[q]] + rank[q];
+            s_keys[pos] = k[q] & ~TB_MASK;
+            s_bin[pos] = (uint16_t)bin[q];
+        }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PART_ITEMS; q++) {  // bin by bin, contiguous: coalesced stores
+        const uint32_t i = (uint32_t)(q * PART_THREADS + tid);
+        if (i < n) {
+            const uint32_t b = s_bin[i];
+            p.keys[s_gbase[b] + (i - s_lstart[b])] = s_keys[i];
         }
     }
 }
@@ -926,7 +1066,11 @@ void launch_bucket_count(hipStream_t s, const BucketParams &p) {
 }
 
 // plus one workgroup for the forward LPT order when p.order is set
-void launch_bucket_scatter(hipStream_t s, const BucketParams &p) { launch_walk<true>(s, p, p.nb + (p.order ? 1u : 0u)); }
+void launch_bucket_scatter(hipStream_t s, const BucketParams &p) {
+    launch_walk<true>(s, p, p.nb + (p.order ? 1u : 0u));
+    // one workgroup per PART_CHUNK keys of the upper bound on R the binning buffer was carved for (extra ones exit)
+    if (p.keys_reg) bk_partition_kernel<<<div_up(p.R, PART_CHUNK), PART_THREADS, 0, s>>>(p);
+}
 
 void launch_seg_sort(hipStream_t s, const SegSortParams &p0) {
     if (p0.T == 0) return;

@@ -93,6 +93,8 @@ inline void carve_sort(Carver &c, SortScratch &s, uint32_t n, bool need_v0) {
 constexpr uint32_t BK_MAX_TILES = 32768;  // 128 KB of LDS counters (4K images: 32400 tiles)
 constexpr uint32_t BK_MAX_BLOCKS = 512;   // rows of the count matrix (carved for the maximum)
 constexpr uint32_t BK_MAX_MEAN = 1024;    // default path choice: mean instances per tile up to this
+constexpr uint32_t BK_REGION = 16;        // tiles per region of the region scatter (consecutive tile ids)
+constexpr int BK_REG_SHIFT = 28;          // the region scatter carries a key's tile-in-region in u's bits 28-31
 constexpr uint32_t SEG_CAP = 511;         // longest tile the per-wave register sort takes (8 keys per lane);
                                           // SEG_CAP + 1 is a multiple of the LPT bucket width (seg_block)
 constexpr uint32_t SEG_BLOCK_CAP = 2048;  // longest tile one workgroup sorts (4 waves x 512 keys); longer: chunks
@@ -192,7 +194,8 @@ struct BinningState {
     uint32_t *keys_sorted; // radix path: R tile ids of the sorted instances
     SortScratch sort;      // radix path: tile sort (R keys); its final value buffer is sorted_u
     unsigned long long *bk_keys;  // bucket path: R keys (depth << 32 | u) bucketed by tile
-    unsigned long long *bk_keys2; // bucket path: R, chunk-sorted keys of tiles longer than SEG_BLOCK_CAP
+    unsigned long long *bk_keys2; // bucket path: R, the region scatter's keys grouped by region, then the chunk-sorted
+                                  //    keys of tiles longer than SEG_BLOCK_CAP (seg_huge)
     // segmented backward (small images, num_tiles <= SEG_MAX_TILES; else null): the forward's per-pixel checkpoints
     // at every K-th instance of a tile (CK_FLOATS each: T, then the colour / inverse-depth sums so far), tile t's
     // checkpoint j (before instance (j + 1) K) at index ranges[t].x / K + t + j; and the backward's work list
@@ -252,7 +255,8 @@ struct ImageState {
     uint32_t *bk_hist;       // BK_MAX_BLOCKS x T count matrix (empty above BK_MAX_TILES)
     uint32_t *bk_hist_pre;   // its column prefixes (a separate array: the counts stay readable for the look-back's
                              // fallback while later column workgroups run)
-    uint32_t *bk_tile_cnt;   // T
+    uint32_t *bk_tile_next;  // T: tile starts, advanced by the region partition's slot atomics
+    uint32_t *bk_reg_start;  // T / BK_REGION + 2: region starts
     uint32_t *bk_tile_start; // T + 1
     uint32_t *bk_long_list;  // 2 x (T + 1): tiles of (SEG_CAP, SEG_BLOCK_CAP] instances, longer tiles
     uint32_t *bk_tie_list;   // T + 1: tiles whose 32-bit proxy-key sort did not converge
@@ -292,7 +296,8 @@ inline size_t carve_image(char *base, int W, int H, ImageState &im) {
     const size_t nt = (size_t)gx * gy;
     im.bk_hist = c.take<uint32_t>((nt <= BK_MAX_TILES ? (size_t)BK_MAX_BLOCKS * nt : 0) + 1);
     im.bk_hist_pre = c.take<uint32_t>((nt <= BK_MAX_TILES ? (size_t)BK_MAX_BLOCKS * nt : 0) + 1);
-    im.bk_tile_cnt = c.take<uint32_t>(nt + 1);
+    im.bk_tile_next = c.take<uint32_t>(nt + 1);
+    im.bk_reg_start = c.take<uint32_t>(nt / BK_REGION + 2);
     im.bk_tile_start = c.take<uint32_t>(nt + 1);
     im.bk_long_list = c.take<uint32_t>(2 * (nt + 1));
     im.bk_tie_list = c.take<uint32_t>(nt + 1);

@@ -88,6 +88,7 @@ void launch_identify_ranges16(hipStream_t s, const uint16_t *keys_sorted, uint32
 // ---- bucket binning (gsr_bin.hip) ----
 struct BucketParams {
     uint32_t P, T, nb, gper;  // Gaussians, tiles, walk blocks, Gaussians per block
+    uint32_t R;               // instances (scatter; the region partition's grid)
     const uint32_t *nbig;     // big-Gaussian count (device word written by the preprocess)
     int gx;
     const uint32_t *tiles, *depth_key, *big_list;
@@ -96,7 +97,7 @@ struct BucketParams {
     const uint4 *exp_rec;
     uint32_t *hist;        // nb x T counts (the count pass writes them; read-only for the column pass)
     uint32_t *hist_pre;    // nb x T column prefixes (column pass), seeding the scatter's bucket slots
-    uint32_t *tile_cnt;    // T
+    uint32_t *tile_next;   // T: the tiles' starts (column pass), then the region partition's next free slots (atomics)
     uint32_t *tile_start;  // T + 1
     uint2 *ranges;         // T
     uint32_t *long_list;   // 2 x (T + 1): tiles of (SEG_CAP, SEG_BLOCK_CAP] instances, longer tiles
@@ -111,6 +112,11 @@ struct BucketParams {
     uint32_t *inv;         // R: reset to INV_NONE beside inst_gid (the forward composite fills it)
     uint32_t *lpt_bcnt;    // 256: cleared by the column pass (the forward's backward-LPT bucket counts)
     unsigned long long *keys;  // R: depth << 32 | u, bucketed by tile
+    // region scatter (keys_reg != null; R <= 2^28): the scatter writes each key into its tile's REGION (BK_REGION
+    // consecutive tile ids) with the tile's index in the region in bits 28-31 of u (BK_REG_SHIFT), and
+    // bk_partition_kernel then moves the keys of each region into their tile buckets (keys), without those bits
+    unsigned long long *keys_reg;  // R, or null
+    uint32_t *reg_start;           // T / BK_REGION + 2: region starts (tile_start of each region's first tile), column pass
     uint32_t *inst_gid;    // R
     uint32_t *order;       // scatter: an extra workgroup writes the forward LPT order here (or null: none)
     int lpt_shift;
