@@ -20,6 +20,7 @@ struct CullIn {
     int rx, ry, rw;   // rect origin and width (tiles)
     uint32_t depth;   // float bits of the view depth
     bool need;        // cull the rect's tiles cooperatively
+    bool vis;         // rendered (radius > 0): its colour is needed, even when culling leaves no tile
 };
 
 // Projection, conic, radius, SH colour and render records of one Gaussian.  Returns the area of its tile
@@ -87,6 +88,7 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
     const uint32_t area = (uint32_t)((rmax.x - rmin.x) * (rmax.y - rmin.y));
     if (area == 0) return 0u;
 
+    ci.vis = true;
     const float opacity = opacity_in * hscale;
     float3 rgb = make_float3(0.f, 0.f, 0.f);
     uint8_t clamp_bits = 0;
@@ -140,6 +142,38 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
     return tarea;
 }
 
+// The colour of Gaussian i (one the projection kept) from its coefficient row sh, with its direction Jacobian: the
+// expressions of preprocess_gaussian's inline colour, so records, clamp bits and Jacobian are bitwise those of the
+// fused kernel whichever kernel runs it (the colour kernel of a split preprocess, or the late colour phase).
+template <int DEG>
+__device__ __forceinline__ void color_finish(const PreprocessParams &p, int i, const float *sh) {
+#pragma clang fp contract(off)
+    const GeomState &g = p.g;
+    const float3 mean = load_f3(p.means3D, i);
+    const float3 campos = make_float3(p.campos[0], p.campos[1], p.campos[2]);
+    float3 dir = mean - campos;
+    const float len = sqrtf(dot3(dir, dir));
+    dir = make_float3(dir.x / len, dir.y / len, dir.z / len);
+    float3 rgb;
+    if (DEG > 0) {
+        float3 jx, jy, jz;
+        rgb = sh_eval_jac<DEG>(sh, dir, jx, jy, jz);
+        const size_t n = (size_t)p.P;
+        float *J = g.sh_jac + i;
+        J[0] = jx.x; J[n] = jx.y; J[2 * n] = jx.z;
+        J[3 * n] = jy.x; J[4 * n] = jy.y; J[5 * n] = jy.z;
+        J[6 * n] = jz.x; J[7 * n] = jz.y; J[8 * n] = jz.z;
+    } else {
+        rgb = sh_eval<0>(sh, dir);
+    }
+    rgb = sh_offset(rgb);
+    const uint8_t clamp_bits = (rgb.x < 0.f ? 1 : 0) | (rgb.y < 0.f ? 2 : 0) | (rgb.z < 0.f ? 4 : 0);
+    rgb = make_float3(fmaxf(rgb.x, 0.f), fmaxf(rgb.y, 0.f), fmaxf(rgb.z, 0.f));
+    *reinterpret_cast<float2 *>(&g.rec[i].b.z) = make_float2(rgb.x, rgb.y);
+    g.rec[i].c.x = rgb.z;
+    g.clamped[i] = clamp_bits;
+}
+
 // Exact tile culling is balanced across the wave: the (Gaussian, tile) pairs of all 64 lanes' rects are
 // enumerated jointly (prefix sum of the rect areas, each lane takes every 64th pair, owner found by marks and a
 // max-scan), so a wave costs ceil(sum of areas / 64) tile tests instead of its largest rect.
@@ -155,19 +189,37 @@ struct PreCullLds {
     unsigned long long mask[64];
     int own[64];    // lane whose rect's pair run starts at this pair of the step, else -1
 };
+// Late colour phase (PRE_LATE): after the culling a wave's LDS slice holds 32 coefficient rows at a time (a padded
+// 52-float stride: the lanes' 16-B row reads fall in distinct banks)
+constexpr int PRE_SH_STRIDE = 52;
+union PreLds {
+    PreCullLds cull;
+    float sh[32 * PRE_SH_STRIDE];
+};
+enum PreMode : int { PRE_FUSED = 0, PRE_SPLIT = 1, PRE_LATE = 2 };
 #ifndef GSR_PRE_SPLIT_MINW
 #define GSR_PRE_SPLIT_MINW 7  // split (no colour): 70 VGPRs, 7 waves per SIMD (asking for 8 does not get under 64)
 #endif
-template <bool SPLIT>
-__global__ __launch_bounds__(256, SPLIT ? GSR_PRE_SPLIT_MINW : GSR_PRE_MINW) void preprocess_kernel(PreprocessParams p) {
-    __shared__ PreCullLds s_lds[4];
+__device__ __forceinline__ void publish_total(const PreprocessParams &p);
+
+// MODE: PRE_FUSED (colour inside preprocess_gaussian, each lane reading its own 192-B coefficient row), PRE_SPLIT (colour
+// left to preprocess_color_kernel), PRE_LATE (colour after the culling: the wave stages 32 rows at a time into LDS with
+// coalesced 16-B loads, each lane then reads its row from LDS).  Per lane, 64 strided 192-B rows per wave cycle each
+// load instruction over 96 cache lines, which the waves of a CU re-fetch from L2; the staged loads read every line once.
+// LATE_MINW: waves per SIMD the late-colour kernel is built for (4: 100 VGPRs; 5: 96 + a 20-B spill; 6: 80 + 92 B).
+template <int MODE, int LATE_MINW = 4>
+__global__ __launch_bounds__(256, MODE == PRE_SPLIT ? GSR_PRE_SPLIT_MINW : MODE == PRE_LATE ? LATE_MINW : GSR_PRE_MINW)
+void preprocess_kernel(PreprocessParams p) {
+    constexpr bool SPLIT = MODE != PRE_FUSED;  // colour not inside preprocess_gaussian
+    __shared__ PreLds s_lds[4];
     __shared__ uint32_t s_w[4];
     const uint32_t bid = blockIdx.x;
     const int i = (int)bid * 256 + threadIdx.x;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    PreCullLds &L = s_lds[w];
+    PreCullLds &L = s_lds[w].cull;
     CullIn ci;
     ci.need = false;
+    ci.vis = false;
     const uint32_t area = i < p.P ? preprocess_gaussian<SPLIT>(p, i, ci) : 0u;
     const uint32_t need_area = ci.need ? area : 0u;
     const uint32_t incl = wave_inclusive_scan(need_area, lane);
@@ -258,13 +310,47 @@ __global__ __launch_bounds__(256, SPLIT ? GSR_PRE_SPLIT_MINW : GSR_PRE_MINW) voi
             s_last = atomicAdd(&p.g.counters[CNT_PRE_DONE], 1u) == gridDim.x - 1;
         }
     }
-    if (!p.host_words) return;
-    __syncthreads();
-    if (!s_last) return;
-    // The last workgroup publishes {instance total lo, hi, big count, seq} to pinned host memory in ONE 16-B store
-    // (the host reads it with one 16-B load and trusts it when the sequence word matches), so no release fence is
-    // needed: a system-scope release writes back the L2 first and delayed the host's view by ~35 us.
-    if (threadIdx.x >= 64) return;
+    if (p.host_words) {
+        __syncthreads();
+        if (s_last && threadIdx.x < 64) publish_total(p);
+    }
+    if constexpr (MODE == PRE_LATE) {  // the colours, after the total is out (the host's wait does not include them)
+        const bool need = ci.vis;  // every rendered Gaussian, as the fused colour (a culled rect's too)
+        float *sw = s_lds[w].sh;
+        const int g0w = (int)bid * 256 + w * 64;
+        for (int h = 0; h < 2; h++) {  // wave-uniform
+            const int gh = g0w + 32 * h;  // first Gaussian of this half
+            if (__ballot(need && (lane >> 5) == h) == 0) continue;
+            const float4 *src = reinterpret_cast<const float4 *>(p.shs) + (size_t)gh * 12;
+            float4 v[6];
+#pragma unroll
+            for (int q = 0; q < 6; q++) {  // 32 rows = 384 float4, 6 per lane, coalesced
+                const int f = q * 64 + lane;
+                v[q] = gh + f / 12 < p.P ? src[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            wave_lds_sync();  // the slice's previous readers (culling state, previous half) are done
+#pragma unroll
+            for (int q = 0; q < 6; q++) {
+                const int f = q * 64 + lane, row = f / 12;
+                *reinterpret_cast<float4 *>(sw + row * PRE_SH_STRIDE + (f - row * 12) * 4) = v[q];
+            }
+            wave_lds_sync();
+            if (need && (lane >> 5) == h) {
+                const float *row = sw + (lane & 31) * PRE_SH_STRIDE;
+                switch (p.D) {
+                    case 1: color_finish<1>(p, i, row); break;
+                    case 2: color_finish<2>(p, i, row); break;
+                    default: color_finish<3>(p, i, row); break;
+                }
+            }
+        }
+    }
+}
+
+// The last preprocess workgroup publishes {instance total lo, hi, big count, seq} to pinned host memory in ONE 16-B
+// store (the host reads it with one 16-B load and trusts it when the sequence word matches), so no release fence is
+// needed: a system-scope release writes back the L2 first and delayed the host's view by ~35 us.  Threads 0-63.
+__device__ __forceinline__ void publish_total(const PreprocessParams &p) {
     const unsigned long long part = __hip_atomic_load(
         reinterpret_cast<unsigned long long *>(p.g.counters + CNT_PARTIALS) + threadIdx.x, __ATOMIC_RELAXED,
         __HIP_MEMORY_SCOPE_AGENT);  // CNT_NPART == 64: one partial per lane
@@ -292,8 +378,11 @@ __global__ __launch_bounds__(256, SPLIT ? GSR_PRE_SPLIT_MINW : GSR_PRE_MINW) voi
 
 void launch_preprocess(hipStream_t s, const PreprocessParams &p) {
     if (p.P <= 0) return;
-    if (p.split) preprocess_kernel<true><<<div_up(p.P, 256), 256, 0, s>>>(p);
-    else preprocess_kernel<false><<<div_up(p.P, 256), 256, 0, s>>>(p);
+    if (p.split) preprocess_kernel<PRE_SPLIT><<<div_up(p.P, 256), 256, 0, s>>>(p);
+    else if (p.late && tuning("pre_late_minw", 4) >= 6) preprocess_kernel<PRE_LATE, 6><<<div_up(p.P, 256), 256, 0, s>>>(p);
+    else if (p.late && tuning("pre_late_minw", 4) == 5) preprocess_kernel<PRE_LATE, 5><<<div_up(p.P, 256), 256, 0, s>>>(p);
+    else if (p.late) preprocess_kernel<PRE_LATE, 4><<<div_up(p.P, 256), 256, 0, s>>>(p);
+    else preprocess_kernel<PRE_FUSED><<<div_up(p.P, 256), 256, 0, s>>>(p);
 }
 
 // The colour half of a split preprocess: one thread per Gaussian the projection kept (radii != 0, exactly the ones
@@ -303,34 +392,9 @@ void launch_preprocess(hipStream_t s, const PreprocessParams &p) {
 // the GPU would otherwise wait for the host's readback of the instance total.
 template <int DEG>
 __global__ __launch_bounds__(256) void preprocess_color_kernel(PreprocessParams p) {
-#pragma clang fp contract(off)
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= p.P || p.radii[i] == 0) return;
-    const GeomState &g = p.g;
-    const float3 mean = load_f3(p.means3D, i);
-    const float3 campos = make_float3(p.campos[0], p.campos[1], p.campos[2]);
-    float3 dir = mean - campos;
-    const float len = sqrtf(dot3(dir, dir));
-    dir = make_float3(dir.x / len, dir.y / len, dir.z / len);
-    const float *sh = p.shs + (size_t)i * p.M * 3;
-    float3 rgb;
-    if (DEG > 0) {
-        float3 jx, jy, jz;
-        rgb = sh_eval_jac<DEG>(sh, dir, jx, jy, jz);
-        const size_t n = (size_t)p.P;
-        float *J = g.sh_jac + i;
-        J[0] = jx.x; J[n] = jx.y; J[2 * n] = jx.z;
-        J[3 * n] = jy.x; J[4 * n] = jy.y; J[5 * n] = jy.z;
-        J[6 * n] = jz.x; J[7 * n] = jz.y; J[8 * n] = jz.z;
-    } else {
-        rgb = sh_eval<0>(sh, dir);
-    }
-    rgb = sh_offset(rgb);
-    const uint8_t clamp_bits = (rgb.x < 0.f ? 1 : 0) | (rgb.y < 0.f ? 2 : 0) | (rgb.z < 0.f ? 4 : 0);
-    rgb = make_float3(fmaxf(rgb.x, 0.f), fmaxf(rgb.y, 0.f), fmaxf(rgb.z, 0.f));
-    *reinterpret_cast<float2 *>(&g.rec[i].b.z) = make_float2(rgb.x, rgb.y);
-    g.rec[i].c.x = rgb.z;
-    g.clamped[i] = clamp_bits;
+    color_finish<DEG>(p, i, p.shs + (size_t)i * p.M * 3);
 }
 
 void launch_preprocess_color(hipStream_t s, const PreprocessParams &p) {

@@ -64,6 +64,7 @@ struct PreprocessParams {
     uint32_t *host_words;
     uint32_t seq;
     int split = 0;  // colour left to launch_preprocess_color (SH colours only)
+    int late = 0;   // colour evaluated at the end of the preprocess from LDS-staged coefficient rows (M = 16, 16-B aligned)
     int depth_range = 0;  // publish the kept depth keys' range with the instance total (relative depth sort)
 };
 void launch_preprocess(hipStream_t s, const PreprocessParams &p);

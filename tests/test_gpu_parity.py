@@ -798,22 +798,20 @@ def test_prefix_binning_is_bitwise_the_full_sort(gpu_device, n, k, dup):
         assert np.any((b["tile_sorted"] > 64) & (nt > b["tile_sorted"]))  # walks extended their prefix
 
 
-@pytest.mark.parametrize("deg,bucket", [(3, 1), (2, 1), (1, 0), (0, 1)])
-def test_split_colour_preprocess_is_bitwise_the_fused_one(gpu_device, deg, bucket):
-    """The SH colour evaluated by its own kernel behind the bucket count pass ("pre_split" 1) gives bitwise
-    the records, outputs and gradients of the fused preprocess (colour inside the projection kernel)."""
+@pytest.mark.parametrize("mode", ["split", "late4", "late6"])
+@pytest.mark.parametrize("deg,cdeg,bucket", [(3, 3, 1), (2, 3, 1), (1, 3, 0), (1, 1, 0), (0, 0, 1)])
+def test_split_colour_preprocess_is_bitwise_the_fused_one(gpu_device, deg, cdeg, bucket, mode):
+    """The SH colour evaluated by its own kernel behind the bucket count pass ("pre_split" 1), or at the end of the
+    preprocess from LDS-staged coefficient rows ("pre_late" 1, 16 coefficients; built for 4 or 6 waves per SIMD), gives bitwise the records, outputs and gradients of the fused preprocess (colour inside the projection)."""
+    knobs = {"split": dict(pre_split=1, pre_late=0), "late4": dict(pre_split=0, pre_late=1, pre_late_minw=4),
+             "late6": dict(pre_split=0, pre_late=1, pre_late_minw=6)}[mode]
     from gaussian_splatting_lightning_amd import _native
-    inp = scene_inputs(60_000, 640, 480, sh_degree=deg, seed=12 + deg)
+    inp = scene_inputs(60_000, 640, 480, sh_degree=deg, seed=12 + deg, coeff_degree=cdeg)
     dc, di = upstream(640, 480, 12 + deg)
-    try:
-        _native.set_tuning("bucket", bucket)
-        _native.set_tuning("pre_split", 0)
+    with _native.tuned(bucket=bucket, pre_split=0, pre_late=0):
         ref = run_hip(inp, gpu_device, dc, di)
-        _native.set_tuning("pre_split", 1)
+    with _native.tuned(bucket=bucket, **knobs):
         alt = run_hip(inp, gpu_device, dc, di)
-    finally:
-        _native.unset_tuning("bucket")
-        _native.unset_tuning("pre_split")
     a, b = hip_state_arrays(ref), hip_state_arrays(alt)
     for key in ("rec", "clamped", "ranges", "point_list", "n_contrib"):
         assert np.array_equal(a[key], b[key]), key
