@@ -492,7 +492,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     // 16-B aligned rows, degree > 0).  Measured slower (cfg 3 preprocess 0.105 -> 0.120 / 0.124 / 0.133 ms at 4 / 5 / 6
     // waves per SIMD, cfg 5 0.454 -> 0.533 ms: profiles/r4l_ab_late_cfg*.txt), so off by default
     pp.late = (!pp.split && a->shs && !a->colors_precomp && a->M == 16 && a->D > 0 &&
-               ((uintptr_t)a->shs & 15) == 0 && tuning("pre_late", 0)) ? 1 : 0;
+               ((uintptr_t)a->shs & 15) == 0) ? tuning("pre_late", 0) : 0;  // 2: late, rows read directly
     // the kept depth keys' range, for the radix path's relative depth sort: only where that sort can run (multi-kernel
     // depth sorts, P above the onesweep limit); else the range words stay empty and the sort takes its 32-bit keys
     const uint32_t os_max = (uint32_t)tuning("onesweep_max_n", 3 << 20);

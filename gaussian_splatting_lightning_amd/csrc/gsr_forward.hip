@@ -196,7 +196,7 @@ union PreLds {
     PreCullLds cull;
     float sh[32 * PRE_SH_STRIDE];
 };
-enum PreMode : int { PRE_FUSED = 0, PRE_SPLIT = 1, PRE_LATE = 2 };
+enum PreMode : int { PRE_FUSED = 0, PRE_SPLIT = 1, PRE_LATE = 2, PRE_LATE_DIRECT = 3 };
 #ifndef GSR_PRE_SPLIT_MINW
 #define GSR_PRE_SPLIT_MINW 7  // split (no colour): 70 VGPRs, 7 waves per SIMD (asking for 8 does not get under 64)
 #endif
@@ -207,8 +207,11 @@ __device__ __forceinline__ void publish_total(const PreprocessParams &p);
 // coalesced 16-B loads, each lane then reads its row from LDS).  Per lane, 64 strided 192-B rows per wave cycle each
 // load instruction over 96 cache lines, which the waves of a CU re-fetch from L2; the staged loads read every line once.
 // LATE_MINW: waves per SIMD the late-colour kernel is built for (4: 100 VGPRs; 5: 96 + a 20-B spill; 6: 80 + 92 B).
+// PRE_LATE_DIRECT: the late colour phase reading each lane's row straight from global memory (no staging): only the
+// register peak moves (the colour no longer overlaps the projection state).
 template <int MODE, int LATE_MINW = 4>
-__global__ __launch_bounds__(256, MODE == PRE_SPLIT ? GSR_PRE_SPLIT_MINW : MODE == PRE_LATE ? LATE_MINW : GSR_PRE_MINW)
+__global__ __launch_bounds__(256, MODE == PRE_SPLIT ? GSR_PRE_SPLIT_MINW
+                                  : (MODE == PRE_LATE || MODE == PRE_LATE_DIRECT) ? LATE_MINW : GSR_PRE_MINW)
 void preprocess_kernel(PreprocessParams p) {
     constexpr bool SPLIT = MODE != PRE_FUSED;  // colour not inside preprocess_gaussian
     __shared__ PreLds s_lds[4];
@@ -314,6 +317,16 @@ void preprocess_kernel(PreprocessParams p) {
         __syncthreads();
         if (s_last && threadIdx.x < 64) publish_total(p);
     }
+    if constexpr (MODE == PRE_LATE_DIRECT) {
+        if (ci.vis) {
+            const float *row = p.shs + (size_t)i * 48;
+            switch (p.D) {
+                case 1: color_finish<1>(p, i, row); break;
+                case 2: color_finish<2>(p, i, row); break;
+                default: color_finish<3>(p, i, row); break;
+            }
+        }
+    }
     if constexpr (MODE == PRE_LATE) {  // the colours, after the total is out (the host's wait does not include them)
         const bool need = ci.vis;  // every rendered Gaussian, as the fused colour (a culled rect's too)
         float *sw = s_lds[w].sh;
@@ -379,6 +392,11 @@ __device__ __forceinline__ void publish_total(const PreprocessParams &p) {
 void launch_preprocess(hipStream_t s, const PreprocessParams &p) {
     if (p.P <= 0) return;
     if (p.split) preprocess_kernel<PRE_SPLIT><<<div_up(p.P, 256), 256, 0, s>>>(p);
+    else if (p.late == 2 && tuning("pre_late_minw", 4) >= 6)
+        preprocess_kernel<PRE_LATE_DIRECT, 6><<<div_up(p.P, 256), 256, 0, s>>>(p);
+    else if (p.late == 2 && tuning("pre_late_minw", 4) == 5)
+        preprocess_kernel<PRE_LATE_DIRECT, 5><<<div_up(p.P, 256), 256, 0, s>>>(p);
+    else if (p.late == 2) preprocess_kernel<PRE_LATE_DIRECT, 4><<<div_up(p.P, 256), 256, 0, s>>>(p);
     else if (p.late && tuning("pre_late_minw", 4) >= 6) preprocess_kernel<PRE_LATE, 6><<<div_up(p.P, 256), 256, 0, s>>>(p);
     else if (p.late && tuning("pre_late_minw", 4) == 5) preprocess_kernel<PRE_LATE, 5><<<div_up(p.P, 256), 256, 0, s>>>(p);
     else if (p.late) preprocess_kernel<PRE_LATE, 4><<<div_up(p.P, 256), 256, 0, s>>>(p);
