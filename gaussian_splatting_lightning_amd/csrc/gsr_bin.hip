@@ -387,9 +387,13 @@ __global__ __launch_bounds__(PART_THREADS) void bk_partition_kernel(BucketParams
         const uint32_t i = (uint32_t)(q * PART_THREADS + tid);
         k[q] = i < n ? p.keys_reg[c0 + i] : 0ull;
     }
-    if (tid == 0) {  // the chunk's first and last regions: searches over the compact region starts (L2-resident)
-        s_nle[0] = bk_region_of(p.reg_start, 0, nr, c0);
-        s_nle[1] = bk_region_of(p.reg_start, 0, nr, c0 + n - 1);
+    if (tid < 64) {  // the chunk's first and last regions: 64-probe wave searches over the compact region starts
+        const uint32_t rlo = wave_last_le(p.reg_start, nr - 1, c0, tid);
+        const uint32_t rhi = wave_last_le(p.reg_start, nr - 1, c0 + n - 1, tid);
+        if (tid == 0) {
+            s_nle[0] = rlo;
+            s_nle[1] = rhi;
+        }
     }
     __syncthreads();
     const uint32_t rlo = s_nle[0], nreg = s_nle[1] - rlo + 1;  // regions rlo .. rlo + nreg - 1 hold the chunk

@@ -833,6 +833,27 @@ __device__ __forceinline__ uint32_t nth_set_bit(uint64_t m, uint32_t j) {
     }
     return c;
 }
+// Wave-cooperative search: last index r in [0, n] with off[r] <= u (off non-decreasing, off[0] <= u).
+// 64 probes per step, so ~log64(n) dependent global loads instead of log2(n).
+__device__ __forceinline__ uint32_t wave_last_le(const uint32_t *__restrict__ off, uint32_t n, uint32_t u,
+                                                 int lane) {
+    uint32_t lo = 0, hi = n;
+    while (hi - lo >= 64) {
+        const uint32_t step = (hi - lo) / 65;
+        const uint32_t st = step ? step : 1;
+        const uint32_t probe = lo + (uint32_t)(lane + 1) * st;
+        const bool pred = probe <= hi && off[probe] <= u;
+        const uint32_t c = (uint32_t)__popcll(__ballot(pred));
+        const uint32_t nlo = lo + c * st;
+        const uint32_t nhi = (c < 64) ? lo + (c + 1) * st - 1 : hi;
+        lo = nlo;
+        hi = nhi;
+    }
+    const uint32_t probe = lo + (uint32_t)lane;
+    const bool pred = probe <= hi && off[probe] <= u;
+    return lo + (uint32_t)__popcll(__ballot(pred)) - 1;
+}
+
 // Orders LDS writes before later LDS reads of other lanes of the SAME wave (no s_barrier).
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

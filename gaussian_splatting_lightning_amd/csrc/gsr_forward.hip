@@ -436,27 +436,6 @@ void launch_preprocess_color(hipStream_t s, const PreprocessParams &p) {
 constexpr int EXP_PER = 4;  // 1024 instances per block, 36 KB of LDS: 4 blocks/CU (cfg 5: 0.396 -> 0.380 ms; 2: 0.400)
 constexpr int EXP_TILE = 256 * EXP_PER;
 
-// Wave-cooperative search: last index r in [0, n] with off[r] <= u (off non-decreasing, off[0] <= u).
-// 64 probes per step, so ~log64(n) dependent global loads instead of log2(n).
-__device__ __forceinline__ uint32_t wave_last_le(const uint32_t *__restrict__ off, uint32_t n, uint32_t u,
-                                                 int lane) {
-    uint32_t lo = 0, hi = n;
-    while (hi - lo >= 64) {
-        const uint32_t step = (hi - lo) / 65;
-        const uint32_t st = step ? step : 1;
-        const uint32_t probe = lo + (uint32_t)(lane + 1) * st;
-        const bool pred = probe <= hi && off[probe] <= u;
-        const uint32_t c = (uint32_t)__popcll(__ballot(pred));
-        const uint32_t nlo = lo + c * st;
-        const uint32_t nhi = (c < 64) ? lo + (c + 1) * st - 1 : hi;
-        lo = nlo;
-        hi = nhi;
-    }
-    const uint32_t probe = lo + (uint32_t)lane;
-    const bool pred = probe <= hi && off[probe] <= u;
-    return lo + (uint32_t)__popcll(__ballot(pred)) - 1;
-}
-
 __global__ __launch_bounds__(256) void expand_kernel(ExpandParams p) {
     __shared__ uint32_t s_off[EXP_TILE + 2];
     __shared__ uint4 s_e[EXP_TILE + 1];     // expansion record: kept-tile mask lo, hi (0: all tiles), rmin, width
