@@ -36,6 +36,9 @@ def _hipcc() -> str:
 FILE_FLAGS = {
     "gsr_forward.hip": ["-fno-slp-vectorize"],
     "gsr_preprocess_bwd.hip": ["-fno-slp-vectorize"],
+    # render_bwd without its 25 packed ops: 0.319 / 0.323 -> 0.317 / 0.315 ms at cfg 3, 0.856 / 0.870 -> 0.851 / 0.848 ms
+    # at cfg 5 in two interleaved library A/Bs (profiles/r4o_lib_ab_noslp_cfg*.txt)
+    "gsr_backward.hip": ["-fno-slp-vectorize"],
 }
 
 
