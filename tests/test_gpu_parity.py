@@ -1035,12 +1035,14 @@ def test_inverse_permutation_marks_exactly_the_loaded_instances(gpu_device, W, H
     assert rest.any() and np.all(hs["inv"][rest] == 0xFFFFFFFF)
 
 
-@pytest.mark.parametrize("W,H,n,stress", [(1920, 1080, 300_000, 0.01), (320, 240, 20_000, 0.0), (1280, 720, 100_000, 0.05)])
+@pytest.mark.parametrize("W,H,n,stress", [(1920, 1080, 300_000, 0.01), (320, 240, 20_000, 0.0), (1280, 720, 100_000, 0.05),
+                                          (1920, 1080, 3_000, 0.0)])
 def test_region_scatter_is_bitwise_the_direct_scatter(gpu_device, W, H, n, stress):
     """The bucket scatter through 16-tile regions plus the partition pass ("bk_region" 2: always; 1, default: above
     4096 tiles) fills every tile
     bucket with exactly the instances of the direct scatter (order inside a bucket is free), so the sorted list,
-    ranges, outputs and gradients are bitwise the same -- whole tiles, row-strip parts, many big Gaussians."""
+    ranges, outputs and gradients are bitwise the same -- whole tiles, row-strip parts, many big Gaussians, and a sparse
+    scene whose partition chunks span more regions than their LDS bins (the per-key fallback)."""
     from gaussian_splatting_lightning_amd import _native
     inp = scene_inputs(n, W, H, sh_degree=3, seed=33, stress_fraction=stress)
     dc, di = upstream(W, H, 33)
