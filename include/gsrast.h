@@ -268,7 +268,9 @@ typedef struct gsr_state_layout {
     size_t geom_tiles, geom_order, geom_inst_off, geom_inst_start, geom_clamped; /* u32, u32, u32, u32, u8 */
     size_t geom_depth_key;    /* u32 float bits of each Gaussian's view depth (0xffffffff: not rendered) */
     size_t geom_expand_rec;   /* uint4 {kept-tile mask lo, hi, rmin.x | rmin.y << 16, rect width} (mask 0 = all) */
-    size_t bin_point_list, bin_inv, bin_keys_sorted;                  /* u32 per instance (bin_inv: unused, 0) */
+    size_t bin_point_list, bin_inv, bin_keys_sorted;                  /* u32 per instance (bin_inv: sorted position of
+                                                                         each instance the composite loaded, else
+                                                                         0xffffffff: the backward's row markers) */
     size_t bin_sorted_u, bin_inst_gid;                                /* u32 per instance */
     size_t img_final_T, img_n_contrib, img_ranges, img_tile_last;     /* f32/u32 per pixel, uint2/u32 per tile */
     size_t img_tile_loaded;                                           /* u32 per tile */
