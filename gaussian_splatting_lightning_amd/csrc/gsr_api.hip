@@ -510,7 +510,13 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
         bp.P = (uint32_t)P; bp.T = T; bp.gx = gx; bp.nbig = g.counters + CNT_BIG;
         bp.nb = std::max(1u, std::min({(uint32_t)tuning("bk_blocks", 256), BK_MAX_BLOCKS, div_up(P, 1024)}));
         bp.gper = div_up(div_up(P, bp.nb), 256) * 256;  // whole preprocess blocks
-        bp.nb = div_up(P, bp.gper);
+        bp.nr = div_up(P, bp.gper);
+        // extra walk blocks for the big rects (used only when the device's big-Gaussian count exceeds nr: bk_walk_blocks);
+        // the block count is fixed here, before that count is read back.  2000 sparse-scene Gaussians at 1080p ran their
+        // big rects on 2 blocks (count + scatter walks 220 + 310 us).  Only below half of that count of
+        // range blocks: at cfg 3 (245 range blocks) 11 extra blocks measured +10 us of scatter (profiles/r4s_*)
+        const uint32_t big_blocks = std::min((uint32_t)tuning("bk_big_blocks", 256), BK_MAX_BLOCKS);
+        bp.nb = 2 * bp.nr < big_blocks ? big_blocks : bp.nr;
         bp.tiles = g.tiles; bp.inst_start = g.inst_start; bp.block_sums = g.block_sums; bp.depth_key = g.depth_key;
         bp.big_list = g.big_list; bp.exp_rec = g.exp_rec;
         bp.hist = im.bk_hist; bp.hist_pre = im.bk_hist_pre; bp.tile_next = im.bk_tile_next; bp.reg_start = im.bk_reg_start; bp.tile_start = im.bk_tile_start; bp.ranges = im.ranges;

@@ -80,6 +80,14 @@ __device__ void bk_instance_offsets(const BucketParams &p, uint32_t g_lo, uint32
     if (g_hi == p.P && tid == 0) p.inst_start[p.P] = base;
 }
 
+// The walk blocks in use: the range blocks, plus extra blocks (launched up to p.nb) when there are more big Gaussians
+// than range blocks, so a few Gaussians with large footprints are not walked by a handful of workgroups.  Read from
+// the device count by all three passes, so they agree.
+__device__ __forceinline__ uint32_t bk_walk_blocks(const BucketParams &p) {
+    const uint32_t nbig = *p.nbig;
+    return nbig > p.nr ? min(p.nb, nbig) : p.nr;
+}
+
 template <bool SCATTER, int BKW>  // BKW: waves per workgroup
 __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
     extern __shared__ uint32_t s_tab[];   // T entries: tile counts (count) / next free bucket slot (scatter)
@@ -93,6 +101,8 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
         lpt_order_block(p.ranges, nullptr, 0, (int)T, p.lpt_shift, p.order, reinterpret_cast<uint32_t *>(&s_own[0][0]));
         return;
     }
+    const uint32_t nbw = bk_walk_blocks(p);
+    if (b >= nbw) return;  // uniform: a block the big rects do not need (its count row is never read)
     const bool reg = SCATTER && p.keys_reg != nullptr;  // region scatter (uniform)
     if (SCATTER && reg) {
         // region r's next free slot for this block: the region's first tile start plus this block's column prefixes of
@@ -112,8 +122,8 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
         for (uint32_t t = tid; t < T; t += 64 * BKW) s_tab[t] = 0u;
     }
     s_own[w][lane] = -1;
-    const uint32_t g_lo = b * p.gper, g_hi = min(p.P, g_lo + p.gper);
-    if (!SCATTER) bk_instance_offsets<BKW>(p, g_lo, g_hi, reinterpret_cast<uint32_t *>(&s_aux[0][0]));
+    const uint32_t g_lo = min(p.P, b * p.gper), g_hi = min(p.P, g_lo + p.gper);  // empty above the range blocks
+    if (!SCATTER && b < p.nr) bk_instance_offsets<BKW>(p, g_lo, g_hi, reinterpret_cast<uint32_t *>(&s_aux[0][0]));
     __syncthreads();
     uint32_t g = g_lo + (uint32_t)w * 64 + lane;
     uint32_t n_kept = 0, n_u = 0, n_dep = 0;
@@ -184,7 +194,7 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
         wave_lds_sync();
     }
     const uint32_t nbig = *p.nbig;
-    for (uint32_t bi = b; bi < nbig; bi += p.nb) {
+    for (uint32_t bi = b; bi < nbig; bi += nbw) {
         const uint32_t gb = p.big_list[bi];
         const uint4 e = p.exp_rec[gb];
         const uint32_t area = p.tiles[gb];
@@ -254,7 +264,7 @@ __global__ __launch_bounds__(64 * CW) void bk_columns_kernel(BucketParams p) {
     __shared__ unsigned long long s_excl;
     const uint32_t *__restrict__ hist = p.hist;
     uint32_t *__restrict__ hist_pre = p.hist_pre;
-    const uint32_t nb = p.nb, T = p.T;
+    const uint32_t nb = bk_walk_blocks(p), T = p.T;  // the count rows the walk wrote
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     if (tid == 0) s_bid = atomicAdd(p.ticket, 1u);
     if (blockIdx.x == 0 && tid < 256 && p.lpt_bcnt) p.lpt_bcnt[tid] = 0u;

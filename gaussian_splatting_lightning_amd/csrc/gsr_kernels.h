@@ -88,7 +88,10 @@ void launch_identify_ranges16(hipStream_t s, const uint16_t *keys_sorted, uint32
 
 // ---- bucket binning (gsr_bin.hip) ----
 struct BucketParams {
-    uint32_t P, T, nb, gper;  // Gaussians, tiles, walk blocks, Gaussians per block
+    uint32_t P, T, nb, gper;  // Gaussians, tiles, walk blocks launched, Gaussians per block
+    // walk blocks owning a Gaussian range (nr <= nb).  Blocks nr.. only walk big rects: bk_walk_blocks() is the count
+    // the passes use, nr raised to min(nb, big-Gaussian count); the blocks above it exit and their rows are not read
+    uint32_t nr;
     uint32_t R;               // instances (scatter; the region partition's grid)
     const uint32_t *nbig;     // big-Gaussian count (device word written by the preprocess)
     int gx;

@@ -1057,3 +1057,24 @@ def test_region_scatter_is_bitwise_the_direct_scatter(gpu_device, W, H, n, stres
         assert np.array_equal(ref[key], alt[key]), key
     for key in GRADS:
         assert np.array_equal(ref["grads"][key], alt["grads"][key]), key
+
+
+@pytest.mark.parametrize("W,H,n,stress", [(1920, 1080, 2_000, 0.3), (320, 240, 1_500, 0.5), (1280, 720, 40_000, 0.05)])
+def test_big_rect_walk_blocks_are_bitwise_the_range_blocks(gpu_device, W, H, n, stress):
+    """Few Gaussians with large footprints: the bucket walks add blocks that only walk big rects when the big-Gaussian
+    count exceeds the blocks owning Gaussian ranges ("bk_big_blocks", default 256; 0 = the range blocks only).  Every
+    tile bucket gets the same instances, so the sorted list, ranges, outputs and gradients are bitwise the same."""
+    from gaussian_splatting_lightning_amd import _native
+    inp = scene_inputs(n, W, H, sh_degree=3, seed=41, stress_fraction=stress)
+    dc, di = upstream(W, H, 41)
+    with _native.tuned(bk_big_blocks=0):
+        ref = run_hip(inp, gpu_device, dc, di)
+    alt = run_hip(inp, gpu_device, dc, di)
+    a, b = hip_state_arrays(ref), hip_state_arrays(alt)
+    assert a["num_rendered"] == b["num_rendered"] > 0
+    for key in ("point_list", "ranges", "tiles", "n_contrib", "tile_last", "tile_loaded", "inv"):
+        assert np.array_equal(a[key], b[key]), key
+    for key in ("color", "invdepth", "radii"):
+        assert np.array_equal(ref[key], alt[key]), key
+    for key in GRADS:
+        assert np.array_equal(ref["grads"][key], alt["grads"][key]), key
