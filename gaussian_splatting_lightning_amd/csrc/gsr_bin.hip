@@ -365,8 +365,14 @@ __global__ __launch_bounds__(64 * CW) void bk_columns_kernel(BucketParams p) {
 // per non-empty bin for its slots in the tile's bucket (tile_next), then each bin's run stored contiguously.  A chunk
 // over more than PART_MAXR regions (sparse ones) sends its keys one by one.  Bucket order is arbitrary (the per-tile
 // sorts make it irrelevant).
-constexpr int PART_THREADS = 256;
-constexpr int PART_ITEMS = 8;
+#ifndef GSR_PART_THREADS  // chunk shape (overridable for library A/B builds, tools/build_variant.py)
+#define GSR_PART_THREADS 256
+#endif
+#ifndef GSR_PART_ITEMS
+#define GSR_PART_ITEMS 4
+#endif
+constexpr int PART_THREADS = GSR_PART_THREADS;
+constexpr int PART_ITEMS = GSR_PART_ITEMS;
 constexpr uint32_t PART_CHUNK = PART_THREADS * PART_ITEMS;
 constexpr uint32_t PART_MAXR = 32;
 constexpr uint32_t PART_BINS = PART_MAXR * BK_REGION;
