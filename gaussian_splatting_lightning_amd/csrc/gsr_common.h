@@ -93,8 +93,11 @@ inline void carve_sort(Carver &c, SortScratch &s, uint32_t n, bool need_v0) {
 constexpr uint32_t BK_MAX_TILES = 32768;  // 128 KB of LDS counters (4K images: 32400 tiles)
 constexpr uint32_t BK_MAX_BLOCKS = 512;   // rows of the count matrix (carved for the maximum)
 constexpr uint32_t BK_MAX_MEAN = 1024;    // default path choice: mean instances per tile up to this
-constexpr uint32_t BK_REGION = 16;        // tiles per region of the region scatter (consecutive tile ids)
-constexpr int BK_REG_SHIFT = 28;          // the region scatter carries a key's tile-in-region in u's bits 28-31
+#ifndef GSR_BK_REGION_LOG2  // overridable for library A/B builds (tools/build_variant.py)
+#define GSR_BK_REGION_LOG2 4
+#endif
+constexpr uint32_t BK_REGION = 1u << GSR_BK_REGION_LOG2;  // tiles per region of the region scatter (consecutive tile ids)
+constexpr int BK_REG_SHIFT = 32 - GSR_BK_REGION_LOG2;    // the region scatter carries a key's tile-in-region in u's top bits
 constexpr uint32_t SEG_CAP = 511;         // longest tile the per-wave register sort takes (8 keys per lane);
                                           // SEG_CAP + 1 is a multiple of the LPT bucket width (seg_block)
 constexpr uint32_t SEG_BLOCK_CAP = 2048;  // longest tile one workgroup sorts (4 waves x 512 keys); longer: chunks
