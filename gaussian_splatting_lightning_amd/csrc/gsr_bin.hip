@@ -374,8 +374,12 @@ __global__ __launch_bounds__(64 * CW) void bk_columns_kernel(BucketParams p) {
 constexpr int PART_THREADS = GSR_PART_THREADS;
 constexpr int PART_ITEMS = GSR_PART_ITEMS;
 constexpr uint32_t PART_CHUNK = PART_THREADS * PART_ITEMS;
-constexpr uint32_t PART_MAXR = 32;
+#ifndef GSR_PART_MAXR
+#define GSR_PART_MAXR 4
+#endif
+constexpr uint32_t PART_MAXR = GSR_PART_MAXR;
 constexpr uint32_t PART_BINS = PART_MAXR * BK_REGION;
+static_assert(PART_BINS % 64 == 0 && PART_BINS >= 64, "the bin scan gives each lane of one wave PART_BINS / 64 bins");
 // region of sorted position i: the last r < n with rs[r] <= i (rs non-decreasing, rs[0] <= i)
 __device__ __forceinline__ uint32_t bk_region_of(const uint32_t *rs, uint32_t lo, uint32_t n, uint32_t i) {
     uint32_t hi = n - 1;
