@@ -68,10 +68,14 @@ def parse():
     ap.add_argument("--no-stage-events", action="store_true", help="time without per-stage hipEvents")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"))
-    ap.add_argument("--exchange", default="compact", choices=("compact", "dense"),
-                    help="N>1 gradient exchange (gaussian_splatting_lightning_amd/multiview.py)")
-    ap.add_argument("--exchange-chunks", type=int, default=4,
-                    help="N>1: Gaussian chunks whose exchange overlaps the rest of the backward (1: after it)")
+    ap.add_argument("--exchange", default="auto", choices=("auto", "compact", "dense"),
+                    help="N>1 gradient exchange (gaussian_splatting_lightning_amd/multiview.py); auto: the cost model's "
+                         "choice (multiview.plan_exchange)")
+    ap.add_argument("--exchange-chunks", type=int, default=0,
+                    help="N>1: Gaussian chunks whose exchange overlaps the rest of the backward (1: after it; 0: the "
+                         "cost model's choice)")
+    ap.add_argument("--exchange-expand", default=None, choices=("chunk", "once"),
+                    help="compact exchange: SH expansion per chunk or once after the last gather (default: model)")
     ap.add_argument("--force-dist", action="store_true",
                     help="take the N>1 path (process group, RCCL exchange) even with one rank, e.g. under "
                          "torchrun --nproc-per-node 1")
@@ -123,12 +127,16 @@ def main():
         sh_degree=deg, campos=c.campos, prefiltered=False, debug=False, antialiasing=False)
     M = sc.shs.shape[1]
 
-    # Per-Gaussian gradient destinations + the cross-rank exchange (multiview.py): one view per rank; dense
-    # all-reduce at N=1 (nothing to exchange), compact SH exchange at N>1 unless --exchange dense.
-    mode = args.exchange if distributed else "dense"
-    # N>1: the backward's per-Gaussian stage runs in --exchange-chunks Gaussian ranges and each range's collectives
-    # are issued as soon as it is enqueued (overlap with the rest of the backward); N=1: one chunk, nothing to send
-    red = ViewGradReducer(n, M, deg, dev, mode=mode, chunks=args.exchange_chunks if distributed else 1)
+    # Per-Gaussian gradient destinations + the cross-rank exchange (multiview.py): one view per rank.  N=1: dense
+    # destinations, one chunk, no collectives.  N>1 (or --force-dist): mode, chunk count and SH-expansion schedule
+    # from the cost model (multiview.plan_exchange) unless given; the backward's per-Gaussian stage runs in the
+    # chunks' Gaussian ranges and each range's collectives (one RCCL group) are issued as soon as it is enqueued.
+    if distributed:
+        red = ViewGradReducer(n, M, deg, dev, mode=args.exchange, chunks=args.exchange_chunks or None,
+                              expand=args.exchange_expand)
+    else:
+        red = ViewGradReducer(n, M, deg, dev, mode="dense", chunks=1)
+    mode = red.mode
     assert red.distributed == distributed
 
     def step():
@@ -338,13 +346,14 @@ def main():
         "warmup": args.warmup, "warmup_settle_s": SETTLE_S, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": cfg["desc"], "gaussians": n, "width": W, "height": H, "sh_degree": deg,
-                   "views_per_step": world, "parallelism": f"dp{world} (one view per GPU, RCCL gradient exchange: {mode}, "
-                                                  f"{red.chunks} overlapped chunk(s))",
+                   "views_per_step": world, "parallelism": f"dp{world} (one view per GPU, gradient exchange: "
+                                                  f"{red.describe() if distributed else 'none'})",
                    "instances_per_view": I, "sum_n_contrib": sum_contrib,
                    "stage_events": (f"timed steps: dominant kernel only, every {EVENT_EVERY}th step; stages_ms: "
                                     "separate untimed pass"
                                     if use_events else "none")},
-        **({"distributed": {"backend": dist.get_backend(), "world_size": world,
+        **({"distributed": {"backend": dist.get_backend(), "world_size": world, "exchange": red.describe(),
+                            "plan": red.plan,
                             "note": "process group initialised: every step ran the exchange's collectives"}}
            if distributed else {}),
         # also the contributing (pixel, Gaussian) pairs per second (this rank's sum(n_contrib) x N)

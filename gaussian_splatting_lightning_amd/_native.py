@@ -92,7 +92,8 @@ class StateLayout(ctypes.Structure):
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t)
 
 EXPORTED_SYMBOLS = (
-    "gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_sh_backward_views", "gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes",
+    "gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_sh_backward_views", "gsr_sh_backward_views_chunked",
+    "gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes",
     "gsr_image_buffer_bytes", "gsr_bwd_scratch_bytes", "gsr_set_profiling", "gsr_num_stages", "gsr_stage_name",
     "gsr_stage_times", "gsr_reset_stage_times", "gsr_last_error", "gsr_build_info", "gsr_state_layout_query",
     "gsr_set_tuning", "gsr_get_tuning", "gsr_ssim_num_partials", "gsr_ssim_forward", "gsr_ssim_backward", "gsr_adam_step", "gsr_sparse_adam_step",
@@ -124,6 +125,9 @@ def load(path: str | None = None):
     lib.gsr_sh_backward_views.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _fp, _fp, _fp, _fp,
                                           ctypes.c_void_p]
     lib.gsr_sh_backward_views.restype = ctypes.c_int
+    lib.gsr_sh_backward_views_chunked.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                  ctypes.c_int64, _fp, _fp, _fp, _fp, ctypes.c_void_p]
+    lib.gsr_sh_backward_views_chunked.restype = ctypes.c_int
     lib.gsr_adam_step.argtypes = [ctypes.POINTER(AdamGroup), ctypes.c_int, ctypes.c_double, ctypes.c_double,
                                   ctypes.c_double, ctypes.c_void_p]
     lib.gsr_adam_step.restype = ctypes.c_int

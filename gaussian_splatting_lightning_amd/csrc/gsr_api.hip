@@ -871,18 +871,25 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     return GSR_OK;
 }
 
-int gsr_sh_backward_views(int P, int D, int M, int V, const float *means3D, const float *campos,
-                          const float *dL_dcolors_sh, float *dL_dsh, void *stream_ptr) {
+int gsr_sh_backward_views_chunked(int P, int D, int M, int V, int64_t chunk_len, const float *means3D,
+                                  const float *campos, const float *dL_dcolors_sh, float *dL_dsh, void *stream_ptr) {
     if (P < 0 || V < 0) return fail(GSR_ERR_ARG, "P and V must be >= 0");
     if (D < 0 || D > 3) return fail(GSR_ERR_ARG, "sh_degree must be in [0, 3]");
     if (M <= 0 || M > 16 || (D + 1) * (D + 1) > M)
         return fail(GSR_ERR_ARG, "M must hold (deg+1)^2 <= M <= 16 coefficients");
+    if (chunk_len < 0) return fail(GSR_ERR_ARG, "chunk_len must be >= 0");
     if (P == 0) return GSR_OK;
     if (!means3D || !dL_dsh || (V > 0 && (!campos || !dL_dcolors_sh))) return fail(GSR_ERR_ARG, "null argument");
     hipStream_t stream = (hipStream_t)stream_ptr;
     StreamDeviceGuard device_guard(stream);
-    GSR_STAGE(ST_SH_VIEWS, 0, launch_sh_backward_views(stream, P, D, M, V, means3D, campos, dL_dcolors_sh, dL_dsh));
+    const int L = (chunk_len == 0 || chunk_len >= P) ? P : (int)chunk_len;
+    GSR_STAGE(ST_SH_VIEWS, 0, launch_sh_backward_views(stream, P, D, M, V, L, means3D, campos, dL_dcolors_sh, dL_dsh));
     return GSR_OK;
+}
+
+int gsr_sh_backward_views(int P, int D, int M, int V, const float *means3D, const float *campos,
+                          const float *dL_dcolors_sh, float *dL_dsh, void *stream_ptr) {
+    return gsr_sh_backward_views_chunked(P, D, M, V, 0, means3D, campos, dL_dcolors_sh, dL_dsh, stream_ptr);
 }
 
 int gsr_adam_step(const gsr_adam_group *groups, int num_groups, double beta1, double beta2, double eps,

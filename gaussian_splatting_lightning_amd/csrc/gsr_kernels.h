@@ -246,8 +246,8 @@ struct PreprocessBwdParams {
 void launch_preprocess_bwd(hipStream_t s, const PreprocessBwdParams &p);
 
 // ---- multi-view SH gradient (gsr_views.hip) ----
-void launch_sh_backward_views(hipStream_t s, int P, int D, int M, int V, const float *means3D, const float *campos,
-                              const float *dcolors_sh, float *dsh);
+void launch_sh_backward_views(hipStream_t s, int P, int D, int M, int V, int chunk_len, const float *means3D,
+                              const float *campos, const float *dcolors_sh, float *dsh);
 
 // ---- fused Adam (gsr_adam.hip) ----
 constexpr int ADAM_MAX_GROUPS = 16;

@@ -13,8 +13,11 @@ namespace gsr {
 // M = 16 with a 16-B aligned output (STAGED): each half-wave's 32 rows are staged in LDS at a 52-float stride (as
 // preprocess_bwd's dL/dsh) and the wave stores them as coalesced float4s, not 12 stores per lane 192 B apart.
 constexpr int VIEWS_STRIDE = 52;
+// The factors are laid out chunk-major (the multi-view exchange gathers them per Gaussian chunk): chunk c holds
+// Gaussians [c L, min(P, (c+1) L)) as a (V, L_c, 3) block at offset c V L 3; L >= P is the plain (V, P, 3) array.
 template <int DEG, bool STAGED>
-__global__ __launch_bounds__(256) void sh_backward_views_kernel(int P, int M, int V, const float *__restrict__ means3D,
+__global__ __launch_bounds__(256) void sh_backward_views_kernel(int P, int M, int V, int L,
+                                                                const float *__restrict__ means3D,
                                                                 const float *__restrict__ campos,
                                                                 const float *__restrict__ dc,
                                                                 float *__restrict__ dsh) {
@@ -25,11 +28,13 @@ __global__ __launch_bounds__(256) void sh_backward_views_kernel(int P, int M, in
     const bool live = i < P;
     const int ii = live ? i : P - 1;
     const float mx = means3D[3 * ii], my = means3D[3 * ii + 1], mz = means3D[3 * ii + 2];
+    const int c = ii / L, g0 = c * L, Lc = min(L, P - g0);
+    const float *dchunk = dc + (size_t)g0 * V * 3 + (size_t)(ii - g0) * 3;
     float acc[3 * NB];
 #pragma unroll
     for (int k = 0; k < 3 * NB; k++) acc[k] = 0.f;
     for (int v = 0; v < V; v++) {
-        const float *d = dc + ((size_t)v * P + ii) * 3;
+        const float *d = dchunk + (size_t)v * Lc * 3;
         const float r = d[0], g = d[1], b = d[2];
         if (r == 0.f && g == 0.f && b == 0.f) continue;  // not rendered (or fully clamped) in view v
         const float dx = mx - campos[3 * v], dy = my - campos[3 * v + 1], dz = mz - campos[3 * v + 2];
@@ -87,12 +92,13 @@ __global__ __launch_bounds__(256) void sh_backward_views_kernel(int P, int M, in
     }
 }
 
-void launch_sh_backward_views(hipStream_t s, int P, int D, int M, int V, const float *means3D, const float *campos,
-                              const float *dcolors_sh, float *dsh) {
+void launch_sh_backward_views(hipStream_t s, int P, int D, int M, int V, int chunk_len, const float *means3D,
+                              const float *campos, const float *dcolors_sh, float *dsh) {
     if (P <= 0) return;
     const dim3 grid(div_up(P, 256)), block(256);
     const bool staged = M == 16 && (((uintptr_t)dsh) & 15) == 0 && tuning("views_staged", 1);
-#define GSR_VIEWS(D_, S_) sh_backward_views_kernel<D_, S_><<<grid, block, 0, s>>>(P, M, V, means3D, campos, dcolors_sh, dsh)
+    const int L = chunk_len <= 0 || chunk_len > P ? P : chunk_len;
+#define GSR_VIEWS(D_, S_) sh_backward_views_kernel<D_, S_><<<grid, block, 0, s>>>(P, M, V, L, means3D, campos, dcolors_sh, dsh)
     switch (D) {
         case 0: if (staged) GSR_VIEWS(0, true); else GSR_VIEWS(0, false); break;
         case 1: if (staged) GSR_VIEWS(1, true); else GSR_VIEWS(1, false); break;

@@ -16,18 +16,23 @@ Per step only the parameter gradients cross the links:
 ``dense``   one SUM all-reduce of the per-Gaussian gradient block [means3D 3 | scales 3 | rotations 4 | opacity 1 |
             shs 3M] floats per Gaussian (59 floats = 236 B at SH degree 3).
 ``compact`` the SH gradient of one view is rank one per Gaussian -- basis(dir_v) (x) dRGB_v -- so ranks
-            all-gather the 3-float factors dRGB_v (clamp-masked colour gradient) and their camera positions, and
-            each rank expands sum_v on the GPU (gsr_sh_backward_views).  The all-reduce carries the other 11 floats.
-            Per-rank ring traffic at 8 ranks and SH degree 3: 2*(7/8)*44 B + (7/8)*96 B = 161 B per Gaussian
-            instead of 2*(7/8)*236 B = 413 B.
+            all-gather the 3-float factors dRGB_v (clamp-masked colour gradient) and each rank expands sum_v on the
+            GPU (gsr_sh_backward_views_chunked).  The all-reduce carries the other 11 floats, plus one (world, 3)
+            block of camera positions (each rank writes its own row, zeros elsewhere: the sum is every rank's
+            campos, exactly), so no separate camera gather runs.  Per-rank ring traffic at 8 ranks and SH degree 3:
+            2*(7/8)*44 B + (7/8)*96 B = 161 B per Gaussian instead of 2*(7/8)*236 B = 413 B.
 
 Overlap with the backward (``chunks`` = K > 1): the Gaussians are split into K contiguous ranges and the
 gradient buffer is laid out chunk-major -- chunk c's block holds [means3D | scales | rotations | opacity (| shs)]
-of its Gaussians only -- so a chunk's exchange is ONE all-reduce (+ one all-gather of its colour factors).  The
-backward runs its per-Gaussian stage chunk by chunk (rasterizer.backward_chunked) and the exchange of chunk c is
-issued as soon as chunk c is enqueued; RCCL runs it on its own stream while the GPU computes chunk c + 1.  The SH
-expansions follow once each chunk's gather has arrived.  Results are bitwise those of K = 1: every element is the
-same sum of the same per-rank values (tests/test_multiview.py checks K = 1 against K = 4 on world_size 2).
+of its Gaussians only -- so a chunk's exchange is ONE all-reduce (+ one all-gather of its colour factors), issued
+as one RCCL group (ncclGroupStart/End through the process group's coalescing calls) as soon as chunk c is
+enqueued; RCCL runs it on its own stream while the GPU computes chunk c + 1.  The SH expansion runs per chunk as
+each group lands (``expand="chunk"``), or once over the chunk-major gather buffer after the last one
+(``expand="once"``).  Results are bitwise those of K = 1: every element is the same sum of the same per-rank values
+(tests/test_multiview.py checks K = 1 against K = 4 on world_size 2).
+
+``plan_exchange`` picks the mode, K and the expansion schedule from a cost model (measured per-Gaussian kernel
+times, the measured fixed cost of one collective group, an assumed xGMI bus bandwidth) and predicts the step.
 
 Both modes give the sum of the single-view gradients (fp32 summation order aside); tests/test_multiview.py
 checks them on world_size 2 with gloo, tests/test_gpu_parity.py checks the expansion kernel on the GPU.
@@ -43,10 +48,92 @@ from .rasterizer import sh_backward_views
 
 FIELDS_DENSE = ("means3D", "scales", "rotations", "opacities", "shs")
 FIELDS_COMPACT = ("means3D", "scales", "rotations", "opacities")
+NON_SH_FLOATS = 11  # means3D 3 + scales 3 + rotations 4 + opacity 1
+
+# Cost-model constants.  Kernel times are per 1e6 Gaussians at SH degree 3 on one MI355X (rocprofv3 kernel
+# averages at cfg 3); `group_ms` is the fixed cost of one collective group on a one-rank RCCL group
+# (launch + stream handoff, no data); the bus bandwidth is an ASSUMPTION (no 8-GPU node has run this code):
+# 7 xGMI links x 153 GB/s per direction at `bus_efficiency` of RCCL's ring/tree schedules.
+EXCHANGE_COSTS = dict(
+    pb_dense_ms=0.106,     # preprocess_bwd writing dL/dsh (192 B/G)
+    pb_compact_ms=0.088,   # preprocess_bwd writing the 12-B colour factor instead
+    exp_ms=0.040,          # gsr_sh_backward_views: 192 B/G written + means
+    exp_view_ms=0.003,     # + 12 B/G read per view
+    chunk_ms=0.004,        # per extra per-Gaussian-stage launch (launch gap + tail)
+    group_ms=0.012,        # one collective group, fixed
+    copy_GBps=4000.0,      # one-rank all-gather: RCCL copies input -> output on the device
+    link_GBps=153.0,
+    links=7,
+    bus_efficiency=0.6,
+)
+
+
+def exchange_bytes_per_gaussian(mode: str, world: int, M: int = 16) -> float:
+    """Per-rank bytes over the links per Gaussian for one step's exchange (ring algorithms: all-reduce 2(N-1)/N of
+    the buffer, all-gather (N-1)/N of the gathered output)."""
+    N = max(1, int(world))
+    if mode == "dense":
+        return 2.0 * (N - 1) / N * 4 * (NON_SH_FLOATS + 3 * M)
+    return 2.0 * (N - 1) / N * 4 * NON_SH_FLOATS + (N - 1) / N * 12.0 * N
+
+
+def simulate_exchange(n: int, world: int, mode: str, chunks: int, expand: str = "chunk", M: int = 16,
+                      costs: Optional[dict] = None) -> Dict[str, float]:
+    """Timeline of the backward's per-Gaussian stage + the exchange (ms after the compositing backward ends).
+
+    compute stream: K per-Gaussian chunks, then the SH expansions (compact), each after its chunk's group landed;
+    comm stream (RCCL): group c starts when chunk c is enqueued-and-computed and group c-1 is done."""
+    c = dict(EXCHANGE_COSTS, **(costs or {}))
+    scale = n / 1e6
+    K = max(1, int(chunks))
+    N = max(1, int(world))
+    pb = (c["pb_compact_ms"] if mode == "compact" else c["pb_dense_ms"]) * scale
+    bus = c["link_GBps"] * c["links"] * c["bus_efficiency"] * 1e9  # B/s
+    link_bytes = exchange_bytes_per_gaussian(mode, N, M) * n
+    comm = link_bytes / bus * 1e3 if N > 1 else 0.0
+    if N == 1 and mode == "compact":  # the one-rank all-gather is a device copy (read + write of 12 B/G)
+        comm += 24.0 * n / (c["copy_GBps"] * 1e9) * 1e3
+    t_chunk = [pb / K + (c["chunk_ms"] if k > 0 else 0.0) for k in range(K)]
+    comp_end = 0.0
+    comm_end = 0.0
+    group_end = []
+    for k in range(K):
+        comp_end += t_chunk[k]
+        start = max(comp_end, comm_end)
+        comm_end = start + c["group_ms"] + comm / K
+        group_end.append(comm_end)
+    t = comp_end
+    if mode == "compact":
+        exp = (c["exp_ms"] + c["exp_view_ms"] * N) * scale
+        if expand == "once":
+            t = max(t, group_end[-1]) + exp
+        else:
+            for k in range(K):
+                t = max(t, group_end[k]) + exp / K + (c["chunk_ms"] if k > 0 else 0.0)
+    end = max(t, comm_end)
+    return {"mode": mode, "chunks": K, "expand": expand, "per_gaussian_stage_ms": round(pb, 4),
+            "link_MB": round(link_bytes / 1e6, 1), "comm_ms": round(comm, 4), "end_ms": round(end, 4),
+            "exposed_ms": round(end - pb, 4)}
+
+
+def plan_exchange(n: int, world: int, M: int = 16, costs: Optional[dict] = None,
+                  modes=("compact", "dense"), chunk_options=(1, 2, 4, 8)) -> Dict[str, float]:
+    """The (mode, chunks, expand) with the smallest predicted end time (ties: fewer chunks, compact first)."""
+    best = None
+    for mode in modes:
+        for K in chunk_options:
+            if K > 1 and n < 256 * K:
+                continue
+            for expand in (("chunk", "once") if (mode == "compact" and K > 1) else ("once",)):
+                r = simulate_exchange(n, world, mode, K, expand, M, costs)
+                if best is None or r["end_ms"] < best["end_ms"] - 1e-6:
+                    best = r
+    return best
 
 
 def chunk_bounds(n: int, k: int, align: int = 256) -> List[Tuple[int, int]]:
-    """K contiguous Gaussian ranges covering [0, n), boundaries on multiples of `align` (whole preprocess blocks)."""
+    """K contiguous Gaussian ranges covering [0, n), boundaries on multiples of `align` (whole preprocess blocks).
+    Every range but the last has the same length (the chunk-major gather layout relies on it)."""
     k = max(1, int(k))
     step = -(-n // k)
     step = max(align, -(-step // align) * align)
@@ -75,18 +162,22 @@ class ViewGradReducer:
 
     With chunks == 1, ``backward_raw(..., out=red.backward_out(), ...)`` followed by ``red.reduce(means3D, campos)``
     is the same exchange without overlap.
+
+    mode="auto" / chunks=None take ``plan_exchange``'s choice for this world size.  coalesce (default: on for the
+    nccl backend) issues a chunk's all-gather and all-reduce as one RCCL group; sync_ops (default: on when there is
+    one chunk) issues them as blocking ops, which torch's RCCL process group enqueues on the current stream -- with
+    nothing to overlap, that saves the hand-off to the communication stream and back.
     """
 
     def __init__(self, n: int, M: int, sh_degree: int, device, mode: str = "compact", group=None,
                  world_size: Optional[int] = None,
-                 sh_views_fn: Optional[Callable[..., torch.Tensor]] = None, chunks: int = 1,
-                 distributed: Optional[bool] = None):
-        if mode not in ("dense", "compact"):
-            raise ValueError(f"mode must be 'dense' or 'compact', got {mode!r}")
+                 sh_views_fn: Optional[Callable[..., torch.Tensor]] = None, chunks: Optional[int] = 1,
+                 distributed: Optional[bool] = None, expand: Optional[str] = None,
+                 coalesce: Optional[bool] = None, sync_ops: Optional[bool] = None):
+        if mode not in ("dense", "compact", "auto"):
+            raise ValueError(f"mode must be 'dense', 'compact' or 'auto', got {mode!r}")
         self.n, self.M, self.D = int(n), int(M), int(sh_degree)
         self.device = torch.device(device)
-        self.mode = mode
-        self.compact = mode == "compact"
         self.group = group
         # Collectives run whenever a process group exists, even of one rank (the RCCL code path then executes on a
         # single GPU exactly as it does on eight); distributed=False keeps a reducer local inside a process group.
@@ -95,20 +186,39 @@ class ViewGradReducer:
         self.distributed = bool(distributed)
         self.world = int(world_size if world_size is not None else
                          (dist.get_world_size(group) if self.distributed else 1))
+        self.rank = dist.get_rank(group) if self.distributed else 0
+        self.plan = None
+        if mode == "auto" or chunks is None:
+            self.plan = plan_exchange(self.n, self.world, self.M,
+                                      modes=("compact", "dense") if mode == "auto" else (mode,),
+                                      chunk_options=(1, 2, 4, 8) if chunks is None else (int(chunks),))
+            mode = self.plan["mode"]
+            chunks = self.plan["chunks"]
+            if expand is None:
+                expand = self.plan["expand"]
+        self.mode = mode
+        self.compact = mode == "compact"
+        self.expand = expand or "chunk"
+        if self.expand not in ("chunk", "once"):
+            raise ValueError(f"expand must be 'chunk' or 'once', got {self.expand!r}")
         self._sh_views = sh_views_fn or sh_backward_views
         self.widths = dict(means3D=3, scales=3, rotations=4, opacities=1, shs=3 * self.M)
         self.fields = FIELDS_COMPACT if self.compact else FIELDS_DENSE
         cols = sum(self.widths[k] for k in self.fields)
         f32 = dict(dtype=torch.float32, device=self.device)
         self.bounds = chunk_bounds(self.n, chunks)
+        self.chunk_len = self.bounds[0][1] - self.bounds[0][0]
+        # compact: chunk 0's all-reduce block ends with a (world, 3) camera-position block
+        cam_floats = 3 * self.world if self.compact else 0
         # chunk-major blocks, each [field][Gaussian of the chunk][width]: every destination is a contiguous view
-        self.flat = torch.zeros(cols * self.n, **f32)
+        self.flat = torch.zeros(cols * self.n + cam_floats, **f32)
         self.chunk_flat: List[torch.Tensor] = []
         self.chunk_views: List[Dict[str, torch.Tensor]] = []
         off = 0
-        for g0, g1 in self.bounds:
+        for c, (g0, g1) in enumerate(self.bounds):
             L = g1 - g0
-            blk = self.flat[off:off + cols * L]
+            extra = cam_floats if c == 0 else 0
+            blk = self.flat[off:off + cols * L + extra]
             views, o = {}, 0
             for k in self.fields:
                 w = self.widths[k]
@@ -116,30 +226,42 @@ class ViewGradReducer:
                 o += w
             self.chunk_flat.append(blk)
             self.chunk_views.append(views)
-            off += cols * L
+            off += cols * L + extra
         self.means2D = torch.zeros(self.n, 3, **f32)
         # densification statistics of this rank's views since the last reset (local until sync_densify_stats)
         self.stats_accum = torch.zeros(self.n, 2, **f32)
         self.radii_max = torch.zeros(self.n, dtype=torch.int32, device=self.device)
         if self.compact:
-            # per chunk: this rank's colour factors and everyone's; camera positions once per step
-            self.gather_in = [torch.zeros(g1 - g0, 3, **f32) for g0, g1 in self.bounds]
-            self.gather_all = [torch.zeros(self.world, g1 - g0, 3, **f32) for g0, g1 in self.bounds]
-            self.campos_in = torch.zeros(3, **f32)
-            self.campos_all = torch.zeros(self.world, 3, **f32)
+            L0 = self.bounds[0][1] - self.bounds[0][0]
+            self.campos_all = self.chunk_flat[0][NON_SH_FLOATS * L0:].view(self.world, 3)
+            self._campos_onehot = torch.zeros(self.world, 1, **f32)
+            self._campos_onehot[self.rank, 0] = 1.0
+            # this rank's colour factors (n, 3) and everyone's, chunk-major: chunk c = (world, L_c, 3)
+            self.gather_in_flat = torch.zeros(self.n, 3, **f32)
+            self.gather_all_flat = torch.zeros(self.world * self.n * 3, **f32)
+            self.gather_in = [self.gather_in_flat[g0:g1] for g0, g1 in self.bounds]
+            self.gather_all = [self.gather_all_flat[3 * self.world * g0:3 * self.world * g1].view(self.world, g1 - g0, 3)
+                               for g0, g1 in self.bounds]
             self.shs = torch.zeros(self.n, self.M, 3, **f32)
         elif len(self.bounds) == 1:
             self.shs = self.chunk_views[0]["shs"].view(self.n, self.M, 3)
         else:
             self.shs = None  # materialised by `grads`
+        nccl = self.distributed and dist.get_backend(group) == "nccl"
+        self.coalesce = nccl if coalesce is None else (bool(coalesce) and nccl)
+        self.sync_ops = (self.chunks == 1) if sync_ops is None else bool(sync_ops)
         self._pending: List[tuple] = []
-        self._campos_work = None
         self._materialised: Optional[Dict[str, torch.Tensor]] = None
         self._stats_synced = False  # sync_densify_stats has reduced the statistics since the last reset
 
     @property
     def chunks(self) -> int:
         return len(self.bounds)
+
+    def describe(self) -> str:
+        return (f"{self.mode}, {self.chunks} chunk(s), expand={self.expand if self.compact else '-'}, "
+                f"{'one RCCL group per chunk' if self.coalesce else 'separate collectives'}, "
+                f"{'blocking' if self.sync_ops else 'async'} ops")
 
     # ---- destinations ----
     def backward_out(self) -> Dict[str, torch.Tensor]:
@@ -188,44 +310,88 @@ class ViewGradReducer:
 
     # ---- exchange ----
     def begin_step(self, campos: torch.Tensor) -> None:
-        """Start of a step's exchange: the camera positions of every rank's view (compact mode)."""
+        """Start of a step's exchange: this rank's camera position into its row of the camera block that chunk 0's
+        all-reduce carries (compact mode; one elementwise launch, zeros in the other ranks' rows)."""
         self._check_not_synced()
         self._pending = []
         self._materialised = None
-        if not self.compact:
-            return
-        self.campos_in.copy_(campos.reshape(3))
-        if self.distributed:
-            self._campos_work = _all_gather(self.campos_all, self.campos_in, self.group)
-        else:
-            self.campos_all[0].copy_(self.campos_in)
-            self._campos_work = None
+        if self.compact:
+            torch.mul(self._campos_onehot, campos.reshape(1, 3).to(self.campos_all.dtype), out=self.campos_all)
+
+    def _pg(self):
+        return self.group if self.group is not None else dist.distributed_c10d._get_default_group()
+
+    def _issue(self, c: int):
+        """Chunk c's collectives: (gather work, reduce work); None for a completed blocking op."""
+        if self.coalesce:
+            try:
+                return self._issue_group(c)
+            except (RuntimeError, AttributeError, NotImplementedError) as e:  # backend without coalescing support
+                import warnings
+                warnings.warn(f"coalesced RCCL group unavailable ({e}); issuing separate collectives")
+                self.coalesce = False
+        gather = None
+        if self.compact:
+            gather = _all_gather(self.gather_all[c], self.gather_in[c], self.group, not self.sync_ops)
+        reduce = dist.all_reduce(self.chunk_flat[c], group=self.group, async_op=not self.sync_ops)
+        return gather, reduce
+
+    def _issue_group(self, c: int):
+        """One ncclGroupStart/End around the chunk's all-gather and all-reduce (torch's _coalescing_manager only
+        coalesces collectives of one kind, so the process group's coalescing calls are used directly)."""
+        pg = self._pg()
+        asynchronous = not self.sync_ops
+        pg._start_coalescing(self.device)
+        try:
+            if self.compact:
+                go = dist.distributed_c10d.AllgatherOptions()
+                go.asyncOp = asynchronous
+                pg._allgather_base(self.gather_all[c].view(-1), self.gather_in[c].reshape(-1), go)
+            ro = dist.AllreduceOptions()
+            ro.reduceOp = dist.ReduceOp.SUM
+            ro.asyncOp = asynchronous
+            pg.allreduce([self.chunk_flat[c]], ro)
+        finally:
+            work = pg._end_coalescing(self.device)
+        if not asynchronous:
+            if work is not None:
+                work.wait()
+            return None, None
+        return work, work
 
     def start_chunk(self, c: int) -> None:
-        """Chunk c's gradients have been enqueued on the current stream: issue its collectives (async).  The
-        all-gather goes first, so the SH expansion that needs it can start while the all-reduce still runs."""
+        """Chunk c's gradients have been enqueued on the current stream: issue its collectives (one group, or the
+        all-gather first, so the SH expansion that needs it can start while the all-reduce still runs)."""
         gather = reduce = None
         if self.distributed:
-            if self.compact:
-                gather = _all_gather(self.gather_all[c], self.gather_in[c], self.group)
-            reduce = dist.all_reduce(self.chunk_flat[c], group=self.group, async_op=True)
+            gather, reduce = self._issue(c)
         self._pending.append((c, gather, reduce))
 
+    def _expand(self, means3D: torch.Tensor, g0: int, g1: int, factors: torch.Tensor, chunk_len: int) -> None:
+        self._sh_views(means3D[g0:g1], self.campos_all, factors, self.D, self.M, out=self.shs[g0:g1],
+                       chunk_len=chunk_len)
+
     def finish(self, means3D: torch.Tensor) -> None:
-        """SH expansion per chunk (after its gather) and the wait for every collective of the step."""
-        if self._campos_work is not None:
-            self._campos_work.wait()
-            self._campos_work = None
+        """SH expansion (per chunk after its gather, or once after the last) and the wait for every collective."""
+        if self.compact and self._pending:
+            # the camera block rides in chunk 0's all-reduce
+            c0 = self._pending[0]
+            if c0[2] is not None and c0[2] is not c0[1]:
+                c0[2].wait()
         for c, gather, _ in self._pending:
             if not self.compact:
                 continue
             if gather is not None:
                 gather.wait()
-            g0, g1 = self.bounds[c]
-            factors = self.gather_all[c] if self.distributed else self.gather_in[c].unsqueeze(0)
-            self._sh_views(means3D[g0:g1], self.campos_all, factors, self.D, self.M, out=self.shs[g0:g1])
-        for _, _, reduce in self._pending:
-            if reduce is not None:
+            if self.expand == "chunk" or self.chunks == 1:
+                g0, g1 = self.bounds[c]
+                factors = self.gather_all[c] if self.distributed else self.gather_in[c].unsqueeze(0)
+                self._expand(means3D, g0, g1, factors, 0)
+        if self.compact and self.expand == "once" and self.chunks > 1 and self._pending:
+            factors = self.gather_all_flat if self.distributed else self.gather_in_flat
+            self._expand(means3D, 0, self.n, factors, self.chunk_len)
+        for _, gather, reduce in self._pending:
+            if reduce is not None and reduce is not gather:
                 reduce.wait()
         self._pending = []
 
@@ -280,10 +446,21 @@ class ViewGradReducer:
         return self.stats_accum
 
 
-def _all_gather(out: torch.Tensor, inp: torch.Tensor, group):
+def unchunk_factors(flat: torch.Tensor, V: int, n: int, chunk_len: int) -> torch.Tensor:
+    """(V, n, 3) colour factors from the chunk-major gather layout (test / oracle helper)."""
+    if not chunk_len or chunk_len >= n:
+        return flat.reshape(V, n, 3)
+    parts = []
+    for g0 in range(0, n, chunk_len):
+        L = min(chunk_len, n - g0)
+        parts.append(flat.reshape(-1)[3 * V * g0:3 * V * (g0 + L)].view(V, L, 3))
+    return torch.cat(parts, 1)
+
+
+def _all_gather(out: torch.Tensor, inp: torch.Tensor, group, async_op: bool = True):
     """all_gather into a (world, ...) tensor; gloo lacks the single-tensor form on some builds."""
     inp = inp.contiguous()
     if dist.get_backend(group) == "nccl":
-        return dist.all_gather_into_tensor(out.view(-1), inp.view(-1), group=group, async_op=True)
+        return dist.all_gather_into_tensor(out.view(-1), inp.view(-1), group=group, async_op=async_op)
     dist.all_gather(list(out.unbind(0)), inp.view(out.shape[1:]), group=group)
     return None

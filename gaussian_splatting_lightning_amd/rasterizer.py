@@ -349,24 +349,29 @@ def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales,
 
 
 def sh_backward_views(means3D: torch.Tensor, campos: torch.Tensor, dcolors_sh: torch.Tensor, sh_degree: int, M: int,
-                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                      out: Optional[torch.Tensor] = None, chunk_len: int = 0) -> torch.Tensor:
     """dL/dshs (P,M,3) summed over V views from the compact per-view factors: campos (V,3) and the clamp-masked
-    colour gradients dcolors_sh (V,P,3) that backward_raw(..., compact_sh=True) returns (gsr_sh_backward_views)."""
+    colour gradients dcolors_sh (V,P,3) that backward_raw(..., compact_sh=True) returns (gsr_sh_backward_views).
+    chunk_len > 0: dcolors_sh is the flat chunk-major layout of multiview.py's chunked gather -- chunk c covers
+    Gaussians [c*chunk_len, min(P, (c+1)*chunk_len)) as a (V, L_c, 3) block (gsr_sh_backward_views_chunked)."""
     lib = _native.load()
     device = means3D.device
     m = _prep(means3D, device, "means3D")
     c = _prep(campos, device, "campos").reshape(-1, 3)
     d = _prep(dcolors_sh, device, "dcolors_sh")
     P, V = m.shape[0], c.shape[0]
-    if tuple(d.shape) != (V, P, 3):
+    if chunk_len and chunk_len < P:
+        if d.numel() != V * P * 3:
+            raise RuntimeError(f"chunked dcolors_sh must hold {V * P * 3} floats, got {d.numel()}")
+    elif tuple(d.shape) != (V, P, 3):
         raise RuntimeError(f"dcolors_sh must have shape {(V, P, 3)}, got {tuple(d.shape)}")
     if out is None:
         out = torch.empty(P, M, 3, dtype=torch.float32, device=device)
     elif tuple(out.shape) != (P, M, 3) or out.dtype != torch.float32 or not out.is_contiguous():
         raise RuntimeError(f"out must be a contiguous float32 tensor of shape {(P, M, 3)}")
     with torch.cuda.device(device):
-        rc = lib.gsr_sh_backward_views(P, int(sh_degree), int(M), V, _ptr(m), _ptr(c), _ptr(d), out.data_ptr(),
-                                       _stream_handle(device))
+        rc = lib.gsr_sh_backward_views_chunked(P, int(sh_degree), int(M), V, int(chunk_len), _ptr(m), _ptr(c), _ptr(d),
+                                               out.data_ptr(), _stream_handle(device))
     _native.check(rc, "sh_backward_views")
     return out
 

@@ -151,6 +151,12 @@ int gsr_backward(const gsr_backward_args *args, gsr_alloc_fn alloc, void *alloc_
 int gsr_sh_backward_views(int P, int D, int M, int V, const float *means3D, const float *campos,
                           const float *dL_dcolors_sh, float *dL_dsh, void *stream);
 
+/* The same expansion over factors gathered per Gaussian chunk (multiview.py's chunked exchange), in ONE launch:
+ * dL_dcolors_sh is chunk-major -- chunk c covers Gaussians [c*chunk_len, min(P, (c+1)*chunk_len)) and is a
+ * (V, L_c, 3) block at offset c*V*chunk_len*3.  chunk_len = 0 (or >= P) is gsr_sh_backward_views' (V,P,3). */
+int gsr_sh_backward_views_chunked(int P, int D, int M, int V, int64_t chunk_len, const float *means3D,
+                                  const float *campos, const float *dL_dcolors_sh, float *dL_dsh, void *stream);
+
 /* Replaces `_C.mark_visible` (checkFrustum): present[i] = z_view(means3D[i]) > 0.2. */
 int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
                      uint8_t *present, void *stream);

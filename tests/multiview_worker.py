@@ -30,21 +30,24 @@ def oracle_view(view, world):
     return g
 
 
-def oracle_sh_views(means3D, campos, dcolors_sh, sh_degree, M, out):
+def oracle_sh_views(means3D, campos, dcolors_sh, sh_degree, M, out, chunk_len=0):
+    from gaussian_splatting_lightning_amd.multiview import unchunk_factors
     from oracle import oracle as O
-    r = O.sh_backward_views(means3D.numpy(), campos.numpy(), dcolors_sh.numpy(), sh_degree, M)
+    d = unchunk_factors(dcolors_sh, campos.shape[0], means3D.shape[0], chunk_len)
+    r = O.sh_backward_views(means3D.numpy(), campos.numpy(), d.numpy(), sh_degree, M)
     out.copy_(torch.from_numpy(r))
     return out
 
 
-def worker(rank, world, port, mode, result_dir, chunks=1):
+def worker(rank, world, port, mode, result_dir, chunks=1, expand="chunk"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from gaussian_splatting_lightning_amd.multiview import ViewGradReducer
         g = oracle_view(rank, world)
-        red = ViewGradReducer(N, 16, DEG, "cpu", mode=mode, sh_views_fn=oracle_sh_views, chunks=chunks)
+        red = ViewGradReducer(N, 16, DEG, "cpu", mode=mode, sh_views_fn=oracle_sh_views, chunks=chunks,
+                              expand=expand)
         means3D = torch.from_numpy(g["means3D_in"])
 
         def fill(out, g0, g1):  # what the backward writes for Gaussians [g0, g1)

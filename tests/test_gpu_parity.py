@@ -531,6 +531,14 @@ def test_compact_sh_views_matches_dense(gpu_device):
     np.testing.assert_allclose(got.cpu().numpy(), ds, rtol=1e-5, atol=1e-6 * np.abs(ds).max())
     ref = O_sh_views(t["means3D"], torch.stack(camposes), torch.stack(factors))
     np.testing.assert_allclose(got.cpu().numpy(), ref, rtol=1e-5, atol=1e-6 * np.abs(ref).max())
+    # the chunk-major layout of the chunked exchange's gather (gsr_sh_backward_views_chunked): bitwise the same
+    from gaussian_splatting_lightning_amd.multiview import chunk_bounds
+    fs = torch.stack(factors)
+    for K in (2, 3):
+        b = chunk_bounds(fs.shape[1], K)
+        flat = torch.cat([fs[:, g0:g1].reshape(-1) for g0, g1 in b])
+        chunked = sh_backward_views(t["means3D"], torch.stack(camposes), flat, 3, 16, chunk_len=b[0][1] - b[0][0])
+        assert torch.equal(chunked, got), K
 
 
 def O_sh_views(means3D, campos, factors):

@@ -31,12 +31,12 @@ def expected():
     return exp
 
 
-def _run(tmp_path, mode, chunks, world=2):
+def _run(tmp_path, mode, chunks, world=2, expand="chunk"):
     ctx = mp.get_context("spawn")
     port = _free_port()
-    d = os.path.join(str(tmp_path), f"{mode}_{chunks}")
+    d = os.path.join(str(tmp_path), f"{mode}_{chunks}_{expand}")
     os.makedirs(d, exist_ok=True)
-    procs = [ctx.Process(target=MW.worker, args=(r, world, port, mode, d, chunks)) for r in range(world)]
+    procs = [ctx.Process(target=MW.worker, args=(r, world, port, mode, d, chunks, expand)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -73,6 +73,44 @@ def test_chunked_exchange_is_bitwise_the_unchunked_one(tmp_path, mode):
     for r in range(2):
         for k in ("means3D", "scales", "rotations", "opacities", "stats", "radii_max", "shs"):
             assert np.array_equal(one[r][k], four[r][k]), (r, k)
+    if mode == "compact":  # one SH expansion over the chunk-major gather buffer after the last chunk: same bits
+        once = _run(tmp_path, mode, 4, expand="once")
+        for r in range(2):
+            for k in ("means3D", "scales", "rotations", "opacities", "stats", "radii_max", "shs"):
+                assert np.array_equal(one[r][k], once[r][k]), (r, k)
+
+
+def test_exchange_plan_cost_model():
+    """plan_exchange: per-rank link bytes follow the ring formulas (413 B/G dense, 161 B/G compact
+    at 8 ranks, SH 3); more ranks never pick dense over compact; the predicted end time is monotone in the assumed
+    bus bandwidth; every simulated schedule ends no earlier than its compute and its communication."""
+    from gaussian_splatting_lightning_amd.multiview import (exchange_bytes_per_gaussian, plan_exchange,
+                                                            simulate_exchange)
+    assert abs(exchange_bytes_per_gaussian("dense", 8) - 413.0) < 0.01
+    assert abs(exchange_bytes_per_gaussian("compact", 8) - 161.0) < 0.01
+    assert exchange_bytes_per_gaussian("compact", 1) == 0.0
+    for N in (2, 4, 8):
+        p = plan_exchange(1_000_000, N)
+        assert p["mode"] == "compact", (N, p)
+        slow = plan_exchange(1_000_000, N, costs=dict(bus_efficiency=0.2))
+        assert slow["end_ms"] > p["end_ms"]
+    for mode in ("dense", "compact"):
+        for K in (1, 2, 4, 8):
+            for expand in ("chunk", "once"):
+                r = simulate_exchange(1_000_000, 8, mode, K, expand)
+                assert r["end_ms"] >= r["comm_ms"] and r["end_ms"] >= r["per_gaussian_stage_ms"]
+
+
+def test_unchunk_factors_round_trip():
+    import torch
+    from gaussian_splatting_lightning_amd.multiview import chunk_bounds, unchunk_factors
+    V, n = 3, 1000
+    full = torch.randn(V, n, 3)
+    for K in (1, 2, 4):
+        b = chunk_bounds(n, K)
+        L = b[0][1] - b[0][0]
+        flat = torch.cat([full[:, g0:g1].reshape(-1) for g0, g1 in b])
+        assert torch.equal(unchunk_factors(flat, V, n, L), full)
 
 
 def test_one_rank_group_takes_the_collective_path_and_guards_resync():

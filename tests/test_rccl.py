@@ -28,11 +28,11 @@ def _step(red, st, rs, dc, di, means3D, chunked):
         red.reduce(means3D, rs.campos)
 
 
-def _run(dev, distributed, mode, chunks, views=2):
+def _run(dev, distributed, mode, chunks, views=2, **kw):
     from gaussian_splatting_lightning_amd.multiview import ViewGradReducer
     from gaussian_splatting_lightning_amd.rasterizer import forward_raw
     n, W, H = 30_000, 320, 240
-    red = ViewGradReducer(n, 16, 3, dev, mode=mode, chunks=chunks, distributed=distributed)
+    red = ViewGradReducer(n, 16, 3, dev, mode=mode, chunks=chunks, distributed=distributed, **kw)
     assert red.distributed == distributed
     for v in range(views):  # two steps: the statistics accumulate over views before the sync
         inp = scene_inputs(n, W, H, sh_degree=3, seed=12, stress_fraction=0.01, view_index=v, num_views=4)
@@ -49,15 +49,22 @@ def _run(dev, distributed, mode, chunks, views=2):
     return grads, stats.clone(), rmax.clone(), red
 
 
-@pytest.mark.parametrize("mode,chunks", [("compact", 4), ("dense", 4), ("compact", 1)])
-def test_rccl_exchange_one_rank_is_bitwise_local(gpu_device, mode, chunks):
+VARIANTS = [  # (mode, chunks, reducer options): one RCCL group per chunk unless coalesce=False
+    ("compact", 4, {}), ("compact", 4, dict(expand="once")), ("dense", 4, {}), ("compact", 1, {}), ("dense", 1, {}),
+    ("compact", 4, dict(coalesce=False)), ("compact", 1, dict(sync_ops=False)), ("dense", 1, dict(coalesce=False)),
+]
+
+
+@pytest.mark.parametrize("mode,chunks,kw", VARIANTS)
+def test_rccl_exchange_one_rank_is_bitwise_local(gpu_device, mode, chunks, kw):
     ref = _run(gpu_device, False, mode, chunks)
     assert not dist.is_initialized()
     torch.cuda.set_device(gpu_device)
     dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=gpu_device)
     try:
-        got = _run(gpu_device, True, mode, chunks)
+        got = _run(gpu_device, True, mode, chunks, **kw)
         red = got[3]
+        assert red.coalesce == kw.get("coalesce", True)  # the grouped path really ran (no fallback)
         # the RCCL branch really ran: the chunk gathers landed in the (world, L, 3) buffers
         if mode == "compact":
             for c in range(red.chunks):
@@ -67,7 +74,7 @@ def test_rccl_exchange_one_rank_is_bitwise_local(gpu_device, mode, chunks):
             red.begin_step(torch.zeros(3, device=gpu_device))
         red.reset_densify_stats()
         red.begin_step(torch.zeros(3, device=gpu_device))
-        red.finish(None)  # waits for the camera-position gather before the group goes
+        red.finish(None)  # nothing pending: returns at once
     finally:
         dist.destroy_process_group()
     for k in ref[0]:

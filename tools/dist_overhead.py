@@ -2,12 +2,14 @@
 """Where the multi-GPU step's extra time goes, on ONE GPU with a one-rank RCCL group (bench.py --force-dist measured
 1.14 ms/step against 0.81 for the plain step at cfg 3).
 
-    python tools/dist_overhead.py [--config cfg3] [--steps 20]
+    python tools/dist_overhead.py [--config cfg3] [--steps 20] [--rounds 3]
 
-Variants (each: wall ms per step over --steps steps bracketed by synchronize, and the host's issue time per step):
+Variants (each: wall ms per step over --steps steps bracketed by synchronize; median over --rounds interleaved
+rounds):
   plain            backward_raw into a dense reducer, no process group (bench.py at N = 1)
-  local_cK_mode    the reducer's chunked / compact arithmetic with distributed=False (no collectives)
-  dist_cK_mode     the same with the one-rank RCCL group (every collective issued and waited)
+  local_*          the reducer's chunked / compact arithmetic with distributed=False (no collectives)
+  dist_*           the same with the one-rank RCCL group: grouped (one RCCL group per chunk) or separate
+                   collectives, blocking or async ops; dist_auto is multiview.plan_exchange's choice
 """
 import argparse
 import json
@@ -22,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg3")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -54,7 +57,7 @@ def main():
         return step
 
     def timeit(step):
-        for _ in range(5):
+        for _ in range(10):
             step()
         torch.cuda.synchronize()
         host = 0.0
@@ -67,18 +70,39 @@ def main():
         wall = time.perf_counter() - t0
         return {"wall_ms": round(1e3 * wall / args.steps, 4), "host_ms": round(1e3 * host / args.steps, 4)}
 
-    res = {"plain": timeit(make_step(ViewGradReducer(n, M, cfg["deg"], dev, mode="dense", chunks=1,
-                                                     distributed=False)))}
-    variants = [("dense", 1), ("compact", 1), ("dense", 4), ("compact", 4), ("compact", 2)]
-    for mode, k in variants:
-        res[f"local_c{k}_{mode}"] = timeit(make_step(ViewGradReducer(n, M, cfg["deg"], dev, mode=mode, chunks=k,
-                                                                     distributed=False)))
+    local = {"plain": dict(mode="dense", chunks=1), "local_compact1": dict(mode="compact", chunks=1),
+             "local_compact4_chunk": dict(mode="compact", chunks=4, expand="chunk"),
+             "local_compact4_once": dict(mode="compact", chunks=4, expand="once"),
+             "local_dense4": dict(mode="dense", chunks=4)}
+    remote = {"dist_dense1_sync_group": dict(mode="dense", chunks=1),
+              "dist_dense1_async_sep": dict(mode="dense", chunks=1, sync_ops=False, coalesce=False),
+              "dist_compact1_sync_group": dict(mode="compact", chunks=1),
+              "dist_compact1_async_sep": dict(mode="compact", chunks=1, sync_ops=False, coalesce=False),
+              "dist_compact4_chunk_group": dict(mode="compact", chunks=4, expand="chunk"),
+              "dist_compact4_once_group": dict(mode="compact", chunks=4, expand="once"),
+              "dist_compact4_chunk_sep": dict(mode="compact", chunks=4, expand="chunk", coalesce=False),
+              "dist_dense4_group": dict(mode="dense", chunks=4),
+              "dist_auto": dict(mode="auto", chunks=None)}
+    steps = {k: make_step(ViewGradReducer(n, M, cfg["deg"], dev, distributed=False, **kw)) for k, kw in local.items()}
     dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
+    res = {}
     try:
-        for mode, k in variants:
-            res[f"dist_c{k}_{mode}"] = timeit(make_step(ViewGradReducer(n, M, cfg["deg"], dev, mode=mode, chunks=k)))
+        reds = {k: ViewGradReducer(n, M, cfg["deg"], dev, **kw) for k, kw in remote.items()}
+        steps.update({k: make_step(r) for k, r in reds.items()})
+        samples = {k: [] for k in steps}
+        for _ in range(args.rounds):  # interleaved rounds: clocks and box noise hit every variant alike
+            for k, f in steps.items():
+                samples[k].append(timeit(f))
+        for k, v in samples.items():
+            w = sorted(x["wall_ms"] for x in v)
+            res[k] = {"wall_ms_median": w[len(w) // 2], "wall_ms_all": w}
+        res["dist_auto"]["exchange"] = reds["dist_auto"].describe()
+        res["dist_auto"]["plan"] = reds["dist_auto"].plan
     finally:
         dist.destroy_process_group()
+    base = res["plain"]["wall_ms_median"]
+    for k in res:
+        res[k]["vs_plain"] = round(res[k]["wall_ms_median"] / base, 4)
     print(json.dumps(res, indent=1))
 
 
