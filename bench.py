@@ -146,9 +146,9 @@ def main():
         # only when the model densifies (ViewGradReducer.sync_densify_stats), not every step
         if red.chunks == 1:
             backward_raw(st, settings, dcolor, dinv, **red.backward_kwargs())
-            red.reduce(sc.means3D, c.campos)
+            red.reduce(sc.means3D)
         else:
-            red.begin_step(c.campos)
+            red.begin_step()
             backward_chunked(st, settings, dcolor, dinv, red.chunk_outputs(), on_chunk=red.start_chunk,
                              compact_sh=red.compact, accumulate_stats=True)
             red.finish(sc.means3D)

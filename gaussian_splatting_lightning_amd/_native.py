@@ -44,6 +44,7 @@ class BackwardArgs(ctypes.Structure):
         ("densify_stats", _fp),
         ("densify_accumulate", ctypes.c_int), ("max_radii2D", _fp),
         ("stages", ctypes.c_int), ("g_begin", ctypes.c_int64), ("g_end", ctypes.c_int64), ("bwd_scratch", _fp),
+        ("campos_rows", _fp), ("campos_rank", ctypes.c_int), ("campos_nrows", ctypes.c_int),
     ]
 
 

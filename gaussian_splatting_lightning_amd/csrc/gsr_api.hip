@@ -762,6 +762,8 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
         return fail(GSR_ERR_ARG, "dL_dsh (or dL_dcolors_sh) is required when shs are given");
     if (a->R < 0 || a->R > 0xffffffffLL) return fail(GSR_ERR_ARG, "bad num_rendered");
     if (a->stages < GSR_BWD_ALL || a->stages > GSR_BWD_GAUSSIANS) return fail(GSR_ERR_ARG, "bad backward stages");
+    if (a->campos_rows && (!a->campos || a->campos_nrows < 1 || a->campos_rank < 0 || a->campos_rank >= a->campos_nrows))
+        return fail(GSR_ERR_ARG, "campos_rows needs campos and 0 <= campos_rank < campos_nrows");
     int64_t g0 = a->g_begin, g1 = a->g_end;
     if (g0 == 0 && g1 == 0) g1 = a->P;
     if (g0 < 0 || g1 < g0 || g1 > a->P) return fail(GSR_ERR_ARG, "bad Gaussian range [g_begin, g_end)");
@@ -862,6 +864,7 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     pp.densify_accumulate = a->densify_accumulate;
     pp.max_radii2D = rel(a->max_radii2D, 1);
     pp.dL_dscales = rel(a->dL_dscales, 3); pp.dL_drot = rel(a->dL_drotations, 4);
+    pp.campos_rows = a->campos_rows; pp.campos_rank = a->campos_rank; pp.campos_nrows = a->campos_nrows;
     const size_t ng = (size_t)(g1 - g0);
     if (pp.shs == nullptr && a->dL_dsh && a->M > 0)
         GSR_HIP(hipMemsetAsync(a->dL_dsh, 0, sizeof(float) * ng * a->M * 3, stream));

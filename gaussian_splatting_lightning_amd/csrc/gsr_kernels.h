@@ -242,6 +242,8 @@ struct PreprocessBwdParams {
     float *densify_stats;  // (P,2) |dL/dmeans2D[:2]|, radii > 0 (may be null)
     int densify_accumulate;  // densify_stats += instead of =
     int *max_radii2D;        // (P) max(max_radii2D, radii) (may be null)
+    float *campos_rows;      // (campos_nrows, 3): campos in row campos_rank, zeros elsewhere (may be null)
+    int campos_rank, campos_nrows;
 };
 void launch_preprocess_bwd(hipStream_t s, const PreprocessBwdParams &p);
 

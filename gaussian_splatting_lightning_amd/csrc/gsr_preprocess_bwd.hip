@@ -298,6 +298,9 @@ constexpr int PBWD_STAGE = 32 * SH_STRIDE;  // floats of LDS per wave
 template <bool LDS_SH>
 __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams p) {
     const int i = p.g0 + blockIdx.x * 256 + threadIdx.x;
+    if (p.campos_rows && blockIdx.x == 0)  // the exchange's camera block (row campos_rank = campos, others zero)
+        for (int t = threadIdx.x; t < 3 * p.campos_nrows; t += 256)
+            p.campos_rows[t] = t / 3 == p.campos_rank ? p.campos[t % 3] : 0.f;
     if (!LDS_SH) {
         const float none[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         float3 d3, v3;

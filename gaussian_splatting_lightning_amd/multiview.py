@@ -26,7 +26,9 @@ Overlap with the backward (``chunks`` = K > 1): the Gaussians are split into K c
 gradient buffer is laid out chunk-major -- chunk c's block holds [means3D | scales | rotations | opacity (| shs)]
 of its Gaussians only -- so a chunk's exchange is ONE all-reduce (+ one all-gather of its colour factors), issued
 as one RCCL group (ncclGroupStart/End through the process group's coalescing calls) as soon as chunk c is
-enqueued; RCCL runs it on its own stream while the GPU computes chunk c + 1.  The SH expansion runs per chunk as
+enqueued, on the reducer's side stream behind an event on the compute stream, so it runs while the GPU computes
+chunk c + 1.  (With one chunk the group is issued blocking on the compute stream itself: no hand-off.)  The SH
+expansion runs per chunk as
 each group lands (``expand="chunk"``), or once over the chunk-major gather buffer after the last one
 (``expand="once"``).  Results are bitwise those of K = 1: every element is the same sum of the same per-rank values
 (tests/test_multiview.py checks K = 1 against K = 4 on world_size 2).
@@ -50,18 +52,21 @@ FIELDS_DENSE = ("means3D", "scales", "rotations", "opacities", "shs")
 FIELDS_COMPACT = ("means3D", "scales", "rotations", "opacities")
 NON_SH_FLOATS = 11  # means3D 3 + scales 3 + rotations 4 + opacity 1
 
-# Cost-model constants.  Kernel times are per 1e6 Gaussians at SH degree 3 on one MI355X (rocprofv3 kernel
-# averages at cfg 3); `group_ms` is the fixed cost of one collective group on a one-rank RCCL group
-# (launch + stream handoff, no data); the bus bandwidth is an ASSUMPTION (no 8-GPU node has run this code):
-# 7 xGMI links x 153 GB/s per direction at `bus_efficiency` of RCCL's ring/tree schedules.
+# Cost-model constants, measured on one MI355X at cfg 3 (1M Gaussians, SH degree 3; rocprofv3 kernel trace of
+# tools/dist_overhead.py with a one-rank RCCL group, profiles/r5e_*): kernel times per 1e6 Gaussians, and the
+# fixed GPU-timeline cost of one collective group -- blocking (issued on the compute stream: one event marker, no
+# hand-off) or async (the process group's own stream: a marker on the compute queue that stalls its next kernel,
+# the communication stream's wait, and the compute stream's wait for the result).  The bus bandwidth is an
+# ASSUMPTION (no 8-GPU node has run this code): 7 xGMI links x 153 GB/s per direction at
+# `bus_efficiency` of RCCL's ring schedules.
 EXCHANGE_COSTS = dict(
-    pb_dense_ms=0.106,     # preprocess_bwd writing dL/dsh (192 B/G)
-    pb_compact_ms=0.088,   # preprocess_bwd writing the 12-B colour factor instead
-    exp_ms=0.040,          # gsr_sh_backward_views: 192 B/G written + means
-    exp_view_ms=0.003,     # + 12 B/G read per view
-    chunk_ms=0.004,        # per extra per-Gaussian-stage launch (launch gap + tail)
-    group_ms=0.012,        # one collective group, fixed
-    copy_GBps=4000.0,      # one-rank all-gather: RCCL copies input -> output on the device
+    pb_dense_ms=0.104,       # preprocess_bwd writing dL/dsh (192 B/G)
+    pb_compact_ms=0.080,     # preprocess_bwd writing the 12-B colour factor instead
+    exp_ms=0.036,            # gsr_sh_backward_views: 192 B/G written + means + one view's factors
+    exp_view_ms=0.002,       # + 12 B/G read per further view
+    chunk_ms=0.0043,         # per extra chunk: one more per-Gaussian-stage launch (and SH-expansion launch)
+    group_sync_ms=0.007,     # one blocking collective group (chunks == 1)
+    group_async_ms=0.011,    # one async collective group (chunks > 1, on the reducer's side stream)
     link_GBps=153.0,
     links=7,
     bus_efficiency=0.6,
@@ -90,9 +95,8 @@ def simulate_exchange(n: int, world: int, mode: str, chunks: int, expand: str = 
     pb = (c["pb_compact_ms"] if mode == "compact" else c["pb_dense_ms"]) * scale
     bus = c["link_GBps"] * c["links"] * c["bus_efficiency"] * 1e9  # B/s
     link_bytes = exchange_bytes_per_gaussian(mode, N, M) * n
-    comm = link_bytes / bus * 1e3 if N > 1 else 0.0
-    if N == 1 and mode == "compact":  # the one-rank all-gather is a device copy (read + write of 12 B/G)
-        comm += 24.0 * n / (c["copy_GBps"] * 1e9) * 1e3
+    comm = link_bytes / bus * 1e3 if N > 1 else 0.0  # one rank: in-place collectives move nothing
+    group = c["group_sync_ms"] if K == 1 else c["group_async_ms"]
     t_chunk = [pb / K + (c["chunk_ms"] if k > 0 else 0.0) for k in range(K)]
     comp_end = 0.0
     comm_end = 0.0
@@ -100,11 +104,11 @@ def simulate_exchange(n: int, world: int, mode: str, chunks: int, expand: str = 
     for k in range(K):
         comp_end += t_chunk[k]
         start = max(comp_end, comm_end)
-        comm_end = start + c["group_ms"] + comm / K
+        comm_end = start + group + comm / K
         group_end.append(comm_end)
     t = comp_end
     if mode == "compact":
-        exp = (c["exp_ms"] + c["exp_view_ms"] * N) * scale
+        exp = (c["exp_ms"] + c["exp_view_ms"] * (N - 1)) * scale
         if expand == "once":
             t = max(t, group_end[-1]) + exp
         else:
@@ -173,7 +177,7 @@ class ViewGradReducer:
                  world_size: Optional[int] = None,
                  sh_views_fn: Optional[Callable[..., torch.Tensor]] = None, chunks: Optional[int] = 1,
                  distributed: Optional[bool] = None, expand: Optional[str] = None,
-                 coalesce: Optional[bool] = None, sync_ops: Optional[bool] = None):
+                 coalesce: Optional[bool] = None, sync_ops: Optional[bool] = None, comm_stream: Optional[str] = None):
         if mode not in ("dense", "compact", "auto"):
             raise ValueError(f"mode must be 'dense', 'compact' or 'auto', got {mode!r}")
         self.n, self.M, self.D = int(n), int(M), int(sh_degree)
@@ -236,12 +240,12 @@ class ViewGradReducer:
             self.campos_all = self.chunk_flat[0][NON_SH_FLOATS * L0:].view(self.world, 3)
             self._campos_onehot = torch.zeros(self.world, 1, **f32)
             self._campos_onehot[self.rank, 0] = 1.0
-            # this rank's colour factors (n, 3) and everyone's, chunk-major: chunk c = (world, L_c, 3)
-            self.gather_in_flat = torch.zeros(self.n, 3, **f32)
+            # everyone's colour factors, chunk-major: chunk c = (world, L_c, 3); this rank's (L_c, 3) factors are its
+            # row of the gathered block, written there by the backward (an in-place all-gather: nothing to copy)
             self.gather_all_flat = torch.zeros(self.world * self.n * 3, **f32)
-            self.gather_in = [self.gather_in_flat[g0:g1] for g0, g1 in self.bounds]
             self.gather_all = [self.gather_all_flat[3 * self.world * g0:3 * self.world * g1].view(self.world, g1 - g0, 3)
                                for g0, g1 in self.bounds]
+            self.gather_in = [blk[self.rank] for blk in self.gather_all]
             self.shs = torch.zeros(self.n, self.M, 3, **f32)
         elif len(self.bounds) == 1:
             self.shs = self.chunk_views[0]["shs"].view(self.n, self.M, 3)
@@ -250,6 +254,20 @@ class ViewGradReducer:
         nccl = self.distributed and dist.get_backend(group) == "nccl"
         self.coalesce = nccl if coalesce is None else (bool(coalesce) and nccl)
         self.sync_ops = (self.chunks == 1) if sync_ops is None else bool(sync_ops)
+        # comm_stream="side" (chunked exchange on a HIP device): the reducer's own stream carries the
+        # collectives as blocking ops behind one event per chunk, and the compute stream waits for chunk c's group
+        # only before chunk c's SH expansion.  torch's RCCL process group otherwise runs async ops on its pool stream,
+        # which can share the compute stream's hardware queue (then the chunks serialise behind each hand-off).
+        self.comm_stream = None
+        if comm_stream not in (None, "pg", "side"):
+            raise ValueError(f"comm_stream must be 'pg' or 'side', got {comm_stream!r}")
+        if comm_stream is None:  # measured (one rank, 4 chunks): side 0.901 ms/step against 0.923 for the pg stream
+            comm_stream = "side" if self.chunks > 1 else "pg"
+        if comm_stream == "side" and self.distributed and self.device.type == "cuda":
+            self.comm_stream = torch.cuda.Stream(self.device)
+            self._ready = [torch.cuda.Event() for _ in self.bounds]   # chunk c's gradients are written
+            self._landed = [torch.cuda.Event() for _ in self.bounds]  # chunk c's collectives are done
+            self.sync_ops = True
         self._pending: List[tuple] = []
         self._materialised: Optional[Dict[str, torch.Tensor]] = None
         self._stats_synced = False  # sync_densify_stats has reduced the statistics since the last reset
@@ -261,7 +279,8 @@ class ViewGradReducer:
     def describe(self) -> str:
         return (f"{self.mode}, {self.chunks} chunk(s), expand={self.expand if self.compact else '-'}, "
                 f"{'one RCCL group per chunk' if self.coalesce else 'separate collectives'}, "
-                f"{'blocking' if self.sync_ops else 'async'} ops")
+                f"{'blocking' if self.sync_ops else 'async'} ops"
+                f"{' on a side stream' if self.comm_stream is not None else ''}")
 
     # ---- destinations ----
     def backward_out(self) -> Dict[str, torch.Tensor]:
@@ -274,6 +293,7 @@ class ViewGradReducer:
                    means2D=self.means2D, densify_stats=self.stats_accum, max_radii2D=self.radii_max)
         if self.compact:
             out["colors_sh"] = self.gather_in[0]
+            out["campos_rows"] = (self.campos_all, self.rank)
         else:
             out["shs"] = self.shs
         return out
@@ -295,6 +315,8 @@ class ViewGradReducer:
                        max_radii2D=self.radii_max[g0:g1])
             if self.compact:
                 out["colors_sh"] = self.gather_in[c]
+                if c == 0:  # the camera block rides in chunk 0's all-reduce; chunk 0's backward call writes it
+                    out["campos_rows"] = (self.campos_all, self.rank)
             else:
                 out["shs"] = v["shs"]
             res.append((g0, g1, out))
@@ -309,13 +331,15 @@ class ViewGradReducer:
         torch.maximum(self.radii_max, radii.to(torch.int32), out=self.radii_max)
 
     # ---- exchange ----
-    def begin_step(self, campos: torch.Tensor) -> None:
-        """Start of a step's exchange: this rank's camera position into its row of the camera block that chunk 0's
-        all-reduce carries (compact mode; one elementwise launch, zeros in the other ranks' rows)."""
+    def begin_step(self, campos: Optional[torch.Tensor] = None) -> None:
+        """Start of a step's exchange.  The camera block that chunk 0's all-reduce carries (this rank's campos in its
+        row, zeros elsewhere) is written by the backward call that receives backward_out() / chunk_outputs()
+        ("campos_rows"); a caller whose backward does not (a custom gradient source) passes campos here instead (one
+        elementwise launch)."""
         self._check_not_synced()
         self._pending = []
         self._materialised = None
-        if self.compact:
+        if self.compact and campos is not None:
             torch.mul(self._campos_onehot, campos.reshape(1, 3).to(self.campos_all.dtype), out=self.campos_all)
 
     def _pg(self):
@@ -363,7 +387,15 @@ class ViewGradReducer:
         """Chunk c's gradients have been enqueued on the current stream: issue its collectives (one group, or the
         all-gather first, so the SH expansion that needs it can start while the all-reduce still runs)."""
         gather = reduce = None
-        if self.distributed:
+        if self.distributed and self.comm_stream is not None:
+            cur = torch.cuda.current_stream(self.device)
+            self._ready[c].record(cur)
+            with torch.cuda.stream(self.comm_stream):
+                self.comm_stream.wait_event(self._ready[c])
+                self._issue(c)  # blocking ops: they run on the side stream itself
+                self._landed[c].record(self.comm_stream)
+            gather = reduce = _StreamEventWork(self._landed[c], self.device)
+        elif self.distributed:
             gather, reduce = self._issue(c)
         self._pending.append((c, gather, reduce))
 
@@ -385,18 +417,17 @@ class ViewGradReducer:
                 gather.wait()
             if self.expand == "chunk" or self.chunks == 1:
                 g0, g1 = self.bounds[c]
-                factors = self.gather_all[c] if self.distributed else self.gather_in[c].unsqueeze(0)
-                self._expand(means3D, g0, g1, factors, 0)
+                self._expand(means3D, g0, g1, self.gather_all[c], 0)
         if self.compact and self.expand == "once" and self.chunks > 1 and self._pending:
-            factors = self.gather_all_flat if self.distributed else self.gather_in_flat
-            self._expand(means3D, 0, self.n, factors, self.chunk_len)
+            self._expand(means3D, 0, self.n, self.gather_all_flat, self.chunk_len)
         for _, gather, reduce in self._pending:
             if reduce is not None and reduce is not gather:
                 reduce.wait()
         self._pending = []
 
-    def reduce(self, means3D: torch.Tensor, campos: torch.Tensor) -> None:
-        """The whole exchange after an unchunked backward (backward_out()): every chunk at once."""
+    def reduce(self, means3D: torch.Tensor, campos: Optional[torch.Tensor] = None) -> None:
+        """The whole exchange after an unchunked backward (backward_out()): every chunk at once.  campos: only when
+        the backward did not write the camera block (see begin_step)."""
         self.begin_step(campos)
         for c in range(self.chunks):
             self.start_chunk(c)
@@ -446,6 +477,16 @@ class ViewGradReducer:
         return self.stats_accum
 
 
+class _StreamEventWork:
+    """work.wait() for a collective run on the reducer's side stream: the current stream waits for its event."""
+
+    def __init__(self, event, device):
+        self.event, self.device = event, device
+
+    def wait(self):
+        torch.cuda.current_stream(self.device).wait_event(self.event)
+
+
 def unchunk_factors(flat: torch.Tensor, V: int, n: int, chunk_len: int) -> torch.Tensor:
     """(V, n, 3) colour factors from the chunk-major gather layout (test / oracle helper)."""
     if not chunk_len or chunk_len >= n:
@@ -459,8 +500,7 @@ def unchunk_factors(flat: torch.Tensor, V: int, n: int, chunk_len: int) -> torch
 
 def _all_gather(out: torch.Tensor, inp: torch.Tensor, group, async_op: bool = True):
     """all_gather into a (world, ...) tensor; gloo lacks the single-tensor form on some builds."""
-    inp = inp.contiguous()
-    if dist.get_backend(group) == "nccl":
-        return dist.all_gather_into_tensor(out.view(-1), inp.view(-1), group=group, async_op=async_op)
-    dist.all_gather(list(out.unbind(0)), inp.view(out.shape[1:]), group=group)
+    if dist.get_backend(group) == "nccl":  # in place: inp is this rank's row of out
+        return dist.all_gather_into_tensor(out.view(-1), inp.reshape(-1), group=group, async_op=async_op)
+    dist.all_gather(list(out.unbind(0)), inp.clone().view(out.shape[1:]), group=group)
     return None

@@ -178,7 +178,8 @@ def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_
     `out` may supply preallocated contiguous float32 destinations (e.g. views into one flat buffer that is
     then all-reduced): keys means2D (P,3), colors (P,3), opacities (P,1), means3D (P,3), cov3D (P,6),
     shs (P,M,3), scales (P,3), rotations (P,4), colors_sh (P,3), densify_stats (P,2) (|dL/dmeans2D[:2]| and
-    radii > 0 of this view, gaussian_model.py:175-181), max_radii2D (P,) int32.
+    radii > 0 of this view, gaussian_model.py:175-181), max_radii2D (P,) int32, and campos_rows = (rows (V,3),
+    rank): the multi-view exchange's camera block, written by the backward (campos in row `rank`, zeros elsewhere).
     accumulate_stats=True adds this view's densify_stats to out["densify_stats"] (the reference's
     add_densification_stats); out["max_radii2D"] is always max-accumulated with this view's radii.
     compact_sh=True skips dL/dshs and returns the clamp-masked colour gradient "colors_sh" instead -- the
@@ -220,6 +221,7 @@ def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_
         raise RuntimeError(f"out['max_radii2D'] must be a contiguous int32 tensor of shape ({P},)")
     dscales = dst("scales", P, 3)
     drot = dst("rotations", P, 4)
+    cam_rows, cam_rank, cam_n = _campos_rows(out.get("campos_rows"))
     bufs = _Buffers(device)
     a = _native.BackwardArgs(
         P=P, D=int(rs.sh_degree), M=M, W=W, H=H, R=st.num_rendered, num_big=st.num_big, background=_ptr(st.bg),
@@ -233,7 +235,8 @@ def backward_raw(state: ForwardState, raster_settings, grad_out_color, grad_out_
         dL_dmeans2D=dmeans2D.data_ptr(), dL_dcolors=_ptr(dcolors), dL_dopacity=dopac.data_ptr(),
         dL_dmeans3D=dmeans3D.data_ptr(), dL_dcov3D=_ptr(dcov), dL_dsh=_ptr(dsh),
         dL_dscales=dscales.data_ptr(), dL_drotations=drot.data_ptr(), dL_dcolors_sh=_ptr(dcsh),
-        densify_stats=_ptr(dstats), densify_accumulate=int(bool(accumulate_stats)), max_radii2D=_ptr(mrad))
+        densify_stats=_ptr(dstats), densify_accumulate=int(bool(accumulate_stats)), max_radii2D=_ptr(mrad),
+        campos_rows=cam_rows, campos_rank=cam_rank, campos_nrows=cam_n)
     with torch.cuda.device(device):
         rc = lib.gsr_backward(ctypes.byref(a), bufs.callback, None, _stream_handle(device))
     bufs.raise_pending()
@@ -288,7 +291,10 @@ def backward_chunked(state: ForwardState, raster_settings, grad_out_color, grad_
                       colors_sh=3, densify_stats=2)
         for k, (g0, g1, out) in enumerate(chunks):
             n = int(g1) - int(g0)
+            cam_rows, cam_rank, cam_n = _campos_rows(out.get("campos_rows"))
             for name, t in out.items():
+                if name == "campos_rows":
+                    continue
                 want = (torch.int32, (n,)) if name == "max_radii2D" else (torch.float32, None)
                 if t.dtype != want[0] or not t.is_contiguous() or t.shape[0] != n or (
                         name in widths and t.numel() != n * widths[name]):
@@ -302,12 +308,25 @@ def backward_chunked(state: ForwardState, raster_settings, grad_out_color, grad_
                 dL_dcov3D=_ptr(out.get("cov3D")), dL_dsh=None if compact_sh else _ptr(out.get("shs")),
                 dL_dscales=_ptr(out.get("scales")), dL_drotations=_ptr(out.get("rotations")),
                 dL_dcolors_sh=_ptr(out.get("colors_sh")), densify_stats=_ptr(out.get("densify_stats")),
-                max_radii2D=_ptr(out.get("max_radii2D")), **base)
+                max_radii2D=_ptr(out.get("max_radii2D")), campos_rows=cam_rows, campos_rank=cam_rank,
+                campos_nrows=cam_n, **base)
             rc = lib.gsr_backward(ctypes.byref(a), bufs.callback, None, _stream_handle(device))
             _native.check(rc, f"rasterize_gaussians_backward (chunk {k})")
             if on_chunk is not None:
                 on_chunk(k)
     return scratch
+
+
+def _campos_rows(spec):
+    """(pointer, rank, rows) of an out["campos_rows"] = (rows (V, 3) contiguous float32, rank) entry."""
+    if spec is None:
+        return None, 0, 0
+    rows, rank = spec
+    if rows.dtype != torch.float32 or not rows.is_contiguous() or rows.ndim != 2 or rows.shape[1] != 3:
+        raise RuntimeError("out['campos_rows'] must be (contiguous float32 (V, 3) tensor, rank)")
+    if not 0 <= int(rank) < rows.shape[0]:
+        raise RuntimeError(f"campos_rows rank {rank} outside [0, {rows.shape[0]})")
+    return rows.data_ptr(), int(rank), int(rows.shape[0])
 
 
 class _RasterizeGaussians(torch.autograd.Function):

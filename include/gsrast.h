@@ -135,6 +135,11 @@ typedef struct gsr_backward_args {
     int stages;
     int64_t g_begin, g_end;
     char *bwd_scratch;
+    /* Camera block of the multi-view exchange (multiview.py), written by the per-Gaussian stage so that no extra
+     * launch is needed: campos_rows (campos_nrows, 3) gets campos in row campos_rank and zeros in the others (a
+     * SUM all-reduce of the block then yields every rank's camera).  NULL to skip. */
+    float *campos_rows;
+    int campos_rank, campos_nrows;
 } gsr_backward_args;
 
 enum { GSR_BWD_ALL = 0, GSR_BWD_COMPOSITE = 1, GSR_BWD_GAUSSIANS = 2 };

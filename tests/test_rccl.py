@@ -19,13 +19,13 @@ pytestmark = pytest.mark.gpu
 def _step(red, st, rs, dc, di, means3D, chunked):
     from gaussian_splatting_lightning_amd.rasterizer import backward_chunked, backward_raw
     if chunked:
-        red.begin_step(rs.campos)
+        red.begin_step()
         backward_chunked(st, rs, dc, di, red.chunk_outputs(), on_chunk=red.start_chunk, compact_sh=red.compact,
                          accumulate_stats=True)
         red.finish(means3D)
     else:
         backward_raw(st, rs, dc, di, **red.backward_kwargs())
-        red.reduce(means3D, rs.campos)
+        red.reduce(means3D)
 
 
 def _run(dev, distributed, mode, chunks, views=2, **kw):
@@ -52,6 +52,7 @@ def _run(dev, distributed, mode, chunks, views=2, **kw):
 VARIANTS = [  # (mode, chunks, reducer options): one RCCL group per chunk unless coalesce=False
     ("compact", 4, {}), ("compact", 4, dict(expand="once")), ("dense", 4, {}), ("compact", 1, {}), ("dense", 1, {}),
     ("compact", 4, dict(coalesce=False)), ("compact", 1, dict(sync_ops=False)), ("dense", 1, dict(coalesce=False)),
+    ("compact", 4, dict(comm_stream="pg")), ("compact", 2, dict(comm_stream="side", expand="once")),
 ]
 
 

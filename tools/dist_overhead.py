@@ -48,9 +48,9 @@ def main():
             _, _, _, st = forward_raw(sc.means3D, sc.shs, None, sc.opacities, sc.scales, sc.rotations, None, rs)
             if red.chunks == 1:
                 backward_raw(st, rs, dc, di, **red.backward_kwargs())
-                red.reduce(sc.means3D, cam.campos)
+                red.reduce(sc.means3D)
             else:
-                red.begin_step(cam.campos)
+                red.begin_step()
                 backward_chunked(st, rs, dc, di, red.chunk_outputs(), on_chunk=red.start_chunk,
                                  compact_sh=red.compact, accumulate_stats=True)
                 red.finish(sc.means3D)
@@ -82,6 +82,10 @@ def main():
               "dist_compact4_once_group": dict(mode="compact", chunks=4, expand="once"),
               "dist_compact4_chunk_sep": dict(mode="compact", chunks=4, expand="chunk", coalesce=False),
               "dist_dense4_group": dict(mode="dense", chunks=4),
+              "dist_compact4_chunk_side": dict(mode="compact", chunks=4, expand="chunk", comm_stream="side"),
+              "dist_compact2_chunk_side": dict(mode="compact", chunks=2, expand="chunk", comm_stream="side"),
+              "dist_compact4_once_side": dict(mode="compact", chunks=4, expand="once", comm_stream="side"),
+              "dist_dense4_side": dict(mode="dense", chunks=4, comm_stream="side"),
               "dist_auto": dict(mode="auto", chunks=None)}
     steps = {k: make_step(ViewGradReducer(n, M, cfg["deg"], dev, distributed=False, **kw)) for k, kw in local.items()}
     dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)

@@ -5,7 +5,7 @@
 #   tools/gpu_batch.sh TAG STEP [STEP ...]
 #
 # Steps (arguments after ':' separated by ':'):
-#   tests[:EXPR]              pytest -m gpu (optionally -k EXPR); writes the achieved-parity record parity.json
+#   tests[:EXPR]              pytest -m gpu (optionally -k EXPR, "+" for " or "); writes parity.json
 #   rccl                      tests/test_rccl.py (one-rank RCCL group)
 #   smoke                     __graft_entry__.smoke()
 #   bench[:CFG[:ARGS]]        bench.py --config CFG (ARGS: extra flags, ',' for spaces)
@@ -43,7 +43,7 @@ for step in "$@"; do
   case $kind in
     tests)
       sel=()
-      [ -n "${a1:-}" ] && sel=(-k "$a1")
+      [ -n "${a1:-}" ] && sel=(-k "${a1//+/ or }")
       ALLOW_RC1=1 GSR_PARITY_JSON=$O/parity.json run 600 "tests" python -u -m pytest tests/ -m gpu -v \
         --timeout 120 --timeout-method thread "${sel[@]}" > "$O/gpu_tests_$n.log" 2>&1
       tail -2 "$O/gpu_tests_$n.log" ;;
