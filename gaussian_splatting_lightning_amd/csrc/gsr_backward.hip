@@ -282,7 +282,7 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
 // checkpoint at the segment's end: T = T_e and D = (colour still to come . dL/dpix + T_final bg . dL/dpix) / T_e, the
 // scalar accumulator's value there (D_k T_(k+1) = sum_(j > k) w_j c_j . dL/dpix + T_final bg . dL/dpix).  Without
 // checkpoints every tile is one segment.  Rows agree with the one-walk backward to rounding.
-template <bool HAS_INV, bool LASTC, bool UNION = false, bool SEG = false>
+template <bool HAS_INV, bool LASTC, bool UNION = false, bool SEG = false, bool GUARD = false>
 __global__ __launch_bounds__(64, SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MINW) void render_bwd_v5_kernel(RenderBwdParams p) {
     __shared__ FwdRec s_rec[BWD_BATCH];
     __shared__ __attribute__((aligned(16))) float s_part[BWD_BATCH][PART];  // [instance][10 sums]
@@ -377,6 +377,7 @@ __global__ __launch_bounds__(64, SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MINW) void ren
             const uint32_t s_me = r0 + (uint32_t)(bend - 1 - lane);
             my_row = p.sorted_u[s_me];
             const uint32_t gid = p.point_list[s_me];
+            if (GUARD) s_rec[lane].pad.x = __uint_as_float(gid);  // the guard's slow path reloads the raw record
             my_a = p.rec[gid].a;
             my_b = p.rec[gid].b;
             s_rec[lane].a = stage_rec_a(my_a);
@@ -422,7 +423,15 @@ __global__ __launch_bounds__(64, SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MINW) void ren
                 // !(alpha < 1/255) and, where some lane of the strip may have finished, idx < n_contrib
                 const bool need = (nd[k] >> j) & 1u;  // wave-uniform
                 uint64_t ok = __builtin_amdgcn_fcmpf(power2, 0.0f, FCMP_ULE) &
-                              __builtin_amdgcn_fcmpf(alpha, 1.0f / 255.0f, FCMP_UGE);
+                              __builtin_amdgcn_fcmpf(alpha, GUARD ? GUARD_A_LO : 1.0f / 255.0f, FCMP_UGE);
+                if constexpr (GUARD) {  // the forward's guarded alpha decision, taken by the same test (gsr_common.h)
+                    const uint64_t near = ok & ~__builtin_amdgcn_fcmpf(alpha, GUARD_A_HI, FCMP_UGE);
+                    if (near) {  // rare
+                        const uint32_t g = __float_as_uint(r.pad.x);
+                        const uint64_t okx = __ballot(guard_alpha_pass(p.rec, g, pfx, pfy0 + (float)(4 * k)));
+                        ok = (ok & ~near) | (okx & near);
+                    }
+                }
                 if (need) ok &= __builtin_amdgcn_uicmp(idx, lastc[k], ICMP_ULT);
                 any |= ok;
                 if (!__builtin_amdgcn_inverse_ballot_w64(ok)) continue;  // exec = ok
@@ -577,11 +586,15 @@ void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
     RenderBwdParams q = p;
     q.strip_exact = tuning("strip_exact", 1);
     q.stamps = tuning("stamp", 0) ? stamp_buffer(1) : nullptr;
+    // threshold guard band ("guard" 1, the forward's knob; the segmented and whole-tile walks, not the parts form)
+    const bool gd = tuning("guard", 0) != 0;
     if (p.seg_list && p.ck_flag && p.ckpt && p.ctot && p.seg_count && p.num_tiles <= (int)SEG_MAX_TILES) {
         // segmented walk (800x800, 2500 tiles: one wave per 128-instance segment against 4 part-waves per tile)
         seg_list_kernel<<<1, 1024, 0, s>>>(p.tile_order, p.tile_last, p.num_tiles, p.ck_flag, q.seg_list, q.seg_count);
         const dim3 grid((uint32_t)seg_slots((int64_t)p.num_rendered, (uint32_t)p.num_tiles)), block(64);
-        if (p.dL_dinvdepth) render_bwd_v5_kernel<true, false, false, true><<<grid, block, 0, s>>>(q);
+        if (gd && p.dL_dinvdepth) render_bwd_v5_kernel<true, false, false, true, true><<<grid, block, 0, s>>>(q);
+        else if (gd) render_bwd_v5_kernel<false, false, false, true, true><<<grid, block, 0, s>>>(q);
+        else if (p.dL_dinvdepth) render_bwd_v5_kernel<true, false, false, true><<<grid, block, 0, s>>>(q);
         else render_bwd_v5_kernel<false, false, false, true><<<grid, block, 0, s>>>(q);
         return;
     }
@@ -591,6 +604,7 @@ void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
     int parts = tuning("bwd_parts", 0);
     const int slots = tuning("bwd_part_slots", 12288);
     if (parts == 0) parts = p.num_tiles * 4 <= slots ? 4 : p.num_tiles * 2 <= slots ? 2 : 1;
+    if (gd) parts = 1;
     if (parts == 2 || parts == 4) {
         const dim3 grid(p.num_tiles), block(64 * parts);
         if (p.dL_dinvdepth) {
@@ -610,6 +624,13 @@ void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
     const bool lc = tuning("bwd_lastc", 0) != 0;
     const int un = tuning("bwd_union", -1);
     const bool u = un < 0 ? p.num_rendered > (uint64_t)1024 * (uint64_t)p.num_tiles : un != 0;
+    if (gd) {
+        if (p.dL_dinvdepth && u) render_bwd_v5_kernel<true, false, true, false, true><<<grid, block, 0, s>>>(q);
+        else if (p.dL_dinvdepth) render_bwd_v5_kernel<true, false, false, false, true><<<grid, block, 0, s>>>(q);
+        else if (u) render_bwd_v5_kernel<false, false, true, false, true><<<grid, block, 0, s>>>(q);
+        else render_bwd_v5_kernel<false, false, false, false, true><<<grid, block, 0, s>>>(q);
+        return;
+    }
     if (p.dL_dinvdepth) {
         if (u) render_bwd_v5_kernel<true, false, true><<<grid, block, 0, s>>>(q);
         else if (lc) render_bwd_v5_kernel<true, true><<<grid, block, 0, s>>>(q);

@@ -575,6 +575,34 @@ __device__ __forceinline__ float power2_at(float C, float dy, float P0, float L)
     return fmaf(dy, fmaf(C, dy, L), P0);
 }
 
+// Threshold guard band (knob "guard"; off by default).  The fast alpha above differs from the oracle's
+// expf(power) by a few ulps of the exponent's term magnitudes, so a pair whose alpha lies within that error of 1/255,
+// or whose T (1 - alpha) lies within it of 1e-4, may be decided differently from the oracle (a threshold flip).
+// With the guard, such a pair's DECISIONS are re-taken from the oracle's own arithmetic: the exponent in its
+// uncontracted order from the raw record, and exp in double rounded once to fp32 (the correctly rounded expf, which
+// glibc's equals but for its rare 0.502-ulp misroundings).  The values (alpha in the colour and T updates) stay the
+// fast ones, so the backward, which re-takes the alpha decision by the same test, stays consistent with the forward.
+constexpr float GUARD_A_LO = (1.0f / 255.0f) * (1.0f - 2e-5f), GUARD_A_HI = (1.0f / 255.0f) * (1.0f + 2e-5f);
+// oracle order (gsr_oracle.c render loop): -0.5 (a dx dx + c dy dy) - b dx dy, no contraction; ra = raw rec a
+// (x, y, conic a, conic b), cz = conic c
+__device__ __forceinline__ float guard_power(float4 ra, float cz, float pfx, float pfy) {
+#pragma clang fp contract(off)
+    const float dx = ra.x - pfx, dy = ra.y - pfy;
+    return -0.5f * (ra.z * dx * dx + cz * dy * dy) - ra.w * dx * dy;
+}
+__device__ __forceinline__ float guard_alpha(float power, float o) {
+    return fminf(0.99f, o * (float)exp((double)power));
+}
+// The oracle's alpha decision for Gaussian g at pixel (pfx, pfy): power <= 0 and alpha >= 1/255.  Out of line, so
+// the rare guarded pairs' double-precision exp does not raise the register pressure of the compositing loops.
+static __device__ __attribute__((noinline)) bool guard_alpha_pass(const GRec *__restrict__ rec, uint32_t g, float pfx,
+                                                                  float pfy) {
+    const float4 ra = rec[g].a;
+    const float2 rb = *reinterpret_cast<const float2 *>(&rec[g].b);
+    const float pw = guard_power(ra, rb.x, pfx, pfy);
+    return pw <= 0.0f && guard_alpha(pw, rb.y) >= 1.0f / 255.0f;
+}
+
 // Conservative 4-bit mask of the 4-row strips of a 16-row tile (first row row0) that hold a pixel where
 // the Gaussian can pass the compositor's alpha >= 1/255 test.  a = raw rec_a (x, y, conic a, conic b),
 // b = raw rec_b (conic c, opacity, ...).  alpha = min(0.99, o exp(power)) >= 1/255 needs

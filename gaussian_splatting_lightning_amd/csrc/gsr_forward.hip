@@ -767,7 +767,7 @@ __device__ __forceinline__ unsigned long long prefix_extend(const unsigned long 
     return __shfl(best, (int)cnt - 1);
 }
 
-template <int NPIX, int MIN_WAVES, bool CKPT = false, bool PREFIX = false>
+template <int NPIX, int MIN_WAVES, bool CKPT = false, bool PREFIX = false, bool GUARD = false>
 __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwdParams p) {
     constexpr int PARTS = 4 / NPIX;
     __shared__ FwdRec s_rec[4][64];
@@ -843,6 +843,7 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
             sr[lane].a = stage_rec_a(ga);
             sr[lane].b = stage_rec_b(gb);
             sr[lane].c = p.rec[gid].c;
+            if (GUARD) sr[lane].pad.x = __uint_as_float(gid);  // the guard's slow path reloads the raw record
             m = cell_mask(p.strip_exact, ga, gb, row0, col0) >> kbase;
         }
         uint64_t sk[NPIX];
@@ -876,9 +877,20 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
                 const float test_T = T[k] * (1 - alpha);
                 // lane masks straight from the compares (scalar registers): ok = power2 <= 0 (ordered, so false
                 // for a retired pixel's NaN exponent; power2 is never NaN otherwise) and !(alpha < 1/255)
-                const uint64_t ok = __builtin_amdgcn_fcmpf(power2, 0.0f, FCMP_OLE) &
-                                    __builtin_amdgcn_fcmpf(alpha, 1.0f / 255.0f, FCMP_UGE);
+                // GUARD: the alpha test at the band's lower edge, then the pairs inside the band re-decided (one
+                // extra compare per pair: outside the band alpha >= A_LO <=> alpha >= 1/255)
+                uint64_t ok = __builtin_amdgcn_fcmpf(power2, 0.0f, FCMP_OLE) &
+                              __builtin_amdgcn_fcmpf(alpha, GUARD ? GUARD_A_LO : 1.0f / 255.0f, FCMP_UGE);
                 const uint64_t low = __builtin_amdgcn_fcmpf(test_T, 0.0001f, FCMP_OLT);
+                if constexpr (GUARD) {  // alpha decisions near 1/255 from the oracle's arithmetic (gsr_common.h)
+                    const uint64_t near = ok & ~__builtin_amdgcn_fcmpf(alpha, GUARD_A_HI, FCMP_UGE);
+                    if (near) {  // rare
+                        const uint32_t g = __float_as_uint(sr[j].pad.x);
+                        const uint64_t okx = __ballot(
+                            guard_alpha_pass(p.rec, g, pfx, pfy0 + (float)(4 * (kbase + k))));
+                        ok = (ok & ~near) | (okx & near);
+                    }
+                }
                 const uint64_t take = ok & ~low, stop = ok & low;
                 const float wgt = select_mask(take, alpha * T[k], 0.f);
                 C0[k] = fmaf(b.z, wgt, C0[k]);
@@ -978,6 +990,16 @@ void launch_render_fwd(hipStream_t s, const RenderFwdParams &p0) {
     p.stamps = tuning("stamp", 0) ? stamp_buffer(0) : nullptr;
     const int parts = render_fwd_parts(p.num_tiles);
     const dim3 grid(div_up((uint64_t)p.num_tiles * parts, 4)), block(256);
+    // threshold guard band ("guard" 1; the default launch shapes only, and the backward must run with the same knob)
+    if (tuning("guard", 0) && !(p.tile_sorted && p.bk_keys)) {
+        if (parts == 1) render_fwd_v6_kernel<4, 8, false, false, true><<<grid, block, 0, s>>>(p);
+        else if (parts == 4 && p.ckpt && p.ctot && p.ck_k >= CK_MIN_K && p.ck_k % 32 == 0 &&
+                 (p.ck_k == 32 || p.ck_k % 64 == 0))
+            render_fwd_v6_kernel<1, 8, true, false, true><<<grid, block, 0, s>>>(p);
+        else if (parts == 2) render_fwd_v6_kernel<2, 8, false, false, true><<<grid, block, 0, s>>>(p);
+        else render_fwd_v6_kernel<1, 8, false, false, true><<<grid, block, 0, s>>>(p);
+        return;
+    }
     if (parts == 1) {
         // 8 waves per SIMD (64 VGPRs, one 8-byte spill outside the pair loop): cfg3 0.180 -> 0.172 ms, cfg5 0.517 ->
         // 0.478 ms against 6 waves (65 VGPRs, i.e. 7 resident)

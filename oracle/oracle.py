@@ -51,6 +51,7 @@ def _load():
     lib.oracle_get_image_state.argtypes = [ctypes.c_void_p, _f, _u32]
     lib.oracle_get_geom.argtypes = [ctypes.c_void_p, _f, _f, _f, _f, _u32]
     lib.oracle_threshold_margin.argtypes = [ctypes.c_void_p, _f]
+    lib.oracle_flip_census.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong)]
     lib.oracle_mark_visible.argtypes = [ctypes.c_int, _f, _f, _f, _u8]
     lib.oracle_num_threads.restype = ctypes.c_int
     lib.oracle_bin_count.restype = ctypes.c_longlong
@@ -160,6 +161,13 @@ class OracleRun:
         out = np.zeros(self.W * self.H, dtype=np.float32)
         self._lib.oracle_threshold_margin(self._h, _fp(out))
         return out.reshape(self.H, self.W)
+
+    def flip_census(self) -> dict:
+        """Pixels whose walk under the device composite's fp32 arithmetic (restated on the CPU) first decides
+        differently at the exponent sign / alpha / transmittance test (oracle_flip_census)."""
+        c = (ctypes.c_longlong * 4)()
+        self._lib.oracle_flip_census(self._h, c)
+        return {"pixels": c[0], "power": c[1], "alpha": c[2], "transmittance": c[3]}
 
     def geom(self):
         P = self.P

@@ -1086,3 +1086,47 @@ def test_big_rect_walk_blocks_are_bitwise_the_range_blocks(gpu_device, W, H, n, 
         assert np.array_equal(ref[key], alt[key]), key
     for key in GRADS:
         assert np.array_equal(ref["grads"][key], alt["grads"][key]), key
+
+
+@pytest.mark.parametrize("case", ["cfg1_golden", "cfg3_full", "cfg5_full"])
+def test_threshold_guard_band(gpu_device, case):
+    """Knob "guard" (off by default): pairs whose alpha lies within 2e-5 (relative) of 1/255, or whose
+    T (1 - alpha) within 1e-4 of 1e-4, take their decisions from the oracle's own arithmetic (uncontracted exponent,
+    exp in double).  Contributor counts that differ from the oracle's (threshold flips) must not increase with it, and
+    the guarded forward + backward keep every bar of the unguarded run; achieved flips and all-Gaussian gradient
+    errors of both runs go to the parity record."""
+    from gaussian_splatting_lightning_amd import _native
+    if case == "cfg1_golden":
+        z = load_golden("cfg1_10k_256_sh0")
+        inp = golden_inputs(z)
+        dc, di = z["dL_dcolor"], z["dL_dinvdepth"]
+    elif case == "cfg3_full":
+        inp = scene_inputs(1_000_000, 1920, 1080, sh_degree=3, seed=0)
+        dc, di = upstream(1920, 1080, 0)
+    else:
+        inp = scene_inputs(5_000_000, 3840, 2160, sh_degree=3, seed=0, stress_fraction=0.01)
+        dc, di = upstream(3840, 2160, 0)
+    out = run_oracle(inp)
+    run = out[3]
+    g = run.backward(dc, di)
+    _, nc_ref = run.image_state()
+    rec = {}
+    try:
+        for guard in (0, 1):
+            _native.set_tuning("guard", guard)
+            hip = run_hip(inp, gpu_device, dc, di)
+            nc = hip_state_arrays(hip)["n_contrib"]
+            e = {"n_contrib_mismatch_pixels": int((nc != nc_ref).sum()),
+                 "color_maxabs": float(np.abs(hip["color"] - out[0]).max())}
+            for k in GRADS:
+                if hip["grads"].get(k) is not None:
+                    e[f"grad_rel_l2_{k}"] = rel_l2(hip["grads"][k], g[k])
+            rec[f"guard{guard}"] = e
+    finally:
+        _native.set_tuning("guard", 0)
+    parity.record(_case(), "guard_band", rec)
+    assert rec["guard1"]["n_contrib_mismatch_pixels"] <= rec["guard0"]["n_contrib_mismatch_pixels"], rec
+    assert rec["guard1"]["color_maxabs"] <= max(2 * rec["guard0"]["color_maxabs"], 1e-5), rec
+    for k in GRADS:
+        if f"grad_rel_l2_{k}" in rec["guard1"]:
+            assert rec["guard1"][f"grad_rel_l2_{k}"] <= max(2 * rec["guard0"][f"grad_rel_l2_{k}"], 1e-5), rec
