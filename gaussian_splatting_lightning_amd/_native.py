@@ -83,11 +83,12 @@ PLY_TYPES = {"float": 0, "float32": 0, "double": 1, "float64": 1, "uchar": 2, "u
 PLY_TYPE_SIZE = (4, 8, 1, 1, 2, 2, 4, 4)
 
 
-class StateLayout(ctypes.Structure):
+class StateLayout(ctypes.Structure):  # include/gsrast.h gsr_state_layout (versioned by struct_size)
     _fields_ = [(n, ctypes.c_size_t) for n in (
-        "geom_rec_a", "geom_rec_b", "geom_rec_c", "geom_tiles", "geom_order", "geom_inst_off", "geom_inst_start",
-        "geom_clamped", "geom_depth_key", "geom_expand_rec", "bin_point_list", "bin_inv", "bin_keys_sorted", "bin_sorted_u", "bin_inst_gid",
-        "img_final_T", "img_n_contrib", "img_ranges", "img_tile_last", "img_tile_loaded", "geom_rec_stride", "img_tile_sorted", "bin_bk_keys", "img_tile_lastkey")]
+        "struct_size", "geom_rec_a", "geom_rec_b", "geom_rec_c", "geom_tiles", "geom_order", "geom_inst_off",
+        "geom_inst_start", "geom_clamped", "geom_depth_key", "geom_expand_rec", "bin_point_list", "bin_inv",
+        "bin_keys_sorted", "bin_sorted_u", "bin_inst_gid", "img_final_T", "img_n_contrib", "img_ranges",
+        "img_tile_last", "img_tile_loaded", "geom_rec_stride", "bin_bk_keys")]
 
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t)
@@ -231,9 +232,13 @@ def stage_mask(*names: str) -> int:
 
 
 def state_layout(P: int, R: int, W: int, H: int) -> dict:
+    """Byte offsets of the forward buffers' arrays; only the fields the loaded library filled (struct_size)."""
     out = StateLayout()
+    out.struct_size = ctypes.sizeof(StateLayout)
     load().gsr_state_layout_query(int(P), int(R), int(W), int(H), ctypes.byref(out))
-    return {name: getattr(out, name) for name, _ in StateLayout._fields_}
+    filled = out.struct_size or ctypes.sizeof(StateLayout)
+    return {name: getattr(out, name) for name, _ in StateLayout._fields_[1:]
+            if getattr(StateLayout, name).offset + ctypes.sizeof(ctypes.c_size_t) <= filled}
 
 
 def set_tuning(name: str, value: int) -> None:

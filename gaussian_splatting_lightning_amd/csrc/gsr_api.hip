@@ -378,8 +378,13 @@ size_t gsr_image_buffer_bytes(int W, int H) {
 }
 size_t gsr_bwd_scratch_bytes(int64_t R, int64_t num_big) { return bwd_scratch_bytes(R, num_big); }
 
-void gsr_state_layout_query(int P, int64_t R, int W, int H, gsr_state_layout *out) {
-    if (!out) return;
+void gsr_state_layout_query(int P, int64_t R, int W, int H, gsr_state_layout *caller) {
+    if (!caller) return;
+    // versioned: fill a full struct here, copy back only the caller's size (fields are only appended)
+    const size_t want = caller->struct_size ? std::min(caller->struct_size, sizeof(gsr_state_layout))
+                                            : sizeof(gsr_state_layout);
+    gsr_state_layout full{};
+    gsr_state_layout *out = &full;
     char *const base = reinterpret_cast<char *>(size_t(1) << 40);  // any aligned non-null base
     auto off = [&](const void *p) { return (size_t)(reinterpret_cast<const char *>(p) - base); };
     GeomState g;
@@ -406,13 +411,13 @@ void gsr_state_layout_query(int P, int64_t R, int W, int H, gsr_state_layout *ou
     out->bin_sorted_u = off(b.sorted_u);
     out->bin_inst_gid = off(b.inst_gid);
     out->img_tile_loaded = off(im.tile_loaded);
-    out->img_tile_sorted = off(im.tile_sorted);
     out->bin_bk_keys = off(b.bk_keys);
-    out->img_tile_lastkey = off(im.tile_lastkey);
     out->img_final_T = off(im.final_T);
     out->img_n_contrib = off(im.n_contrib);
     out->img_ranges = off(im.ranges);
     out->img_tile_last = off(im.tile_last);
+    full.struct_size = want;
+    memcpy(caller, &full, want);
 }
 
 int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *stream_ptr,
@@ -520,14 +525,14 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
         bp.tiles = g.tiles; bp.inst_start = g.inst_start; bp.block_sums = g.block_sums; bp.depth_key = g.depth_key;
         bp.big_list = g.big_list; bp.exp_rec = g.exp_rec;
         bp.hist = im.bk_hist; bp.hist_pre = im.bk_hist_pre; bp.tile_next = im.bk_tile_next; bp.reg_start = im.bk_reg_start; bp.tile_start = im.bk_tile_start; bp.ranges = im.ranges;
-        bp.tile_last = im.tile_last; bp.tile_loaded = im.tile_loaded; bp.tile_lastkey = im.tile_lastkey;
+        bp.tile_last = im.tile_last; bp.tile_loaded = im.tile_loaded;
         bp.lpt_bcnt = im.lpt_bcnt;
         bp.ticket = g.counters + CNT_COL_TICKET; bp.tile_status = g.tile_status; bp.err = g.counters + CNT_OVERFLOW;
         bp.long_list = im.bk_long_list; bp.long_cnt = g.counters + CNT_LONG;
         bp.lb_patience = (uint32_t)tuning("lb_patience", 1 << 16); bp.lb_force = tuning("lb_force", 0);
         bp.xcd_major = tuning("bk_xcd", 1);
         // every buffer the column pass clears must be wired (a null one would fault the GPU, not fail here)
-        if (!bp.tile_last || !bp.tile_loaded || !bp.tile_lastkey || !bp.ranges || !bp.tile_start || !bp.hist_pre)
+        if (!bp.tile_last || !bp.tile_loaded || !bp.ranges || !bp.tile_start || !bp.hist_pre)
             return fail(GSR_ERR_ARG, "internal: bucket binning buffer not set");
         GSR_STAGE(ST_BK_COUNT, dbg, launch_bucket_count(stream, bp));
     }
@@ -577,7 +582,6 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     // Otherwise the radix path: depth sort, depth-ordered expansion, stable tile sort.
     const bool bucket = bk_possible && (bk == 2 || (uint64_t)R <= (uint64_t)BK_MAX_MEAN * T);
     bool sorted_exp = false;
-    bool prefix = false;  // prefix binning: buckets sorted only up to tile_sorted (render_fwd extends them)
     bool depth_onesweep = false, tile_onesweep = false;  // which sorts ran on the onesweep path (diagnostics)
     if (bucket) gsr_set_tuning("stat_depth_passes", 0);
     if (!bucket) {
@@ -652,19 +656,9 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
                                 ? im.order_fwd : nullptr; sp.keys = b.bk_keys; sp.keys2 = b.bk_keys2;
             sp.sorted_u = b.sorted_u; sp.long_list = im.bk_long_list; sp.long_cnt = g.counters + CNT_LONG;
             sp.tie_list = im.bk_tie_list; sp.tie_cnt = g.counters + CNT_TIES;
-            // prefix binning ("bk_prefix" instances, a multiple of 64 <= 512; 0: sort every bucket whole) where the
-            // composite runs whole tiles: tiles longer than that get only their front-most instances sorted, and a
-            // walk that outlives them selects its further batches itself (render_fwd)
-            // Measured at cfg 3 (profiles/r4d_ab_prefix_cfg3.txt): seg_sort 0.053 -> 0.060 ms and render_fwd 0.171 ->
-            // 0.176 ms with 512-instance prefixes (the radix select's passes over a long bucket cost more than the
-            // bitonic sort they spare), so whole sorts are the default.
-            const int pk = tuning("bk_prefix", 0);
-            if (pk > 0 && render_fwd_parts((int)T) == 1) {
-                sp.prefix_k = (uint32_t)std::min(512, std::max(64, pk / 64 * 64));
-                sp.tile_sorted = im.tile_sorted;
-                sp.tile_thresh = im.tile_thresh;
-                prefix = true;
-            }
+            // (Round 4's prefix binning -- radix-select each long bucket's 512 front-most keys, sort only those, and
+            // let render_fwd extend a walk that outlives them -- measured slower at cfg 3, seg_sort 0.053 -> 0.060 ms
+            // and render_fwd 0.171 -> 0.176 ms, and was removed in round 5: DESIGN.md appendix)
             GSR_STAGE(ST_SEG_SORT, dbg, launch_seg_sort(stream, sp));
         } else {
             GSR_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * T, stream));
@@ -713,17 +707,11 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     rp.tile_order = lpt ? im.order_fwd : nullptr;
     rp.ranges = im.ranges; rp.sorted_u = b.sorted_u; rp.inst_gid = b.inst_gid;
     rp.point_list = b.point_list; rp.tile_loaded = im.tile_loaded;
-    rp.depth_key = g.depth_key; rp.tile_lastkey = im.tile_lastkey;
     rp.inv = b.inv;
     rp.rec = g.rec;
     rp.bg = a->background;
     rp.out_color = a->out_color; rp.out_invdepth = a->out_invdepth; rp.final_T = im.final_T;
     rp.n_contrib = im.n_contrib; rp.tile_last = im.tile_last;
-    rp.prefix_flag = im.tile_sorted + T;
-    if (prefix) {
-        rp.bk_keys = b.bk_keys; rp.tile_sorted = im.tile_sorted; rp.tile_thresh = im.tile_thresh;
-        rp.sorted_u_w = b.sorted_u;
-    }
     // checkpoints for the segmented backward ("bwd_seg" 1, spacing "seg_k" instances: 32 or a multiple of 64) while the image
     // has few tiles; the forward records in ck_flag whether it wrote them, so the backward never reads stale ones
     rp.ck_flag = im.ck_flag;
@@ -737,7 +725,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
         const int k = tuning("seg_k", 64);  // cfg 2: 32 / 64 / 128 -> render_bwd 0.106 / 0.107 / 0.129 ms, render_fwd 0.070 / 0.065 / 0.062
         rp.ck_k = k <= 32 ? 32u : (uint32_t)(k / 64) * 64u;
     }
-    if (R > 0 && (!rp.depth_key || !rp.tile_lastkey || !rp.point_list || !rp.inst_gid || !rp.sorted_u))
+    if (R > 0 && (!rp.point_list || !rp.inst_gid || !rp.sorted_u))
         return fail(GSR_ERR_ARG, "internal: composite buffer not set");
     GSR_STAGE(ST_RENDER_FWD, dbg, launch_render_fwd(stream, rp));
     (void)depth_onesweep;

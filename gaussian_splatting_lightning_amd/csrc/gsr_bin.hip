@@ -310,7 +310,6 @@ __global__ __launch_bounds__(64 * CW) void bk_columns_kernel(BucketParams p) {
             if (t % BK_REGION == 0) p.reg_start[t / BK_REGION] = st;  // compact region starts (the region partition)
             p.tile_last[t] = 0u;
             p.tile_loaded[t] = 0u;
-            p.tile_lastkey[t] = 0ull;
             if (t == T - 1) {
                 p.tile_start[T] = st + tot;
                 p.reg_start[(T + BK_REGION - 1) / BK_REGION] = st + tot;
@@ -815,135 +814,6 @@ __device__ __forceinline__ bool seg_lds_sort(const unsigned long long *__restric
     return true;
 }
 
-// Prefix binning: the K front-most instances of a long tile (K < n, K <= 512), sorted, into sorted_u[start, start + K).
-// At cfg 3 every tile longer than 511 instances stops compositing before instance 410 (the oracle's tile_last), so
-// sorting its whole bucket is wasted work; render_fwd extends the prefix in the rare tile whose walk outlives it.
-// 1. the workgroup radix-selects the K-th smallest key: keys are taken relative to the tile's smallest depth (r = key
-//    - dmin << 32, same order), digits of 8 bits from the top significant one; per round an LDS histogram of the next
-//    digit over the keys still in the candidate bin, and one wave finds the bin holding rank k.  It stops as soon as
-//    that whole bin lies inside the K smallest (keys are unique: at the lowest digit a bin holds one key), so the
-//    selection is the keys whose digit prefix is <= the found prefix -- exactly K of them;
-// 2. the selected keys are compacted into LDS and wave 0 sorts them (the 32-bit proxy network, seg_sort_wave32).
-// Returns false if the proxy sort met a tie run it could not order (nothing written): the tile's sorted length is 0 and
-// render_fwd selects every batch itself.  *thresh = the largest selected key.  Uses 10 KB of s_x.
-__device__ bool seg_prefix_sort(const unsigned long long *__restrict__ keys, uint32_t start, uint32_t n, uint32_t K,
-                                uint32_t *__restrict__ sorted_u, unsigned long long *s_x, int w, int lane,
-                                unsigned long long *thresh) {
-    uint32_t *hist = reinterpret_cast<uint32_t *>(s_x);  // 256 bins
-    uint32_t *misc = hist + 256;                          // 64 words of broadcast scratch
-    unsigned long long *cbuf = s_x + 192;                 // K selected keys (from byte 1536)
-    unsigned long long *scr = cbuf + 512;                 // the proxy sort's gather scratch
-    const int tid = threadIdx.x;
-    const unsigned long long *k0 = keys + start;
-    // depth range
-    uint32_t dmin = 0xffffffffu, dmax = 0u;
-    for (uint32_t i = tid; i < n; i += 256) {
-        const uint32_t d = (uint32_t)(k0[i] >> 32);
-        dmin = min(dmin, d);
-        dmax = max(dmax, d);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        dmin = min(dmin, (uint32_t)__shfl_xor((int)dmin, o));
-        dmax = max(dmax, (uint32_t)__shfl_xor((int)dmax, o));
-    }
-    if (lane == 0) {
-        misc[w] = dmin;
-        misc[4 + w] = dmax;
-    }
-    __syncthreads();
-    dmin = min(min(misc[0], misc[1]), min(misc[2], misc[3]));
-    dmax = max(max(misc[4], misc[5]), max(misc[6], misc[7]));
-    const unsigned long long base = (unsigned long long)dmin << 32;
-    const uint32_t range = dmax - dmin;
-    const int top = 32 + (range ? 32 - __builtin_clz(range) : 0);  // r < 2^top
-    int sh = ((top - 1) / 8) * 8;                                   // digits at multiples of 8 bits
-    unsigned long long P = 0;  // digits fixed so far (r >> (sh + 8) must equal P)
-    uint32_t k = K;            // rank (1-based) of the wanted key inside the candidate bin
-    __syncthreads();           // misc is reused below
-    while (true) {
-        for (int i = tid; i < 256; i += 256) hist[i] = 0u;
-        __syncthreads();
-        for (uint32_t i = tid; i < n; i += 256) {
-            const unsigned long long r = k0[i] - base;
-            const bool in = sh + 8 >= 64 || (r >> (sh + 8)) == P;
-            if (in) atomicAdd(&hist[(uint32_t)(r >> sh) & 255u], 1u);
-        }
-        __syncthreads();
-        if (w == 0) {  // bin holding rank k: lane l scans bins 4l .. 4l + 3
-            uint32_t h[4], sum = 0;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                h[q] = hist[4 * lane + q];
-                sum += h[q];
-            }
-            uint32_t before = wave_inclusive_scan(sum, lane) - sum;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (before < k && k <= before + h[q]) {
-                    misc[8] = (uint32_t)(4 * lane + q);
-                    misc[9] = before;
-                    misc[10] = h[q];
-                }
-                before += h[q];
-            }
-        }
-        __syncthreads();
-        const uint32_t d = misc[8], before = misc[9], hd = misc[10];
-        k -= before;
-        P = (P << 8) | d;
-        __syncthreads();  // every thread has read misc before the next round rewrites it
-        if (hd == k || sh == 0) break;  // the whole bin is inside the K smallest (at sh == 0 it holds one key)
-        sh -= 8;
-    }
-    // compaction of the selected keys ((r >> sh) <= P) into cbuf, in thread order
-    uint32_t c = 0;
-    unsigned long long kmax = 0;
-    for (uint32_t i = tid; i < n; i += 256) {
-        const unsigned long long key = k0[i];
-        if (((key - base) >> sh) <= P) {
-            c++;
-            kmax = key > kmax ? key : kmax;
-        }
-    }
-    const uint32_t inc = wave_inclusive_scan(c, lane);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long y = __shfl_xor(kmax, o);
-        kmax = y > kmax ? y : kmax;
-    }
-    if (lane == 63) misc[16 + w] = inc;
-    if (lane == 0) reinterpret_cast<unsigned long long *>(misc + 24)[w] = kmax;
-    __syncthreads();
-    uint32_t pos = inc - c;
-    for (int q = 0; q < w; q++) pos += misc[16 + q];
-    for (uint32_t i = tid; i < n; i += 256) {
-        const unsigned long long key = k0[i];
-        if (((key - base) >> sh) <= P && pos < 512u) cbuf[pos++] = key;  // exactly K <= 512 are selected
-    }
-    __syncthreads();
-    if (w == 0) {
-        unsigned long long y[8];
-        const bool ok = seg_sort_wave32<8>(cbuf, 0, K, scr, lane, y);
-        if (ok) {
-            const uint32_t b = (uint32_t)lane * 8;
-#pragma unroll
-            for (int r = 0; r < 8; r++)
-                if (b + r < K) sorted_u[start + b + r] = (uint32_t)y[r];
-        }
-        if (lane == 0) misc[12] = ok ? 1u : 0u;
-    }
-    __syncthreads();
-    const bool ok = misc[12] != 0;
-    const unsigned long long *km = reinterpret_cast<const unsigned long long *>(misc + 24);
-    unsigned long long t = km[0];
-#pragma unroll
-    for (int q = 1; q < 4; q++) t = km[q] > t ? km[q] : t;
-    *thresh = t;
-    __syncthreads();  // s_x is reused by the next tile
-    return ok;
-}
-
 // Every tile up to SEG_BLOCK_CAP instances, in one persistent launch (the workgroups loop over the tiles, whose
 // counts are only known on the device, so every wave reaches the exit), on 32-bit proxy keys (P32, else on
 // the 64-bit keys: the A/B reference, knob "seg32"):
@@ -960,34 +830,19 @@ __global__ __launch_bounds__(256, MIN_WAVES) void seg_sort_kernel(SegSortParams 
     if (threadIdx.x == 0) s_flag = 0u;
     __syncthreads();
     const uint32_t n0 = p.long_cnt[0], nlong = n0 + p.long_cnt[1];
-    const uint32_t pk = p.prefix_k;
-    const uint32_t nl = (p.tile_order || pk) ? nlong : n0;  // prefix mode takes the > SEG_BLOCK_CAP tiles here too
+    const uint32_t nl = p.tile_order ? nlong : n0;
     for (uint32_t i = blockIdx.x; i < nl; i += gridDim.x) {
-        const uint32_t tile = p.tile_order ? p.tile_order[i] : (i < n0 ? p.long_list[i] : p.long_list[p.T + 1 + (i - n0)]);
+        const uint32_t tile = p.tile_order ? p.tile_order[i] : p.long_list[i];
         const uint2 rg = p.ranges[tile];
         const uint32_t n = rg.y - rg.x;
-        if (n <= SEG_CAP) continue;  // workgroup-uniform
-        if (pk && n > pk) {
-            unsigned long long th = 0;
-            const bool ok = seg_prefix_sort(p.keys, rg.x, n, pk, p.sorted_u, s_x, w, lane, &th);
-            if (threadIdx.x == 0) {
-                p.tile_sorted[tile] = ok ? pk : 0u;
-                p.tile_thresh[tile] = ok ? th : 0ull;
-            }
-            continue;
-        }
-        if (n > SEG_BLOCK_CAP) continue;
+        if (n <= SEG_CAP || n > SEG_BLOCK_CAP) continue;  // workgroup-uniform
         const uint32_t t0 = p.stamps ? stamp_now() : 0u;
         uint32_t t1 = 0;
         if (!seg_lds_sort<P32>(p.keys, rg.x, n, p.sorted_u, nullptr, s_x, w, lane, &s_flag, i + 1u,
                                p.stamps ? &t1 : nullptr)) {
-            if (threadIdx.x == 0) {
-                if (pk) p.tile_sorted[tile] = 0u;  // render_fwd selects every batch of this tile
-                else p.tie_list[atomicAdd(p.tie_cnt, 1u)] = tile;
-            }
+            if (threadIdx.x == 0) p.tie_list[atomicAdd(p.tie_cnt, 1u)] = tile;
             continue;
         }
-        if (pk && threadIdx.x == 0) p.tile_sorted[tile] = n;
         if (p.stamps && threadIdx.x == 0 && i < (uint32_t)STAMP_SLOTS) p.stamps[i] = make_uint4(t0, t1, stamp_now(), n);
     }
     const uint32_t s0 = p.tile_order ? nlong : 0u;
@@ -1004,10 +859,7 @@ __global__ __launch_bounds__(256, MIN_WAVES) void seg_sort_kernel(SegSortParams 
         else if (n <= 128u) ok = seg_sort_wave<2, P32>(p.keys, rg.x, n, p.sorted_u, lane, scratch);
         else if (n <= 256u) ok = seg_sort_wave<4, P32>(p.keys, rg.x, n, p.sorted_u, lane, scratch);
         else ok = seg_sort_wave<8, P32>(p.keys, rg.x, n, p.sorted_u, lane, scratch);
-        if (lane == 0) {
-            if (pk) p.tile_sorted[tile] = ok ? n : 0u;
-            else if (!ok) p.tie_list[atomicAdd(p.tie_cnt, 1u)] = tile;
-        }
+        if (lane == 0 && !ok) p.tie_list[atomicAdd(p.tie_cnt, 1u)] = tile;
     }
 }
 
@@ -1107,7 +959,6 @@ void launch_seg_sort(hipStream_t s, const SegSortParams &p0) {
     else if (tuning("seg32", 1) && minw == 5) seg_sort_kernel<true, 5><<<grid, 256, 0, s>>>(p);
     else if (tuning("seg32", 1)) seg_sort_kernel<true><<<grid, 256, 0, s>>>(p);
     else seg_sort_kernel<false><<<grid, 256, 0, s>>>(p);
-    if (p.prefix_k) return;  // prefix mode: no tile is left to seg_huge (ties: render_fwd's selection)
     constexpr uint32_t HUGE_LDS_KEYS = 8192;  // 64 KB
     seg_huge_kernel<<<512, 256, HUGE_LDS_KEYS * sizeof(unsigned long long), s>>>(p, HUGE_LDS_KEYS);
 }

@@ -247,8 +247,6 @@ struct ImageState {
     uint2 *ranges;        // T
     uint32_t *tile_last;  // T: max n_contrib over the tile's pixels
     uint32_t *tile_loaded; // T: instances of the tile the forward composite gathered (>= tile_last)
-    unsigned long long *tile_lastkey;  // T: key (depth bits << 32 | u) of the last instance the composite gathered, 0 if
-                                       //    none (zeroed with tile_last / tile_loaded; a diagnostic the tests check)
     uint32_t *lpt_bcnt;    // 256: tiles per backward LPT bucket, appended by the forward's whole-tile waves (cleared
                            //      with tile_last / tile_loaded)
     uint32_t *order_fwd;   // tiles in descending forward work (instances in range), LPT launch order
@@ -272,10 +270,6 @@ struct ImageState {
     uint32_t *lpt_hist;      // (T / 4096 + 1) x 256: per-workgroup bucket histograms of the multi-workgroup LPT order
     uint32_t *lpt_blist;     // 256 x T in lpt_append_range (else 1): bucket b's tiles at [b T, b T + lpt_bcnt[b])
     uint32_t *lpt_valid;     // 1 when this forward appended every tile to the bucket lists, else 0
-    // prefix binning (bucket path, whole-tile composite): per tile the sorted length of its bucket and the largest
-    // sorted key (SegSortParams::prefix_k)
-    uint32_t *tile_sorted;   // T
-    unsigned long long *tile_thresh;  // T
 };
 // Between these tile counts the forward's whole-tile waves append each finished tile to its backward LPT bucket, so
 // the backward needs no ordering launch (1080p, 8160 tiles: step -13 us).  At 4K (32400 tiles of similar weight in a
@@ -292,7 +286,6 @@ inline size_t carve_image(char *base, int W, int H, ImageState &im) {
     im.ranges = c.take<uint2>((size_t)gx * gy + 1);
     im.tile_last = c.take<uint32_t>((size_t)gx * gy + 1);
     im.tile_loaded = c.take<uint32_t>((size_t)gx * gy + 1);
-    im.tile_lastkey = c.take<unsigned long long>((size_t)gx * gy + 1);  // inside the range the radix path zeroes
     im.lpt_bcnt = c.take<uint32_t>(256);
     im.order_fwd = c.take<uint32_t>((size_t)gx * gy + 1);
     im.order_bwd = c.take<uint32_t>((size_t)gx * gy + 1);
@@ -310,8 +303,6 @@ inline size_t carve_image(char *base, int W, int H, ImageState &im) {
     im.lpt_hist = c.take<uint32_t>((nt / 4096 + 1) * 256);
     im.lpt_blist = c.take<uint32_t>(lpt_append_range((uint32_t)nt) ? 256 * nt : 1);
     im.lpt_valid = c.take<uint32_t>(1);
-    im.tile_sorted = c.take<uint32_t>(nt + 1);
-    im.tile_thresh = c.take<unsigned long long>(nt + 1);
     return c.off + 256;
 }
 

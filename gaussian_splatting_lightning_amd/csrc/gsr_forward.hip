@@ -713,9 +713,9 @@ void launch_tile_order(hipStream_t s, const uint2 *ranges, const uint32_t *tile_
 // would take T below 1e-4.  No block barriers: the four waves of a block work on four independent tiles.
 // The batch gather also materialises, for exactly the instances it loads, the sorted Gaussian id list
 // (point_list) the backward walks and the inverse permutation inv[u] = s the backward's per-Gaussian gather reads
-// (the binning filled it with INV_NONE: no row), and per tile the key of the last instance it loaded (tile_lastkey).
-// (Round 4 replaced inv by testing each row against tile_lastkey in the backward: preprocess_bwd 0.094 -> 0.118 ms at
-// cfg 3 for the row-tile search, for ~3 us of forward stores saved; measured and reverted.)
+// (the binning filled it with INV_NONE: no row).  (Round 4 replaced inv by testing each row against a per-tile key of
+// the last loaded instance in the backward: preprocess_bwd 0.094 -> 0.118 ms at cfg 3 for the row-tile search, for
+// ~3 us of forward stores saved; measured and reverted, and round 5 removed the per-tile key.)
 // Every piece of per-instance control is wave-uniform: the tile, its range and the contributor counter live
 // in SGPRs, each batch's strip masks (cell_mask) are ballots (bit j = instance j can reach the strip), and the
 // records of a batch sit in one LDS array of 48-byte entries read with immediate offsets.
@@ -731,43 +731,7 @@ void launch_tile_order(hipStream_t s, const uint2 *ranges, const uint32_t *tile_
 // + j), and at the end the pixel's final sums (ctot); the backward walks each ck_k-instance segment from the
 // checkpoint at its end.  A pixel still compositing at instance e is still walked when its wave reaches e, so every
 // checkpoint the backward reads (e < the pixel's n_contrib) is written.
-// Prefix binning (seg_sort sorted only a tile's front-most instances): the next batch of a walk that outlives the
-// sorted prefix -- the cnt smallest bucketed keys of the tile above `last` (all keys when `none`), sorted, written to
-// out[0, cnt) -- selected by the wave in one pass over the tile's n keys: each 64-key chunk is sorted descending across
-// the lanes (bitonic, one key per lane) and merged into the running ascending best-64 (elementwise min, then a
-// bitonic clean).  Returns the largest selected key.  ~160 VALU per 64 keys of the tile: a slow path for the rare
-// tile that composites past its prefix (none at cfg 3).
-__device__ __forceinline__ unsigned long long u64_sel(bool take_min, unsigned long long a, unsigned long long b) {
-    return take_min == (a < b) ? a : b;
-}
-__device__ __forceinline__ unsigned long long prefix_extend(const unsigned long long *__restrict__ keys, uint32_t n,
-                                                            bool none, unsigned long long last,
-                                                            uint32_t *__restrict__ out, uint32_t cnt, int lane,
-                                                            uint32_t &mine) {
-    unsigned long long best = ~0ull;
-    for (uint32_t c0 = 0; c0 < n; c0 += 64) {
-        unsigned long long x = c0 + lane < n ? keys[c0 + lane] : ~0ull;
-        if (!none && x <= last) x = ~0ull;
-        if (__ballot(x != ~0ull) == 0) continue;
-        for (int k = 2; k <= 64; k <<= 1) {      // descending bitonic sort of the chunk
-            const bool desc = k == 64 || (lane & k) == 0;
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                const unsigned long long y = __shfl_xor(x, j);
-                x = u64_sel(((lane & j) == 0) != desc, x, y);
-            }
-        }
-        best = best < x ? best : x;              // the 64 smallest of both, as a bitonic sequence
-        for (int j = 32; j > 0; j >>= 1) {       // clean it ascending
-            const unsigned long long y = __shfl_xor(best, j);
-            best = u64_sel((lane & j) == 0, best, y);
-        }
-    }
-    mine = (uint32_t)best;  // this lane's instance of the batch (its expansion index)
-    if ((uint32_t)lane < cnt) out[lane] = mine;
-    return __shfl(best, (int)cnt - 1);
-}
-
-template <int NPIX, int MIN_WAVES, bool CKPT = false, bool PREFIX = false, bool GUARD = false>
+template <int NPIX, int MIN_WAVES, bool CKPT = false, bool GUARD = false>
 __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwdParams p) {
     constexpr int PARTS = 4 / NPIX;
     __shared__ FwdRec s_rec[4][64];
@@ -776,7 +740,6 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
     const int slot = blockIdx.x * 4 + w;
     if (p.ck_flag && slot == 0 && lane == 0) *p.ck_flag = CKPT ? p.ck_k : 0u;
     if (p.lpt_valid && slot == 0 && lane == 0) *p.lpt_valid = (PARTS == 1 && p.lpt_blist) ? 1u : 0u;
-    if (p.prefix_flag && slot == 0 && lane == 0) *p.prefix_flag = PREFIX ? 1u : 0u;
     if (slot >= p.num_tiles * PARTS) return;
     const int half = slot % PARTS;
     const int tile = __builtin_amdgcn_readfirstlane(p.tile_order ? (int)p.tile_order[slot / PARTS] : slot / PARTS);
@@ -804,12 +767,7 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
     const uint32_t r0 = __builtin_amdgcn_readfirstlane(rg.x), r1 = __builtin_amdgcn_readfirstlane(rg.y);
     uint32_t contributor = 0;
     uint32_t loaded_end = r0;
-    uint32_t u_last = 0, g_last = 0;  // the last loaded instance (its key is recorded per tile)
     FwdRec *sr = s_rec[w];
-    // prefix binning: instances [r0, r0 + ks) are sorted; a walk past them selects further batches itself
-    uint32_t ks = PREFIX ? __builtin_amdgcn_readfirstlane(p.tile_sorted[tile]) : 0u;
-    const uint32_t ks0 = ks;
-    unsigned long long last_key = PREFIX && ks ? p.tile_thresh[tile] : 0ull;
     // checkpoint before tile-relative instance e (a multiple of ck_k)
     auto store_ck = [&](uint32_t e) {
         float *ck = p.ckpt + (size_t)(r0 / p.ck_k + (uint32_t)tile + e / p.ck_k - 1) * CK_FLOATS;
@@ -825,18 +783,11 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
     };
     for (uint32_t base = r0; base < r1; base += 64) {
         if (CKPT && base > r0 && (base - r0) % p.ck_k == 0) store_ck(base - r0);
-        uint32_t u_sel = 0;
-        const bool ext = PREFIX && base >= r0 + ks;  // batch boundary: ks is a multiple of 64 or the whole tile
-        if (ext) {
-            const uint32_t cnt = min(64u, r1 - base);
-            last_key = prefix_extend(p.bk_keys + r0, r1 - r0, ks == 0, last_key, p.sorted_u_w + base, cnt, lane, u_sel);
-            ks += cnt;
-        }
         const uint32_t s = base + lane;
-        uint32_t m = 0, u = 0, gid = 0;
+        uint32_t m = 0;
         if (s < r1) {
-            u = ext ? u_sel : p.sorted_u[s];
-            gid = p.inst_gid[u];
+            const uint32_t u = p.sorted_u[s];
+            const uint32_t gid = p.inst_gid[u];
             p.point_list[s] = gid;
             p.inv[u] = s;
             const float4 ga = p.rec[gid].a, gb = p.rec[gid].b;
@@ -850,8 +801,6 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
 #pragma unroll
         for (int k = 0; k < NPIX; k++) sk[k] = livek[k] ? __ballot((m >> k) & 1u) : 0ull;  // finished strips: none
         loaded_end = min(r1, base + 64u);
-        u_last = __builtin_amdgcn_readlane((int)u, (int)(loaded_end - 1 - base));
-        g_last = __builtin_amdgcn_readlane((int)gid, (int)(loaded_end - 1 - base));
         wave_lds_sync();
         // walk only the batch's instances that reach a live strip (in order): instances whose strips are all
         // unreachable or finished cost nothing
@@ -958,12 +907,9 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
         }
     }
     mx = wave_max_u32(mx);
-    if (PREFIX && ks != ks0 && lane == 0) p.tile_sorted[tile] = ks;
     if (lane == 0) {
         atomicMax(&p.tile_last[tile], mx);
         atomicMax(&p.tile_loaded[tile], loaded_end - r0);
-        if (loaded_end > r0)  // parts of a tile: the largest key is the one at the furthest loaded position
-            atomicMax(&p.tile_lastkey[tile], ((unsigned long long)p.depth_key[g_last] << 32) | u_last);
         if (PARTS == 1 && p.lpt_blist) {  // whole tile: mx is final; append it to its backward LPT bucket
             const uint32_t b = lpt_log_bucket(mx);
             const uint32_t pos = atomicAdd(&p.lpt_bcnt[b], 1u);
@@ -991,23 +937,19 @@ void launch_render_fwd(hipStream_t s, const RenderFwdParams &p0) {
     const int parts = render_fwd_parts(p.num_tiles);
     const dim3 grid(div_up((uint64_t)p.num_tiles * parts, 4)), block(256);
     // threshold guard band ("guard" 1; the default launch shapes only, and the backward must run with the same knob)
-    if (tuning("guard", 0) && !(p.tile_sorted && p.bk_keys)) {
-        if (parts == 1) render_fwd_v6_kernel<4, 8, false, false, true><<<grid, block, 0, s>>>(p);
+    if (tuning("guard", 0)) {
+        if (parts == 1) render_fwd_v6_kernel<4, 8, false, true><<<grid, block, 0, s>>>(p);
         else if (parts == 4 && p.ckpt && p.ctot && p.ck_k >= CK_MIN_K && p.ck_k % 32 == 0 &&
                  (p.ck_k == 32 || p.ck_k % 64 == 0))
-            render_fwd_v6_kernel<1, 8, true, false, true><<<grid, block, 0, s>>>(p);
-        else if (parts == 2) render_fwd_v6_kernel<2, 8, false, false, true><<<grid, block, 0, s>>>(p);
-        else render_fwd_v6_kernel<1, 8, false, false, true><<<grid, block, 0, s>>>(p);
+            render_fwd_v6_kernel<1, 8, true, true><<<grid, block, 0, s>>>(p);
+        else if (parts == 2) render_fwd_v6_kernel<2, 8, false, true><<<grid, block, 0, s>>>(p);
+        else render_fwd_v6_kernel<1, 8, false, true><<<grid, block, 0, s>>>(p);
         return;
     }
     if (parts == 1) {
         // 8 waves per SIMD (64 VGPRs, one 8-byte spill outside the pair loop): cfg3 0.180 -> 0.172 ms, cfg5 0.517 ->
         // 0.478 ms against 6 waves (65 VGPRs, i.e. 7 resident)
         const int mw = tuning("fwd_whole_waves", 8);
-        if (p.tile_sorted && p.bk_keys) {
-            render_fwd_v6_kernel<4, 8, false, true><<<grid, block, 0, s>>>(p);
-            return;
-        }
         if (mw >= 8) render_fwd_v6_kernel<4, 8><<<grid, block, 0, s>>>(p);
         else if (mw >= 6) render_fwd_v6_kernel<4, 6><<<grid, block, 0, s>>>(p);
         else render_fwd_v6_kernel<4, 4><<<grid, block, 0, s>>>(p);

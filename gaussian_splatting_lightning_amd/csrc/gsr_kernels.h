@@ -112,7 +112,6 @@ struct BucketParams {
     uint32_t lb_patience;  // look-back polls before recomputing an unpublished predecessor
     int lb_force;          // recompute every predecessor (tests the fallback)
     uint32_t *tile_last, *tile_loaded;  // T each: cleared by the column pass for the forward composite
-    unsigned long long *tile_lastkey;   // T: likewise
     uint32_t *inv;         // R: reset to INV_NONE beside inst_gid (the forward composite fills it)
     uint32_t *lpt_bcnt;    // 256: cleared by the column pass (the forward's backward-LPT bucket counts)
     unsigned long long *keys;  // R: depth << 32 | u, bucketed by tile
@@ -139,13 +138,6 @@ struct SegSortParams {
     const uint32_t *long_list, *long_cnt;
     uint32_t *tie_list, *tie_cnt;  // tiles whose proxy-key sort met a tie (count zeroed), re-sorted by seg_huge
     uint4 *stamps;  // diagnostics (set by launch): per long-tile slot (start, chunks sorted, end, n), or null
-    // prefix binning (prefix_k > 0, a multiple of 64 <= 512): tiles longer than prefix_k get only their prefix_k
-    // front-most instances sorted (radix-selected); tile_sorted[t] = sorted length (n, prefix_k, or 0 after a proxy
-    // tie: nothing sorted), tile_thresh[t] = the largest key of the sorted prefix.  render_fwd extends a prefix its
-    // walk outlives (launch_render_fwd's prefix mode); seg_huge is not needed.
-    uint32_t prefix_k = 0;
-    uint32_t *tile_sorted = nullptr;
-    unsigned long long *tile_thresh = nullptr;
 };
 void launch_seg_sort(hipStream_t s, const SegSortParams &p);
 
@@ -159,8 +151,6 @@ struct RenderFwdParams {
     const uint32_t *tile_order;  // launch slot -> tile (heaviest first), or null for identity
     const uint32_t *sorted_u, *inst_gid;
     uint32_t *point_list, *tile_loaded;
-    const uint32_t *depth_key;            // per Gaussian: the key of the last loaded instance needs its depth bits
-    unsigned long long *tile_lastkey;     // T: key of the last instance each tile's walk loaded (atomicMax, zeroed)
     uint32_t *inv;                        // R: inv[u] = sorted position of every instance the walk loads
     const GRec *rec;
     const float *bg;
@@ -176,13 +166,6 @@ struct RenderFwdParams {
     // backward LPT bucket lists (ImageState::lpt_*), or null: whole-tile waves append their tile; *lpt_valid = 1 if
     // every tile was appended (whole tiles and lists given), else 0
     uint32_t *lpt_bcnt = nullptr, *lpt_blist = nullptr, *lpt_valid = nullptr;
-    // prefix binning (SegSortParams::prefix_k): per tile the sorted length and the largest sorted key; the bucketed
-    // keys the walk selects further batches from when it outlives the sorted prefix (whole tiles only), or null
-    const unsigned long long *bk_keys = nullptr;
-    uint32_t *tile_sorted = nullptr;
-    unsigned long long *tile_thresh = nullptr;
-    uint32_t *sorted_u_w = nullptr;  // = sorted_u, written by a prefix extension
-    uint32_t *prefix_flag = nullptr;  // written 1 by a prefix-mode launch, 0 otherwise (tile_sorted[T] for the tests)
 };
 void launch_render_fwd(hipStream_t s, const RenderFwdParams &p);
 int render_fwd_parts(int num_tiles);  // row-strip parts per tile launch_render_fwd uses (1: whole tiles)

@@ -274,6 +274,10 @@ size_t gsr_bwd_scratch_bytes(int64_t R, int64_t num_big);
  * the parity tests to compare the integer binning state (sorted instance list, tile ranges,
  * per-pixel contributor counts) bit for bit against the oracle. */
 typedef struct gsr_state_layout {
+    /* in: sizeof(gsr_state_layout) as the caller was built (a caller built against an older header passes its
+     * smaller size and gets only the fields it knows); out: the size the library filled (fields are only ever
+     * appended).  0 is taken as the library's own size (callers that predate this field zero-fill the struct). */
+    size_t struct_size;
     size_t geom_rec_a, geom_rec_b, geom_rec_c; /* float4, float4, float2 of Gaussian 0's record; Gaussian i's at
                                                   + i * geom_rec_stride */
     size_t geom_tiles, geom_order, geom_inst_off, geom_inst_start, geom_clamped; /* u32, u32, u32, u32, u8 */
@@ -286,11 +290,7 @@ typedef struct gsr_state_layout {
     size_t img_final_T, img_n_contrib, img_ranges, img_tile_last;     /* f32/u32 per pixel, uint2/u32 per tile */
     size_t img_tile_loaded;                                           /* u32 per tile */
     size_t geom_rec_stride;                                           /* bytes per render record (48) */
-    size_t img_tile_sorted;   /* u32 per tile: length of the tile's bucket sorted by the forward (prefix binning: a
-                                 prefix when the tile's walk ended before it; else the whole bucket); entry [T] is 1
-                                 when the forward ran in prefix mode */
     size_t bin_bk_keys;       /* u64 per instance: the bucket binning's keys (depth bits << 32 | u) grouped by tile */
-    size_t img_tile_lastkey;  /* u64 per tile: key of the last instance the forward composite loaded (0: none) */
 } gsr_state_layout;
 void gsr_state_layout_query(int P, int64_t R, int W, int H, gsr_state_layout *out);
 

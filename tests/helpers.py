@@ -99,8 +99,6 @@ def hip_state_arrays(out: dict) -> dict:
     i32 = torch.int32
     sorted_u = view(st.binning_buffer, lay["bin_sorted_u"], R, i32).astype(np.int64)
     inst_gid = view(st.binning_buffer, lay["bin_inst_gid"], R, i32).astype(np.uint32)
-    # in prefix binning mode sorted_u is written only over each tile's sorted prefix; the positions beyond it hold
-    # whatever the buffer held before (check_point_list compares the prefixes only), so index defensively
     ok = (sorted_u >= 0) & (sorted_u < R)
     point_list = np.full(R, 0xFFFFFFFF, np.uint32)
     point_list[ok] = inst_gid[sorted_u[ok]]
@@ -116,16 +114,6 @@ def hip_state_arrays(out: dict) -> dict:
         final_T=view(st.image_buffer, lay["img_final_T"], W * H, torch.float32).reshape(H, W),
         tiles=view(st.geom_buffer, lay["geom_tiles"], P, i32).astype(np.uint32),
         num_rendered=R)
-    # prefix binning: entry T is 1 when the forward ran in prefix mode, then entry t < T is the length
-    # of tile t's bucket in sorted order (>= its loaded instances); the rest of the bucket holds the same instances
-    ts = view(st.image_buffer, lay["img_tile_sorted"], T + 1, i32).astype(np.uint32)
-    res["prefix_mode"] = bool(ts[T] == 1)
-    res["tile_sorted"] = ts[:T]
-    if res["prefix_mode"]:  # the bucket keys: the rest of each bucket, beyond its sorted prefix
-        bk = view(st.binning_buffer, lay["bin_bk_keys"], R, torch.int64).view(np.uint64)
-        res["bucket_point_list"] = inst_gid[(bk & np.uint64(0xFFFFFFFF)).astype(np.int64)] if R else np.zeros(0, np.uint32)
-    lk = view(st.image_buffer, lay["img_tile_lastkey"], T, torch.int64).view(np.uint64)
-    res["tile_lastkey"] = lk
     res["depth_bits"] = view(st.geom_buffer, lay["geom_depth_key"], P, i32).astype(np.uint32)
     # render records: one 48-B (12-float) record per Gaussian, a = floats 0..3, b = 4..7, c = 8..9
     stride = lay["geom_rec_stride"] // 4

@@ -73,13 +73,6 @@ def compare_forward(inp, hip, oracle_out):
     assert np.array_equal(hs["point_list_written"][loaded], pl[loaded])
     su = hs["sorted_u"][loaded].astype(np.int64)
     assert np.array_equal(hs["inv"][su], np.nonzero(loaded)[0].astype(np.uint32))
-    ld = hs["tile_loaded"].astype(np.int64)
-    has = ld > 0
-    s_last = rg[has, 0].astype(np.int64) + ld[has] - 1
-    u_last = hs["sorted_u"][s_last].astype(np.uint64)
-    want = (hs["depth_bits"][pl[s_last]].astype(np.uint64) << np.uint64(32)) | u_last
-    assert np.array_equal(hs["tile_lastkey"][has], want)
-    assert np.all(hs["tile_lastkey"][~has] == 0)
     # pixels
     _, nc = run.image_state()
     flip = run.threshold_margin() < FLIP_MARGIN
@@ -114,23 +107,8 @@ def compare_forward(inp, hip, oracle_out):
 
 
 def check_point_list(hs, pl, rg):
-    """The sorted instance list against the reference order: bit-exact everywhere, or -- in prefix binning mode -- on
-    every tile's sorted prefix (which covers every instance the forward loaded), with the rest of each tile's bucket
-    holding exactly the reference's instances."""
-    hp = hs["point_list"]
-    if not hs["prefix_mode"]:
-        assert np.array_equal(hp, pl)
-        return
-    n = (rg[:, 1] - rg[:, 0]).astype(np.int64)
-    ts = hs["tile_sorted"].astype(np.int64)
-    live = n > 0
-    assert np.all(ts[live] <= n[live]) and np.all(ts[live] >= hs["tile_loaded"][live])
-    tile_of = np.repeat(np.arange(len(n)), n)
-    rel = np.arange(len(pl)) - rg[tile_of, 0].astype(np.int64)
-    srt = rel < ts[tile_of]
-    assert np.array_equal(hp[srt], pl[srt])
-    bp = hs["bucket_point_list"]  # each bucket holds exactly the reference's instances of its tile
-    assert np.array_equal(bp[np.lexsort((bp, tile_of))], pl[np.lexsort((pl, tile_of))])
+    """The sorted instance list against the reference order, bit-exact."""
+    assert np.array_equal(hs["point_list"], pl)
 
 
 def compare_backward(hip, run, dc, di, tol):
@@ -768,44 +746,6 @@ def test_tile_sort_digit_width_is_invisible(gpu_device, db):
         assert np.array_equal(a[k], b[k]), k
     for k in ("color", "invdepth", "radii"):
         assert np.array_equal(ref[k], alt[k]), k
-
-
-@pytest.mark.parametrize("n,k,dup", [(600_000, 512, False), (600_000, 64, False), (300_000, 512, True)])
-def test_prefix_binning_is_bitwise_the_full_sort(gpu_device, n, k, dup):
-    """Prefix binning (whole-tile composite, > 4096 tiles): buckets longer than k get only their k front-most instances
-    sorted and the forward selects further batches itself when a tile's walk outlives them.  Every output, gradient and
-    loaded instance is bitwise that of sorting every bucket whole -- with the default k (no walk outlives it here),
-    with k = 64 (most walks extend their prefix, batch after batch), and on duplicated Gaussians whose exact depth ties
-    the proxy-key sort cannot order (those tiles get no sorted prefix at all)."""
-    from gaussian_splatting_lightning_amd import _native
-    W, H = 1920, 1080
-    inp = scene_inputs(n, W, H, sh_degree=3, seed=8)
-    if dup:
-        for key in ("means3D", "scales", "rotations", "opacities", "shs"):
-            inp[key][1000:1400] = inp[key][1000]
-            inp[key][7000:7300] = inp[key][7001]
-    dc, di = upstream(W, H, 8)
-    try:
-        _native.set_tuning("bk_prefix", 0)
-        ref = run_hip(inp, gpu_device, dc, di)
-        _native.set_tuning("bk_prefix", k)
-        alt = run_hip(inp, gpu_device, dc, di)
-    finally:
-        _native.unset_tuning("bk_prefix")
-    a, b = hip_state_arrays(ref), hip_state_arrays(alt)
-    assert not a["prefix_mode"] and b["prefix_mode"]
-    for key in ("ranges", "tiles", "n_contrib", "tile_last", "tile_loaded"):
-        assert np.array_equal(a[key], b[key]), key
-    for key in ("color", "invdepth", "radii"):
-        assert np.array_equal(ref[key], alt[key]), key
-    for key in GRADS:
-        assert np.array_equal(ref["grads"][key], alt["grads"][key]), key
-    rg = a["ranges"]
-    check_point_list(b, a["point_list"], rg)
-    nt = (rg[:, 1] - rg[:, 0]).astype(np.int64)
-    assert np.any(b["tile_sorted"] < nt)  # some bucket really was sorted only in part
-    if k == 64:
-        assert np.any((b["tile_sorted"] > 64) & (nt > b["tile_sorted"]))  # walks extended their prefix
 
 
 @pytest.mark.parametrize("mode", ["split", "late4", "late6", "direct"])

@@ -48,6 +48,22 @@ def test_buffer_sizes_and_layout():
     assert len(set(geom)) == len(geom)
 
 
+def test_state_layout_query_is_versioned_by_struct_size():
+    """gsr_state_layout.struct_size: a caller built against an older (shorter) header gets only its own fields and
+    nothing is written past them; the library reports the size it filled."""
+    lib = _native.load()
+    L = _native.StateLayout
+    short = L.bin_bk_keys.offset  # a caller whose struct ends before the last field
+    buf = (ctypes.c_size_t * (ctypes.sizeof(L) // 8))(*([0xDEAD] * (ctypes.sizeof(L) // 8)))
+    buf[0] = short
+    lib.gsr_state_layout_query(1000, 5000, 100, 80, ctypes.cast(buf, ctypes.POINTER(L)))
+    assert buf[0] == short
+    assert buf[L.bin_bk_keys.offset // 8] == 0xDEAD  # untouched
+    full = _native.state_layout(1000, 5000, 100, 80)
+    assert buf[L.geom_rec_a.offset // 8] == full["geom_rec_a"]
+    assert "bin_bk_keys" in full
+
+
 def test_invalid_arguments_fail_before_touching_the_device():
     lib = _native.load()
     a = _native.ForwardArgs(P=-1, W=10, H=10)
