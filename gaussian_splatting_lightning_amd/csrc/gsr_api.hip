@@ -717,6 +717,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     rp.ck_flag = im.ck_flag;
     // the backward's LPT order from bucket lists the whole-tile waves append (no ordering launch in the backward)
     rp.lpt_valid = im.lpt_valid;
+    rp.strip_mask = b.strip_mask; rp.smask_valid = im.smask_valid;
     if (lpt_append_range(T) && lpt && tuning("bwd_order", 1) && tuning("lpt_append", 1)) {
         rp.lpt_bcnt = im.lpt_bcnt; rp.lpt_blist = im.lpt_blist;
     }
@@ -806,6 +807,7 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
         rp.bg = a->background; rp.final_T = im.final_T; rp.dL_dpix = a->dL_dpix; rp.dL_dinvdepth = a->dL_dinvdepth;
         rp.rows = rows;
         rp.sorted_u = b.sorted_u;
+        rp.strip_mask = b.strip_mask; rp.smask_valid = im.smask_valid;
         if (T <= SEG_MAX_TILES && tuning("bwd_seg", 1)) {  // segmented walk (from the forward's checkpoints, if any)
             rp.ckpt = b.ckpt; rp.ctot = im.ctot; rp.ck_flag = im.ck_flag;
             rp.seg_list = b.seg_list; rp.seg_count = im.seg_count;

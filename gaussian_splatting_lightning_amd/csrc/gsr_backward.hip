@@ -283,7 +283,7 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
 // scalar accumulator's value there (D_k T_(k+1) = sum_(j > k) w_j c_j . dL/dpix + T_final bg . dL/dpix).  Without
 // checkpoints every tile is one segment.  Rows agree with the one-walk backward to rounding.
 template <bool HAS_INV, bool LASTC, bool UNION = false, bool SEG = false, bool GUARD = false>
-__global__ __launch_bounds__(64, SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MINW) void render_bwd_v5_kernel(RenderBwdParams p) {
+__global__ __launch_bounds__(64, GUARD ? 4 : SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MINW) void render_bwd_v5_kernel(RenderBwdParams p) {
     __shared__ FwdRec s_rec[BWD_BATCH];
     __shared__ __attribute__((aligned(16))) float s_part[BWD_BATCH][PART];  // [instance][10 sums]
     const int lane = threadIdx.x;
@@ -368,6 +368,8 @@ __global__ __launch_bounds__(64, SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MINW) void ren
         }
     }
     const float hW = 0.5f * p.W, hH = 0.5f * p.H;
+    // the forward's exact strip masks (whole-tile forwards write them), else the conservative cell masks
+    const bool smask = p.strip_mask && __builtin_amdgcn_readfirstlane(*p.smask_valid);
 
     for (int bend = (int)hi; bend > (int)lo; bend -= BWD_BATCH) {
         const int cnt = min(BWD_BATCH, bend - (int)lo);
@@ -383,7 +385,7 @@ __global__ __launch_bounds__(64, SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MINW) void ren
             s_rec[lane].a = stage_rec_a(my_a);
             s_rec[lane].b = stage_rec_b(my_b);
             s_rec[lane].c = p.rec[gid].c;
-            my_m = cell_mask(p.strip_exact, my_a, my_b, row0, col0);
+            my_m = smask ? (uint32_t)p.strip_mask[s_me] : cell_mask(p.strip_exact, my_a, my_b, row0, col0);
         }
         // sk[k] bit j: strip k of instance j (idx = bend - 1 - j) may hold a contributing pixel;
         // nd[k] bit j: some lane of strip k may have n_contrib <= idx (the per-lane compare is needed)
@@ -426,7 +428,7 @@ __global__ __launch_bounds__(64, SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MINW) void ren
                               __builtin_amdgcn_fcmpf(alpha, GUARD ? GUARD_A_LO : 1.0f / 255.0f, FCMP_UGE);
                 if constexpr (GUARD) {  // the forward's guarded alpha decision, taken by the same test (gsr_common.h)
                     const uint64_t near = ok & ~__builtin_amdgcn_fcmpf(alpha, GUARD_A_HI, FCMP_UGE);
-                    if (near) {  // rare
+                    if (__builtin_expect(near != 0, 0)) {  // rare
                         const uint32_t g = __float_as_uint(r.pad.x);
                         const uint64_t okx = __ballot(guard_alpha_pass(p.rec, g, pfx, pfy0 + (float)(4 * k)));
                         ok = (ok & ~near) | (okx & near);

@@ -193,6 +193,8 @@ struct BinningState {
     uint32_t *sorted_u;    // R: expansion index of each sorted instance
     uint32_t *inv;         // R: sorted position of instance u (its gradient-row marker), INV_NONE where the forward
                            //    composite did not load it (filled by the binning, set by the composite)
+    uint8_t *strip_mask;   // R: per sorted instance the 4-row strips of its tile where some pixel took it (bit k =
+                           //    strip k), written by the whole-tile forward composite for every instance it loaded
     // scratch of the two binning paths (overlapping: only one runs per forward)
     uint32_t *keys_sorted; // radix path: R tile ids of the sorted instances
     SortScratch sort;      // radix path: tile sort (R keys); its final value buffer is sorted_u
@@ -220,6 +222,7 @@ inline size_t carve_binning(char *base, int64_t R, uint32_t num_tiles, BinningSt
     b.point_list = c.take<uint32_t>(n ? n : 1);
     b.sorted_u = c.take<uint32_t>(n ? n : 1);
     b.inv = c.take<uint32_t>(n ? n : 1);
+    b.strip_mask = c.take<uint8_t>(n ? n : 1);
     Carver cr = c;  // radix view
     const int passes = tile_sort_plan(num_tiles).passes;
     carve_sort(cr, b.sort, n, passes >= 2);
@@ -270,6 +273,7 @@ struct ImageState {
     uint32_t *lpt_hist;      // (T / 4096 + 1) x 256: per-workgroup bucket histograms of the multi-workgroup LPT order
     uint32_t *lpt_blist;     // 256 x T in lpt_append_range (else 1): bucket b's tiles at [b T, b T + lpt_bcnt[b])
     uint32_t *lpt_valid;     // 1 when this forward appended every tile to the bucket lists, else 0
+    uint32_t *smask_valid;   // 1 when this forward wrote every loaded instance's strip_mask (whole tiles), else 0
 };
 // Between these tile counts the forward's whole-tile waves append each finished tile to its backward LPT bucket, so
 // the backward needs no ordering launch (1080p, 8160 tiles: step -13 us).  At 4K (32400 tiles of similar weight in a
@@ -303,6 +307,7 @@ inline size_t carve_image(char *base, int W, int H, ImageState &im) {
     im.lpt_hist = c.take<uint32_t>((nt / 4096 + 1) * 256);
     im.lpt_blist = c.take<uint32_t>(lpt_append_range((uint32_t)nt) ? 256 * nt : 1);
     im.lpt_valid = c.take<uint32_t>(1);
+    im.smask_valid = c.take<uint32_t>(1);
     return c.off + 256;
 }
 
@@ -581,13 +586,34 @@ __device__ __forceinline__ float guard_power(float4 ra, float cz, float pfx, flo
     const float dx = ra.x - pfx, dy = ra.y - pfy;
     return -0.5f * (ra.z * dx * dx + cz * dy * dy) - ra.w * dx * dy;
 }
-__device__ __forceinline__ float guard_alpha(float power, float o) {
-    return fminf(0.99f, o * (float)exp((double)power));
+// exp(x) rounded once to fp32 (the correctly rounded expf but for double-rounding ties): Cody-Waite reduction by ln 2
+// and a degree-11 Taylor polynomial in double (relative error ~1e-15), lighter in registers than the library's
+// double exp.  For the guard's exponents (about -6 .. 0; anything below -87 underflows to 0 as expf does).
+__device__ __forceinline__ float guard_expf(float x) {
+    if (!(x > -87.5f)) return 0.0f;
+    const double xd = (double)x;
+    const double n = __builtin_rint(xd * 1.4426950408889634);
+    const double r = __builtin_fma(n, -1.90821492927058770002e-10, __builtin_fma(n, -6.93147180369123816490e-01, xd));
+    double p = 2.505210838544172e-08;  // 1/11!
+    p = __builtin_fma(p, r, 2.755731922398589e-07);
+    p = __builtin_fma(p, r, 2.755731922398589e-06);
+    p = __builtin_fma(p, r, 2.48015873015873e-05);
+    p = __builtin_fma(p, r, 1.984126984126984e-04);
+    p = __builtin_fma(p, r, 1.388888888888889e-03);
+    p = __builtin_fma(p, r, 8.333333333333333e-03);
+    p = __builtin_fma(p, r, 4.166666666666666e-02);
+    p = __builtin_fma(p, r, 1.666666666666667e-01);
+    p = __builtin_fma(p, r, 0.5);
+    p = __builtin_fma(p, r, 1.0);
+    p = __builtin_fma(p, r, 1.0);
+    return (float)__builtin_ldexp(p, (int)n);
 }
-// The oracle's alpha decision for Gaussian g at pixel (pfx, pfy): power <= 0 and alpha >= 1/255.  Out of line, so
-// the rare guarded pairs' double-precision exp does not raise the register pressure of the compositing loops.
-static __device__ __attribute__((noinline)) bool guard_alpha_pass(const GRec *__restrict__ rec, uint32_t g, float pfx,
-                                                                  float pfy) {
+__device__ __forceinline__ float guard_alpha(float power, float o) {
+    return fminf(0.99f, o * guard_expf(power));
+}
+// The oracle's alpha decision for Gaussian g at pixel (pfx, pfy): power <= 0 and alpha >= 1/255.  Inlined into a
+// branch marked unlikely (an out-of-line call made the compositing loops save their scalar state around it and spill).
+__device__ __forceinline__ bool guard_alpha_pass(const GRec *__restrict__ rec, uint32_t g, float pfx, float pfy) {
     const float4 ra = rec[g].a;
     const float2 rb = *reinterpret_cast<const float2 *>(&rec[g].b);
     const float pw = guard_power(ra, rb.x, pfx, pfy);

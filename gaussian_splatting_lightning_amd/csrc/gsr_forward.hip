@@ -731,15 +731,20 @@ void launch_tile_order(hipStream_t s, const uint2 *ranges, const uint32_t *tile_
 // + j), and at the end the pixel's final sums (ctot); the backward walks each ck_k-instance segment from the
 // checkpoint at its end.  A pixel still compositing at instance e is still walked when its wave reaches e, so every
 // checkpoint the backward reads (e < the pixel's n_contrib) is written.
-template <int NPIX, int MIN_WAVES, bool CKPT = false, bool GUARD = false>
+// SMASK (whole tiles): per batch, scalar masks cb[k] collect the instances some pixel of strip k took, and each loaded
+// instance's 4-bit strip mask goes to strip_mask[s] -- the backward then walks exactly the strips that contributed
+// instead of the conservative cell_mask (bitwise the same gradients: a skipped strip has no contributing pixel).
+template <int NPIX, int MIN_WAVES, bool CKPT = false, bool GUARD = false, bool SMASK = false>
 __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwdParams p) {
     constexpr int PARTS = 4 / NPIX;
+    static_assert(!SMASK || PARTS == 1, "strip masks are recorded by whole-tile waves");
     __shared__ FwdRec s_rec[4][64];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int slot = blockIdx.x * 4 + w;
     if (p.ck_flag && slot == 0 && lane == 0) *p.ck_flag = CKPT ? p.ck_k : 0u;
     if (p.lpt_valid && slot == 0 && lane == 0) *p.lpt_valid = (PARTS == 1 && p.lpt_blist) ? 1u : 0u;
+    if (p.smask_valid && slot == 0 && lane == 0) *p.smask_valid = SMASK ? 1u : 0u;
     if (slot >= p.num_tiles * PARTS) return;
     const int half = slot % PARTS;
     const int tile = __builtin_amdgcn_readfirstlane(p.tile_order ? (int)p.tile_order[slot / PARTS] : slot / PARTS);
@@ -808,6 +813,9 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
 #pragma unroll
         for (int k = 0; k < NPIX; k++) un |= sk[k];
         const uint32_t cbase = contributor;
+        uint64_t cb[NPIX];  // SMASK: bit j of cb[k] = some pixel of strip k took instance j
+#pragma unroll
+        for (int k = 0; k < NPIX; k++) cb[k] = 0;
         auto walk = [&](uint64_t &un) {
         while (un) {
             const uint32_t j = (uint32_t)__builtin_ctzll(un);
@@ -833,7 +841,7 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
                 const uint64_t low = __builtin_amdgcn_fcmpf(test_T, 0.0001f, FCMP_OLT);
                 if constexpr (GUARD) {  // alpha decisions near 1/255 from the oracle's arithmetic (gsr_common.h)
                     const uint64_t near = ok & ~__builtin_amdgcn_fcmpf(alpha, GUARD_A_HI, FCMP_UGE);
-                    if (near) {  // rare
+                    if (__builtin_expect(near != 0, 0)) {  // rare
                         const uint32_t g = __float_as_uint(sr[j].pad.x);
                         const uint64_t okx = __ballot(
                             guard_alpha_pass(p.rec, g, pfx, pfy0 + (float)(4 * (kbase + k))));
@@ -841,6 +849,7 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
                     }
                 }
                 const uint64_t take = ok & ~low, stop = ok & low;
+                if (SMASK && take) cb[k] |= bit;
                 const float wgt = select_mask(take, alpha * T[k], 0.f);
                 C0[k] = fmaf(b.z, wgt, C0[k]);
                 C1[k] = fmaf(b.w, wgt, C1[k]);
@@ -875,6 +884,12 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
             walk(un);
         }
         contributor = cbase + min(64u, r1 - base);
+        if (SMASK && s < r1) {
+            uint32_t mk = 0;
+#pragma unroll
+            for (int k = 0; k < NPIX; k++) mk |= (uint32_t)((cb[k] >> lane) & 1ull) << k;
+            p.strip_mask[s] = (uint8_t)mk;
+        }
         wave_lds_sync();
         uint64_t anylive = 0;
 #pragma unroll
@@ -937,8 +952,12 @@ void launch_render_fwd(hipStream_t s, const RenderFwdParams &p0) {
     const int parts = render_fwd_parts(p.num_tiles);
     const dim3 grid(div_up((uint64_t)p.num_tiles * parts, 4)), block(256);
     // threshold guard band ("guard" 1; the default launch shapes only, and the backward must run with the same knob)
-    if (tuning("guard", 0)) {
-        if (parts == 1) render_fwd_v6_kernel<4, 8, false, true><<<grid, block, 0, s>>>(p);
+    // exact strip masks for the backward ("smask" 1): whole tiles only
+    const bool sm = parts == 1 && p.strip_mask && tuning("smask", 1);
+    if (!sm) p.strip_mask = nullptr;
+    if (tuning("guard", 0)) {  // 6 waves per SIMD whole-tile: the guard's double exp needs the registers
+        if (parts == 1 && sm) render_fwd_v6_kernel<4, 6, false, true, true><<<grid, block, 0, s>>>(p);
+        else if (parts == 1) render_fwd_v6_kernel<4, 6, false, true><<<grid, block, 0, s>>>(p);
         else if (parts == 4 && p.ckpt && p.ctot && p.ck_k >= CK_MIN_K && p.ck_k % 32 == 0 &&
                  (p.ck_k == 32 || p.ck_k % 64 == 0))
             render_fwd_v6_kernel<1, 8, true, true><<<grid, block, 0, s>>>(p);
@@ -950,7 +969,8 @@ void launch_render_fwd(hipStream_t s, const RenderFwdParams &p0) {
         // 8 waves per SIMD (64 VGPRs, one 8-byte spill outside the pair loop): cfg3 0.180 -> 0.172 ms, cfg5 0.517 ->
         // 0.478 ms against 6 waves (65 VGPRs, i.e. 7 resident)
         const int mw = tuning("fwd_whole_waves", 8);
-        if (mw >= 8) render_fwd_v6_kernel<4, 8><<<grid, block, 0, s>>>(p);
+        if (sm) render_fwd_v6_kernel<4, 8, false, false, true><<<grid, block, 0, s>>>(p);
+        else if (mw >= 8) render_fwd_v6_kernel<4, 8><<<grid, block, 0, s>>>(p);
         else if (mw >= 6) render_fwd_v6_kernel<4, 6><<<grid, block, 0, s>>>(p);
         else render_fwd_v6_kernel<4, 4><<<grid, block, 0, s>>>(p);
         return;

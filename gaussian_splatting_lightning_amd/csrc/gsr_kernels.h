@@ -166,6 +166,10 @@ struct RenderFwdParams {
     // backward LPT bucket lists (ImageState::lpt_*), or null: whole-tile waves append their tile; *lpt_valid = 1 if
     // every tile was appended (whole tiles and lists given), else 0
     uint32_t *lpt_bcnt = nullptr, *lpt_blist = nullptr, *lpt_valid = nullptr;
+    // exact per-instance strip masks for the backward (BinningState::strip_mask), or null: whole-tile waves record
+    // which strips took each loaded instance; *smask_valid = 1 if this launch wrote them, else 0
+    uint8_t *strip_mask = nullptr;
+    uint32_t *smask_valid = nullptr;
 };
 void launch_render_fwd(hipStream_t s, const RenderFwdParams &p);
 int render_fwd_parts(int num_tiles);  // row-strip parts per tile launch_render_fwd uses (1: whole tiles)
@@ -193,6 +197,9 @@ struct RenderBwdParams {
     uint32_t ck_k = 0;
     // launch order from the forward's LPT bucket lists when *lpt_valid (else tile_order / identity)
     const uint32_t *lpt_bcnt = nullptr, *lpt_blist = nullptr, *lpt_valid = nullptr;
+    // the forward's exact strip masks when *smask_valid (else the conservative cell_mask of the record)
+    const uint8_t *strip_mask = nullptr;
+    const uint32_t *smask_valid = nullptr;
 };
 void launch_render_bwd(hipStream_t s, const RenderBwdParams &p);
 

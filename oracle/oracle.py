@@ -52,6 +52,7 @@ def _load():
     lib.oracle_get_geom.argtypes = [ctypes.c_void_p, _f, _f, _f, _f, _u32]
     lib.oracle_threshold_margin.argtypes = [ctypes.c_void_p, _f]
     lib.oracle_flip_census.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong)]
+    lib.oracle_strip_census.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong)]
     lib.oracle_mark_visible.argtypes = [ctypes.c_int, _f, _f, _f, _u8]
     lib.oracle_num_threads.restype = ctypes.c_int
     lib.oracle_bin_count.restype = ctypes.c_longlong
@@ -168,6 +169,13 @@ class OracleRun:
         c = (ctypes.c_longlong * 4)()
         self._lib.oracle_flip_census(self._h, c)
         return {"pixels": c[0], "power": c[1], "alpha": c[2], "transmittance": c[3]}
+
+    def strip_census(self) -> dict:
+        """(instance, 4-row strip) pairs before each tile's last contributor: geometrically reached vs contributing
+        (oracle_strip_census)."""
+        c = (ctypes.c_longlong * 3)()
+        self._lib.oracle_strip_census(self._h, c)
+        return {"reach": c[0], "contribute": c[2]}
 
     def geom(self):
         P = self.P

@@ -548,20 +548,21 @@ def test_densify_stats_from_backward(gpu_device):
 
 @pytest.mark.parametrize("knobs", [{"fwd_parts": 1}, {"fwd_parts": 2}, {"fwd_parts": 4}, {"fwd_whole_waves": 6},
                                    {"strip_exact": 0}, {"bwd_lastc": 1}, {"bwd_parts": 2}, {"bwd_parts": 4},
-                                   {"bwd_union": 1}, {"fwd_parts": 1, "bwd_union": 1}])
+                                   {"bwd_union": 1}, {"fwd_parts": 1, "bwd_union": 1}, {"fwd_parts": 1, "smask": 0}])
 def test_composite_variants_are_bitwise_identical(gpu_device, knobs):
     """Every composite launch shape gives the same bits: a tile composited whole (4 pixels per lane) or in 2 / 4
     row-strip parts gives the same pixels and contributor counts; strip skipping (row-band or exact column-band
     masks) only skips strips where every pixel fails alpha >= 1/255; the backward's n_contrib strip bounds only
     skip strips and compares that cannot contribute; the union walk (pairs formed only from instances that reach a
-    strip) gives each instance the same reduction tree whatever its partner.  Outputs and gradients must match bit
+    strip) gives each instance the same reduction tree whatever its partner; the whole-tile forward's exact strip
+    masks ("smask") only skip strips where no pixel took the instance.  Outputs and gradients must match bit
     for bit (with a non-zero background).  The parts backward adds its waves' per-instance sums: gradients agree to
     rounding only."""
     from gaussian_splatting_lightning_amd import _native
     inp = scene_inputs(200_000, 1280, 720, sh_degree=3, seed=4, bg=(0.3, 0.6, 0.9))
     dc, di = upstream(1280, 720, 4)
     defaults = {"fwd_parts": 0, "fwd_whole_waves": 8, "strip_exact": 1, "bwd_lastc": 0, "bwd_parts": 0,
-                "bwd_union": -1}
+                "bwd_union": -1, "smask": 1}
     try:
         _native.set_tuning("bwd_seg", 0)  # 3600 tiles: the default walks segments (test_segmented_backward)
         _native.set_tuning("bwd_parts", 1)  # the reference side: one wave per tile (the default here is 2)
