@@ -655,7 +655,6 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             sp.tile_order = (lpt && (((SEG_CAP + 1) >> tuning("lpt_shift", 3)) << tuning("lpt_shift", 3)) == SEG_CAP + 1)
                                 ? im.order_fwd : nullptr; sp.keys = b.bk_keys; sp.keys2 = b.bk_keys2;
             sp.sorted_u = b.sorted_u; sp.long_list = im.bk_long_list; sp.long_cnt = g.counters + CNT_LONG;
-            sp.tie_list = im.bk_tie_list; sp.tie_cnt = g.counters + CNT_TIES;
             // (Round 4's prefix binning -- radix-select each long bucket's 512 front-most keys, sort only those, and
             // let render_fwd extend a walk that outlives them -- measured slower at cfg 3, seg_sort 0.053 -> 0.060 ms
             // and render_fwd 0.171 -> 0.176 ms, and was removed in round 5: DESIGN.md appendix)

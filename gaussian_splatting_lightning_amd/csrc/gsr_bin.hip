@@ -15,9 +15,9 @@
 //                  position.  Keys are unique inside a tile (one instance per Gaussian), so the order inside
 //                  a bucket after step 4 does not matter and the result is exactly the reference's (tile,
 //                  depth, index) order.  Tiles above SEG_CAP instances are sorted by a whole workgroup (four
-//                  waves sort 512-key chunks, then merge ranks through LDS); tiles above SEG_BLOCK_CAP, and
-//                  tiles whose ties did not resolve, by seg_huge on the 64-bit keys (in LDS up to 8192
-//                  keys, else in chunks placed by merge ranks).
+//                  waves sort 512-key chunks, then merge ranks through LDS); tiles above SEG_BLOCK_CAP by
+//                  a workgroup in SEG_BLOCK_CAP-key chunks placed by merge ranks; ties of the 32-bit proxy
+//                  keys are repaired on the full keys by odd-even passes run to convergence.
 // Everything is integer work; nothing depends on scheduling, so the result is deterministic.
 #include <algorithm>
 
@@ -110,9 +110,14 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
         const uint32_t *hrow = p.hist_pre + (size_t)b * T;
         const uint32_t nr = (T + BK_REGION - 1) / BK_REGION;
         for (uint32_t r = tid; r < nr; r += 64 * BKW) {
-            const uint32_t t0 = r * BK_REGION, t1 = min(T, t0 + BK_REGION);
-            uint32_t acc = p.tile_start[t0];
-            for (uint32_t t = t0; t < t1; t++) acc += hrow[t];
+            const uint32_t t0 = r * BK_REGION;
+            uint32_t acc = p.tile_start[t0], v[BK_REGION];
+            // the region's BK_REGION prefixes loaded together (clamped index, masked sum): a rolled loop waited for
+            // each load before issuing the next, BK_REGION serial round trips per region
+#pragma unroll
+            for (int q = 0; q < BK_REGION; q++) v[q] = hrow[min(t0 + q, T - 1)];
+#pragma unroll
+            for (int q = 0; q < BK_REGION; q++) acc += t0 + q < T ? v[q] : 0u;
             s_tab[r] = acc;
         }
     } else if (SCATTER) {
@@ -402,10 +407,8 @@ __global__ __launch_bounds__(PART_THREADS) void bk_partition_kernel(BucketParams
     const int tid = threadIdx.x;
     unsigned long long k[PART_ITEMS];  // the chunk's keys, loaded first (they do not depend on the region search)
 #pragma unroll
-    for (int q = 0; q < PART_ITEMS; q++) {
-        const uint32_t i = (uint32_t)(q * PART_THREADS + tid);
-        k[q] = i < n ? p.keys_reg[c0 + i] : 0ull;
-    }
+    for (int q = 0; q < PART_ITEMS; q++)  // unconditional loads (clamped index): issued together, one wait
+        k[q] = p.keys_reg[c0 + min((uint32_t)(q * PART_THREADS + tid), n - 1)];
     if (tid < 64) {  // the chunk's first and last regions: 64-probe wave searches over the compact region starts
         const uint32_t rlo = wave_last_le(p.reg_start, nr - 1, c0, tid);
         const uint32_t rhi = wave_last_le(p.reg_start, nr - 1, c0 + n - 1, tid);
@@ -500,8 +503,12 @@ __device__ __forceinline__ void seg_sort_wave_impl(const unsigned long long *__r
     constexpr int LOGE = (E >= 64) ? 6 : (E >= 32) ? 5 : (E >= 16) ? 4 : (E >= 8) ? 3 : (E >= 4) ? 2 : (E >= 2) ? 1 : 0;
     unsigned long long x[E];
     const uint32_t base = (uint32_t)lane * E;
+    // every lane loads (a clamped index past n): loads in a branch each wait for their data before the next
+    // is issued, E serial memory round trips per sort
 #pragma unroll
-    for (int r = 0; r < E; r++) x[r] = (base + r < n) ? keys[start + base + r] : ~0ull;
+    for (int r = 0; r < E; r++) x[r] = keys[start + min(base + r, n - 1)];
+#pragma unroll
+    for (int r = 0; r < E; r++) x[r] = (base + r < n) ? x[r] : ~0ull;
 #pragma unroll
     for (int lk = 1; lk < LOGE; lk++) {
 #pragma unroll
@@ -568,13 +575,16 @@ __device__ __forceinline__ void seg_sort_wave_impl(const unsigned long long *__r
 // pairs and lane exchanges one ds_bpermute (about 2.5x fewer VALU ops than 64-bit keys).  The proxy orders
 // exactly like (depth, u) unless two keys share a quantised depth (~8 % of 512-key sorts at cfg 3).  Such ties
 // (a ballot over adjacent sorted keys) are put in order after the gather by odd-even transposition passes on
-// the full keys: keys of different quantised depth are already ordered, so only the tie runs move.  After
-// TIE_PASSES pass pairs without convergence the sort returns false and the caller hands the tile to the 64-bit
-// sort.  Descending merge halves run on complemented keys, so
+// the full keys: keys of different quantised depth are already ordered, so only the tie runs move, and a run of L
+// keys settles within L pass pairs (odd-even transposition sorts any n keys in n phases; the loop stops at the first
+// pass pair without a swap, and at n pass pairs at the latest).  Round 4 gave up after 8 pass pairs and re-sorted
+// such tiles on the 64-bit keys in a second launch (seg_huge), whose ~5-us floor every step paid; a tie run of
+// hundreds of keys (duplicated Gaussians) now costs its wave ~20 us once.  Descending merge halves run on
+// complemented keys, so
 // every stage of a merge level is an ascending min / max.  scratch: 64 E keys of LDS (the full keys, gathered
 // back by index after the sort).
 template <int E>
-__device__ __forceinline__ bool seg_sort_wave32(const unsigned long long *__restrict__ keys, uint32_t start, uint32_t n,
+__device__ __forceinline__ void seg_sort_wave32(const unsigned long long *__restrict__ keys, uint32_t start, uint32_t n,
                                                 unsigned long long *__restrict__ scratch, int lane,
                                                 unsigned long long (&out)[E]) {
     constexpr int LOGE = (E >= 8) ? 3 : (E >= 4) ? 2 : (E >= 2) ? 1 : 0;
@@ -583,9 +593,11 @@ __device__ __forceinline__ bool seg_sort_wave32(const unsigned long long *__rest
     unsigned long long x64[E];
     uint32_t dmin = 0xffffffffu, dmax = 0u;
 #pragma unroll
+    for (int r = 0; r < E; r++) x64[r] = keys[start + min(base + r, n - 1)];  // unconditional loads (as above)
+#pragma unroll
     for (int r = 0; r < E; r++) {
         const bool valid = base + r < n;
-        x64[r] = valid ? keys[start + base + r] : ~0ull;
+        x64[r] = valid ? x64[r] : ~0ull;
         scratch[base + r] = x64[r];
         const uint32_t d = (uint32_t)(x64[r] >> 32);
         if (valid) {
@@ -661,9 +673,8 @@ __device__ __forceinline__ bool seg_sort_wave32(const unsigned long long *__rest
     wave_lds_sync();  // scratch written by every lane above
 #pragma unroll
     for (int r = 0; r < E; r++) out[r] = scratch[x[r] & ((1u << IDXB) - 1u)];
-    if (!any_tie) return true;
-    constexpr int TIE_PASSES = 8;
-    for (int it = 0; it < TIE_PASSES; it++) {
+    if (!any_tie) return;
+    for (uint32_t it = 0; it < n; it++) {
         bool sw = false;
         auto ce = [&](unsigned long long &a, unsigned long long &b) {
             const bool s = b < a;
@@ -697,44 +708,39 @@ __device__ __forceinline__ bool seg_sort_wave32(const unsigned long long *__rest
             out[0] = pv;
             sw = true;
         }
-        if (!__ballot(sw)) return true;
+        if (!__ballot(sw)) return;
     }
-    return false;
 }
 
-// Wrappers.  P32: the proxy-key sort, false on a tie (nothing written; seg_huge sorts the tile again on its
-// 64-bit keys).  P32 = false: the 64-bit network.  The two live in separate kernels (seg_sort / seg_huge), so
-// the common kernel carries only the 32-bit network's registers.
+// Wrappers.  P32: the proxy-key sort; P32 = false: the 64-bit network (knob "seg32" 0, the A/B reference).
 template <int E, bool P32>
-__device__ __forceinline__ bool seg_sort_wave(const unsigned long long *keys, uint32_t start, uint32_t n,
+__device__ __forceinline__ void seg_sort_wave(const unsigned long long *keys, uint32_t start, uint32_t n,
                                               uint32_t *sorted_u, int lane, unsigned long long *scratch) {
     if (!P32) {
         seg_sort_wave_impl<E>(keys, start, n, sorted_u, nullptr, lane);
-        return true;
+        return;
     }
     unsigned long long y[E];
-    if (!seg_sort_wave32<E>(keys, start, n, scratch, lane, y)) return false;
+    seg_sort_wave32<E>(keys, start, n, scratch, lane, y);
     const uint32_t base = (uint32_t)lane * E;
 #pragma unroll
     for (int r = 0; r < E; r++)
         if (base + r < n) sorted_u[start + base + r] = (uint32_t)y[r];
-    return true;
 }
 // sorted (padded) keys into lds_out, which is also the scratch
 template <int E, bool P32>
-__device__ __forceinline__ bool seg_sort_wave_to_lds(const unsigned long long *keys, uint32_t start, uint32_t n,
+__device__ __forceinline__ void seg_sort_wave_to_lds(const unsigned long long *keys, uint32_t start, uint32_t n,
                                                      unsigned long long *lds_out, int lane) {
     if (!P32) {
         seg_sort_wave_impl<E>(keys, start, n, nullptr, lds_out, lane);
-        return true;
+        return;
     }
     unsigned long long y[E];
-    if (!seg_sort_wave32<E>(keys, start, n, lds_out, lane, y)) return false;
+    seg_sort_wave32<E>(keys, start, n, lds_out, lane, y);
     wave_lds_sync();  // every lane's gathers done before the scratch is overwritten
     const uint32_t base = (uint32_t)lane * E;
 #pragma unroll
     for (int r = 0; r < E; r++) lds_out[base + r] = y[r];
-    return true;
 }
 
 // Workgroup sort of up to 16 x 512 keys in LDS: the waves sort 512-key chunks in registers (as
@@ -789,60 +795,80 @@ __device__ __forceinline__ void seg_merge_ranks(const unsigned long long *__rest
     }
 }
 
-// With P32 a chunk sort that meets a tie stores tag into *s_flag and the whole sort returns false (uniform over
-// the workgroup, nothing written); a workgroup's calls use distinct tags, so the flag is never cleared.
 template <bool P32>
-__device__ __forceinline__ bool seg_lds_sort(const unsigned long long *__restrict__ keys, uint32_t start, uint32_t n,
+__device__ __forceinline__ void seg_lds_sort(const unsigned long long *__restrict__ keys, uint32_t start, uint32_t n,
                                              uint32_t *__restrict__ sorted_u, unsigned long long *__restrict__ keys_out,
-                                             unsigned long long *__restrict__ s_x, int w, int lane, uint32_t *s_flag,
-                                             uint32_t tag, uint32_t *t_mid = nullptr) {
+                                             unsigned long long *__restrict__ s_x, int w, int lane,
+                                             uint32_t *t_mid = nullptr) {
     const uint32_t nch = (n + SB_CHUNK - 1) / SB_CHUNK;
     for (uint32_t c = (uint32_t)w; c < nch; c += 4) {
         const uint32_t c0 = c * SB_CHUNK;
-        if (!seg_sort_wave_to_lds<8, P32>(keys, start + c0, min(SB_CHUNK, n - c0), s_x + c0, lane) && lane == 0)
-            *s_flag = tag;
+        seg_sort_wave_to_lds<8, P32>(keys, start + c0, min(SB_CHUNK, n - c0), s_x + c0, lane);
     }
     __syncthreads();
-    if (P32 && *s_flag == tag) {
-        __syncthreads();  // every thread has read the flag before the LDS is reused
-        return false;
-    }
     if (t_mid) *t_mid = stamp_now();
     if (n <= 256u * 4u) seg_merge_ranks<4>(s_x, n, nch, start, sorted_u, keys_out);
     else seg_merge_ranks<8>(s_x, n, nch, start, sorted_u, keys_out);
     __syncthreads();  // s_x is reused by the next chunk / tile
-    return true;
 }
 
-// Every tile up to SEG_BLOCK_CAP instances, in one persistent launch (the workgroups loop over the tiles, whose
-// counts are only known on the device, so every wave reaches the exit), on 32-bit proxy keys (P32, else on
-// the 64-bit keys: the A/B reference, knob "seg32"):
-//   1. tiles of (SEG_CAP, SEG_BLOCK_CAP] instances, one workgroup each (seg_lds_sort).  With the LPT order
-//      they are exactly its first long_cnt[0] + long_cnt[1] slots (SEG_CAP + 1 is a multiple of the LPT
-//      bucket width), taken longest first; tiles above SEG_BLOCK_CAP among them are left to seg_huge;
+// A tile above SEG_BLOCK_CAP instances, by one workgroup: SEG_BLOCK_CAP-key chunks sorted in LDS and written to
+// keys2, then every key placed by its rank in each other chunk (binary searches over the workgroup's own stores,
+// ordered by a device-scope fence).
+template <bool P32>
+__device__ void seg_tile_chunked(const SegSortParams &p, uint2 rg, uint32_t n, unsigned long long *s_x, int w,
+                                 int lane) {
+    for (uint32_t c0 = 0; c0 < n; c0 += SEG_BLOCK_CAP)
+        seg_lds_sort<P32>(p.keys, rg.x + c0, min(SEG_BLOCK_CAP, n - c0), nullptr, p.keys2, s_x, w, lane);
+    __threadfence();
+    __syncthreads();
+    const unsigned long long *kk = p.keys2 + rg.x;
+    const uint32_t nch = (n + SEG_BLOCK_CAP - 1) / SEG_BLOCK_CAP;
+    for (uint32_t e = threadIdx.x; e < n; e += 256) {
+        const unsigned long long key = kk[e];
+        const uint32_t c = e / SEG_BLOCK_CAP;
+        uint32_t pos = e - c * SEG_BLOCK_CAP;
+        for (uint32_t c2 = 0; c2 < nch; c2++) {
+            if (c2 == c) continue;
+            const unsigned long long *ch = kk + c2 * SEG_BLOCK_CAP;
+            uint32_t lo = 0, hi = min(SEG_BLOCK_CAP, n - c2 * SEG_BLOCK_CAP);  // first index with ch[i] >= key
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (ch[mid] < key) lo = mid + 1; else hi = mid;
+            }
+            pos += lo;
+        }
+        p.sorted_u[rg.x + pos] = (uint32_t)key;
+    }
+    __syncthreads();
+}
+
+// Every tile, in one persistent launch (the workgroups loop over the tiles, whose counts are only known on the
+// device, so every wave reaches the exit), on 32-bit proxy keys (P32, else on the 64-bit keys: the A/B reference,
+// knob "seg32"):
+//   1. tiles above SEG_CAP instances, one workgroup each: up to SEG_BLOCK_CAP in LDS (seg_lds_sort), longer ones in
+//      chunks (seg_tile_chunked).  With the LPT order they are exactly its first long_cnt[0] + long_cnt[1] slots
+//      (SEG_CAP + 1 is a multiple of the LPT bucket width), taken longest first; without it, lists 0 and 1;
 //   2. then the short tiles, one wave each (seg_sort_wave), again longest first.
-// A tile whose proxy keys tie is appended to tie_list for seg_huge.
+// Proxy-key ties are repaired in place (seg_sort_wave32), so no second launch is needed (round 4 handed unresolved
+// tie tiles, and the tiles above SEG_BLOCK_CAP, to a seg_huge launch whose ~5-us floor every step paid).
 template <bool P32, int MIN_WAVES = 1>
 __global__ __launch_bounds__(256, MIN_WAVES) void seg_sort_kernel(SegSortParams p) {
     __shared__ unsigned long long s_x[SEG_BLOCK_CAP];
-    __shared__ uint32_t s_flag;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    if (threadIdx.x == 0) s_flag = 0u;
-    __syncthreads();
     const uint32_t n0 = p.long_cnt[0], nlong = n0 + p.long_cnt[1];
-    const uint32_t nl = p.tile_order ? nlong : n0;
-    for (uint32_t i = blockIdx.x; i < nl; i += gridDim.x) {
-        const uint32_t tile = p.tile_order ? p.tile_order[i] : p.long_list[i];
+    for (uint32_t i = blockIdx.x; i < nlong; i += gridDim.x) {
+        const uint32_t tile = p.tile_order ? p.tile_order[i] : i < n0 ? p.long_list[i] : p.long_list[p.T + 1 + (i - n0)];
         const uint2 rg = p.ranges[tile];
         const uint32_t n = rg.y - rg.x;
-        if (n <= SEG_CAP || n > SEG_BLOCK_CAP) continue;  // workgroup-uniform
-        const uint32_t t0 = p.stamps ? stamp_now() : 0u;
-        uint32_t t1 = 0;
-        if (!seg_lds_sort<P32>(p.keys, rg.x, n, p.sorted_u, nullptr, s_x, w, lane, &s_flag, i + 1u,
-                               p.stamps ? &t1 : nullptr)) {
-            if (threadIdx.x == 0) p.tie_list[atomicAdd(p.tie_cnt, 1u)] = tile;
+        if (n <= SEG_CAP) continue;  // workgroup-uniform
+        if (n > SEG_BLOCK_CAP) {
+            seg_tile_chunked<P32>(p, rg, n, s_x, w, lane);
             continue;
         }
+        const uint32_t t0 = p.stamps ? stamp_now() : 0u;
+        uint32_t t1 = 0;
+        seg_lds_sort<P32>(p.keys, rg.x, n, p.sorted_u, nullptr, s_x, w, lane, p.stamps ? &t1 : nullptr);
         if (p.stamps && threadIdx.x == 0 && i < (uint32_t)STAMP_SLOTS) p.stamps[i] = make_uint4(t0, t1, stamp_now(), n);
     }
     const uint32_t s0 = p.tile_order ? nlong : 0u;
@@ -854,64 +880,10 @@ __global__ __launch_bounds__(256, MIN_WAVES) void seg_sort_kernel(SegSortParams 
         const uint32_t n = rg.y - rg.x;
         if (n == 0 || n > SEG_CAP) continue;  // wave-uniform
         unsigned long long *scratch = s_x + w * SB_WAVE_SCRATCH;
-        bool ok;
-        if (n <= 64u) ok = seg_sort_wave<1, P32>(p.keys, rg.x, n, p.sorted_u, lane, scratch);
-        else if (n <= 128u) ok = seg_sort_wave<2, P32>(p.keys, rg.x, n, p.sorted_u, lane, scratch);
-        else if (n <= 256u) ok = seg_sort_wave<4, P32>(p.keys, rg.x, n, p.sorted_u, lane, scratch);
-        else ok = seg_sort_wave<8, P32>(p.keys, rg.x, n, p.sorted_u, lane, scratch);
-        if (lane == 0 && !ok) p.tie_list[atomicAdd(p.tie_cnt, 1u)] = tile;
-    }
-}
-
-// On the full 64-bit keys, one workgroup per tile: the tiles above SEG_BLOCK_CAP instances (list 1), then the
-// tiles seg_sort handed over after a proxy-key tie.  A short tie tile is sorted by wave 0 in registers; the
-// others in LDS (dynamic, lds_keys keys) when they fit, else in SEG_BLOCK_CAP-key chunks written to keys2 and
-// placed by merge ranks searched in global memory (the workgroup's own stores, ordered by a device-scope fence).
-__global__ __launch_bounds__(256) void seg_huge_kernel(SegSortParams p, uint32_t lds_keys) {
-    extern __shared__ unsigned long long s_k[];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t nh = p.long_cnt[1], nt = *p.tie_cnt;
-    for (uint32_t h = blockIdx.x; h < nh + nt; h += gridDim.x) {
-        const uint32_t tile = h < nh ? p.long_list[p.T + 1 + h] : p.tie_list[h - nh];
-        const uint2 rg = p.ranges[tile];
-        const uint32_t n = rg.y - rg.x;
-        if (n <= SEG_CAP) {  // workgroup-uniform; waves 1-3 go on to the next tile
-            if (w == 0) {
-                if (n <= 64u) seg_sort_wave<1, false>(p.keys, rg.x, n, p.sorted_u, lane, nullptr);
-                else if (n <= 128u) seg_sort_wave<2, false>(p.keys, rg.x, n, p.sorted_u, lane, nullptr);
-                else if (n <= 256u) seg_sort_wave<4, false>(p.keys, rg.x, n, p.sorted_u, lane, nullptr);
-                else seg_sort_wave<8, false>(p.keys, rg.x, n, p.sorted_u, lane, nullptr);
-            }
-            continue;
-        }
-        if (n <= lds_keys) {
-            seg_lds_sort<false>(p.keys, rg.x, n, p.sorted_u, nullptr, s_k, w, lane, nullptr, 0u);
-            continue;
-        }
-        for (uint32_t c0 = 0; c0 < n; c0 += SEG_BLOCK_CAP)
-            seg_lds_sort<false>(p.keys, rg.x + c0, min(SEG_BLOCK_CAP, n - c0), nullptr, p.keys2, s_k, w, lane,
-                                nullptr, 0u);
-        __threadfence();
-        __syncthreads();
-        const unsigned long long *kk = p.keys2 + rg.x;
-        const uint32_t nch = (n + SEG_BLOCK_CAP - 1) / SEG_BLOCK_CAP;
-        for (uint32_t e = threadIdx.x; e < n; e += 256) {
-            const unsigned long long key = kk[e];
-            const uint32_t c = e / SEG_BLOCK_CAP;
-            uint32_t pos = e - c * SEG_BLOCK_CAP;
-            for (uint32_t c2 = 0; c2 < nch; c2++) {
-                if (c2 == c) continue;
-                const unsigned long long *ch = kk + c2 * SEG_BLOCK_CAP;
-                uint32_t lo = 0, hi = min(SEG_BLOCK_CAP, n - c2 * SEG_BLOCK_CAP);  // first index with ch[i] >= key
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (ch[mid] < key) lo = mid + 1; else hi = mid;
-                }
-                pos += lo;
-            }
-            p.sorted_u[rg.x + pos] = (uint32_t)key;
-        }
-        __syncthreads();
+        if (n <= 64u) seg_sort_wave<1, P32>(p.keys, rg.x, n, p.sorted_u, lane, scratch);
+        else if (n <= 128u) seg_sort_wave<2, P32>(p.keys, rg.x, n, p.sorted_u, lane, scratch);
+        else if (n <= 256u) seg_sort_wave<4, P32>(p.keys, rg.x, n, p.sorted_u, lane, scratch);
+        else seg_sort_wave<8, P32>(p.keys, rg.x, n, p.sorted_u, lane, scratch);
     }
 }
 
@@ -959,8 +931,6 @@ void launch_seg_sort(hipStream_t s, const SegSortParams &p0) {
     else if (tuning("seg32", 1) && minw == 5) seg_sort_kernel<true, 5><<<grid, 256, 0, s>>>(p);
     else if (tuning("seg32", 1)) seg_sort_kernel<true><<<grid, 256, 0, s>>>(p);
     else seg_sort_kernel<false><<<grid, 256, 0, s>>>(p);
-    constexpr uint32_t HUGE_LDS_KEYS = 8192;  // 64 KB
-    seg_huge_kernel<<<512, 256, HUGE_LDS_KEYS * sizeof(unsigned long long), s>>>(p, HUGE_LDS_KEYS);
 }
 
 }  // namespace gsr

@@ -27,7 +27,7 @@ constexpr int GRAD_ROW = 10;                   // floats per instance gradient r
 // counters: [CNT_BIG] big-Gaussian count, [CNT_OVERFLOW] scan overflow flag, then CNT_NPART 64-bit partial
 // sums of the instance total (spread over addresses so the per-block atomics do not serialise), then CNT_NPART
 // partial maxima of the complemented kept depth keys (their minimum) and CNT_NPART of the kept depth keys
-enum Counter : int { CNT_BIG = 0, CNT_OVERFLOW = 2, CNT_SCAN_TICKET = 3, CNT_COL_TICKET = 4, CNT_LONG = 6, CNT_TIES = 8, CNT_PRE_DONE = 10, CNT_PARTIALS = 16, CNT_NPART = 64,
+enum Counter : int { CNT_BIG = 0, CNT_OVERFLOW = 2, CNT_SCAN_TICKET = 3, CNT_COL_TICKET = 4, CNT_LONG = 6, CNT_PRE_DONE = 10, CNT_PARTIALS = 16, CNT_NPART = 64,
                      CNT_DMIN = 16 + 2 * 64, CNT_DMAX = CNT_DMIN + 64, CNT_WORDS = CNT_DMAX + 64 };
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }
@@ -263,7 +263,6 @@ struct ImageState {
     uint32_t *bk_reg_start;  // T / BK_REGION + 2: region starts
     uint32_t *bk_tile_start; // T + 1
     uint32_t *bk_long_list;  // 2 x (T + 1): tiles of (SEG_CAP, SEG_BLOCK_CAP] instances, longer tiles
-    uint32_t *bk_tie_list;   // T + 1: tiles whose 32-bit proxy-key sort did not converge
     // segmented backward (num_tiles <= SEG_MAX_TILES): each pixel's final colour / inverse-depth sums, tile-major
     // (tile t, plane c, pixel i at t * 1024 + c * 256 + i); the checkpoint spacing K the forward used (0: none);
     // the backward's segment count
@@ -300,7 +299,6 @@ inline size_t carve_image(char *base, int W, int H, ImageState &im) {
     im.bk_reg_start = c.take<uint32_t>(nt / BK_REGION + 2);
     im.bk_tile_start = c.take<uint32_t>(nt + 1);
     im.bk_long_list = c.take<uint32_t>(2 * (nt + 1));
-    im.bk_tie_list = c.take<uint32_t>(nt + 1);
     im.ctot = c.take<float>(nt <= SEG_MAX_TILES ? nt * 1024 : 1);
     im.ck_flag = c.take<uint32_t>(1);
     im.seg_count = c.take<uint32_t>(1);
@@ -1006,10 +1004,17 @@ __device__ __forceinline__ void lpt_order_block(const uint2 *__restrict__ ranges
     const bool cached = T <= nt * LPT_KMAX;
     uint32_t wt[LPT_KMAX];
     uint32_t mx = 0;
+    if (cached) {
+        // every load issued before any use: unconditional (clamped index), since a load in a branch waits for its
+        // data before the next one is issued
 #pragma unroll
-    for (int k = 0; k < LPT_KMAX; k++) {  // every load issued before any use
-        const int t = tid + k * nt;
-        wt[k] = (cached && t < T) ? load_w(t) : 0u;
+        for (int k = 0; k < LPT_KMAX; k++) wt[k] = load_w(min(tid + k * nt, max(T - 1, 0)));
+#pragma unroll
+        for (int k = 0; k < LPT_KMAX; k++)
+            if (tid + k * nt >= T) wt[k] = 0u;
+    } else {
+#pragma unroll
+        for (int k = 0; k < LPT_KMAX; k++) wt[k] = 0u;
     }
 #pragma unroll
     for (int k = 0; k < LPT_KMAX; k++) mx = max(mx, wt[k]);

@@ -848,8 +848,16 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
                         ok = (ok & ~near) | (okx & near);
                     }
                 }
-                const uint64_t take = ok & ~low, stop = ok & low;
-                if (SMASK && take) cb[k] |= bit;
+                uint64_t take;
+                if constexpr (SMASK) {  // cb[k] |= bit when take != 0: a select on the flag the s_andn2 forming take
+                                        // sets (the compiler re-tests take and selects both halves: 4 SALU, not 2)
+                    const uint64_t cbt = cb[k] | bit;
+                    asm("s_andn2_b64 %0, %2, %3\n\ts_cselect_b64 %1, %4, %1"
+                        : "=&s"(take), "+s"(cb[k]) : "s"(ok), "s"(low), "s"(cbt) : "scc");
+                } else {
+                    take = ok & ~low;
+                }
+                const uint64_t stop = ok & low;
                 const float wgt = select_mask(take, alpha * T[k], 0.f);
                 C0[k] = fmaf(b.z, wgt, C0[k]);
                 C1[k] = fmaf(b.w, wgt, C1[k]);

@@ -136,7 +136,6 @@ struct SegSortParams {
     unsigned long long *keys2;  // R: chunk-sorted keys of the tiles longer than SEG_BLOCK_CAP
     uint32_t *sorted_u;
     const uint32_t *long_list, *long_cnt;
-    uint32_t *tie_list, *tie_cnt;  // tiles whose proxy-key sort met a tie (count zeroed), re-sorted by seg_huge
     uint4 *stamps;  // diagnostics (set by launch): per long-tile slot (start, chunks sorted, end, n), or null
 };
 void launch_seg_sort(hipStream_t s, const SegSortParams &p);

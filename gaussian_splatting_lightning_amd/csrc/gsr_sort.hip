@@ -492,11 +492,16 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const KT *__restrict__ 
     uint32_t key[ITEMS], val[ITEMS], rank[ITEMS];
     const uint64_t lt = lanemask_lt(lane);
 #pragma unroll
-    for (int it = 0; it < ITEMS; it++) {  // loads first (see rs_onesweep_kernel)
+    for (int it = 0; it < ITEMS; it++) {  // loads first (see rs_onesweep_kernel), unconditional: clamped index
+        const uint32_t j = blk + w * ((ITEMS * 256) / 4) + it * 64 + lane, jc = min(j, n - 1);
+        key[it] = (uint32_t)keys_in[jc];
+        val[it] = IOTA_IN ? j : vals_in[jc];
+    }
+#pragma unroll
+    for (int it = 0; it < ITEMS; it++) {  // (a load in a branch waits for its data before the next is issued)
         const uint32_t j = blk + w * ((ITEMS * 256) / 4) + it * 64 + lane;
-        const bool valid = j < n;
-        key[it] = valid ? rs_rel_key<REL>((uint32_t)keys_in[j], kbase, kcap) : 0u;
-        val[it] = IOTA_IN ? j : (valid ? vals_in[j] : 0u);
+        key[it] = j < n ? rs_rel_key<REL>(key[it], kbase, kcap) : 0u;
+        if (!IOTA_IN && j >= n) val[it] = 0u;
     }
 #pragma unroll
     for (int it = 0; it < ITEMS; it++) {
@@ -568,17 +573,16 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const KT *__restrict__ 
             uint32_t g[8], gp[8];
             uint4 g4[8];
 #pragma unroll
-            for (int it = 0; it < 8; it++) {
-                const uint32_t i = i0 + tid + it * 256;
-                gp[it] = 0xffffffffu;
+            for (int it = 0; it < 8; it++) {  // gathers unconditional (clamped slot) so they issue together
+                const uint32_t i = i0 + tid + it * 256, ic = min(i, cnt_blk - 1);
+                const uint32_t k = s_keys[ic], v = s_vals[ic];
+                const uint32_t d = (k >> shift) & dmask;
+                gp[it] = i < cnt_blk ? s_gbase[d] + (i - s_dstart[d]) : 0xffffffffu;
+                if (ga.dst) g[it] = ga.src[v];
+                if (ga.dst4) g4[it] = ga.src4[v];
                 if (i < cnt_blk) {
-                    const uint32_t k = s_keys[i], v = s_vals[i];
-                    const uint32_t d = (k >> shift) & dmask;
-                    gp[it] = s_gbase[d] + (i - s_dstart[d]);
                     keys_out[gp[it]] = (KT)k;
                     vals_out[gp[it]] = v;
-                    if (ga.dst) g[it] = ga.src[v];
-                    if (ga.dst4) g4[it] = ga.src4[v];
                 }
             }
 #pragma unroll
