@@ -27,7 +27,10 @@ struct CullIn {
 // rect (0: not rendered); the tile culling, tile count and sort key are finished by preprocess_kernel.
 // SPLIT: the colour (SH evaluation, its Jacobian, the clamp bits and the colour words of the record) is left to
 // preprocess_color_kernel, launched behind the bucket count pass.
-template <bool SPLIT>
+// SHD >= 0: the SH degree at compile time (the common degree-3 launch).  With the runtime switch the compiler hoists the
+// degree-0 term common to every case (the first coefficient's load and multiply) above the switch, so the other 45
+// coefficients were only requested after that load had returned: one more memory round trip per wave.
+template <bool SPLIT, int SHD = -1>
 __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &p, const int i, CullIn &ci) {
     // uncontracted like the helpers it calls (gsr_common.h): radii, rects and render records bit-equal the oracle's
 #pragma clang fp contract(off)
@@ -49,6 +52,9 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
         q = make_float4(p.rotations[4 * i], p.rotations[4 * i + 1], p.rotations[4 * i + 2], p.rotations[4 * i + 3]);
         sc = load_f3(p.scales, i);
     }
+    // the camera position too (it was loaded, and waited for, just before the coefficients)
+    const float3 campos = p.campos ? make_float3(p.campos[0], p.campos[1], p.campos[2]) : make_float3(0.f, 0.f, 0.f);
+    const float3 dir_raw = mean - campos;  // formed here: later the compiler re-loaded the mean (another round trip)
     const float3 pv = xform3(mean, view);
     if (!(pv.z > 0.2f)) return 0u;  // in_frustum (camera_tools.py:5-8)
 
@@ -96,13 +102,13 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
     } else if (p.colors_precomp) {
         rgb = load_f3(p.colors_precomp, i);
     } else {
-        const float3 campos = make_float3(p.campos[0], p.campos[1], p.campos[2]);
-        float3 dir = mean - campos;
+        float3 dir = dir_raw;
         const float len = sqrtf(dot3(dir, dir));
         dir = make_float3(dir.x / len, dir.y / len, dir.z / len);
-        if (p.D > 0) {  // the colour and its direction Jacobian for the backward (9 planes, coalesced)
+        if (SHD > 0 || (SHD < 0 && p.D > 0)) {  // the colour and its direction Jacobian for the backward (9 planes)
             float3 jx, jy, jz;
-            rgb = sh_eval_jac_dispatch(p.D, p.shs + (size_t)i * p.M * 3, dir, jx, jy, jz);
+            if constexpr (SHD > 0) rgb = sh_eval_jac<SHD>(p.shs + (size_t)i * p.M * 3, dir, jx, jy, jz);
+            else rgb = sh_eval_jac_dispatch(p.D, p.shs + (size_t)i * p.M * 3, dir, jx, jy, jz);
             const size_t n = (size_t)p.P;
             float *J = g.sh_jac + i;
             J[0] = jx.x; J[n] = jx.y; J[2 * n] = jx.z;
@@ -209,7 +215,7 @@ __device__ __forceinline__ void publish_total(const PreprocessParams &p);
 // LATE_MINW: waves per SIMD the late-colour kernel is built for (4: 100 VGPRs; 5: 96 + a 20-B spill; 6: 80 + 92 B).
 // PRE_LATE_DIRECT: the late colour phase reading each lane's row straight from global memory (no staging): only the
 // register peak moves (the colour no longer overlaps the projection state).
-template <int MODE, int LATE_MINW = 4>
+template <int MODE, int LATE_MINW = 4, int SHD = -1>
 __global__ __launch_bounds__(256, MODE == PRE_SPLIT ? GSR_PRE_SPLIT_MINW
                                   : (MODE == PRE_LATE || MODE == PRE_LATE_DIRECT) ? LATE_MINW : GSR_PRE_MINW)
 void preprocess_kernel(PreprocessParams p) {
@@ -223,7 +229,7 @@ void preprocess_kernel(PreprocessParams p) {
     CullIn ci;
     ci.need = false;
     ci.vis = false;
-    const uint32_t area = i < p.P ? preprocess_gaussian<SPLIT>(p, i, ci) : 0u;
+    const uint32_t area = i < p.P ? preprocess_gaussian<SPLIT, SHD>(p, i, ci) : 0u;
     const uint32_t need_area = ci.need ? area : 0u;
     const uint32_t incl = wave_inclusive_scan(need_area, lane);
     const uint32_t total = __shfl((int)incl, 63);
@@ -400,6 +406,8 @@ void launch_preprocess(hipStream_t s, const PreprocessParams &p) {
     else if (p.late && tuning("pre_late_minw", 4) >= 6) preprocess_kernel<PRE_LATE, 6><<<div_up(p.P, 256), 256, 0, s>>>(p);
     else if (p.late && tuning("pre_late_minw", 4) == 5) preprocess_kernel<PRE_LATE, 5><<<div_up(p.P, 256), 256, 0, s>>>(p);
     else if (p.late) preprocess_kernel<PRE_LATE, 4><<<div_up(p.P, 256), 256, 0, s>>>(p);
+    else if (p.D == 3 && !p.colors_precomp && tuning("pre_shd", 1))
+        preprocess_kernel<PRE_FUSED, 4, 3><<<div_up(p.P, 256), 256, 0, s>>>(p);
     else preprocess_kernel<PRE_FUSED><<<div_up(p.P, 256), 256, 0, s>>>(p);
 }
 

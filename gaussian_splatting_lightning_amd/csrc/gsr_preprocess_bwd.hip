@@ -5,6 +5,10 @@
 #include "gsr_kernels.h"
 #include "gsr_sh.h"
 
+#ifndef GSR_PBWD_HOIST
+#define GSR_PBWD_HOIST 1
+#endif
+
 namespace gsr {
 
 // ------------------------------------------------------------------------------------------------
@@ -129,6 +133,25 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
     }
     const Mat4 view = load_mat4(p.view);
     const float3 mean = load_f3(p.means3D, i);
+    // The SH stage's inputs (clamp bits, camera, the forward's colour Jacobian) requested with the geometry's: issued
+    // at the SH stage, the clamp byte's round trip came before the Jacobian's nine loads were issued, two more memory
+    // round trips per wave after the geometry's (GSR_PBWD_HOIST 0: the old placement, for library A/Bs)
+    const bool sh_stage = p.shs && p.M > 0;  // uniform
+    uint8_t cl = 0;
+    float3 campos = make_float3(0, 0, 0), jx = campos, jy = campos, jz = campos;
+#if GSR_PBWD_HOIST
+    if (sh_stage) {
+        cl = p.clamped[i];
+        campos = make_float3(p.campos[0], p.campos[1], p.campos[2]);
+        if (p.D > 0) {
+            const size_t n = (size_t)p.P;
+            const float *J = p.sh_jac + i;
+            jx = make_float3(J[0], J[n], J[2 * n]);
+            jy = make_float3(J[3 * n], J[4 * n], J[5 * n]);
+            jz = make_float3(J[6 * n], J[7 * n], J[8 * n]);
+        }
+    }
+#endif
     float c6[6];
     float3 scale = make_float3(0, 0, 0);
     float4 rot = make_float4(1, 0, 0, 0);
@@ -228,16 +251,18 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
     // dL/dsh = basis(dir) (x) dRGB needs only the direction; the direction term of dL/dmeans3D uses the colour's
     // direction Jacobian the forward stored (sh_jac), so the 48 coefficients are not read here.  (The backward's
     // shs are the forward's, as in the autograd function and the upstream API.)
-    if (p.shs && p.M > 0) {
-        const uint8_t cl = p.clamped[i];
+    if (sh_stage) {
+#if !GSR_PBWD_HOIST
+        cl = p.clamped[i];
+        campos = make_float3(p.campos[0], p.campos[1], p.campos[2]);
+#endif
         const float3 dRGB = make_float3((cl & 1) ? 0.f : gs[6], (cl & 2) ? 0.f : gs[7], (cl & 4) ? 0.f : gs[8]);
-        const float3 campos = make_float3(p.campos[0], p.campos[1], p.campos[2]);
         if (p.dL_dcolors_sh) {
             p.dL_dcolors_sh[3 * i] = dRGB.x;
             p.dL_dcolors_sh[3 * i + 1] = dRGB.y;
             p.dL_dcolors_sh[3 * i + 2] = dRGB.z;
         }
-        float3 jx = make_float3(0, 0, 0), jy = jx, jz = jx;
+#if !GSR_PBWD_HOIST
         if (p.D > 0) {
             const size_t n = (size_t)p.P;
             const float *J = p.sh_jac + i;
@@ -245,6 +270,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
             jy = make_float3(J[3 * n], J[4 * n], J[5 * n]);
             jz = make_float3(J[6 * n], J[7 * n], J[8 * n]);
         }
+#endif
         float *dsh = p.dL_dsh ? p.dL_dsh + (size_t)i * ncoef : nullptr;  // null only with dL_dcolors_sh (API)
         if (LDS) {
             // LDS-staged block (M = 16): the kernel writes dL/dsh = basis (x) dRGB through LDS
