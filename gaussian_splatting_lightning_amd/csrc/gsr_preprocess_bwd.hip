@@ -58,16 +58,46 @@ __device__ __forceinline__ void cov3d_backward(float3 scale, float mod, float4 r
 // One Gaussian.  In the LDS-staged path (LDS) dL/dsh is not written here: the Gaussian's clamp-masked colour
 // gradient and view direction go to dRGB_out / dir_out (dRGB zero when not visible) for the kernel's staged
 // coalesced store; otherwise dL/dsh is written directly.
+// The camera, read at the kernel's start before any store, so the compiler proves nothing clobbers it and loads it
+// through the scalar unit (SGPRs) instead of vector loads with their own round trips (view at the geometry, projection
+// matrix and position after it)
+struct PbwdCamera {
+    Mat4 view, proj;
+    float3 campos;
+};
+__device__ __forceinline__ PbwdCamera load_camera(const PreprocessBwdParams &p) {
+    PbwdCamera c;
+    c.view = load_mat4(p.view);
+    c.proj = load_mat4(p.proj);
+    c.campos = (p.shs && p.M > 0) ? make_float3(p.campos[0], p.campos[1], p.campos[2]) : make_float3(0, 0, 0);
+    return c;
+}
 template <bool LDS>
-__device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p, const int i, bool have_gs,
+__device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p, const PbwdCamera &cam, const int i,
+                                                   const int radius, const uint32_t n_tiles, bool have_gs,
                                                    const float (&gs_in)[10], float3 &dRGB_out, float3 &dir_out) {
-    const bool vis = p.radii[i] > 0;
+    // radius and kept-tile count: the caller's loads (reloaded here they took a round trip of their own)
+    const bool vis = radius > 0;
+    // The densification statistics' read-modify-writes: the reads issued here, the writes at the end (put_stats).
+    // Read and written in place they cost two memory round trips before the geometry's loads were issued.
+    float2 st_old = make_float2(0.f, 0.f);
+    int mr_old = 0;
+    if (p.densify_stats && p.densify_accumulate) st_old = *reinterpret_cast<const float2 *>(p.densify_stats + 2 * i);
+    if (p.max_radii2D) mr_old = p.max_radii2D[i];
     float gs[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    if (vis && have_gs && p.tiles[i] <= BIG_GAUSSIAN_TILES) {
+    auto put_stats = [&]() {
+        if (p.densify_stats) {  // torch.linalg.vector_norm(grad[:, :2]) and the visibility count of this view
+            float2 st = make_float2(sqrtf(gs[0] * gs[0] + gs[1] * gs[1]), vis ? 1.f : 0.f);
+            if (p.densify_accumulate) st = make_float2(st_old.x + st.x, st_old.y + st.y);
+            *reinterpret_cast<float2 *>(p.densify_stats + 2 * i) = st;
+        }
+        if (p.max_radii2D) p.max_radii2D[i] = max(mr_old, radius);
+    };
+    if (vis && have_gs && n_tiles <= BIG_GAUSSIAN_TILES) {
 #pragma unroll
         for (int k = 0; k < 10; k++) gs[k] = gs_in[k];
     } else if (vis) {
-        const uint32_t start = p.inst_start[i], cnt = p.tiles[i];
+        const uint32_t start = p.inst_start[i], cnt = n_tiles;
         if (cnt > BIG_GAUSSIAN_TILES) {
             add_row(p.bigsum, p.big_slot[i], gs);
         } else {
@@ -100,16 +130,6 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
         p.dL_dmeans2D[3 * i + 1] = gs[1];
         p.dL_dmeans2D[3 * i + 2] = 0.f;
     }
-    if (p.densify_stats) {  // torch.linalg.vector_norm(grad[:, :2]) and the visibility count of this view
-        float2 st = make_float2(sqrtf(gs[0] * gs[0] + gs[1] * gs[1]), vis ? 1.f : 0.f);
-        float2 *dst = reinterpret_cast<float2 *>(p.densify_stats + 2 * i);
-        if (p.densify_accumulate) {
-            const float2 old = *dst;
-            st = make_float2(old.x + st.x, old.y + st.y);
-        }
-        *dst = st;
-    }
-    if (p.max_radii2D) p.max_radii2D[i] = max(p.max_radii2D[i], p.radii[i]);
     if (p.dL_dcolors) {
         p.dL_dcolors[3 * i] = gs[6];
         p.dL_dcolors[3 * i + 1] = gs[7];
@@ -129,20 +149,21 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
         if (p.dL_dscales) { p.dL_dscales[3 * i] = 0.f; p.dL_dscales[3 * i + 1] = 0.f; p.dL_dscales[3 * i + 2] = 0.f; }
         if (p.dL_drot)
             for (int k = 0; k < 4; k++) p.dL_drot[4 * i + k] = 0.f;
+        put_stats();
         return;
     }
-    const Mat4 view = load_mat4(p.view);
+    const Mat4 &view = cam.view;
     const float3 mean = load_f3(p.means3D, i);
     // The SH stage's inputs (clamp bits, camera, the forward's colour Jacobian) requested with the geometry's: issued
     // at the SH stage, the clamp byte's round trip came before the Jacobian's nine loads were issued, two more memory
     // round trips per wave after the geometry's (GSR_PBWD_HOIST 0: the old placement, for library A/Bs)
     const bool sh_stage = p.shs && p.M > 0;  // uniform
     uint8_t cl = 0;
-    float3 campos = make_float3(0, 0, 0), jx = campos, jy = campos, jz = campos;
+    const float3 campos = cam.campos;
+    float3 jx = make_float3(0, 0, 0), jy = jx, jz = jx;
 #if GSR_PBWD_HOIST
     if (sh_stage) {
         cl = p.clamped[i];
-        campos = make_float3(p.campos[0], p.campos[1], p.campos[2]);
         if (p.D > 0) {
             const size_t n = (size_t)p.P;
             const float *J = p.sh_jac + i;
@@ -237,7 +258,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
     float3 dm = make_float3(vm[0] * dtx + vm[1] * dty + vm[2] * dtz, vm[4] * dtx + vm[5] * dty + vm[6] * dtz,
                             vm[8] * dtx + vm[9] * dty + vm[10] * dtz);
     // ---- 2D mean -> 3D mean through the projection ----
-    const Mat4 proj = load_mat4(p.proj);
+    const Mat4 &proj = cam.proj;
     const float *pm = proj.m;
     const float4 mh = xform4(mean, proj);
     const float m_w = 1.0f / (mh.w + 0.0000001f);
@@ -254,7 +275,6 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
     if (sh_stage) {
 #if !GSR_PBWD_HOIST
         cl = p.clamped[i];
-        campos = make_float3(p.campos[0], p.campos[1], p.campos[2]);
 #endif
         const float3 dRGB = make_float3((cl & 1) ? 0.f : gs[6], (cl & 2) ? 0.f : gs[7], (cl & 4) ? 0.f : gs[8]);
         if (p.dL_dcolors_sh) {
@@ -307,6 +327,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
         if (p.dL_drot)
             for (int k = 0; k < 4; k++) p.dL_drot[4 * i + k] = 0.f;
     }
+    put_stats();
 }
 
 // dL/dsh (192 B per Gaussian at M = 16) is written through LDS: each half of a wave's 64 Gaussians writes its
@@ -324,13 +345,17 @@ constexpr int PBWD_STAGE = 32 * SH_STRIDE;  // floats of LDS per wave
 template <bool LDS_SH>
 __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams p) {
     const int i = p.g0 + blockIdx.x * 256 + threadIdx.x;
+    const PbwdCamera cam = load_camera(p);  // before the first store (scalar loads)
     if (p.campos_rows && blockIdx.x == 0)  // the exchange's camera block (row campos_rank = campos, others zero)
         for (int t = threadIdx.x; t < 3 * p.campos_nrows; t += 256)
             p.campos_rows[t] = t / 3 == p.campos_rank ? p.campos[t % 3] : 0.f;
     if (!LDS_SH) {
         const float none[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         float3 d3, v3;
-        if (i < p.g1) preprocess_bwd_one<false>(p, i, false, none, d3, v3);
+        if (i < p.g1) {
+            const int rad = p.radii[i];
+            preprocess_bwd_one<false>(p, cam, i, rad, rad > 0 ? p.tiles[i] : 0u, false, none, d3, v3);
+        }
         return;
     }
     __shared__ __attribute__((aligned(16))) float s_sh[4][PBWD_STAGE];
@@ -345,9 +370,12 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
     // loops of dependent loads cost ~40 % of the kernel otherwise.  Gaussians above BIG_GAUSSIAN_TILES rows
     // take their block-reduced sum in preprocess_bwd_one.
     float gs[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    int rad;
+    uint32_t cnt;
     {
-        const bool vis = i < p.g1 && p.radii[i] > 0;
-        const uint32_t cnt = vis ? p.tiles[i] : 0u;
+        rad = i < p.g1 ? p.radii[i] : 0;
+        const bool vis = rad > 0;
+        cnt = vis ? p.tiles[i] : 0u;
         const uint32_t len = cnt <= BIG_GAUSSIAN_TILES ? cnt : 0u;
         const uint32_t incl = wave_inclusive_scan(len, lane);
         const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
@@ -420,7 +448,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         }
     }
     float3 dRGB = make_float3(0.f, 0.f, 0.f), dir = make_float3(1.f, 0.f, 0.f);
-    if (i < p.g1) preprocess_bwd_one<true>(p, i, true, gs, dRGB, dir);
+    if (i < p.g1) preprocess_bwd_one<true>(p, cam, i, rad, cnt, true, gs, dRGB, dir);
     if (!p.dL_dsh) return;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
