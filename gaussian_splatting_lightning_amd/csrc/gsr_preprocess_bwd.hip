@@ -105,23 +105,18 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
             // group, before summing (memory-level parallelism)
             for (uint32_t k0 = 0; k0 < cnt; k0 += 4) {
                 bool use[4];
+                uint32_t iv[4];
 #pragma unroll
-                for (int j = 0; j < 4; j++)
-                    use[j] = k0 + j < cnt && p.inv[start + k0 + j] != INV_NONE;
+                for (int j = 0; j < 4; j++) iv[j] = p.inv[start + min(k0 + j, cnt - 1)];  // unconditional (clamped)
+#pragma unroll
+                for (int j = 0; j < 4; j++) use[j] = k0 + j < cnt && iv[j] != INV_NONE;
                 float rw[4][10];
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    if (use[j]) {
-                        load_row(p.rows, (size_t)(start + k0 + j), rw[j]);
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < 10; k++) rw[j][k] = 0.f;
-                    }
-                }
+                for (int j = 0; j < 4; j++) load_row(p.rows, use[j] ? (size_t)(start + k0 + j) : 0u, rw[j]);  // row 0: dropped
 #pragma unroll
                 for (int j = 0; j < 4; j++)
 #pragma unroll
-                    for (int k = 0; k < 10; k++) gs[k] += rw[j][k];
+                    for (int k = 0; k < 10; k++) gs[k] += use[j] ? rw[j][k] : 0.f;
             }
         }
     }
@@ -373,9 +368,13 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
     int rad;
     uint32_t cnt;
     {
-        rad = i < p.g1 ? p.radii[i] : 0;
+        // radius, kept-tile count and first expansion index loaded together (clamped index, selected after)
+        const int ic = min(i, p.g1 - 1);
+        const int rad_l = p.radii[ic];
+        const uint32_t cnt_l = p.tiles[ic], ist_l = p.inst_start[ic];
+        rad = i < p.g1 ? rad_l : 0;
         const bool vis = rad > 0;
-        cnt = vis ? p.tiles[i] : 0u;
+        cnt = vis ? cnt_l : 0u;
         const uint32_t len = cnt <= BIG_GAUSSIAN_TILES ? cnt : 0u;
         const uint32_t incl = wave_inclusive_scan(len, lane);
         const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
@@ -384,24 +383,22 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         // (first pair, first expansion index) of each lane's Gaussian, behind the chunk
         uint2 *s_meta = reinterpret_cast<uint2 *>(sw + CH * 10);
         static_assert(CH * 10 + 128 <= PBWD_STAGE, "row chunk + meta fit the staging area");
-        s_meta[lane] = make_uint2(pst, len ? p.inst_start[i] : 0u);
+        s_meta[lane] = make_uint2(pst, len ? ist_l : 0u);
         wave_lds_sync();
-        // the inv words of chunk c0 (expansion index uu, written-row marker sidx)
+        // the inv words of chunk c0 (expansion index uu, written-row marker sidx; pairs past the wave's total read
+        // inv[0] and are dropped at use).  Every load is unconditional: a load (or a row load) under a branch made the
+        // compiler wait for it before the next pair's test, one memory round trip per pair instead of per chunk.
         auto inv_chunk = [&](uint32_t c0, uint32_t (&uu)[PER], uint32_t (&sidx)[PER]) {
 #pragma unroll
             for (uint32_t r = 0; r < PER; r++) {
                 const uint32_t j = c0 + r * 64 + lane;
-                sidx[r] = INV_NONE;
-                uu[r] = 0;
-                if (j < total) {
-                    int o = 0;
+                int o = 0;
 #pragma unroll
-                    for (int step = 32; step; step >>= 1)
-                        if (s_meta[o + step].x <= j) o += step;
-                    const uint2 m = s_meta[o];
-                    uu[r] = m.y + (j - m.x);
-                    sidx[r] = p.inv[uu[r]];
-                }
+                for (int step = 32; step; step >>= 1)
+                    if (s_meta[o + step].x <= j) o += step;
+                const uint2 m = s_meta[o];
+                uu[r] = j < total ? m.y + (j - m.x) : 0u;
+                sidx[r] = p.inv[uu[r]];
             }
         };
 #if GSR_PBWD_INV_AHEAD
@@ -421,11 +418,11 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
 #else
             inv_chunk(c0, uu, sidx);  // all inv words of the chunk first ...
 #endif
+            bool use[PER];
 #pragma unroll
-            for (uint32_t r = 0; r < PER; r++) {  // ... then only the rows the composite wrote
-#pragma unroll
-                for (int k = 0; k < 10; k++) rw[r][k] = 0.f;
-                if (sidx[r] != INV_NONE) load_row(p.rows, uu[r], rw[r]);
+            for (uint32_t r = 0; r < PER; r++) {  // ... then the rows the composite wrote (others read row 0, dropped)
+                use[r] = c0 + r * 64 + lane < total && sidx[r] != INV_NONE;
+                load_row(p.rows, use[r] ? uu[r] : 0u, rw[r]);
             }
 #if GSR_PBWD_INV_AHEAD
             if (c0 + CH < total) inv_chunk(c0 + CH, uu_n, sidx_n);  // the next chunk's inv words meanwhile
@@ -435,7 +432,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
                 const uint32_t q = r * 64 + lane;  // pair within the chunk
                 float *d = sw + q * 10;
 #pragma unroll
-                for (int k = 0; k < 10; k++) d[k] = rw[r][k];
+                for (int k = 0; k < 10; k++) d[k] = use[r] ? rw[r][k] : 0.f;
             }
             wave_lds_sync();
             const uint32_t lo = max(pst, c0), hi = min(pst + len, c0 + CH);
