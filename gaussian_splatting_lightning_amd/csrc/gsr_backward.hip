@@ -668,14 +668,14 @@ __global__ __launch_bounds__(256) void big_reduce_kernel(BigReduceParams p) {
         for (uint32_t k0 = threadIdx.x; k0 < cnt; k0 += 256 * BR_UNROLL) {
             float r[BR_UNROLL][10];
             bool use[BR_UNROLL];
-            uint32_t iv[BR_UNROLL];
+            // (guarded loads: unconditional clamped inv loads measured +10 us at cfg 5, where most of the 4 x 256 slots
+            // of a big Gaussian lie past its count)
 #pragma unroll
-            for (int q = 0; q < BR_UNROLL; q++)  // unconditional (clamped): a load under `k < cnt &&` waited for its
-                iv[q] = p.inv[start + min(k0 + 256 * q, cnt - 1)];  // data before the next was issued
-#pragma unroll
-            for (int q = 0; q < BR_UNROLL; q++) use[q] = k0 + 256 * q < cnt && iv[q] != INV_NONE;
-            // (rows stay under `if (use)`: loading row 0 for the unwritten ones, so that no load sits in a branch,
-            // measured +5 us at cfg 5, where most rows of a big Gaussian are unwritten)
+            for (int q = 0; q < BR_UNROLL; q++) {
+                const uint32_t k = k0 + 256 * q;
+                use[q] = k < cnt && p.inv[start + k] != INV_NONE;
+            }
+            // (rows stay under `if (use)`: loading row 0 for the unwritten ones instead measured slower at cfg 5)
 #pragma unroll
             for (int q = 0; q < BR_UNROLL; q++)
                 if (use[q]) load_row(p.rows, start + k0 + 256 * q, r[q]);
