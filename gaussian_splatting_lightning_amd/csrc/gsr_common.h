@@ -1008,7 +1008,8 @@ __device__ __forceinline__ void lpt_order_block(const uint2 *__restrict__ ranges
         // every load issued before any use: unconditional (clamped index), since a load in a branch waits for its
         // data before the next one is issued
 #pragma unroll
-        for (int k = 0; k < LPT_KMAX; k++) wt[k] = load_w(min(tid + k * nt, max(T - 1, 0)));
+        for (int k = 0; k < LPT_KMAX; k++)
+            wt[k] = k * nt < T ? load_w(min(tid + k * nt, T - 1)) : 0u;  // (k * nt < T: uniform, only rounds in use)
 #pragma unroll
         for (int k = 0; k < LPT_KMAX; k++)
             if (tid + k * nt >= T) wt[k] = 0u;
