@@ -749,15 +749,18 @@ def test_tile_sort_digit_width_is_invisible(gpu_device, db):
         assert np.array_equal(ref[k], alt[k]), k
 
 
-@pytest.mark.parametrize("mode", ["split", "late4", "late6", "direct"])
+@pytest.mark.parametrize("mode", ["split", "late4", "late6", "direct", "runtime_degree"])
 @pytest.mark.parametrize("deg,cdeg,bucket", [(3, 3, 1), (2, 3, 1), (1, 3, 0), (1, 1, 0), (0, 0, 1)])
 def test_split_colour_preprocess_is_bitwise_the_fused_one(gpu_device, deg, cdeg, bucket, mode):
     """The SH colour evaluated by its own kernel behind the bucket count pass ("pre_split" 1), or at the end of the
     preprocess from LDS-staged coefficient rows ("pre_late" 1, 16 coefficients; built for 4 or 6 waves per SIMD) or
-    from rows read directly ("pre_late" 2), gives bitwise the records, outputs and gradients of the fused preprocess (colour inside the projection)."""
+    from rows read directly ("pre_late" 2), or with the SH degree dispatched at run time instead of the compile-time
+    degree-3 kernel ("pre_shd" 0), gives bitwise the records, outputs and gradients of the fused preprocess (colour inside the
+    projection)."""
     knobs = {"split": dict(pre_split=1, pre_late=0), "late4": dict(pre_split=0, pre_late=1, pre_late_minw=4),
              "late6": dict(pre_split=0, pre_late=1, pre_late_minw=6),
-             "direct": dict(pre_split=0, pre_late=2, pre_late_minw=6)}[mode]
+             "direct": dict(pre_split=0, pre_late=2, pre_late_minw=6),
+             "runtime_degree": dict(pre_split=0, pre_late=0, pre_shd=0)}[mode]
     from gaussian_splatting_lightning_amd import _native
     inp = scene_inputs(60_000, 640, 480, sh_degree=deg, seed=12 + deg, coeff_degree=cdeg)
     dc, di = upstream(640, 480, 12 + deg)
