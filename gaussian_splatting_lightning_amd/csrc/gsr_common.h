@@ -200,7 +200,7 @@ struct BinningState {
     SortScratch sort;      // radix path: tile sort (R keys); its final value buffer is sorted_u
     unsigned long long *bk_keys;  // bucket path: R keys (depth << 32 | u) bucketed by tile
     unsigned long long *bk_keys2; // bucket path: R, the region scatter's keys grouped by region, then the chunk-sorted
-                                  //    keys of tiles longer than SEG_BLOCK_CAP (seg_huge)
+                                  //    keys of tiles longer than SEG_BLOCK_CAP (seg_sort's chunked path)
     // segmented backward (small images, num_tiles <= SEG_MAX_TILES; else null): the forward's per-pixel checkpoints
     // at every K-th instance of a tile (CK_FLOATS each: T, then the colour / inverse-depth sums so far), tile t's
     // checkpoint j (before instance (j + 1) K) at index ranges[t].x / K + t + j; and the backward's work list

@@ -644,8 +644,9 @@ def test_segmented_backward_without_checkpoints(gpu_device):
 
 @pytest.mark.parametrize("n,W,H", [(60_000, 96, 64), (50_000, 32, 32)])
 def test_long_tiles_and_depth_ties(gpu_device, n, W, H):
-    """Bucket binning on tiles beyond one wave's register sort (> 511 instances: seg_block; > 2048: seg_huge in
-    LDS; > 8192: seg_huge's chunks placed by merge ranks) and on exact depth ties (duplicated Gaussians: the
+    """Bucket binning on tiles beyond one wave's register sort (> 511 instances: a workgroup's chunk sorts merged in
+    LDS; > 2048: 2048-key chunks placed by merge ranks in global memory) and on exact depth ties (duplicated Gaussians:
+    proxy-key tie runs of 200 and 300 repaired by odd-even passes to convergence; the
     (tile, depth, index) order falls back to the Gaussian index, as the reference's stable radix sort does)."""
     inp = scene_inputs(n, W, H, sh_degree=1, seed=23)
     for k in ("means3D", "scales", "rotations", "opacities", "shs"):

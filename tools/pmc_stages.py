@@ -23,7 +23,7 @@ FIXED = [  # (substring of the kernel name, stage) for kernels that always belon
     ("render_fwd", "render_fwd"), ("render_bwd", "render_bwd"), ("big_reduce", "big_reduce"),
     ("bk_walk_kernel<false", "bucket_count_walk"), ("bk_walk_kernel<true", "bucket_scatter"),
     ("bk_partition_kernel", "bucket_partition"),
-    ("bk_columns", "bucket_columns"), ("seg_sort_kernel", "seg_sort"), ("seg_huge_kernel", "seg_huge"),
+    ("bk_columns", "bucket_columns"), ("seg_sort_kernel", "seg_sort"),
     ("expand_owner_kernel", "expand"), ("expand_kernel", "expand"), ("identify_ranges", "tile_ranges"),
     ("tile_order_kernel", "tile_order"), ("sh_backward_views", "sh_views"),
 ]
