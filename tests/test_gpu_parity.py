@@ -1071,7 +1071,10 @@ def test_threshold_guard_band(gpu_device, case):
         _native.set_tuning("guard", 0)
     parity.record(_case(), "guard_band", rec)
     assert rec["guard1"]["n_contrib_mismatch_pixels"] <= rec["guard0"]["n_contrib_mismatch_pixels"], rec
-    assert rec["guard1"]["color_maxabs"] <= max(2 * rec["guard0"]["color_maxabs"], 1e-5), rec
+    # with the guard, SURVEY A13's tolerances hold over ALL pixels and Gaussians (no flip-candidate exclusion):
+    # colour <= 1e-4 (achieved <= 3.8e-5, the remaining transmittance flips), every gradient rel-L2 <= 1e-5
+    # (achieved <= 1.4e-6; unguarded up to 4.9e-4)
+    assert rec["guard1"]["color_maxabs"] <= 1e-4, rec
     for k in GRADS:
         if f"grad_rel_l2_{k}" in rec["guard1"]:
-            assert rec["guard1"][f"grad_rel_l2_{k}"] <= max(2 * rec["guard0"][f"grad_rel_l2_{k}"], 1e-5), rec
+            assert rec["guard1"][f"grad_rel_l2_{k}"] <= 1e-5, rec
