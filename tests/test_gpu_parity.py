@@ -1033,7 +1033,7 @@ def test_big_rect_walk_blocks_are_bitwise_the_range_blocks(gpu_device, W, H, n, 
         assert np.array_equal(ref["grads"][key], alt["grads"][key]), key
 
 
-@pytest.mark.parametrize("case", ["cfg1_golden", "cfg3_full", "cfg5_full"])
+@pytest.mark.parametrize("case", ["cfg1_golden", "big_stress", "cfg3_full", "cfg5_full"])
 def test_threshold_guard_band(gpu_device, case):
     """Knob "guard" (off by default): pairs whose alpha lies within 2e-5 (relative) of 1/255, or whose
     T (1 - alpha) within 1e-4 of 1e-4, take their decisions from the oracle's own arithmetic (uncontracted exponent,
@@ -1045,6 +1045,9 @@ def test_threshold_guard_band(gpu_device, case):
         z = load_golden("cfg1_10k_256_sh0")
         inp = golden_inputs(z)
         dc, di = z["dL_dcolor"], z["dL_dinvdepth"]
+    elif case == "big_stress":  # test_big_gaussians_and_partial_tiles' scene (unguarded: 1.6e-4)
+        inp = scene_inputs(20_000, 517, 301, sh_degree=3, seed=5, stress_fraction=0.01)
+        dc, di = upstream(517, 301, 5)
     elif case == "cfg3_full":
         inp = scene_inputs(1_000_000, 1920, 1080, sh_degree=3, seed=0)
         dc, di = upstream(1920, 1080, 0)
