@@ -371,19 +371,24 @@ __device__ __forceinline__ void get_rect(float2 p, int radius, int gx, int gy, i
 
 // Exact tile culling.  A (Gaussian, tile) instance is dropped only when NO pixel centre of the tile can
 // pass the compositing test `o * exp(power) >= 1/255` as the kernels evaluate it in fp32, so every output
-// and gradient is bitwise unchanged (the skipped instances would all hit `alpha < 1/255`).  q_min is the
-// exact minimum of the conic quadratic form over the tile's pixel rectangle (double precision); the fp32
-// evaluation of q at any pixel is within eps*q of the exact value, eps = 1e-5 (|a|+|b|+|c|) / lambda_min
-// (>= 25x the worst-case rounding of the prescaled 5-op power2 expression), and v_exp_f32 is within 1e-5
-// relative.
+// and gradient is bitwise unchanged (the skipped instances would all hit `alpha < 1/255`).  The per-Gaussian
+// threshold on q (cull_setup, double) allows for the fp32 evaluation of q at any pixel being within eps*q of the
+// exact value, eps = 1e-5 (|a|+|b|+|c|) / lambda_min (>= 25x the worst-case rounding of the prescaled 5-op power2
+// expression), and v_exp_f32 within 1e-5 relative.  The per-tile minimum of q over the tile's pixel rectangle is then
+// evaluated in fp32 (round 5; it was double, whose dependent chains left the preprocess's waves issue-stalled).  Two
+// allowances raise the threshold before it is rounded up to fp32: the rounding of q itself, at most
+// 8 u (|a| dx^2 + 2|b dx dy| + |c| dy^2) <= 8 u R q with R = (|a|+|b|+|c|)/lambda_min (factor 1 + 1e-6 R), and the
+// rounding of each edge's minimiser, off by d <= 4 u (|coordinate| + tight-rect half-width + 16 + |b/c| (...)) pixels,
+// which overestimates the edge minimum by at most c d^2 (vertical edges) or a d^2 (horizontal ones), added absolutely.
 constexpr int CULL_MAX_AREA = 64;
 struct CullGauss {
-    double x, y, a, b, c, inv_a, inv_c, thr;
-    int mode;  // 0: test each tile, 1: keep every tile, 2: drop every tile
+    float x, y, a, b2, c, ba, bc, thr;  // b2 = 2 b, ba = b / a, bc = b / c, thr: fp32 threshold on q_min (rounded up)
+    int mode;                           // 0: test each tile, 1: keep every tile, 2: drop every tile
+    double ex, ey;                      // half-widths of the ellipse q <= thr's bounding box (cull_rect)
 };
 // Per-Gaussian part of the test (once per Gaussian): the error-adjusted threshold on q_min.
 __host__ __device__ inline CullGauss cull_setup(double x, double y, double a, double b, double c, double o) {
-    CullGauss g{x, y, a, b, c, 0.0, 0.0, 0.0, 0};
+    CullGauss g{(float)x, (float)y, (float)a, (float)(2.0 * b), (float)c, 0.f, 0.f, 0.f, 0, 0.0, 0.0};
     if (!(o * 255.0 * (1.0 + 1e-5) >= 1.0)) {  // o*G <= o < 1/255 everywhere
         g.mode = 2;
         return g;
@@ -394,38 +399,46 @@ __host__ __device__ inline CullGauss cull_setup(double x, double y, double a, do
         g.mode = 1;
         return g;
     }
-    const double eps = 1e-5 * (fabs(a) + fabs(b) + fabs(c)) / lmin;
+    const double R = (fabs(a) + fabs(b) + fabs(c)) / lmin;
+    const double eps = 1e-5 * R;
     if (eps > 0.1) {
         g.mode = 1;
         return g;
     }
-    g.inv_a = 1.0 / a;
-    g.inv_c = 1.0 / c;
     // cull iff q_min (1 - eps) - 1e-6 > 2 ln(255 o (1 + 1e-5))
-    g.thr = (2.0 * log(255.0 * o * (1.0 + 1e-5)) + 1e-6) / (1.0 - eps);
+    const double thr = (2.0 * log(255.0 * o * (1.0 + 1e-5)) + 1e-6) / (1.0 - eps);
+    const double det = a * c - b * b;  // > 0 (lambda_min > 0)
+    g.ex = sqrt(thr * c / det) * (1.0 + 1e-9) + 1e-6;
+    g.ey = sqrt(thr * a / det) * (1.0 + 1e-9) + 1e-6;
+    const double ba = b / a, bc = b / c, u4 = 4.0 * 0x1p-24;
+    const double dv = u4 * (fabs(y) + g.ey + 16.0 + fabs(bc) * (g.ex + 16.0));
+    const double dh = u4 * (fabs(x) + g.ex + 16.0 + fabs(ba) * (g.ey + 16.0));
+    g.ba = (float)ba;
+    g.bc = (float)bc;
+    g.thr = (float)((thr * (1.0 + 1e-6 * R) + c * dv * dv + a * dh * dh) * (1.0 + 1e-7));
     return g;
 }
-// Per-tile part: exact minimum of the quadratic form over the tile's pixel rectangle (4 edges).
+// Per-tile part: minimum of the quadratic form over the tile's pixel rectangle (4 edges), in fp32.
 __host__ __device__ inline bool cull_keep(const CullGauss &g, int tx, int ty, int W, int H) {
     if (g.mode == 2) return false;
     if (g.mode == 1) return true;
-    const double lx = tx * BLOCK_X, ly = ty * BLOCK_Y;
-    const double hx = fmin((double)(tx * BLOCK_X + BLOCK_X - 1), (double)(W - 1));
-    const double hy = fmin((double)(ty * BLOCK_Y + BLOCK_Y - 1), (double)(H - 1));
+    const float lx = (float)(tx * BLOCK_X), ly = (float)(ty * BLOCK_Y);
+    const float hx = (float)min(tx * BLOCK_X + BLOCK_X - 1, W - 1);
+    const float hy = (float)min(ty * BLOCK_Y + BLOCK_Y - 1, H - 1);
     if (g.x >= lx && g.x <= hx && g.y >= ly && g.y <= hy) return true;
-    double qmin = 1e300;
-    const double xs[2] = {lx, hx}, ys[2] = {ly, hy};
+    float qmin = 3.0e38f;
+    const float xs[2] = {lx, hx}, ys[2] = {ly, hy};
     for (int e = 0; e < 2; e++) {  // vertical edges x = X: minimise over y
-        const double dx = g.x - xs[e];
-        const double py = fmin(fmax(g.y + g.b * dx * g.inv_c, ly), hy);
-        const double dy = g.y - py;
-        qmin = fmin(qmin, g.a * dx * dx + 2.0 * g.b * dx * dy + g.c * dy * dy);
+        const float dx = g.x - xs[e];
+        const float py = fminf(fmaxf(g.y + g.bc * dx, ly), hy);
+        const float dy = g.y - py;
+        qmin = fminf(qmin, g.a * dx * dx + g.b2 * dx * dy + g.c * dy * dy);
     }
     for (int e = 0; e < 2; e++) {  // horizontal edges y = Y: minimise over x
-        const double dy = g.y - ys[e];
-        const double px = fmin(fmax(g.x + g.b * dy * g.inv_a, lx), hx);
-        const double dx = g.x - px;
-        qmin = fmin(qmin, g.a * dx * dx + 2.0 * g.b * dx * dy + g.c * dy * dy);
+        const float dy = g.y - ys[e];
+        const float px = fminf(fmaxf(g.x + g.ba * dy, lx), hx);
+        const float dx = g.x - px;
+        qmin = fminf(qmin, g.a * dx * dx + g.b2 * dx * dy + g.c * dy * dy);
     }
     return !(qmin > g.thr);
 }
@@ -442,9 +455,7 @@ __host__ __device__ inline void cull_rect(const CullGauss &g, int &x0, int &y0, 
         return;
     }
     if (g.mode == 1) return;
-    const double det = g.a * g.c - g.b * g.b;  // > 0 (lambda_min > 0)
-    const double ex = sqrt(g.thr * g.c / det) * (1.0 + 1e-9) + 1e-6;
-    const double ey = sqrt(g.thr * g.a / det) * (1.0 + 1e-9) + 1e-6;
+    const double ex = g.ex, ey = g.ey;
     const int tx0 = (int)floor((g.x - ex) / BLOCK_X), tx1 = (int)floor((g.x + ex) / BLOCK_X) + 1;
     const int ty0 = (int)floor((g.y - ey) / BLOCK_Y), ty1 = (int)floor((g.y + ey) / BLOCK_Y) + 1;
     x0 = x0 > tx0 ? x0 : tx0;
