@@ -484,6 +484,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     const bool rb_spin = tuning("rb_spin", 1) != 0 && !dbg;
     const uint32_t seq = next_readback_seq(device_guard.dev);
     pp.host_words = rb_spin ? hw : nullptr;
+    pp.stamps = tuning("stamp", 0) ? stamp_buffer(3) : nullptr;
     pp.seq = seq;
     InflightReadback inflight;  // armed before the launch: an error reported after it still waits for the kernel
     inflight.s = stream;

@@ -380,7 +380,7 @@ __device__ __forceinline__ void get_rect(float2 p, int radius, int gx, int gy, i
 // 8 u (|a| dx^2 + 2|b dx dy| + |c| dy^2) <= 8 u R q with R = (|a|+|b|+|c|)/lambda_min (factor 1 + 1e-6 R), and the
 // rounding of each edge's minimiser, off by d <= 4 u (|coordinate| + tight-rect half-width + 16 + |b/c| (...)) pixels,
 // which overestimates the edge minimum by at most c d^2 (vertical edges) or a d^2 (horizontal ones), added absolutely.
-constexpr int CULL_MAX_AREA = 64;
+constexpr int CULL_MAX_AREA = 64;  // <= 64: the preprocess keeps the kept tiles in a 64-bit mask (and divides by rw with a multiply)
 struct CullGauss {
     float x, y, a, b2, c, ba, bc, thr;  // b2 = 2 b, ba = b / a, bc = b / c, thr: fp32 threshold on q_min (rounded up)
     int mode;                           // 0: test each tile, 1: keep every tile, 2: drop every tile
@@ -418,29 +418,28 @@ __host__ __device__ inline CullGauss cull_setup(double x, double y, double a, do
     g.thr = (float)((thr * (1.0 + 1e-6 * R) + c * dv * dv + a * dh * dh) * (1.0 + 1e-7));
     return g;
 }
-// Per-tile part: minimum of the quadratic form over the tile's pixel rectangle (4 edges), in fp32.
+// Per-tile part: minimum of the quadratic form over the tile's pixel rectangle, in fp32.  The minimum of the convex q
+// over a rectangle that does not hold the centre lies on an edge facing the centre: on the interior of an edge the
+// gradient is normal to it, pointing out of the rectangle, and the line of conditional minima through that point runs
+// to the centre, which therefore lies beyond that edge.  So at most one vertical edge (the one facing the centre, when
+// x is outside [lx, hx]) and one horizontal edge are evaluated, each at its clamped stationary point; a corner minimum
+// is the clamp of both.
 __host__ __device__ inline bool cull_keep(const CullGauss &g, int tx, int ty, int W, int H) {
-    if (g.mode == 2) return false;
-    if (g.mode == 1) return true;
     const float lx = (float)(tx * BLOCK_X), ly = (float)(ty * BLOCK_Y);
     const float hx = (float)min(tx * BLOCK_X + BLOCK_X - 1, W - 1);
     const float hy = (float)min(ty * BLOCK_Y + BLOCK_Y - 1, H - 1);
-    if (g.x >= lx && g.x <= hx && g.y >= ly && g.y <= hy) return true;
-    float qmin = 3.0e38f;
-    const float xs[2] = {lx, hx}, ys[2] = {ly, hy};
-    for (int e = 0; e < 2; e++) {  // vertical edges x = X: minimise over y
-        const float dx = g.x - xs[e];
-        const float py = fminf(fmaxf(g.y + g.bc * dx, ly), hy);
-        const float dy = g.y - py;
-        qmin = fminf(qmin, g.a * dx * dx + g.b2 * dx * dy + g.c * dy * dy);
-    }
-    for (int e = 0; e < 2; e++) {  // horizontal edges y = Y: minimise over x
-        const float dy = g.y - ys[e];
-        const float px = fminf(fmaxf(g.x + g.ba * dy, lx), hx);
-        const float dx = g.x - px;
-        qmin = fminf(qmin, g.a * dx * dx + g.b2 * dx * dy + g.c * dy * dy);
-    }
-    return !(qmin > g.thr);
+    const bool in_x = g.x >= lx && g.x <= hx, in_y = g.y >= ly && g.y <= hy;
+    // both edges are evaluated unconditionally and the one not facing the centre is replaced afterwards (branch-free:
+    // the lanes of a wave test different tiles)
+    float dx = g.x - (g.x < lx ? lx : hx);  // the vertical edge x = X facing the centre: minimise over y
+    float dy = g.y - fminf(fmaxf(g.y + g.bc * dx, ly), hy);
+    const float qv = g.a * dx * dx + g.b2 * dx * dy + g.c * dy * dy;
+    dy = g.y - (g.y < ly ? ly : hy);  // the horizontal edge y = Y facing the centre: minimise over x
+    dx = g.x - fminf(fmaxf(g.x + g.ba * dy, lx), hx);
+    const float qh = g.a * dx * dx + g.b2 * dx * dy + g.c * dy * dy;
+    const float qmin = fminf(in_x ? 3.0e38f : qv, in_y ? 3.0e38f : qh);
+    // mode 1 keeps and mode 2 drops every tile (their conic fields are not set up)
+    return g.mode == 1 || (g.mode == 0 && ((in_x && in_y) || !(qmin > g.thr)));
 }
 
 // Tight rect: the tiles of [x0, x1) x [y0, y1) (the reference rect on entry) that meet the bounding box of the ellipse

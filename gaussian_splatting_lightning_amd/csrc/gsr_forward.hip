@@ -229,12 +229,18 @@ void preprocess_kernel(PreprocessParams p) {
     CullIn ci;
     ci.need = false;
     ci.vis = false;
+    const uint32_t t_start = p.stamps ? stamp_now() : 0u;
     const uint32_t area = i < p.P ? preprocess_gaussian<SPLIT, SHD>(p, i, ci) : 0u;
+    const uint32_t t_proj = p.stamps ? stamp_now() : 0u;
     const uint32_t need_area = ci.need ? area : 0u;
     const uint32_t incl = wave_inclusive_scan(need_area, lane);
     const uint32_t total = __shfl((int)incl, 63);
     if (ci.need) L.cg[lane] = ci.cg;
-    L.rect[lane] = make_int4(ci.rx, ci.ry, ci.rw, (int)(incl - need_area));
+    // rw <= CULL_MAX_AREA and a pair's offset t < CULL_MAX_AREA = 64, so t / rw == (t * ceil(4096 / rw)) >> 12 exactly
+    // (the rounding up adds t * (ceil - 4096 / rw) / 4096 < 64 / 4096 = 1/64 to a quotient whose fraction is at most
+    // 63/64): two integer multiplies instead of the ~20-instruction unsigned division in the loop
+    L.rect[lane] = make_int4(ci.rx, ci.ry, ci.rw | (ci.need ? (int)((4096u + ci.rw - 1) / ci.rw) << 16 : 0),
+                             (int)(incl - need_area));
     L.mask[lane] = 0ull;
     // pair owners by marks and a max-scan (as the bucket walk): the lane whose pair run starts inside the step
     // marks its start, and every pair takes the largest marking lane at or before it (or the previous step's last
@@ -255,11 +261,13 @@ void preprocess_kernel(PreprocessParams p) {
         if (marks) L.own[my_start - B] = -1;
         if (j >= total) continue;
         const int4 r = L.rect[o];
-        const uint32_t t = j - (uint32_t)r.w;
-        const int tx = r.x + (int)(t % (uint32_t)r.z), ty = r.y + (int)(t / (uint32_t)r.z);
+        const uint32_t t = j - (uint32_t)r.w, rw = (uint32_t)r.z & 0xffffu;
+        const uint32_t qy = (t * ((uint32_t)r.z >> 16)) >> 12;
+        const int tx = r.x + (int)(t - qy * rw), ty = r.y + (int)qy;
         if (cull_keep(L.cg[o], tx, ty, p.W, p.H)) atomicOr(&L.mask[o], 1ull << t);
     }
     wave_lds_sync();
+    const uint32_t t_cull = p.stamps ? stamp_now() : 0u;
     uint32_t kept = area;
     if (i < p.P && area > 0) {
         const GeomState &g = p.g;
@@ -322,6 +330,12 @@ void preprocess_kernel(PreprocessParams p) {
     if (p.host_words) {
         __syncthreads();
         if (s_last && threadIdx.x < 64) publish_total(p);
+    }
+    if (p.stamps && lane == 0 && (int)(bid * 4 + w) < STAMP_SLOTS / 2) {
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+        p.stamps[2 * (bid * 4 + w)] = make_uint4(t_start, t_proj, t_cull, stamp_now());
+        p.stamps[2 * (bid * 4 + w) + 1] = make_uint4(hw, xcc, 0u, 0u);
     }
     if constexpr (MODE == PRE_LATE_DIRECT) {
         if (ci.vis) {

@@ -66,6 +66,7 @@ struct PreprocessParams {
     int split = 0;  // colour left to launch_preprocess_color (SH colours only)
     int late = 0;   // colour evaluated at the end of the preprocess from LDS-staged coefficient rows (M = 16, 16-B aligned)
     int depth_range = 0;  // publish the kept depth keys' range with the instance total (relative depth sort)
+    uint4 *stamps = nullptr;  // diagnostics ("stamp" knob): per wave {start, projected, culled, end}, {HW_ID, XCC_ID}
 };
 void launch_preprocess(hipStream_t s, const PreprocessParams &p);
 void launch_preprocess_color(hipStream_t s, const PreprocessParams &p);  // the colour half of a split preprocess
