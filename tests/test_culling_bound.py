@@ -55,3 +55,13 @@ def test_culling_drops_only_invisible_instances(n, W, H, seed, stress):
     best = max_alpha(g, pairs, W, H)
     print("dropped", len(pairs), "of", n_full, "max alpha x 255 =", float(best.max()) * 255)
     assert best.max() < 1.0 / 255.0, (best.max(), pairs[int(best.argmax())])
+
+
+def test_pair_loop_division_by_multiply():
+    """preprocess_kernel's culling loop divides a pair's offset t < 64 by the rect width rw <= 64 as
+    (t * ceil(4096 / rw)) >> 12 (gsr_forward.hip): exact over the whole domain."""
+    for rw in range(1, 65):
+        magic = (4096 + rw - 1) // rw
+        assert magic < 1 << 16  # packed beside rw in one 32-bit LDS word
+        for t in range(64):
+            assert (t * magic) >> 12 == t // rw, (t, rw)
