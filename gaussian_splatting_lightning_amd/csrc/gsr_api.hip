@@ -455,7 +455,8 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     // next array starts there) so the memset is one aligned fill kernel, not an aligned fill plus a tail
     const size_t clear_bytes = align_up((size_t)(reinterpret_cast<char *>(g.tile_status + BK_MAX_TILES / 64 + 1) -
                                                  reinterpret_cast<char *>(g.counters)), 256);
-    GSR_HIP(hipMemsetAsync(g.counters, 0, clear_bytes, stream));
+    if (tuning("zero_kernel", 1)) launch_zero16(stream, g.counters, clear_bytes);
+    else GSR_HIP(hipMemsetAsync(g.counters, 0, clear_bytes, stream));
 
     PreprocessParams pp;
     pp.P = P; pp.D = a->D; pp.M = a->M; pp.W = W; pp.H = H; pp.gx = gx; pp.gy = gy;

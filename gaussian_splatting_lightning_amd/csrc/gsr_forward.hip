@@ -448,6 +448,17 @@ void launch_preprocess_color(hipStream_t s, const PreprocessParams &p) {
     }
 }
 
+// Zero fill of the forward's counter block (16-B aligned, a multiple of 16 B) by a plain kernel: the runtime's fill
+// (hipMemsetAsync) ran 4.4 us at cfg 3 and the trace showed a ~6-us gap in front of it every step.
+__global__ __launch_bounds__(256) void zero16_kernel(uint4 *__restrict__ p, uint32_t n16) {
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256) p[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+void launch_zero16(hipStream_t s, void *p, size_t bytes) {
+    const uint32_t n16 = (uint32_t)(bytes / 16);
+    if (n16 == 0) return;
+    zero16_kernel<<<std::min(div_up(n16, 256u), 256u), 256, 0, s>>>(reinterpret_cast<uint4 *>(p), n16);
+}
+
 // ------------------------------------------------------------------------------------------------
 // expand: instances are laid out in depth-rank order (Gaussian order[r] owns [inst_off[r], inst_off[r+1])).
 // Each block owns a fixed slice of EXP_TILE instances (load balanced whatever the per-Gaussian tile

@@ -69,6 +69,7 @@ struct PreprocessParams {
     uint4 *stamps = nullptr;  // diagnostics ("stamp" knob): per wave {start, projected, culled, end}, {HW_ID, XCC_ID}
 };
 void launch_preprocess(hipStream_t s, const PreprocessParams &p);
+void launch_zero16(hipStream_t s, void *p, size_t bytes);  // bytes: a multiple of 16, p 16-B aligned
 void launch_preprocess_color(hipStream_t s, const PreprocessParams &p);  // the colour half of a split preprocess
 
 struct ExpandParams {
