@@ -135,9 +135,10 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
     const int kbase = w * NP;
     const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
     const size_t HW = (size_t)p.W * p.H;
-    float T[NP], dp0[NP], dp1[NP], dp2[NP], dinv[NP], D[NP];
+    float T[NP], dp0[NP], dp1[NP], dp2[NP], dinv[NP], D[NP], prow[NP];
     uint32_t lastc[NP];
-    const float pfy0 = (float)py0;
+#pragma unroll
+    for (int k = 0; k < NP; k++) prow[k] = (float)(py0 + 4 * (kbase + k));  // pixel rows (dy = y - row, as the forward)
 #pragma unroll
     for (int k = 0; k < NP; k++) {
         const int py = py0 + 4 * (kbase + k);
@@ -178,14 +179,14 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
             const uint32_t idx = (uint32_t)(bend - 1 - j);
             const float4 a = s_a[j], b = s_b[j];  // a: x, y, A, B; b: C, o, r, g
             const float2 c = s_c[j];              // b, 1/depth
-            const float dx = a.x - pfx, dy0 = a.y - pfy0;
+            const float dx = a.x - pfx;
             const float P0 = (a.z * dx) * dx, L = a.w * dx;
             float Q0 = 0.f, Q1 = 0.f, Q2 = 0.f, w0 = 0.f, w1 = 0.f, w2 = 0.f, w3 = 0.f;
             bool any = false;
 #pragma unroll
             for (int k = 0; k < NP; k++) {
                 if (!((sk[k] >> j) & 1u)) continue;  // wave-uniform
-                const float dy = dy0 - (float)(4 * (kbase + k));
+                const float dy = a.y - prow[k];
                 const float power2 = power2_at(b.x, dy, P0, L);
                 const float G = __builtin_amdgcn_exp2f(power2);
                 const float alpha = fminf(0.99f, b.y * G);
@@ -332,7 +333,7 @@ __global__ __launch_bounds__(64, GUARD ? 4 : SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MI
     const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
     const size_t HW = (size_t)p.W * p.H;
     float T[PIX_PER_LANE], dp0[PIX_PER_LANE], dp1[PIX_PER_LANE], dp2[PIX_PER_LANE], dinv[PIX_PER_LANE];
-    float D[PIX_PER_LANE];
+    float D[PIX_PER_LANE], prow[PIX_PER_LANE];
     uint32_t lastc[PIX_PER_LANE], smax[PIX_PER_LANE], smin[PIX_PER_LANE];
 #pragma unroll
     for (int k = 0; k < PIX_PER_LANE; k++) {
@@ -346,6 +347,7 @@ __global__ __launch_bounds__(64, GUARD ? 4 : SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MI
         dp2[k] = inside ? p.dL_dpix[2 * HW + pid] : 0.f;
         dinv[k] = (HAS_INV && inside) ? p.dL_dinvdepth[pid] : 0.f;
         D[k] = fmaf(bg2, dp2[k], fmaf(bg1, dp1[k], bg0 * dp0[k]));
+        prow[k] = (float)py;  // dy = y - pixel row in one subtraction, as the forward
         if (LASTC) {
             smax[k] = __builtin_amdgcn_readfirstlane(wave_max_u32(lastc[k]));
             smin[k] = __builtin_amdgcn_readfirstlane(wave_min_u32(lastc[k]));
@@ -410,14 +412,14 @@ __global__ __launch_bounds__(64, GUARD ? 4 : SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MI
             const FwdRec &r = s_rec[j];
             const float4 a = r.a, b = r.b;  // a: x, y, A, B; b: C, o, r, g
             const float2 c = r.c;           // b, 1/depth
-            const float dx = a.x - pfx, dy0 = a.y - pfy0;
+            const float dx = a.x - pfx;
             const float P0 = (a.z * dx) * dx, L = a.w * dx;
             float Q0 = 0.f, Q1 = 0.f, Q2 = 0.f, w0 = 0.f, w1 = 0.f, w2 = 0.f, w3 = 0.f;
             uint64_t any = 0;
 #pragma unroll
             for (int k = 0; k < PIX_PER_LANE; k++) {
                 if (!((sk[k] >> j) & 1u)) continue;  // wave-uniform
-                const float dy = dy0 - (float)(4 * k);
+                const float dy = a.y - prow[k];
                 const float power2 = power2_at(b.x, dy, P0, L);
                 const float G = __builtin_amdgcn_exp2f(power2);
                 const float alpha = fminf(0.99f, b.y * G);

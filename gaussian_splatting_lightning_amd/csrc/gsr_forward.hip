@@ -795,7 +795,7 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
     for (int k = 0; k < NPIX; k++) {
         const int py = py0 + 4 * (kbase + k);
         const bool inside = px < p.W && py < p.H;
-        off[k] = inside ? (float)(4 * (kbase + k)) : __builtin_nanf("");
+        off[k] = inside ? (float)py : __builtin_nanf("");  // the pixel's row (exact); NaN retires the pixel
         livek[k] = __ballot(inside);
         T[k] = 1.0f;
         C0[k] = C1[k] = C2[k] = ID[k] = 0.f;
@@ -857,12 +857,13 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
             const float4 a = sr[j].a, b = sr[j].b;
             const float2 c = sr[j].c;
             contributor = cbase + j + 1;
-            const float dx = a.x - pfx, dy0 = a.y - pfy0;
+            const float dx = a.x - pfx;
             const float P0 = (a.z * dx) * dx, L = a.w * dx;
 #pragma unroll
             for (int k = 0; k < NPIX; k++) {
                 if (!(sk[k] & bit)) continue;  // wave-uniform
-                const float power2 = power2_at(b.x, dy0 - off[k], P0, L);
+                // dy = y - pixel row in one subtraction (the reference's own form): no per-instance row offset
+                const float power2 = power2_at(b.x, a.y - off[k], P0, L);
                 const float alpha = fminf(0.99f, b.y * __builtin_amdgcn_exp2f(power2));
                 const float test_T = T[k] * (1 - alpha);
                 // lane masks straight from the compares (scalar registers): ok = power2 <= 0 (ordered, so false
