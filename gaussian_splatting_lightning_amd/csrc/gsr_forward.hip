@@ -941,9 +941,14 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
     const float bg0 = p.bg[0], bg1 = p.bg[1], bg2 = p.bg[2];
     const size_t HW = (size_t)p.W * p.H;
     uint32_t mx = 0;
+    // the pixel column and row re-derived from the lane id (mbcnt, not threadIdx, so the compiler does not keep the
+    // integer column live across the walk just to reuse it here: it re-materialised the float column from it instead,
+    // one conversion per instance)
+    const int lid = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    const int pxe = tx * BLOCK_X + (lid & 15), py0e = ty * BLOCK_Y + (lid >> 4);
 #pragma unroll
     for (int k = 0; k < NPIX; k++) {
-        const int py = py0 + 4 * (kbase + k);
+        const int py = py0e + 4 * (kbase + k), px = pxe;
         if (px < p.W && py < p.H) {
             const size_t pid = (size_t)py * p.W + px;
             const float Tk = T[k];
