@@ -453,7 +453,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     carve_image(img, W, H, im);
     // counters + instance-scan and tile-scan look-back words; rounded up to the carver's 256-B alignment (the
     // next array starts there) so the memset is one aligned fill kernel, not an aligned fill plus a tail
-    const size_t clear_bytes = align_up((size_t)(reinterpret_cast<char *>(g.tile_status + BK_MAX_TILES / 64 + 1) -
+    const size_t clear_bytes = align_up((size_t)(reinterpret_cast<char *>(g.tile_status + BK_MAX_TILES / 32 + 1) -
                                                  reinterpret_cast<char *>(g.counters)), 256);
     if (tuning("zero_kernel", 1)) launch_zero16(stream, g.counters, clear_bytes);
     else GSR_HIP(hipMemsetAsync(g.counters, 0, clear_bytes, stream));

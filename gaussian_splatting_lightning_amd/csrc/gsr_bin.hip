@@ -262,8 +262,12 @@ __device__ __forceinline__ uint32_t bk_row_block(uint32_t r, uint32_t nb, int xc
     return k * 8 + x;
 }
 
-template <int CW>
+// TW tiles per workgroup (64: one lane per tile; 32: the two lane halves of a wave split the wave's rows, so twice the
+// workgroups (255 at 1080p instead of 128, i.e. every CU) walk half as long a dependent load chain each).
+template <int CW, int TW = 64>
 __global__ __launch_bounds__(64 * CW) void bk_columns_kernel(BucketParams p) {
+    static_assert(TW == 64 || TW == 32, "tiles per workgroup");
+    constexpr int NH = 64 / TW;  // row halves per wave
     __shared__ uint32_t s_sum[CW][64];
     __shared__ uint32_t s_bid;
     __shared__ unsigned long long s_excl;
@@ -271,12 +275,14 @@ __global__ __launch_bounds__(64 * CW) void bk_columns_kernel(BucketParams p) {
     uint32_t *__restrict__ hist_pre = p.hist_pre;
     const uint32_t nb = bk_walk_blocks(p), T = p.T;  // the count rows the walk wrote
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int sub = lane % TW, h = lane / TW;  // the lane's tile in the workgroup, its half of the wave's rows
     if (tid == 0) s_bid = atomicAdd(p.ticket, 1u);
     if (blockIdx.x == 0 && tid < 256 && p.lpt_bcnt) p.lpt_bcnt[tid] = 0u;
     __syncthreads();
     const uint32_t bid = s_bid;
-    const uint32_t t = bid * 64 + lane;
-    const uint32_t q = (nb + CW - 1) / CW, r0 = min(nb, w * q), r1 = min(nb, r0 + q);
+    const uint32_t t = bid * TW + sub;
+    const uint32_t q = (nb + CW - 1) / CW, r0w = min(nb, w * q), r1w = min(nb, r0w + q);
+    const uint32_t qh = (q + NH - 1) / NH, r0 = min(r1w, r0w + h * qh), r1 = min(r1w, r0 + qh);
     uint32_t sum = 0;
     const int xm = p.xcd_major;
     if (t < T) {
@@ -290,24 +296,32 @@ __global__ __launch_bounds__(64 * CW) void bk_columns_kernel(BucketParams p) {
         }
         for (; r < r1; r++) sum += hist[(size_t)bk_row_block(r, nb, xm) * T + t];
     }
-    s_sum[w][lane] = sum;
+    uint32_t lowsum = 0;  // the wave's rows before this lane's half (the other half's sum, for the upper half)
+    if constexpr (NH == 2) {
+        const uint32_t other = (uint32_t)__shfl_xor((int)sum, 32);
+        lowsum = h ? other : 0u;
+        sum += other;  // both halves: the wave's column sum
+    }
+    if (h == 0) s_sum[w][sub] = sum;
     __syncthreads();
     uint32_t tot = 0;  // tile total
 #pragma unroll
-    for (int i = 0; i < CW; i++) tot += s_sum[i][lane];
+    for (int i = 0; i < CW; i++) tot += s_sum[i][sub];
     if (w == 0) {
-        const uint32_t inc = wave_inclusive_scan(tot, lane);
-        // fallback aggregate of column workgroup q: its 64 tiles' totals, summed from the (read-only) counts
-        auto agg_of = [&](uint32_t q) -> uint64_t {
-            const uint32_t tq = q * 64 + lane;
+        const uint32_t tv = h == 0 ? tot : 0u;  // lanes of the upper half repeat the tiles: they count nothing here
+        const uint32_t inc = wave_inclusive_scan(tv, lane);
+        // fallback aggregate of column workgroup q: its TW tiles' totals, summed from the (read-only) counts
+        auto agg_of = [&](uint32_t qq) -> uint64_t {
+            const uint32_t tq = qq * TW + sub;
             uint64_t v = 0;
-            if (tq < T)
+            if (tq < T && h == 0)
                 for (uint32_t r = 0; r < nb; r++) v += hist[(size_t)r * T + tq];
             return wave_sum_u64(v);
         };
         const uint64_t excl = wave_lookback(p.tile_status, bid, (uint64_t)__builtin_amdgcn_readlane((int)inc, 63),
                                             lane, p.err, p.lb_patience, p.lb_force != 0, agg_of);
-        if (t < T) {
+        const bool mine = t < T && h == 0;
+        if (mine) {
             const uint32_t st = (uint32_t)(excl + inc - tot);
             p.tile_start[t] = st;
             p.ranges[t] = tot ? make_uint2(st, st + tot) : make_uint2(0, 0);  // empty: (0, 0), as the reference
@@ -320,7 +334,7 @@ __global__ __launch_bounds__(64 * CW) void bk_columns_kernel(BucketParams p) {
                 p.reg_start[(T + BK_REGION - 1) / BK_REGION] = st + tot;
             }
         }
-        const bool l0 = t < T && tot > SEG_CAP && tot <= SEG_BLOCK_CAP, l1 = t < T && tot > SEG_BLOCK_CAP;
+        const bool l0 = mine && tot > SEG_CAP && tot <= SEG_BLOCK_CAP, l1 = mine && tot > SEG_BLOCK_CAP;
         const uint64_t m0 = __ballot(l0), m1 = __ballot(l1);
         uint32_t b0 = 0, b1 = 0;
         if (lane == 0) {
@@ -333,8 +347,8 @@ __global__ __launch_bounds__(64 * CW) void bk_columns_kernel(BucketParams p) {
         if (l0) p.long_list[b0 + __popcll(m0 & lt)] = t;
         if (l1) p.long_list[(T + 1) + b1 + __popcll(m1 & lt)] = t;
     }
-    uint32_t run = 0;
-    for (int i = 0; i < w; i++) run += s_sum[i][lane];
+    uint32_t run = lowsum;
+    for (int i = 0; i < w; i++) run += s_sum[i][sub];
     if (t < T) {
         uint32_t r = r0;
         for (; r + 8 <= r1; r += 8) {
@@ -909,7 +923,9 @@ static void launch_walk(hipStream_t s, const BucketParams &p, uint32_t grid) {
 
 void launch_bucket_count(hipStream_t s, const BucketParams &p) {
     launch_walk<false>(s, p, p.nb);
-    if (tuning("bk_colw", 16) >= 16) bk_columns_kernel<16><<<div_up(p.T, 64), 1024, 0, s>>>(p);
+    // "bk_colt" 32 (default): 32 tiles per column workgroup, the lane halves splitting the rows; 64: one lane per tile
+    if (tuning("bk_colw", 16) >= 16 && tuning("bk_colt", 32) == 32) bk_columns_kernel<16, 32><<<div_up(p.T, 32), 1024, 0, s>>>(p);
+    else if (tuning("bk_colw", 16) >= 16) bk_columns_kernel<16><<<div_up(p.T, 64), 1024, 0, s>>>(p);
     else bk_columns_kernel<4><<<div_up(p.T, 64), 256, 0, s>>>(p);
 }
 

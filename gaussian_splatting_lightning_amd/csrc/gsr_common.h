@@ -141,7 +141,7 @@ inline size_t carve_geom(char *base, int P, GeomState &g) {
     uint32_t n = (uint32_t)P;
     g.counters = c.take<uint32_t>(CNT_WORDS);
     g.scan_status = c.take<uint64_t>(div_up(n + 1, SCAN_TILE) + 1);  // cleared together with the counters
-    g.tile_status = c.take<uint64_t>(BK_MAX_TILES / 64 + 1);         // cleared together with the counters
+    g.tile_status = c.take<uint64_t>(BK_MAX_TILES / 32 + 1);         // cleared together with the counters (32-tile column groups)
     g.rec = c.take<GRec>(n);
     g.tiles = c.take<uint32_t>(n);
     g.clamped = c.take<uint8_t>(n);

@@ -109,7 +109,7 @@ struct BucketParams {
     uint32_t *long_list;   // 2 x (T + 1): tiles of (SEG_CAP, SEG_BLOCK_CAP] instances, longer tiles
     uint32_t *long_cnt;    // 2 counts (zeroed)
     uint32_t *ticket;      // zeroed: column-pass workgroup ticket
-    uint64_t *tile_status; // zeroed: div_up(T, 64) look-back words of the column pass
+    uint64_t *tile_status; // zeroed: div_up(T, 32) look-back words of the column pass
     uint32_t *err;         // look-back flags (bit 2: a decoupled fallback ran; diagnostic)
     uint32_t lb_patience;  // look-back polls before recomputing an unpublished predecessor
     int lb_force;          // recompute every predecessor (tests the fallback)
