@@ -1015,11 +1015,11 @@ __device__ __forceinline__ void lpt_order_block(const uint2 *__restrict__ ranges
     uint32_t wt[LPT_KMAX];
     uint32_t mx = 0;
     if (cached) {
-        // every load issued before any use: unconditional (clamped index), since a load in a branch waits for its
-        // data before the next one is issued
+        // every load issued before any use, unconditional (clamped index): a load in a branch -- even a uniform one,
+        // `k * nt < T ? load : 0` per round -- was waited for at the branch's join, one round trip per round in use
+        // (rounds past T re-read the last tile: the same cache line)
 #pragma unroll
-        for (int k = 0; k < LPT_KMAX; k++)
-            wt[k] = k * nt < T ? load_w(min(tid + k * nt, T - 1)) : 0u;  // (k * nt < T: uniform, only rounds in use)
+        for (int k = 0; k < LPT_KMAX; k++) wt[k] = load_w(min(tid + k * nt, T - 1));
 #pragma unroll
         for (int k = 0; k < LPT_KMAX; k++)
             if (tid + k * nt >= T) wt[k] = 0u;
