@@ -674,10 +674,14 @@ __global__ __launch_bounds__(1024) void lpt_hist_kernel(const uint2 *__restrict_
     __syncthreads();
     constexpr int PER = LPT_WG_TILES / 1024;
     uint32_t b[PER];
+    uint32_t wq[PER];  // weights loaded unconditionally (clamped tile): a load under `t < T` waited at its join
+#pragma unroll
+    for (int q = 0; q < PER; q++)
+        wq[q] = lpt_weight(ranges, tile_last, use_last, min(blockIdx.x * LPT_WG_TILES + q * 1024 + tid, T - 1));
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int t = blockIdx.x * LPT_WG_TILES + q * 1024 + tid;
-        b[q] = t < T ? lpt_log_bucket(lpt_weight(ranges, tile_last, use_last, t)) : 0u;
+        b[q] = t < T ? lpt_log_bucket(wq[q]) : 0u;
     }
 #pragma unroll
     for (int q = 0; q < PER; q++) {
@@ -696,20 +700,37 @@ __global__ __launch_bounds__(1024) void lpt_scatter_kernel(const uint2 *__restri
     const uint64_t lt = lanemask_lt(lane);
     constexpr int PER = LPT_WG_TILES / 1024;
     uint32_t b[PER];
+    uint32_t wq[PER];  // weights loaded unconditionally (clamped tile): a load under `t < T` waited at its join
+#pragma unroll
+    for (int q = 0; q < PER; q++)
+        wq[q] = lpt_weight(ranges, tile_last, use_last, min(blockIdx.x * LPT_WG_TILES + q * 1024 + tid, T - 1));
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int t = blockIdx.x * LPT_WG_TILES + q * 1024 + tid;
-        b[q] = t < T ? lpt_log_bucket(lpt_weight(ranges, tile_last, use_last, t)) : 0u;
+        b[q] = t < T ? lpt_log_bucket(wq[q]) : 0u;
     }
     if (tid < 64) {  // bucket bases: all workgroups' earlier buckets, plus this bucket in earlier workgroups
+        // the workgroups' rows 8 at a time, one 16-B load each, all issued before any is used (a rolled loop waited
+        // for every row in turn: one round trip per workgroup)
         uint32_t tot[4] = {0, 0, 0, 0}, pre[4] = {0, 0, 0, 0};
-        for (int g = 0; g < (int)gridDim.x; g++)
+        const int G = (int)gridDim.x;
+        for (int g0 = 0; g0 < G; g0 += 8) {
+            uint4 v[8];
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint32_t v = ghist[g * 256 + 4 * tid + q];
-                tot[q] += v;
-                if (g < (int)blockIdx.x) pre[q] += v;
+            for (int i = 0; i < 8; i++)
+                v[i] = *reinterpret_cast<const uint4 *>(ghist + (size_t)min(g0 + i, G - 1) * 256 + 4 * tid);
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int g = g0 + i;
+                const uint32_t x[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t vv = g < G ? x[q] : 0u;
+                    tot[q] += vv;
+                    if (g < (int)blockIdx.x) pre[q] += vv;
+                }
             }
+        }
         const uint32_t sum = tot[0] + tot[1] + tot[2] + tot[3];
         uint32_t run = wave_inclusive_scan(sum, tid) - sum;
 #pragma unroll
