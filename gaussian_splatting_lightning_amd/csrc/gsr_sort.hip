@@ -923,7 +923,9 @@ static void launch_radix_sort_multi(hipStream_t s, SortScratch &sc, uint32_t n, 
     const uint32_t nb = div_up(n, (uint32_t)ITEMS * 256u);  // <= the RS_TILE block count carve_sort sized
     // "rs_cscan" 1 (default): the one-launch count scan (look-back counts < 2^30); 0: the three-launch column scan
     const bool one = BINS != RS_BINS || (tuning("rs_cscan", 1) != 0 && n <= RS_ONESWEEP_MAX_N);
-    constexpr uint32_t CS_C = 32;
+    // count-scan rows per workgroup: 64 for long 256-bin matrices ("rs_cs64"; the 16-bit tile sort at 16 keys per
+    // thread has ~9.6 k rows at cfg 5), else 32
+    const uint32_t CS_C = (BINS == RS_BINS && nb > 4096 && tuning("rs_cs64", 1)) ? 64u : 32u;
     const uint32_t nch = div_up(nb, CS_C);  // <= RS_MAX_PASSES * nb_os rows of sc.status per pass
     const uint32_t pat = (uint32_t)tuning("lb_patience", 1 << 16);
     const int force = tuning("lb_force", 0);
@@ -942,9 +944,14 @@ static void launch_radix_sort_multi(hipStream_t s, SortScratch &sc, uint32_t n, 
                                                                     p == 0 ? sc.ctrl + RS_CTRL_ERR : nullptr);
         const uint32_t *scanned = sc.counts, *doff = nullptr;
         if (one) {
-            rs_countscan_kernel<CS_C, BINS><<<nch, BINS, 0, s>>>(sc.counts, nb, sc.counts_pre, cs_status,
-                                                                sc.ctrl + RS_CTRL_COUNTER + p, sc.ctrl + RS_CTRL_ERR,
-                                                                pat, force);
+            if (CS_C == 64)
+                rs_countscan_kernel<64, BINS><<<nch, BINS, 0, s>>>(sc.counts, nb, sc.counts_pre, cs_status,
+                                                                  sc.ctrl + RS_CTRL_COUNTER + p, sc.ctrl + RS_CTRL_ERR,
+                                                                  pat, force);
+            else
+                rs_countscan_kernel<32, BINS><<<nch, BINS, 0, s>>>(sc.counts, nb, sc.counts_pre, cs_status,
+                                                                  sc.ctrl + RS_CTRL_COUNTER + p, sc.ctrl + RS_CTRL_ERR,
+                                                                  pat, force);
             scanned = sc.counts_pre;
             doff = sc.counts_pre + (size_t)nb * BINS;
         } else {
@@ -1019,8 +1026,10 @@ void launch_depth_sort_rel(hipStream_t s, SortScratch &sc, uint32_t n, const uin
 void launch_radix_sort16(hipStream_t s, SortScratch &sc, uint32_t n, int dbits, int passes) {
     if (n == 0) return;
     const uint16_t *k0 = reinterpret_cast<const uint16_t *>(sc.k[0]);
+    // 16 keys per thread at every size for the 16-bit tile keys (cfg 5, 39.5 M keys: 0.454 -> 0.427 ms against 32, whose
+    // scatter holds 148 VGPRs, 3 waves per SIMD; profiles/r5ax_ab_rs_items_cfg5.txt)
     int items = tuning("rs_items", 0);
-    if (items == 0) items = n <= (8u << 20) ? 16 : 32;
+    if (items == 0) items = 16;
     if (items >= 32) launch_radix_sort_multi<32, uint16_t>(s, sc, n, passes, false, k0, nullptr, dbits);
     else launch_radix_sort_multi<RS_ITEMS, uint16_t>(s, sc, n, passes, false, k0, nullptr, dbits);
 }
