@@ -682,7 +682,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             ep.inst_gid = b.inst_gid; ep.inst_start = g.inst_start; ep.inv_none = b.inv;
             GSR_STAGE(ST_EXPAND, dbg, launch_expand(stream, ep));
             if (k16)
-                GSR_STAGE(ST_TILE_SORT, dbg, launch_radix_sort16(stream, b.sort, R, plan.digit_bits, plan.passes));
+                GSR_STAGE(ST_TILE_SORT, dbg, launch_radix_sort16(stream, b.sort, R, plan.digit_bits, plan.passes, tile_key_bits(T)));
             else
                 GSR_STAGE(ST_TILE_SORT, dbg,
                           launch_radix_sort(stream, b.sort, R, tile_key_bits(T), false, nullptr, nullptr,

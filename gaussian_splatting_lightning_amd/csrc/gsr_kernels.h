@@ -46,7 +46,7 @@ void launch_depth_sort_rel(hipStream_t s, SortScratch &sc, uint32_t n, const uin
                            uint32_t kcap, int bits, const SortGather *gather);
 // The same sort on 16-bit keys in `passes` digits of digit_bits bits (multi-kernel passes): sc.k[] hold uint16_t keys,
 // values as above.  The radix binning's tile sort takes it up to 65536 tiles (tile_sort_plan).
-void launch_radix_sort16(hipStream_t s, SortScratch &sc, uint32_t n, int digit_bits, int passes);
+void launch_radix_sort16(hipStream_t s, SortScratch &sc, uint32_t n, int digit_bits, int passes, int bits);  // bits: key bits in use
 
 // ---- forward (gsr_forward.hip) ----
 struct PreprocessParams {

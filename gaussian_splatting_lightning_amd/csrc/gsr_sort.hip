@@ -917,8 +917,9 @@ static void launch_radix_sort_onesweep(hipStream_t s, SortScratch &sc, uint32_t 
 template <int ITEMS, typename KT = uint32_t, int BINS = RS_BINS>
 static void launch_radix_sort_multi(hipStream_t s, SortScratch &sc, uint32_t n, int passes, bool keyed,
                                     const KT *keys0, const SortGather *gather, int dbits = 8, uint32_t kbase = 0,
-                                    uint32_t kcap = 0, int flip = 0) {
-    const uint32_t dmask = (1u << dbits) - 1u;
+                                    uint32_t kcap = 0, int flip = 0, int dbits0 = 0) {
+    // dbits0 > 0: the first pass ranks the low dbits0 bits, the later ones dbits each above them
+    const int d0 = dbits0 > 0 ? dbits0 : dbits;
     KT *k[2] = {reinterpret_cast<KT *>(sc.k[0]), reinterpret_cast<KT *>(sc.k[1])};
     const uint32_t nb = div_up(n, (uint32_t)ITEMS * 256u);  // <= the RS_TILE block count carve_sort sized
     // "rs_cscan" 1 (default): the one-launch count scan (look-back counts < 2^30); 0: the three-launch column scan
@@ -930,7 +931,8 @@ static void launch_radix_sort_multi(hipStream_t s, SortScratch &sc, uint32_t n, 
     const uint32_t pat = (uint32_t)tuning("lb_patience", 1 << 16);
     const int force = tuning("lb_force", 0);
     for (int p = 0; p < passes; p++) {
-        const int shift = dbits * p, in = (p + flip) & 1, out = (p + 1 + flip) & 1;
+        const int shift = p == 0 ? 0 : d0 + dbits * (p - 1), in = (p + flip) & 1, out = (p + 1 + flip) & 1;
+        const uint32_t dmask = (1u << (p == 0 ? d0 : dbits)) - 1u;
         const KT *kin = p == 0 ? keys0 : k[in];
         const uint32_t cap = p == 0 ? kcap : 0u;
         uint32_t *cs_status = one ? sc.status + (size_t)p * nch * BINS : nullptr;
@@ -1023,15 +1025,18 @@ void launch_depth_sort_rel(hipStream_t s, SortScratch &sc, uint32_t n, const uin
     }
 }
 
-void launch_radix_sort16(hipStream_t s, SortScratch &sc, uint32_t n, int dbits, int passes) {
+void launch_radix_sort16(hipStream_t s, SortScratch &sc, uint32_t n, int dbits, int passes, int bits) {
     if (n == 0) return;
     const uint16_t *k0 = reinterpret_cast<const uint16_t *>(sc.k[0]);
     // 16 keys per thread at every size for the 16-bit tile keys (cfg 5, 39.5 M keys: 0.454 -> 0.427 ms against 32, whose
     // scatter holds 148 VGPRs, 3 waves per SIMD; profiles/r5ax_ab_rs_items_cfg5.txt)
     int items = tuning("rs_items", 0);
     if (items == 0) items = 16;
-    if (items >= 32) launch_radix_sort_multi<32, uint16_t>(s, sc, n, passes, false, k0, nullptr, dbits);
-    else launch_radix_sort_multi<RS_ITEMS, uint16_t>(s, sc, n, passes, false, k0, nullptr, dbits);
+    // "tile_lo_short" 1: the first pass takes the short digit (15-bit keys: 7 + 8 bits instead of 8 + 7), so its 128
+    // digit runs per block are twice as long as 256 would be
+    const int d0 = (tuning("tile_lo_short", 1) && passes >= 2 && bits < dbits * passes) ? bits - dbits * (passes - 1) : 0;
+    if (items >= 32) launch_radix_sort_multi<32, uint16_t>(s, sc, n, passes, false, k0, nullptr, dbits, 0, 0, 0, d0);
+    else launch_radix_sort_multi<RS_ITEMS, uint16_t>(s, sc, n, passes, false, k0, nullptr, dbits, 0, 0, 0, d0);
 }
 
 }  // namespace gsr
