@@ -131,21 +131,22 @@ void launch_exclusive_scan(hipStream_t s, const uint32_t *in, const uint32_t *id
 // atomic ticket so a block only waits on blocks that started before it; its first wave inspects 64
 // predecessors per round trip.  Status words: 2-bit flag | 62-bit inclusive/aggregate sum.
 
-template <bool GATHER>
-__global__ __launch_bounds__(256) void scan_lookback_kernel(const uint32_t *__restrict__ in,
+template <bool GATHER, int NT = 256, int PER = SCAN_TILE / 256>
+__global__ __launch_bounds__(NT) void scan_lookback_kernel(const uint32_t *__restrict__ in,
                                                             const uint32_t *__restrict__ idx, uint32_t n,
                                                             uint32_t *__restrict__ out, uint64_t *__restrict__ status,
                                                             uint32_t *__restrict__ ticket,
                                                             uint32_t *__restrict__ flags, uint32_t patience,
                                                             int force) {
-    constexpr int PER = SCAN_TILE / 256;
-    __shared__ uint32_t s_bid, s_w[4];
+    // NT threads x PER items per workgroup (1024 x 16: a quarter of the workgroups, so the look-back chain is shorter)
+    constexpr int TILE = NT * PER, NW = NT / 64;
+    __shared__ uint32_t s_bid, s_w[NW];
     __shared__ unsigned long long s_excl;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (tid == 0) s_bid = atomicAdd(ticket, 1u);
     __syncthreads();
     const uint32_t bid = s_bid;
-    const uint32_t base = bid * SCAN_TILE + tid * PER;
+    const uint32_t base = bid * TILE + tid * PER;
     uint32_t v[PER];
     uint32_t local = 0;
     static_assert(PER % 4 == 0, "16-B loads");
@@ -169,18 +170,20 @@ __global__ __launch_bounds__(256) void scan_lookback_kernel(const uint32_t *__re
     if (lane == 63) s_w[w] = inc;
     __syncthreads();
     if (w == 0) {
-        const uint64_t agg = (uint64_t)s_w[0] + s_w[1] + s_w[2] + s_w[3];
-        // fallback aggregate of block q: the sum of its SCAN_TILE inputs (the input is never written here)
+        uint64_t agg = 0;
+#pragma unroll
+        for (int i = 0; i < NW; i++) agg += s_w[i];
+        // fallback aggregate of block q: the sum of its TILE inputs (the input is never written here)
         auto agg_of = [&](uint32_t q) -> uint64_t {
             uint64_t a = 0;
-            for (uint32_t j = q * SCAN_TILE + lane; j < min(n, (q + 1) * SCAN_TILE); j += 64)
+            for (uint32_t j = q * TILE + lane; j < min(n, (q + 1) * TILE); j += 64)
                 a += scan_load<GATHER>(in, idx, j);
             return wave_sum_u64(a);
         };
         const uint64_t excl = wave_lookback(status, bid, agg, lane, flags, patience, force != 0, agg_of);
         if (lane == 0) {
             s_excl = excl;
-            if (base <= n && n < bid * SCAN_TILE + SCAN_TILE) {  // the block holding element n writes the total
+            if (n >= bid * TILE && n < bid * TILE + TILE) {  // the block holding element n writes the total
                 const uint64_t tot = excl + agg;
                 out[n] = (uint32_t)tot;
                 if (tot > 0xffffffffull) atomicOr(flags, 1u);
@@ -210,9 +213,26 @@ __global__ __launch_bounds__(256) void scan_lookback_kernel(const uint32_t *__re
 void launch_exclusive_scan_lookback(hipStream_t s, const uint32_t *in, const uint32_t *idx, uint32_t n, uint32_t *out,
                                     uint64_t *status, uint32_t *ticket, uint32_t *flags) {
     // status (div_up(n + 1, SCAN_TILE) words) and *ticket must be zero (cleared with the forward's counters)
-    const uint32_t nb = div_up(n + 1, (uint32_t)SCAN_TILE);
     const uint32_t pat = (uint32_t)tuning("lb_patience", 1 << 16);
     const int force = tuning("lb_force", 0);
+    const int snt = tuning("scan_nt", 2048);  // 256: 256 x 16 per workgroup
+    if (snt == 2048) {  // 1024 threads x 32 items
+        const uint32_t nb8 = div_up(n + 1, (uint32_t)(8 * SCAN_TILE));
+        if (idx)
+            scan_lookback_kernel<true, 1024, 32><<<nb8, 1024, 0, s>>>(in, idx, n, out, status, ticket, flags, pat, force);
+        else
+            scan_lookback_kernel<false, 1024, 32><<<nb8, 1024, 0, s>>>(in, nullptr, n, out, status, ticket, flags, pat, force);
+        return;
+    }
+    if (snt == 1024) {  // status words: div_up(n + 1, 4 * SCAN_TILE) of the cleared ones
+        const uint32_t nb4 = div_up(n + 1, (uint32_t)(4 * SCAN_TILE));
+        if (idx)
+            scan_lookback_kernel<true, 1024><<<nb4, 1024, 0, s>>>(in, idx, n, out, status, ticket, flags, pat, force);
+        else
+            scan_lookback_kernel<false, 1024><<<nb4, 1024, 0, s>>>(in, nullptr, n, out, status, ticket, flags, pat, force);
+        return;
+    }
+    const uint32_t nb = div_up(n + 1, (uint32_t)SCAN_TILE);
     if (idx)
         scan_lookback_kernel<true><<<nb, 256, 0, s>>>(in, idx, n, out, status, ticket, flags, pat, force);
     else

@@ -871,6 +871,35 @@ def test_lookback_fallback_is_bitwise_invisible(gpu_device, bucket, onesweep):
         assert np.array_equal(a["grads"][k], b["grads"][k]), k
 
 
+@pytest.mark.parametrize("force", [0, 1])
+@pytest.mark.parametrize("nt", [1024, 2048])
+def test_instance_scan_width_is_invisible(gpu_device, force, nt):
+    """The radix path's instance scan at 1024 threads x 16 counts per workgroup ("scan_nt" 1024: 4x fewer
+    workgroups, a 4x shorter look-back chain) or x 32 ("scan_nt" 2048) gives the 256 x 16 scan's bits, with its look-back on the
+    status words and forced onto the recomputed-aggregate fallback."""
+    from gaussian_splatting_lightning_amd import _native
+    inp = scene_inputs(70_000, 480, 320, sh_degree=1, seed=47, stress_fraction=0.01)
+    dc, di = upstream(480, 320, 47)
+    try:
+        _native.set_tuning("bucket", 0)
+        _native.set_tuning("onesweep", 0)
+        _native.set_tuning("lb_force", force)
+        _native.set_tuning("scan_nt", 256)
+        a = run_hip(inp, gpu_device, dc, di)
+        _native.set_tuning("scan_nt", nt)
+        b = run_hip(inp, gpu_device, dc, di)
+    finally:
+        for k in ("scan_nt", "lb_force", "bucket", "onesweep"):
+            _native.unset_tuning(k)
+    sa, sb = hip_state_arrays(a), hip_state_arrays(b)
+    for k in ("point_list", "ranges", "tiles", "n_contrib"):
+        assert np.array_equal(sa[k], sb[k]), k
+    for k in ("color", "invdepth", "radii"):
+        assert np.array_equal(a[k], b[k]), k
+    for k in GRADS:
+        assert np.array_equal(a["grads"][k], b["grads"][k]), k
+
+
 @pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2, reason="needs two HIP devices")
 def test_render_on_non_current_device():
     """Inputs on cuda:1 while cuda:0 is current (and the reverse afterwards): the library runs on its stream's
