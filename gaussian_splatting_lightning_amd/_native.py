@@ -12,6 +12,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgsrast.so")
+ABI_VERSION = 2  # include/gsrast.h GSR_ABI_VERSION
 
 GSR_BUF_GEOM, GSR_BUF_BINNING, GSR_BUF_IMAGE, GSR_BUF_BWD_SCRATCH = 0, 1, 2, 3
 
@@ -97,7 +98,7 @@ EXPORTED_SYMBOLS = (
     "gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_sh_backward_views", "gsr_sh_backward_views_chunked",
     "gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes",
     "gsr_image_buffer_bytes", "gsr_bwd_scratch_bytes", "gsr_set_profiling", "gsr_num_stages", "gsr_stage_name",
-    "gsr_stage_times", "gsr_reset_stage_times", "gsr_last_error", "gsr_build_info", "gsr_state_layout_query",
+    "gsr_stage_times", "gsr_reset_stage_times", "gsr_last_error", "gsr_build_info", "gsr_abi_version", "gsr_state_layout_query",
     "gsr_set_tuning", "gsr_get_tuning", "gsr_ssim_num_partials", "gsr_ssim_forward", "gsr_ssim_backward", "gsr_adam_step", "gsr_sparse_adam_step",
     "gsr_densify_workspace_bytes", "gsr_densify_classify", "gsr_densify_apply", "gsr_ply_unpack", "gsr_ply_pack",
     "gsr_knn_workspace_bytes", "gsr_knn_mean_dist2", "gsr_debug_wave_stamps",
@@ -190,6 +191,10 @@ def load(path: str | None = None):
     lib.gsr_debug_wave_stamps.restype = ctypes.c_int
     lib.gsr_last_error.restype = ctypes.c_char_p
     lib.gsr_build_info.restype = ctypes.c_char_p
+    if hasattr(lib, "gsr_abi_version"):  # absent from pre-round-6 builds loaded for A/Bs through GSR_LIB
+        lib.gsr_abi_version.restype = ctypes.c_int
+        if lib.gsr_abi_version() != ABI_VERSION:
+            raise RuntimeError(f"{path}: C ABI version {lib.gsr_abi_version()}, this package needs {ABI_VERSION}")
     _lib = lib
     # A/B experiments from the command line: GSR_TUNE="knob=value,knob=value" (gsr_set_tuning before first use)
     for kv in filter(None, os.environ.get("GSR_TUNE", "").split(",")):

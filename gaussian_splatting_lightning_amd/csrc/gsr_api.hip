@@ -1212,6 +1212,7 @@ void gsr_reset_stage_times(void) {
     }
 }
 const char *gsr_last_error(void) { return g_err.c_str(); }
+int gsr_abi_version(void) { return GSR_ABI_VERSION; }
 const char *gsr_build_info(void) {
     return "gsrast: MI355X (gfx950) HIP rasterizer; wave64 tile compositing, LSD radix binning, "
            "deterministic gradient rows; built " __DATE__ " " __TIME__;

@@ -253,6 +253,10 @@ class ViewGradReducer:
             self.shs = None  # materialised by `grads`
         nccl = self.distributed and dist.get_backend(group) == "nccl"
         self.coalesce = nccl if coalesce is None else (bool(coalesce) and nccl)
+        # decided once, before any group starts: a group that failed half-way could not be re-issued safely (the
+        # process group would flush the ops queued before the failure and the fallback would issue them again)
+        if self.coalesce and not _coalescing_supported(self._pg()):
+            self.coalesce = False
         self.sync_ops = (self.chunks == 1) if sync_ops is None else bool(sync_ops)
         # comm_stream="side" (chunked exchange on a HIP device): the reducer's own stream carries the
         # collectives as blocking ops behind one event per chunk, and the compute stream waits for chunk c's group
@@ -269,6 +273,10 @@ class ViewGradReducer:
             self._landed = [torch.cuda.Event() for _ in self.bounds]  # chunk c's collectives are done
             self.sync_ops = True
         self._pending: List[tuple] = []
+        # who writes this step's camera block (compact): "backward" once backward_out()/chunk_outputs() handed
+        # campos_rows to the backward, "begin_step" when the caller passed campos; finish() refuses a step with
+        # neither (the block would still hold the previous step's all-reduced cameras, summed again)
+        self._camera_source: Optional[str] = None
         self._materialised: Optional[Dict[str, torch.Tensor]] = None
         self._stats_synced = False  # sync_densify_stats has reduced the statistics since the last reset
 
@@ -294,6 +302,7 @@ class ViewGradReducer:
         if self.compact:
             out["colors_sh"] = self.gather_in[0]
             out["campos_rows"] = (self.campos_all, self.rank)
+            self._camera_source = "backward"
         else:
             out["shs"] = self.shs
         return out
@@ -317,6 +326,7 @@ class ViewGradReducer:
                 out["colors_sh"] = self.gather_in[c]
                 if c == 0:  # the camera block rides in chunk 0's all-reduce; chunk 0's backward call writes it
                     out["campos_rows"] = (self.campos_all, self.rank)
+                    self._camera_source = "backward"
             else:
                 out["shs"] = v["shs"]
             res.append((g0, g1, out))
@@ -341,6 +351,12 @@ class ViewGradReducer:
         self._materialised = None
         if self.compact and campos is not None:
             torch.mul(self._campos_onehot, campos.reshape(1, 3).to(self.campos_all.dtype), out=self.campos_all)
+            self._camera_source = "begin_step"
+
+    def _check_camera_block(self) -> None:
+        if self._camera_source is None:
+            raise RuntimeError("compact exchange: nothing wrote this step's camera block -- pass the destinations of "
+                               "backward_out()/chunk_outputs() to the backward, or campos to begin_step()/reduce()")
 
     def _pg(self):
         return self.group if self.group is not None else dist.distributed_c10d._get_default_group()
@@ -348,12 +364,7 @@ class ViewGradReducer:
     def _issue(self, c: int):
         """Chunk c's collectives: (gather work, reduce work); None for a completed blocking op."""
         if self.coalesce:
-            try:
-                return self._issue_group(c)
-            except (RuntimeError, AttributeError, NotImplementedError) as e:  # backend without coalescing support
-                import warnings
-                warnings.warn(f"coalesced RCCL group unavailable ({e}); issuing separate collectives")
-                self.coalesce = False
+            return self._issue_group(c)
         gather = None
         if self.compact:
             gather = _all_gather(self.gather_all[c], self.gather_in[c], self.group, not self.sync_ops)
@@ -386,6 +397,8 @@ class ViewGradReducer:
     def start_chunk(self, c: int) -> None:
         """Chunk c's gradients have been enqueued on the current stream: issue its collectives (one group, or the
         all-gather first, so the SH expansion that needs it can start while the all-reduce still runs)."""
+        if c == 0 and self.compact:
+            self._check_camera_block()  # before chunk 0's all-reduce sums the camera block
         gather = reduce = None
         if self.distributed and self.comm_stream is not None:
             cur = torch.cuda.current_stream(self.device)
@@ -404,26 +417,32 @@ class ViewGradReducer:
                        chunk_len=chunk_len)
 
     def finish(self, means3D: torch.Tensor) -> None:
-        """SH expansion (per chunk after its gather, or once after the last) and the wait for every collective."""
+        """SH expansion (per chunk after its gather, or once after the last) and the wait for every collective.
+
+        Every work object is waited exactly once: a chunk's gather and reduce are often ONE object (a coalesced group,
+        or the side stream's event), and dense mode has no gather to wait on, so each is tracked by identity."""
+        waited = set()
+
+        def wait(w) -> None:
+            if w is not None and id(w) not in waited:
+                waited.add(id(w))
+                w.wait()
+
         if self.compact and self._pending:
-            # the camera block rides in chunk 0's all-reduce
-            c0 = self._pending[0]
-            if c0[2] is not None and c0[2] is not c0[1]:
-                c0[2].wait()
-        for c, gather, _ in self._pending:
-            if not self.compact:
-                continue
-            if gather is not None:
-                gather.wait()
-            if self.expand == "chunk" or self.chunks == 1:
-                g0, g1 = self.bounds[c]
-                self._expand(means3D, g0, g1, self.gather_all[c], 0)
-        if self.compact and self.expand == "once" and self.chunks > 1 and self._pending:
-            self._expand(means3D, 0, self.n, self.gather_all_flat, self.chunk_len)
+            self._check_camera_block()
+            wait(self._pending[0][2])  # the camera block rides in chunk 0's all-reduce
+            for c, gather, _ in self._pending:
+                wait(gather)
+                if self.expand == "chunk" or self.chunks == 1:
+                    g0, g1 = self.bounds[c]
+                    self._expand(means3D, g0, g1, self.gather_all[c], 0)
+            if self.expand == "once" and self.chunks > 1:
+                self._expand(means3D, 0, self.n, self.gather_all_flat, self.chunk_len)
         for _, gather, reduce in self._pending:
-            if reduce is not None and reduce is not gather:
-                reduce.wait()
+            wait(gather)
+            wait(reduce)
         self._pending = []
+        self._camera_source = None
 
     def reduce(self, means3D: torch.Tensor, campos: Optional[torch.Tensor] = None) -> None:
         """The whole exchange after an unchunked backward (backward_out()): every chunk at once.  campos: only when
@@ -475,6 +494,17 @@ class ViewGradReducer:
     def stats(self) -> torch.Tensor:
         """(n, 2) accumulated statistics (this rank's until sync_densify_stats, then the global ones)."""
         return self.stats_accum
+
+
+def _coalescing_supported(pg) -> bool:
+    """The process group's coalescing calls and the async flag on both option structs (torch builds differ)."""
+    try:
+        return (hasattr(pg, "_start_coalescing") and hasattr(pg, "_end_coalescing")
+                and hasattr(pg, "_allgather_base")
+                and hasattr(dist.distributed_c10d.AllgatherOptions(), "asyncOp")
+                and hasattr(dist.AllreduceOptions(), "asyncOp"))
+    except Exception:  # noqa: BLE001
+        return False
 
 
 class _StreamEventWork:

@@ -275,8 +275,9 @@ size_t gsr_bwd_scratch_bytes(int64_t R, int64_t num_big);
  * per-pixel contributor counts) bit for bit against the oracle. */
 typedef struct gsr_state_layout {
     /* in: sizeof(gsr_state_layout) as the caller was built (a caller built against an older header passes its
-     * smaller size and gets only the fields it knows); out: the size the library filled (fields are only ever
-     * appended).  0 is taken as the library's own size (callers that predate this field zero-fill the struct). */
+     * smaller size and gets only the fields it knows); out: the size the library filled (from GSR_ABI_VERSION 2
+     * on, fields are only ever appended).  0 is taken as the library's own size.  Version-1 callers (before this
+     * field existed) are NOT compatible: see gsr_abi_version(). */
     size_t struct_size;
     size_t geom_rec_a, geom_rec_b, geom_rec_c; /* float4, float4, float2 of Gaussian 0's record; Gaussian i's at
                                                   + i * geom_rec_stride */
@@ -318,6 +319,13 @@ int gsr_debug_wave_stamps(int which, uint32_t *host_dst, int max_slots);
 
 const char *gsr_last_error(void);
 const char *gsr_build_info(void);
+
+/* ABI version of this header.  2: gsr_state_layout gained struct_size at offset 0 and lost img_tile_sorted /
+ * img_tile_lastkey (a one-time break: a caller built against a version-1 header reads shifted offsets, so it must
+ * check gsr_abi_version() == GSR_ABI_VERSION before using the layout).  From version 2 on, fields of the versioned
+ * structs are only appended, and callers built against this header or a later one interoperate. */
+#define GSR_ABI_VERSION 2
+int gsr_abi_version(void);
 
 #ifdef __cplusplus
 }

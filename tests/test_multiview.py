@@ -149,3 +149,66 @@ def test_one_rank_group_takes_the_collective_path_and_guards_resync():
         red.record_view(dm, radii)
     finally:
         dist.destroy_process_group()
+
+
+class _CountingWork:
+    def __init__(self):
+        self.waits = 0
+
+    def wait(self):
+        self.waits += 1
+
+
+@pytest.mark.parametrize("mode", ["dense", "compact"])
+@pytest.mark.parametrize("shape", ["one_object", "separate", "no_gather"])
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_finish_waits_on_every_collective_once(mode, shape, chunks):
+    """finish() waits on each chunk's collectives exactly once, whatever the work objects look like: ONE object for a
+    chunk's gather and reduce (a coalesced async group, or the side stream's event -- both hand back the same object
+    twice), two objects, or a reduce alone (dense without a gather).  Dense mode once skipped every reduce that was
+    the same object as its gather, so nothing waited and the optimizer could read a half-reduced buffer; a one-rank
+    group cannot show that (its in-place sum leaves the data unchanged), hence the counting works here."""
+    import torch
+    from gaussian_splatting_lightning_amd.multiview import ViewGradReducer
+    red = ViewGradReducer(2048, 16, 3, "cpu", mode=mode, chunks=chunks)
+    red.distributed = True  # collectives mocked below: no process group needed
+    issued = []
+
+    def issue(c):
+        g, r = _CountingWork(), _CountingWork()
+        pair = {"one_object": (g, g), "separate": (g, r), "no_gather": (None, r)}[shape]
+        issued.append(pair)
+        return pair
+
+    red._issue = issue
+    red._sh_views = lambda *a, **k: None  # the SH expansion itself is not under test
+    red.begin_step(torch.zeros(3))
+    for c in range(red.chunks):
+        red.start_chunk(c)
+    red.finish(torch.zeros(2048, 3))
+    assert len(issued) == red.chunks
+    for g, r in issued:
+        for w in {id(x): x for x in (g, r) if x is not None}.values():
+            assert w.waits == 1, (mode, shape, chunks, w.waits)
+    assert red._pending == []
+
+
+def test_compact_exchange_refuses_an_unwritten_camera_block():
+    """Without campos in begin_step and without handing the camera destination to a backward, chunk 0's all-reduce
+    would sum the previous step's already-reduced camera rows again: the reducer raises instead."""
+    import torch
+    from gaussian_splatting_lightning_amd.multiview import ViewGradReducer
+    red = ViewGradReducer(1024, 16, 3, "cpu", mode="compact", chunks=1)
+    red.distributed = True
+    red._issue = lambda c: (None, None)
+    red._sh_views = lambda *a, **k: None
+    red.begin_step()
+    with pytest.raises(RuntimeError, match="camera block"):
+        red.start_chunk(0)
+    red._pending = []
+    red.backward_out()  # the backward now writes the block
+    red.start_chunk(0)
+    red.finish(torch.zeros(1024, 3))
+    red.begin_step()  # the next step starts unwritten again
+    with pytest.raises(RuntimeError, match="camera block"):
+        red.start_chunk(0)
