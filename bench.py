@@ -74,8 +74,14 @@ def parse():
     ap.add_argument("--exchange-chunks", type=int, default=0,
                     help="N>1: Gaussian chunks whose exchange overlaps the rest of the backward (1: after it; 0: the "
                          "cost model's choice)")
-    ap.add_argument("--exchange-expand", default=None, choices=("chunk", "once"),
-                    help="compact exchange: SH expansion per chunk or once after the last gather (default: model)")
+    ap.add_argument("--exchange-expand", default=None, choices=("chunk", "once", "side"),
+                    help="compact exchange: SH expansion per chunk or once after the last gather on the compute "
+                         "stream, or per chunk on the side stream behind its group (default: the cost model's)")
+    ap.add_argument("--plan-world", type=int, default=0,
+                    help="N>1 path: plan the exchange (mode, chunks, SH expansion) for this many ranks instead of "
+                         "WORLD_SIZE -- a one-rank rehearsal (--force-dist) of the N-GPU schedule")
+    ap.add_argument("--no-train-step", action="store_true",
+                    help="skip the extra train_step_ms pass (forward + backward + exchange + Adam)")
     ap.add_argument("--force-dist", action="store_true",
                     help="take the N>1 path (process group, RCCL exchange) even with one rank, e.g. under "
                          "torchrun --nproc-per-node 1")
@@ -133,7 +139,7 @@ def main():
     # chunks' Gaussian ranges and each range's collectives (one RCCL group) are issued as soon as it is enqueued.
     if distributed:
         red = ViewGradReducer(n, M, deg, dev, mode=args.exchange, chunks=args.exchange_chunks or None,
-                              expand=args.exchange_expand)
+                              expand=args.exchange_expand, plan_world=args.plan_world or None)
     else:
         red = ViewGradReducer(n, M, deg, dev, mode="dense", chunks=1)
     mode = red.mode
@@ -148,7 +154,7 @@ def main():
             backward_raw(st, settings, dcolor, dinv, **red.backward_kwargs())
             red.reduce(sc.means3D)
         else:
-            red.begin_step()
+            red.begin_step(means3D=sc.means3D)  # side stream: each chunk's SH expansion runs right behind its group
             backward_chunked(st, settings, dcolor, dinv, red.chunk_outputs(), on_chunk=red.start_chunk,
                              compact_sh=red.compact, accumulate_stats=True)
             red.finish(sc.means3D)
@@ -239,6 +245,70 @@ def main():
     step_events = {"steps": n_ev, "p50_ms": round(per_step[n_ev // 2], 4),
                    "p90_ms": round(per_step[min(n_ev - 1, (9 * n_ev) // 10)], 4),
                    "min_ms": round(per_step[0], 4), "mean_ms": round(sum(per_step) / n_ev, 4)}
+
+    # ---- training step (separate pass, extra field, not the headline): forward + backward + exchange + Adam ----
+    # The reference steps torch.optim.Adam(eps=1e-15) over its six per-Gaussian groups right after the backward
+    # (gs_lightning_module.py:114-134,168-170).  Here the Adam step runs on the rasterizer inputs themselves (means3D,
+    # scales, rotations, opacities and the SH coefficients as features_dc / features_rest, i.e. without the
+    # reference's exp / sigmoid / normalize activations in front of three of them), with the learning rates of
+    # configs/train_gs.yaml; the SH groups take their gradient in factored form through the fused SH Adam
+    # (compact exchange, GaussianAdam.step(sh_views=...)), so no (P, 16, 3) gradient is written at any N.
+    train = None
+    if not args.no_train_step:
+        from gaussian_splatting_lightning_amd.optim import GaussianAdam
+        tp = {k: getattr(sc, k).clone() for k in ("means3D", "scales", "rotations", "opacities", "shs")}
+        f_dc, f_rest = tp["shs"][:, :1], tp["shs"][:, 1:]  # column blocks of the one (P, 16, 3) tensor
+        topt = GaussianAdam([{"params": [tp["means3D"]], "lr": 0.00016, "name": "xyz"},
+                             {"params": [f_dc], "lr": 0.0025, "name": "features_dc"},
+                             {"params": [f_rest], "lr": 0.0025 / 20.0, "name": "features_rest"},
+                             {"params": [tp["opacities"]], "lr": 0.05, "name": "opacity"},
+                             {"params": [tp["scales"]], "lr": 0.005, "name": "scaling"},
+                             {"params": [tp["rotations"]], "lr": 0.001, "name": "rotation"}], lr=0.0, eps=1e-15)
+        tred = ViewGradReducer(n, M, deg, dev, mode="compact", chunks=None if distributed else 1,
+                               plan_world=args.plan_world or None) if distributed else \
+            ViewGradReducer(n, M, deg, dev, mode="compact", chunks=1)
+
+        def train_step():
+            _, _, _, tst = forward_raw(tp["means3D"], tp["shs"], None, tp["opacities"], tp["scales"], tp["rotations"],
+                                       None, settings)
+            if tred.chunks == 1:
+                backward_raw(tst, settings, dcolor, dinv, **tred.backward_kwargs())
+                tred.reduce(tp["means3D"], expand_sh=False)
+            else:
+                tred.begin_step()
+                backward_chunked(tst, settings, dcolor, dinv, tred.chunk_outputs(), on_chunk=tred.start_chunk,
+                                 compact_sh=True, accumulate_stats=True)
+                tred.finish(tp["means3D"], expand_sh=False)
+            gr = tred.grads
+            for k in ("means3D", "scales", "rotations", "opacities"):
+                tp[k].grad = gr[k].view_as(tp[k])
+            topt.step(sh_views=(f_dc, f_rest, tred.sh_views_gradient(tp["means3D"])))
+
+        for _ in range(max(args.warmup, 3)):
+            train_step()
+        gc.disable()
+        if distributed:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t_tr = time.perf_counter()
+        for _ in range(args.steps):
+            train_step()
+        torch.cuda.synchronize()
+        if distributed:
+            dist.barrier()
+        el_tr = time.perf_counter() - t_tr
+        gc.enable()
+        if distributed:
+            t = torch.tensor([el_tr], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el_tr = float(t.item())
+        train = {"train_step_ms": round(1e3 * el_tr / args.steps, 4), "steps": args.steps,
+                 "exchange": tred.describe() if distributed else "none (one view, compact SH gradient)",
+                 "note": "forward + backward + exchange + Adam over the six per-Gaussian groups (GaussianAdam; the SH "
+                         "groups by the fused SH Adam on the factored multi-view gradient), timed like the headline "
+                         "(barrier + synchronize, max over ranks); Adam steps the rasterizer inputs directly (no "
+                         "activation functions in front of scales / rotations / opacities)"}
+        del tp, topt, tred
 
     # ---- per-launch statistics for the roofline (untimed) ----
     lay = _native.state_layout(n, st.num_rendered, W, H)
@@ -359,7 +429,7 @@ def main():
         # also the contributing (pixel, Gaussian) pairs per second (this rank's sum(n_contrib) x N)
         "contrib_pairs_per_s": world * sum_contrib / (ms_per_step * 1e-3),
         "step_events_ms": step_events,
-        "roofline": roofline, "cpu_baseline": cpu,
+        "roofline": roofline, "cpu_baseline": cpu, "train_step": train,
         "stages_ms": {k: round(v, 4) for k, v in stage_avg.items() if v > 0},
     }
     if rank == 0:

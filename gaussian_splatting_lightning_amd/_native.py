@@ -57,6 +57,15 @@ class AdamGroup(ctypes.Structure):
                 ("lr", ctypes.c_double), ("step", ctypes.c_int64)]
 
 
+class AdamShViewsArgs(ctypes.Structure):  # include/gsrast.h gsr_adam_sh_views_args
+    _fields_ = [("P", ctypes.c_int), ("D", ctypes.c_int), ("M", ctypes.c_int), ("V", ctypes.c_int),
+                ("chunk_len", ctypes.c_int64), ("means3D", _fp), ("campos", _fp), ("dL_dcolors_sh", _fp),
+                ("dc_param", _fp), ("dc_exp_avg", _fp), ("dc_exp_avg_sq", _fp), ("dc_lr", ctypes.c_double),
+                ("dc_step", ctypes.c_int64),
+                ("rest_param", _fp), ("rest_exp_avg", _fp), ("rest_exp_avg_sq", _fp), ("rest_lr", ctypes.c_double),
+                ("rest_step", ctypes.c_int64), ("param_row_stride", ctypes.c_int64)]
+
+
 class DensifyArgs(ctypes.Structure):
     _fields_ = [("N", ctypes.c_int64), ("opacity", _fp), ("scaling", _fp), ("max_radii2D", _fp),
                 ("xyz_grad_accum", _fp), ("xyz_grad_count", _fp),
@@ -98,7 +107,7 @@ EXPORTED_SYMBOLS = (
     "gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_sh_backward_views", "gsr_sh_backward_views_chunked",
     "gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes",
     "gsr_image_buffer_bytes", "gsr_bwd_scratch_bytes", "gsr_set_profiling", "gsr_num_stages", "gsr_stage_name",
-    "gsr_stage_times", "gsr_reset_stage_times", "gsr_last_error", "gsr_build_info", "gsr_abi_version", "gsr_state_layout_query",
+    "gsr_stage_times", "gsr_reset_stage_times", "gsr_last_error", "gsr_build_info", "gsr_abi_version", "gsr_adam_sh_views_step", "gsr_state_layout_query",
     "gsr_set_tuning", "gsr_get_tuning", "gsr_ssim_num_partials", "gsr_ssim_forward", "gsr_ssim_backward", "gsr_adam_step", "gsr_sparse_adam_step",
     "gsr_densify_workspace_bytes", "gsr_densify_classify", "gsr_densify_apply", "gsr_ply_unpack", "gsr_ply_pack",
     "gsr_knn_workspace_bytes", "gsr_knn_mean_dist2", "gsr_debug_wave_stamps",
@@ -134,6 +143,10 @@ def load(path: str | None = None):
     lib.gsr_adam_step.argtypes = [ctypes.POINTER(AdamGroup), ctypes.c_int, ctypes.c_double, ctypes.c_double,
                                   ctypes.c_double, ctypes.c_void_p]
     lib.gsr_adam_step.restype = ctypes.c_int
+    if hasattr(lib, "gsr_adam_sh_views_step"):  # absent from pre-round-6 builds loaded for A/Bs through GSR_LIB
+        lib.gsr_adam_sh_views_step.argtypes = [ctypes.POINTER(AdamShViewsArgs), ctypes.c_double, ctypes.c_double,
+                                               ctypes.c_double, ctypes.c_void_p]
+        lib.gsr_adam_sh_views_step.restype = ctypes.c_int
     lib.gsr_sparse_adam_step.argtypes = [ctypes.POINTER(AdamGroup), ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
                                          ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_void_p]
     lib.gsr_sparse_adam_step.restype = ctypes.c_int

@@ -81,12 +81,14 @@ enum Stage {
     ST_BK_SCATTER,
     ST_SEG_SORT,
     ST_PRE_COLOR,
+    ST_ADAM_SH,
     ST_COUNT
 };
 const char *kStageNames[ST_COUNT] = {"preprocess", "depth_sort", "instance_scan", "readback",
                                      "expand",     "tile_sort",  "tile_ranges",   "render_fwd",
                                      "render_bwd", "big_reduce", "preprocess_bwd", "sh_views",
-                                     "bucket_count", "bucket_scatter", "seg_sort", "preprocess_color"};
+                                     "bucket_count", "bucket_scatter", "seg_sort", "preprocess_color",
+                                     "adam_sh_views"};
 
 struct Profiler {
     std::mutex mu;
@@ -884,6 +886,46 @@ int gsr_sh_backward_views_chunked(int P, int D, int M, int V, int64_t chunk_len,
 int gsr_sh_backward_views(int P, int D, int M, int V, const float *means3D, const float *campos,
                           const float *dL_dcolors_sh, float *dL_dsh, void *stream_ptr) {
     return gsr_sh_backward_views_chunked(P, D, M, V, 0, means3D, campos, dL_dcolors_sh, dL_dsh, stream_ptr);
+}
+
+int gsr_adam_sh_views_step(const gsr_adam_sh_views_args *a, double beta1, double beta2, double eps, void *stream_ptr) {
+    if (!a) return fail(GSR_ERR_ARG, "adam sh views: null arguments");
+    if (a->P < 0 || a->V < 0) return fail(GSR_ERR_ARG, "P and V must be >= 0");
+    if (a->D < 0 || a->D > 3) return fail(GSR_ERR_ARG, "sh_degree must be in [0, 3]");
+    if (a->M != 16) return fail(GSR_ERR_ARG, "adam sh views: M must be 16");
+    if (a->chunk_len < 0) return fail(GSR_ERR_ARG, "chunk_len must be >= 0");
+    if (a->dc_step < 1 || a->rest_step < 1) return fail(GSR_ERR_ARG, "adam: step must be >= 1");
+    if (a->P == 0) return GSR_OK;
+    if (!a->means3D || (a->V > 0 && (!a->campos || !a->dL_dcolors_sh)) || !a->dc_param || !a->dc_exp_avg ||
+        !a->dc_exp_avg_sq || !a->rest_param || !a->rest_exp_avg || !a->rest_exp_avg_sq)
+        return fail(GSR_ERR_ARG, "null argument");
+    AdamShLaunch L{};
+    L.P = a->P; L.V = a->V;
+    L.L = (a->chunk_len == 0 || a->chunk_len >= a->P) ? a->P : (int)a->chunk_len;
+    L.means3D = a->means3D; L.campos = a->campos; L.dc = a->dL_dcolors_sh;
+    if (a->param_row_stride != 0 && a->param_row_stride != 48)
+        return fail(GSR_ERR_ARG, "adam sh views: param_row_stride must be 0 (packed) or 48 (one (P, 16, 3) tensor)");
+    auto group = [&](AdamShGroup &g, float *p, float *m, float *v, double lr, int64_t step, int64_t width) {
+        const double bc1 = 1.0 - std::pow(beta1, (double)step), bc2 = 1.0 - std::pow(beta2, (double)step);
+        g.param = p; g.exp_avg = m; g.exp_avg_sq = v;
+        g.param_stride = a->param_row_stride ? a->param_row_stride : width;
+        g.step_size = (float)(lr / bc1);  // as gsr_adam_step
+        g.bc2_sqrt = (float)std::sqrt(bc2);
+    };
+    group(L.dc_group, a->dc_param, a->dc_exp_avg, a->dc_exp_avg_sq, a->dc_lr, a->dc_step, 3);
+    group(L.rest_group, a->rest_param, a->rest_exp_avg, a->rest_exp_avg_sq, a->rest_lr, a->rest_step, 45);
+    // float4 moments (and parameters when packed) need 16-B aligned bases
+    const uintptr_t params = a->param_row_stride ? 0 : (((uintptr_t)a->dc_param) | ((uintptr_t)a->rest_param));
+    L.vec4 = ((params | ((uintptr_t)a->dc_exp_avg) | ((uintptr_t)a->dc_exp_avg_sq) | ((uintptr_t)a->rest_exp_avg) |
+               ((uintptr_t)a->rest_exp_avg_sq)) & 15) == 0;
+    L.one_minus_beta1 = (float)(1.0 - beta1);
+    L.beta2 = (float)beta2;
+    L.one_minus_beta2 = (float)(1.0 - beta2);
+    L.eps = (float)eps;
+    hipStream_t stream = (hipStream_t)stream_ptr;
+    StreamDeviceGuard device_guard(stream);
+    GSR_STAGE(ST_ADAM_SH, 0, launch_adam_sh_views(stream, L, a->D));
+    return GSR_OK;
 }
 
 int gsr_adam_step(const gsr_adam_group *groups, int num_groups, double beta1, double beta2, double eps,

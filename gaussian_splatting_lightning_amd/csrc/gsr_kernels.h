@@ -242,6 +242,21 @@ void launch_preprocess_bwd(hipStream_t s, const PreprocessBwdParams &p);
 void launch_sh_backward_views(hipStream_t s, int P, int D, int M, int V, int chunk_len, const float *means3D,
                               const float *campos, const float *dcolors_sh, float *dsh);
 
+// fused Adam of the SH groups on the multi-view expansion (gsr_views.hip; M = 16)
+struct AdamShGroup {
+    float *param, *exp_avg, *exp_avg_sq;
+    float step_size, bc2_sqrt;
+    int64_t param_stride;  // floats between the parameter's rows: 3 / 45 (own tensors) or 48 (one (P, 16, 3) tensor)
+};
+struct AdamShLaunch {
+    int P, V, L;
+    const float *means3D, *campos, *dc;
+    AdamShGroup dc_group, rest_group;
+    float one_minus_beta1, beta2, one_minus_beta2, eps;
+    int vec4;
+};
+void launch_adam_sh_views(hipStream_t s, const AdamShLaunch &L, int D);
+
 // ---- fused Adam (gsr_adam.hip) ----
 constexpr int ADAM_MAX_GROUPS = 16;
 struct AdamGroupDev {

@@ -15,22 +15,16 @@ namespace gsr {
 constexpr int VIEWS_STRIDE = 52;
 // The factors are laid out chunk-major (the multi-view exchange gathers them per Gaussian chunk): chunk c holds
 // Gaussians [c L, min(P, (c+1) L)) as a (V, L_c, 3) block at offset c V L 3; L >= P is the plain (V, P, 3) array.
-template <int DEG, bool STAGED>
-__global__ __launch_bounds__(256) void sh_backward_views_kernel(int P, int M, int V, int L,
-                                                                const float *__restrict__ means3D,
-                                                                const float *__restrict__ campos,
-                                                                const float *__restrict__ dc,
-                                                                float *__restrict__ dsh) {
+// Gaussian ii's expanded gradient row, in registers (shared by the expansion and the fused SH Adam, so the two
+// produce the same bits).
+template <int DEG>
+__device__ __forceinline__ void views_accumulate(int ii, int P, int V, int L, const float *__restrict__ means3D,
+                                                 const float *__restrict__ campos, const float *__restrict__ dc,
+                                                 float (&acc)[3 * (DEG + 1) * (DEG + 1)]) {
     constexpr int NB = (DEG + 1) * (DEG + 1);
-    __shared__ __attribute__((aligned(16))) float s_row[STAGED ? 4 : 1][STAGED ? 32 * VIEWS_STRIDE : 1];
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (!STAGED && i >= P) return;
-    const bool live = i < P;
-    const int ii = live ? i : P - 1;
     const float mx = means3D[3 * ii], my = means3D[3 * ii + 1], mz = means3D[3 * ii + 2];
     const int c = ii / L, g0 = c * L, Lc = min(L, P - g0);
     const float *dchunk = dc + (size_t)g0 * V * 3 + (size_t)(ii - g0) * 3;
-    float acc[3 * NB];
 #pragma unroll
     for (int k = 0; k < 3 * NB; k++) acc[k] = 0.f;
     for (int v = 0; v < V; v++) {
@@ -48,6 +42,38 @@ __global__ __launch_bounds__(256) void sh_backward_views_kernel(int P, int M, in
             acc[3 * k + 2] += basis[k] * b;
         }
     }
+}
+
+// One half-wave's 32 gradient rows (48 floats, zero beyond the active degree's coefficients) into LDS at a
+// VIEWS_STRIDE-float stride.
+template <int NB>
+__device__ __forceinline__ void stage_rows(float *sw, int lane, int h, const float (&acc)[3 * NB]) {
+    if ((lane >> 5) == h) {
+        float *r = sw + (lane & 31) * VIEWS_STRIDE;
+#pragma unroll
+        for (int k = 0; k < 12; k++)
+            *reinterpret_cast<float4 *>(r + 4 * k) =
+                make_float4(4 * k < 3 * NB ? acc[4 * k < 3 * NB ? 4 * k : 0] : 0.f,
+                            4 * k + 1 < 3 * NB ? acc[4 * k + 1 < 3 * NB ? 4 * k + 1 : 0] : 0.f,
+                            4 * k + 2 < 3 * NB ? acc[4 * k + 2 < 3 * NB ? 4 * k + 2 : 0] : 0.f,
+                            4 * k + 3 < 3 * NB ? acc[4 * k + 3 < 3 * NB ? 4 * k + 3 : 0] : 0.f);
+    }
+}
+
+template <int DEG, bool STAGED>
+__global__ __launch_bounds__(256) void sh_backward_views_kernel(int P, int M, int V, int L,
+                                                                const float *__restrict__ means3D,
+                                                                const float *__restrict__ campos,
+                                                                const float *__restrict__ dc,
+                                                                float *__restrict__ dsh) {
+    constexpr int NB = (DEG + 1) * (DEG + 1);
+    __shared__ __attribute__((aligned(16))) float s_row[STAGED ? 4 : 1][STAGED ? 32 * VIEWS_STRIDE : 1];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (!STAGED && i >= P) return;
+    const bool live = i < P;
+    const int ii = live ? i : P - 1;
+    float acc[3 * NB];
+    views_accumulate<DEG>(ii, P, V, L, means3D, campos, dc, acc);
     if constexpr (STAGED) {
         const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
         float *sw = s_row[w];
@@ -55,16 +81,7 @@ __global__ __launch_bounds__(256) void sh_backward_views_kernel(int P, int M, in
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             wave_lds_sync();
-            if ((lane >> 5) == h) {
-                float *r = sw + (lane & 31) * VIEWS_STRIDE;
-#pragma unroll
-                for (int k = 0; k < 12; k++)
-                    *reinterpret_cast<float4 *>(r + 4 * k) =
-                        make_float4(4 * k < 3 * NB ? acc[4 * k < 3 * NB ? 4 * k : 0] : 0.f,
-                                    4 * k + 1 < 3 * NB ? acc[4 * k + 1 < 3 * NB ? 4 * k + 1 : 0] : 0.f,
-                                    4 * k + 2 < 3 * NB ? acc[4 * k + 2 < 3 * NB ? 4 * k + 2 : 0] : 0.f,
-                                    4 * k + 3 < 3 * NB ? acc[4 * k + 3 < 3 * NB ? 4 * k + 3 : 0] : 0.f);
-            }
+            stage_rows<NB>(sw, lane, h, acc);
             wave_lds_sync();
 #pragma unroll
             for (int c = 0; c < 6; c++) {  // 32 rows x 48 floats = 384 float4, 6 per lane
@@ -89,6 +106,105 @@ __global__ __launch_bounds__(256) void sh_backward_views_kernel(int P, int M, in
 #pragma unroll
         for (int k = 0; k < 3 * NB; k++) o[k] = acc[k];
         for (int k = 3 * NB; k < 3 * M; k++) o[k] = 0.f;
+    }
+}
+
+// Fused Adam step of the two SH parameter groups whose gradient is the multi-view expansion above: features_dc
+// (P, 1, 3) holds coefficient 0 of each row, features_rest (P, M - 1, 3) coefficients 1..15 (M = 16).  The row is
+// formed in registers exactly as sh_backward_views_kernel forms it, staged in LDS, and every lane then updates
+// consecutive float4s of the half-wave's 32-row block of each group (coalesced param / moment traffic) with
+// adam_one's arithmetic, so the result is bitwise that of the expansion followed by adam_kernel -- without the
+// 192-B gradient row written and read back.
+__device__ __forceinline__ void adam_elem(float &p, float g, float &m, float &v, const AdamShGroup &G,
+                                          const AdamShLaunch &L) {
+    m = m + L.one_minus_beta1 * (g - m);
+    v = v * L.beta2 + L.one_minus_beta2 * (g * g);
+    const float denom = sqrtf(v) / G.bc2_sqrt + L.eps;
+    p = p + (-G.step_size) * (m / denom);
+}
+
+// The group's elements of this half-wave block: element e of the block is row e / W, coefficient column e % W + C0 of
+// the staged row (W = 3 for features_dc, 45 for features_rest).  The moments are contiguous (row r's elements at
+// r W); the parameter either too (param_stride == W) or rows of a joint (P, 16, 3) SH tensor (param_stride == 48,
+// the pointer at the group's first column): then the parameter is read and written per element.
+template <int W, int C0>
+__device__ __forceinline__ void adam_block(const AdamShGroup &G, const AdamShLaunch &L, const float *sw, int lane,
+                                           int64_t r0, int64_t rows_end, bool vec4) {
+    constexpr int N = 32 * W;
+    const int64_t e0 = r0 * W, e_end = rows_end * W;
+    const bool packed = G.param_stride == W;
+    for (int q = lane; 4 * q < N; q += 64) {
+        const int e = 4 * q;
+        const int64_t ge = e0 + e;
+        if (ge >= e_end) break;
+        if (vec4 && ge + 4 <= e_end) {
+            float4 m = *reinterpret_cast<const float4 *>(G.exp_avg + ge);
+            float4 v = *reinterpret_cast<const float4 *>(G.exp_avg_sq + ge);
+            float p[4];
+            if (packed) {
+                const float4 p4 = *reinterpret_cast<const float4 *>(G.param + ge);
+                p[0] = p4.x; p[1] = p4.y; p[2] = p4.z; p[3] = p4.w;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++) p[j] = G.param[(r0 + (e + j) / W) * G.param_stride + (e + j) % W];
+            }
+            adam_elem(p[0], sw[(e / W) * VIEWS_STRIDE + e % W + C0], m.x, v.x, G, L);
+            adam_elem(p[1], sw[((e + 1) / W) * VIEWS_STRIDE + (e + 1) % W + C0], m.y, v.y, G, L);
+            adam_elem(p[2], sw[((e + 2) / W) * VIEWS_STRIDE + (e + 2) % W + C0], m.z, v.z, G, L);
+            adam_elem(p[3], sw[((e + 3) / W) * VIEWS_STRIDE + (e + 3) % W + C0], m.w, v.w, G, L);
+            if (packed) {
+                *reinterpret_cast<float4 *>(G.param + ge) = make_float4(p[0], p[1], p[2], p[3]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++) G.param[(r0 + (e + j) / W) * G.param_stride + (e + j) % W] = p[j];
+            }
+            *reinterpret_cast<float4 *>(G.exp_avg + ge) = m;
+            *reinterpret_cast<float4 *>(G.exp_avg_sq + ge) = v;
+        } else {
+            for (int j = 0; j < 4 && ge + j < e_end; j++) {
+                const int64_t pi = (r0 + (e + j) / W) * G.param_stride + (e + j) % W;
+                float p = G.param[pi], m = G.exp_avg[ge + j], v = G.exp_avg_sq[ge + j];
+                adam_elem(p, sw[((e + j) / W) * VIEWS_STRIDE + (e + j) % W + C0], m, v, G, L);
+                G.param[pi] = p;
+                G.exp_avg[ge + j] = m;
+                G.exp_avg_sq[ge + j] = v;
+            }
+        }
+    }
+}
+
+template <int DEG>
+__global__ __launch_bounds__(256) void adam_sh_views_kernel(AdamShLaunch L) {
+    constexpr int NB = (DEG + 1) * (DEG + 1);
+    __shared__ __attribute__((aligned(16))) float s_row[4][32 * VIEWS_STRIDE];
+    const int P = L.P;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ii = i < P ? i : P - 1;
+    float acc[3 * NB];
+    views_accumulate<DEG>(ii, P, L.V, L.L, L.means3D, L.campos, L.dc, acc);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float *sw = s_row[w];
+    const int64_t row0 = (int64_t)blockIdx.x * 256 + (int64_t)w * 64;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        wave_lds_sync();
+        stage_rows<NB>(sw, lane, h, acc);
+        wave_lds_sync();
+        const int64_t r = row0 + 32 * h;
+        if (r >= P) break;
+        adam_block<3, 0>(L.dc_group, L, sw, lane, r, P, L.vec4);
+        adam_block<45, 3>(L.rest_group, L, sw, lane, r, P, L.vec4);
+    }
+}
+
+void launch_adam_sh_views(hipStream_t s, const AdamShLaunch &L, int D) {
+    if (L.P <= 0) return;
+    const dim3 grid(div_up(L.P, 256)), block(256);
+    switch (D) {
+        case 0: adam_sh_views_kernel<0><<<grid, block, 0, s>>>(L); break;
+        case 1: adam_sh_views_kernel<1><<<grid, block, 0, s>>>(L); break;
+        case 2: adam_sh_views_kernel<2><<<grid, block, 0, s>>>(L); break;
+        default: adam_sh_views_kernel<3><<<grid, block, 0, s>>>(L); break;
     }
 }
 

@@ -67,6 +67,7 @@ EXCHANGE_COSTS = dict(
     chunk_ms=0.0043,         # per extra chunk: one more per-Gaussian-stage launch (and SH-expansion launch)
     group_sync_ms=0.007,     # one blocking collective group (chunks == 1)
     group_async_ms=0.011,    # one async collective group (chunks > 1, on the reducer's side stream)
+    event_ms=0.003,          # one event record / wait hand-off between the compute and the side stream
     link_GBps=153.0,
     links=7,
     bus_efficiency=0.6,
@@ -86,8 +87,11 @@ def simulate_exchange(n: int, world: int, mode: str, chunks: int, expand: str = 
                       costs: Optional[dict] = None) -> Dict[str, float]:
     """Timeline of the backward's per-Gaussian stage + the exchange (ms after the compositing backward ends).
 
-    compute stream: K per-Gaussian chunks, then the SH expansions (compact), each after its chunk's group landed;
-    comm stream (RCCL): group c starts when chunk c is enqueued-and-computed and group c-1 is done."""
+    K = 1: the group runs blocking on the compute stream after the per-Gaussian stage, then the SH expansion.
+    K > 1: compute stream = K per-Gaussian chunks, each followed by an event record; the reducer's side stream = per
+    chunk [wait for its event, group] in order.  The SH expansion (compact) runs on the compute stream after the
+    chunk's group landed ("chunk"), once after the last ("once"), or on the side stream right behind each group
+    ("side"); the step ends when the compute stream has waited for the side stream's last event."""
     c = dict(EXCHANGE_COSTS, **(costs or {}))
     scale = n / 1e6
     K = max(1, int(chunks))
@@ -96,25 +100,25 @@ def simulate_exchange(n: int, world: int, mode: str, chunks: int, expand: str = 
     bus = c["link_GBps"] * c["links"] * c["bus_efficiency"] * 1e9  # B/s
     link_bytes = exchange_bytes_per_gaussian(mode, N, M) * n
     comm = link_bytes / bus * 1e3 if N > 1 else 0.0  # one rank: in-place collectives move nothing
-    group = c["group_sync_ms"] if K == 1 else c["group_async_ms"]
-    t_chunk = [pb / K + (c["chunk_ms"] if k > 0 else 0.0) for k in range(K)]
-    comp_end = 0.0
-    comm_end = 0.0
-    group_end = []
-    for k in range(K):
-        comp_end += t_chunk[k]
-        start = max(comp_end, comm_end)
-        comm_end = start + group + comm / K
-        group_end.append(comm_end)
-    t = comp_end
-    if mode == "compact":
-        exp = (c["exp_ms"] + c["exp_view_ms"] * (N - 1)) * scale
-        if expand == "once":
-            t = max(t, group_end[-1]) + exp
-        else:
+    exp = (c["exp_ms"] + c["exp_view_ms"] * (N - 1)) * scale if mode == "compact" else 0.0
+    if K == 1:
+        end = pb + c["group_sync_ms"] + comm + exp
+    else:
+        comp_end = comm_end = 0.0
+        landed = []
+        for k in range(K):
+            comp_end += pb / K + (c["chunk_ms"] if k > 0 else 0.0) + c["event_ms"]
+            comm_end = max(comp_end, comm_end) + c["group_async_ms"] + comm / K
+            if expand == "side" and exp:
+                comm_end += exp / K + (c["chunk_ms"] if k > 0 else 0.0)
+            landed.append(comm_end)
+        t = comp_end
+        if exp and expand == "chunk":
             for k in range(K):
-                t = max(t, group_end[k]) + exp / K + (c["chunk_ms"] if k > 0 else 0.0)
-    end = max(t, comm_end)
+                t = max(t, landed[k] + c["event_ms"]) + exp / K + (c["chunk_ms"] if k > 0 else 0.0)
+        elif exp and expand == "once":
+            t = max(t, landed[-1] + c["event_ms"]) + exp
+        end = max(t, comm_end + c["event_ms"])
     return {"mode": mode, "chunks": K, "expand": expand, "per_gaussian_stage_ms": round(pb, 4),
             "link_MB": round(link_bytes / 1e6, 1), "comm_ms": round(comm, 4), "end_ms": round(end, 4),
             "exposed_ms": round(end - pb, 4)}
@@ -128,7 +132,7 @@ def plan_exchange(n: int, world: int, M: int = 16, costs: Optional[dict] = None,
         for K in chunk_options:
             if K > 1 and n < 256 * K:
                 continue
-            for expand in (("chunk", "once") if (mode == "compact" and K > 1) else ("once",)):
+            for expand in (("chunk", "once", "side") if (mode == "compact" and K > 1) else ("once",)):
                 r = simulate_exchange(n, world, mode, K, expand, M, costs)
                 if best is None or r["end_ms"] < best["end_ms"] - 1e-6:
                     best = r
@@ -177,7 +181,8 @@ class ViewGradReducer:
                  world_size: Optional[int] = None,
                  sh_views_fn: Optional[Callable[..., torch.Tensor]] = None, chunks: Optional[int] = 1,
                  distributed: Optional[bool] = None, expand: Optional[str] = None,
-                 coalesce: Optional[bool] = None, sync_ops: Optional[bool] = None, comm_stream: Optional[str] = None):
+                 coalesce: Optional[bool] = None, sync_ops: Optional[bool] = None, comm_stream: Optional[str] = None,
+                 plan_world: Optional[int] = None):
         if mode not in ("dense", "compact", "auto"):
             raise ValueError(f"mode must be 'dense', 'compact' or 'auto', got {mode!r}")
         self.n, self.M, self.D = int(n), int(M), int(sh_degree)
@@ -193,7 +198,8 @@ class ViewGradReducer:
         self.rank = dist.get_rank(group) if self.distributed else 0
         self.plan = None
         if mode == "auto" or chunks is None:
-            self.plan = plan_exchange(self.n, self.world, self.M,
+            # plan_world: plan for that many ranks (a one-rank rehearsal of the N-GPU schedule, bench.py --plan-world)
+            self.plan = plan_exchange(self.n, int(plan_world or self.world), self.M,
                                       modes=("compact", "dense") if mode == "auto" else (mode,),
                                       chunk_options=(1, 2, 4, 8) if chunks is None else (int(chunks),))
             mode = self.plan["mode"]
@@ -203,8 +209,8 @@ class ViewGradReducer:
         self.mode = mode
         self.compact = mode == "compact"
         self.expand = expand or "chunk"
-        if self.expand not in ("chunk", "once"):
-            raise ValueError(f"expand must be 'chunk' or 'once', got {self.expand!r}")
+        if self.expand not in ("chunk", "once", "side"):
+            raise ValueError(f"expand must be 'chunk', 'once' or 'side', got {self.expand!r}")
         self._sh_views = sh_views_fn or sh_backward_views
         self.widths = dict(means3D=3, scales=3, rotations=4, opacities=1, shs=3 * self.M)
         self.fields = FIELDS_COMPACT if self.compact else FIELDS_DENSE
@@ -273,10 +279,13 @@ class ViewGradReducer:
             self._landed = [torch.cuda.Event() for _ in self.bounds]  # chunk c's collectives are done
             self.sync_ops = True
         self._pending: List[tuple] = []
+        self._side_means: Optional[torch.Tensor] = None  # begin_step(means3D=...): expansions on the side stream
+        self._expanded: set = set()
         # who writes this step's camera block (compact): "backward" once backward_out()/chunk_outputs() handed
         # campos_rows to the backward, "begin_step" when the caller passed campos; finish() refuses a step with
         # neither (the block would still hold the previous step's all-reduced cameras, summed again)
         self._camera_source: Optional[str] = None
+        self._sh_expanded = True  # finish(expand_sh=False) leaves dL/dshs in factored form (sh_views_gradient)
         self._materialised: Optional[Dict[str, torch.Tensor]] = None
         self._stats_synced = False  # sync_densify_stats has reduced the statistics since the last reset
 
@@ -341,14 +350,22 @@ class ViewGradReducer:
         torch.maximum(self.radii_max, radii.to(torch.int32), out=self.radii_max)
 
     # ---- exchange ----
-    def begin_step(self, campos: Optional[torch.Tensor] = None) -> None:
+    def begin_step(self, campos: Optional[torch.Tensor] = None, means3D: Optional[torch.Tensor] = None,
+                   expand_sh: bool = True) -> None:
         """Start of a step's exchange.  The camera block that chunk 0's all-reduce carries (this rank's campos in its
         row, zeros elsewhere) is written by the backward call that receives backward_out() / chunk_outputs()
         ("campos_rows"); a caller whose backward does not (a custom gradient source) passes campos here instead (one
-        elementwise launch)."""
+        elementwise launch).
+
+        means3D (expand="side": the side stream, compact mode): each chunk's SH expansion runs on the side stream right
+        behind its group, overlapping the compute stream's next chunks, and finish() only waits; expand_sh=False for
+        the factored form (see finish).  Without means3D, "side" expands in finish() like "chunk"."""
         self._check_not_synced()
         self._pending = []
         self._materialised = None
+        side = self.compact and self.distributed and self.comm_stream is not None and self.expand == "side"
+        self._side_means = means3D if (side and expand_sh and means3D is not None) else None
+        self._expanded = set()
         if self.compact and campos is not None:
             torch.mul(self._campos_onehot, campos.reshape(1, 3).to(self.campos_all.dtype), out=self.campos_all)
             self._camera_source = "begin_step"
@@ -406,6 +423,10 @@ class ViewGradReducer:
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(self._ready[c])
                 self._issue(c)  # blocking ops: they run on the side stream itself
+                if self._side_means is not None:  # the SH expansion behind the group, off the compute stream
+                    g0, g1 = self.bounds[c]
+                    self._expand(self._side_means, g0, g1, self.gather_all[c], 0)
+                    self._expanded.add(c)
                 self._landed[c].record(self.comm_stream)
             gather = reduce = _StreamEventWork(self._landed[c], self.device)
         elif self.distributed:
@@ -416,8 +437,12 @@ class ViewGradReducer:
         self._sh_views(means3D[g0:g1], self.campos_all, factors, self.D, self.M, out=self.shs[g0:g1],
                        chunk_len=chunk_len)
 
-    def finish(self, means3D: torch.Tensor) -> None:
+    def finish(self, means3D: torch.Tensor, expand_sh: bool = True) -> None:
         """SH expansion (per chunk after its gather, or once after the last) and the wait for every collective.
+
+        expand_sh=False (compact mode): no expansion -- the optimizer takes the SH gradient in factored form
+        (sh_views_gradient() with GaussianAdam.step(sh_views=...), which forms it inside the update); grads["shs"] is
+        then None for this step.
 
         Every work object is waited exactly once: a chunk's gather and reduce are often ONE object (a coalesced group,
         or the side stream's event), and dense mode has no gather to wait on, so each is tracked by identity."""
@@ -430,27 +455,46 @@ class ViewGradReducer:
 
         if self.compact and self._pending:
             self._check_camera_block()
-            wait(self._pending[0][2])  # the camera block rides in chunk 0's all-reduce
+            todo = [c for c, _, _ in self._pending if c not in self._expanded] if expand_sh else []
+            if todo:
+                wait(self._pending[0][2])  # the camera block rides in chunk 0's all-reduce
             for c, gather, _ in self._pending:
+                if c not in todo:
+                    continue
                 wait(gather)
-                if self.expand == "chunk" or self.chunks == 1:
+                if self.expand != "once" or self.chunks == 1:
                     g0, g1 = self.bounds[c]
                     self._expand(means3D, g0, g1, self.gather_all[c], 0)
-            if self.expand == "once" and self.chunks > 1:
+            if todo and self.expand == "once" and self.chunks > 1:
                 self._expand(means3D, 0, self.n, self.gather_all_flat, self.chunk_len)
+        self._sh_expanded = expand_sh or not self.compact
+        if self.comm_stream is not None and self._pending:
+            # the side stream runs every chunk's group (and expansion) in order: its last event covers them all
+            wait(self._pending[-1][2])
+            waited.update(id(w) for _, g, r in self._pending for w in (g, r))
         for _, gather, reduce in self._pending:
             wait(gather)
             wait(reduce)
         self._pending = []
         self._camera_source = None
 
-    def reduce(self, means3D: torch.Tensor, campos: Optional[torch.Tensor] = None) -> None:
+    def reduce(self, means3D: torch.Tensor, campos: Optional[torch.Tensor] = None, expand_sh: bool = True) -> None:
         """The whole exchange after an unchunked backward (backward_out()): every chunk at once.  campos: only when
         the backward did not write the camera block (see begin_step)."""
         self.begin_step(campos)
         for c in range(self.chunks):
             self.start_chunk(c)
-        self.finish(means3D)
+        self.finish(means3D, expand_sh)
+
+    def sh_views_gradient(self, means3D: torch.Tensor):
+        """The step's summed SH gradient in factored form (compact mode, after finish()): every rank's colour factors
+        (the chunk-major gather buffer) and cameras, for GaussianAdam.step(sh_views=(features_dc, features_rest,
+        this)), which expands it inside the update instead of reading a (P, M, 3) gradient."""
+        from .optim import ShViewsGradient
+        if not self.compact:
+            raise RuntimeError("sh_views_gradient: the dense exchange carries dL/dshs itself")
+        return ShViewsGradient(means3D=means3D.contiguous(), campos=self.campos_all, factors=self.gather_all_flat,
+                               sh_degree=self.D, chunk_len=self.chunk_len if self.chunks > 1 else 0)
 
     def sync_densify_stats(self):
         """SUM the accumulated statistics and MAX the radii over ranks, in place; returns (stats, radii_max):
@@ -480,13 +524,14 @@ class ViewGradReducer:
     def grads(self) -> Dict[str, torch.Tensor]:
         """Per-field (n, w) gradients: views of the exchange buffer with one chunk, else gathered from the chunk
         blocks once per step (one copy of 11 (compact) / 59 (dense) floats per Gaussian)."""
+        shs = self.shs if self._sh_expanded else None
         if self.chunks == 1:
             v = self.chunk_views[0]
             return dict(means3D=v["means3D"], scales=v["scales"], rotations=v["rotations"],
-                        opacities=v["opacities"], shs=self.shs)
+                        opacities=v["opacities"], shs=shs)
         if self._materialised is None:
             m = {k: torch.cat([v[k] for v in self.chunk_views], 0) for k in self.fields}
-            m["shs"] = self.shs if self.compact else m["shs"].view(self.n, self.M, 3)
+            m["shs"] = shs if self.compact else m["shs"].view(self.n, self.M, 3)
             self._materialised = m
         return dict(self._materialised)
 

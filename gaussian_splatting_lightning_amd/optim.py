@@ -14,16 +14,29 @@ non-fp32 or CPU parameters -- these raise instead of falling back.
 from __future__ import annotations
 
 import ctypes
-from typing import Iterable
+from dataclasses import dataclass
+from typing import Iterable, Optional
 
 import torch
 
 from . import _native
 from .rasterizer import _stream_handle
 
-__all__ = ["GaussianAdam", "SparseGaussianAdam"]
+__all__ = ["GaussianAdam", "SparseGaussianAdam", "ShViewsGradient"]
 
 _MAX_GROUPS = 16  # ADAM_MAX_GROUPS in csrc/gsr_kernels.h
+
+
+@dataclass
+class ShViewsGradient:
+    """The summed SH gradient of a multi-view step in factored form (multiview.ViewGradReducer.sh_views_gradient):
+    dL/dshs[g] = sum_v basis(normalize(means3D[g] - campos[v])) (x) factors_v[g] (csrc/gsr_views.hip).  factors is the
+    exchange's chunk-major (V, L_c, 3) gather buffer (chunk_len = L; 0: one (V, P, 3) block)."""
+    means3D: torch.Tensor
+    campos: torch.Tensor
+    factors: torch.Tensor
+    sh_degree: int
+    chunk_len: int = 0
 
 
 class GaussianAdam(torch.optim.Optimizer):
@@ -39,18 +52,27 @@ class GaussianAdam(torch.optim.Optimizer):
         super().__init__(params, defaults)
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, sh_views: Optional[tuple] = None):
+        """One Adam step of every parameter with a gradient.
+
+        sh_views = (features_dc, features_rest, ShViewsGradient): the two SH parameters (M = 16 coefficients in all)
+        take their gradient from the multi-view factors instead of .grad -- the expansion happens inside the update
+        (gsr_adam_sh_views_step), bitwise the same as expanding into .grad and stepping (their .grad is ignored)."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        fused = None
+        if sh_views is not None:
+            fused = self._sh_views_args(*sh_views)
+        skip = {id(t) for t in sh_views[:2]} if sh_views is not None else set()
         batches = {}
         keep_alive = []
         for group in self.param_groups:
             b1, b2 = group["betas"]
             lr = float(group["lr"])
             for p in group["params"]:
-                if p.grad is None:
+                if p.grad is None or id(p) in skip:
                     continue
                 g = p.grad
                 if g.is_sparse:
@@ -82,8 +104,58 @@ class GaussianAdam(torch.optim.Optimizer):
                 chunk = groups[i:i + _MAX_GROUPS]
                 arr = (_native.AdamGroup * len(chunk))(*chunk)
                 _native.check(lib.gsr_adam_step(arr, len(chunk), b1, b2, eps, stream), "gsr_adam_step")
+        if fused is not None:
+            a, (b1, b2, eps), dev = fused
+            lib = _native.load()
+            _native.check(lib.gsr_adam_sh_views_step(ctypes.byref(a), b1, b2, eps, _stream_handle(dev)),
+                          "gsr_adam_sh_views_step")
         del keep_alive
         return loss
+
+    def _sh_views_args(self, dc: torch.Tensor, rest: torch.Tensor, grad: ShViewsGradient):
+        groups = {}
+        for group in self.param_groups:
+            for p in group["params"]:
+                groups[id(p)] = group
+        P = dc.shape[0]
+        # either two packed tensors, or the column blocks [:, :1] and [:, 1:] of ONE contiguous (P, 16, 3) tensor
+        joint = (not dc.is_contiguous() and dc.stride() == (48, 3, 1) and rest.stride() == (48, 3, 1)
+                 and rest.data_ptr() == dc.data_ptr() + 12)
+        for t, name, width in ((dc, "features_dc", 1), (rest, "features_rest", 15)):
+            if id(t) not in groups:
+                raise RuntimeError(f"sh_views: {name} is not a parameter of this optimizer")
+            if t.dtype != torch.float32 or t.device.type != "cuda" or not (joint or t.is_contiguous()) or \
+                    tuple(t.shape) != (P, width, 3):
+                raise RuntimeError(f"sh_views: {name} must be a contiguous fp32 ({P}, {width}, 3) GPU tensor (or "
+                                   "both the [:, :1] / [:, 1:] blocks of one contiguous (P, 16, 3) tensor)")
+        gd, gr = groups[id(dc)], groups[id(rest)]
+        if gd["betas"] != gr["betas"] or gd["eps"] != gr["eps"]:
+            raise RuntimeError("sh_views: features_dc and features_rest must share betas and eps")
+        V = grad.campos.shape[0]
+        for t in (grad.means3D, grad.campos, grad.factors):
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.device != dc.device:
+                raise RuntimeError("sh_views: means3D, campos and factors must be contiguous fp32 on the parameters' "
+                                   "device")
+        if grad.means3D.shape != (P, 3) or grad.factors.numel() != V * P * 3:
+            raise RuntimeError("sh_views: means3D (P, 3) and factors (V * P * 3) do not match the parameters")
+        steps = []
+        for t in (dc, rest):
+            state = self.state[t]
+            if len(state) == 0:
+                state["step"] = torch.tensor(0.0, dtype=torch.float32)
+                state["exp_avg"] = torch.zeros_like(t, memory_format=torch.contiguous_format)
+                state["exp_avg_sq"] = torch.zeros_like(t, memory_format=torch.contiguous_format)
+            state["step"] += 1
+            steps.append(int(state["step"].item()))
+        sd, sr = self.state[dc], self.state[rest]
+        a = _native.AdamShViewsArgs(
+            P=P, D=int(grad.sh_degree), M=16, V=V, chunk_len=int(grad.chunk_len), means3D=grad.means3D.data_ptr(),
+            campos=grad.campos.data_ptr(), dL_dcolors_sh=grad.factors.data_ptr(),
+            dc_param=dc.data_ptr(), dc_exp_avg=sd["exp_avg"].data_ptr(), dc_exp_avg_sq=sd["exp_avg_sq"].data_ptr(),
+            dc_lr=float(gd["lr"]), dc_step=steps[0], rest_param=rest.data_ptr(), rest_exp_avg=sr["exp_avg"].data_ptr(),
+            rest_exp_avg_sq=sr["exp_avg_sq"].data_ptr(), rest_lr=float(gr["lr"]), rest_step=steps[1],
+            param_row_stride=48 if joint else 0)
+        return a, (float(gd["betas"][0]), float(gd["betas"][1]), float(gd["eps"])), dc.device
 
 
 class SparseGaussianAdam(torch.optim.Adam):

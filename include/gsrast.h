@@ -194,6 +194,29 @@ typedef struct gsr_adam_group {
 } gsr_adam_group;
 int gsr_adam_step(const gsr_adam_group *groups, int num_groups, double beta1, double beta2, double eps, void *stream);
 
+/* Fused Adam step of the two SH parameter groups of a multi-view (one view per GPU) step, on the gradient that
+ * gsr_sh_backward_views_chunked would expand -- sum_v basis(dir_v) (x) dL_dcolors_sh_v -- formed inside the update, so
+ * the (P, M, 3) gradient is never written: features_dc (P, 1, 3) and features_rest (P, M - 1, 3) with their Adam
+ * moments, updated in place with gsr_adam_step's arithmetic (each group with its own lr and 1-based step).  The
+ * result is bitwise that of the expansion followed by gsr_adam_step.  M must be 16; V, chunk_len, means3D, campos and
+ * dL_dcolors_sh as for gsr_sh_backward_views_chunked. */
+typedef struct gsr_adam_sh_views_args {
+    int P, D, M, V;
+    int64_t chunk_len;
+    const float *means3D, *campos, *dL_dcolors_sh;
+    float *dc_param, *dc_exp_avg, *dc_exp_avg_sq;
+    double dc_lr;
+    int64_t dc_step;
+    float *rest_param, *rest_exp_avg, *rest_exp_avg_sq;
+    double rest_lr;
+    int64_t rest_step;
+    /* floats between consecutive Gaussians' rows of each parameter: 0 = packed ((P, 1, 3) / (P, M - 1, 3) tensors);
+     * 48 = the two groups are the column blocks of ONE (P, 16, 3) tensor (dc_param = its base, rest_param = base + 3),
+     * which the forward reads as shs without a concatenation.  The moments are always packed. */
+    int64_t param_row_stride;
+} gsr_adam_sh_views_args;
+int gsr_adam_sh_views_step(const gsr_adam_sh_views_args *a, double beta1, double beta2, double eps, void *stream);
+
 /* SparseGaussianAdam.step(visibility, N) of the upstream rasterizer package (diff_gaussian_rasterization, taken by
  * the reference's third_party GaussianModel with optimizer_type "sparse_adam": gaussian_model.py:26,194-196).  Each
  * group's n elements are N Gaussians of n / N elements; only the Gaussians with visible[g] != 0 are updated, as

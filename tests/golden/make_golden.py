@@ -65,7 +65,9 @@ def _import_reference():
     return R, RR
 
 
-def reference_fwd_bwd(R, RR, scene, cam, bg, dcolor, dinv, scale_modifier=1.0, backward=True):
+def reference_fwd_bwd(R, RR, scene, cam, bg, dcolor, dinv, scale_modifier=1.0, backward=True, upstream_fn=None):
+    """upstream_fn(color, invdepth) -> (dcolor, dinv): upstream gradients formed from the forward's outputs (numpy),
+    in place of the fixed dcolor / dinv."""
     N = scene.means3D.shape[0]
     M = scene.shs.shape[1]
     means = scene.means3D.clone().requires_grad_(backward)
@@ -88,6 +90,9 @@ def reference_fwd_bwd(R, RR, scene, cam, bg, dcolor, dinv, scale_modifier=1.0, b
     out = dict(color=img.detach().numpy(), radii=radius.detach().numpy().astype(np.int32),
                invdepth=depth.detach().numpy())
     if backward:
+        if upstream_fn is not None:
+            dcolor, dinv = upstream_fn(out["color"], out["invdepth"])
+            out.update(dL_dcolor=dcolor.numpy(), dL_dinvdepth=dinv.numpy())
         loss = (img * dcolor).sum() + (depth * dinv).sum()
         loss.backward()
         W, H = cam.image_width, cam.image_height

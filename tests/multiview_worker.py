@@ -39,7 +39,7 @@ def oracle_sh_views(means3D, campos, dcolors_sh, sh_degree, M, out, chunk_len=0)
     return out
 
 
-def worker(rank, world, port, mode, result_dir, chunks=1, expand="chunk"):
+def worker(rank, world, port, mode, result_dir, chunks=1, expand="chunk", expand_sh=True):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -61,15 +61,21 @@ def worker(rank, world, port, mode, result_dir, chunks=1, expand="chunk"):
         red.means2D.copy_(torch.from_numpy(g["means2D"]))
         if red.chunks == 1:
             fill(red.backward_out(), 0, N)
-            red.reduce(means3D, torch.from_numpy(g["campos"]))
+            red.reduce(means3D, torch.from_numpy(g["campos"]), expand_sh=expand_sh)
         else:  # the overlapped form: each chunk's exchange starts as soon as its gradients exist
             red.begin_step(torch.from_numpy(g["campos"]))
             for c, (g0, g1, out) in enumerate(red.chunk_outputs()):
                 fill(out, g0, g1)
                 red.start_chunk(c)
-            red.finish(means3D)
+            red.finish(means3D, expand_sh=expand_sh)
         red.record_view(red.means2D, torch.from_numpy(g["radii"]))
-        res = {k: v.numpy() for k, v in red.grads.items()}
+        grads = red.grads
+        if not expand_sh:  # the factored form GaussianAdam.step(sh_views=...) consumes, expanded here by the oracle
+            assert grads["shs"] is None
+            f = red.sh_views_gradient(means3D)
+            grads["shs"] = oracle_sh_views(f.means3D, f.campos, f.factors, f.sh_degree, 16, torch.zeros(N, 16, 3),
+                                           f.chunk_len)
+        res = {k: v.numpy() for k, v in grads.items()}
         stats, radii_max = red.sync_densify_stats()
         res["stats"] = stats.numpy()
         res["radii_max"] = radii_max.numpy()

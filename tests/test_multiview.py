@@ -31,12 +31,13 @@ def expected():
     return exp
 
 
-def _run(tmp_path, mode, chunks, world=2, expand="chunk"):
+def _run(tmp_path, mode, chunks, world=2, expand="chunk", expand_sh=True):
     ctx = mp.get_context("spawn")
     port = _free_port()
-    d = os.path.join(str(tmp_path), f"{mode}_{chunks}_{expand}")
+    d = os.path.join(str(tmp_path), f"{mode}_{chunks}_{expand}_{expand_sh}")
     os.makedirs(d, exist_ok=True)
-    procs = [ctx.Process(target=MW.worker, args=(r, world, port, mode, d, chunks, expand)) for r in range(world)]
+    procs = [ctx.Process(target=MW.worker, args=(r, world, port, mode, d, chunks, expand, expand_sh))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -78,6 +79,18 @@ def test_chunked_exchange_is_bitwise_the_unchunked_one(tmp_path, mode):
         for r in range(2):
             for k in ("means3D", "scales", "rotations", "opacities", "stats", "radii_max", "shs"):
                 assert np.array_equal(one[r][k], once[r][k]), (r, k)
+
+
+@pytest.mark.parametrize("chunks", [1, 4])
+def test_factored_sh_gradient_is_the_expanded_one(tmp_path, chunks):
+    """finish(expand_sh=False): no expansion on the ranks; the factored SH gradient the fused Adam consumes
+    (sh_views_gradient: every rank's colour factors in the chunk-major gather buffer, every rank's camera) expands to
+    exactly what the expanding exchange produced, on every rank."""
+    ref = _run(tmp_path, "compact", chunks)
+    fac = _run(tmp_path, "compact", chunks, expand_sh=False)
+    for r in range(2):
+        for k in ("means3D", "scales", "rotations", "opacities", "stats", "radii_max", "shs"):
+            assert np.array_equal(ref[r][k], fac[r][k]), (r, k)
 
 
 def test_exchange_plan_cost_model():

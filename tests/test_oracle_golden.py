@@ -101,3 +101,17 @@ def test_oracle_cfg1_backward_against_reference_autograd():
     g = run.backward(z["dL_dcolor"], z["dL_dinvdepth"])
     for k in ("means3D", "means2D", "opacities", "scales", "rotations", "shs"):
         assert rel_l2(g[k], z["ref_grad_" + k]) <= 2e-3, k
+
+
+@pytest.mark.parametrize("name", ["ref_sat_sh3_20k_white", "ref_cfg2_100k_800_sh3"])
+def test_oracle_saturated_sh3_against_reference(name):
+    """Saturated SH-3 scenes (BASELINE config 2 and a white-background mini scene) against the reference Python
+    rasterizer's own outputs and autograd gradients (tests/golden/make_golden_ref.py): A13's tolerances on the
+    pixels the CUDA and Python compositing rules share, the A2/A3 transmittance bound on every other pixel."""
+    from tests.helpers import compare_to_reference, load_ref_golden
+    z = load_ref_golden(name)
+    color, radii, invd, run = run_oracle(z["inp"])
+    ft, _ = run.image_state()
+    g = run.backward(z["dL_dcolor"], z["dL_dinvdepth"])
+    rgb_max = float(np.abs(run.geom()["rgb"][radii > 0]).max())
+    compare_to_reference(z, color, invd, radii, ft, rgb_max, run.threshold_margin(), g)

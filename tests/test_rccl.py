@@ -16,10 +16,10 @@ from tests.helpers import scene_inputs, settings_for, upstream
 pytestmark = pytest.mark.gpu
 
 
-def _step(red, st, rs, dc, di, means3D, chunked):
+def _step(red, st, rs, dc, di, means3D, chunked, early=True):
     from gaussian_splatting_lightning_amd.rasterizer import backward_chunked, backward_raw
-    if chunked:
-        red.begin_step()
+    if chunked:  # early: SH expansions queued on the side stream behind each group (begin_step(means3D=...))
+        red.begin_step(means3D=means3D if early else None)
         backward_chunked(st, rs, dc, di, red.chunk_outputs(), on_chunk=red.start_chunk, compact_sh=red.compact,
                          accumulate_stats=True)
         red.finish(means3D)
@@ -28,7 +28,7 @@ def _step(red, st, rs, dc, di, means3D, chunked):
         red.reduce(means3D)
 
 
-def _run(dev, distributed, mode, chunks, views=2, **kw):
+def _run(dev, distributed, mode, chunks, views=2, early=True, **kw):
     from gaussian_splatting_lightning_amd.multiview import ViewGradReducer
     from gaussian_splatting_lightning_amd.rasterizer import forward_raw
     n, W, H = 30_000, 320, 240
@@ -41,7 +41,7 @@ def _run(dev, distributed, mode, chunks, views=2, **kw):
         dc, di = (torch.as_tensor(a, device=dev) for a in upstream(W, H, seed=12 + v))
         _, radii, _, st = forward_raw(t["means3D"], t["shs"], None, t["opacities"], t["scales"], t["rotations"],
                                       None, rs)
-        _step(red, st, rs, dc, di, t["means3D"], chunks > 1)
+        _step(red, st, rs, dc, di, t["means3D"], chunks > 1, early)
     torch.cuda.synchronize()
     grads = {k: g.clone() for k, g in red.grads.items()}
     stats, rmax = red.sync_densify_stats()
@@ -53,6 +53,8 @@ VARIANTS = [  # (mode, chunks, reducer options): one RCCL group per chunk unless
     ("compact", 4, {}), ("compact", 4, dict(expand="once")), ("dense", 4, {}), ("compact", 1, {}), ("dense", 1, {}),
     ("compact", 4, dict(coalesce=False)), ("compact", 1, dict(sync_ops=False)), ("dense", 1, dict(coalesce=False)),
     ("compact", 4, dict(comm_stream="pg")), ("compact", 2, dict(comm_stream="side", expand="once")),
+    ("compact", 4, dict(expand="side")),  # each chunk's expansion on the side stream behind its group
+    ("compact", 2, dict(expand="side", early=False)),  # "side" without means3D at begin_step: expands in finish()
 ]
 
 
@@ -66,6 +68,8 @@ def test_rccl_exchange_one_rank_is_bitwise_local(gpu_device, mode, chunks, kw):
         got = _run(gpu_device, True, mode, chunks, **kw)
         red = got[3]
         assert red.coalesce == kw.get("coalesce", True)  # the grouped path really ran (no fallback)
+        if kw.get("expand") == "side" and kw.get("early", True):
+            assert red._expanded == set(range(red.chunks))  # the expansions ran on the side stream
         # the RCCL branch really ran: the chunk gathers landed in the (world, L, 3) buffers
         if mode == "compact":
             for c in range(red.chunks):

@@ -50,7 +50,7 @@ def main():
                 backward_raw(st, rs, dc, di, **red.backward_kwargs())
                 red.reduce(sc.means3D)
             else:
-                red.begin_step()
+                red.begin_step(means3D=sc.means3D)
                 backward_chunked(st, rs, dc, di, red.chunk_outputs(), on_chunk=red.start_chunk,
                                  compact_sh=red.compact, accumulate_stats=True)
                 red.finish(sc.means3D)
