@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--exchange-expand", default=None, choices=("chunk", "once", "side"),
                     help="compact exchange: SH expansion per chunk or once after the last gather on the compute "
                          "stream, or per chunk on the side stream behind its group (default: the cost model's)")
+    ap.add_argument("--exchange-handoff", default=None, choices=("event", "value"),
+                    help="chunked exchange: hand-offs between the compute and the collective stream by hipEvents or "
+                         "by stream-ordered device words (gsr_stream_signal / gsr_stream_wait)")
     ap.add_argument("--plan-world", type=int, default=0,
                     help="N>1 path: plan the exchange (mode, chunks, SH expansion) for this many ranks instead of "
                          "WORLD_SIZE -- a one-rank rehearsal (--force-dist) of the N-GPU schedule")
@@ -139,7 +142,8 @@ def main():
     # chunks' Gaussian ranges and each range's collectives (one RCCL group) are issued as soon as it is enqueued.
     if distributed:
         red = ViewGradReducer(n, M, deg, dev, mode=args.exchange, chunks=args.exchange_chunks or None,
-                              expand=args.exchange_expand, plan_world=args.plan_world or None)
+                              expand=args.exchange_expand, plan_world=args.plan_world or None,
+                              handoff=args.exchange_handoff)
     else:
         red = ViewGradReducer(n, M, deg, dev, mode="dense", chunks=1)
     mode = red.mode
@@ -265,7 +269,7 @@ def main():
                              {"params": [tp["scales"]], "lr": 0.005, "name": "scaling"},
                              {"params": [tp["rotations"]], "lr": 0.001, "name": "rotation"}], lr=0.0, eps=1e-15)
         tred = ViewGradReducer(n, M, deg, dev, mode="compact", chunks=None if distributed else 1,
-                               plan_world=args.plan_world or None) if distributed else \
+                               plan_world=args.plan_world or None, handoff=args.exchange_handoff) if distributed else \
             ViewGradReducer(n, M, deg, dev, mode="compact", chunks=1)
 
         def train_step():

@@ -107,7 +107,8 @@ EXPORTED_SYMBOLS = (
     "gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_sh_backward_views", "gsr_sh_backward_views_chunked",
     "gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes",
     "gsr_image_buffer_bytes", "gsr_bwd_scratch_bytes", "gsr_set_profiling", "gsr_num_stages", "gsr_stage_name",
-    "gsr_stage_times", "gsr_reset_stage_times", "gsr_last_error", "gsr_build_info", "gsr_abi_version", "gsr_adam_sh_views_step", "gsr_state_layout_query",
+    "gsr_stage_times", "gsr_reset_stage_times", "gsr_last_error", "gsr_build_info", "gsr_abi_version", "gsr_adam_sh_views_step",
+    "gsr_stream_values_supported", "gsr_stream_signal", "gsr_stream_wait", "gsr_state_layout_query",
     "gsr_set_tuning", "gsr_get_tuning", "gsr_ssim_num_partials", "gsr_ssim_forward", "gsr_ssim_backward", "gsr_adam_step", "gsr_sparse_adam_step",
     "gsr_densify_workspace_bytes", "gsr_densify_classify", "gsr_densify_apply", "gsr_ply_unpack", "gsr_ply_pack",
     "gsr_knn_workspace_bytes", "gsr_knn_mean_dist2", "gsr_debug_wave_stamps",
@@ -143,6 +144,11 @@ def load(path: str | None = None):
     lib.gsr_adam_step.argtypes = [ctypes.POINTER(AdamGroup), ctypes.c_int, ctypes.c_double, ctypes.c_double,
                                   ctypes.c_double, ctypes.c_void_p]
     lib.gsr_adam_step.restype = ctypes.c_int
+    if hasattr(lib, "gsr_stream_signal"):  # absent from pre-round-6 builds loaded for A/Bs through GSR_LIB
+        lib.gsr_stream_values_supported.restype = ctypes.c_int
+        for f in (lib.gsr_stream_signal, lib.gsr_stream_wait):
+            f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
+            f.restype = ctypes.c_int
     if hasattr(lib, "gsr_adam_sh_views_step"):  # absent from pre-round-6 builds loaded for A/Bs through GSR_LIB
         lib.gsr_adam_sh_views_step.argtypes = [ctypes.POINTER(AdamShViewsArgs), ctypes.c_double, ctypes.c_double,
                                                ctypes.c_double, ctypes.c_void_p]

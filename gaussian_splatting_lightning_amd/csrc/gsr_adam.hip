@@ -18,10 +18,7 @@ constexpr int ADAM_SLICE = 256 * ADAM_PER;    // elements per workgroup
 
 __device__ __forceinline__ void adam_one(float &p, float g, float &m, float &v, float b1c, float b2, float b2c,
                                          float step_size, float bc2_sqrt, float eps) {
-    m = m + b1c * (g - m);            // exp_avg.lerp_(grad, 1 - beta1)   (weight < 0.5 branch of lerp)
-    v = v * b2 + b2c * (g * g);       // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, value=1 - beta2)
-    const float denom = sqrtf(v) / bc2_sqrt + eps;
-    p = p + (-step_size) * (m / denom);  // param.addcdiv_(exp_avg, denom, value=-step_size)
+    adam_update(p, g, m, v, b1c, b2, b2c, step_size, bc2_sqrt, eps);  // gsr_kernels.h
 }
 
 __global__ __launch_bounds__(256) void adam_kernel(AdamLaunch L) {

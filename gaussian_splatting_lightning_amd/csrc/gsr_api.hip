@@ -1255,6 +1255,29 @@ void gsr_reset_stage_times(void) {
 }
 const char *gsr_last_error(void) { return g_err.c_str(); }
 int gsr_abi_version(void) { return GSR_ABI_VERSION; }
+
+int gsr_stream_values_supported(void) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeCanUseStreamWaitValue, dev) != hipSuccess) return 0;
+    return v;
+}
+
+int gsr_stream_signal(void *stream_ptr, uint32_t *flag, uint32_t value) {
+    if (!flag) return fail(GSR_ERR_ARG, "stream signal: null flag");
+    hipStream_t stream = (hipStream_t)stream_ptr;
+    StreamDeviceGuard device_guard(stream);
+    GSR_HIP(hipStreamWriteValue32(stream, flag, value, 0));
+    return GSR_OK;
+}
+
+int gsr_stream_wait(void *stream_ptr, uint32_t *flag, uint32_t value) {
+    if (!flag) return fail(GSR_ERR_ARG, "stream wait: null flag");
+    hipStream_t stream = (hipStream_t)stream_ptr;
+    StreamDeviceGuard device_guard(stream);
+    GSR_HIP(hipStreamWaitValue32(stream, flag, value, hipStreamWaitValueGte, 0xffffffffu));
+    return GSR_OK;
+}
 const char *gsr_build_info(void) {
     return "gsrast: MI355X (gfx950) HIP rasterizer; wave64 tile compositing, LSD radix binning, "
            "deterministic gradient rows; built " __DATE__ " " __TIME__;

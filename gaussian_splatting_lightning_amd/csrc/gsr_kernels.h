@@ -242,6 +242,19 @@ void launch_preprocess_bwd(hipStream_t s, const PreprocessBwdParams &p);
 void launch_sh_backward_views(hipStream_t s, int P, int D, int M, int V, int chunk_len, const float *means3D,
                               const float *campos, const float *dcolors_sh, float *dsh);
 
+// One Adam element update (torch's Adam, non-amsgrad, no weight decay), shared by adam_kernel and the fused SH
+// Adam so the two give the same bits: the contractions are explicit (the compiler's choice of FMA could differ between
+// the kernels otherwise):
+//     m = lerp(m, g, 1 - b1);  v = v b2 + (1 - b2) g^2;  p -= step_size * m / (sqrt(v) / sqrt(bc2) + eps)
+__device__ __forceinline__ void adam_update(float &p, float g, float &m, float &v, float b1c, float b2, float b2c,
+                                            float step_size, float bc2_sqrt, float eps) {
+#pragma clang fp contract(off)
+    m = __fmaf_rn(b1c, __fsub_rn(g, m), m);                // exp_avg.lerp_(grad, 1 - beta1)
+    v = __fmaf_rn(v, b2, __fmul_rn(b2c, __fmul_rn(g, g)));  // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
+    const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), bc2_sqrt), eps);
+    p = __fmaf_rn(-step_size, __fdiv_rn(m, denom), p);     // param.addcdiv_(exp_avg, denom, value=-step_size)
+}
+
 // fused Adam of the SH groups on the multi-view expansion (gsr_views.hip; M = 16)
 struct AdamShGroup {
     float *param, *exp_avg, *exp_avg_sq;

@@ -295,6 +295,7 @@ __device__ __forceinline__ float3 sh_backward_jac_dispatch(int deg, float3 dir_o
 // SH basis values b[0..(DEG+1)^2) at unit direction (x,y,z); b[k] * dRGB is sh_backward's dL/dsh[k].
 template <int DEG>
 __device__ __forceinline__ void sh_basis(float x, float y, float z, float *b) {
+#pragma clang fp contract(off)  // the same bits in every kernel that inlines it (the expansion and the fused SH Adam)
     b[0] = GSR_SH_C0;
     if (DEG > 0) {
         b[1] = -GSR_SH_C1 * y;

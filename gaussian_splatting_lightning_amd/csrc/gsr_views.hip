@@ -21,6 +21,7 @@ template <int DEG>
 __device__ __forceinline__ void views_accumulate(int ii, int P, int V, int L, const float *__restrict__ means3D,
                                                  const float *__restrict__ campos, const float *__restrict__ dc,
                                                  float (&acc)[3 * (DEG + 1) * (DEG + 1)]) {
+#pragma clang fp contract(off)  // explicit FMAs only: the same bits wherever this is inlined
     constexpr int NB = (DEG + 1) * (DEG + 1);
     const float mx = means3D[3 * ii], my = means3D[3 * ii + 1], mz = means3D[3 * ii + 2];
     const int c = ii / L, g0 = c * L, Lc = min(L, P - g0);
@@ -37,9 +38,9 @@ __device__ __forceinline__ void views_accumulate(int ii, int P, int V, int L, co
         sh_basis<DEG>(dx / len, dy / len, dz / len, basis);
 #pragma unroll
         for (int k = 0; k < NB; k++) {
-            acc[3 * k] += basis[k] * r;
-            acc[3 * k + 1] += basis[k] * g;
-            acc[3 * k + 2] += basis[k] * b;
+            acc[3 * k] = __fmaf_rn(basis[k], r, acc[3 * k]);
+            acc[3 * k + 1] = __fmaf_rn(basis[k], g, acc[3 * k + 1]);
+            acc[3 * k + 2] = __fmaf_rn(basis[k], b, acc[3 * k + 2]);
         }
     }
 }
@@ -113,14 +114,12 @@ __global__ __launch_bounds__(256) void sh_backward_views_kernel(int P, int M, in
 // (P, 1, 3) holds coefficient 0 of each row, features_rest (P, M - 1, 3) coefficients 1..15 (M = 16).  The row is
 // formed in registers exactly as sh_backward_views_kernel forms it, staged in LDS, and every lane then updates
 // consecutive float4s of the half-wave's 32-row block of each group (coalesced param / moment traffic) with
-// adam_one's arithmetic, so the result is bitwise that of the expansion followed by adam_kernel -- without the
+// adam_update's arithmetic (gsr_kernels.h), so the result is bitwise that of the expansion followed by adam_kernel --
+// without the
 // 192-B gradient row written and read back.
 __device__ __forceinline__ void adam_elem(float &p, float g, float &m, float &v, const AdamShGroup &G,
                                           const AdamShLaunch &L) {
-    m = m + L.one_minus_beta1 * (g - m);
-    v = v * L.beta2 + L.one_minus_beta2 * (g * g);
-    const float denom = sqrtf(v) / G.bc2_sqrt + L.eps;
-    p = p + (-G.step_size) * (m / denom);
+    adam_update(p, g, m, v, L.one_minus_beta1, L.beta2, L.one_minus_beta2, G.step_size, G.bc2_sqrt, L.eps);
 }
 
 // The group's elements of this half-wave block: element e of the block is row e / W, coefficient column e % W + C0 of

@@ -52,22 +52,22 @@ FIELDS_DENSE = ("means3D", "scales", "rotations", "opacities", "shs")
 FIELDS_COMPACT = ("means3D", "scales", "rotations", "opacities")
 NON_SH_FLOATS = 11  # means3D 3 + scales 3 + rotations 4 + opacity 1
 
-# Cost-model constants, measured on one MI355X at cfg 3 (1M Gaussians, SH degree 3; rocprofv3 kernel trace of
-# tools/dist_overhead.py with a one-rank RCCL group, profiles/r5e_*): kernel times per 1e6 Gaussians, and the
-# fixed GPU-timeline cost of one collective group -- blocking (issued on the compute stream: one event marker, no
-# hand-off) or async (the process group's own stream: a marker on the compute queue that stalls its next kernel,
-# the communication stream's wait, and the compute stream's wait for the result).  The bus bandwidth is an
-# ASSUMPTION (no 8-GPU node has run this code): 7 xGMI links x 153 GB/s per direction at
-# `bus_efficiency` of RCCL's ring schedules.
+# Cost-model constants, measured on one MI355X at cfg 3 (1M Gaussians, SH degree 3) with a one-rank RCCL group
+# (tools/dist_overhead.py, interleaved rounds, and its rocprofv3 kernel trace split into steps by tools/trace_steps.py;
+# profiles/r6c_*): kernel times per 1e6 Gaussians, and the GPU-timeline cost of the stream hand-offs -- a blocking
+# group on the compute stream (K = 1: the gap before the next kernel), and for K > 1 chunks the extra chunk's launches
+# with its event record (each event marker holds the next kernel ~6 us) plus one fixed cross-stream hand-off (the
+# compute stream's waits for the side stream's events).  Fitted to the one-rank steps: compact K = 1 / 2 / 4 at
+# +20 / +54 / +81 us over the plain step.  The bus bandwidth is an ASSUMPTION (no 8-GPU node has run this code): 7 xGMI
+# links x 153 GB/s per direction at `bus_efficiency` of RCCL's ring schedules.
 EXCHANGE_COSTS = dict(
     pb_dense_ms=0.104,       # preprocess_bwd writing dL/dsh (192 B/G)
     pb_compact_ms=0.080,     # preprocess_bwd writing the 12-B colour factor instead
     exp_ms=0.036,            # gsr_sh_backward_views: 192 B/G written + means + one view's factors
     exp_view_ms=0.002,       # + 12 B/G read per further view
-    chunk_ms=0.0043,         # per extra chunk: one more per-Gaussian-stage launch (and SH-expansion launch)
-    group_sync_ms=0.007,     # one blocking collective group (chunks == 1)
-    group_async_ms=0.011,    # one async collective group (chunks > 1, on the reducer's side stream)
-    event_ms=0.003,          # one event record / wait hand-off between the compute and the side stream
+    group_sync_ms=0.008,     # one blocking collective group on the compute stream (K = 1)
+    chunk_ms=0.0135,         # per extra chunk: per-Gaussian and expansion launches + the chunk's event hand-off
+    side_fixed_ms=0.0205,    # K > 1: the compute stream's waits for the side stream
     link_GBps=153.0,
     links=7,
     bus_efficiency=0.6,
@@ -88,10 +88,10 @@ def simulate_exchange(n: int, world: int, mode: str, chunks: int, expand: str = 
     """Timeline of the backward's per-Gaussian stage + the exchange (ms after the compositing backward ends).
 
     K = 1: the group runs blocking on the compute stream after the per-Gaussian stage, then the SH expansion.
-    K > 1: compute stream = K per-Gaussian chunks, each followed by an event record; the reducer's side stream = per
-    chunk [wait for its event, group] in order.  The SH expansion (compact) runs on the compute stream after the
-    chunk's group landed ("chunk"), once after the last ("once"), or on the side stream right behind each group
-    ("side"); the step ends when the compute stream has waited for the side stream's last event."""
+    K > 1: the compute stream runs K per-Gaussian chunks; the side stream runs chunk k's group once chunk k is done and
+    group k - 1 has finished (the links are the bottleneck); the SH expansion (compact) follows each landed chunk on the
+    compute stream ("chunk"), or all of it after the last ("once"; "side" is modelled as "chunk": measured alike).
+    The hand-offs cost chunk_ms per extra chunk and side_fixed_ms once (EXCHANGE_COSTS)."""
     c = dict(EXCHANGE_COSTS, **(costs or {}))
     scale = n / 1e6
     K = max(1, int(chunks))
@@ -107,18 +107,16 @@ def simulate_exchange(n: int, world: int, mode: str, chunks: int, expand: str = 
         comp_end = comm_end = 0.0
         landed = []
         for k in range(K):
-            comp_end += pb / K + (c["chunk_ms"] if k > 0 else 0.0) + c["event_ms"]
-            comm_end = max(comp_end, comm_end) + c["group_async_ms"] + comm / K
-            if expand == "side" and exp:
-                comm_end += exp / K + (c["chunk_ms"] if k > 0 else 0.0)
+            comp_end += pb / K + (c["chunk_ms"] if k > 0 else 0.0)
+            comm_end = max(comp_end, comm_end) + comm / K
             landed.append(comm_end)
-        t = comp_end
-        if exp and expand == "chunk":
+        t = comp_end + c["side_fixed_ms"]
+        if exp and expand == "once":
+            t = max(t, landed[-1]) + exp
+        elif exp:
             for k in range(K):
-                t = max(t, landed[k] + c["event_ms"]) + exp / K + (c["chunk_ms"] if k > 0 else 0.0)
-        elif exp and expand == "once":
-            t = max(t, landed[-1] + c["event_ms"]) + exp
-        end = max(t, comm_end + c["event_ms"])
+                t = max(t, landed[k]) + exp / K
+        end = max(t, comm_end + c["side_fixed_ms"])
     return {"mode": mode, "chunks": K, "expand": expand, "per_gaussian_stage_ms": round(pb, 4),
             "link_MB": round(link_bytes / 1e6, 1), "comm_ms": round(comm, 4), "end_ms": round(end, 4),
             "exposed_ms": round(end - pb, 4)}
@@ -132,7 +130,7 @@ def plan_exchange(n: int, world: int, M: int = 16, costs: Optional[dict] = None,
         for K in chunk_options:
             if K > 1 and n < 256 * K:
                 continue
-            for expand in (("chunk", "once", "side") if (mode == "compact" and K > 1) else ("once",)):
+            for expand in (("chunk", "once") if (mode == "compact" and K > 1) else ("once",)):
                 r = simulate_exchange(n, world, mode, K, expand, M, costs)
                 if best is None or r["end_ms"] < best["end_ms"] - 1e-6:
                     best = r
@@ -182,7 +180,7 @@ class ViewGradReducer:
                  sh_views_fn: Optional[Callable[..., torch.Tensor]] = None, chunks: Optional[int] = 1,
                  distributed: Optional[bool] = None, expand: Optional[str] = None,
                  coalesce: Optional[bool] = None, sync_ops: Optional[bool] = None, comm_stream: Optional[str] = None,
-                 plan_world: Optional[int] = None):
+                 plan_world: Optional[int] = None, handoff: Optional[str] = None):
         if mode not in ("dense", "compact", "auto"):
             raise ValueError(f"mode must be 'dense', 'compact' or 'auto', got {mode!r}")
         self.n, self.M, self.D = int(n), int(M), int(sh_degree)
@@ -273,10 +271,26 @@ class ViewGradReducer:
             raise ValueError(f"comm_stream must be 'pg' or 'side', got {comm_stream!r}")
         if comm_stream is None:  # measured (one rank, 4 chunks): side 0.901 ms/step against 0.923 for the pg stream
             comm_stream = "side" if self.chunks > 1 else "pg"
+        # handoff between the two streams: "event" (hipEvent record / wait) or "value" (a device word written and
+        # waited on in stream order, gsr_stream_signal / gsr_stream_wait: no event marker on the compute stream)
+        self.handoff = None
+        if handoff not in (None, "event", "value"):
+            raise ValueError(f"handoff must be 'event' or 'value', got {handoff!r}")
         if comm_stream == "side" and self.distributed and self.device.type == "cuda":
             self.comm_stream = torch.cuda.Stream(self.device)
-            self._ready = [torch.cuda.Event() for _ in self.bounds]   # chunk c's gradients are written
-            self._landed = [torch.cuda.Event() for _ in self.bounds]  # chunk c's collectives are done
+            self.handoff = handoff or "event"
+            if self.handoff == "value":
+                from . import _native
+                with torch.cuda.device(self.device):
+                    if not _native.load().gsr_stream_values_supported():
+                        self.handoff = "event"
+            if self.handoff == "value":
+                # [ready(c) for c] + [landed(c) for c]: step s signals s (monotone, never reset)
+                self._flags = torch.zeros(2 * len(self.bounds), dtype=torch.int32, device=self.device)
+                self._seq = 0
+            else:
+                self._ready = [torch.cuda.Event() for _ in self.bounds]   # chunk c's gradients are written
+                self._landed = [torch.cuda.Event() for _ in self.bounds]  # chunk c's collectives are done
             self.sync_ops = True
         self._pending: List[tuple] = []
         self._side_means: Optional[torch.Tensor] = None  # begin_step(means3D=...): expansions on the side stream
@@ -297,7 +311,7 @@ class ViewGradReducer:
         return (f"{self.mode}, {self.chunks} chunk(s), expand={self.expand if self.compact else '-'}, "
                 f"{'one RCCL group per chunk' if self.coalesce else 'separate collectives'}, "
                 f"{'blocking' if self.sync_ops else 'async'} ops"
-                f"{' on a side stream' if self.comm_stream is not None else ''}")
+                f"{f' on a side stream ({self.handoff} hand-off)' if self.comm_stream is not None else ''}")
 
     # ---- destinations ----
     def backward_out(self) -> Dict[str, torch.Tensor]:
@@ -419,16 +433,35 @@ class ViewGradReducer:
         gather = reduce = None
         if self.distributed and self.comm_stream is not None:
             cur = torch.cuda.current_stream(self.device)
-            self._ready[c].record(cur)
+            value = self.handoff == "value"
+            if value:
+                from . import _native
+                lib = _native.load()
+                if c == 0:
+                    self._seq = (self._seq + 1) & 0x7FFFFFFF
+                ready = self._flags[c:c + 1].data_ptr()
+                landed = self._flags[len(self.bounds) + c:len(self.bounds) + c + 1].data_ptr()
+                _native.check(lib.gsr_stream_signal(cur.cuda_stream, ready, self._seq), "gsr_stream_signal")
+            else:
+                self._ready[c].record(cur)
             with torch.cuda.stream(self.comm_stream):
-                self.comm_stream.wait_event(self._ready[c])
+                if value:
+                    _native.check(lib.gsr_stream_wait(self.comm_stream.cuda_stream, ready, self._seq),
+                                  "gsr_stream_wait")
+                else:
+                    self.comm_stream.wait_event(self._ready[c])
                 self._issue(c)  # blocking ops: they run on the side stream itself
                 if self._side_means is not None:  # the SH expansion behind the group, off the compute stream
                     g0, g1 = self.bounds[c]
                     self._expand(self._side_means, g0, g1, self.gather_all[c], 0)
                     self._expanded.add(c)
-                self._landed[c].record(self.comm_stream)
-            gather = reduce = _StreamEventWork(self._landed[c], self.device)
+                if value:
+                    _native.check(lib.gsr_stream_signal(self.comm_stream.cuda_stream, landed, self._seq),
+                                  "gsr_stream_signal")
+                else:
+                    self._landed[c].record(self.comm_stream)
+            gather = reduce = (_StreamValueWork(landed, self._seq, self.device) if value else
+                               _StreamEventWork(self._landed[c], self.device))
         elif self.distributed:
             gather, reduce = self._issue(c)
         self._pending.append((c, gather, reduce))
@@ -560,6 +593,19 @@ class _StreamEventWork:
 
     def wait(self):
         torch.cuda.current_stream(self.device).wait_event(self.event)
+
+
+class _StreamValueWork:
+    """work.wait() for a collective run on the reducer's side stream, value hand-off: the current stream waits until
+    the side stream has written the step's sequence number to the chunk's landed word."""
+
+    def __init__(self, flag_ptr: int, value: int, device):
+        self.flag_ptr, self.value, self.device = flag_ptr, value, device
+
+    def wait(self):
+        from . import _native
+        _native.check(_native.load().gsr_stream_wait(torch.cuda.current_stream(self.device).cuda_stream,
+                                                     self.flag_ptr, self.value), "gsr_stream_wait")
 
 
 def unchunk_factors(flat: torch.Tensor, V: int, n: int, chunk_len: int) -> torch.Tensor:

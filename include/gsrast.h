@@ -343,6 +343,15 @@ int gsr_debug_wave_stamps(int which, uint32_t *host_dst, int max_slots);
 const char *gsr_last_error(void);
 const char *gsr_build_info(void);
 
+/* Stream-ordered hand-off between two streams without events (the multi-view exchange's chunk hand-offs between the
+ * compute stream and the collective stream): gsr_stream_signal writes `value` to the 4-B device word `flag` once the
+ * stream's earlier work is done (hipStreamWriteValue32); gsr_stream_wait holds the stream's later work until
+ * *flag >= value (hipStreamWaitValue32).  gsr_stream_values_supported() is 0 where the device lacks stream wait
+ * values (the caller then uses events). */
+int gsr_stream_values_supported(void);
+int gsr_stream_signal(void *stream, uint32_t *flag, uint32_t value);
+int gsr_stream_wait(void *stream, uint32_t *flag, uint32_t value);
+
 /* ABI version of this header.  2: gsr_state_layout gained struct_size at offset 0 and lost img_tile_sorted /
  * img_tile_lastkey (a one-time break: a caller built against a version-1 header reads shifted offsets, so it must
  * check gsr_abi_version() == GSR_ABI_VERSION before using the layout).  From version 2 on, fields of the versioned

@@ -160,11 +160,17 @@ def case_inputs(name):
     return sc, cam, torch.tensor(bg, dtype=torch.float32), dc, di
 
 
+# Inputs a reference fixture stores instead of regenerating them: everything the generator forms with more than a
+# seeded randn and one rounding (scales = exp(...), opacities = sigmoid(...), rotations = normalize(...), the camera's
+# inverse and matrix products) can round differently on another CPU's vector units.  The rest -- means3D, shs and the
+# upstream gradients, plain randn (x 0.3) -- is regenerated and checked against the fixture's SHA-256.
+REF_STORED_INPUTS = ("scales", "rotations", "opacities", "viewmatrix", "projmatrix", "campos")
+
+
 def input_hash(sc, cam, dc, di) -> str:
     import hashlib
     h = hashlib.sha256()
-    for t in (sc.means3D, sc.scales, sc.rotations, sc.opacities, sc.shs, cam.viewmatrix, cam.projmatrix, cam.campos,
-              dc, di):
+    for t in (sc.means3D, sc.shs, dc, di):
         h.update(np.ascontiguousarray(t.numpy(), np.float32).tobytes())
     return h.hexdigest()
 
@@ -197,11 +203,10 @@ def load_ref_golden(name: str) -> dict:
     n, W, H = REF_CASES[name][:3]
     mask = np.unpackbits(z["mask_bits"])[:W * H].reshape(H, W).astype(bool)
     out["mask"] = mask
-    out["inp"] = dict(means3D=sc.means3D.numpy(), opacities=sc.opacities.numpy(), scales=sc.scales.numpy(),
-                      rotations=sc.rotations.numpy(), shs=sc.shs.numpy(), viewmatrix=cam.viewmatrix.numpy(),
-                      projmatrix=cam.projmatrix.numpy(), campos=cam.campos.numpy(), bg=bg.numpy(),
+    out["inp"] = dict(means3D=sc.means3D.numpy(), shs=sc.shs.numpy(), bg=bg.numpy(),
                       tanfovx=cam.tanfovx, tanfovy=cam.tanfovy, image_height=H, image_width=W,
-                      sh_degree=sc.sh_degree, scale_modifier=1.0)
+                      sh_degree=sc.sh_degree, scale_modifier=1.0,
+                      **{k: out.pop("input_" + k) for k in REF_STORED_INPUTS})
     out["dL_dcolor"] = (dc * torch.from_numpy(mask.astype(np.float32))).numpy()
     out["dL_dinvdepth"] = (di * torch.from_numpy(mask.astype(np.float32))).numpy()
     return out

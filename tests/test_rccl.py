@@ -55,6 +55,8 @@ VARIANTS = [  # (mode, chunks, reducer options): one RCCL group per chunk unless
     ("compact", 4, dict(comm_stream="pg")), ("compact", 2, dict(comm_stream="side", expand="once")),
     ("compact", 4, dict(expand="side")),  # each chunk's expansion on the side stream behind its group
     ("compact", 2, dict(expand="side", early=False)),  # "side" without means3D at begin_step: expands in finish()
+    ("compact", 4, dict(handoff="value")), ("compact", 4, dict(expand="side", handoff="value")),
+    ("dense", 2, dict(handoff="value")),  # stream-value hand-offs (gsr_stream_signal / gsr_stream_wait)
 ]
 
 
@@ -68,6 +70,8 @@ def test_rccl_exchange_one_rank_is_bitwise_local(gpu_device, mode, chunks, kw):
         got = _run(gpu_device, True, mode, chunks, **kw)
         red = got[3]
         assert red.coalesce == kw.get("coalesce", True)  # the grouped path really ran (no fallback)
+        if kw.get("handoff") == "value":
+            assert red.handoff == "value"  # the device supports stream wait values: no silent event fallback
         if kw.get("expand") == "side" and kw.get("early", True):
             assert red._expanded == set(range(red.chunks))  # the expansions ran on the side stream
         # the RCCL branch really ran: the chunk gathers landed in the (world, L, 3) buffers

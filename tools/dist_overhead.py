@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--config", default="cfg3")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--only", default="", help="comma-separated variant names (plain always runs)")
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -50,7 +51,7 @@ def main():
                 backward_raw(st, rs, dc, di, **red.backward_kwargs())
                 red.reduce(sc.means3D)
             else:
-                red.begin_step(means3D=sc.means3D)
+                red.begin_step(means3D=sc.means3D)  # expand="side": expansions on the side stream
                 backward_chunked(st, rs, dc, di, red.chunk_outputs(), on_chunk=red.start_chunk,
                                  compact_sh=red.compact, accumulate_stats=True)
                 red.finish(sc.means3D)
@@ -70,23 +71,26 @@ def main():
         wall = time.perf_counter() - t0
         return {"wall_ms": round(1e3 * wall / args.steps, 4), "host_ms": round(1e3 * host / args.steps, 4)}
 
-    local = {"plain": dict(mode="dense", chunks=1), "local_compact1": dict(mode="compact", chunks=1),
-             "local_compact4_chunk": dict(mode="compact", chunks=4, expand="chunk"),
-             "local_compact4_once": dict(mode="compact", chunks=4, expand="once"),
-             "local_dense4": dict(mode="dense", chunks=4)}
-    remote = {"dist_dense1_sync_group": dict(mode="dense", chunks=1),
-              "dist_dense1_async_sep": dict(mode="dense", chunks=1, sync_ops=False, coalesce=False),
-              "dist_compact1_sync_group": dict(mode="compact", chunks=1),
-              "dist_compact1_async_sep": dict(mode="compact", chunks=1, sync_ops=False, coalesce=False),
-              "dist_compact4_chunk_group": dict(mode="compact", chunks=4, expand="chunk"),
-              "dist_compact4_once_group": dict(mode="compact", chunks=4, expand="once"),
-              "dist_compact4_chunk_sep": dict(mode="compact", chunks=4, expand="chunk", coalesce=False),
-              "dist_dense4_group": dict(mode="dense", chunks=4),
-              "dist_compact4_chunk_side": dict(mode="compact", chunks=4, expand="chunk", comm_stream="side"),
-              "dist_compact2_chunk_side": dict(mode="compact", chunks=2, expand="chunk", comm_stream="side"),
-              "dist_compact4_once_side": dict(mode="compact", chunks=4, expand="once", comm_stream="side"),
-              "dist_dense4_side": dict(mode="dense", chunks=4, comm_stream="side"),
-              "dist_auto": dict(mode="auto", chunks=None)}
+    local = {"plain": dict(mode="dense", chunks=1), "local_compact1": dict(mode="compact", chunks=1)}
+    remote = {"dist_dense1": dict(mode="dense", chunks=1),
+              "dist_compact1": dict(mode="compact", chunks=1),
+              "dist_compact2_chunk": dict(mode="compact", chunks=2, expand="chunk"),
+              "dist_compact2_once": dict(mode="compact", chunks=2, expand="once"),
+              "dist_compact2_side": dict(mode="compact", chunks=2, expand="side"),
+              "dist_compact4_chunk": dict(mode="compact", chunks=4, expand="chunk"),
+              "dist_compact4_once": dict(mode="compact", chunks=4, expand="once"),
+              "dist_compact4_side": dict(mode="compact", chunks=4, expand="side"),
+              "dist_dense2": dict(mode="dense", chunks=2),
+              "dist_compact2_chunk_value": dict(mode="compact", chunks=2, expand="chunk", handoff="value"),
+              "dist_compact4_chunk_value": dict(mode="compact", chunks=4, expand="chunk", handoff="value"),
+              "dist_compact4_once_value": dict(mode="compact", chunks=4, expand="once", handoff="value"),
+              "dist_compact4_side_value": dict(mode="compact", chunks=4, expand="side", handoff="value"),
+              "dist_auto": dict(mode="auto", chunks=None),
+              "dist_auto_w8": dict(mode="auto", chunks=None, plan_world=8)}
+    if args.only:
+        keep = set(args.only.split(","))
+        local = {k: v for k, v in local.items() if k in keep or k == "plain"}
+        remote = {k: v for k, v in remote.items() if k in keep}
     steps = {k: make_step(ViewGradReducer(n, M, cfg["deg"], dev, distributed=False, **kw)) for k, kw in local.items()}
     dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
     res = {}
@@ -100,8 +104,10 @@ def main():
         for k, v in samples.items():
             w = sorted(x["wall_ms"] for x in v)
             res[k] = {"wall_ms_median": w[len(w) // 2], "wall_ms_all": w}
-        res["dist_auto"]["exchange"] = reds["dist_auto"].describe()
-        res["dist_auto"]["plan"] = reds["dist_auto"].plan
+        for k in ("dist_auto", "dist_auto_w8"):
+            if k in reds:
+                res[k]["exchange"] = reds[k].describe()
+                res[k]["plan"] = reds[k].plan
     finally:
         dist.destroy_process_group()
     base = res["plain"]["wall_ms_median"]
