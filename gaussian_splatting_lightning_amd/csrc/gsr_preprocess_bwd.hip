@@ -5,10 +5,6 @@
 #include "gsr_kernels.h"
 #include "gsr_sh.h"
 
-#ifndef GSR_PBWD_HOIST
-#define GSR_PBWD_HOIST 1
-#endif
-
 namespace gsr {
 
 // ------------------------------------------------------------------------------------------------
@@ -151,12 +147,11 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
     const float3 mean = load_f3(p.means3D, i);
     // The SH stage's inputs (clamp bits, camera, the forward's colour Jacobian) requested with the geometry's: issued
     // at the SH stage, the clamp byte's round trip came before the Jacobian's nine loads were issued, two more memory
-    // round trips per wave after the geometry's (GSR_PBWD_HOIST 0: the old placement, for library A/Bs)
+    // round trips per wave after the geometry's (measured in round 5: Appendix A.4 of DESIGN.md)
     const bool sh_stage = p.shs && p.M > 0;  // uniform
     uint8_t cl = 0;
     const float3 campos = cam.campos;
     float3 jx = make_float3(0, 0, 0), jy = jx, jz = jx;
-#if GSR_PBWD_HOIST
     if (sh_stage) {
         cl = p.clamped[i];
         if (p.D > 0) {
@@ -167,7 +162,6 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
             jz = make_float3(J[6 * n], J[7 * n], J[8 * n]);
         }
     }
-#endif
     float c6[6];
     float3 scale = make_float3(0, 0, 0);
     float4 rot = make_float4(1, 0, 0, 0);
@@ -268,24 +262,12 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
     // direction Jacobian the forward stored (sh_jac), so the 48 coefficients are not read here.  (The backward's
     // shs are the forward's, as in the autograd function and the upstream API.)
     if (sh_stage) {
-#if !GSR_PBWD_HOIST
-        cl = p.clamped[i];
-#endif
         const float3 dRGB = make_float3((cl & 1) ? 0.f : gs[6], (cl & 2) ? 0.f : gs[7], (cl & 4) ? 0.f : gs[8]);
         if (p.dL_dcolors_sh) {
             p.dL_dcolors_sh[3 * i] = dRGB.x;
             p.dL_dcolors_sh[3 * i + 1] = dRGB.y;
             p.dL_dcolors_sh[3 * i + 2] = dRGB.z;
         }
-#if !GSR_PBWD_HOIST
-        if (p.D > 0) {
-            const size_t n = (size_t)p.P;
-            const float *J = p.sh_jac + i;
-            jx = make_float3(J[0], J[n], J[2 * n]);
-            jy = make_float3(J[3 * n], J[4 * n], J[5 * n]);
-            jz = make_float3(J[6 * n], J[7 * n], J[8 * n]);
-        }
-#endif
         float *dsh = p.dL_dsh ? p.dL_dsh + (size_t)i * ncoef : nullptr;  // null only with dL_dcolors_sh (API)
         if (LDS) {
             // LDS-staged block (M = 16): the kernel writes dL/dsh = basis (x) dRGB through LDS
@@ -332,9 +314,8 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
 // writes to its own Gaussian (52 = 4 x 13, 13 odd: 16 lanes of a b128 lane group hit 16 distinct 4-bank windows)
 // are free of bank conflicts.  The coefficients themselves are not read (sh_jac).  A half-wave staging area
 // (6.5 KB, shared with the row-gather chunks) keeps the block at 26 KB of LDS: six blocks, the VGPR limit, per CU.
-#ifndef GSR_PBWD_INV_AHEAD
-#define GSR_PBWD_INV_AHEAD 1  // next chunk's loaded tests during this chunk's row loads: cfg3 0.104 -> 0.100 ms, cfg5 0.521 -> 0.507
-#endif
+// The next chunk's loaded tests (inverse-permutation words) are issued during this chunk's row loads: cfg3 0.104 ->
+// 0.100 ms, cfg5 0.521 -> 0.507 against all of a chunk's inv words first (round 5).
 constexpr int SH_STRIDE = 52;
 constexpr int PBWD_STAGE = 32 * SH_STRIDE;  // floats of LDS per wave
 template <bool LDS_SH>
@@ -401,32 +382,24 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
                 sidx[r] = p.inv[uu[r]];
             }
         };
-#if GSR_PBWD_INV_AHEAD
         uint32_t uu_n[PER], sidx_n[PER];
         if (total) inv_chunk(0, uu_n, sidx_n);
-#endif
         for (uint32_t c0 = 0; c0 < total; c0 += CH) {
             float rw[PER][10];
             uint32_t sidx[PER];
             uint32_t uu[PER];
-#if GSR_PBWD_INV_AHEAD
 #pragma unroll
             for (uint32_t r = 0; r < PER; r++) {  // this chunk's loaded tests, made during the previous chunk
                 uu[r] = uu_n[r];
                 sidx[r] = sidx_n[r];
             }
-#else
-            inv_chunk(c0, uu, sidx);  // all inv words of the chunk first ...
-#endif
             bool use[PER];
 #pragma unroll
-            for (uint32_t r = 0; r < PER; r++) {  // ... then the rows the composite wrote (others read row 0, dropped)
+            for (uint32_t r = 0; r < PER; r++) {  // the rows the composite wrote (others read row 0, dropped)
                 use[r] = c0 + r * 64 + lane < total && sidx[r] != INV_NONE;
                 load_row(p.rows, use[r] ? uu[r] : 0u, rw[r]);
             }
-#if GSR_PBWD_INV_AHEAD
             if (c0 + CH < total) inv_chunk(c0 + CH, uu_n, sidx_n);  // the next chunk's inv words meanwhile
-#endif
 #pragma unroll
             for (uint32_t r = 0; r < PER; r++) {
                 const uint32_t q = r * 64 + lane;  // pair within the chunk
