@@ -80,15 +80,13 @@ enum Stage {
     ST_BK_COUNT,
     ST_BK_SCATTER,
     ST_SEG_SORT,
-    ST_PRE_COLOR,
     ST_ADAM_SH,
     ST_COUNT
 };
 const char *kStageNames[ST_COUNT] = {"preprocess", "depth_sort", "instance_scan", "readback",
                                      "expand",     "tile_sort",  "tile_ranges",   "render_fwd",
                                      "render_bwd", "big_reduce", "preprocess_bwd", "sh_views",
-                                     "bucket_count", "bucket_scatter", "seg_sort", "preprocess_color",
-                                     "adam_sh_views"};
+                                     "bucket_count", "bucket_scatter", "seg_sort", "adam_sh_views"};
 
 struct Profiler {
     std::mutex mu;
@@ -457,8 +455,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     // next array starts there) so the memset is one aligned fill kernel, not an aligned fill plus a tail
     const size_t clear_bytes = align_up((size_t)(reinterpret_cast<char *>(g.tile_status + BK_MAX_TILES / 32 + 1) -
                                                  reinterpret_cast<char *>(g.counters)), 256);
-    if (tuning("zero_kernel", 1)) launch_zero16(stream, g.counters, clear_bytes);
-    else GSR_HIP(hipMemsetAsync(g.counters, 0, clear_bytes, stream));
+    launch_zero16(stream, g.counters, clear_bytes);  // a plain kernel: the runtime's fill measured slower
 
     PreprocessParams pp;
     pp.P = P; pp.D = a->D; pp.M = a->M; pp.W = W; pp.H = H; pp.gx = gx; pp.gy = gy;
@@ -492,16 +489,6 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     InflightReadback inflight;  // armed before the launch: an error reported after it still waits for the kernel
     inflight.s = stream;
     inflight.armed = rb_spin;
-    // SH colours in a second kernel (preprocess_color_kernel, "pre_split" 1): the projection kernel drops the 192-B
-    // coefficient stream and ~40 registers, and the colour stream runs behind the bucket count pass, while the
-    // host waits for the instance total.  Measured slower (cfg 3: preprocess 0.101 ms fused against 0.073 + 0.071 split,
-    // the host's wait is too short to hide the colour kernel; cfg 5: 0.32 + 0.35 ms), so the fused kernel is the default.
-    pp.split = (a->shs && !a->colors_precomp && tuning("pre_split", 0)) ? 1 : 0;
-    // the late colour phase ("pre_late" 1): coefficient rows staged through LDS by coalesced loads (16 coefficients,
-    // 16-B aligned rows, degree > 0).  Measured slower (cfg 3 preprocess 0.105 -> 0.120 / 0.124 / 0.133 ms at 4 / 5 / 6
-    // waves per SIMD, cfg 5 0.454 -> 0.533 ms: profiles/r4l_ab_late_cfg*.txt), so off by default
-    pp.late = (!pp.split && a->shs && !a->colors_precomp && a->M == 16 && a->D > 0 &&
-               ((uintptr_t)a->shs & 15) == 0) ? tuning("pre_late", 0) : 0;  // 2: late, rows read directly
     // the kept depth keys' range, for the radix path's relative depth sort: only where that sort can run (multi-kernel
     // depth sorts, P above the onesweep limit); else the range words stay empty and the sort takes its 32-bit keys
     const uint32_t os_max = (uint32_t)tuning("onesweep_max_n", 3 << 20);
@@ -540,7 +527,6 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             return fail(GSR_ERR_ARG, "internal: bucket binning buffer not set");
         GSR_STAGE(ST_BK_COUNT, dbg, launch_bucket_count(stream, bp));
     }
-    GSR_STAGE(ST_PRE_COLOR, dbg, launch_preprocess_color(stream, pp));
     // The binning buffer's size depends on the instance total.  Requesting it through the caller's allocator
     // (a Python callback from rasterizer.py) after the readback put ~40 us of host work between the preprocess and
     // the next launch, longer than the queued count passes cover; so with a total from an earlier call on this
@@ -589,12 +575,12 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     bool depth_onesweep = false, tile_onesweep = false;  // which sorts ran on the onesweep path (diagnostics)
     if (bucket) gsr_set_tuning("stat_depth_passes", 0);
     if (!bucket) {
-        // the depth sort's last pass also writes the tile counts and expansion records in depth order ("sort_gather"
-        // bit 0 / bit 1; unset: the scan / the expansion gathers them through the order instead)
-        const int sg = tuning("sort_gather", 1);
+        // the depth sort's last pass also writes the tile counts and expansion records in depth order, so the scan and
+        // the expansion read them coalesced instead of gathering them through the order
+        constexpr int sg = 3;
         SortGather ga;
-        if (sg & 1) { ga.src = g.tiles; ga.dst = g.tiles_sorted; }
-        if (sg & 2) { ga.src4 = g.exp_rec; ga.dst4 = g.exp_sorted; }
+        ga.src = g.tiles; ga.dst = g.tiles_sorted;
+        ga.src4 = g.exp_rec; ga.dst4 = g.exp_sorted;
         bool sorted_recs = false;
         // Relative depth keys ("depth_rel" 1) where the sort takes the multi-kernel path: the kept keys span
         // kmax - kmin, so rs_rel_key maps them onto [0, span] and the culled ones onto span + 1, and the sort runs
@@ -617,16 +603,11 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
         }
         const bool sorted_tiles = sorted_recs && (sg & 1);
         sorted_exp = sorted_recs && (sg & 2);
-        if (tuning("scan_lookback", 1))
-            GSR_STAGE(ST_SCAN, dbg,
-                      launch_exclusive_scan_lookback(stream, sorted_tiles ? g.tiles_sorted : g.tiles,
-                                                     sorted_tiles ? nullptr : g.order, (uint32_t)P, g.inst_off,
-                                                     g.scan_status, g.counters + CNT_SCAN_TICKET,
-                                                     g.counters + CNT_OVERFLOW));
-        else
-            GSR_STAGE(ST_SCAN, dbg,
-                      launch_exclusive_scan(stream, g.tiles, g.order, (uint32_t)P, g.inst_off, g.scan_tmp,
-                                            g.counters + CNT_OVERFLOW));
+        GSR_STAGE(ST_SCAN, dbg,
+                  launch_exclusive_scan_lookback(stream, sorted_tiles ? g.tiles_sorted : g.tiles,
+                                                 sorted_tiles ? nullptr : g.order, (uint32_t)P, g.inst_off,
+                                                 g.scan_status, g.counters + CNT_SCAN_TICKET,
+                                                 g.counters + CNT_OVERFLOW));
     }
 
     r_hint = R;
@@ -674,7 +655,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             ep.P = (uint32_t)P; ep.R = R; ep.gx = gx; ep.gy = gy;
             ep.order = g.order; ep.inst_off = g.inst_off; ep.tiles = g.tiles; ep.exp_rec = g.exp_rec;
             ep.exp_sorted = sorted_exp ? g.exp_sorted : nullptr;
-            ep.exp_owner = tuning("exp_owner", 1) ? b.exp_owner : nullptr;
+            ep.exp_owner = b.exp_owner;
             // 16-bit tile keys up to 65536 tiles ("tile_key16" 0: 32-bit): the tile sort, the expansion's key stores and
             // the range search move 2 bytes per key instead of 4
             const TileSortPlan plan = tile_sort_plan(T);
@@ -721,7 +702,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     // the backward's LPT order from bucket lists the whole-tile waves append (no ordering launch in the backward)
     rp.lpt_valid = im.lpt_valid;
     rp.strip_mask = b.strip_mask; rp.smask_valid = im.smask_valid;
-    if (lpt_append_range(T) && lpt && tuning("bwd_order", 1) && tuning("lpt_append", 1)) {
+    if (lpt_append_range(T) && lpt && tuning("lpt_append", 1)) {
         rp.lpt_bcnt = im.lpt_bcnt; rp.lpt_blist = im.lpt_blist;
     }
     if (T <= SEG_MAX_TILES && tuning("bwd_seg", 1)) {
@@ -794,8 +775,8 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
         rp.W = W; rp.H = H; rp.gx = gx; rp.gy = gy; rp.num_tiles = (int)T; rp.num_rendered = R;
         rp.ranges = im.ranges; rp.point_list = b.point_list; rp.n_contrib = im.n_contrib;
         const int lpt = tuning("lpt", 1);
-        // "bwd_order" 0: reuse the forward's order (range lengths) and skip the tile_last ordering launch
-        const bool own_order = lpt && tuning("bwd_order", 1);
+        // the backward's own order (by tile_last; reusing the forward's range-length order measured slower)
+        const bool own_order = lpt != 0;
         // in lpt_append_range the forward's whole-tile waves filled the bucket lists (render_bwd falls back to the
         // identity order if that forward did not, *lpt_valid = 0: the order never changes a result)
         const bool lists = own_order && lpt_append_range(T) && tuning("lpt_append", 1);
@@ -847,8 +828,7 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     pp.sh_jac = g.sh_jac;  // the forward's d rgb / d dir: the SH term of dL/dmeans3D reads no coefficient
     pp.big_slot = g.big_slot; pp.bigsum = bigsum;
     pp.rows = rows;
-    pp.sh_vec16 = pp.shs && a->M == 16 && (((uintptr_t)pp.shs | (uintptr_t)a->dL_dsh) & 15) == 0 &&
-                  tuning("sh_vec16", 1);
+    pp.sh_vec16 = pp.shs && a->M == 16 && (((uintptr_t)pp.shs | (uintptr_t)a->dL_dsh) & 15) == 0;
     pp.dL_dmeans2D = rel(a->dL_dmeans2D, 3); pp.dL_dcolors = rel(a->dL_dcolors, 3);
     pp.dL_dopacity = rel(a->dL_dopacity, 1); pp.dL_dmeans3D = rel(a->dL_dmeans3D, 3);
     pp.dL_dcov3D = rel(a->dL_dcov3D, 6); pp.dL_dsh = rel(a->dL_dsh, (int64_t)a->M * 3);

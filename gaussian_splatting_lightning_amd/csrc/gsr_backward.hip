@@ -265,13 +265,10 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
 }
 
 // render_bwd_v5_kernel: one wave per tile, the pair-reduced update with the per-instance control on the scalar unit.
-//   render_bwd is VALU-issue-bound (SQ_INSTS_VALU x issue cost ~ 80 % of its cycles at cfg 3), so every saved
-//   vector instruction counts:
-//   * strip liveness by contributor count: a pixel takes part in instance idx only while idx < n_contrib, so strip
-//     k is dead for every idx >= its lanes' largest n_contrib (smax[k]); those batch bits are cleared from the
-//     strip mask with scalar ops, and for idx < the strips' smallest n_contrib (smin[k]) the per-lane
-//     `idx < n_contrib` compare is skipped (a scalar bit test selects the variant);
-//   * the staged records are one 48-byte FwdRec array.
+//   render_bwd is VALU-issue-bound (SQ_INSTS_VALU x issue cost ~ 85 % of its cycles at cfg 3), so every saved
+//   vector instruction counts: the strips an instance cannot reach are skipped by scalar bit tests (the forward's
+//   exact strip masks), the contributing lanes come straight from compares as scalar masks, and the staged records
+//   are one 48-byte FwdRec array.
 #ifndef GSR_BWD_MINW
 #define GSR_BWD_MINW 5
 #endif
@@ -283,7 +280,7 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
 // checkpoint at the segment's end: T = T_e and D = (colour still to come . dL/dpix + T_final bg . dL/dpix) / T_e, the
 // scalar accumulator's value there (D_k T_(k+1) = sum_(j > k) w_j c_j . dL/dpix + T_final bg . dL/dpix).  Without
 // checkpoints every tile is one segment.  Rows agree with the one-walk backward to rounding.
-template <bool HAS_INV, bool LASTC, bool UNION = false, bool SEG = false, bool GUARD = false>
+template <bool HAS_INV, bool UNION = false, bool SEG = false, bool GUARD = false>
 __global__ __launch_bounds__(64, GUARD ? 4 : SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MINW) void render_bwd_v5_kernel(RenderBwdParams p) {
     __shared__ FwdRec s_rec[BWD_BATCH];
     __shared__ __attribute__((aligned(16))) float s_part[BWD_BATCH][PART];  // [instance][10 sums]
@@ -334,7 +331,7 @@ __global__ __launch_bounds__(64, GUARD ? 4 : SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MI
     const size_t HW = (size_t)p.W * p.H;
     float T[PIX_PER_LANE], dp0[PIX_PER_LANE], dp1[PIX_PER_LANE], dp2[PIX_PER_LANE], dinv[PIX_PER_LANE];
     float D[PIX_PER_LANE], prow[PIX_PER_LANE];
-    uint32_t lastc[PIX_PER_LANE], smax[PIX_PER_LANE], smin[PIX_PER_LANE];
+    uint32_t lastc[PIX_PER_LANE];
 #pragma unroll
     for (int k = 0; k < PIX_PER_LANE; k++) {
         const int py = py0 + 4 * k;
@@ -348,10 +345,6 @@ __global__ __launch_bounds__(64, GUARD ? 4 : SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MI
         dinv[k] = (HAS_INV && inside) ? p.dL_dinvdepth[pid] : 0.f;
         D[k] = fmaf(bg2, dp2[k], fmaf(bg1, dp1[k], bg0 * dp0[k]));
         prow[k] = (float)py;  // dy = y - pixel row in one subtraction, as the forward
-        if (LASTC) {
-            smax[k] = __builtin_amdgcn_readfirstlane(wave_max_u32(lastc[k]));
-            smin[k] = __builtin_amdgcn_readfirstlane(wave_min_u32(lastc[k]));
-        }
     }
     if (SEG && !last_seg) {  // start from the checkpoint before instance hi
         const float *ck = p.ckpt + (size_t)(r0 / ck_k + (uint32_t)tile + seg) * CK_FLOATS;
@@ -389,21 +382,11 @@ __global__ __launch_bounds__(64, GUARD ? 4 : SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MI
             s_rec[lane].c = p.rec[gid].c;
             my_m = smask ? (uint32_t)p.strip_mask[s_me] : cell_mask(p.strip_exact, my_a, my_b, row0, col0);
         }
-        // sk[k] bit j: strip k of instance j (idx = bend - 1 - j) may hold a contributing pixel;
-        // nd[k] bit j: some lane of strip k may have n_contrib <= idx (the per-lane compare is needed)
-        uint64_t sk[PIX_PER_LANE], nd[PIX_PER_LANE];
+        // sk[k] bit j: strip k of instance j (idx = bend - 1 - j) may hold a contributing pixel.  (Strip liveness and
+        // compare skipping from the strips' n_contrib bounds measured 2.5 % slower -- SALU -- and was removed.)
+        uint64_t sk[PIX_PER_LANE];
 #pragma unroll
-        for (int k = 0; k < PIX_PER_LANE; k++) {
-            sk[k] = __ballot((my_m >> k) & 1u);
-            if (LASTC) {
-                const int lo = bend - (int)smax[k];  // j < lo: idx >= smax, no lane of the strip contributes
-                const int hi = bend - (int)smin[k];  // j < hi: idx >= smin, some lane may not contribute
-                sk[k] &= lo <= 0 ? ~0ull : lo >= 64 ? 0ull : ~0ull << lo;
-                nd[k] = hi <= 0 ? 0ull : hi >= 64 ? ~0ull : (1ull << hi) - 1ull;
-            } else {
-                nd[k] = ~0ull;
-            }
-        }
+        for (int k = 0; k < PIX_PER_LANE; k++) sk[k] = __ballot((my_m >> k) & 1u);
         wave_lds_sync();
         // one instance's pass over the lane's pixels: updates T / D, returns the lane's raw sums (Q0, Q1, Q2, w0..w3) and dx in m and the
         // ballot of the lanes that contributed
@@ -424,8 +407,7 @@ __global__ __launch_bounds__(64, GUARD ? 4 : SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MI
                 const float G = __builtin_amdgcn_exp2f(power2);
                 const float alpha = fminf(0.99f, b.y * G);
                 // the contributing lanes as a scalar mask straight from the compares: !(power2 > 0),
-                // !(alpha < 1/255) and, where some lane of the strip may have finished, idx < n_contrib
-                const bool need = (nd[k] >> j) & 1u;  // wave-uniform
+                // !(alpha < 1/255) and idx < n_contrib
                 uint64_t ok = __builtin_amdgcn_fcmpf(power2, 0.0f, FCMP_ULE) &
                               __builtin_amdgcn_fcmpf(alpha, GUARD ? GUARD_A_LO : 1.0f / 255.0f, FCMP_UGE);
                 if constexpr (GUARD) {  // the forward's guarded alpha decision, taken by the same test (gsr_common.h)
@@ -436,7 +418,7 @@ __global__ __launch_bounds__(64, GUARD ? 4 : SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MI
                         ok = (ok & ~near) | (okx & near);
                     }
                 }
-                if (need) ok &= __builtin_amdgcn_uicmp(idx, lastc[k], ICMP_ULT);
+                ok &= __builtin_amdgcn_uicmp(idx, lastc[k], ICMP_ULT);
                 any |= ok;
                 if (!__builtin_amdgcn_inverse_ballot_w64(ok)) continue;  // exec = ok
                 T[k] = T[k] * fast_rcp(1.f - alpha);
@@ -596,10 +578,10 @@ void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
         // segmented walk (800x800, 2500 tiles: one wave per 128-instance segment against 4 part-waves per tile)
         seg_list_kernel<<<1, 1024, 0, s>>>(p.tile_order, p.tile_last, p.num_tiles, p.ck_flag, q.seg_list, q.seg_count);
         const dim3 grid((uint32_t)seg_slots((int64_t)p.num_rendered, (uint32_t)p.num_tiles)), block(64);
-        if (gd && p.dL_dinvdepth) render_bwd_v5_kernel<true, false, false, true, true><<<grid, block, 0, s>>>(q);
-        else if (gd) render_bwd_v5_kernel<false, false, false, true, true><<<grid, block, 0, s>>>(q);
-        else if (p.dL_dinvdepth) render_bwd_v5_kernel<true, false, false, true><<<grid, block, 0, s>>>(q);
-        else render_bwd_v5_kernel<false, false, false, true><<<grid, block, 0, s>>>(q);
+        if (gd && p.dL_dinvdepth) render_bwd_v5_kernel<true, false, true, true><<<grid, block, 0, s>>>(q);
+        else if (gd) render_bwd_v5_kernel<false, false, true, true><<<grid, block, 0, s>>>(q);
+        else if (p.dL_dinvdepth) render_bwd_v5_kernel<true, false, true><<<grid, block, 0, s>>>(q);
+        else render_bwd_v5_kernel<false, false, true><<<grid, block, 0, s>>>(q);
         return;
     }
     // "bwd_parts" 1, 2 or 4; 0 (default): 4 or 2 while that many part-waves fit within bwd_part_slots
@@ -621,28 +603,24 @@ void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
         return;
     }
     const dim3 grid(p.num_tiles), block(64);
-    // "bwd_lastc" 1: strip liveness and compare skipping by n_contrib bounds (measured 2.5 % slower: SALU).
     // "bwd_union" -1 (auto): pair only the instances that reach a strip when tiles are long (mean above 1024
     // instances: cfg 5 render_bwd 0.93 -> 0.90 ms; at cfg 3's 517 the plain walk is faster, 0.305 vs 0.329 ms);
     // 0 / 1 force it
-    const bool lc = tuning("bwd_lastc", 0) != 0;
     const int un = tuning("bwd_union", -1);
     const bool u = un < 0 ? p.num_rendered > (uint64_t)1024 * (uint64_t)p.num_tiles : un != 0;
     if (gd) {
-        if (p.dL_dinvdepth && u) render_bwd_v5_kernel<true, false, true, false, true><<<grid, block, 0, s>>>(q);
-        else if (p.dL_dinvdepth) render_bwd_v5_kernel<true, false, false, false, true><<<grid, block, 0, s>>>(q);
-        else if (u) render_bwd_v5_kernel<false, false, true, false, true><<<grid, block, 0, s>>>(q);
-        else render_bwd_v5_kernel<false, false, false, false, true><<<grid, block, 0, s>>>(q);
+        if (p.dL_dinvdepth && u) render_bwd_v5_kernel<true, true, false, true><<<grid, block, 0, s>>>(q);
+        else if (p.dL_dinvdepth) render_bwd_v5_kernel<true, false, false, true><<<grid, block, 0, s>>>(q);
+        else if (u) render_bwd_v5_kernel<false, true, false, true><<<grid, block, 0, s>>>(q);
+        else render_bwd_v5_kernel<false, false, false, true><<<grid, block, 0, s>>>(q);
         return;
     }
     if (p.dL_dinvdepth) {
-        if (u) render_bwd_v5_kernel<true, false, true><<<grid, block, 0, s>>>(q);
-        else if (lc) render_bwd_v5_kernel<true, true><<<grid, block, 0, s>>>(q);
-        else render_bwd_v5_kernel<true, false><<<grid, block, 0, s>>>(q);
+        if (u) render_bwd_v5_kernel<true, true><<<grid, block, 0, s>>>(q);
+        else render_bwd_v5_kernel<true><<<grid, block, 0, s>>>(q);
     } else {
-        if (u) render_bwd_v5_kernel<false, false, true><<<grid, block, 0, s>>>(q);
-        else if (lc) render_bwd_v5_kernel<false, true><<<grid, block, 0, s>>>(q);
-        else render_bwd_v5_kernel<false, false><<<grid, block, 0, s>>>(q);
+        if (u) render_bwd_v5_kernel<false, true><<<grid, block, 0, s>>>(q);
+        else render_bwd_v5_kernel<false><<<grid, block, 0, s>>>(q);
     }
 }
 

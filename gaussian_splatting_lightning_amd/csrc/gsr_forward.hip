@@ -25,12 +25,10 @@ struct CullIn {
 
 // Projection, conic, radius, SH colour and render records of one Gaussian.  Returns the area of its tile
 // rect (0: not rendered); the tile culling, tile count and sort key are finished by preprocess_kernel.
-// SPLIT: the colour (SH evaluation, its Jacobian, the clamp bits and the colour words of the record) is left to
-// preprocess_color_kernel, launched behind the bucket count pass.
 // SHD >= 0: the SH degree at compile time (the common degree-3 launch).  With the runtime switch the compiler hoists the
 // degree-0 term common to every case (the first coefficient's load and multiply) above the switch, so the other 45
 // coefficients were only requested after that load had returned: one more memory round trip per wave.
-template <bool SPLIT, int SHD = -1>
+template <int SHD = -1>
 __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &p, const int i, CullIn &ci) {
     // uncontracted like the helpers it calls (gsr_common.h): radii, rects and render records bit-equal the oracle's
 #pragma clang fp contract(off)
@@ -98,8 +96,7 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
     const float opacity = opacity_in * hscale;
     float3 rgb = make_float3(0.f, 0.f, 0.f);
     uint8_t clamp_bits = 0;
-    if (SPLIT) {
-    } else if (p.colors_precomp) {
+    if (p.colors_precomp) {
         rgb = load_f3(p.colors_precomp, i);
     } else {
         float3 dir = dir_raw;
@@ -122,14 +119,9 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
         rgb = make_float3(fmaxf(rgb.x, 0.f), fmaxf(rgb.y, 0.f), fmaxf(rgb.z, 0.f));
     }
     g.rec[i].a = make_float4(pimg.x, pimg.y, conic_x, conic_y);
-    if (SPLIT) {
-        *reinterpret_cast<float2 *>(&g.rec[i].b) = make_float2(conic_z, opacity);
-        g.rec[i].c.y = 1.f / pv.z;
-    } else {
-        g.rec[i].b = make_float4(conic_z, opacity, rgb.x, rgb.y);
-        g.rec[i].c = make_float2(rgb.z, 1.f / pv.z);
-        g.clamped[i] = clamp_bits;
-    }
+    g.rec[i].b = make_float4(conic_z, opacity, rgb.x, rgb.y);
+    g.rec[i].c = make_float2(rgb.z, 1.f / pv.z);
+    g.clamped[i] = clamp_bits;
     p.radii[i] = (int)radius;
     // culling (p.cull): the reference rect shrinks to the tight rect (cull_rect), whose tiles are then tested one by
     // one when there are at most CULL_MAX_AREA of them
@@ -148,38 +140,6 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
     return tarea;
 }
 
-// The colour of Gaussian i (one the projection kept) from its coefficient row sh, with its direction Jacobian: the
-// expressions of preprocess_gaussian's inline colour, so records, clamp bits and Jacobian are bitwise those of the
-// fused kernel whichever kernel runs it (the colour kernel of a split preprocess, or the late colour phase).
-template <int DEG>
-__device__ __forceinline__ void color_finish(const PreprocessParams &p, int i, const float *sh) {
-#pragma clang fp contract(off)
-    const GeomState &g = p.g;
-    const float3 mean = load_f3(p.means3D, i);
-    const float3 campos = make_float3(p.campos[0], p.campos[1], p.campos[2]);
-    float3 dir = mean - campos;
-    const float len = sqrtf(dot3(dir, dir));
-    dir = make_float3(dir.x / len, dir.y / len, dir.z / len);
-    float3 rgb;
-    if (DEG > 0) {
-        float3 jx, jy, jz;
-        rgb = sh_eval_jac<DEG>(sh, dir, jx, jy, jz);
-        const size_t n = (size_t)p.P;
-        float *J = g.sh_jac + i;
-        J[0] = jx.x; J[n] = jx.y; J[2 * n] = jx.z;
-        J[3 * n] = jy.x; J[4 * n] = jy.y; J[5 * n] = jy.z;
-        J[6 * n] = jz.x; J[7 * n] = jz.y; J[8 * n] = jz.z;
-    } else {
-        rgb = sh_eval<0>(sh, dir);
-    }
-    rgb = sh_offset(rgb);
-    const uint8_t clamp_bits = (rgb.x < 0.f ? 1 : 0) | (rgb.y < 0.f ? 2 : 0) | (rgb.z < 0.f ? 4 : 0);
-    rgb = make_float3(fmaxf(rgb.x, 0.f), fmaxf(rgb.y, 0.f), fmaxf(rgb.z, 0.f));
-    *reinterpret_cast<float2 *>(&g.rec[i].b.z) = make_float2(rgb.x, rgb.y);
-    g.rec[i].c.x = rgb.z;
-    g.clamped[i] = clamp_bits;
-}
-
 // Exact tile culling is balanced across the wave: the (Gaussian, tile) pairs of all 64 lanes' rects are
 // enumerated jointly (prefix sum of the rect areas, each lane takes every 64th pair, owner found by marks and a
 // max-scan), so a wave costs ceil(sum of areas / 64) tile tests instead of its largest rect.
@@ -195,42 +155,24 @@ struct PreCullLds {
     unsigned long long mask[64];
     int own[64];    // lane whose rect's pair run starts at this pair of the step, else -1
 };
-// Late colour phase (PRE_LATE): after the culling a wave's LDS slice holds 32 coefficient rows at a time (a padded
-// 52-float stride: the lanes' 16-B row reads fall in distinct banks)
-constexpr int PRE_SH_STRIDE = 52;
-union PreLds {
-    PreCullLds cull;
-    float sh[32 * PRE_SH_STRIDE];
-};
-enum PreMode : int { PRE_FUSED = 0, PRE_SPLIT = 1, PRE_LATE = 2, PRE_LATE_DIRECT = 3 };
-#ifndef GSR_PRE_SPLIT_MINW
-#define GSR_PRE_SPLIT_MINW 7  // split (no colour): 70 VGPRs, 7 waves per SIMD (asking for 8 does not get under 64)
-#endif
 __device__ __forceinline__ void publish_total(const PreprocessParams &p);
 
-// MODE: PRE_FUSED (colour inside preprocess_gaussian, each lane reading its own 192-B coefficient row), PRE_SPLIT (colour
-// left to preprocess_color_kernel), PRE_LATE (colour after the culling: the wave stages 32 rows at a time into LDS with
-// coalesced 16-B loads, each lane then reads its row from LDS).  Per lane, 64 strided 192-B rows per wave cycle each
-// load instruction over 96 cache lines, which the waves of a CU re-fetch from L2; the staged loads read every line once.
-// LATE_MINW: waves per SIMD the late-colour kernel is built for (4: 100 VGPRs; 5: 96 + a 20-B spill; 6: 80 + 92 B).
-// PRE_LATE_DIRECT: the late colour phase reading each lane's row straight from global memory (no staging): only the
-// register peak moves (the colour no longer overlaps the projection state).
-template <int MODE, int LATE_MINW = 4, int SHD = -1>
-__global__ __launch_bounds__(256, MODE == PRE_SPLIT ? GSR_PRE_SPLIT_MINW
-                                  : (MODE == PRE_LATE || MODE == PRE_LATE_DIRECT) ? LATE_MINW : GSR_PRE_MINW)
-void preprocess_kernel(PreprocessParams p) {
-    constexpr bool SPLIT = MODE != PRE_FUSED;  // colour not inside preprocess_gaussian
-    __shared__ PreLds s_lds[4];
+// The colour is evaluated inside preprocess_gaussian, each lane reading its own 192-B coefficient row.  (Rounds 4-5
+// measured a split colour kernel behind the bucket count pass and a late, LDS-staged colour phase: both slower,
+// DESIGN.md Appendix A.4; removed in round 6.)
+template <int SHD = -1>
+__global__ __launch_bounds__(256, GSR_PRE_MINW) void preprocess_kernel(PreprocessParams p) {
+    __shared__ PreCullLds s_lds[4];
     __shared__ uint32_t s_w[4];
     const uint32_t bid = blockIdx.x;
     const int i = (int)bid * 256 + threadIdx.x;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    PreCullLds &L = s_lds[w].cull;
+    PreCullLds &L = s_lds[w];
     CullIn ci;
     ci.need = false;
     ci.vis = false;
     const uint32_t t_start = p.stamps ? stamp_now() : 0u;
-    const uint32_t area = i < p.P ? preprocess_gaussian<SPLIT, SHD>(p, i, ci) : 0u;
+    const uint32_t area = i < p.P ? preprocess_gaussian<SHD>(p, i, ci) : 0u;
     const uint32_t t_proj = p.stamps ? stamp_now() : 0u;
     const uint32_t need_area = ci.need ? area : 0u;
     const uint32_t incl = wave_inclusive_scan(need_area, lane);
@@ -337,47 +279,6 @@ void preprocess_kernel(PreprocessParams p) {
         p.stamps[2 * (bid * 4 + w)] = make_uint4(t_start, t_proj, t_cull, stamp_now());
         p.stamps[2 * (bid * 4 + w) + 1] = make_uint4(hw, xcc, 0u, 0u);
     }
-    if constexpr (MODE == PRE_LATE_DIRECT) {
-        if (ci.vis) {
-            const float *row = p.shs + (size_t)i * 48;
-            switch (p.D) {
-                case 1: color_finish<1>(p, i, row); break;
-                case 2: color_finish<2>(p, i, row); break;
-                default: color_finish<3>(p, i, row); break;
-            }
-        }
-    }
-    if constexpr (MODE == PRE_LATE) {  // the colours, after the total is out (the host's wait does not include them)
-        const bool need = ci.vis;  // every rendered Gaussian, as the fused colour (a culled rect's too)
-        float *sw = s_lds[w].sh;
-        const int g0w = (int)bid * 256 + w * 64;
-        for (int h = 0; h < 2; h++) {  // wave-uniform
-            const int gh = g0w + 32 * h;  // first Gaussian of this half
-            if (__ballot(need && (lane >> 5) == h) == 0) continue;
-            const float4 *src = reinterpret_cast<const float4 *>(p.shs) + (size_t)gh * 12;
-            float4 v[6];
-#pragma unroll
-            for (int q = 0; q < 6; q++) {  // 32 rows = 384 float4, 6 per lane, coalesced
-                const int f = q * 64 + lane;
-                v[q] = gh + f / 12 < p.P ? src[f] : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-            wave_lds_sync();  // the slice's previous readers (culling state, previous half) are done
-#pragma unroll
-            for (int q = 0; q < 6; q++) {
-                const int f = q * 64 + lane, row = f / 12;
-                *reinterpret_cast<float4 *>(sw + row * PRE_SH_STRIDE + (f - row * 12) * 4) = v[q];
-            }
-            wave_lds_sync();
-            if (need && (lane >> 5) == h) {
-                const float *row = sw + (lane & 31) * PRE_SH_STRIDE;
-                switch (p.D) {
-                    case 1: color_finish<1>(p, i, row); break;
-                    case 2: color_finish<2>(p, i, row); break;
-                    default: color_finish<3>(p, i, row); break;
-                }
-            }
-        }
-    }
 }
 
 // The last preprocess workgroup publishes {instance total lo, hi, big count, seq} to pinned host memory in ONE 16-B
@@ -411,41 +312,8 @@ __device__ __forceinline__ void publish_total(const PreprocessParams &p) {
 
 void launch_preprocess(hipStream_t s, const PreprocessParams &p) {
     if (p.P <= 0) return;
-    if (p.split) preprocess_kernel<PRE_SPLIT><<<div_up(p.P, 256), 256, 0, s>>>(p);
-    else if (p.late == 2 && tuning("pre_late_minw", 4) >= 6)
-        preprocess_kernel<PRE_LATE_DIRECT, 6><<<div_up(p.P, 256), 256, 0, s>>>(p);
-    else if (p.late == 2 && tuning("pre_late_minw", 4) == 5)
-        preprocess_kernel<PRE_LATE_DIRECT, 5><<<div_up(p.P, 256), 256, 0, s>>>(p);
-    else if (p.late == 2) preprocess_kernel<PRE_LATE_DIRECT, 4><<<div_up(p.P, 256), 256, 0, s>>>(p);
-    else if (p.late && tuning("pre_late_minw", 4) >= 6) preprocess_kernel<PRE_LATE, 6><<<div_up(p.P, 256), 256, 0, s>>>(p);
-    else if (p.late && tuning("pre_late_minw", 4) == 5) preprocess_kernel<PRE_LATE, 5><<<div_up(p.P, 256), 256, 0, s>>>(p);
-    else if (p.late) preprocess_kernel<PRE_LATE, 4><<<div_up(p.P, 256), 256, 0, s>>>(p);
-    else if (p.D == 3 && !p.colors_precomp && tuning("pre_shd", 1))
-        preprocess_kernel<PRE_FUSED, 4, 3><<<div_up(p.P, 256), 256, 0, s>>>(p);
-    else preprocess_kernel<PRE_FUSED><<<div_up(p.P, 256), 256, 0, s>>>(p);
-}
-
-// The colour half of a split preprocess: one thread per Gaussian the projection kept (radii != 0, exactly the ones
-// preprocess_gaussian colours), the same expressions as there, so the record, clamp bits and Jacobian are bitwise
-// those of the fused kernel.  A pure stream (192 B of coefficients in, 49 B out) at a fraction of the fused
-// kernel's registers, so it runs at full occupancy; the forward queues it behind the bucket count pass, where
-// the GPU would otherwise wait for the host's readback of the instance total.
-template <int DEG>
-__global__ __launch_bounds__(256) void preprocess_color_kernel(PreprocessParams p) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= p.P || p.radii[i] == 0) return;
-    color_finish<DEG>(p, i, p.shs + (size_t)i * p.M * 3);
-}
-
-void launch_preprocess_color(hipStream_t s, const PreprocessParams &p) {
-    if (p.P <= 0 || !p.split) return;
-    const dim3 grid(div_up(p.P, 256)), block(256);
-    switch (p.D) {
-        case 0: preprocess_color_kernel<0><<<grid, block, 0, s>>>(p); break;
-        case 1: preprocess_color_kernel<1><<<grid, block, 0, s>>>(p); break;
-        case 2: preprocess_color_kernel<2><<<grid, block, 0, s>>>(p); break;
-        default: preprocess_color_kernel<3><<<grid, block, 0, s>>>(p); break;
-    }
+    if (p.D == 3 && !p.colors_precomp) preprocess_kernel<3><<<div_up(p.P, 256), 256, 0, s>>>(p);
+    else preprocess_kernel<><<<div_up(p.P, 256), 256, 0, s>>>(p);
 }
 
 // Zero fill of the forward's counter block (16-B aligned, a multiple of 16 B) by a plain kernel: the runtime's fill
@@ -477,25 +345,13 @@ __global__ __launch_bounds__(256) void expand_kernel(ExpandParams p) {
     __shared__ uint32_t s_lo, s_n;
     const uint32_t u0 = blockIdx.x * EXP_TILE;
     const uint32_t u1 = min(p.R, u0 + (uint32_t)EXP_TILE);
-    if (p.exp_owner) {  // owners of the block starts from expand_owner_kernel: one load instead of two searches
-        if (threadIdx.x == 0) {
-            const uint32_t lo = p.exp_owner[blockIdx.x];
-            // the next block's first owner, or (last block) every remaining rank; ranks between two block starts
-            // own >= 1 instance each, so at most EXP_TILE + 1 of them
-            const uint32_t hi = blockIdx.x + 1 < gridDim.x ? p.exp_owner[blockIdx.x + 1] : p.P - 1;
-            s_lo = lo;
-            s_n = min(hi - lo + 1, (uint32_t)EXP_TILE + 1);
-        }
-    } else if (threadIdx.x < 64) {
-        // owner(u) = last r with inst_off[r] <= u.  Every Gaussian that renders owns >= 1 instance and the
-        // others are sorted to the end, so the owners of [u0, u1) are consecutive ranks.
-        const int lane = threadIdx.x;
-        const uint32_t lo = wave_last_le(p.inst_off, p.P, u0, lane);
-        const uint32_t hi = wave_last_le(p.inst_off, p.P, u1 - 1, lane);
-        if (lane == 0) {
-            s_lo = lo;
-            s_n = hi - lo + 1;
-        }
+    if (threadIdx.x == 0) {  // owners of the block starts from expand_owner_kernel: one load instead of two searches
+        const uint32_t lo = p.exp_owner[blockIdx.x];
+        // the next block's first owner, or (last block) every remaining rank; ranks between two block starts
+        // own >= 1 instance each, so at most EXP_TILE + 1 of them
+        const uint32_t hi = blockIdx.x + 1 < gridDim.x ? p.exp_owner[blockIdx.x + 1] : p.P - 1;
+        s_lo = lo;
+        s_n = min(hi - lo + 1, (uint32_t)EXP_TILE + 1);
     }
     __syncthreads();
     const uint32_t r_lo = s_lo, nr = s_n;  // nr <= EXP_TILE + 1
@@ -588,7 +444,7 @@ __global__ __launch_bounds__(256) void expand_owner_kernel(const uint32_t *__res
 
 void launch_expand(hipStream_t s, const ExpandParams &p) {
     if (p.R == 0) return;
-    if (p.exp_owner) expand_owner_kernel<<<div_up(p.P, 256u), 256, 0, s>>>(p.inst_off, p.P, p.exp_owner);
+    expand_owner_kernel<<<div_up(p.P, 256u), 256, 0, s>>>(p.inst_off, p.P, p.exp_owner);
     expand_kernel<<<div_up(p.R, EXP_TILE), 256, 0, s>>>(p);
 }
 

@@ -16,8 +16,6 @@ uint4 *stamp_buffer(int which);
 // ---- scan / sort (gsr_sort.hip) ----
 // Exclusive scan of n u32 values (optionally gathered through idx: v[i] = in[idx[i]]).
 // out has n+1 entries; out[n] = total.  overflow_flag (device u32) is set if the total exceeds 2^32-1.
-void launch_exclusive_scan(hipStream_t s, const uint32_t *in, const uint32_t *idx, uint32_t n, uint32_t *out,
-                           uint32_t *block_tmp, uint32_t *overflow_flag);
 // Same result in one launch (decoupled look-back); status (div_up(n + 1, SCAN_TILE) words) and *ticket zeroed.
 void launch_exclusive_scan_lookback(hipStream_t s, const uint32_t *in, const uint32_t *idx, uint32_t n, uint32_t *out,
                                     uint64_t *status, uint32_t *ticket, uint32_t *overflow_flag);
@@ -63,14 +61,11 @@ struct PreprocessParams {
     // to host_words[CNT_WORDS .. +4) in one 16-B store (the forward's readback without a copy or an event)
     uint32_t *host_words;
     uint32_t seq;
-    int split = 0;  // colour left to launch_preprocess_color (SH colours only)
-    int late = 0;   // colour evaluated at the end of the preprocess from LDS-staged coefficient rows (M = 16, 16-B aligned)
     int depth_range = 0;  // publish the kept depth keys' range with the instance total (relative depth sort)
     uint4 *stamps = nullptr;  // diagnostics ("stamp" knob): per wave {start, projected, culled, end}, {HW_ID, XCC_ID}
 };
 void launch_preprocess(hipStream_t s, const PreprocessParams &p);
 void launch_zero16(hipStream_t s, void *p, size_t bytes);  // bytes: a multiple of 16, p 16-B aligned
-void launch_preprocess_color(hipStream_t s, const PreprocessParams &p);  // the colour half of a split preprocess
 
 struct ExpandParams {
     uint32_t P, R;
@@ -78,7 +73,7 @@ struct ExpandParams {
     const uint32_t *order, *inst_off, *tiles;
     const uint4 *exp_rec;
     const uint4 *exp_sorted;  // optional: exp_rec already in depth order (read by rank, no gather)
-    uint32_t *exp_owner;      // optional: owner ranks of the block starts (div_up(R, EXP_TILE) + 1 words)
+    uint32_t *exp_owner;      // owner ranks of the block starts (div_up(R, EXP_TILE) + 1 words)
     uint32_t *keys_out, *inst_gid, *inst_start;
     uint16_t *keys16_out;     // optional: 16-bit tile keys (launch_radix_sort16) instead of keys_out
     uint32_t *inv_none;       // optional: inv, set to INV_NONE for every instance here (no separate fill)

@@ -22,111 +22,6 @@ __device__ __forceinline__ uint32_t scan_load(const uint32_t *__restrict__ in, c
     return GATHER ? in[idx[j]] : in[j];
 }
 
-template <bool GATHER>
-__global__ __launch_bounds__(256) void scan_reduce_kernel(const uint32_t *__restrict__ in,
-                                                          const uint32_t *__restrict__ idx, uint32_t n,
-                                                          uint32_t *__restrict__ block_sums) {
-    __shared__ uint32_t s_w[4];
-    const uint32_t base = blockIdx.x * SCAN_TILE;
-    uint32_t sum = 0;
-    for (int i = threadIdx.x; i < SCAN_TILE; i += 256) {
-        const uint32_t j = base + i;
-        if (j < n) sum += scan_load<GATHER>(in, idx, j);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) sum += (uint32_t)__shfl_xor((int)sum, o);
-    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = sum;
-    __syncthreads();
-    if (threadIdx.x == 0) block_sums[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-}
-
-// One block of 1024 threads scans up to SCAN_MAX_BLOCKS block sums in place (exclusive).
-__global__ __launch_bounds__(1024) void scan_sums_kernel(uint32_t *__restrict__ sums, uint32_t nb,
-                                                         uint32_t *__restrict__ total_out,
-                                                         uint32_t *__restrict__ overflow) {
-    __shared__ unsigned long long s_w[16];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    constexpr int PER = SCAN_MAX_BLOCKS / 1024;
-    uint32_t v[PER];
-    unsigned long long local = 0;
-#pragma unroll
-    for (int k = 0; k < PER; k++) {
-        const uint32_t j = tid * PER + k;
-        v[k] = j < nb ? sums[j] : 0u;
-        local += v[k];
-    }
-    // inclusive scan of 64-bit thread totals across the block
-    unsigned long long inc = local;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        unsigned long long t = __shfl_up(inc, o);
-        if (lane >= o) inc += t;
-    }
-    if (lane == 63) s_w[w] = inc;
-    __syncthreads();
-    unsigned long long woff = 0;
-    for (int i = 0; i < w; i++) woff += s_w[i];
-    unsigned long long run = woff + inc - local;
-#pragma unroll
-    for (int k = 0; k < PER; k++) {
-        const uint32_t j = tid * PER + k;
-        if (j < nb) sums[j] = (uint32_t)run;
-        run += v[k];
-    }
-    if (tid == 1023) {
-        if (total_out) *total_out = (uint32_t)run;
-        if (overflow && run > 0xffffffffull) *overflow = 1u;
-    }
-}
-
-template <bool GATHER>
-__global__ __launch_bounds__(256) void scan_down_kernel(const uint32_t *__restrict__ in,
-                                                        const uint32_t *__restrict__ idx, uint32_t n,
-                                                        const uint32_t *__restrict__ block_off,
-                                                        uint32_t *__restrict__ out) {
-    __shared__ uint32_t s_w[4];
-    constexpr int PER = SCAN_TILE / 256;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint32_t base = blockIdx.x * SCAN_TILE + tid * PER;
-    uint32_t v[PER];
-    uint32_t local = 0;
-#pragma unroll
-    for (int k = 0; k < PER; k++) {
-        const uint32_t j = base + k;
-        v[k] = j < n ? scan_load<GATHER>(in, idx, j) : 0u;
-        local += v[k];
-    }
-    uint32_t inc = wave_inclusive_scan(local, lane);
-    if (lane == 63) s_w[w] = inc;
-    __syncthreads();
-    uint32_t run = block_off[blockIdx.x] + inc - local;
-    for (int i = 0; i < w; i++) run += s_w[i];
-#pragma unroll
-    for (int k = 0; k < PER; k++) {
-        const uint32_t j = base + k;
-        if (j < n) out[j] = run;
-        run += v[k];
-    }
-}
-
-void launch_exclusive_scan(hipStream_t s, const uint32_t *in, const uint32_t *idx, uint32_t n, uint32_t *out,
-                           uint32_t *block_tmp, uint32_t *overflow_flag) {
-    if (n == 0) {
-        (void)hipMemsetAsync(out, 0, sizeof(uint32_t), s);
-        return;
-    }
-    const uint32_t nb = div_up(n, SCAN_TILE);
-    if (idx) {
-        scan_reduce_kernel<true><<<nb, 256, 0, s>>>(in, idx, n, block_tmp);
-        scan_sums_kernel<<<1, 1024, 0, s>>>(block_tmp, nb, out + n, overflow_flag);
-        scan_down_kernel<true><<<nb, 256, 0, s>>>(in, idx, n, block_tmp, out);
-    } else {
-        scan_reduce_kernel<false><<<nb, 256, 0, s>>>(in, nullptr, n, block_tmp);
-        scan_sums_kernel<<<1, 1024, 0, s>>>(block_tmp, nb, out + n, overflow_flag);
-        scan_down_kernel<false><<<nb, 256, 0, s>>>(in, nullptr, n, block_tmp, out);
-    }
-}
-
 // Single-kernel exclusive scan with decoupled look-back (one launch instead of three).  Block ids come from an
 // atomic ticket so a block only waits on blocks that started before it; its first wave inspects 64
 // predecessors per round trip.  Status words: 2-bit flag | 62-bit inclusive/aggregate sum.
@@ -946,7 +841,7 @@ static void launch_radix_sort_multi(hipStream_t s, SortScratch &sc, uint32_t n, 
     const bool one = BINS != RS_BINS || (tuning("rs_cscan", 1) != 0 && n <= RS_ONESWEEP_MAX_N);
     // count-scan rows per workgroup: 64 for long 256-bin matrices ("rs_cs64"; the 16-bit tile sort at 16 keys per
     // thread has ~9.6 k rows at cfg 5), else 32
-    const uint32_t CS_C = (BINS == RS_BINS && nb > 4096 && tuning("rs_cs64", 1)) ? 64u : 32u;
+    const uint32_t CS_C = (BINS == RS_BINS && nb > 4096) ? 64u : 32u;
     const uint32_t nch = div_up(nb, CS_C);  // <= RS_MAX_PASSES * nb_os rows of sc.status per pass
     const uint32_t pat = (uint32_t)tuning("lb_patience", 1 << 16);
     const int force = tuning("lb_force", 0);

@@ -211,7 +211,7 @@ void launch_sh_backward_views(hipStream_t s, int P, int D, int M, int V, int chu
                               const float *campos, const float *dcolors_sh, float *dsh) {
     if (P <= 0) return;
     const dim3 grid(div_up(P, 256)), block(256);
-    const bool staged = M == 16 && (((uintptr_t)dsh) & 15) == 0 && tuning("views_staged", 1);
+    const bool staged = M == 16 && (((uintptr_t)dsh) & 15) == 0;
     const int L = chunk_len <= 0 || chunk_len > P ? P : chunk_len;
 #define GSR_VIEWS(D_, S_) sh_backward_views_kernel<D_, S_><<<grid, block, 0, s>>>(P, M, V, L, means3D, campos, dcolors_sh, dsh)
     switch (D) {

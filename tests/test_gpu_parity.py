@@ -585,7 +585,7 @@ def test_densify_stats_from_backward(gpu_device):
 
 
 @pytest.mark.parametrize("knobs", [{"fwd_parts": 1}, {"fwd_parts": 2}, {"fwd_parts": 4}, {"fwd_whole_waves": 6},
-                                   {"strip_exact": 0}, {"bwd_lastc": 1}, {"bwd_parts": 2}, {"bwd_parts": 4},
+                                   {"strip_exact": 0}, {"bwd_parts": 2}, {"bwd_parts": 4},
                                    {"bwd_union": 1}, {"fwd_parts": 1, "bwd_union": 1}, {"fwd_parts": 1, "smask": 0}])
 def test_composite_variants_are_bitwise_identical(gpu_device, knobs):
     """Every composite launch shape gives the same bits: a tile composited whole (4 pixels per lane) or in 2 / 4
@@ -599,8 +599,7 @@ def test_composite_variants_are_bitwise_identical(gpu_device, knobs):
     from gaussian_splatting_lightning_amd import _native
     inp = scene_inputs(200_000, 1280, 720, sh_degree=3, seed=4, bg=(0.3, 0.6, 0.9))
     dc, di = upstream(1280, 720, 4)
-    defaults = {"fwd_parts": 0, "fwd_whole_waves": 8, "strip_exact": 1, "bwd_lastc": 0, "bwd_parts": 0,
-                "bwd_union": -1, "smask": 1}
+    defaults = {"fwd_parts": 0, "fwd_whole_waves": 8, "strip_exact": 1, "bwd_parts": 0, "bwd_union": -1, "smask": 1}
     try:
         _native.set_tuning("bwd_seg", 0)  # 3600 tiles: the default walks segments (test_segmented_backward)
         _native.set_tuning("bwd_parts", 1)  # the reference side: one wave per tile (the default here is 2)
@@ -786,34 +785,6 @@ def test_tile_sort_digit_width_is_invisible(gpu_device, db):
         assert np.array_equal(a[k], b[k]), k
     for k in ("color", "invdepth", "radii"):
         assert np.array_equal(ref[k], alt[k]), k
-
-
-@pytest.mark.parametrize("mode", ["split", "late4", "late6", "direct", "runtime_degree"])
-@pytest.mark.parametrize("deg,cdeg,bucket", [(3, 3, 1), (2, 3, 1), (1, 3, 0), (1, 1, 0), (0, 0, 1)])
-def test_split_colour_preprocess_is_bitwise_the_fused_one(gpu_device, deg, cdeg, bucket, mode):
-    """The SH colour evaluated by its own kernel behind the bucket count pass ("pre_split" 1), or at the end of the
-    preprocess from LDS-staged coefficient rows ("pre_late" 1, 16 coefficients; built for 4 or 6 waves per SIMD) or
-    from rows read directly ("pre_late" 2), or with the SH degree dispatched at run time instead of the compile-time
-    degree-3 kernel ("pre_shd" 0), gives bitwise the records, outputs and gradients of the fused preprocess (colour inside the
-    projection)."""
-    knobs = {"split": dict(pre_split=1, pre_late=0), "late4": dict(pre_split=0, pre_late=1, pre_late_minw=4),
-             "late6": dict(pre_split=0, pre_late=1, pre_late_minw=6),
-             "direct": dict(pre_split=0, pre_late=2, pre_late_minw=6),
-             "runtime_degree": dict(pre_split=0, pre_late=0, pre_shd=0)}[mode]
-    from gaussian_splatting_lightning_amd import _native
-    inp = scene_inputs(60_000, 640, 480, sh_degree=deg, seed=12 + deg, coeff_degree=cdeg)
-    dc, di = upstream(640, 480, 12 + deg)
-    with _native.tuned(bucket=bucket, pre_split=0, pre_late=0):
-        ref = run_hip(inp, gpu_device, dc, di)
-    with _native.tuned(bucket=bucket, **knobs):
-        alt = run_hip(inp, gpu_device, dc, di)
-    a, b = hip_state_arrays(ref), hip_state_arrays(alt)
-    for key in ("rec", "clamped", "ranges", "point_list", "n_contrib"):
-        assert np.array_equal(a[key], b[key]), key
-    for key in ("color", "invdepth", "radii"):
-        assert np.array_equal(ref[key], alt[key]), key
-    for key in GRADS:
-        assert np.array_equal(ref["grads"][key], alt["grads"][key]), key
 
 
 @pytest.mark.parametrize("n,depth_scale", [(150_000, 1.0), (150_000, 40.0), (2_000, 1.0)])
