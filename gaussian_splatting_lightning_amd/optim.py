@@ -62,9 +62,12 @@ class GaussianAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        fused = None
         if sh_views is not None:
-            fused = self._sh_views_args(*sh_views)
+            # first: the expansion reads means3D, which this step's xyz group is about to update (the gradient
+            # belongs to the forward's positions)
+            a, (b1, b2, eps), dev = self._sh_views_args(*sh_views)
+            _native.check(_native.load().gsr_adam_sh_views_step(ctypes.byref(a), b1, b2, eps, _stream_handle(dev)),
+                          "gsr_adam_sh_views_step")
         skip = {id(t) for t in sh_views[:2]} if sh_views is not None else set()
         batches = {}
         keep_alive = []
@@ -104,11 +107,6 @@ class GaussianAdam(torch.optim.Optimizer):
                 chunk = groups[i:i + _MAX_GROUPS]
                 arr = (_native.AdamGroup * len(chunk))(*chunk)
                 _native.check(lib.gsr_adam_step(arr, len(chunk), b1, b2, eps, stream), "gsr_adam_step")
-        if fused is not None:
-            a, (b1, b2, eps), dev = fused
-            lib = _native.load()
-            _native.check(lib.gsr_adam_sh_views_step(ctypes.byref(a), b1, b2, eps, _stream_handle(dev)),
-                          "gsr_adam_sh_views_step")
         del keep_alive
         return loss
 
