@@ -63,7 +63,8 @@ class AdamShViewsArgs(ctypes.Structure):  # include/gsrast.h gsr_adam_sh_views_a
                 ("dc_param", _fp), ("dc_exp_avg", _fp), ("dc_exp_avg_sq", _fp), ("dc_lr", ctypes.c_double),
                 ("dc_step", ctypes.c_int64),
                 ("rest_param", _fp), ("rest_exp_avg", _fp), ("rest_exp_avg_sq", _fp), ("rest_lr", ctypes.c_double),
-                ("rest_step", ctypes.c_int64), ("param_row_stride", ctypes.c_int64)]
+                ("rest_step", ctypes.c_int64), ("param_row_stride", ctypes.c_int64),
+                ("moment_row_stride", ctypes.c_int64)]
 
 
 class DensifyArgs(ctypes.Structure):

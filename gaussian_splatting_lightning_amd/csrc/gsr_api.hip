@@ -883,8 +883,14 @@ int gsr_adam_sh_views_step(const gsr_adam_sh_views_args *a, double beta1, double
     L.P = a->P; L.V = a->V;
     L.L = (a->chunk_len == 0 || a->chunk_len >= a->P) ? a->P : (int)a->chunk_len;
     L.means3D = a->means3D; L.campos = a->campos; L.dc = a->dL_dcolors_sh;
-    if (a->param_row_stride != 0 && a->param_row_stride != 48)
-        return fail(GSR_ERR_ARG, "adam sh views: param_row_stride must be 0 (packed) or 48 (one (P, 16, 3) tensor)");
+    if ((a->param_row_stride != 0 && a->param_row_stride != 48) || (a->moment_row_stride != 0 && a->moment_row_stride != 48))
+        return fail(GSR_ERR_ARG, "adam sh views: row strides must be 0 (packed) or 48 (one (P, 16, 3) tensor)");
+    if (a->moment_row_stride == 48 && a->param_row_stride != 48)
+        return fail(GSR_ERR_ARG, "adam sh views: joint moments need the joint parameter");
+    if (a->param_row_stride == 48 && (a->rest_param != a->dc_param + 3 ||
+                                      (a->moment_row_stride == 48 && (a->rest_exp_avg != a->dc_exp_avg + 3 ||
+                                                                      a->rest_exp_avg_sq != a->dc_exp_avg_sq + 3))))
+        return fail(GSR_ERR_ARG, "adam sh views: a joint tensor's rest block must start 3 floats after its dc block");
     auto group = [&](AdamShGroup &g, float *p, float *m, float *v, double lr, int64_t step, int64_t width) {
         const double bc1 = 1.0 - std::pow(beta1, (double)step), bc2 = 1.0 - std::pow(beta2, (double)step);
         g.param = p; g.exp_avg = m; g.exp_avg_sq = v;
@@ -902,6 +908,8 @@ int gsr_adam_sh_views_step(const gsr_adam_sh_views_args *a, double beta1, double
     L.beta2 = (float)beta2;
     L.one_minus_beta2 = (float)(1.0 - beta2);
     L.eps = (float)eps;
+    L.joint = a->moment_row_stride == 48 &&
+              ((((uintptr_t)a->dc_param) | ((uintptr_t)a->dc_exp_avg) | ((uintptr_t)a->dc_exp_avg_sq)) & 15) == 0;
     hipStream_t stream = (hipStream_t)stream_ptr;
     StreamDeviceGuard device_guard(stream);
     GSR_STAGE(ST_ADAM_SH, 0, launch_adam_sh_views(stream, L, a->D));

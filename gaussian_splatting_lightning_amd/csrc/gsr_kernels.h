@@ -262,6 +262,7 @@ struct AdamShLaunch {
     AdamShGroup dc_group, rest_group;
     float one_minus_beta1, beta2, one_minus_beta2, eps;
     int vec4;
+    int joint;  // parameter and moments each one 16-B aligned (P, 16, 3) tensor (dc_group's pointers: its base)
 };
 void launch_adam_sh_views(hipStream_t s, const AdamShLaunch &L, int D);
 

@@ -126,85 +126,157 @@ __device__ __forceinline__ void adam_elem(float &p, float g, float &m, float &v,
 // the staged row (W = 3 for features_dc, 45 for features_rest).  The moments are contiguous (row r's elements at
 // r W); the parameter either too (param_stride == W) or rows of a joint (P, 16, 3) SH tensor (param_stride == 48,
 // the pointer at the group's first column): then the parameter is read and written per element.
-template <int W, int C0>
+template <int W, int C0, bool PACKED>
 __device__ __forceinline__ void adam_block(const AdamShGroup &G, const AdamShLaunch &L, const float *sw, int lane,
                                            int64_t r0, int64_t rows_end, bool vec4) {
     constexpr int N = 32 * W;
     const int64_t e0 = r0 * W, e_end = rows_end * W;
-    const bool packed = G.param_stride == W;
-    for (int q = lane; 4 * q < N; q += 64) {
+    // the block's parameter base, then 32-bit offsets within it
+    float *const pb = G.param + (PACKED ? e0 : r0 * G.param_stride);
+    const int ps = (int)G.param_stride;
+    auto pidx = [&](int e) { return PACKED ? e : (e / W) * ps + e % W; };
+    if (vec4 && e0 + N <= e_end) {
+        // a whole block: each lane's loads (parameter, both moments) for SUB float4s are issued together, then the
+        // updates and stores -- a load-update-store loop waited for each iteration's loads in turn (the stores may
+        // alias them)
+        constexpr int NQ = (N / 4 + 63) / 64, SUB = 3;
+#pragma unroll
+        for (int i0 = 0; i0 < NQ; i0 += SUB) {
+            float4 Pv[SUB], Mv[SUB], Vv[SUB];
+#pragma unroll
+            for (int i = 0; i < SUB && i0 + i < NQ; i++) {
+                const int e = 4 * (lane + 64 * (i0 + i));
+                if (e >= N) continue;
+                Mv[i] = *reinterpret_cast<const float4 *>(G.exp_avg + e0 + e);
+                Vv[i] = *reinterpret_cast<const float4 *>(G.exp_avg_sq + e0 + e);
+                if (PACKED)
+                    Pv[i] = *reinterpret_cast<const float4 *>(pb + e);
+                else
+                    Pv[i] = make_float4(pb[pidx(e)], pb[pidx(e + 1)], pb[pidx(e + 2)], pb[pidx(e + 3)]);
+            }
+#pragma unroll
+            for (int i = 0; i < SUB && i0 + i < NQ; i++) {
+                const int e = 4 * (lane + 64 * (i0 + i));
+                if (e >= N) continue;
+                adam_elem(Pv[i].x, sw[(e / W) * VIEWS_STRIDE + e % W + C0], Mv[i].x, Vv[i].x, G, L);
+                adam_elem(Pv[i].y, sw[((e + 1) / W) * VIEWS_STRIDE + (e + 1) % W + C0], Mv[i].y, Vv[i].y, G, L);
+                adam_elem(Pv[i].z, sw[((e + 2) / W) * VIEWS_STRIDE + (e + 2) % W + C0], Mv[i].z, Vv[i].z, G, L);
+                adam_elem(Pv[i].w, sw[((e + 3) / W) * VIEWS_STRIDE + (e + 3) % W + C0], Mv[i].w, Vv[i].w, G, L);
+                if (PACKED) {
+                    *reinterpret_cast<float4 *>(pb + e) = Pv[i];
+                } else {
+                    pb[pidx(e)] = Pv[i].x;
+                    pb[pidx(e + 1)] = Pv[i].y;
+                    pb[pidx(e + 2)] = Pv[i].z;
+                    pb[pidx(e + 3)] = Pv[i].w;
+                }
+                *reinterpret_cast<float4 *>(G.exp_avg + e0 + e) = Mv[i];
+                *reinterpret_cast<float4 *>(G.exp_avg_sq + e0 + e) = Vv[i];
+            }
+        }
+        return;
+    }
+    for (int q = lane; 4 * q < N; q += 64) {  // the last, partial block (or unaligned arrays): element by element
         const int e = 4 * q;
         const int64_t ge = e0 + e;
         if (ge >= e_end) break;
-        if (vec4 && ge + 4 <= e_end) {
-            float4 m = *reinterpret_cast<const float4 *>(G.exp_avg + ge);
-            float4 v = *reinterpret_cast<const float4 *>(G.exp_avg_sq + ge);
-            float p[4];
-            if (packed) {
-                const float4 p4 = *reinterpret_cast<const float4 *>(G.param + ge);
-                p[0] = p4.x; p[1] = p4.y; p[2] = p4.z; p[3] = p4.w;
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; j++) p[j] = G.param[(r0 + (e + j) / W) * G.param_stride + (e + j) % W];
-            }
-            adam_elem(p[0], sw[(e / W) * VIEWS_STRIDE + e % W + C0], m.x, v.x, G, L);
-            adam_elem(p[1], sw[((e + 1) / W) * VIEWS_STRIDE + (e + 1) % W + C0], m.y, v.y, G, L);
-            adam_elem(p[2], sw[((e + 2) / W) * VIEWS_STRIDE + (e + 2) % W + C0], m.z, v.z, G, L);
-            adam_elem(p[3], sw[((e + 3) / W) * VIEWS_STRIDE + (e + 3) % W + C0], m.w, v.w, G, L);
-            if (packed) {
-                *reinterpret_cast<float4 *>(G.param + ge) = make_float4(p[0], p[1], p[2], p[3]);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; j++) G.param[(r0 + (e + j) / W) * G.param_stride + (e + j) % W] = p[j];
-            }
-            *reinterpret_cast<float4 *>(G.exp_avg + ge) = m;
-            *reinterpret_cast<float4 *>(G.exp_avg_sq + ge) = v;
-        } else {
-            for (int j = 0; j < 4 && ge + j < e_end; j++) {
-                const int64_t pi = (r0 + (e + j) / W) * G.param_stride + (e + j) % W;
-                float p = G.param[pi], m = G.exp_avg[ge + j], v = G.exp_avg_sq[ge + j];
-                adam_elem(p, sw[((e + j) / W) * VIEWS_STRIDE + (e + j) % W + C0], m, v, G, L);
-                G.param[pi] = p;
-                G.exp_avg[ge + j] = m;
-                G.exp_avg_sq[ge + j] = v;
-            }
+        for (int j = 0; j < 4 && ge + j < e_end; j++) {
+            const int pi = pidx(e + j);
+            float p = pb[pi], m = G.exp_avg[ge + j], v = G.exp_avg_sq[ge + j];
+            adam_elem(p, sw[((e + j) / W) * VIEWS_STRIDE + (e + j) % W + C0], m, v, G, L);
+            pb[pi] = p;
+            G.exp_avg[ge + j] = m;
+            G.exp_avg_sq[ge + j] = v;
         }
     }
 }
 
-template <int DEG>
+// Fully joint layout: parameter and both moments are (P, 16, 3) tensors whose [:, :1] / [:, 1:] blocks are the two
+// groups, so a half-wave's 32 rows are ONE contiguous 384-float4 run of each array, read and written as coalesced
+// float4s; an element's group (its step size) is its column < 3.
+__device__ __forceinline__ void adam_block_joint(const AdamShLaunch &L, const float *sw, int lane, int64_t r0,
+                                                 int64_t rows_end) {
+    constexpr int N = 32 * 48, SUB = 3;
+    const int64_t e0 = r0 * 48, e_end = rows_end * 48;
+    float *const pb = L.dc_group.param + e0, *const mb = L.dc_group.exp_avg + e0, *const vb = L.dc_group.exp_avg_sq + e0;
+    const bool whole = e0 + N <= e_end;
+#pragma unroll
+    for (int i0 = 0; i0 < 6; i0 += SUB) {
+        float4 Pv[SUB], Mv[SUB], Vv[SUB];
+#pragma unroll
+        for (int i = 0; i < SUB; i++) {
+            const int e = 4 * (lane + 64 * (i0 + i));
+            if (!whole && e0 + e >= e_end) continue;  // rows are whole float4s: 48 = 12 x 4
+            Pv[i] = *reinterpret_cast<const float4 *>(pb + e);
+            Mv[i] = *reinterpret_cast<const float4 *>(mb + e);
+            Vv[i] = *reinterpret_cast<const float4 *>(vb + e);
+        }
+#pragma unroll
+        for (int i = 0; i < SUB; i++) {
+            const int e = 4 * (lane + 64 * (i0 + i));
+            if (!whole && e0 + e >= e_end) continue;
+            const int row = e / 48, col = e - 48 * row;  // col % 4 == 0: at most col 0's float4 mixes the groups
+            const float *g = sw + row * VIEWS_STRIDE + col;
+            const AdamShGroup &G0 = col == 0 ? L.dc_group : L.rest_group;
+            adam_elem(Pv[i].x, g[0], Mv[i].x, Vv[i].x, G0, L);
+            adam_elem(Pv[i].y, g[1], Mv[i].y, Vv[i].y, G0, L);
+            adam_elem(Pv[i].z, g[2], Mv[i].z, Vv[i].z, G0, L);
+            adam_elem(Pv[i].w, g[3], Mv[i].w, Vv[i].w, L.rest_group, L);
+            *reinterpret_cast<float4 *>(pb + e) = Pv[i];
+            *reinterpret_cast<float4 *>(mb + e) = Mv[i];
+            *reinterpret_cast<float4 *>(vb + e) = Vv[i];
+        }
+    }
+}
+
+// LAYOUT 0: packed groups (tensors of their own); 1: the parameter is one (P, 16, 3) tensor, the moments packed;
+// 2: parameter and moments each one (P, 16, 3) tensor (adam_block_joint).
+template <int DEG, int LAYOUT>
 __global__ __launch_bounds__(256) void adam_sh_views_kernel(AdamShLaunch L) {
     constexpr int NB = (DEG + 1) * (DEG + 1);
-    __shared__ __attribute__((aligned(16))) float s_row[4][32 * VIEWS_STRIDE];
+    // the wave's 64 gradient rows all staged first (two half-wave stores), so the 48 accumulators are dead before the
+    // Adam phase's batched loads start
+    __shared__ __attribute__((aligned(16))) float s_row[4][64 * VIEWS_STRIDE];
     const int P = L.P;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int ii = i < P ? i : P - 1;
-    float acc[3 * NB];
-    views_accumulate<DEG>(ii, P, L.V, L.L, L.means3D, L.campos, L.dc, acc);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    float *sw = s_row[w];
+    {
+        float acc[3 * NB];
+        views_accumulate<DEG>(ii, P, L.V, L.L, L.means3D, L.campos, L.dc, acc);
+        stage_rows<NB>(s_row[w], lane, 0, acc);
+        stage_rows<NB>(s_row[w] + 32 * VIEWS_STRIDE, lane, 1, acc);
+    }
+    wave_lds_sync();
     const int64_t row0 = (int64_t)blockIdx.x * 256 + (int64_t)w * 64;
-#pragma unroll
+#pragma unroll 1
     for (int h = 0; h < 2; h++) {
-        wave_lds_sync();
-        stage_rows<NB>(sw, lane, h, acc);
-        wave_lds_sync();
+        const float *sw = s_row[w] + 32 * VIEWS_STRIDE * h;
         const int64_t r = row0 + 32 * h;
         if (r >= P) break;
-        adam_block<3, 0>(L.dc_group, L, sw, lane, r, P, L.vec4);
-        adam_block<45, 3>(L.rest_group, L, sw, lane, r, P, L.vec4);
+        if constexpr (LAYOUT == 2) {
+            adam_block_joint(L, sw, lane, r, P);
+        } else {
+            adam_block<3, 0, LAYOUT == 0>(L.dc_group, L, sw, lane, r, P, L.vec4);
+            adam_block<45, 3, LAYOUT == 0>(L.rest_group, L, sw, lane, r, P, L.vec4);
+        }
     }
 }
 
 void launch_adam_sh_views(hipStream_t s, const AdamShLaunch &L, int D) {
     if (L.P <= 0) return;
     const dim3 grid(div_up(L.P, 256)), block(256);
+    const int layout = L.joint ? 2 : L.dc_group.param_stride == 3 ? 0 : 1;
+#define GSR_ADAM_SH(D_) (layout == 2 ? adam_sh_views_kernel<D_, 2><<<grid, block, 0, s>>>(L) \
+                         : layout == 0 ? adam_sh_views_kernel<D_, 0><<<grid, block, 0, s>>>(L) \
+                                       : adam_sh_views_kernel<D_, 1><<<grid, block, 0, s>>>(L))
     switch (D) {
-        case 0: adam_sh_views_kernel<0><<<grid, block, 0, s>>>(L); break;
-        case 1: adam_sh_views_kernel<1><<<grid, block, 0, s>>>(L); break;
-        case 2: adam_sh_views_kernel<2><<<grid, block, 0, s>>>(L); break;
-        default: adam_sh_views_kernel<3><<<grid, block, 0, s>>>(L); break;
+        case 0: GSR_ADAM_SH(0); break;
+        case 1: GSR_ADAM_SH(1); break;
+        case 2: GSR_ADAM_SH(2); break;
+        default: GSR_ADAM_SH(3); break;
     }
+#undef GSR_ADAM_SH
 }
 
 void launch_sh_backward_views(hipStream_t s, int P, int D, int M, int V, int chunk_len, const float *means3D,

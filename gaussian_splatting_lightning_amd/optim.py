@@ -136,6 +136,14 @@ class GaussianAdam(torch.optim.Optimizer):
                                    "device")
         if grad.means3D.shape != (P, 3) or grad.factors.numel() != V * P * 3:
             raise RuntimeError("sh_views: means3D (P, 3) and factors (V * P * 3) do not match the parameters")
+        if joint and len(self.state[dc]) == 0 and len(self.state[rest]) == 0:
+            # a joint parameter gets joint moments too: each moment is one (P, 16, 3) tensor whose column blocks are
+            # the two groups' states, so the update streams three arrays of one layout
+            jm = torch.zeros(P, 16, 3, dtype=torch.float32, device=dc.device)
+            jv = torch.zeros_like(jm)
+            for t, sl in ((dc, slice(0, 1)), (rest, slice(1, 16))):
+                self.state[t].update(step=torch.tensor(0.0, dtype=torch.float32), exp_avg=jm[:, sl],
+                                     exp_avg_sq=jv[:, sl])
         steps = []
         for t in (dc, rest):
             state = self.state[t]
@@ -146,13 +154,21 @@ class GaussianAdam(torch.optim.Optimizer):
             state["step"] += 1
             steps.append(int(state["step"].item()))
         sd, sr = self.state[dc], self.state[rest]
+        joint_m = joint and all(
+            sd[k].stride() == (48, 3, 1) and sr[k].stride() == (48, 3, 1) and sr[k].data_ptr() == sd[k].data_ptr() + 12
+            for k in ("exp_avg", "exp_avg_sq"))
+        for t, st, w in ((dc, sd, 1), (rest, sr, 15)):
+            for k in ("exp_avg", "exp_avg_sq"):
+                m = st[k]
+                if tuple(m.shape) != (P, w, 3) or m.dtype != torch.float32 or not (joint_m or m.is_contiguous()):
+                    raise RuntimeError("sh_views: optimizer state does not match its parameter")
         a = _native.AdamShViewsArgs(
             P=P, D=int(grad.sh_degree), M=16, V=V, chunk_len=int(grad.chunk_len), means3D=grad.means3D.data_ptr(),
             campos=grad.campos.data_ptr(), dL_dcolors_sh=grad.factors.data_ptr(),
             dc_param=dc.data_ptr(), dc_exp_avg=sd["exp_avg"].data_ptr(), dc_exp_avg_sq=sd["exp_avg_sq"].data_ptr(),
             dc_lr=float(gd["lr"]), dc_step=steps[0], rest_param=rest.data_ptr(), rest_exp_avg=sr["exp_avg"].data_ptr(),
             rest_exp_avg_sq=sr["exp_avg_sq"].data_ptr(), rest_lr=float(gr["lr"]), rest_step=steps[1],
-            param_row_stride=48 if joint else 0)
+            param_row_stride=48 if joint else 0, moment_row_stride=48 if joint_m else 0)
         return a, (float(gd["betas"][0]), float(gd["betas"][1]), float(gd["eps"])), dc.device
 
 

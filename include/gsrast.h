@@ -214,6 +214,9 @@ typedef struct gsr_adam_sh_views_args {
      * 48 = the two groups are the column blocks of ONE (P, 16, 3) tensor (dc_param = its base, rest_param = base + 3),
      * which the forward reads as shs without a concatenation.  The moments are always packed. */
     int64_t param_row_stride;
+    /* the same for the moments: 0 = packed, 48 = exp_avg / exp_avg_sq are each one (P, 16, 3) tensor too (dc_* the
+     * base, rest_* = base + 3).  With both at 48 every array is streamed as one coalesced run per 32 rows. */
+    int64_t moment_row_stride;
 } gsr_adam_sh_views_args;
 int gsr_adam_sh_views_step(const gsr_adam_sh_views_args *a, double beta1, double beta2, double eps, void *stream);
 

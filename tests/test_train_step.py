@@ -36,14 +36,15 @@ def _params(P, seed, dev, layout="packed"):
         r = buf[1:].view(P, 15, 3)
         r.copy_(rest)
         return torch.nn.Parameter(dc.to(dev)), torch.nn.Parameter(r)
-    if layout == "joint":  # the column blocks of one (P, 16, 3) tensor (what the forward reads as shs)
+    if layout.startswith("joint"):  # the column blocks of one (P, 16, 3) tensor (what the forward reads as shs)
         shs = torch.cat([dc, rest], 1).to(dev)
         return shs[:, :1], shs[:, 1:]
     return torch.nn.Parameter(dc.to(dev)), torch.nn.Parameter(rest.to(dev))
 
 
 @pytest.mark.parametrize("deg,chunk_len,layout", [(3, 0, "packed"), (3, 2560, "packed"), (1, 0, "packed"),
-                                                  (0, 1024, "packed"), (3, 0, "misaligned"), (3, 2560, "joint")])
+                                                  (0, 1024, "packed"), (3, 0, "misaligned"), (3, 2560, "joint"),
+                                                  (2, 0, "joint"), (3, 0, "joint_packed_state")])
 def test_fused_sh_adam_is_bitwise_expand_then_adam(gpu_device, deg, chunk_len, layout):
     from gaussian_splatting_lightning_amd.optim import GaussianAdam, ShViewsGradient
     from gaussian_splatting_lightning_amd.rasterizer import sh_backward_views
@@ -57,6 +58,10 @@ def test_fused_sh_adam_is_bitwise_expand_then_adam(gpu_device, deg, chunk_len, l
                            {"params": [r], "lr": 0.0025 / 20.0, "name": "f_rest"}]
     opt_a = GaussianAdam(groups(a_dc, a_rest), lr=0.0, eps=1e-15)
     opt_b = GaussianAdam(groups(b_dc, b_rest), lr=0.0, eps=1e-15)
+    if layout == "joint_packed_state":  # a joint parameter whose moments are tensors of their own (layout 1)
+        for t in (b_dc, b_rest):
+            opt_b.state[t].update(step=torch.tensor(0.0), exp_avg=torch.zeros(t.shape, device=dev),
+                                  exp_avg_sq=torch.zeros(t.shape, device=dev))
     for step in range(3):
         campos = (torch.randn(V, 3, generator=g) * 3.0).to(dev)
         f = _factors(P, V, chunk_len, 100 + step, dev)
@@ -73,8 +78,10 @@ def test_fused_sh_adam_is_bitwise_expand_then_adam(gpu_device, deg, chunk_len, l
         assert int(opt_b.state[pb]["step"]) == 3
     moved = a_rest if deg > 0 else a_dc  # degree 0: the higher coefficients see zero gradients and stay
     assert not torch.equal(moved.detach().cpu(), _params(P, 1, "cpu")[0 if deg == 0 else 1].detach())
-    if layout == "joint":
+    if layout.startswith("joint"):
         assert b_dc.data_ptr() + 12 == b_rest.data_ptr()  # updated in place, still one tensor
+    if layout == "joint":  # the moments were made joint too (one coalesced stream per array)
+        assert opt_b.state[b_rest]["exp_avg"].data_ptr() == opt_b.state[b_dc]["exp_avg"].data_ptr() + 12
 
 
 def _free_port():
