@@ -252,29 +252,34 @@ def main():
 
     # ---- training step (separate pass, extra field, not the headline): forward + backward + exchange + Adam ----
     # The reference steps torch.optim.Adam(eps=1e-15) over its six per-Gaussian groups right after the backward
-    # (gs_lightning_module.py:114-134,168-170).  Here the Adam step runs on the rasterizer inputs themselves (means3D,
-    # scales, rotations, opacities and the SH coefficients as features_dc / features_rest, i.e. without the
-    # reference's exp / sigmoid / normalize activations in front of three of them), with the learning rates of
-    # configs/train_gs.yaml; the SH groups take their gradient in factored form through the fused SH Adam
-    # (compact exchange, GaussianAdam.step(sh_views=...)), so no (P, 16, 3) gradient is written at any N.
+    # (gs_lightning_module.py:114-134,168-170).  As there, the optimizer steps the RAW parameters (xyz, features_dc,
+    # features_rest and the pre-activation _opacity / _scaling / _rotation of gaussian_model.py) and the rasterizer
+    # sees their activations (sigmoid / exp / normalize: activations.activate and its chain rule, one launch each),
+    # with the learning rates of configs/train_gs.yaml; the SH groups take their gradient in factored form through
+    # the fused SH Adam (compact exchange, GaussianAdam.step(sh_views=...)), so no (P, 16, 3) gradient is written.
     train = None
     if not args.no_train_step:
         from gaussian_splatting_lightning_amd.optim import GaussianAdam
-        tp = {k: getattr(sc, k).clone() for k in ("means3D", "scales", "rotations", "opacities", "shs")}
+        from gaussian_splatting_lightning_amd.activations import activate, activate_backward
+        tp = {"means3D": sc.means3D.clone(), "shs": sc.shs.clone(), "_scaling": sc.scales.log(),
+              "_opacity": torch.logit(sc.opacities.clamp(1e-6, 1 - 1e-6)).contiguous(),
+              "_rotation": sc.rotations.clone()}
+        act = (torch.empty_like(sc.scales), torch.empty_like(sc.opacities), torch.empty_like(sc.rotations))
+        raw_grad = (torch.empty_like(act[0]), torch.empty_like(act[1]), torch.empty_like(act[2]))
         f_dc, f_rest = tp["shs"][:, :1], tp["shs"][:, 1:]  # column blocks of the one (P, 16, 3) tensor
         topt = GaussianAdam([{"params": [tp["means3D"]], "lr": 0.00016, "name": "xyz"},
                              {"params": [f_dc], "lr": 0.0025, "name": "features_dc"},
                              {"params": [f_rest], "lr": 0.0025 / 20.0, "name": "features_rest"},
-                             {"params": [tp["opacities"]], "lr": 0.05, "name": "opacity"},
-                             {"params": [tp["scales"]], "lr": 0.005, "name": "scaling"},
-                             {"params": [tp["rotations"]], "lr": 0.001, "name": "rotation"}], lr=0.0, eps=1e-15)
+                             {"params": [tp["_opacity"]], "lr": 0.05, "name": "opacity"},
+                             {"params": [tp["_scaling"]], "lr": 0.005, "name": "scaling"},
+                             {"params": [tp["_rotation"]], "lr": 0.001, "name": "rotation"}], lr=0.0, eps=1e-15)
         tred = ViewGradReducer(n, M, deg, dev, mode="compact", chunks=None if distributed else 1,
                                plan_world=args.plan_world or None, handoff=args.exchange_handoff) if distributed else \
             ViewGradReducer(n, M, deg, dev, mode="compact", chunks=1)
 
         def train_step():
-            _, _, _, tst = forward_raw(tp["means3D"], tp["shs"], None, tp["opacities"], tp["scales"], tp["rotations"],
-                                       None, settings)
+            activate(tp["_scaling"], tp["_opacity"], tp["_rotation"], out=act)
+            _, _, _, tst = forward_raw(tp["means3D"], tp["shs"], None, act[1], act[0], act[2], None, settings)
             if tred.chunks == 1:
                 backward_raw(tst, settings, dcolor, dinv, **tred.backward_kwargs())
                 tred.reduce(tp["means3D"], expand_sh=False)
@@ -284,8 +289,10 @@ def main():
                                  compact_sh=True, accumulate_stats=True)
                 tred.finish(tp["means3D"], expand_sh=False)
             gr = tred.grads
-            for k in ("means3D", "scales", "rotations", "opacities"):
-                tp[k].grad = gr[k].view_as(tp[k])
+            activate_backward(tp["_rotation"], act[0], act[1], act[2], gr["scales"].view_as(act[0]),
+                              gr["opacities"].view_as(act[1]), gr["rotations"].view_as(act[2]), out=raw_grad)
+            tp["means3D"].grad = gr["means3D"].view_as(tp["means3D"])
+            tp["_scaling"].grad, tp["_opacity"].grad, tp["_rotation"].grad = raw_grad
             topt.step(sh_views=(f_dc, f_rest, tred.sh_views_gradient(tp["means3D"])))
 
         for _ in range(max(args.warmup, 3)):
@@ -308,11 +315,11 @@ def main():
             el_tr = float(t.item())
         train = {"train_step_ms": round(1e3 * el_tr / args.steps, 4), "steps": args.steps,
                  "exchange": tred.describe() if distributed else "none (one view, compact SH gradient)",
-                 "note": "forward + backward + exchange + Adam over the six per-Gaussian groups (GaussianAdam; the SH "
-                         "groups by the fused SH Adam on the factored multi-view gradient), timed like the headline "
-                         "(barrier + synchronize, max over ranks); Adam steps the rasterizer inputs directly (no "
-                         "activation functions in front of scales / rotations / opacities)"}
-        del tp, topt, tred
+                 "note": "activations (exp / sigmoid / normalize) + forward + backward + exchange + their chain rule "
+                         "+ Adam over the six raw per-Gaussian groups (GaussianAdam; the SH groups by the fused SH Adam "
+                         "on the factored multi-view gradient), timed like the headline (barrier + synchronize, max "
+                         "over ranks)"}
+        del tp, topt, tred, act, raw_grad
 
     # ---- per-launch statistics for the roofline (untimed) ----
     lay = _native.state_layout(n, st.num_rendered, W, H)

@@ -111,6 +111,7 @@ EXPORTED_SYMBOLS = (
     "gsr_stage_times", "gsr_reset_stage_times", "gsr_last_error", "gsr_build_info", "gsr_abi_version", "gsr_adam_sh_views_step",
     "gsr_stream_values_supported", "gsr_stream_signal", "gsr_stream_wait", "gsr_state_layout_query",
     "gsr_set_tuning", "gsr_get_tuning", "gsr_ssim_num_partials", "gsr_ssim_forward", "gsr_ssim_backward", "gsr_adam_step", "gsr_sparse_adam_step",
+    "gsr_activations_forward", "gsr_activations_backward",
     "gsr_densify_workspace_bytes", "gsr_densify_classify", "gsr_densify_apply", "gsr_ply_unpack", "gsr_ply_pack",
     "gsr_knn_workspace_bytes", "gsr_knn_mean_dist2", "gsr_debug_wave_stamps",
 )
@@ -154,6 +155,11 @@ def load(path: str | None = None):
         lib.gsr_adam_sh_views_step.argtypes = [ctypes.POINTER(AdamShViewsArgs), ctypes.c_double, ctypes.c_double,
                                                ctypes.c_double, ctypes.c_void_p]
         lib.gsr_adam_sh_views_step.restype = ctypes.c_int
+    if hasattr(lib, "gsr_activations_forward"):  # absent from pre-round-6 builds loaded for A/Bs through GSR_LIB
+        lib.gsr_activations_forward.argtypes = [ctypes.c_int64] + [ctypes.c_void_p] * 7
+        lib.gsr_activations_forward.restype = ctypes.c_int
+        lib.gsr_activations_backward.argtypes = [ctypes.c_int64] + [ctypes.c_void_p] * 11
+        lib.gsr_activations_backward.restype = ctypes.c_int
     lib.gsr_sparse_adam_step.argtypes = [ctypes.POINTER(AdamGroup), ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
                                          ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_void_p]
     lib.gsr_sparse_adam_step.restype = ctypes.c_int

@@ -118,6 +118,52 @@ void launch_sparse_adam(hipStream_t s, const AdamLaunch &L, int64_t total_slices
     sparse_adam_kernel<<<(unsigned)total_slices, 256, 0, s>>>(L);
 }
 
+// Parameter activations of the reference's GaussianModel in front of the rasterizer (gaussian_model.py: get_scaling
+// = exp, get_opacity = sigmoid, get_rotation = torch.nn.functional.normalize with eps 1e-12), forward and the chain
+// rule back to the raw parameters, one thread per Gaussian.  torch runs these as ~15 elementwise kernels per step
+// (forward + autograd); here two launches, HBM-bound: 64 B/Gaussian forward, 112 B/Gaussian backward.
+constexpr float NORMALIZE_EPS = 1e-12f;
+
+__global__ __launch_bounds__(256) void activations_forward_kernel(ActivationArgs A) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= A.N) return;
+#pragma unroll
+    for (int k = 0; k < 3; k++) A.scales[3 * i + k] = expf(A.scaling[3 * i + k]);
+    A.opacities[i] = 1.0f / (1.0f + expf(-A.opacity[i]));
+    const float4 q = *reinterpret_cast<const float4 *>(A.rotation + 4 * i);
+    const float n = fmaxf(sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w), NORMALIZE_EPS);
+    *reinterpret_cast<float4 *>(A.rotations + 4 * i) = make_float4(q.x / n, q.y / n, q.z / n, q.w / n);
+}
+
+__global__ __launch_bounds__(256) void activations_backward_kernel(ActivationArgs A) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= A.N) return;
+#pragma unroll
+    for (int k = 0; k < 3; k++) A.dL_dscaling[3 * i + k] = A.dL_dscales[3 * i + k] * A.scales[3 * i + k];
+    const float o = A.opacities[i];
+    A.dL_dopacity[i] = A.dL_dopacities[i] * (1.0f - o) * o;  // torch's sigmoid_backward: g * (1 - y) * y
+    const float4 q = *reinterpret_cast<const float4 *>(A.rotation + 4 * i);
+    const float4 u = *reinterpret_cast<const float4 *>(A.rotations + 4 * i);
+    const float4 g = *reinterpret_cast<const float4 *>(A.dL_drotations + 4 * i);
+    const float nr = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+    float4 d;
+    if (nr > NORMALIZE_EPS) {  // d(q / |q|) = (g - u (u . g)) / |q|
+        const float ug = u.x * g.x + u.y * g.y + u.z * g.z + u.w * g.w;
+        d = make_float4((g.x - u.x * ug) / nr, (g.y - u.y * ug) / nr, (g.z - u.z * ug) / nr, (g.w - u.w * ug) / nr);
+    } else {                   // clamped norm: q / eps is linear in q
+        d = make_float4(g.x / NORMALIZE_EPS, g.y / NORMALIZE_EPS, g.z / NORMALIZE_EPS, g.w / NORMALIZE_EPS);
+    }
+    *reinterpret_cast<float4 *>(A.dL_drotation + 4 * i) = d;
+}
+
+void launch_activations_forward(hipStream_t s, const ActivationArgs &A) {
+    if (A.N > 0) activations_forward_kernel<<<(unsigned)((A.N + 255) / 256), 256, 0, s>>>(A);
+}
+
+void launch_activations_backward(hipStream_t s, const ActivationArgs &A) {
+    if (A.N > 0) activations_backward_kernel<<<(unsigned)((A.N + 255) / 256), 256, 0, s>>>(A);
+}
+
 int64_t adam_slices(int64_t n) { return (n + ADAM_SLICE - 1) / ADAM_SLICE; }
 
 void launch_adam(hipStream_t s, const AdamLaunch &L, int64_t total_slices) {

@@ -951,6 +951,49 @@ int gsr_adam_step(const gsr_adam_group *groups, int num_groups, double beta1, do
     return GSR_OK;
 }
 
+static bool aligned16(const void *p) { return (((uintptr_t)p) & 15) == 0; }
+
+int gsr_activations_forward(int64_t N, const float *scaling, const float *opacity, const float *rotation,
+                            float *scales, float *opacities, float *rotations, void *stream_ptr) {
+    if (N < 0 || N > 0x7fffffffLL * 256) return fail(GSR_ERR_ARG, "activations: bad N");
+    if (N == 0) return GSR_OK;
+    if (!scaling || !opacity || !rotation || !scales || !opacities || !rotations)
+        return fail(GSR_ERR_ARG, "activations: null array");
+    if (!aligned16(rotation) || !aligned16(rotations)) return fail(GSR_ERR_ARG, "activations: rotation arrays must be 16-B aligned");
+    ActivationArgs A{};
+    A.N = N;
+    A.scaling = scaling; A.opacity = opacity; A.rotation = rotation;
+    A.scales = scales; A.opacities = opacities; A.rotations = rotations;
+    StreamDeviceGuard device_guard((hipStream_t)stream_ptr);
+    launch_activations_forward((hipStream_t)stream_ptr, A);
+    GSR_HIP(hipGetLastError());
+    return GSR_OK;
+}
+
+int gsr_activations_backward(int64_t N, const float *rotation, const float *scales, const float *opacities,
+                             const float *rotations, const float *dL_dscales, const float *dL_dopacities,
+                             const float *dL_drotations, float *dL_dscaling, float *dL_dopacity, float *dL_drotation,
+                             void *stream_ptr) {
+    if (N < 0 || N > 0x7fffffffLL * 256) return fail(GSR_ERR_ARG, "activations: bad N");
+    if (N == 0) return GSR_OK;
+    if (!rotation || !scales || !opacities || !rotations || !dL_dscales || !dL_dopacities || !dL_drotations ||
+        !dL_dscaling || !dL_dopacity || !dL_drotation)
+        return fail(GSR_ERR_ARG, "activations: null array");
+    if (!aligned16(rotation) || !aligned16(rotations) || !aligned16(dL_drotations) || !aligned16(dL_drotation))
+        return fail(GSR_ERR_ARG, "activations: rotation arrays must be 16-B aligned");
+    ActivationArgs A{};
+    A.N = N;
+    A.rotation = rotation;
+    A.scales = const_cast<float *>(scales); A.opacities = const_cast<float *>(opacities);
+    A.rotations = const_cast<float *>(rotations);
+    A.dL_dscales = dL_dscales; A.dL_dopacities = dL_dopacities; A.dL_drotations = dL_drotations;
+    A.dL_dscaling = dL_dscaling; A.dL_dopacity = dL_dopacity; A.dL_drotation = dL_drotation;
+    StreamDeviceGuard device_guard((hipStream_t)stream_ptr);
+    launch_activations_backward((hipStream_t)stream_ptr, A);
+    GSR_HIP(hipGetLastError());
+    return GSR_OK;
+}
+
 int gsr_sparse_adam_step(const gsr_adam_group *groups, int num_groups, const uint8_t *visible, int64_t N,
                          double beta1, double beta2, double eps, void *stream_ptr) {
     if (num_groups < 0 || num_groups > ADAM_MAX_GROUPS) return fail(GSR_ERR_ARG, "sparse adam: 0..16 parameter groups");

@@ -290,6 +290,17 @@ int64_t adam_slices(int64_t n);
 void launch_adam(hipStream_t s, const AdamLaunch &L, int64_t total_slices);
 void launch_sparse_adam(hipStream_t s, const AdamLaunch &L, int64_t total_slices);
 
+// ---- parameter activations (gsr_adam.hip) ----
+struct ActivationArgs {
+    int64_t N;
+    const float *scaling, *opacity, *rotation;        // raw parameters (N,3) (N) (N,4)
+    float *scales, *opacities, *rotations;            // forward outputs / backward inputs (activated)
+    const float *dL_dscales, *dL_dopacities, *dL_drotations;
+    float *dL_dscaling, *dL_dopacity, *dL_drotation;  // backward outputs
+};
+void launch_activations_forward(hipStream_t s, const ActivationArgs &A);
+void launch_activations_backward(hipStream_t s, const ActivationArgs &A);
+
 // ---- densify_and_prune (gsr_densify.hip) ----
 struct DensifyParams {
     int64_t N;

@@ -220,6 +220,20 @@ typedef struct gsr_adam_sh_views_args {
 } gsr_adam_sh_views_args;
 int gsr_adam_sh_views_step(const gsr_adam_sh_views_args *a, double beta1, double beta2, double eps, void *stream);
 
+/* The parameter activations the reference's GaussianModel puts in front of the rasterizer
+ * (gs_lightning/modules/gaussian_model.py: get_scaling = exp(_scaling), get_opacity = sigmoid(_opacity),
+ * get_rotation = torch.nn.functional.normalize(_rotation), i.e. q / max(|q|, 1e-12)) and their chain rule, so a
+ * training step that keeps the raw parameters (what the optimizer steps) needs two launches instead of torch's
+ * elementwise autograd graph.  Shapes: scaling / scales (N,3), opacity / opacities (N) or (N,1), rotation / rotations
+ * (N,4); fp32 device arrays, the (N,4) ones 16-B aligned.  The backward takes the raw rotation and the forward's
+ * outputs and writes dL/d(raw) from dL/d(activated). */
+int gsr_activations_forward(int64_t N, const float *scaling, const float *opacity, const float *rotation,
+                            float *scales, float *opacities, float *rotations, void *stream);
+int gsr_activations_backward(int64_t N, const float *rotation, const float *scales, const float *opacities,
+                             const float *rotations, const float *dL_dscales, const float *dL_dopacities,
+                             const float *dL_drotations, float *dL_dscaling, float *dL_dopacity, float *dL_drotation,
+                             void *stream);
+
 /* SparseGaussianAdam.step(visibility, N) of the upstream rasterizer package (diff_gaussian_rasterization, taken by
  * the reference's third_party GaussianModel with optimizer_type "sparse_adam": gaussian_model.py:26,194-196).  Each
  * group's n elements are N Gaussians of n / N elements; only the Gaussians with visible[g] != 0 are updated, as
