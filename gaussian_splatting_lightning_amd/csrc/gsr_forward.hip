@@ -33,10 +33,8 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
     // uncontracted like the helpers it calls (gsr_common.h): radii, rects and render records bit-equal the oracle's
 #pragma clang fp contract(off)
     const GeomState &g = p.g;
-    p.radii[i] = 0;
-    g.tiles[i] = 0;
-    g.depth_key[i] = 0xffffffffu;
-    g.clamped[i] = 0;
+    // radii / clamped are stored once, below, for a rendered Gaussian; preprocess_kernel stores the zeros of the
+    // others and the tile count and depth key of every Gaussian (one store per word, not a zero then the value)
 
     // Every per-Gaussian input except the SH block is loaded up front, before the frustum test, so a wave waits
     // for one memory round trip instead of one per dependent stage (the 27 % of loads for culled Gaussians at
@@ -120,7 +118,8 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreprocessParams &
     }
     g.rec[i].a = make_float4(pimg.x, pimg.y, conic_x, conic_y);
     g.rec[i].b = make_float4(conic_z, opacity, rgb.x, rgb.y);
-    g.rec[i].c = make_float2(rgb.z, 1.f / pv.z);
+    // the whole 48-B row (pad included), so the record array is written in full lines
+    *reinterpret_cast<float4 *>(&g.rec[i].c) = make_float4(rgb.z, 1.f / pv.z, 0.f, 0.f);
     g.clamped[i] = clamp_bits;
     p.radii[i] = (int)radius;
     // culling (p.cull): the reference rect shrinks to the tight rect (cull_rect), whose tiles are then tested one by
@@ -211,21 +210,26 @@ __global__ __launch_bounds__(256, GSR_PRE_MINW) void preprocess_kernel(Preproces
     wave_lds_sync();
     const uint32_t t_cull = p.stamps ? stamp_now() : 0u;
     uint32_t kept = area;
-    if (i < p.P && area > 0) {
+    if (i < p.P) {
         const GeomState &g = p.g;
-        const uint64_t mask = ci.need ? L.mask[lane] : 0ull;
-        if (ci.need) kept = (uint32_t)__popcll(mask);
-        g.exp_rec[i] = make_uint4((uint32_t)mask, (uint32_t)(mask >> 32), (uint32_t)ci.rx | ((uint32_t)ci.ry << 16),
-                                  (uint32_t)ci.rw);
+        if (area > 0) {
+            const uint64_t mask = ci.need ? L.mask[lane] : 0ull;
+            if (ci.need) kept = (uint32_t)__popcll(mask);
+            g.exp_rec[i] = make_uint4((uint32_t)mask, (uint32_t)(mask >> 32), (uint32_t)ci.rx | ((uint32_t)ci.ry << 16),
+                                      (uint32_t)ci.rw);
+            if (kept > BIG_GAUSSIAN_TILES) {
+                const uint32_t slot = atomicAdd(&g.counters[CNT_BIG], 1u);
+                g.big_list[slot] = (uint32_t)i;
+                g.big_slot[i] = slot;
+            }
+        } else if (!ci.vis) {  // not rendered: no radius, no clamp bits
+            p.radii[i] = 0;
+            g.clamped[i] = 0;
+        }
         g.tiles[i] = kept;
         // A Gaussian whose every tile is culled keeps its radius (reference output) but renders nothing; it
         // is sorted behind all rendered ones so the expansion never meets an empty rank.
         g.depth_key[i] = kept ? ci.depth : 0xffffffffu;
-        if (kept > BIG_GAUSSIAN_TILES) {
-            const uint32_t slot = atomicAdd(&g.counters[CNT_BIG], 1u);
-            g.big_list[slot] = (uint32_t)i;
-            g.big_slot[i] = slot;
-        }
     }
     // instance total for the early host readback (gsr_forward): block sum, one 64-bit atomic per block into
     // one of CNT_NPART partial counters; likewise the range of the kept depth keys (the radix path's relative
