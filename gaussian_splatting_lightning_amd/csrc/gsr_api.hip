@@ -571,6 +571,7 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     // takes 0.20 ms against the radix path's 0.30; at 5M / 4K stress (1240 per tile) 4.4 ms against 1.4.
     // Otherwise the radix path: depth sort, depth-ordered expansion, stable tile sort.
     const bool bucket = bk_possible && (bk == 2 || (uint64_t)R <= (uint64_t)BK_MAX_MEAN * T);
+    bool xcd_fwd = false;  // the forward composite runs the per-XCD LPT orders (set by the bucket scatter below)
     bool sorted_exp = false;
     bool depth_onesweep = false, tile_onesweep = false;  // which sorts ran on the onesweep path (diagnostics)
     if (bucket) gsr_set_tuning("stat_depth_passes", 0);
@@ -632,6 +633,10 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
             bp.keys_reg = ((bkr == 2 || (bkr == 1 && T > 4096 && R >= 256u * nreg)) && R <= (1u << BK_REG_SHIFT))
                               ? b.bk_keys2 : nullptr;
             bp.order = lpt ? im.order_fwd : nullptr;
+            // per-XCD LPT orders for the whole-tile composites ("xcd_lpt" 1, with the backward's bucket lists)
+            xcd_fwd = lpt && lpt_append_range(T) && tuning("lpt_append", 1) && tuning("xcd_lpt", 1) &&
+                      render_fwd_parts((int)T) == 1;
+            bp.order_xcd = xcd_fwd ? im.order_xcd : nullptr;
             bp.lpt_shift = tuning("lpt_shift", 3);
             GSR_STAGE(ST_BK_SCATTER, dbg, launch_bucket_scatter(stream, bp));  // and the forward LPT order
             SegSortParams sp;
@@ -683,12 +688,13 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     // bucket path's column pass clears them)
     if (!bucket || R == 0)
         GSR_HIP(hipMemsetAsync(im.tile_last, 0,
-                               (size_t)(reinterpret_cast<char *>(im.lpt_bcnt + 256) -
+                               (size_t)(reinterpret_cast<char *>(im.lpt_bcnt + LPT_BCNT_WORDS) -
                                         reinterpret_cast<char *>(im.tile_last)),
                                stream));
     RenderFwdParams rp;
     rp.W = W; rp.H = H; rp.gx = gx; rp.gy = gy; rp.num_tiles = (int)T;
-    rp.tile_order = lpt ? im.order_fwd : nullptr;
+    rp.tile_order = lpt ? (xcd_fwd ? im.order_xcd : im.order_fwd) : nullptr;
+    rp.xcd = xcd_fwd ? 1 : 0;
     rp.ranges = im.ranges; rp.sorted_u = b.sorted_u; rp.inst_gid = b.inst_gid;
     rp.point_list = b.point_list; rp.tile_loaded = im.tile_loaded;
     rp.inv = b.inv;

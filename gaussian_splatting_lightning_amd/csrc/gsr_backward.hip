@@ -295,10 +295,19 @@ __global__ __launch_bounds__(64, GUARD ? 4 : SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MI
         tile = __builtin_amdgcn_readfirstlane((int)item.x);
         seg = __builtin_amdgcn_readfirstlane(item.y);
         ck_k = __builtin_amdgcn_readfirstlane(*p.ck_flag);
-    } else if (p.lpt_blist && __builtin_amdgcn_readfirstlane(*p.lpt_valid)) {
-        tile = lpt_list_tile(p.lpt_bcnt, p.lpt_blist, (uint32_t)p.num_tiles, (uint32_t)slot, lane);
     } else {
-        tile = __builtin_amdgcn_readfirstlane(p.tile_order ? (int)p.tile_order[slot] : slot);
+        // the forward's bucket lists (per XCD group: xcd_slots(T) launch slots, lpt_list_tile_xcd), else the order
+        const uint32_t lists = p.lpt_blist ? __builtin_amdgcn_readfirstlane(*p.lpt_valid) : 0u;
+        if (lists == LPT_LISTS_XCD) {
+            tile = lpt_list_tile_xcd(p.lpt_bcnt, p.lpt_blist, (uint32_t)p.num_tiles, (uint32_t)slot, lane);
+        } else if (slot >= p.num_tiles) {
+            tile = -1;
+        } else if (lists == LPT_LISTS) {
+            tile = lpt_list_tile(p.lpt_bcnt, p.lpt_blist, (uint32_t)p.num_tiles, (uint32_t)slot, lane, slot);
+        } else {
+            tile = __builtin_amdgcn_readfirstlane(p.tile_order ? (int)p.tile_order[slot] : slot);
+        }
+        if (tile < 0) return;  // a slot without a tile (uniform)
     }
     const int tx = tile % p.gx, ty = tile / p.gx;
     const int px = tx * BLOCK_X + (lane & 15);
@@ -602,7 +611,8 @@ void launch_render_bwd(hipStream_t s, const RenderBwdParams &p) {
         }
         return;
     }
-    const dim3 grid(p.num_tiles), block(64);
+    // with the forward's bucket lists the slots run to xcd_slots(T) (per-XCD lists); the extra ones exit
+    const dim3 grid(p.lpt_blist ? xcd_slots((uint32_t)p.num_tiles) : (uint32_t)p.num_tiles), block(64);
     // "bwd_union" -1 (auto): pair only the instances that reach a strip when tiles are long (mean above 1024
     // instances: cfg 5 render_bwd 0.93 -> 0.90 ms; at cfg 3's 517 the plain walk is faster, 0.305 vs 0.329 ms);
     // 0 / 1 force it

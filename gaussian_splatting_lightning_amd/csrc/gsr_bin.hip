@@ -98,7 +98,11 @@ __global__ __launch_bounds__(64 * BKW) void bk_walk_kernel(BucketParams p) {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const uint32_t b = blockIdx.x, T = p.T, gx = (uint32_t)p.gx;
     if (SCATTER && b == p.nb) {  // the extra workgroup: the forward LPT order (the column pass wrote the ranges)
-        lpt_order_block(p.ranges, nullptr, 0, (int)T, p.lpt_shift, p.order, reinterpret_cast<uint32_t *>(&s_own[0][0]));
+        // (the per-XCD map needs the 1024-thread form, which every T of lpt_append_range takes: launch_walk)
+        constexpr bool xok = 64 * BKW == 1024 && sizeof(s_rec) >= 4 * (LPT_BCNT_WORDS + LPT_XCD + 17);
+        lpt_order_block(p.ranges, nullptr, 0, (int)T, p.lpt_shift, p.order, reinterpret_cast<uint32_t *>(&s_own[0][0]),
+                        xok ? p.order_xcd : nullptr, reinterpret_cast<uint32_t *>(&s_rec[0][0]), p.gx,
+                        (int)((T + gx - 1) / gx), 4);
         return;
     }
     const uint32_t nbw = bk_walk_blocks(p);
@@ -277,7 +281,8 @@ __global__ __launch_bounds__(64 * CW) void bk_columns_kernel(BucketParams p) {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int sub = lane % TW, h = lane / TW;  // the lane's tile in the workgroup, its half of the wave's rows
     if (tid == 0) s_bid = atomicAdd(p.ticket, 1u);
-    if (blockIdx.x == 0 && tid < 256 && p.lpt_bcnt) p.lpt_bcnt[tid] = 0u;
+    if (blockIdx.x == 0 && p.lpt_bcnt)
+        for (uint32_t k = (uint32_t)tid; k < LPT_BCNT_WORDS; k += blockDim.x) p.lpt_bcnt[k] = 0u;
     __syncthreads();
     const uint32_t bid = s_bid;
     const uint32_t t = bid * TW + sub;
@@ -931,6 +936,7 @@ void launch_bucket_count(hipStream_t s, const BucketParams &p) {
 
 // plus one workgroup for the forward LPT order when p.order is set
 void launch_bucket_scatter(hipStream_t s, const BucketParams &p) {
+    // (order_xcd is set only within lpt_append_range, T <= 16384: launch_walk's 1024-thread form, which builds it)
     launch_walk<true>(s, p, p.nb + (p.order ? 1u : 0u));
     // one workgroup per PART_CHUNK keys of the upper bound on R the binning buffer was carved for (extra ones exit)
     if (p.keys_reg) bk_partition_kernel<<<div_up(p.R, PART_CHUNK), PART_THREADS, 0, s>>>(p);

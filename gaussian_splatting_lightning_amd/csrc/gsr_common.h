@@ -250,9 +250,10 @@ struct ImageState {
     uint2 *ranges;        // T
     uint32_t *tile_last;  // T: max n_contrib over the tile's pixels
     uint32_t *tile_loaded; // T: instances of the tile the forward composite gathered (>= tile_last)
-    uint32_t *lpt_bcnt;    // 256: tiles per backward LPT bucket, appended by the forward's whole-tile waves (cleared
-                           //      with tile_last / tile_loaded)
+    uint32_t *lpt_bcnt;    // LPT_BCNT_WORDS: tiles per backward LPT bucket (per XCD group with the XCD lists), appended
+                           //      by the forward's whole-tile waves (cleared with tile_last / tile_loaded)
     uint32_t *order_fwd;   // tiles in descending forward work (instances in range), LPT launch order
+    uint32_t *order_xcd;   // xcd_slots(T): the forward's launch slot -> tile map of the per-XCD LPT orders (~0: none)
     uint32_t *order_bwd;   // tiles in descending backward work (tile_last)
     // bucket path count-pass scratch (gsr_bin.hip), here rather than in the binning buffer so that the pass
     // can run before the instance total (the binning buffer's size) reaches the host
@@ -270,8 +271,10 @@ struct ImageState {
     uint32_t *ck_flag;
     uint32_t *seg_count;
     uint32_t *lpt_hist;      // (T / 4096 + 1) x 256: per-workgroup bucket histograms of the multi-workgroup LPT order
-    uint32_t *lpt_blist;     // 256 x T in lpt_append_range (else 1): bucket b's tiles at [b T, b T + lpt_bcnt[b])
-    uint32_t *lpt_valid;     // 1 when this forward appended every tile to the bucket lists, else 0
+    uint32_t *lpt_blist;     // 256 x (T + 128) in lpt_append_range (else 1): bucket b's tiles at [b T, b T + lpt_bcnt[b]),
+                             // or with the XCD lists bucket b of XCD group x at [(256 x + b) C, + lpt_bcnt[256 x + b])
+                             // (C = xcd_slots(T) / 8)
+    uint32_t *lpt_valid;     // LPT_LISTS / LPT_LISTS_XCD when this forward appended every tile to the bucket lists, else 0
     uint32_t *smask_valid;   // 1 when this forward wrote every loaded instance's strip_mask (whole tiles), else 0
 };
 // Between these tile counts the forward's whole-tile waves append each finished tile to its backward LPT bucket, so
@@ -279,6 +282,36 @@ struct ImageState {
 // few buckets) the appends' atomics on the same counters cost render_fwd 27 us, more than the launch they save.
 constexpr uint32_t LPT_APPEND_TILES = 4096, LPT_APPEND_MAX_TILES = 16384;
 inline bool lpt_append_range(uint32_t T) { return T > LPT_APPEND_TILES && T <= LPT_APPEND_MAX_TILES; }
+
+// Per-XCD LPT orders (bucket path, lpt_append_range).  Workgroups b and b + 8 share an XCD and its L2 (round-robin
+// dispatch, MI355X_MICROARCH.md "Workgroup dispatch"); neighbouring tiles gather the same Gaussians' render records.
+// So the tiles are dealt to 8 XCD groups in spatial runs -- a band order (column bands XCD_BAND tiles wide, row-major
+// inside a band) cut into runs of XCD_GROUP tiles, run r to group r % 8 -- and each group runs its own LPT order on the slots
+// of one XCD: launch slot s of a composite with `per` tiles per workgroup belongs to group (s / per) % 8, as its
+// q-th tile with q = (s / (8 per)) per + s % per.  Slots run to xcd_slots(T); the extra ones hold no tile.
+#ifndef GSR_XCD_GROUP  // overridable for library A/B builds (tools/build_variant.py)
+#define GSR_XCD_GROUP 16
+#endif
+#ifndef GSR_XCD_BAND
+#define GSR_XCD_BAND 8
+#endif
+constexpr uint32_t LPT_XCD = 8;
+constexpr uint32_t XCD_GROUP = GSR_XCD_GROUP;
+constexpr uint32_t XCD_BAND = GSR_XCD_BAND;  // band width (tiles) of the XCD groups' band order
+constexpr uint32_t LPT_BCNT_WORDS = 256 * LPT_XCD;
+constexpr uint32_t LPT_LISTS = 1, LPT_LISTS_XCD = 2;  // lpt_valid values
+constexpr uint32_t XCD_NONE = 0xffffffffu;            // an order_xcd slot without a tile
+__host__ __device__ inline uint32_t xcd_slots(uint32_t T) {
+    return (T + LPT_XCD * XCD_GROUP - 1) / (LPT_XCD * XCD_GROUP) * (LPT_XCD * XCD_GROUP);
+}
+__host__ __device__ inline uint32_t xcd_group_of(uint32_t t, uint32_t gx, uint32_t gy) {
+    const uint32_t tx = t % gx, ty = t / gx, band = tx / XCD_BAND, bw = min(XCD_BAND, gx - band * XCD_BAND);
+    const uint32_t k = band * XCD_BAND * gy + ty * bw + (tx - band * XCD_BAND);
+    return (k / XCD_GROUP) % LPT_XCD;
+}
+__host__ __device__ inline uint32_t xcd_slot(uint32_t x, uint32_t q, uint32_t per) {
+    return ((q / per) * LPT_XCD + x) * per + q % per;
+}
 
 inline size_t carve_image(char *base, int W, int H, ImageState &im) {
     Carver c(base);
@@ -289,8 +322,9 @@ inline size_t carve_image(char *base, int W, int H, ImageState &im) {
     im.ranges = c.take<uint2>((size_t)gx * gy + 1);
     im.tile_last = c.take<uint32_t>((size_t)gx * gy + 1);
     im.tile_loaded = c.take<uint32_t>((size_t)gx * gy + 1);
-    im.lpt_bcnt = c.take<uint32_t>(256);
+    im.lpt_bcnt = c.take<uint32_t>(LPT_BCNT_WORDS);
     im.order_fwd = c.take<uint32_t>((size_t)gx * gy + 1);
+    im.order_xcd = c.take<uint32_t>((size_t)xcd_slots(gx * gy) + 1);
     im.order_bwd = c.take<uint32_t>((size_t)gx * gy + 1);
     const size_t nt = (size_t)gx * gy;
     im.bk_hist = c.take<uint32_t>((nt <= BK_MAX_TILES ? (size_t)BK_MAX_BLOCKS * nt : 0) + 1);
@@ -303,7 +337,7 @@ inline size_t carve_image(char *base, int W, int H, ImageState &im) {
     im.ck_flag = c.take<uint32_t>(1);
     im.seg_count = c.take<uint32_t>(1);
     im.lpt_hist = c.take<uint32_t>((nt / 4096 + 1) * 256);
-    im.lpt_blist = c.take<uint32_t>(lpt_append_range((uint32_t)nt) ? 256 * nt : 1);
+    im.lpt_blist = c.take<uint32_t>(lpt_append_range((uint32_t)nt) ? 256 * (nt + 128) : 1);
     im.lpt_valid = c.take<uint32_t>(1);
     im.smask_valid = c.take<uint32_t>(1);
     return c.off + 256;
@@ -930,15 +964,17 @@ __device__ __forceinline__ void wave_lds_sync() {
 //   not serialise.
 // Backward launch slot -> tile from the forward's bucket lists (heaviest bucket first): the wave forms the exclusive
 // prefix of the 256 bucket counts (4 per lane) and picks the bucket holding the slot.  Uniform result.
+// Launch slot -> tile from bucket lists: bcnt[0..255] the bucket sizes, bucket b's tiles at blist[b stride ..];
+// returns `none` when slot is past the lists' total.
 __device__ __forceinline__ int lpt_list_tile(const uint32_t *__restrict__ bcnt, const uint32_t *__restrict__ blist,
-                                             uint32_t T, uint32_t slot, int lane) {
+                                             uint32_t stride, uint32_t slot, int lane, int none) {
     const uint4 c = reinterpret_cast<const uint4 *>(bcnt)[lane];
     const uint32_t sum = c.x + c.y + c.z + c.w;
     const uint32_t pre = wave_inclusive_scan(sum, lane) - sum;
     const uint32_t p1 = pre + c.x, p2 = p1 + c.y, p3 = p2 + c.z, p4 = p3 + c.w;
     const bool mine = slot >= pre && slot < p4;
     const uint64_t m = __ballot(mine);
-    int tile = (int)slot;  // unreachable fallback (the counts cover every tile)
+    int tile = none;
     if (m) {
         const int src = __builtin_ctzll(m);
         uint32_t b = 0, off = 0;
@@ -948,9 +984,16 @@ __device__ __forceinline__ int lpt_list_tile(const uint32_t *__restrict__ bcnt, 
         }
         b = (uint32_t)__shfl((int)b, src);
         off = (uint32_t)__shfl((int)off, src);
-        tile = (int)blist[(size_t)b * T + off];
+        tile = (int)blist[(size_t)b * stride + off];
     }
     return __builtin_amdgcn_readfirstlane(tile);
+}
+// The same over the per-XCD lists (one tile per workgroup): slot s is the (s / 8)-th tile of XCD group s % 8; -1 when
+// that group has fewer tiles.
+__device__ __forceinline__ int lpt_list_tile_xcd(const uint32_t *__restrict__ bcnt, const uint32_t *__restrict__ blist,
+                                                 uint32_t T, uint32_t slot, int lane) {
+    const uint32_t x = slot % LPT_XCD, cap = xcd_slots(T) / LPT_XCD;
+    return lpt_list_tile(bcnt + 256u * x, blist + (size_t)256u * x * cap, cap, slot / LPT_XCD, lane, -1);
 }
 
 constexpr int LPT_KMAX = 32;
@@ -1006,9 +1049,12 @@ __device__ __forceinline__ void lpt_walk(int T, bool cached, const uint32_t (&wt
         }
     }
 }
+// xmap (optional, with xhist: LPT_BCNT_WORDS + LPT_XCD + 16 words of LDS): also the per-XCD LPT slot map of a composite
+// with `per` tiles per workgroup (order_xcd; gx, gy the tile grid)
 __device__ __forceinline__ void lpt_order_block(const uint2 *__restrict__ ranges, const uint32_t *__restrict__ tile_last,
                                                 int use_last, int T, int shift0, uint32_t *__restrict__ order,
-                                                uint32_t *hist) {
+                                                uint32_t *hist, uint32_t *__restrict__ xmap = nullptr,
+                                                uint32_t *xhist = nullptr, int gx = 0, int gy = 0, int per = 4) {
     const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, w = tid >> 6;
     auto load_w = [&](int t) -> uint32_t { return use_last ? tile_last[t] : ranges[t].y - ranges[t].x; };
     const bool cached = T <= nt * LPT_KMAX;
@@ -1052,6 +1098,64 @@ __device__ __forceinline__ void lpt_order_block(const uint2 *__restrict__ ranges
     }
     __syncthreads();
     lpt_walk(T, cached, wt, load_w, shift, hist, order);
+    if (!xmap) return;
+    // per-XCD orders: the same buckets per XCD group, x-major; group x's tiles take its slots in bucket order
+    uint32_t *xstart = xhist + LPT_BCNT_WORDS;  // LPT_XCD + 1 segment starts
+    uint32_t *wsum = xstart + LPT_XCD + 1;      // per-wave sums of the scan (<= 16 waves)
+    for (int k = tid; k < (int)LPT_BCNT_WORDS; k += nt) xhist[k] = 0;
+    __syncthreads();
+    auto xbucket = [&](int t, uint32_t wgt) -> uint32_t {
+        return 256u * xcd_group_of((uint32_t)t, (uint32_t)gx, (uint32_t)gy) + (255u - min(255u, wgt >> shift));
+    };
+    // fn(t, bucket) over the tiles, the weights from registers when cached (a static index: no scratch)
+    auto each_tile = [&](auto fn) {
+        if (cached) {
+#pragma unroll
+            for (int k = 0; k < LPT_KMAX; k++) {
+                if (k * nt >= T) break;  // uniform
+                const int t = tid + k * nt;
+                if (t < T) fn(t, xbucket(t, wt[k]));
+            }
+        } else {
+            for (int t = tid; t < T; t += nt) fn(t, xbucket(t, load_w(t)));
+        }
+    };
+    each_tile([&](int, uint32_t bb) { atomicAdd(&xhist[bb], 1u); });
+    __syncthreads();
+    // exclusive scan of the LPT_BCNT_WORDS counts, 2 per thread (the caller runs 1024 threads)
+    constexpr int XPER = (int)LPT_BCNT_WORDS / 1024;
+    uint32_t v[XPER], loc = 0;
+#pragma unroll
+    for (int j = 0; j < XPER; j++) {
+        v[j] = tid < 1024 ? xhist[tid * XPER + j] : 0u;
+        loc += v[j];
+    }
+    const uint32_t inc = wave_inclusive_scan(loc, lane);
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t run = inc - loc;
+    for (int i = 0; i < w; i++) run += wsum[i];
+    __syncthreads();
+    if (tid < 1024) {
+#pragma unroll
+        for (int j = 0; j < XPER; j++) {
+            const int idx = tid * XPER + j;
+            xhist[idx] = run;
+            if (idx % 256 == 0) xstart[idx / 256] = run;
+            run += v[j];
+        }
+        if (tid == 1023) xstart[LPT_XCD] = run;
+    }
+    __syncthreads();
+    const uint32_t cap = xcd_slots((uint32_t)T) / LPT_XCD;
+    for (uint32_t i = (uint32_t)tid; i < LPT_XCD * cap; i += (uint32_t)nt) {  // the slots no tile takes
+        const uint32_t x = i / cap, q = i % cap;
+        if (q >= xstart[x + 1] - xstart[x]) xmap[xcd_slot(x, q, (uint32_t)per)] = XCD_NONE;
+    }
+    each_tile([&](int t, uint32_t bb) {
+        const uint32_t x = bb / 256u, q = atomicAdd(&xhist[bb], 1u) - xstart[x];
+        xmap[xcd_slot(x, q, (uint32_t)per)] = (uint32_t)t;
+    });
 }
 
 #endif  // __HIPCC__

@@ -657,11 +657,18 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
     const int lane = threadIdx.x & 63;
     const int slot = blockIdx.x * 4 + w;
     if (p.ck_flag && slot == 0 && lane == 0) *p.ck_flag = CKPT ? p.ck_k : 0u;
-    if (p.lpt_valid && slot == 0 && lane == 0) *p.lpt_valid = (PARTS == 1 && p.lpt_blist) ? 1u : 0u;
+    if (p.lpt_valid && slot == 0 && lane == 0)
+        *p.lpt_valid = (PARTS == 1 && p.lpt_blist) ? (p.xcd ? LPT_LISTS_XCD : LPT_LISTS) : 0u;
     if (p.smask_valid && slot == 0 && lane == 0) *p.smask_valid = SMASK ? 1u : 0u;
-    if (slot >= p.num_tiles * PARTS) return;
+    int tile;
+    if (PARTS == 1 && p.xcd) {  // per-XCD LPT slot map (xcd_slots(T) slots)
+        tile = __builtin_amdgcn_readfirstlane((int)p.tile_order[slot]);
+        if (tile < 0) return;  // XCD_NONE
+    } else {
+        if (slot >= p.num_tiles * PARTS) return;
+        tile = __builtin_amdgcn_readfirstlane(p.tile_order ? (int)p.tile_order[slot / PARTS] : slot / PARTS);
+    }
     const int half = slot % PARTS;
-    const int tile = __builtin_amdgcn_readfirstlane(p.tile_order ? (int)p.tile_order[slot / PARTS] : slot / PARTS);
     const uint32_t t_start = p.stamps ? stamp_now() : 0u;
     const int tx = tile % p.gx, ty = tile / p.gx;
     const int px = tx * BLOCK_X + (lane & 15);
@@ -854,9 +861,13 @@ __global__ __launch_bounds__(256, MIN_WAVES) void render_fwd_v6_kernel(RenderFwd
         atomicMax(&p.tile_last[tile], mx);
         atomicMax(&p.tile_loaded[tile], loaded_end - r0);
         if (PARTS == 1 && p.lpt_blist) {  // whole tile: mx is final; append it to its backward LPT bucket
-            const uint32_t b = lpt_log_bucket(mx);
+            uint32_t b = lpt_log_bucket(mx), stride = (uint32_t)p.num_tiles;
+            if (p.xcd) {  // the bucket of its XCD group (lpt_list_tile_xcd)
+                b += 256u * xcd_group_of((uint32_t)tile, (uint32_t)p.gx, (uint32_t)p.gy);
+                stride = xcd_slots((uint32_t)p.num_tiles) / LPT_XCD;
+            }
             const uint32_t pos = atomicAdd(&p.lpt_bcnt[b], 1u);
-            p.lpt_blist[(size_t)b * (uint32_t)p.num_tiles + pos] = (uint32_t)tile;
+            p.lpt_blist[(size_t)b * stride + pos] = (uint32_t)tile;
         }
     }
     stamp_store(p.stamps, slot, t_start, lane);
@@ -878,7 +889,9 @@ void launch_render_fwd(hipStream_t s, const RenderFwdParams &p0) {
     p.strip_exact = tuning("strip_exact", 1);
     p.stamps = tuning("stamp", 0) ? stamp_buffer(0) : nullptr;
     const int parts = render_fwd_parts(p.num_tiles);
-    const dim3 grid(div_up((uint64_t)p.num_tiles * parts, 4)), block(256);
+    if (parts != 1) p.xcd = 0;
+    const dim3 grid(div_up(p.xcd ? (uint64_t)xcd_slots((uint32_t)p.num_tiles) : (uint64_t)p.num_tiles * parts, 4)),
+        block(256);
     // threshold guard band ("guard" 1; the default launch shapes only, and the backward must run with the same knob)
     // exact strip masks for the backward ("smask" 1): whole tiles only
     const bool sm = parts == 1 && p.strip_mask && tuning("smask", 1);

@@ -119,6 +119,7 @@ struct BucketParams {
     uint32_t *reg_start;           // T / BK_REGION + 2: region starts (tile_start of each region's first tile), column pass
     uint32_t *inst_gid;    // R
     uint32_t *order;       // scatter: an extra workgroup writes the forward LPT order here (or null: none)
+    uint32_t *order_xcd;   // and, when set, the per-XCD LPT slot map of the forward composite (xcd_slots(T) words)
     int lpt_shift;
     int xcd_major;         // bucket runs in XCD-major block order (bk_row_block)
 };
@@ -143,6 +144,7 @@ void launch_tile_order(hipStream_t s, const uint2 *ranges, const uint32_t *tile_
 
 struct RenderFwdParams {
     int W, H, gx, gy, num_tiles;
+    int xcd;  // tile_order is the per-XCD slot map (order_xcd, XCD_NONE = no tile) and the appends go to the XCD lists
     const uint2 *ranges;
     const uint32_t *tile_order;  // launch slot -> tile (heaviest first), or null for identity
     const uint32_t *sorted_u, *inst_gid;

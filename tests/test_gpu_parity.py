@@ -584,6 +584,30 @@ def test_densify_stats_from_backward(gpu_device):
     assert torch.equal(mrad, torch.maximum(radii.to(torch.int32), torch.full_like(mrad, 3)))
 
 
+@pytest.mark.gpu
+def test_per_xcd_lpt_order_is_bitwise_invisible(gpu_device):
+    """The per-XCD LPT orders (1080p: 8160 tiles in lpt_append_range; the forward's slot map from the bucket scatter's
+    extra workgroup, the backward's per-XCD bucket lists) only change which tile runs where and when: outputs and
+    gradients bitwise those of the global LPT order ("xcd_lpt" 0) and of no LPT order at all ("lpt" 0)."""
+    from gaussian_splatting_lightning_amd import _native
+    inp = scene_inputs(150_000, 1920, 1080, sh_degree=3, seed=6, bg=(0.3, 0.6, 0.9))
+    dc, di = upstream(1920, 1080, 6)
+    ref = run_hip(inp, gpu_device, dc, di)
+    try:
+        _native.set_tuning("xcd_lpt", 0)
+        glob = run_hip(inp, gpu_device, dc, di)
+        _native.set_tuning("lpt", 0)
+        none = run_hip(inp, gpu_device, dc, di)
+    finally:
+        _native.unset_tuning("xcd_lpt")
+        _native.unset_tuning("lpt")
+    for alt in (glob, none):
+        for k in ("color", "invdepth", "radii"):
+            assert np.array_equal(ref[k], alt[k]), k
+        for k in GRADS:
+            assert np.array_equal(ref["grads"][k], alt["grads"][k]), k
+
+
 @pytest.mark.parametrize("knobs", [{"fwd_parts": 1}, {"fwd_parts": 2}, {"fwd_parts": 4}, {"fwd_whole_waves": 6},
                                    {"strip_exact": 0}, {"bwd_parts": 2}, {"bwd_parts": 4},
                                    {"bwd_union": 1}, {"fwd_parts": 1, "bwd_union": 1}, {"fwd_parts": 1, "smask": 0}])
