@@ -576,12 +576,13 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     bool depth_onesweep = false, tile_onesweep = false;  // which sorts ran on the onesweep path (diagnostics)
     if (bucket) gsr_set_tuning("stat_depth_passes", 0);
     if (!bucket) {
-        // the depth sort's last pass also writes the tile counts and expansion records in depth order, so the scan and
-        // the expansion read them coalesced instead of gathering them through the order
-        constexpr int sg = 3;
+        // the depth sort's last pass also writes the tile counts in depth order, so the instance scan reads them
+        // coalesced instead of gathering them through the order (the 16-B expansion records too measured slower: cfg 5
+        // depth sort 0.232 -> 0.352 ms for expand 0.241 -> 0.221 ms, profiles/r6t_libab_sort_gather_cfg5.txt; the
+        // expansion gathers them by rank)
+        constexpr int sg = 1;
         SortGather ga;
         ga.src = g.tiles; ga.dst = g.tiles_sorted;
-        ga.src4 = g.exp_rec; ga.dst4 = g.exp_sorted;
         bool sorted_recs = false;
         // Relative depth keys ("depth_rel" 1) where the sort takes the multi-kernel path: the kept keys span
         // kmax - kmin, so rs_rel_key maps them onto [0, span] and the culled ones onto span + 1, and the sort runs

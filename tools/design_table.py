@@ -13,7 +13,7 @@ import sys
 NS_VALU, NS_TRANS, SIMDS = 1.29, 3.5, 1024
 # SURVEY.md §8(d) algorithmic bytes per work unit, and the bound, per stage (G Gaussians, I instances, T tiles, M = 16)
 ALGO = {
-    "preprocess": ("G (40 + 12M) read + 84 write = 320 B/G", "HBM / latency"),
+    "preprocess": ("G (40 + 12M) read + 113 write = 345 B/G", "HBM / latency"),
     "bucket_count_walk": ("20 B/G read + 4 B/G offsets + 256 T 4-B count rows", "latency"),
     "bucket_columns": ("2 x the count matrix + 32 B/T", "latency"),
     "bucket_scatter": ("28 B/G read + 16 B/I write (key 8, inst_gid 4, inv 4)", "stores"),
