@@ -30,6 +30,8 @@ def activate(scaling: torch.Tensor, opacity: torch.Tensor, rotation: torch.Tenso
         raise ValueError("activations: expected scaling (N,3), opacity (N) or (N,1), rotation (N,4)")
     if out is None:
         out = (torch.empty_like(scaling), torch.empty_like(opacity), torch.empty_like(rotation))
+    if tuple(o.numel() for o in out) != (3 * N, N, 4 * N):
+        raise ValueError("activations: out must hold (N,3), (N) and (N,4) elements")
     _check(scaling, opacity, rotation, *out)
     lib = _native.load()
     _native.check(lib.gsr_activations_forward(N, scaling.data_ptr(), opacity.data_ptr(), rotation.data_ptr(),
@@ -50,6 +52,8 @@ def activate_backward(rotation: torch.Tensor, scales: torch.Tensor, opacities: t
             raise ValueError("activations: gradient / activation shapes do not match N")
     if out is None:
         out = (torch.empty_like(scales), torch.empty_like(opacities), torch.empty_like(rotation))
+    if tuple(o.numel() for o in out) != (3 * N, N, 4 * N):
+        raise ValueError("activations: out must hold (N,3), (N) and (N,4) elements")
     _check(rotation, scales, opacities, rotations, dL_dscales, dL_dopacities, dL_drotations, *out)
     lib = _native.load()
     _native.check(lib.gsr_activations_backward(
