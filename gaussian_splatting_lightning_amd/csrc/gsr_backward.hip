@@ -284,6 +284,12 @@ template <bool HAS_INV, bool UNION = false, bool SEG = false, bool GUARD = false
 __global__ __launch_bounds__(64, GUARD ? 4 : SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MINW) void render_bwd_v5_kernel(RenderBwdParams p) {
     __shared__ FwdRec s_rec[BWD_BATCH];
     __shared__ __attribute__((aligned(16))) float s_part[BWD_BATCH][PART];  // [instance][10 sums]
+    // zeros the union walk's per-instance accumulators are loaded from (pass() below); one pair per batch slot, so the
+    // loads are loop-variant and stay in the loop rather than being hoisted into registers copied per instance
+    __shared__ float4 s_zero[UNION ? BWD_BATCH : 1][2];
+    if constexpr (UNION) {
+        if (threadIdx.x < 2 * BWD_BATCH) (&s_zero[0][0])[threadIdx.x] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     const int lane = threadIdx.x;
     const int slot = blockIdx.x;
     const uint32_t t_start = p.stamps ? stamp_now() : 0u;
@@ -406,7 +412,15 @@ __global__ __launch_bounds__(64, GUARD ? 4 : SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MI
             const float2 c = r.c;           // b, 1/depth
             const float dx = a.x - pfx;
             const float P0 = (a.z * dx) * dx, L = a.w * dx;
-            float Q0 = 0.f, Q1 = 0.f, Q2 = 0.f, w0 = 0.f, w1 = 0.f, w2 = 0.f, w3 = 0.f;
+                        // The union walk (long tiles) loads the accumulators' zeros from LDS: two ds_read_b128 in place of seven
+            // v_mov per instance (cfg 5 render_bwd 0.801 -> 0.779 ms; the plain walk of cfg 3 measured no gain, and
+            // the segment walk, at its 80-VGPR cap, spilled: profiles/r6x_libab_lds_zero_cfg*.txt)
+            float4 z0 = make_float4(0.f, 0.f, 0.f, 0.f), z1 = z0;
+            if constexpr (UNION) {
+                z0 = s_zero[j][0];
+                z1 = s_zero[j][1];
+            }
+            float Q0 = z0.x, Q1 = z0.y, Q2 = z0.z, w0 = z0.w, w1 = z1.x, w2 = z1.y, w3 = z1.z;
             uint64_t any = 0;
 #pragma unroll
             for (int k = 0; k < PIX_PER_LANE; k++) {
