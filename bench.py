@@ -68,7 +68,7 @@ def parse():
     ap.add_argument("--no-stage-events", action="store_true", help="time without per-stage hipEvents")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"))
-    ap.add_argument("--exchange", default="auto", choices=("auto", "compact", "dense"),
+    ap.add_argument("--exchange", default="auto", choices=("auto", "compact", "dense", "sharded"),
                     help="N>1 gradient exchange (gaussian_splatting_lightning_amd/multiview.py); auto: the cost model's "
                          "choice (multiview.plan_exchange)")
     ap.add_argument("--exchange-chunks", type=int, default=0,
@@ -156,7 +156,7 @@ def main():
         # only when the model densifies (ViewGradReducer.sync_densify_stats), not every step
         if red.chunks == 1:
             backward_raw(st, settings, dcolor, dinv, **red.backward_kwargs())
-            red.reduce(sc.means3D)
+            red.reduce(sc.means3D, c.campos if red.sharded else None)
         else:
             red.begin_step(means3D=sc.means3D)  # side stream: each chunk's SH expansion runs right behind its group
             backward_chunked(st, settings, dcolor, dinv, red.chunk_outputs(), on_chunk=red.start_chunk,
@@ -261,39 +261,72 @@ def main():
     if not args.no_train_step:
         from gaussian_splatting_lightning_amd.optim import GaussianAdam
         from gaussian_splatting_lightning_amd.activations import activate, activate_backward
-        tp = {"means3D": sc.means3D.clone(), "shs": sc.shs.clone(), "_scaling": sc.scales.log(),
-              "_opacity": torch.logit(sc.opacities.clamp(1e-6, 1 - 1e-6)).contiguous(),
-              "_rotation": sc.rotations.clone()}
+        from gaussian_splatting_lightning_amd.multiview import plan_exchange
+        # the training exchange: compact (every rank steps every Gaussian) or sharded (every rank steps its shard
+        # and all-gathers the updated parameters); dense has no factored SH gradient for the fused SH Adam
+        if args.exchange == "auto":
+            tmode = plan_exchange(n, args.plan_world or world, M, modes=("compact", "sharded"))["mode"]
+        else:
+            tmode = "sharded" if args.exchange == "sharded" else "compact"
+        tred = ViewGradReducer(n, M, deg, dev, mode=tmode, chunks=None if tmode == "compact" else 1,
+                               plan_world=args.plan_world or None, handoff=args.exchange_handoff) \
+            if distributed else ViewGradReducer(n, M, deg, dev, mode="compact", chunks=1)
+        # parameters padded to the shards' N S rows (the rasterizer reads the first n), so every rank's updated shard
+        # is all-gathered in place
+        rows = world * tred.shard_len if tred.sharded else n
+
+        def padded(t):
+            out = torch.zeros((rows,) + tuple(t.shape[1:]), device=dev)
+            out[:n] = t
+            return out
+
+        tp = {"means3D": padded(sc.means3D), "shs": padded(sc.shs), "_scaling": padded(sc.scales.log()),
+              "_opacity": padded(torch.logit(sc.opacities.clamp(1e-6, 1 - 1e-6))), "_rotation": padded(sc.rotations)}
+        g0, g1 = tred.shard if tred.sharded else (0, n)
+        L = g1 - g0
         act = (torch.empty_like(sc.scales), torch.empty_like(sc.opacities), torch.empty_like(sc.rotations))
-        raw_grad = (torch.empty_like(act[0]), torch.empty_like(act[1]), torch.empty_like(act[2]))
-        f_dc, f_rest = tp["shs"][:, :1], tp["shs"][:, 1:]  # column blocks of the one (P, 16, 3) tensor
-        topt = GaussianAdam([{"params": [tp["means3D"]], "lr": 0.00016, "name": "xyz"},
+        raw_grad = (torch.empty(L, 3, device=dev), torch.empty(L, 1, device=dev), torch.empty(L, 4, device=dev))
+        own = {k: v[g0:g1] for k, v in tp.items()}  # the rows this rank's optimizer steps
+        f_dc, f_rest = own["shs"][:, :1], own["shs"][:, 1:]  # column blocks of the one (P, 16, 3) tensor
+        topt = GaussianAdam([{"params": [own["means3D"]], "lr": 0.00016, "name": "xyz"},
                              {"params": [f_dc], "lr": 0.0025, "name": "features_dc"},
                              {"params": [f_rest], "lr": 0.0025 / 20.0, "name": "features_rest"},
-                             {"params": [tp["_opacity"]], "lr": 0.05, "name": "opacity"},
-                             {"params": [tp["_scaling"]], "lr": 0.005, "name": "scaling"},
-                             {"params": [tp["_rotation"]], "lr": 0.001, "name": "rotation"}], lr=0.0, eps=1e-15)
-        tred = ViewGradReducer(n, M, deg, dev, mode="compact", chunks=None if distributed else 1,
-                               plan_world=args.plan_world or None, handoff=args.exchange_handoff) if distributed else \
-            ViewGradReducer(n, M, deg, dev, mode="compact", chunks=1)
+                             {"params": [own["_opacity"]], "lr": 0.05, "name": "opacity"},
+                             {"params": [own["_scaling"]], "lr": 0.005, "name": "scaling"},
+                             {"params": [own["_rotation"]], "lr": 0.001, "name": "rotation"}], lr=0.0, eps=1e-15)
+
+        def gather_params():
+            """Every rank's updated shard to every rank (in place: rank r's S rows are its input)."""
+            S = tred.shard_len
+            if dist.get_backend() == "nccl":  # torch's coalesced fast path: one RCCL group
+                with dist.distributed_c10d._coalescing_manager():
+                    for t in tp.values():
+                        dist.all_gather_into_tensor(t.view(-1), t[rank * S:(rank + 1) * S].reshape(-1))
+            else:  # gloo rehearsal: no in-place form
+                for t in tp.values():
+                    dist.all_gather_into_tensor(t.view(-1), t[rank * S:(rank + 1) * S].reshape(-1).clone())
 
         def train_step():
-            activate(tp["_scaling"], tp["_opacity"], tp["_rotation"], out=act)
-            _, _, _, tst = forward_raw(tp["means3D"], tp["shs"], None, act[1], act[0], act[2], None, settings)
+            activate(tp["_scaling"][:n], tp["_opacity"][:n], tp["_rotation"][:n], out=act)
+            _, _, _, tst = forward_raw(tp["means3D"][:n], tp["shs"][:n], None, act[1], act[0], act[2], None, settings)
             if tred.chunks == 1:
                 backward_raw(tst, settings, dcolor, dinv, **tred.backward_kwargs())
-                tred.reduce(tp["means3D"], expand_sh=False)
+                tred.reduce(tp["means3D"][:n], c.campos if tred.sharded else None, expand_sh=False)
             else:
                 tred.begin_step()
                 backward_chunked(tst, settings, dcolor, dinv, tred.chunk_outputs(), on_chunk=tred.start_chunk,
                                  compact_sh=True, accumulate_stats=True)
-                tred.finish(tp["means3D"], expand_sh=False)
+                tred.finish(tp["means3D"][:n], expand_sh=False)
             gr = tred.grads
-            activate_backward(tp["_rotation"], act[0], act[1], act[2], gr["scales"].view_as(act[0]),
-                              gr["opacities"].view_as(act[1]), gr["rotations"].view_as(act[2]), out=raw_grad)
-            tp["means3D"].grad = gr["means3D"].view_as(tp["means3D"])
-            tp["_scaling"].grad, tp["_opacity"].grad, tp["_rotation"].grad = raw_grad
-            topt.step(sh_views=(f_dc, f_rest, tred.sh_views_gradient(tp["means3D"])))
+            if L > 0:
+                activate_backward(own["_rotation"], act[0][g0:g1], act[1][g0:g1], act[2][g0:g1],
+                                  gr["scales"].view(L, 3), gr["opacities"].view(L, 1), gr["rotations"].view(L, 4),
+                                  out=raw_grad)
+                own["means3D"].grad = gr["means3D"].view(L, 3)
+                own["_scaling"].grad, own["_opacity"].grad, own["_rotation"].grad = raw_grad
+                topt.step(sh_views=(f_dc, f_rest, tred.sh_views_gradient(tp["means3D"][:n])))
+            if tred.sharded and tred.distributed:
+                gather_params()
 
         for _ in range(max(args.warmup, 3)):
             train_step()
@@ -317,9 +350,9 @@ def main():
                  "exchange": tred.describe() if distributed else "none (one view, compact SH gradient)",
                  "note": "activations (exp / sigmoid / normalize) + forward + backward + exchange + their chain rule "
                          "+ Adam over the six raw per-Gaussian groups (GaussianAdam; the SH groups by the fused SH Adam "
-                         "on the factored multi-view gradient), timed like the headline (barrier + synchronize, max "
-                         "over ranks)"}
-        del tp, topt, tred, act, raw_grad
+                         "on the factored multi-view gradient; sharded: on this rank's shard, then the updated "
+                         "parameters all-gathered), timed like the headline (barrier + synchronize, max over ranks)"}
+        del tp, own, topt, tred, act, raw_grad
 
     # ---- per-launch statistics for the roofline (untimed) ----
     lay = _native.state_layout(n, st.num_rendered, W, H)

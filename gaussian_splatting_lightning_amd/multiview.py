@@ -22,6 +22,14 @@ Per step only the parameter gradients cross the links:
             campos, exactly), so no separate camera gather runs.  Per-rank ring traffic at 8 ranks and SH degree 3:
             2*(7/8)*44 B + (7/8)*96 B = 161 B per Gaussian instead of 2*(7/8)*236 B = 413 B.
 
+``sharded`` (ZeRO-style: every Gaussian's reduced gradient is needed on ONE rank, its owner, which runs the optimizer
+            for its shard and all-gathers the updated parameters): the 11 non-SH floats go in one reduce-scatter
+            (rank r receives the sum over views for its Gaussian shard [r S, (r + 1) S)), and the colour factors in
+            one all-to-all (rank r receives every view's factors for its shard only), plus the cameras in the
+            reduce-scatter group.  Per-rank traffic at 8 ranks: (7/8)*(44 + 12) B = 49 B per Gaussian; the SH
+            expansion (or the fused SH Adam) covers the shard only.  The training step then all-gathers the updated
+            parameters, (7/8)*236 B per Gaussian, instead of every rank running the whole optimizer.
+
 Overlap with the backward (``chunks`` = K > 1): the Gaussians are split into K contiguous ranges and the
 gradient buffer is laid out chunk-major -- chunk c's block holds [means3D | scales | rotations | opacity (| shs)]
 of its Gaussians only -- so a chunk's exchange is ONE all-reduce (+ one all-gather of its colour factors), issued
@@ -80,6 +88,8 @@ def exchange_bytes_per_gaussian(mode: str, world: int, M: int = 16) -> float:
     N = max(1, int(world))
     if mode == "dense":
         return 2.0 * (N - 1) / N * 4 * (NON_SH_FLOATS + 3 * M)
+    if mode == "sharded":  # reduce-scatter of the 11 floats + all-to-all of the 3-float factors
+        return (N - 1) / N * (4 * NON_SH_FLOATS + 12.0)
     return 2.0 * (N - 1) / N * 4 * NON_SH_FLOATS + (N - 1) / N * 12.0 * N
 
 
@@ -96,11 +106,17 @@ def simulate_exchange(n: int, world: int, mode: str, chunks: int, expand: str = 
     scale = n / 1e6
     K = max(1, int(chunks))
     N = max(1, int(world))
-    pb = (c["pb_compact_ms"] if mode == "compact" else c["pb_dense_ms"]) * scale
+    pb = (c["pb_dense_ms"] if mode == "dense" else c["pb_compact_ms"]) * scale
     bus = c["link_GBps"] * c["links"] * c["bus_efficiency"] * 1e9  # B/s
     link_bytes = exchange_bytes_per_gaussian(mode, N, M) * n
     comm = link_bytes / bus * 1e3 if N > 1 else 0.0  # one rank: in-place collectives move nothing
-    exp = (c["exp_ms"] + c["exp_view_ms"] * (N - 1)) * scale if mode == "compact" else 0.0
+    exp = (c["exp_ms"] + c["exp_view_ms"] * (N - 1)) * scale if mode != "dense" else 0.0
+    if mode == "sharded":  # K = 1: the reduce-scatter group and the all-to-all, then the shard's expansion
+        exp /= N
+        end = pb + 2 * c["group_sync_ms"] + comm + exp
+        return {"mode": mode, "chunks": 1, "expand": "once", "per_gaussian_stage_ms": round(pb, 4),
+                "link_MB": round(link_bytes / 1e6, 1), "comm_ms": round(comm, 4), "end_ms": round(end, 4),
+                "exposed_ms": round(end - pb, 4)}
     if K == 1:
         end = pb + c["group_sync_ms"] + comm + exp
     else:
@@ -123,14 +139,15 @@ def simulate_exchange(n: int, world: int, mode: str, chunks: int, expand: str = 
 
 
 def plan_exchange(n: int, world: int, M: int = 16, costs: Optional[dict] = None,
-                  modes=("compact", "dense"), chunk_options=(1, 2, 4, 8), margin: float = 0.15) -> Dict[str, float]:
+                  modes=("compact", "dense", "sharded"), chunk_options=(1, 2, 4, 8),
+                  margin: float = 0.15) -> Dict[str, float]:
     """The (mode, chunks, expand) with the smallest predicted end time -- but the fewest chunks whose prediction is
     within `margin` (relative) of the best: every extra chunk's hand-offs are measured costs, while the overlap they
     buy rests on the ASSUMED bus bandwidth (ties: fewer chunks, compact first)."""
     cands = []
     for mode in modes:
         for K in chunk_options:
-            if K > 1 and n < 256 * K:
+            if K > 1 and (n < 256 * K or mode == "sharded"):
                 continue
             for expand in (("chunk", "once") if (mode == "compact" and K > 1) else ("once",)):
                 cands.append(simulate_exchange(n, world, mode, K, expand, M, costs))
@@ -183,8 +200,8 @@ class ViewGradReducer:
                  distributed: Optional[bool] = None, expand: Optional[str] = None,
                  coalesce: Optional[bool] = None, sync_ops: Optional[bool] = None, comm_stream: Optional[str] = None,
                  plan_world: Optional[int] = None, handoff: Optional[str] = None):
-        if mode not in ("dense", "compact", "auto"):
-            raise ValueError(f"mode must be 'dense', 'compact' or 'auto', got {mode!r}")
+        if mode not in ("dense", "compact", "sharded", "auto"):
+            raise ValueError(f"mode must be 'dense', 'compact', 'sharded' or 'auto', got {mode!r}")
         self.n, self.M, self.D = int(n), int(M), int(sh_degree)
         self.device = torch.device(device)
         self.group = group
@@ -200,22 +217,28 @@ class ViewGradReducer:
         if mode == "auto" or chunks is None:
             # plan_world: plan for that many ranks (a one-rank rehearsal of the N-GPU schedule, bench.py --plan-world)
             self.plan = plan_exchange(self.n, int(plan_world or self.world), self.M,
-                                      modes=("compact", "dense") if mode == "auto" else (mode,),
+                                      modes=("compact", "dense", "sharded") if mode == "auto" else (mode,),
                                       chunk_options=(1, 2, 4, 8) if chunks is None else (int(chunks),))
             mode = self.plan["mode"]
             chunks = self.plan["chunks"]
             if expand is None:
                 expand = self.plan["expand"]
         self.mode = mode
+        self.sharded = mode == "sharded"
+        if self.sharded and chunks not in (None, 1):
+            raise ValueError("the sharded exchange runs unchunked (chunks=1)")
         self.compact = mode == "compact"
         self.expand = expand or "chunk"
         if self.expand not in ("chunk", "once", "side"):
             raise ValueError(f"expand must be 'chunk', 'once' or 'side', got {self.expand!r}")
         self._sh_views = sh_views_fn or sh_backward_views
         self.widths = dict(means3D=3, scales=3, rotations=4, opacities=1, shs=3 * self.M)
-        self.fields = FIELDS_COMPACT if self.compact else FIELDS_DENSE
+        self.fields = FIELDS_DENSE if mode == "dense" else FIELDS_COMPACT
         cols = sum(self.widths[k] for k in self.fields)
         f32 = dict(dtype=torch.float32, device=self.device)
+        if self.sharded:
+            self._init_sharded(cols, f32, coalesce)
+            return
         self.bounds = chunk_bounds(self.n, chunks)
         self.chunk_len = self.bounds[0][1] - self.bounds[0][0]
         # compact: chunk 0's all-reduce block ends with a (world, 3) camera-position block
@@ -305,11 +328,93 @@ class ViewGradReducer:
         self._materialised: Optional[Dict[str, torch.Tensor]] = None
         self._stats_synced = False  # sync_densify_stats has reduced the statistics since the last reset
 
+    def _init_sharded(self, cols: int, f32: dict, coalesce: Optional[bool]) -> None:
+        """Buffers of the sharded exchange: the backward writes the full (n, w) gradient fields (padded to N S rows)
+        and the (n, 3) colour factors; each field is reduce-scattered to its (S, w) shard, the factors go through one
+        all-to-all into (N, S, 3), and the cameras ride in the reduce-scatter group as an (N, N, 3) block whose block j
+        holds every rank's camera in its own row (block j's sum, rank j's share, is every camera)."""
+        N, n = self.world, self.n
+        S = max(256, -(-(-(-n // N)) // 256) * 256)
+        self.shard_len = S
+        self.shard = (min(n, self.rank * S), min(n, self.rank * S + S))
+        L = self.shard[1] - self.shard[0]
+        Np = N * S
+        self.bounds = [(0, n)]
+        self.chunk_len = n
+        self.flat = torch.zeros(cols * Np, **f32)
+        self.full: Dict[str, torch.Tensor] = {}
+        self.shard_views: Dict[str, torch.Tensor] = {}
+        self.shard_flat = torch.zeros(cols * S, **f32)
+        o = 0
+        for k in self.fields:
+            w = self.widths[k]
+            self.full[k] = self.flat[o * Np:(o + w) * Np].view(Np, w)
+            self.shard_views[k] = self.shard_flat[o * S:(o + w) * S].view(S, w)
+            o += w
+        self.chunk_flat = [self.flat]
+        self.chunk_views = [{k: v[:n] for k, v in self.full.items()}]
+        self.cam_rs = torch.zeros(N * N * 3, **f32)
+        self.campos_all = torch.zeros(N, 3, **f32)
+        self.colors = torch.zeros(Np, 3, **f32)
+        self.factors_all = torch.zeros(N, S, 3, **f32)
+        self.shs = torch.zeros(L, self.M, 3, **f32)
+        self.means2D = torch.zeros(n, 3, **f32)
+        self.stats_accum = torch.zeros(n, 2, **f32)
+        self.radii_max = torch.zeros(n, dtype=torch.int32, device=self.device)
+        nccl = self.distributed and dist.get_backend(self.group) == "nccl"
+        self.coalesce = nccl if coalesce is None else (bool(coalesce) and nccl)  # the reduce-scatters as one group
+        self.sync_ops = True
+        self.comm_stream = None
+        self.handoff = None
+        self._pending = []
+        self._side_means = None
+        self._expanded = set()
+        self._camera_source = None
+        self._sh_expanded = True
+        self._materialised = None
+        self._stats_synced = False
+
+    def _sharded_exchange(self, means3D: torch.Tensor, campos: Optional[torch.Tensor], expand_sh: bool) -> None:
+        if campos is None:
+            raise RuntimeError("sharded exchange: pass this view's campos to reduce() (it rides in the reduce-scatter)")
+        N, S = self.world, self.shard_len
+        self.cam_rs.view(N, N, 3)[:, self.rank].copy_(campos.reshape(1, 3).to(torch.float32).expand(N, 3))
+        pairs = [(self.shard_views[k], self.full[k]) for k in self.fields]
+        pairs.append((self.campos_all, self.cam_rs))
+        if not self.distributed:  # one rank without a group: the shard is everything
+            for out, inp in pairs:
+                out.copy_(inp.view_as(out))
+            self.factors_all.view(-1).copy_(self.colors.view(-1))
+        else:
+            if self.coalesce:
+                # torch's coalesced fast path (reduce_scatter_tensor_coalesced, one RCCL group; FSDP's path)
+                with dist.distributed_c10d._coalescing_manager(group=self.group):
+                    for out, inp in pairs:
+                        dist.reduce_scatter_tensor(out.view(-1), inp.reshape(-1), group=self.group)
+            else:
+                for out, inp in pairs:
+                    dist.reduce_scatter_tensor(out.view(-1), inp.reshape(-1), group=self.group)
+            dist.all_to_all_single(self.factors_all.view(-1), self.colors.view(-1), group=self.group)
+        self._sh_expanded = bool(expand_sh)
+        if expand_sh and self.shs.shape[0] > 0:
+            g0, g1 = self.shard
+            self._sh_views(means3D[g0:g1], self.campos_all, self._shard_factors(), self.D, self.M, out=self.shs,
+                           chunk_len=0)
+
+    def _shard_factors(self) -> torch.Tensor:
+        """(N, L, 3) every view's colour factors of this rank's L Gaussians (a copy only for a short last shard)."""
+        L = self.shard[1] - self.shard[0]
+        f = self.factors_all
+        return f if L == self.shard_len else f[:, :L].contiguous()
+
     @property
     def chunks(self) -> int:
         return len(self.bounds)
 
     def describe(self) -> str:
+        if self.sharded:
+            return (f"sharded (reduce-scatter of 11 floats + cameras{' as one group' if self.coalesce else ''}, "
+                    f"all-to-all of the colour factors; this rank owns Gaussians [{self.shard[0]}, {self.shard[1]}))")
         return (f"{self.mode}, {self.chunks} chunk(s), expand={self.expand if self.compact else '-'}, "
                 f"{'one RCCL group per chunk' if self.coalesce else 'separate collectives'}, "
                 f"{'blocking' if self.sync_ops else 'async'} ops"
@@ -324,7 +429,9 @@ class ViewGradReducer:
         v = self.chunk_views[0]
         out = dict(means3D=v["means3D"], scales=v["scales"], rotations=v["rotations"], opacities=v["opacities"],
                    means2D=self.means2D, densify_stats=self.stats_accum, max_radii2D=self.radii_max)
-        if self.compact:
+        if self.sharded:
+            out["colors_sh"] = self.colors[:self.n]
+        elif self.compact:
             out["colors_sh"] = self.gather_in[0]
             out["campos_rows"] = (self.campos_all, self.rank)
             self._camera_source = "backward"
@@ -336,10 +443,12 @@ class ViewGradReducer:
         """Keyword arguments of backward_raw for this reducer (chunks == 1): the destinations, the SH mode and
         accumulate_stats=True -- the statistics destinations are running sums over views and steps, so a plain
         backward_out() with accumulate_stats left False would overwrite them."""
-        return dict(out=self.backward_out(), compact_sh=self.compact, accumulate_stats=True)
+        return dict(out=self.backward_out(), compact_sh=self.compact or self.sharded, accumulate_stats=True)
 
     def chunk_outputs(self) -> List[Tuple[int, int, Dict[str, torch.Tensor]]]:
         """(g_begin, g_end, destinations) per chunk, for rasterizer.backward_chunked."""
+        if self.sharded:
+            raise RuntimeError("the sharded exchange is unchunked: use backward_kwargs() and reduce()")
         self._check_not_synced()
         res = []
         for c, (g0, g1) in enumerate(self.bounds):
@@ -430,6 +539,8 @@ class ViewGradReducer:
     def start_chunk(self, c: int) -> None:
         """Chunk c's gradients have been enqueued on the current stream: issue its collectives (one group, or the
         all-gather first, so the SH expansion that needs it can start while the all-reduce still runs)."""
+        if self.sharded:
+            raise RuntimeError("the sharded exchange is unchunked: use backward_kwargs() and reduce()")
         if c == 0 and self.compact:
             self._check_camera_block()  # before chunk 0's all-reduce sums the camera block
         gather = reduce = None
@@ -515,7 +626,12 @@ class ViewGradReducer:
 
     def reduce(self, means3D: torch.Tensor, campos: Optional[torch.Tensor] = None, expand_sh: bool = True) -> None:
         """The whole exchange after an unchunked backward (backward_out()): every chunk at once.  campos: only when
-        the backward did not write the camera block (see begin_step)."""
+        the backward did not write the camera block (see begin_step); the sharded exchange always takes it here."""
+        if self.sharded:
+            self._check_not_synced()
+            self._materialised = None
+            self._sharded_exchange(means3D, campos, expand_sh)
+            return
         self.begin_step(campos)
         for c in range(self.chunks):
             self.start_chunk(c)
@@ -526,6 +642,10 @@ class ViewGradReducer:
         (the chunk-major gather buffer) and cameras, for GaussianAdam.step(sh_views=(features_dc, features_rest,
         this)), which expands it inside the update instead of reading a (P, M, 3) gradient."""
         from .optim import ShViewsGradient
+        if self.sharded:  # this rank's shard: every view's factors and camera
+            g0, g1 = self.shard
+            return ShViewsGradient(means3D=means3D[g0:g1].contiguous(), campos=self.campos_all,
+                                   factors=self._shard_factors(), sh_degree=self.D, chunk_len=0)
         if not self.compact:
             raise RuntimeError("sh_views_gradient: the dense exchange carries dL/dshs itself")
         return ShViewsGradient(means3D=means3D.contiguous(), campos=self.campos_all, factors=self.gather_all_flat,
@@ -560,6 +680,11 @@ class ViewGradReducer:
         """Per-field (n, w) gradients: views of the exchange buffer with one chunk, else gathered from the chunk
         blocks once per step (one copy of 11 (compact) / 59 (dense) floats per Gaussian)."""
         shs = self.shs if self._sh_expanded else None
+        if self.sharded:  # this rank's shard [g0, g1) of every field
+            L = self.shard[1] - self.shard[0]
+            return dict(means3D=self.shard_views["means3D"][:L], scales=self.shard_views["scales"][:L],
+                        rotations=self.shard_views["rotations"][:L], opacities=self.shard_views["opacities"][:L],
+                        shs=shs)
         if self.chunks == 1:
             v = self.chunk_views[0]
             return dict(means3D=v["means3D"], scales=v["scales"], rotations=v["rotations"],

@@ -53,13 +53,16 @@ def worker(rank, world, port, mode, result_dir, chunks=1, expand="chunk", expand
         def fill(out, g0, g1):  # what the backward writes for Gaussians [g0, g1)
             for k in ("means3D", "scales", "rotations", "opacities"):
                 out[k].copy_(torch.from_numpy(g[k][g0:g1]).reshape(out[k].shape))
-            if red.compact:
+            if red.compact or red.sharded:
                 out["colors_sh"].copy_(torch.from_numpy(g["colors_sh"][g0:g1]))
             else:
                 out["shs"].copy_(torch.from_numpy(g["shs"][g0:g1]).reshape(out["shs"].shape))
 
         red.means2D.copy_(torch.from_numpy(g["means2D"]))
-        if red.chunks == 1:
+        if red.sharded:  # unchunked; this rank ends with its shard of every reduced field
+            fill(red.backward_out(), 0, N)
+            red.reduce(means3D, torch.from_numpy(g["campos"]), expand_sh=expand_sh)
+        elif red.chunks == 1:
             fill(red.backward_out(), 0, N)
             red.reduce(means3D, torch.from_numpy(g["campos"]), expand_sh=expand_sh)
         else:  # the overlapped form: each chunk's exchange starts as soon as its gradients exist
@@ -73,9 +76,10 @@ def worker(rank, world, port, mode, result_dir, chunks=1, expand="chunk", expand
         if not expand_sh:  # the factored form GaussianAdam.step(sh_views=...) consumes, expanded here by the oracle
             assert grads["shs"] is None
             f = red.sh_views_gradient(means3D)
-            grads["shs"] = oracle_sh_views(f.means3D, f.campos, f.factors, f.sh_degree, 16, torch.zeros(N, 16, 3),
-                                           f.chunk_len)
+            grads["shs"] = oracle_sh_views(f.means3D, f.campos, f.factors, f.sh_degree, 16,
+                                           torch.zeros(f.means3D.shape[0], 16, 3), f.chunk_len)
         res = {k: v.numpy() for k, v in grads.items()}
+        res["shard"] = np.array(red.shard if red.sharded else (0, N))
         stats, radii_max = red.sync_densify_stats()
         res["stats"] = stats.numpy()
         res["radii_max"] = radii_max.numpy()

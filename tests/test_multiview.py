@@ -64,6 +64,25 @@ def test_two_rank_exchange(tmp_path, expected, mode):
     assert (expected["stats1"] == 2).any() and (expected["stats1"] == 1).any()  # views overlap only partly
 
 
+@pytest.mark.parametrize("expand_sh", [True, False])
+def test_sharded_exchange(tmp_path, expected, expand_sh):
+    """The sharded (ZeRO-style) exchange: rank r ends with ITS shard [g0, g1) of every reduced field -- the same sums
+    as the all-reduce of the compact exchange, bitwise (two summands) -- and the SH gradient of its shard, expanded
+    from every view's colour factors delivered by the all-to-all (or, expand_sh=False, the factored form the fused SH
+    Adam takes); the shards tile [0, n); statistics and radii are the full reduced arrays on every rank."""
+    comp = _run(tmp_path, "compact", 1)
+    res = _run(tmp_path, "sharded", 1, expand_sh=expand_sh)
+    bounds = [tuple(int(x) for x in r["shard"]) for r in res]
+    assert bounds[0][0] == 0 and bounds[-1][1] == MW.N and all(a[1] == b[0] for a, b in zip(bounds, bounds[1:]))
+    for r, (g0, g1) in enumerate(bounds):
+        for k in ("means3D", "scales", "rotations", "opacities", "shs"):
+            assert np.array_equal(res[r][k], comp[r][k][g0:g1]), (r, k)
+        for k in ("stats", "radii_max"):
+            assert np.array_equal(res[r][k], comp[r][k]), (r, k)
+        np.testing.assert_allclose(res[r]["means3D"], expected["means3D"][g0:g1].reshape(res[r]["means3D"].shape),
+                                   rtol=1e-6, atol=1e-12)
+
+
 @pytest.mark.parametrize("mode", ["dense", "compact"])
 def test_chunked_exchange_is_bitwise_the_unchunked_one(tmp_path, mode):
     """The overlapped exchange (Gaussian chunks, one all-reduce + all-gather per chunk issued as the chunk's
@@ -101,13 +120,17 @@ def test_exchange_plan_cost_model():
                                                             simulate_exchange)
     assert abs(exchange_bytes_per_gaussian("dense", 8) - 413.0) < 0.01
     assert abs(exchange_bytes_per_gaussian("compact", 8) - 161.0) < 0.01
+    assert abs(exchange_bytes_per_gaussian("sharded", 8) - 49.0) < 0.01
     assert exchange_bytes_per_gaussian("compact", 1) == 0.0
+    assert exchange_bytes_per_gaussian("sharded", 1) == 0.0
     for N in (2, 4, 8):
         p = plan_exchange(1_000_000, N)
-        assert p["mode"] == "compact", (N, p)
+        assert p["mode"] == "sharded", (N, p)
+        assert plan_exchange(1_000_000, N, modes=("compact", "dense"))["mode"] == "compact"
         slow = plan_exchange(1_000_000, N, costs=dict(bus_efficiency=0.2))
         assert slow["end_ms"] > p["end_ms"]
-    for mode in ("dense", "compact"):
+    assert plan_exchange(1_000_000, 1)["mode"] == "dense"  # one rank: nothing crosses a link
+    for mode in ("dense", "compact", "sharded"):
         for K in (1, 2, 4, 8):
             for expand in ("chunk", "once"):
                 r = simulate_exchange(1_000_000, 8, mode, K, expand)

@@ -25,7 +25,7 @@ def _step(red, st, rs, dc, di, means3D, chunked, early=True):
         red.finish(means3D)
     else:
         backward_raw(st, rs, dc, di, **red.backward_kwargs())
-        red.reduce(means3D)
+        red.reduce(means3D, rs.campos if red.sharded else None)
 
 
 def _run(dev, distributed, mode, chunks, views=2, early=True, **kw):
@@ -57,6 +57,7 @@ VARIANTS = [  # (mode, chunks, reducer options): one RCCL group per chunk unless
     ("compact", 2, dict(expand="side", early=False)),  # "side" without means3D at begin_step: expands in finish()
     ("compact", 4, dict(handoff="value")), ("compact", 4, dict(expand="side", handoff="value")),
     ("dense", 2, dict(handoff="value")),  # stream-value hand-offs (gsr_stream_signal / gsr_stream_wait)
+    ("sharded", 1, {}), ("sharded", 1, dict(coalesce=False)),  # reduce-scatter (+ cameras) and all-to-all
 ]
 
 

@@ -143,7 +143,27 @@ def train_step(params, opt, red, views, dev):
     opt.step(sh_views=(params["f_dc"], params["f_rest"], red.sh_views_gradient(params["means3D"].detach())))
 
 
-def _rank_worker(rank, world, port, result, chunks):
+def train_step_sharded(full, own, opt, red, view, rank, dev):
+    """The sharded (ZeRO-style) step: the exchange leaves this rank the reduced gradients of its shard, Adam steps the
+    shard's rows of the padded parameters, and every rank's updated shard is all-gathered back."""
+    import torch.distributed as dist
+    from gaussian_splatting_lightning_amd.rasterizer import backward_raw, forward_raw
+    rs, dc, di = view
+    shs = torch.cat([full["f_dc"][:N], full["f_rest"][:N]], 1).contiguous()
+    _, _, _, st = forward_raw(full["means3D"][:N], shs, None, full["opacities"][:N], full["scales"][:N],
+                              full["rotations"][:N], None, rs)
+    backward_raw(st, rs, dc, di, **red.backward_kwargs())
+    red.reduce(full["means3D"][:N], rs.campos, expand_sh=False)
+    g = red.grads
+    for k in ("means3D", "scales", "rotations", "opacities"):
+        own[k].grad = g[k].view_as(own[k])
+    opt.step(sh_views=(own["f_dc"], own["f_rest"], red.sh_views_gradient(full["means3D"][:N])))
+    S = red.shard_len
+    for t in full.values():
+        dist.all_gather_into_tensor(t.view(-1), t[rank * S:(rank + 1) * S].reshape(-1).clone())
+
+
+def _rank_worker(rank, world, port, result, chunks, mode="compact"):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -152,10 +172,28 @@ def _rank_worker(rank, world, port, result, chunks):
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
         params = _make_params(dev)
-        opt = _optimizer(params)
-        red = ViewGradReducer(N, 16, 3, dev, mode="compact", chunks=chunks)
+        red = ViewGradReducer(N, 16, 3, dev, mode=mode, chunks=chunks)
         out = {}
+        if mode == "sharded":  # parameters padded to the shards' rows, the optimizer over this rank's shard
+            rows = world * red.shard_len
+            full = {}
+            for k, v in params.items():
+                full[k] = torch.zeros((rows,) + tuple(v.shape[1:]), device=dev)
+                full[k][:N] = v.detach()
+            g0, g1 = red.shard
+            own = {k: v[g0:g1] for k, v in full.items()}
+            opt = _optimizer(own)
+        else:
+            opt = _optimizer(params)
         for step in range(2):
+            if mode == "sharded":
+                train_step_sharded(full, own, opt, red, _view(2 * step + rank, dev), rank, dev)
+                torch.cuda.synchronize()
+                out.update({f"{k}_{step}": v[:N].cpu().numpy() for k, v in full.items()})
+                out.update({f"shardgrad_{k}_{step}": v.detach().cpu().numpy() for k, v in red.grads.items()
+                            if v is not None})
+                out["shard"] = np.array(red.shard)
+                continue
             train_step(params, opt, red, [_view(2 * step + rank, dev)], dev)
             torch.cuda.synchronize()
             out.update({f"{k}_{step}": v.detach().cpu().numpy() for k, v in params.items()})
@@ -165,10 +203,11 @@ def _rank_worker(rank, world, port, result, chunks):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("chunks", [1, 2])
-def test_two_rank_train_step_matches_local_sum(gpu_device, tmp_path, chunks):
-    """Two gloo ranks on the one GPU, each rendering its own view per step, compact exchange + fused SH Adam, two
-    steps: both ranks end with the same parameters, bitwise equal to one process that renders both views itself,
+@pytest.mark.parametrize("chunks,mode", [(1, "compact"), (2, "compact"), (1, "sharded")])
+def test_two_rank_train_step_matches_local_sum(gpu_device, tmp_path, chunks, mode):
+    """Two gloo ranks on the one GPU, each rendering its own view per step, compact exchange + fused SH Adam (or the
+    sharded exchange: each rank steps its shard, then the parameters are all-gathered), two steps: both ranks end with
+    the same parameters, bitwise equal to one process that renders both views itself,
     sums their non-SH gradients, expands the SH gradient from both views' colour factors (gsr_sh_backward_views) and
     steps GaussianAdam on the expanded gradient."""
     import torch.multiprocessing as mp
@@ -176,7 +215,7 @@ def test_two_rank_train_step_matches_local_sum(gpu_device, tmp_path, chunks):
     ctx = mp.get_context("spawn")
     port = _free_port()
     res = os.path.join(str(tmp_path), "rank{rank}.npz")
-    procs = [ctx.Process(target=_rank_worker, args=(r, 2, port, res, chunks)) for r in range(2)]
+    procs = [ctx.Process(target=_rank_worker, args=(r, 2, port, res, chunks, mode)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
@@ -184,7 +223,7 @@ def test_two_rank_train_step_matches_local_sum(gpu_device, tmp_path, chunks):
         assert p.exitcode == 0, f"rank exited with {p.exitcode}"
     got = [dict(np.load(res.format(rank=r))) for r in range(2)]
     for k in got[0]:
-        if not k.startswith("grad_"):
+        if not k.startswith(("grad_", "shardgrad_", "shard")):
             _same(got[0][k], got[1][k], k)  # every rank holds the same parameters
     dev = gpu_device
     params = _make_params(dev)
@@ -208,7 +247,13 @@ def test_two_rank_train_step_matches_local_sum(gpu_device, tmp_path, chunks):
             campos[j] = rs.campos
         for k in acc:
             params[k].grad = acc[k].view_as(params[k])
-            _same(got[0][f"grad_{k}_{step}"], acc[k].view(N, -1).cpu().numpy(), f"grad {k} step {step}")
+            if mode == "sharded":  # each rank holds the reduced gradients of its own shard
+                for r in range(2):
+                    g0, g1 = (int(x) for x in got[r]["shard"])
+                    _same(got[r][f"shardgrad_{k}_{step}"], acc[k].view(N, -1)[g0:g1].cpu().numpy(),
+                          f"rank {r} grad {k} step {step}")
+            else:
+                _same(got[0][f"grad_{k}_{step}"], acc[k].view(N, -1).cpu().numpy(), f"grad {k} step {step}")
         dsh = sh_backward_views(params["means3D"].detach(), campos, factors, 3, 16)
         params["f_dc"].grad = dsh[:, :1].contiguous()
         params["f_rest"].grad = dsh[:, 1:].contiguous()
