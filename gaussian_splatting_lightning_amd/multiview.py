@@ -76,6 +76,8 @@ EXCHANGE_COSTS = dict(
     group_sync_ms=0.008,     # one blocking collective group on the compute stream (K = 1)
     chunk_ms=0.0135,         # per extra chunk: per-Gaussian and expansion launches + the chunk's event hand-off
     side_fixed_ms=0.0205,    # K > 1: the compute stream's waits for the side stream
+    sharded_fixed_ms=0.030,  # sharded: the camera rows' fill and two blocking ops (reduce-scatter group, all-to-all),
+                             # ~12 us of compute-queue gap each in the one-rank trace (profiles/r6z_*)
     link_GBps=153.0,
     links=7,
     bus_efficiency=0.6,
@@ -113,7 +115,7 @@ def simulate_exchange(n: int, world: int, mode: str, chunks: int, expand: str = 
     exp = (c["exp_ms"] + c["exp_view_ms"] * (N - 1)) * scale if mode != "dense" else 0.0
     if mode == "sharded":  # K = 1: the reduce-scatter group and the all-to-all, then the shard's expansion
         exp /= N
-        end = pb + 2 * c["group_sync_ms"] + comm + exp
+        end = pb + c["sharded_fixed_ms"] + comm + exp
         return {"mode": mode, "chunks": 1, "expand": "once", "per_gaussian_stage_ms": round(pb, 4),
                 "link_MB": round(link_bytes / 1e6, 1), "comm_ms": round(comm, 4), "end_ms": round(end, 4),
                 "exposed_ms": round(end - pb, 4)}
