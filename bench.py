@@ -273,7 +273,7 @@ def main():
             if distributed else ViewGradReducer(n, M, deg, dev, mode="compact", chunks=1)
         # parameters padded to the shards' N S rows (the rasterizer reads the first n), so every rank's updated shard
         # is all-gathered in place
-        rows = world * tred.shard_len if tred.sharded else n
+        rows = tred.padded_rows()
 
         def padded(t):
             out = torch.zeros((rows,) + tuple(t.shape[1:]), device=dev)
@@ -295,17 +295,6 @@ def main():
                              {"params": [own["_scaling"]], "lr": 0.005, "name": "scaling"},
                              {"params": [own["_rotation"]], "lr": 0.001, "name": "rotation"}], lr=0.0, eps=1e-15)
 
-        def gather_params():
-            """Every rank's updated shard to every rank (in place: rank r's S rows are its input)."""
-            S = tred.shard_len
-            if dist.get_backend() == "nccl":  # torch's coalesced fast path: one RCCL group
-                with dist.distributed_c10d._coalescing_manager():
-                    for t in tp.values():
-                        dist.all_gather_into_tensor(t.view(-1), t[rank * S:(rank + 1) * S].reshape(-1))
-            else:  # gloo rehearsal: no in-place form
-                for t in tp.values():
-                    dist.all_gather_into_tensor(t.view(-1), t[rank * S:(rank + 1) * S].reshape(-1).clone())
-
         def train_step():
             activate(tp["_scaling"][:n], tp["_opacity"][:n], tp["_rotation"][:n], out=act)
             _, _, _, tst = forward_raw(tp["means3D"][:n], tp["shs"][:n], None, act[1], act[0], act[2], None, settings)
@@ -325,8 +314,8 @@ def main():
                 own["means3D"].grad = gr["means3D"].view(L, 3)
                 own["_scaling"].grad, own["_opacity"].grad, own["_rotation"].grad = raw_grad
                 topt.step(sh_views=(f_dc, f_rest, tred.sh_views_gradient(tp["means3D"][:n])))
-            if tred.sharded and tred.distributed:
-                gather_params()
+            if tred.sharded:
+                tred.gather_shards(list(tp.values()))
 
         for _ in range(max(args.warmup, 3)):
             train_step()

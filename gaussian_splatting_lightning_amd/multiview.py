@@ -190,6 +190,10 @@ class ViewGradReducer:
     With chunks == 1, ``backward_raw(..., out=red.backward_out(), ...)`` followed by ``red.reduce(means3D, campos)``
     is the same exchange without overlap.
 
+    mode="sharded" (and mode="auto" when the cost model picks it): ``grads`` and ``sh_views_gradient`` cover only this
+    rank's shard ``self.shard`` = [g0, g1); the caller steps those rows of its parameters (padded to
+    ``padded_rows()``) and calls ``gather_shards(params)``; ``reduce`` takes this view's campos.
+
     mode="auto" / chunks=None take ``plan_exchange``'s choice for this world size.  coalesce (default: on for the
     nccl backend) issues a chunk's all-gather and all-reduce as one RCCL group; sync_ops (default: on when there is
     one chunk) issues them as blocking ops, which torch's RCCL process group enqueues on the current stream -- with
@@ -402,6 +406,30 @@ class ViewGradReducer:
             g0, g1 = self.shard
             self._sh_views(means3D[g0:g1], self.campos_all, self._shard_factors(), self.D, self.M, out=self.shs,
                            chunk_len=0)
+
+    def padded_rows(self) -> int:
+        """Rows of a parameter tensor the sharded training step all-gathers in place (N S >= n; the rasterizer reads
+        the first n)."""
+        return self.world * self.shard_len if self.sharded else self.n
+
+    def gather_shards(self, tensors) -> None:
+        """Sharded training step, after this rank's optimizer stepped its shard: every rank's updated rows to every
+        rank, in place, for tensors of padded_rows() rows (one coalesced RCCL all-gather group)."""
+        if not self.sharded:
+            raise RuntimeError("gather_shards: only the sharded exchange leaves the parameters sharded")
+        if not self.distributed:
+            return
+        S, r = self.shard_len, self.rank
+        for t in tensors:
+            if t.shape[0] != self.padded_rows() or not t.is_contiguous():
+                raise ValueError("gather_shards: contiguous tensors of padded_rows() rows expected")
+        if self.coalesce:  # torch's coalesced fast path (allgather_into_tensor_coalesced): one RCCL group
+            with dist.distributed_c10d._coalescing_manager(group=self.group):
+                for t in tensors:
+                    dist.all_gather_into_tensor(t.view(-1), t[r * S:(r + 1) * S].reshape(-1), group=self.group)
+        else:  # gloo has no in-place form
+            for t in tensors:
+                dist.all_gather_into_tensor(t.view(-1), t[r * S:(r + 1) * S].reshape(-1).clone(), group=self.group)
 
     def _shard_factors(self) -> torch.Tensor:
         """(N, L, 3) every view's colour factors of this rank's L Gaussians (a copy only for a short last shard)."""

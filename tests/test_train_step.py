@@ -146,7 +146,6 @@ def train_step(params, opt, red, views, dev):
 def train_step_sharded(full, own, opt, red, view, rank, dev):
     """The sharded (ZeRO-style) step: the exchange leaves this rank the reduced gradients of its shard, Adam steps the
     shard's rows of the padded parameters, and every rank's updated shard is all-gathered back."""
-    import torch.distributed as dist
     from gaussian_splatting_lightning_amd.rasterizer import backward_raw, forward_raw
     rs, dc, di = view
     shs = torch.cat([full["f_dc"][:N], full["f_rest"][:N]], 1).contiguous()
@@ -158,9 +157,7 @@ def train_step_sharded(full, own, opt, red, view, rank, dev):
     for k in ("means3D", "scales", "rotations", "opacities"):
         own[k].grad = g[k].view_as(own[k])
     opt.step(sh_views=(own["f_dc"], own["f_rest"], red.sh_views_gradient(full["means3D"][:N])))
-    S = red.shard_len
-    for t in full.values():
-        dist.all_gather_into_tensor(t.view(-1), t[rank * S:(rank + 1) * S].reshape(-1).clone())
+    red.gather_shards(list(full.values()))
 
 
 def _rank_worker(rank, world, port, result, chunks, mode="compact"):
@@ -175,7 +172,7 @@ def _rank_worker(rank, world, port, result, chunks, mode="compact"):
         red = ViewGradReducer(N, 16, 3, dev, mode=mode, chunks=chunks)
         out = {}
         if mode == "sharded":  # parameters padded to the shards' rows, the optimizer over this rank's shard
-            rows = world * red.shard_len
+            rows = red.padded_rows()
             full = {}
             for k, v in params.items():
                 full[k] = torch.zeros((rows,) + tuple(v.shape[1:]), device=dev)
