@@ -80,6 +80,9 @@ def parse():
     ap.add_argument("--exchange-handoff", default=None, choices=("event", "value"),
                     help="chunked exchange: hand-offs between the compute and the collective stream by hipEvents or "
                          "by stream-ordered device words (gsr_stream_signal / gsr_stream_wait)")
+    ap.add_argument("--exchange-groups", type=int, default=0, choices=(0, 1, 2),
+                    help="sharded exchange over RCCL: 1 = the reduce-scatters and the all-to-all as one group, 2 = as "
+                         "two (0: the reducer's default)")
     ap.add_argument("--plan-world", type=int, default=0,
                     help="N>1 path: plan the exchange (mode, chunks, SH expansion) for this many ranks instead of "
                          "WORLD_SIZE -- a one-rank rehearsal (--force-dist) of the N-GPU schedule")
@@ -143,7 +146,8 @@ def main():
     if distributed:
         red = ViewGradReducer(n, M, deg, dev, mode=args.exchange, chunks=args.exchange_chunks or None,
                               expand=args.exchange_expand, plan_world=args.plan_world or None,
-                              handoff=args.exchange_handoff)
+                              handoff=args.exchange_handoff,
+                              one_group=None if not args.exchange_groups else args.exchange_groups == 1)
     else:
         red = ViewGradReducer(n, M, deg, dev, mode="dense", chunks=1)
     mode = red.mode
@@ -269,7 +273,8 @@ def main():
         else:
             tmode = "sharded" if args.exchange == "sharded" else "compact"
         tred = ViewGradReducer(n, M, deg, dev, mode=tmode, chunks=None if tmode == "compact" else 1,
-                               plan_world=args.plan_world or None, handoff=args.exchange_handoff) \
+                               plan_world=args.plan_world or None, handoff=args.exchange_handoff,
+                               one_group=None if not args.exchange_groups else args.exchange_groups == 1) \
             if distributed else ViewGradReducer(n, M, deg, dev, mode="compact", chunks=1)
         # parameters padded to the shards' N S rows (the rasterizer reads the first n), so every rank's updated shard
         # is all-gathered in place

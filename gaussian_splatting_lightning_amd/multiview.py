@@ -205,7 +205,8 @@ class ViewGradReducer:
                  sh_views_fn: Optional[Callable[..., torch.Tensor]] = None, chunks: Optional[int] = 1,
                  distributed: Optional[bool] = None, expand: Optional[str] = None,
                  coalesce: Optional[bool] = None, sync_ops: Optional[bool] = None, comm_stream: Optional[str] = None,
-                 plan_world: Optional[int] = None, handoff: Optional[str] = None):
+                 plan_world: Optional[int] = None, handoff: Optional[str] = None,
+                 one_group: Optional[bool] = None):
         if mode not in ("dense", "compact", "sharded", "auto"):
             raise ValueError(f"mode must be 'dense', 'compact', 'sharded' or 'auto', got {mode!r}")
         self.n, self.M, self.D = int(n), int(M), int(sh_degree)
@@ -243,7 +244,7 @@ class ViewGradReducer:
         cols = sum(self.widths[k] for k in self.fields)
         f32 = dict(dtype=torch.float32, device=self.device)
         if self.sharded:
-            self._init_sharded(cols, f32, coalesce)
+            self._init_sharded(cols, f32, coalesce, one_group)
             return
         self.bounds = chunk_bounds(self.n, chunks)
         self.chunk_len = self.bounds[0][1] - self.bounds[0][0]
@@ -292,6 +293,7 @@ class ViewGradReducer:
         # process group would flush the ops queued before the failure and the fallback would issue them again)
         if self.coalesce and not _coalescing_supported(self._pg()):
             self.coalesce = False
+        self.one_group = False  # (sharded exchange only)
         self.sync_ops = (self.chunks == 1) if sync_ops is None else bool(sync_ops)
         # comm_stream="side" (chunked exchange on a HIP device): the reducer's own stream carries the
         # collectives as blocking ops behind one event per chunk, and the compute stream waits for chunk c's group
@@ -334,7 +336,7 @@ class ViewGradReducer:
         self._materialised: Optional[Dict[str, torch.Tensor]] = None
         self._stats_synced = False  # sync_densify_stats has reduced the statistics since the last reset
 
-    def _init_sharded(self, cols: int, f32: dict, coalesce: Optional[bool]) -> None:
+    def _init_sharded(self, cols: int, f32: dict, coalesce: Optional[bool], one_group: Optional[bool]) -> None:
         """Buffers of the sharded exchange: the backward writes the full (n, w) gradient fields (padded to N S rows)
         and the (n, 3) colour factors; each field is reduce-scattered to its (S, w) shard, the factors go through one
         all-to-all into (N, S, 3), and the cameras ride in the reduce-scatter group as an (N, N, 3) block whose block j
@@ -369,6 +371,7 @@ class ViewGradReducer:
         self.radii_max = torch.zeros(n, dtype=torch.int32, device=self.device)
         nccl = self.distributed and dist.get_backend(self.group) == "nccl"
         self.coalesce = nccl if coalesce is None else (bool(coalesce) and nccl)  # the reduce-scatters as one group
+        self.one_group = self.coalesce and (True if one_group is None else bool(one_group))  # + the all-to-all
         self.sync_ops = True
         self.comm_stream = None
         self.handoff = None
@@ -393,14 +396,20 @@ class ViewGradReducer:
             self.factors_all.view(-1).copy_(self.colors.view(-1))
         else:
             if self.coalesce:
-                # torch's coalesced fast path (reduce_scatter_tensor_coalesced, one RCCL group; FSDP's path)
-                with dist.distributed_c10d._coalescing_manager(group=self.group):
+                # torch's coalesced fast path (reduce_scatter_tensor_coalesced, one RCCL group; FSDP's path); with
+                # one_group the all-to-all is issued inside the process group's own coalescing block too, so the
+                # reduce-scatters and it leave as ONE RCCL group (one launch, one hand-off to the compute stream)
+                dev = self.device if self.one_group else None
+                with dist.distributed_c10d._coalescing_manager(group=self.group, device=dev):
                     for out, inp in pairs:
                         dist.reduce_scatter_tensor(out.view(-1), inp.reshape(-1), group=self.group)
+                    if self.one_group:
+                        dist.all_to_all_single(self.factors_all.view(-1), self.colors.view(-1), group=self.group)
             else:
                 for out, inp in pairs:
                     dist.reduce_scatter_tensor(out.view(-1), inp.reshape(-1), group=self.group)
-            dist.all_to_all_single(self.factors_all.view(-1), self.colors.view(-1), group=self.group)
+            if not (self.coalesce and self.one_group):
+                dist.all_to_all_single(self.factors_all.view(-1), self.colors.view(-1), group=self.group)
         self._sh_expanded = bool(expand_sh)
         if expand_sh and self.shs.shape[0] > 0:
             g0, g1 = self.shard

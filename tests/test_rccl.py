@@ -58,6 +58,7 @@ VARIANTS = [  # (mode, chunks, reducer options): one RCCL group per chunk unless
     ("compact", 4, dict(handoff="value")), ("compact", 4, dict(expand="side", handoff="value")),
     ("dense", 2, dict(handoff="value")),  # stream-value hand-offs (gsr_stream_signal / gsr_stream_wait)
     ("sharded", 1, {}), ("sharded", 1, dict(coalesce=False)),  # reduce-scatter (+ cameras) and all-to-all
+    ("sharded", 1, dict(one_group=False)),  # the reduce-scatter group and the all-to-all as two RCCL groups
 ]
 
 
@@ -71,6 +72,8 @@ def test_rccl_exchange_one_rank_is_bitwise_local(gpu_device, mode, chunks, kw):
         got = _run(gpu_device, True, mode, chunks, **kw)
         red = got[3]
         assert red.coalesce == kw.get("coalesce", True)  # the grouped path really ran (no fallback)
+        if mode == "sharded":
+            assert red.one_group == (kw.get("coalesce", True) and kw.get("one_group", True))
         if kw.get("handoff") == "value":
             assert red.handoff == "value"  # the device supports stream wait values: no silent event fallback
         if kw.get("expand") == "side" and kw.get("early", True):
