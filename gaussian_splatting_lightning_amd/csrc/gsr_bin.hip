@@ -946,7 +946,9 @@ void launch_seg_sort(hipStream_t s, const SegSortParams &p0) {
     if (p0.T == 0) return;
     SegSortParams p = p0;
     p.stamps = tuning("stamp", 0) ? stamp_buffer(2) : nullptr;
-    const uint32_t grid = std::min(div_up(p.T, 4), (uint32_t)tuning("seg_grid", 1536));
+    // one wave per tile up to 16384 tiles (cfg 3, 8160 tiles: 2040 workgroups, seg_sort 0.0490 -> 0.0472 ms against a
+    // 1536-workgroup cap, profiles/r6ai_ab_launch_knobs_cfg3.txt)
+    const uint32_t grid = std::min(div_up(p.T, 4), (uint32_t)tuning("seg_grid", 4096));
     const int minw = tuning("seg_minw", 6);  // 80 VGPRs: 0.053 vs 0.060 ms at 4 waves/SIMD
     if (tuning("seg32", 1) && minw >= 7) seg_sort_kernel<true, 7><<<grid, 256, 0, s>>>(p);
     else if (tuning("seg32", 1) && minw == 6) seg_sort_kernel<true, 6><<<grid, 256, 0, s>>>(p);
