@@ -728,6 +728,45 @@ int gsr_forward(gsr_forward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *
     return GSR_OK;
 }
 
+// The per-Gaussian outputs preprocess_bwd writes for Gaussians [g0, g1), as zero-fill segments of the composite backward
+// (RenderBwdParams::zf_*): each output's 16-B aligned interior, its unaligned head / tail words listed.  At cfg 3,
+// 78 % of the Gaussians have an identically zero gradient (culled, or no pixel took one; tools/zero_grad_census.py):
+// their ~250 B of zeros are stored by the VALU-bound walk instead of the HBM-bound per-Gaussian pass.  False (no
+// plan): a pointer not 4-B aligned, or too many segments / odd words.
+static bool zero_fill_plan(const gsr_backward_args *a, int64_t g0, int64_t g1, RenderBwdParams &rp) {
+    const size_t ng = (size_t)(g1 - g0);
+    const bool sh_stage = !a->colors_precomp && a->shs && a->M > 0;  // preprocess_bwd writes the SH outputs
+    struct Out { float *p; size_t w; };
+    const Out outs[] = {{a->dL_dmeans2D, 3}, {a->dL_dcolors, 3}, {a->dL_dopacity, 1}, {a->dL_dmeans3D, 3},
+                        {a->dL_dcov3D, 6}, {sh_stage ? a->dL_dsh : nullptr, (size_t)a->M * 3},
+                        {sh_stage ? a->dL_dcolors_sh : nullptr, 3}, {a->dL_dscales, 3}, {a->dL_drotations, 4}};
+    RenderBwdParams z = rp;
+    z.zf_nseg = z.zf_nodd = 0;
+    z.zf_total16 = 0;
+    for (const Out &o : outs) {
+        if (!o.p || ng == 0) continue;
+        const uintptr_t b = reinterpret_cast<uintptr_t>(o.p), e = b + ng * o.w * sizeof(float);
+        if (b & 3) return false;
+        const uintptr_t ab = std::min((b + 15) & ~(uintptr_t)15, e), ae = std::max(e & ~(uintptr_t)15, ab);
+        for (uintptr_t q = b; q < ab; q += 4) {
+            if (z.zf_nodd >= (uint32_t)RenderBwdParams::ZF_ODD) return false;
+            z.zf_odd[z.zf_nodd++] = reinterpret_cast<uint32_t *>(q);
+        }
+        for (uintptr_t q = ae; q < e; q += 4) {
+            if (z.zf_nodd >= (uint32_t)RenderBwdParams::ZF_ODD) return false;
+            z.zf_odd[z.zf_nodd++] = reinterpret_cast<uint32_t *>(q);
+        }
+        if (ae > ab) {
+            if (z.zf_nseg >= (uint32_t)RenderBwdParams::ZF_SEGS) return false;
+            z.zf_ptr[z.zf_nseg] = reinterpret_cast<uint4 *>(ab);
+            z.zf_total16 += (ae - ab) / 16;
+            z.zf_pre16[++z.zf_nseg] = z.zf_total16;
+        }
+    }
+    rp = z;
+    return true;
+}
+
 int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx, void *stream_ptr) {
     if (!a || !alloc) return fail(GSR_ERR_ARG, "null argument");
     int rc = check_common(a->P, a->D, a->M, a->W, a->H, a->means3D, a->opacities, a->colors_precomp, a->shs,
@@ -777,6 +816,7 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     // the per-Gaussian gather in preprocess_bwd reads each Gaussian's rows contiguously.
     float *bigsum = bwd_bigsum_ptr(scratch, R);
 
+    bool prezero = false;  // the composite zero-fills the per-Gaussian outputs (zero_fill_plan)
     if (R > 0 && a->stages != GSR_BWD_GAUSSIANS) {
         RenderBwdParams rp;
         rp.W = W; rp.H = H; rp.gx = gx; rp.gy = gy; rp.num_tiles = (int)T; rp.num_rendered = R;
@@ -803,6 +843,7 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
             rp.ckpt = b.ckpt; rp.ctot = im.ctot; rp.ck_flag = im.ck_flag;
             rp.seg_list = b.seg_list; rp.seg_count = im.seg_count;
         }
+        if (a->stages == GSR_BWD_ALL && tuning("bwd_prezero", 1)) prezero = zero_fill_plan(a, g0, g1, rp);
         GSR_STAGE(ST_RENDER_BWD, dbg, launch_render_bwd(stream, rp));
         BigReduceParams bp;
         bp.big_list = g.big_list; bp.inst_start = g.inst_start; bp.tiles = g.tiles;
@@ -845,6 +886,7 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     pp.max_radii2D = rel(a->max_radii2D, 1);
     pp.dL_dscales = rel(a->dL_dscales, 3); pp.dL_drot = rel(a->dL_drotations, 4);
     pp.campos_rows = a->campos_rows; pp.campos_rank = a->campos_rank; pp.campos_nrows = a->campos_nrows;
+    pp.prezeroed = prezero ? 1 : 0;
     const size_t ng = (size_t)(g1 - g0);
     if (pp.shs == nullptr && a->dL_dsh && a->M > 0)
         GSR_HIP(hipMemsetAsync(a->dL_dsh, 0, sizeof(float) * ng * a->M * 3, stream));

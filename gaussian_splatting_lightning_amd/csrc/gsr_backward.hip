@@ -31,6 +31,31 @@ namespace gsr {
 //   (Round 1-2 variants -- per-channel accumulators v3, the branch / predication forms of v4 and the scalar-mask
 //   v6 -- were bitwise identical or equal to rounding and measured slower; DESIGN.md §4 keeps their numbers.)
 // ------------------------------------------------------------------------------------------------
+// Zero fill of the per-Gaussian backward outputs (RenderBwdParams::zf_*), this workgroup's share of the virtual
+// array, as non-temporal stores that drain while the other waves' VALU-bound walks run, so the HBM-bound preprocess
+// backward after it stores only the Gaussians whose gradient is not identically zero ...
+typedef unsigned int zf_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void bwd_zero_fill(const RenderBwdParams &p) {
+    if (p.zf_total16 == 0 && p.zf_nodd == 0) return;  // uniform
+    const uint64_t nb = gridDim.x, b = blockIdx.x;
+    const uint64_t per = (p.zf_total16 + nb - 1) / nb;
+    const uint64_t lo = b * per, hi = min(p.zf_total16, lo + per);
+    const zf_u4 z = {0u, 0u, 0u, 0u};
+    for (uint32_t sg = 0; sg < p.zf_nseg; sg++) {
+        const uint64_t s0 = p.zf_pre16[sg], s1 = p.zf_pre16[sg + 1];
+        const uint64_t e = min(hi, s1);
+        zf_u4 *base = reinterpret_cast<zf_u4 *>(p.zf_ptr[sg]) - s0;
+        for (uint64_t k = max(lo, s0) + threadIdx.x; k < e; k += blockDim.x) __builtin_nontemporal_store(z, base + k);
+    }
+    if (b == 0 && threadIdx.x < p.zf_nodd) *p.zf_odd[threadIdx.x] = 0u;
+}
+// ... issued when the workgroup's walk is done (every return path): issued first, the walk's first load wait (vmcnt
+// counts stores too) held each wave until its zero stores had landed
+struct ZeroFillAtExit {
+    const RenderBwdParams &p;
+    __device__ ~ZeroFillAtExit() { bwd_zero_fill(p); }
+};
+
 constexpr int BWD_BATCH = 32;
 constexpr int PART = 12;  // floats per instance in the LDS partial buffer (10 sums + 2 pad)
 
@@ -115,6 +140,7 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
     __shared__ float2 s_c[BWD_BATCH];
     __shared__ uint32_t s_m[BWD_BATCH];
     __shared__ __attribute__((aligned(16))) float s_part[PARTS][BWD_BATCH][PART];
+    const ZeroFillAtExit zero_fill_at_exit{p};
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int slot = blockIdx.x;
     const int tile = p.tile_order ? (int)p.tile_order[slot] : slot;
@@ -290,6 +316,7 @@ __global__ __launch_bounds__(64, GUARD ? 4 : SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MI
     if constexpr (UNION) {
         if (threadIdx.x < 2 * BWD_BATCH) (&s_zero[0][0])[threadIdx.x] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    const ZeroFillAtExit zero_fill_at_exit{p};
     const int lane = threadIdx.x;
     const int slot = blockIdx.x;
     const uint32_t t_start = p.stamps ? stamp_now() : 0u;

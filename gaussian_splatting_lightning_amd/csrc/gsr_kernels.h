@@ -198,6 +198,15 @@ struct RenderBwdParams {
     // the forward's exact strip masks when *smask_valid (else the conservative cell_mask of the record)
     const uint8_t *strip_mask = nullptr;
     const uint32_t *smask_valid = nullptr;
+    // Zero fill of the per-Gaussian backward outputs, spread over the composite's workgroups (bwd_zero_fill): the
+    // 16-B aligned interior of each output as segments of one virtual array of zf_total16 uint4, their unaligned
+    // head / tail words listed one by one.  preprocess_bwd then stores only the Gaussians with a non-zero gradient.
+    static constexpr int ZF_SEGS = 10, ZF_ODD = 60;
+    uint32_t zf_nseg = 0, zf_nodd = 0;
+    uint64_t zf_total16 = 0;
+    uint4 *zf_ptr[ZF_SEGS] = {};
+    uint64_t zf_pre16[ZF_SEGS + 1] = {};  // prefix sums of the segments' lengths
+    uint32_t *zf_odd[ZF_ODD] = {};
 };
 void launch_render_bwd(hipStream_t s, const RenderBwdParams &p);
 
@@ -232,6 +241,7 @@ struct PreprocessBwdParams {
     int *max_radii2D;        // (P) max(max_radii2D, radii) (may be null)
     float *campos_rows;      // (campos_nrows, 3): campos in row campos_rank, zeros elsewhere (may be null)
     int campos_rank, campos_nrows;
+    int prezeroed = 0;       // the outputs were zero-filled (RenderBwdParams::zf_*): store only non-zero gradients
 };
 void launch_preprocess_bwd(hipStream_t s, const PreprocessBwdParams &p);
 

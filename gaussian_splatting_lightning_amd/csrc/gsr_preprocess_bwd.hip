@@ -71,7 +71,8 @@ __device__ __forceinline__ PbwdCamera load_camera(const PreprocessBwdParams &p) 
 template <bool LDS>
 __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p, const PbwdCamera &cam, const int i,
                                                    const int radius, const uint32_t n_tiles, bool have_gs,
-                                                   const float (&gs_in)[10], float3 &dRGB_out, float3 &dir_out) {
+                                                   const float (&gs_in)[10], float3 &dRGB_out, float3 &dir_out,
+                                                   bool &zeroed) {
     // radius and kept-tile count: the caller's loads (reloaded here they took a round trip of their own)
     const bool vis = radius > 0;
     // The densification statistics' read-modify-writes: the reads issued here, the writes at the end (put_stats).
@@ -116,6 +117,21 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
             }
         }
     }
+    dRGB_out = make_float3(0.f, 0.f, 0.f);
+    dir_out = make_float3(1.f, 0.f, 0.f);
+    // Outputs zero-filled by the composite backward (prezeroed): a culled Gaussian, or one no pixel took a gradient
+    // from (all ten row sums zero -- 78 % of the Gaussians at cfg 3), has an identically zero gradient (every output is
+    // a linear function of the sums): only its statistics are written, and none of its geometry is read.
+    if (p.prezeroed) {
+        bool z = true;
+#pragma unroll
+        for (int k = 0; k < 10; k++) z = z && gs[k] == 0.f;
+        if (!vis || z) {
+            zeroed = true;
+            put_stats();
+            return;
+        }
+    }
     if (p.dL_dmeans2D) {
         p.dL_dmeans2D[3 * i] = gs[0];
         p.dL_dmeans2D[3 * i + 1] = gs[1];
@@ -127,8 +143,6 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
         p.dL_dcolors[3 * i + 2] = gs[8];
     }
     const int ncoef = p.M * 3;
-    dRGB_out = make_float3(0.f, 0.f, 0.f);
-    dir_out = make_float3(1.f, 0.f, 0.f);
     if (!vis) {
         if (p.dL_dopacity) p.dL_dopacity[i] = 0.f;
         if (p.dL_dmeans3D) { p.dL_dmeans3D[3 * i] = 0.f; p.dL_dmeans3D[3 * i + 1] = 0.f; p.dL_dmeans3D[3 * i + 2] = 0.f; }
@@ -330,7 +344,8 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         float3 d3, v3;
         if (i < p.g1) {
             const int rad = p.radii[i];
-            preprocess_bwd_one<false>(p, cam, i, rad, rad > 0 ? p.tiles[i] : 0u, false, none, d3, v3);
+            bool zg = false;
+            preprocess_bwd_one<false>(p, cam, i, rad, rad > 0 ? p.tiles[i] : 0u, false, none, d3, v3, zg);
         }
         return;
     }
@@ -418,10 +433,14 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         }
     }
     float3 dRGB = make_float3(0.f, 0.f, 0.f), dir = make_float3(1.f, 0.f, 0.f);
-    if (i < p.g1) preprocess_bwd_one<true>(p, cam, i, rad, cnt, true, gs, dRGB, dir);
+    bool zg = false;
+    if (i < p.g1) preprocess_bwd_one<true>(p, cam, i, rad, cnt, true, gs, dRGB, dir, zg);
     if (!p.dL_dsh) return;
+    // prezeroed: the Gaussians whose dL/dsh rows are stored (the others are zero already)
+    const uint64_t live = p.prezeroed ? __ballot(i < p.g1 && !zg) : ~0ull;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
+        if (((live >> (32 * h)) & 0xffffffffull) == 0ull) continue;  // wave-uniform: no row of this half to store
         wave_lds_sync();  // the area's previous contents (row chunks or the other half) are consumed
         if ((lane >> 5) == h) sh_dsh_dispatch(p.D, dir, dRGB, sw + (lane & 31) * SH_STRIDE);
         wave_lds_sync();
@@ -429,7 +448,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         for (int c = 0; c < 6; c++) {  // 32 Gaussians x 48 floats = 384 float4, 6 per lane
             const uint32_t f = c * 256 + lane * 4;
             const size_t go = gbase + (size_t)h * 1536 + f;
-            if (go < gend)
+            if (go < gend && ((live >> (32 * h + f / 48)) & 1ull))
                 *reinterpret_cast<float4 *>(p.dL_dsh + go) =
                     *reinterpret_cast<const float4 *>(sw + (f / 48) * SH_STRIDE + f % 48);
         }

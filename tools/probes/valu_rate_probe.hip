@@ -56,6 +56,12 @@ __global__ __launch_bounds__(256) void probe(float *out, unsigned long long *cyc
                 if (i & 1) asm volatile("s_and_b64 %0, %0, %1" : "+s"(m64) : "s"(m64b) : "scc");
                 else asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c));
             }
+            if (OP == 13) asm volatile("v_mov_b32 %0, 0" : "=v"(a[i]));  // zeroing (the backward's accumulator init)
+            if (OP == 14) asm volatile("v_mov_b64 %0, 0" : "=v"(p[i]));  // two zeroed registers per instruction
+            if (OP == 15) {  // 1 v_fma : 1 v_mov_b64
+                if (i & 1) asm volatile("v_mov_b64 %0, 0" : "=v"(p[i]));
+                else asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c));
+            }
             if (OP == 8) {  // alternating v_fma / v_pk_fma
                 if (i & 1) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(p[i]) : "v"(b2), "v"(c2));
                 else asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c));
@@ -129,5 +135,8 @@ int main() {
     run<10>("fma / s_add alt", out, cyc);
     run<11>("3 fma : 1 s_add", out, cyc);
     run<12>("fma / s_and_b64 alt", out, cyc);
+    run<13>("v_mov_b32 0", out, cyc);
+    run<14>("v_mov_b64 0", out, cyc);
+    run<15>("fma / v_mov_b64 alt", out, cyc);
     return 0;
 }
