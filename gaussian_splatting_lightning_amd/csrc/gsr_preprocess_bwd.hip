@@ -332,7 +332,96 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
 // 0.100 ms, cfg5 0.521 -> 0.507 against all of a chunk's inv words first (round 5).
 constexpr int SH_STRIDE = 52;
 constexpr int PBWD_STAGE = 32 * SH_STRIDE;  // floats of LDS per wave
-template <bool LDS_SH>
+
+// Outputs zero-filled by the composite (prezeroed): after the row gather, the workgroup's Gaussians with a non-zero
+// gradient (22 % at cfg 3, 4 % at cfg 5) are compacted through LDS onto its first lanes, so the per-Gaussian
+// projection / covariance / SH backward runs on ~a quarter of the waves instead of on every wave that holds one such
+// Gaussian (most of them: without compaction the compute cost was that of every Gaussian).  The others write only
+// their densification statistics.  dL/dsh rows are staged per half-wave as before and stored cooperatively, 12 float4
+// per Gaussian at the entry's own index.  Every workgroup barrier is reached by all four waves.
+__device__ __forceinline__ void zero_gaussian_stats(const PreprocessBwdParams &p, int i, int radius) {
+    if (p.densify_stats) {
+        float2 st = make_float2(0.f, radius > 0 ? 1.f : 0.f);
+        if (p.densify_accumulate) {
+            const float2 o = *reinterpret_cast<const float2 *>(p.densify_stats + 2 * i);
+            st = make_float2(o.x + st.x, o.y + st.y);
+        }
+        *reinterpret_cast<float2 *>(p.densify_stats + 2 * i) = st;
+    }
+    if (p.max_radii2D) p.max_radii2D[i] = max(p.max_radii2D[i], radius);
+}
+__device__ __forceinline__ void compacted_tail(const PreprocessBwdParams &p, const PbwdCamera &cam, const int i,
+                                               const int rad, const uint32_t cnt, const float (&gs)[10], float *sw,
+                                               const int w, const int lane) {
+    __shared__ uint32_t s_wcnt[4];
+    __shared__ int s_gi[256];  // entry -> Gaussian index
+    // every entry's words, [word][entry], over the four waves' staging areas (free between the gather and the staging)
+    float *list = sw - w * PBWD_STAGE;
+    constexpr int NW = 12;  // radius, tile count, 10 sums
+    static_assert(NW * 256 <= 4 * PBWD_STAGE, "the entry list fits the staging areas");
+    bool nz = false;
+    if (i < p.g1 && rad > 0) {
+        nz = cnt > BIG_GAUSSIAN_TILES;  // its sum (big_reduce) is read by preprocess_bwd_one
+#pragma unroll
+        for (int k = 0; k < 10; k++) nz = nz || gs[k] != 0.f;
+    }
+    if (i < p.g1 && !nz) zero_gaussian_stats(p, i, rad);
+    const uint64_t bal = __ballot(nz);
+    if (lane == 0) s_wcnt[w] = (uint32_t)__popcll(bal);
+    __syncthreads();  // every wave's gather is done (its staging area free) and its count published
+    uint32_t off = 0, total = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t c = s_wcnt[q];
+        off += q < w ? c : 0u;
+        total += c;
+    }
+    if (nz) {
+        const uint32_t e = off + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        s_gi[e] = i;
+        list[e] = __int_as_float(rad);
+        list[256 + e] = __uint_as_float(cnt);
+#pragma unroll
+        for (int k = 0; k < 10; k++) list[(2 + k) * 256 + e] = gs[k];
+    }
+    __syncthreads();
+    const uint32_t e = (uint32_t)(w * 64 + lane);
+    const bool has = e < total;
+    int ge = 0, rade = 0;
+    uint32_t cnte = 0;
+    float gse[10];
+    if (has) {
+        ge = s_gi[e];
+        rade = __float_as_int(list[e]);
+        cnte = __float_as_uint(list[256 + e]);
+    }
+#pragma unroll
+    for (int k = 0; k < 10; k++) gse[k] = has ? list[(2 + k) * 256 + e] : 0.f;
+    __syncthreads();  // the list is consumed: the areas are the waves' staging areas again
+    if ((uint32_t)(w * 64) >= total) return;  // wave-uniform: no entry for this wave
+    float3 dRGB = make_float3(0.f, 0.f, 0.f), dir = make_float3(1.f, 0.f, 0.f);
+    bool zg = false;
+    if (has) preprocess_bwd_one<true>(p, cam, ge, rade, cnte, true, gse, dRGB, dir, zg);
+    if (!p.dL_dsh) return;
+    const uint64_t live = __ballot(has && !zg);  // (a big Gaussian whose sum is zero stays zero-filled)
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        if (((live >> (32 * h)) & 0xffffffffull) == 0ull) continue;  // wave-uniform
+        wave_lds_sync();
+        if ((lane >> 5) == h && has) sh_dsh_dispatch(p.D, dir, dRGB, sw + (lane & 31) * SH_STRIDE);
+        wave_lds_sync();
+#pragma unroll
+        for (int c = 0; c < 6; c++) {  // 32 Gaussians x 12 float4, each Gaussian's 192 B by 12 consecutive lanes
+            const uint32_t q = (uint32_t)(c * 64 + lane), gl = q / 12, part = q % 12;
+            if ((live >> (32 * h + gl)) & 1ull) {
+                const int gi = s_gi[w * 64 + 32 * h + (int)gl];
+                *reinterpret_cast<float4 *>(p.dL_dsh + (size_t)gi * 48 + part * 4) =
+                    *reinterpret_cast<const float4 *>(sw + gl * SH_STRIDE + part * 4);
+            }
+        }
+    }
+}
+template <bool LDS_SH, bool COMPACT = false>  // COMPACT: p.prezeroed (compacted_tail)
 __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams p) {
     const int i = p.g0 + blockIdx.x * 256 + threadIdx.x;
     const PbwdCamera cam = load_camera(p);  // before the first store (scalar loads)
@@ -434,13 +523,14 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
     }
     float3 dRGB = make_float3(0.f, 0.f, 0.f), dir = make_float3(1.f, 0.f, 0.f);
     bool zg = false;
+    if constexpr (COMPACT) {
+        compacted_tail(p, cam, i, rad, cnt, gs, sw, w, lane);
+        return;
+    }
     if (i < p.g1) preprocess_bwd_one<true>(p, cam, i, rad, cnt, true, gs, dRGB, dir, zg);
     if (!p.dL_dsh) return;
-    // prezeroed: the Gaussians whose dL/dsh rows are stored (the others are zero already)
-    const uint64_t live = p.prezeroed ? __ballot(i < p.g1 && !zg) : ~0ull;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-        if (((live >> (32 * h)) & 0xffffffffull) == 0ull) continue;  // wave-uniform: no row of this half to store
         wave_lds_sync();  // the area's previous contents (row chunks or the other half) are consumed
         if ((lane >> 5) == h) sh_dsh_dispatch(p.D, dir, dRGB, sw + (lane & 31) * SH_STRIDE);
         wave_lds_sync();
@@ -448,7 +538,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         for (int c = 0; c < 6; c++) {  // 32 Gaussians x 48 floats = 384 float4, 6 per lane
             const uint32_t f = c * 256 + lane * 4;
             const size_t go = gbase + (size_t)h * 1536 + f;
-            if (go < gend && ((live >> (32 * h + f / 48)) & 1ull))
+            if (go < gend)
                 *reinterpret_cast<float4 *>(p.dL_dsh + go) =
                     *reinterpret_cast<const float4 *>(sw + (f / 48) * SH_STRIDE + f % 48);
         }
@@ -460,7 +550,9 @@ void launch_preprocess_bwd(hipStream_t s, const PreprocessBwdParams &p) {
     const uint32_t grid = div_up((uint32_t)(p.g1 - p.g0), 256);
     // the joint row gather and the LDS-staged dL/dsh stores; without dL/dsh (the compact multi-view exchange) only
     // the gather, which the per-lane path pays ~40 % of the kernel for
-    if ((p.dL_dsh ? p.sh_vec16 : true) && tuning("pbwd_lds_sh", 1))
+    if ((p.dL_dsh ? p.sh_vec16 : true) && tuning("pbwd_lds_sh", 1) && p.prezeroed)
+        preprocess_bwd_kernel<true, true><<<grid, 256, 0, s>>>(p);
+    else if ((p.dL_dsh ? p.sh_vec16 : true) && tuning("pbwd_lds_sh", 1))
         preprocess_bwd_kernel<true><<<grid, 256, 0, s>>>(p);
     else
         preprocess_bwd_kernel<false><<<grid, 256, 0, s>>>(p);
