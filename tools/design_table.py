@@ -20,9 +20,11 @@ ALGO = {
     "bucket_partition": ("8 B/I read + 8 B/I write", "latency"),
     "seg_sort": ("8 B/I read + 4 B/I write", "VALU / LDS"),
     "render_fwd": ("8 B/T + 44 B/I loaded + 24 B/px (+4 B inv + 1 B strip mask per loaded I)", "**VALU issue**"),
-    "render_bwd": ("8 B/T + 44 B/I walked + 40 B/I gradient rows + 1 B strip mask", "**VALU issue**"),
+    "render_bwd": ("8 B/T + 44 B/I walked + 40 B/I gradient rows + 1 B strip mask + G (56 + 12M) zero fill",
+                   "**VALU issue**"),
     "big_reduce": ("rows of > 64-tile Gaussians", "latency"),
-    "preprocess_bwd": ("G (40 + 36 + 88) read + G (56 + 12M) write = 412 B/G", "HBM"),
+    "preprocess_bwd": ("12 B/G + 4 B/I + 40 B/row read; G' (76 read + 56 + 12M write), G' = non-zero Gaussians",
+                       "HBM / latency"),
     "depth_sort": ("3 passes x (4 B key + 4 B value) x 2 x G", "HBM / latency"),
     "instance_scan": ("8 B/G", "latency"),
     "expand": ("records 16 B/G + 2 B key, 4 B value, 4 B inv per I", "stores"),
