@@ -1143,3 +1143,44 @@ def test_threshold_guard_band(gpu_device, case):
     for k in GRADS:
         if f"grad_rel_l2_{k}" in rec["guard1"]:
             assert rec["guard1"][f"grad_rel_l2_{k}"] <= 1e-5, rec
+
+
+@pytest.mark.parametrize("compact_sh", [False, True])
+def test_zero_gradients_written_by_the_composite(gpu_device, compact_sh):
+    """With "bwd_prezero" (default) the compositing backward zero-fills the per-Gaussian outputs as its workgroups
+    exit and preprocess_bwd stores only the Gaussians whose gradient is not identically zero.  Every output must hold
+    the values of the full-write path (knob 0) -- also when the outputs start as NaN garbage and sit 4 B off a 16-B
+    boundary (each output's unaligned head / tail words go through the odd-word list), and with the compact SH
+    gradient of the multi-view exchange."""
+    from gaussian_splatting_lightning_amd import _native
+    from gaussian_splatting_lightning_amd.rasterizer import backward_raw, forward_raw
+    n, W, H = 60_001, 640, 480
+    inp = scene_inputs(n, W, H, sh_degree=3, seed=27, stress_fraction=0.01)
+    dc, di = upstream(W, H, 27)
+    rs = settings_for(inp, gpu_device)
+    t = {k: torch.as_tensor(inp[k], device=gpu_device) for k in ("means3D", "opacities", "scales", "rotations", "shs")}
+    dct, dit = torch.as_tensor(dc, device=gpu_device), torch.as_tensor(di, device=gpu_device)
+    _, radii, _, st = forward_raw(t["means3D"], t["shs"], None, t["opacities"], t["scales"], t["rotations"], None, rs)
+    widths = dict(means3D=3, means2D=3, opacities=1, scales=3, rotations=4)
+    widths.update(colors_sh=3) if compact_sh else widths.update(shs=48)
+
+    def outputs():  # NaN-filled, each output 4 B past a 16-B boundary
+        o = {}
+        for k, w in widths.items():
+            buf = torch.full((n * w + 8,), float("nan"), device=gpu_device)
+            v = buf[1:1 + n * w]
+            o[k] = v.view(n, 16, 3) if k == "shs" else v.view(n, w)
+        return o
+
+    res = {}
+    for knob in (0, 1):
+        out = outputs()
+        with _native.tuned(bwd_prezero=knob):
+            g = backward_raw(st, rs, dct, dit, out=out, compact_sh=compact_sh)
+        torch.cuda.synchronize()
+        res[knob] = {k: g[k].detach().cpu().numpy() for k in widths}
+    zero = (radii.cpu().numpy() <= 0)
+    for k in widths:
+        assert not np.isnan(res[1][k]).any(), k
+        assert np.array_equal(res[0][k], res[1][k]), k
+        assert not np.any(res[1][k].reshape(n, -1)[zero]), k  # culled Gaussians: exact zeros
