@@ -183,11 +183,12 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
     for (int bend = (int)tl; bend > 0; bend -= BWD_BATCH) {
         const int cnt = min(BWD_BATCH, bend);
         float4 my_a = make_float4(0, 0, 0, 0), my_b = my_a;
-        uint32_t my_row = 0;
+        uint32_t my_row = 0, my_gid = 0;
         if (w == 0 && lane < cnt) {
             const uint32_t s_me = range.x + (uint32_t)(bend - 1 - lane);
             my_row = p.sorted_u[s_me];
             const uint32_t gid = p.point_list[s_me];
+            my_gid = gid;
             my_a = p.rec[gid].a;
             my_b = p.rec[gid].b;
             s_a[lane] = stage_rec_a(my_a);
@@ -285,6 +286,7 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
             row[8] = u[8];
             row[9] = u[9];
             store_row(p.rows, my_row, row);
+            if (p.live && row_nonzero(row)) p.live[my_gid] = 1;
         }
         __syncthreads();  // the next batch overwrites the staged records and the sums
     }
@@ -411,11 +413,12 @@ __global__ __launch_bounds__(64, GUARD ? 4 : SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MI
     for (int bend = (int)hi; bend > (int)lo; bend -= BWD_BATCH) {
         const int cnt = min(BWD_BATCH, bend - (int)lo);
         float4 my_a = make_float4(0, 0, 0, 0), my_b = my_a;
-        uint32_t my_row = 0, my_m = 0;
+        uint32_t my_row = 0, my_m = 0, my_gid = 0;
         if (lane < cnt) {
             const uint32_t s_me = r0 + (uint32_t)(bend - 1 - lane);
             my_row = p.sorted_u[s_me];
             const uint32_t gid = p.point_list[s_me];
+            my_gid = gid;
             if (GUARD) s_rec[lane].pad.x = __uint_as_float(gid);  // the guard's slow path reloads the raw record
             my_a = p.rec[gid].a;
             my_b = p.rec[gid].b;
@@ -574,6 +577,7 @@ __global__ __launch_bounds__(64, GUARD ? 4 : SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MI
             row[8] = u2.x;
             row[9] = u2.y;
             store_row(p.rows, my_row, row);
+            if (p.live && row_nonzero(row)) p.live[my_gid] = 1;
         }
         wave_lds_sync();
     }

@@ -118,6 +118,7 @@ struct GeomState {
     uint32_t *depth_key;   // P: float bits of view depth, 0xffffffff if culled
     uint32_t *tiles;       // P: tiles touched
     uint8_t *clamped;      // P: bit c set if SH colour channel c was clamped at 0
+    uint8_t *live;         // P: 0 from the preprocess; 1 once a compositing backward stored a non-zero row of it
     float *sh_jac;         // 9 x P: d rgb / d (unit view direction), planes [axis][channel] (SH degree > 0 only)
     uint4 *exp_rec;        // P: expansion record {kept-tile mask lo, hi, rmin.x | rmin.y << 16, rect width}; mask 0 =
                            //    all tiles of the rect (area > 64 or culling off).  One 16-B gather per Gaussian.
@@ -145,6 +146,7 @@ inline size_t carve_geom(char *base, int P, GeomState &g) {
     g.rec = c.take<GRec>(n);
     g.tiles = c.take<uint32_t>(n);
     g.clamped = c.take<uint8_t>(n);
+    g.live = c.take<uint8_t>(n);
     g.sh_jac = c.take<float>((size_t)9 * n);
     g.exp_rec = c.take<uint4>(n);
     g.inst_off = c.take<uint32_t>((size_t)n + 1);
@@ -744,6 +746,13 @@ __device__ __forceinline__ void load_row(const float *__restrict__ rows, size_t 
     }
 }
 
+// a gradient row with a non-zero term: its Gaussian's per-Gaussian backward has work (GeomState::live)
+__device__ __forceinline__ bool row_nonzero(const float r[10]) {
+    bool nz = false;
+#pragma unroll
+    for (int k = 0; k < 10; k++) nz = nz || r[k] != 0.f;
+    return nz;
+}
 __device__ __forceinline__ void store_row(float *__restrict__ rows, uint32_t s, const float r[10]) {
     float2 *dst = reinterpret_cast<float2 *>(rows + (size_t)s * GRAD_ROW);
 #pragma unroll

@@ -227,6 +227,7 @@ __global__ __launch_bounds__(256, GSR_PRE_MINW) void preprocess_kernel(Preproces
             g.clamped[i] = 0;
         }
         g.tiles[i] = kept;
+        g.live[i] = 0;  // (set by the compositing backward for a Gaussian it stores a non-zero row of)
         // A Gaussian whose every tile is culled keeps its radius (reference output) but renders nothing; it
         // is sorted behind all rendered ones so the expansion never meets an empty rank.
         g.depth_key[i] = kept ? ci.depth : 0xffffffffu;

@@ -184,6 +184,7 @@ struct RenderBwdParams {
     const GRec *rec;
     const float *bg, *final_T, *dL_dpix, *dL_dinvdepth;
     float *rows;    // R x GRAD_ROW
+    uint8_t *live;  // P: set to 1 for the Gaussian of every non-zero row stored (GeomState::live), or null
     uint4 *stamps;  // diagnostics (set by launch), or null
     int strip_exact;  // as RenderFwdParams::strip_exact (set by launch)
     uint64_t num_rendered = 0;  // instances (the launch's walk-variant choice)
@@ -232,6 +233,7 @@ struct PreprocessBwdParams {
     const uint32_t *tiles, *inst_start, *big_slot;
     const uint32_t *inv;  // the forward's inverse permutation: INV_NONE where the composite loaded no instance (no row)
     const uint8_t *clamped;
+    const uint8_t *live;  // P: 0 = no non-zero row (the gather is skipped: zero sums), or null = gather every Gaussian
     const float *sh_jac;  // 9 x P direction Jacobian of the colour, from the forward (SH degree > 0)
     const float *rows, *bigsum;
     float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales, *dL_drot;

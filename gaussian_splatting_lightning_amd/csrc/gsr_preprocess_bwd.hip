@@ -93,7 +93,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
     if (vis && have_gs && n_tiles <= BIG_GAUSSIAN_TILES) {
 #pragma unroll
         for (int k = 0; k < 10; k++) gs[k] = gs_in[k];
-    } else if (vis) {
+    } else if (vis && (!p.live || p.live[i])) {  // (no non-zero row stored: zero sums)
         const uint32_t start = p.inst_start[i], cnt = n_tiles;
         if (cnt > BIG_GAUSSIAN_TILES) {
             add_row(p.bigsum, p.big_slot[i], gs);
@@ -351,8 +351,8 @@ __device__ __forceinline__ void zero_gaussian_stats(const PreprocessBwdParams &p
     if (p.max_radii2D) p.max_radii2D[i] = max(p.max_radii2D[i], radius);
 }
 __device__ __forceinline__ void compacted_tail(const PreprocessBwdParams &p, const PbwdCamera &cam, const int i,
-                                               const int rad, const uint32_t cnt, const float (&gs)[10], float *sw,
-                                               const int w, const int lane) {
+                                               const int rad, const uint32_t cnt, const bool has_rows,
+                                               const float (&gs)[10], float *sw, const int w, const int lane) {
     __shared__ uint32_t s_wcnt[4];
     __shared__ int s_gi[256];  // entry -> Gaussian index
     // every entry's words, [word][entry], over the four waves' staging areas (free between the gather and the staging)
@@ -361,7 +361,7 @@ __device__ __forceinline__ void compacted_tail(const PreprocessBwdParams &p, con
     static_assert(NW * 256 <= 4 * PBWD_STAGE, "the entry list fits the staging areas");
     bool nz = false;
     if (i < p.g1 && rad > 0) {
-        nz = cnt > BIG_GAUSSIAN_TILES;  // its sum (big_reduce) is read by preprocess_bwd_one
+        nz = cnt > BIG_GAUSSIAN_TILES && has_rows;  // its sum (big_reduce) is read by preprocess_bwd_one
 #pragma unroll
         for (int k = 0; k < 10; k++) nz = nz || gs[k] != 0.f;
     }
@@ -452,15 +452,18 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
     float gs[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     int rad;
     uint32_t cnt;
+    bool live;
     {
         // radius, kept-tile count and first expansion index loaded together (clamped index, selected after)
         const int ic = min(i, p.g1 - 1);
         const int rad_l = p.radii[ic];
         const uint32_t cnt_l = p.tiles[ic], ist_l = p.inst_start[ic];
+        // no non-zero row stored (GeomState::live): the sums are zero, so its rows are not gathered
+        live = !p.live || p.live[ic] != 0;
         rad = i < p.g1 ? rad_l : 0;
         const bool vis = rad > 0;
         cnt = vis ? cnt_l : 0u;
-        const uint32_t len = cnt <= BIG_GAUSSIAN_TILES ? cnt : 0u;
+        const uint32_t len = (cnt <= BIG_GAUSSIAN_TILES && live) ? cnt : 0u;
         const uint32_t incl = wave_inclusive_scan(len, lane);
         const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         const uint32_t pst = incl - len;
@@ -524,7 +527,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
     float3 dRGB = make_float3(0.f, 0.f, 0.f), dir = make_float3(1.f, 0.f, 0.f);
     bool zg = false;
     if constexpr (COMPACT) {
-        compacted_tail(p, cam, i, rad, cnt, gs, sw, w, lane);
+        compacted_tail(p, cam, i, rad, cnt, live, gs, sw, w, lane);
         return;
     }
     if (i < p.g1) preprocess_bwd_one<true>(p, cam, i, rad, cnt, true, gs, dRGB, dir, zg);
