@@ -838,6 +838,7 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
         rp.bg = a->background; rp.final_T = im.final_T; rp.dL_dpix = a->dL_dpix; rp.dL_dinvdepth = a->dL_dinvdepth;
         rp.rows = rows;
         rp.live = tuning("bwd_live", 1) ? g.live : nullptr;
+        rp.live_valid = g.counters + CNT_LIVE_VALID;
         rp.sorted_u = b.sorted_u;
         rp.strip_mask = b.strip_mask; rp.smask_valid = im.smask_valid;
         if (T <= SEG_MAX_TILES && tuning("bwd_seg", 1)) {  // segmented walk (from the forward's checkpoints, if any)
@@ -874,6 +875,7 @@ int gsr_backward(const gsr_backward_args *a, gsr_alloc_fn alloc, void *alloc_ctx
     pp.view = a->viewmatrix; pp.proj = a->projmatrix; pp.campos = a->campos;
     pp.radii = a->radii; pp.tiles = g.tiles; pp.inst_start = g.inst_start; pp.clamped = g.clamped;
     pp.live = tuning("bwd_live", 1) ? g.live : nullptr;
+    pp.live_valid = g.counters + CNT_LIVE_VALID;
     pp.inv = b.inv;
     pp.sh_jac = g.sh_jac;  // the forward's d rgb / d dir: the SH term of dL/dmeans3D reads no coefficient
     pp.big_slot = g.big_slot; pp.bigsum = bigsum;

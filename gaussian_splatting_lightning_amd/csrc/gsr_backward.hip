@@ -141,6 +141,7 @@ __global__ __launch_bounds__(64 * PARTS) void render_bwd_parts_kernel(RenderBwdP
     __shared__ uint32_t s_m[BWD_BATCH];
     __shared__ __attribute__((aligned(16))) float s_part[PARTS][BWD_BATCH][PART];
     const ZeroFillAtExit zero_fill_at_exit{p};
+    if (p.live_valid && blockIdx.x == 0 && threadIdx.x == 0) *p.live_valid = p.live ? 1u : 0u;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int slot = blockIdx.x;
     const int tile = p.tile_order ? (int)p.tile_order[slot] : slot;
@@ -319,6 +320,7 @@ __global__ __launch_bounds__(64, GUARD ? 4 : SEG ? GSR_BWD_SEG_MINW : GSR_BWD_MI
         if (threadIdx.x < 2 * BWD_BATCH) (&s_zero[0][0])[threadIdx.x] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     const ZeroFillAtExit zero_fill_at_exit{p};
+    if (p.live_valid && blockIdx.x == 0 && threadIdx.x == 0) *p.live_valid = p.live ? 1u : 0u;
     const int lane = threadIdx.x;
     const int slot = blockIdx.x;
     const uint32_t t_start = p.stamps ? stamp_now() : 0u;

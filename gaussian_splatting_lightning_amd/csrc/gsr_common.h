@@ -27,7 +27,7 @@ constexpr int GRAD_ROW = 10;                   // floats per instance gradient r
 // counters: [CNT_BIG] big-Gaussian count, [CNT_OVERFLOW] scan overflow flag, then CNT_NPART 64-bit partial
 // sums of the instance total (spread over addresses so the per-block atomics do not serialise), then CNT_NPART
 // partial maxima of the complemented kept depth keys (their minimum) and CNT_NPART of the kept depth keys
-enum Counter : int { CNT_BIG = 0, CNT_OVERFLOW = 2, CNT_SCAN_TICKET = 3, CNT_COL_TICKET = 4, CNT_LONG = 6, CNT_PRE_DONE = 10, CNT_PARTIALS = 16, CNT_NPART = 64,
+enum Counter : int { CNT_BIG = 0, CNT_OVERFLOW = 2, CNT_SCAN_TICKET = 3, CNT_COL_TICKET = 4, CNT_LONG = 6, CNT_PRE_DONE = 10, CNT_LIVE_VALID = 12, CNT_PARTIALS = 16, CNT_NPART = 64,
                      CNT_DMIN = 16 + 2 * 64, CNT_DMAX = CNT_DMIN + 64, CNT_WORDS = CNT_DMAX + 64 };
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }

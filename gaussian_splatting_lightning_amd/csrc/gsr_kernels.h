@@ -185,6 +185,7 @@ struct RenderBwdParams {
     const float *bg, *final_T, *dL_dpix, *dL_dinvdepth;
     float *rows;    // R x GRAD_ROW
     uint8_t *live;  // P: set to 1 for the Gaussian of every non-zero row stored (GeomState::live), or null
+    uint32_t *live_valid;  // 1 when this composite marked the live flags, 0 when it did not (read by preprocess_bwd)
     uint4 *stamps;  // diagnostics (set by launch), or null
     int strip_exact;  // as RenderFwdParams::strip_exact (set by launch)
     uint64_t num_rendered = 0;  // instances (the launch's walk-variant choice)
@@ -234,6 +235,7 @@ struct PreprocessBwdParams {
     const uint32_t *inv;  // the forward's inverse permutation: INV_NONE where the composite loaded no instance (no row)
     const uint8_t *clamped;
     const uint8_t *live;  // P: 0 = no non-zero row (the gather is skipped: zero sums), or null = gather every Gaussian
+    const uint32_t *live_valid;  // the flags are used only when the last composite marked them
     const float *sh_jac;  // 9 x P direction Jacobian of the colour, from the forward (SH degree > 0)
     const float *rows, *bigsum;
     float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales, *dL_drot;

@@ -93,7 +93,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams &p,
     if (vis && have_gs && n_tiles <= BIG_GAUSSIAN_TILES) {
 #pragma unroll
         for (int k = 0; k < 10; k++) gs[k] = gs_in[k];
-    } else if (vis && (!p.live || p.live[i])) {  // (no non-zero row stored: zero sums)
+    } else if (vis && (!p.live || !*p.live_valid || p.live[i])) {  // (no non-zero row stored: zero sums)
         const uint32_t start = p.inst_start[i], cnt = n_tiles;
         if (cnt > BIG_GAUSSIAN_TILES) {
             add_row(p.bigsum, p.big_slot[i], gs);
@@ -459,7 +459,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdParams
         const int rad_l = p.radii[ic];
         const uint32_t cnt_l = p.tiles[ic], ist_l = p.inst_start[ic];
         // no non-zero row stored (GeomState::live): the sums are zero, so its rows are not gathered
-        live = !p.live || p.live[ic] != 0;
+        live = !p.live || !__builtin_amdgcn_readfirstlane(*p.live_valid) || p.live[ic] != 0;
         rad = i < p.g1 ? rad_l : 0;
         const bool vis = rad > 0;
         cnt = vis ? cnt_l : 0u;

@@ -1184,3 +1184,39 @@ def test_zero_gradients_written_by_the_composite(gpu_device, compact_sh):
         assert not np.isnan(res[1][k]).any(), k
         assert np.array_equal(res[0][k], res[1][k]), k
         assert not np.any(res[1][k].reshape(n, -1)[zero]), k  # culled Gaussians: exact zeros
+
+
+def test_second_backward_on_one_forward_sees_its_own_rows(gpu_device):
+    """The compositing backward marks the Gaussians it stores a non-zero row of (GeomState::live, set-only, cleared
+    by the forward) and the per-Gaussian pass gathers only those.  A second backward on the same forward with another
+    upstream gradient -- one that is zero on half the image, so the first backward's marks differ from what the
+    second needs -- and one run with the marks switched off in its composite must both equal a fresh
+    forward + backward."""
+    from gaussian_splatting_lightning_amd import _native
+    from gaussian_splatting_lightning_amd.rasterizer import backward_raw, forward_raw
+    n, W, H = 50_000, 640, 480
+    inp = scene_inputs(n, W, H, sh_degree=3, seed=31, stress_fraction=0.01)
+    rs = settings_for(inp, gpu_device)
+    t = {k: torch.as_tensor(inp[k], device=gpu_device) for k in ("means3D", "opacities", "scales", "rotations", "shs")}
+    args = (t["means3D"], t["shs"], None, t["opacities"], t["scales"], t["rotations"], None, rs)
+    d1, i1 = (torch.as_tensor(a, device=gpu_device) for a in upstream(W, H, 31))
+    d2, i2 = (torch.as_tensor(a, device=gpu_device) for a in upstream(W, H, 32))
+    d1[:, :, W // 2:] = 0.0  # the first backward: rows only from the left half
+    i1[:, :, W // 2:] = 0.0
+
+    def grads(g):
+        return {k: g[k].detach().cpu().numpy() for k in GRADS}
+
+    _, _, _, st = forward_raw(*args)
+    backward_raw(st, rs, d1, i1)
+    second = grads(backward_raw(st, rs, d2, i2))
+    with _native.tuned(bwd_live=0):
+        unmarked = grads(backward_raw(st, rs, d2, i2))
+    third = grads(backward_raw(st, rs, d2, i2))  # marks valid again
+    _, _, _, st2 = forward_raw(*args)
+    fresh = grads(backward_raw(st2, rs, d2, i2))
+    torch.cuda.synchronize()
+    for k in GRADS:
+        assert np.array_equal(second[k], fresh[k]), k
+        assert np.array_equal(unmarked[k], fresh[k]), k
+        assert np.array_equal(third[k], fresh[k]), k

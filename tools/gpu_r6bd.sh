@@ -1,0 +1,5 @@
+set -e
+O=gpurun_out/r6bd; mkdir -p $O
+timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/ > $O/gpu_pytest.log 2>&1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+timeout -k 10 400 python bench.py > $O/bench_cfg3.json 2> $O/bench.err
